@@ -1,0 +1,12 @@
+// Single Python module for every native component of ddp_practice_amd.
+// Each translation unit exposes a register_* function; nothing here but glue.
+#include <torch/extension.h>
+
+namespace dpa {
+void register_selftest(pybind11::module& m);
+}
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "ddp_practice_amd native extension (gfx950 HIP kernels, RCCL communicator, DDP reducer)";
+  dpa::register_selftest(m);
+}

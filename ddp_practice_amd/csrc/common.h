@@ -1,0 +1,123 @@
+// Shared helpers for the gfx950 (MI355X, CDNA4) kernels of ddp_practice_amd.
+//
+// Conventions used by every kernel file:
+//  * wave = 64 lanes; block sizes are multiples of 64.
+//  * MFMA fragments follow the gfx950 maps documented in
+//    /opt/skills/guides/cdna_hip_programming.md §3:
+//      16x16x32 (bf16/f16): lane l holds A[l&15][8*(l>>4)+j], B[8*(l>>4)+j][l&15],
+//                           C/D: col = l&15, row = 4*(l>>4)+r (r = 0..3)
+//      16x16x4  (f32)     : lane l holds A[l&15][l>>4],      B[l>>4][l&15]
+//  * every launch goes to the caller's current HIP stream (graph-capturable:
+//    no allocation, no host sync inside a launch function).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <ATen/hip/HIPContext.h>
+
+#include <cstdint>
+
+namespace dpa {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned short u16x4;
+typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
+
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define DPA_CHECK_HIP(expr)                                                          \
+  do {                                                                               \
+    hipError_t _e = (expr);                                                          \
+    TORCH_CHECK(_e == hipSuccess, "HIP error ", hipGetErrorString(_e), " at ",       \
+                __FILE__, ":", __LINE__);                                            \
+  } while (0)
+
+#define DPA_CHECK_LAUNCH() DPA_CHECK_HIP(hipGetLastError())
+
+#define DPA_CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a HIP device tensor")
+#define DPA_CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define DPA_CHECK_INPUT(t) \
+  DPA_CHECK_DEV(t);        \
+  DPA_CHECK_CONTIG(t)
+
+// Storage dtype tags for activations: fp32, bf16, fp16.
+enum class DT : int { F32 = 0, BF16 = 1, F16 = 2 };
+
+inline DT dt_of(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return DT::F32;
+    case at::kBFloat16: return DT::BF16;
+    case at::kHalf: return DT::F16;
+    default: TORCH_CHECK(false, "unsupported dtype ", t.scalar_type());
+  }
+  return DT::F32;
+}
+
+// ---- scalar conversions (device) -------------------------------------------
+template <typename T> struct Cvt;
+template <> struct Cvt<float> {
+  __device__ __forceinline__ static float to_f(float x) { return x; }
+  __device__ __forceinline__ static float from_f(float x) { return x; }
+};
+template <> struct Cvt<__hip_bfloat16> {
+  __device__ __forceinline__ static float to_f(__hip_bfloat16 x) { return __bfloat162float(x); }
+  __device__ __forceinline__ static __hip_bfloat16 from_f(float x) { return __float2bfloat16(x); }
+};
+template <> struct Cvt<__half> {
+  __device__ __forceinline__ static float to_f(__half x) { return __half2float(x); }
+  __device__ __forceinline__ static __half from_f(float x) { return __float2half(x); }
+};
+
+template <typename T> __device__ __forceinline__ float ld_f(const T* p) { return Cvt<T>::to_f(*p); }
+template <typename T> __device__ __forceinline__ void st_f(T* p, float v) { *p = Cvt<T>::from_f(v); }
+
+// ---- wave reductions ----------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum of one float; `red` must hold >= blockDim/64 floats of LDS.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+// ---- MFMA wrappers -------------------------------------------------------------
+// Low-precision element type -> 8-element MFMA operand vector.
+template <typename T> struct Mfma16;
+template <> struct Mfma16<__hip_bfloat16> {
+  typedef bf16x8 frag;
+  __device__ __forceinline__ static f32x4 mma(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Mfma16<__half> {
+  typedef f16x8 frag;
+  __device__ __forceinline__ static f32x4 mma(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
+
+__device__ __forceinline__ f32x4 mfma_f32_16x16x4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+}  // namespace dpa
