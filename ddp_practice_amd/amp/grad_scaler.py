@@ -1,0 +1,193 @@
+"""Dynamic loss scaling with all state resident on the device.
+
+Semantics follow ``torch.amp.GradScaler`` (torch/amp/grad_scaler.py:123-129
+defaults; scale :190-222; unscale_ :235-286; step :348-357; update :500-537;
+state_dict :607-632), with one structural difference: ``step`` never calls
+``found_inf.item()``.  When the optimizer is this package's fused SGD the
+inf-check result is consumed on the device (the SGD kernel is predicated on
+``found_inf``), so a whole training step — forward, backward, all-reduce,
+unscale, step, scale update — can be captured in one hipGraph.  For any other
+optimizer the host-synchronising fallback of the reference is used.
+
+reference: /root/reference/ddp_main.py:10,126 (``GradScaler()``), :91-93.
+"""
+from __future__ import annotations
+
+from typing import Any
+
+import torch
+
+from .._ext import load as _load_ext
+
+
+def _native_ok(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+class GradScaler:
+    def __init__(self, device: str = "cuda", init_scale: float = 2.0 ** 16, growth_factor: float = 2.0,
+                 backoff_factor: float = 0.5, growth_interval: int = 2000, enabled: bool = True):
+        if growth_factor <= 1.0:
+            raise ValueError("growth_factor should be > 1")
+        if not (0.0 < backoff_factor < 1.0):
+            raise ValueError("backoff_factor should be < 1")
+        self._device = device if (device != "cuda" or torch.cuda.is_available()) else "cpu"
+        self._enabled = enabled
+        self._init_scale = float(init_scale)
+        self._growth_factor = float(growth_factor)
+        self._backoff_factor = float(backoff_factor)
+        self._growth_interval = int(growth_interval)
+        self._scale: torch.Tensor | None = None
+        self._growth_tracker: torch.Tensor | None = None
+        self._found_inf: torch.Tensor | None = None
+        self._per_opt: dict[int, dict[str, Any]] = {}
+
+    # ------------------------------------------------------------------ state
+    def _lazy_init(self, dev: torch.device):
+        if self._scale is None:
+            self._scale = torch.full((1,), self._init_scale, dtype=torch.float32, device=dev)
+            self._growth_tracker = torch.full((1,), getattr(self, "_pending_tracker", 0), dtype=torch.int32,
+                                              device=dev)
+            self._found_inf = torch.zeros((1,), dtype=torch.float32, device=dev)
+
+    def is_enabled(self) -> bool:
+        return self._enabled
+
+    def get_scale(self) -> float:
+        if not self._enabled:
+            return 1.0
+        return self._init_scale if self._scale is None else float(self._scale.item())
+
+    @property
+    def scale_tensor(self) -> torch.Tensor:
+        return self._scale
+
+    @property
+    def found_inf(self) -> torch.Tensor:
+        return self._found_inf
+
+    # ------------------------------------------------------------------ API
+    def scale(self, outputs):
+        if not self._enabled:
+            return outputs
+        if isinstance(outputs, torch.Tensor):
+            self._lazy_init(outputs.device)
+            return outputs * self._scale.to(outputs.device, non_blocking=True)
+        if isinstance(outputs, (list, tuple)):
+            return type(outputs)(self.scale(o) for o in outputs)
+        raise ValueError("outputs must be a Tensor or an iterable of Tensors")
+
+    def _grads(self, optimizer):
+        gs = []
+        for group in optimizer.param_groups:
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise NotImplementedError("sparse grads are not supported")
+                gs.append(p.grad)
+        return gs
+
+    def unscale_(self, optimizer):
+        if not self._enabled:
+            return
+        st = self._per_opt.setdefault(id(optimizer), {"stage": "ready"})
+        if st["stage"] == "unscaled":
+            raise RuntimeError("unscale_() has already been called on this optimizer since the last update().")
+        if st["stage"] == "stepped":
+            raise RuntimeError("unscale_() is being called after step().")
+        grads = self._grads(optimizer)
+        if self._scale is None:
+            self._lazy_init(grads[0].device if grads else torch.device(self._device))
+        self._found_inf.zero_()
+        if grads and _native_ok(grads[0]) and all(g.dtype == torch.float32 and g.is_contiguous() for g in grads):
+            _load_ext().optim.unscale_check(grads, self._scale, self._found_inf)
+        else:
+            inv = self._scale.double().reciprocal().float()
+            for g in grads:
+                self._found_inf.copy_(torch.maximum(self._found_inf, (~torch.isfinite(g)).any().float().reshape(1)))
+                g.mul_(inv.to(g.dtype))
+        st["stage"] = "unscaled"
+
+    def step(self, optimizer, *args, **kwargs):
+        if not self._enabled:
+            return optimizer.step(*args, **kwargs)
+        if "closure" in kwargs:
+            raise RuntimeError("Closure use is not currently supported if GradScaler is enabled.")
+        st = self._per_opt.setdefault(id(optimizer), {"stage": "ready"})
+        if st["stage"] == "stepped":
+            raise RuntimeError("step() has already been called since the last update().")
+        if st["stage"] == "ready":
+            self.unscale_(optimizer)
+        ret = None
+        if getattr(optimizer, "supports_device_found_inf", False):
+            # fused path: the optimizer kernel reads found_inf on device (no host sync)
+            ret = optimizer.step(*args, found_inf=self._found_inf, **kwargs)
+        else:
+            if not bool(self._found_inf.item()):
+                ret = optimizer.step(*args, **kwargs)
+        st["stage"] = "stepped"
+        return ret
+
+    def update(self, new_scale=None):
+        if not self._enabled:
+            return
+        if self._scale is None:
+            return
+        if new_scale is not None:
+            if isinstance(new_scale, float):
+                self._scale.fill_(new_scale)
+            else:
+                self._scale.copy_(new_scale)
+        else:
+            if self._scale.is_cuda:
+                _load_ext().optim.update_scale(self._scale, self._growth_tracker, self._found_inf,
+                                               self._growth_factor, self._backoff_factor, self._growth_interval)
+            else:
+                torch._amp_update_scale_(self._scale, self._growth_tracker, self._found_inf,
+                                         self._growth_factor, self._backoff_factor, self._growth_interval)
+        self._per_opt = {}
+
+    # ------------------------------------------------------------ checkpoint
+    def get_growth_factor(self):
+        return self._growth_factor
+
+    def get_backoff_factor(self):
+        return self._backoff_factor
+
+    def get_growth_interval(self):
+        return self._growth_interval
+
+    def _get_growth_tracker(self) -> int:
+        if self._growth_tracker is None:
+            return 0
+        return int(self._growth_tracker.item())
+
+    def state_dict(self) -> dict[str, Any]:
+        """Same keys/types as torch.amp.GradScaler.state_dict()."""
+        if not self._enabled:
+            return {}
+        return {
+            "scale": self.get_scale(),
+            "growth_factor": self._growth_factor,
+            "backoff_factor": self._backoff_factor,
+            "growth_interval": self._growth_interval,
+            "_growth_tracker": self._get_growth_tracker(),
+        }
+
+    def load_state_dict(self, state_dict: dict[str, Any]):
+        if not self._enabled:
+            return
+        if len(state_dict) == 0:
+            raise RuntimeError("The source state dict is empty, possibly because it was saved from a disabled "
+                               "instance of GradScaler.")
+        self._init_scale = float(state_dict["scale"])
+        if self._scale is not None:
+            self._scale.fill_(state_dict["scale"])
+        self._growth_factor = float(state_dict["growth_factor"])
+        self._backoff_factor = float(state_dict["backoff_factor"])
+        self._growth_interval = int(state_dict["growth_interval"])
+        if self._growth_tracker is not None:
+            self._growth_tracker.fill_(int(state_dict["_growth_tracker"]))
+        else:
+            self._pending_tracker = int(state_dict["_growth_tracker"])

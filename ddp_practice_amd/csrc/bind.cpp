@@ -4,9 +4,17 @@
 
 namespace dpa {
 void register_selftest(pybind11::module& m);
+void register_convblock(pybind11::module& m);
+void register_head(pybind11::module& m);
+void register_optim(pybind11::module& m);
+void register_data(pybind11::module& m);
 }
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "ddp_practice_amd native extension (gfx950 HIP kernels, RCCL communicator, DDP reducer)";
   dpa::register_selftest(m);
+  dpa::register_convblock(m);
+  dpa::register_head(m);
+  dpa::register_optim(m);
+  dpa::register_data(m);
 }

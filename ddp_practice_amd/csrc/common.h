@@ -120,4 +120,77 @@ __device__ __forceinline__ f32x4 mfma_f32_16x16x4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+typedef __attribute__((ext_vector_type(8))) float f32x8;
+
+// Storage-type traits for the "16 x 16 x (8 per lane-group)" MFMA step used by
+// every GEMM-shaped kernel here.  Each lane supplies 8 K-consecutive operand
+// elements (lane group q = lane>>4 owns logical k = 8q..8q+7 of a 32-deep step):
+//   bf16/f16 : one v_mfma_f32_16x16x32_{bf16,f16}
+//   f32      : eight v_mfma_f32_16x16x4_f32 (exact fp32); sub-step s pairs the
+//              s-th element of every lane group, i.e. logical k = 8q+s, which is
+//              a consistent permutation of K for A and B, so the sum is the same.
+template <typename T> struct MM;
+template <> struct MM<float> {
+  typedef f32x8 frag;
+  typedef float elem;
+  __device__ __forceinline__ static f32x4 mma(const frag& a, const frag& b, f32x4 c) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) c = mfma_f32_16x16x4(a[s], b[s], c);
+    return c;
+  }
+  __device__ __forceinline__ static frag ld(const float* p) {  // 16-B aligned
+    f32x4 lo = *reinterpret_cast<const f32x4*>(p);
+    f32x4 hi = *reinterpret_cast<const f32x4*>(p + 4);
+    frag f;
+    f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+    f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+    return f;
+  }
+  __device__ __forceinline__ static elem cv(float x) { return x; }
+  __device__ __forceinline__ static float rnd(float x) { return x; }
+};
+template <> struct MM<__hip_bfloat16> {
+  typedef bf16x8 frag;
+  typedef __bf16 elem;
+  __device__ __forceinline__ static f32x4 mma(const frag& a, const frag& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  __device__ __forceinline__ static frag ld(const __hip_bfloat16* p) {
+    return *reinterpret_cast<const frag*>(p);
+  }
+  __device__ __forceinline__ static elem cv(float x) { return (__bf16)x; }
+  __device__ __forceinline__ static float rnd(float x) { return (float)(__bf16)x; }
+};
+template <> struct MM<__half> {
+  typedef f16x8 frag;
+  typedef _Float16 elem;
+  __device__ __forceinline__ static f32x4 mma(const frag& a, const frag& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+  __device__ __forceinline__ static frag ld(const __half* p) {
+    return *reinterpret_cast<const frag*>(p);
+  }
+  __device__ __forceinline__ static elem cv(float x) { return (_Float16)x; }
+  __device__ __forceinline__ static float rnd(float x) { return (float)(_Float16)x; }
+};
+
+// Round a float through storage type T (what a stored-then-reloaded value is).
+template <typename T> __device__ __forceinline__ float rnd_t(float x) { return MM<T>::rnd(x); }
+
+// Dispatch a templated lambda over the activation storage dtype.
+#define DPA_DISPATCH_T(dt, ...)                                  \
+  do {                                                           \
+    switch (dt) {                                                \
+      case ::dpa::DT::F32: { typedef float T; __VA_ARGS__; break; }          \
+      case ::dpa::DT::BF16: { typedef __hip_bfloat16 T; __VA_ARGS__; break; } \
+      case ::dpa::DT::F16: { typedef __half T; __VA_ARGS__; break; }         \
+    }                                                            \
+  } while (0)
+
+template <typename T> inline T* dptr(const at::Tensor& t) {
+  return reinterpret_cast<T*>(t.data_ptr());
+}
+
+constexpr int ceil_to(int x, int m) { return (x + m - 1) / m * m; }
+
 }  // namespace dpa

@@ -1,0 +1,312 @@
+// Classifier head: Linear (MFMA small GEMM) and CrossEntropyLoss (fused
+// log-softmax + NLL + analytic gradient), plus the eval accuracy counter.
+// reference: /root/reference/origin_main.py:24,30,63 (fc, criterion),
+//            ddp_main.py:104-107 (argmax == label accumulation).
+#include "common.h"
+
+namespace dpa {
+namespace head {
+
+constexpr int NTHR = 256;
+
+// 8 K-consecutive elements of row `row` of a [rows][K] matrix of storage type
+// S starting at k0, converted to MFMA element type of T; zero outside bounds.
+template <typename T, typename S>
+__device__ __forceinline__ typename MM<T>::frag load_row8(const S* base, int row, int rows, int k0, int K) {
+  typename MM<T>::frag f;
+  const bool rv = row < rows;
+  const S* p = base + (size_t)(rv ? row : 0) * K;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = k0 + j;
+    const float v = (rv && k < K) ? Cvt<S>::to_f(p[k]) : 0.f;
+    f[j] = MM<T>::cv(v);
+  }
+  return f;
+}
+// 8 consecutive-row elements of column `col`: base[(k0+j)*ld + col]
+template <typename T, typename S>
+__device__ __forceinline__ typename MM<T>::frag load_col8(const S* base, int col, int cols, int k0, int K,
+                                                          int ld) {
+  typename MM<T>::frag f;
+  const bool cv = col < cols;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = k0 + j;
+    const float v = (cv && k < K) ? Cvt<S>::to_f(base[(size_t)k * ld + col]) : 0.f;
+    f[j] = MM<T>::cv(v);
+  }
+  return f;
+}
+
+// out[M][N] = x[M][K] . w[N][K]^T + b ; one 16x16 tile per block, K split over
+// the 4 waves, partials reduced through LDS.
+template <typename T>
+__global__ void __launch_bounds__(NTHR)
+linear_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w, const float* __restrict__ b,
+                  T* __restrict__ out, int M, int N, int K) {
+  __shared__ f32x4 part[NTHR / 64][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int mt = blockIdx.x, nt = blockIdx.y;
+  const int KS = (K + 31) / 32;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int s = wv; s < KS; s += NTHR / 64) {
+    const int k0 = 32 * s + 8 * q;
+    const auto a = load_row8<T, T>(x, mt * 16 + r, M, k0, K);
+    const auto bf = load_row8<T, float>(w, nt * 16 + r, N, k0, K);
+    acc = MM<T>::mma(a, bf, acc);
+  }
+  part[wv][lane] = acc;
+  __syncthreads();
+  if (wv == 0) {
+    f32x4 t = part[0][lane];
+#pragma unroll
+    for (int i = 1; i < NTHR / 64; ++i) t += part[i][lane];
+    const int col = nt * 16 + r;
+    if (col < N) {
+      const float bb = b ? b[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = mt * 16 + 4 * q + i;
+        if (row < M) out[(size_t)row * N + col] = Cvt<T>::from_f(t[i] + bb);
+      }
+    }
+  }
+}
+
+// dx[M][K] = dout[M][N] . w[N][K];  dw[N][K] = dout^T . x;  db[N] = sum_m dout
+// Block j owns columns [64j, 64j+64) of K, wave wv 16 of them.
+template <typename T>
+__global__ void __launch_bounds__(NTHR)
+linear_bwd_kernel(const T* __restrict__ dout, const T* __restrict__ x, const float* __restrict__ w,
+                  T* __restrict__ dx, float* __restrict__ dw, float* __restrict__ db, int M, int N, int K) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int c0 = blockIdx.x * 64 + wv * 16;
+  if (dx != nullptr) {
+    const int NS = (N + 31) / 32;
+    for (int mt = 0; mt * 16 < M; ++mt) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < NS; ++s) {
+        const int n0 = 32 * s + 8 * q;
+        const auto a = load_row8<T, T>(dout, mt * 16 + r, M, n0, N);
+        const auto bf = load_col8<T, float>(w, c0 + r, K, n0, N, K);
+        acc = MM<T>::mma(a, bf, acc);
+      }
+      const int col = c0 + r;
+      if (col < K) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = mt * 16 + 4 * q + i;
+          if (row < M) dx[(size_t)row * K + col] = Cvt<T>::from_f(acc[i]);
+        }
+      }
+    }
+  }
+  {
+    const int MS = (M + 31) / 32;
+    for (int nt = 0; nt * 16 < N; ++nt) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < MS; ++s) {
+        const int m0 = 32 * s + 8 * q;
+        const auto a = load_col8<T, T>(dout, nt * 16 + r, N, m0, M, N);  // dout^T row n
+        const auto bf = load_col8<T, T>(x, c0 + r, K, m0, M, K);
+        acc = MM<T>::mma(a, bf, acc);
+      }
+      const int col = c0 + r;
+      if (col < K) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = nt * 16 + 4 * q + i;
+          if (row < N) dw[(size_t)row * K + col] = acc[i];
+        }
+      }
+    }
+  }
+  if (db != nullptr && blockIdx.x == 0) {
+    for (int n = threadIdx.x; n < N; n += NTHR) {
+      float a = 0.f;
+      for (int m = 0; m < M; ++m) a += Cvt<T>::to_f(dout[(size_t)m * N + n]);
+      db[n] = a;
+    }
+  }
+}
+
+// Cross-entropy (mean over non-ignored rows) of logits [B][N] (storage T,
+// math f32).  Writes loss[0] and dlog[b][n] = (softmax - onehot)/count, f32.
+// One workgroup, one wave per row (rows strided over waves).
+template <typename T>
+__global__ void __launch_bounds__(1024)
+ce_fwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ target, float* __restrict__ loss,
+              float* __restrict__ dlog, int B, int N, int64_t ignore_index, float smoothing) {
+  __shared__ float red[2 * 16];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  float lsum = 0.f, cnt = 0.f;
+  for (int b = wv; b < B; b += nw) {
+    const T* row = logits + (size_t)b * N;
+    const int64_t t = target[b];
+    float mx = -INFINITY;
+    for (int n = lane; n < N; n += 64) mx = fmaxf(mx, Cvt<T>::to_f(row[n]));
+    mx = wave_max(mx);
+    float se = 0.f, sx = 0.f;
+    for (int n = lane; n < N; n += 64) {
+      const float v = Cvt<T>::to_f(row[n]);
+      se += __expf(v - mx);
+      sx += v;
+    }
+    se = wave_sum(se);
+    sx = wave_sum(sx);
+    const float lse = mx + __logf(se);
+    if (t != ignore_index) {
+      const float xt = Cvt<T>::to_f(row[t]);
+      // (1-eps)*(lse - x_t) + eps*(lse - mean_n x_n)
+      lsum += (1.f - smoothing) * (lse - xt) + smoothing * (lse - sx / (float)N);
+      cnt += 1.f;
+    }
+    // stash lse in dlog[b][0] temporarily? no: recompute below (cheap)
+  }
+  if (lane == 0) { red[wv] = lsum; red[16 + wv] = cnt; }
+  __syncthreads();
+  float tl = 0.f, tc = 0.f;
+  for (int i = 0; i < nw; ++i) { tl += red[i]; tc += red[16 + i]; }
+  if (threadIdx.x == 0) loss[0] = tc > 0.f ? tl / tc : NAN;
+  const float inv = tc > 0.f ? 1.f / tc : 0.f;
+  for (int b = wv; b < B; b += nw) {
+    const T* row = logits + (size_t)b * N;
+    const int64_t t = target[b];
+    float* drow = dlog + (size_t)b * N;
+    if (t == ignore_index) {
+      for (int n = lane; n < N; n += 64) drow[n] = 0.f;
+      continue;
+    }
+    float mx = -INFINITY;
+    for (int n = lane; n < N; n += 64) mx = fmaxf(mx, Cvt<T>::to_f(row[n]));
+    mx = wave_max(mx);
+    float se = 0.f;
+    for (int n = lane; n < N; n += 64) se += __expf(Cvt<T>::to_f(row[n]) - mx);
+    se = wave_sum(se);
+    const float rs = 1.f / se;
+    for (int n = lane; n < N; n += 64) {
+      const float sm = __expf(Cvt<T>::to_f(row[n]) - mx) * rs;
+      const float oh = (n == t ? 1.f - smoothing : 0.f) + smoothing / (float)N;
+      drow[n] = (sm - oh) * inv;
+    }
+  }
+}
+
+// dlogits (storage T) = dlog * grad[0]
+template <typename T>
+__global__ void ce_bwd_kernel(const float* __restrict__ dlog, const float* __restrict__ grad,
+                              T* __restrict__ out, int n) {
+  const int i = blockIdx.x * NTHR + threadIdx.x;
+  if (i < n) out[i] = Cvt<T>::from_f(dlog[i] * grad[0]);
+}
+
+// counters[0] += B ; counters[1] += #(argmax(logits[b]) == target[b])
+template <typename T>
+__global__ void __launch_bounds__(NTHR)
+accuracy_kernel(const T* __restrict__ logits, const int64_t* __restrict__ target,
+                float* __restrict__ counters, int B, int N) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float correct = 0.f;
+  for (int b = blockIdx.x * (NTHR / 64) + wv; b < B; b += gridDim.x * (NTHR / 64)) {
+    const T* row = logits + (size_t)b * N;
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int n = lane; n < N; n += 64) {
+      const float v = Cvt<T>::to_f(row[n]);
+      if (v > best || (v == best && n < bi)) { best = v; bi = n; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+    }
+    if (lane == 0 && bi == target[b]) correct += 1.f;
+  }
+  if (lane == 0 && correct != 0.f) atomicAdd(&counters[1], correct);
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&counters[0], (float)B);
+}
+
+void linear_fwd(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> b, at::Tensor out) {
+  DPA_CHECK_INPUT(x); DPA_CHECK_INPUT(w); DPA_CHECK_INPUT(out);
+  TORCH_CHECK(w.scalar_type() == at::kFloat && out.scalar_type() == x.scalar_type());
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  TORCH_CHECK(w.size(1) == K && out.size(0) == M && out.size(1) == N);
+  if (M == 0) return;
+  const float* bp = b.has_value() ? b->data_ptr<float>() : nullptr;
+  const dim3 grid((M + 15) / 16, (N + 15) / 16);
+  DPA_DISPATCH_T(dt_of(x), {
+    hipLaunchKernelGGL(linear_fwd_kernel<T>, grid, dim3(NTHR), 0, cur_stream(), dptr<T>(x),
+                       w.data_ptr<float>(), bp, dptr<T>(out), M, N, K);
+  });
+  DPA_CHECK_LAUNCH();
+}
+
+void linear_bwd(at::Tensor dout, at::Tensor x, at::Tensor w, c10::optional<at::Tensor> dx, at::Tensor dw,
+                c10::optional<at::Tensor> db) {
+  DPA_CHECK_INPUT(dout); DPA_CHECK_INPUT(x); DPA_CHECK_INPUT(w); DPA_CHECK_INPUT(dw);
+  TORCH_CHECK(dout.scalar_type() == x.scalar_type());
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  if (M == 0) { dw.zero_(); if (db) db->zero_(); return; }
+  const dim3 grid((K + 63) / 64);
+  DPA_DISPATCH_T(dt_of(x), {
+    hipLaunchKernelGGL(linear_bwd_kernel<T>, grid, dim3(NTHR), 0, cur_stream(), dptr<T>(dout), dptr<T>(x),
+                       w.data_ptr<float>(), dx.has_value() ? dptr<T>(*dx) : nullptr, dw.data_ptr<float>(),
+                       db.has_value() ? db->data_ptr<float>() : nullptr, M, N, K);
+  });
+  DPA_CHECK_LAUNCH();
+}
+
+void ce_fwd(at::Tensor logits, at::Tensor target, at::Tensor loss, at::Tensor dlog, int64_t ignore_index,
+            double smoothing) {
+  DPA_CHECK_INPUT(logits); DPA_CHECK_INPUT(target); DPA_CHECK_INPUT(loss); DPA_CHECK_INPUT(dlog);
+  TORCH_CHECK(target.scalar_type() == at::kLong && dlog.scalar_type() == at::kFloat);
+  const int B = (int)logits.size(0), N = (int)logits.size(1);
+  const int thr = B >= 16 ? 1024 : 256;
+  DPA_DISPATCH_T(dt_of(logits), {
+    hipLaunchKernelGGL(ce_fwd_kernel<T>, dim3(1), dim3(thr), 0, cur_stream(), dptr<T>(logits),
+                       target.data_ptr<int64_t>(), loss.data_ptr<float>(), dlog.data_ptr<float>(), B, N,
+                       ignore_index, (float)smoothing);
+  });
+  DPA_CHECK_LAUNCH();
+}
+
+void ce_bwd(at::Tensor dlog, at::Tensor grad, at::Tensor out) {
+  DPA_CHECK_INPUT(dlog); DPA_CHECK_INPUT(grad); DPA_CHECK_INPUT(out);
+  TORCH_CHECK(grad.scalar_type() == at::kFloat, "loss grad must be f32");
+  const int n = (int)dlog.numel();
+  if (n == 0) return;
+  DPA_DISPATCH_T(dt_of(out), {
+    hipLaunchKernelGGL(ce_bwd_kernel<T>, dim3((n + NTHR - 1) / NTHR), dim3(NTHR), 0, cur_stream(),
+                       dlog.data_ptr<float>(), grad.data_ptr<float>(), dptr<T>(out), n);
+  });
+  DPA_CHECK_LAUNCH();
+}
+
+void accuracy(at::Tensor logits, at::Tensor target, at::Tensor counters) {
+  DPA_CHECK_INPUT(logits); DPA_CHECK_INPUT(target); DPA_CHECK_INPUT(counters);
+  const int B = (int)logits.size(0), N = (int)logits.size(1);
+  if (B == 0) return;
+  const int blocks = std::min(64, (B + 3) / 4);
+  DPA_DISPATCH_T(dt_of(logits), {
+    hipLaunchKernelGGL(accuracy_kernel<T>, dim3(blocks), dim3(NTHR), 0, cur_stream(), dptr<T>(logits),
+                       target.data_ptr<int64_t>(), counters.data_ptr<float>(), B, N);
+  });
+  DPA_CHECK_LAUNCH();
+}
+
+}  // namespace head
+
+void register_head(pybind11::module& m) {
+  auto s = m.def_submodule("head", "Linear (MFMA) / CrossEntropy / accuracy kernels");
+  s.def("linear_fwd", &head::linear_fwd);
+  s.def("linear_bwd", &head::linear_bwd);
+  s.def("ce_fwd", &head::ce_fwd);
+  s.def("ce_bwd", &head::ce_bwd);
+  s.def("accuracy", &head::accuracy);
+}
+
+}  // namespace dpa

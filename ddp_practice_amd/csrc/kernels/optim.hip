@@ -1,0 +1,229 @@
+// Optimizer / AMP kernels (multi-tensor, one launch per <= MAXT tensors):
+//   amp_unscale_check : g *= 1/scale in place; found_inf |= any(!isfinite(g))
+//                       (== torch._amp_foreach_non_finite_check_and_unscale_,
+//                        torch/amp/grad_scaler.py:235-286)
+//   sgd_step          : SGD (momentum/dampening/nesterov/weight decay/maximize)
+//                       predicated on found_inf read ON DEVICE, so GradScaler.step
+//                       needs no found_inf.item() host sync (grad_scaler.py:356)
+//   amp_update_scale  : == torch._amp_update_scale_ (grad_scaler.py:500-537)
+//   flat_copy_scale   : multi-tensor gather into / scatter out of a flat bucket
+//                       with an optional scale (DDP reducer pack/unpack)
+// reference call sites: /root/reference/ddp_main.py:91-93 (scaler.scale/step/update),
+// origin_main.py:87 (SGD lr=1e-4).
+#include "common.h"
+
+#include <vector>
+
+namespace dpa {
+namespace opt {
+
+constexpr int NTHR = 256;
+constexpr int MAXT = 36;
+constexpr int CHUNK = 4096;
+
+struct MTList {
+  int n;
+  int64_t numel[MAXT];
+  int64_t chunk_off[MAXT + 1];  // prefix sum of chunks
+  float* p0[MAXT];
+  float* p1[MAXT];
+  float* p2[MAXT];
+};
+
+__device__ __forceinline__ int find_tensor(const MTList& L, int64_t c) {
+  int t = 0;
+  while (t + 1 < L.n && L.chunk_off[t + 1] <= c) ++t;
+  return t;
+}
+
+__global__ void __launch_bounds__(NTHR)
+unscale_check_kernel(MTList L, const float* __restrict__ scale, float* __restrict__ found_inf) {
+  const float inv = 1.f / scale[0];
+  const int64_t total = L.chunk_off[L.n];
+  bool bad = false;
+  for (int64_t c = blockIdx.x; c < total; c += gridDim.x) {
+    const int t = find_tensor(L, c);
+    const int64_t base = (c - L.chunk_off[t]) * CHUNK;
+    const int64_t end = min(base + (int64_t)CHUNK, L.numel[t]);
+    float* g = L.p0[t];
+    for (int64_t i = base + threadIdx.x; i < end; i += NTHR) {
+      const float v = g[i];
+      bad |= !isfinite(v);
+      g[i] = v * inv;
+    }
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) found_inf[0] = 1.f;
+}
+
+// p0 = param, p1 = grad, p2 = momentum buffer (may be null)
+__global__ void __launch_bounds__(NTHR)
+sgd_kernel(MTList L, float lr, float momentum, float dampening, float wd, int nesterov, int maximize,
+           int first, const float* __restrict__ found_inf, const float* __restrict__ grad_scale) {
+  if (found_inf != nullptr && found_inf[0] != 0.f) return;
+  const float gs = grad_scale ? 1.f / grad_scale[0] : 1.f;
+  const int64_t total = L.chunk_off[L.n];
+  for (int64_t c = blockIdx.x; c < total; c += gridDim.x) {
+    const int t = find_tensor(L, c);
+    const int64_t base = (c - L.chunk_off[t]) * CHUNK;
+    const int64_t end = min(base + (int64_t)CHUNK, L.numel[t]);
+    float* p = L.p0[t];
+    const float* g = L.p1[t];
+    float* buf = L.p2[t];
+    for (int64_t i = base + threadIdx.x; i < end; i += NTHR) {
+      float d = g[i] * gs;
+      if (maximize) d = -d;
+      if (wd != 0.f) d += wd * p[i];
+      if (momentum != 0.f) {
+        float bv = first ? d : momentum * buf[i] + (1.f - dampening) * d;
+        buf[i] = bv;
+        d = nesterov ? d + momentum * bv : bv;
+      }
+      p[i] -= lr * d;
+    }
+  }
+}
+
+__global__ void update_scale_kernel(float* scale, int* tracker, const float* found_inf, float growth,
+                                    float backoff, int interval) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (found_inf[0] != 0.f) {
+    scale[0] = scale[0] * backoff;
+    tracker[0] = 0;
+  } else {
+    const int succ = tracker[0] + 1;
+    if (succ == interval) {
+      const float ns = scale[0] * growth;
+      if (isfinite(ns)) scale[0] = ns;
+      tracker[0] = 0;
+    } else {
+      tracker[0] = succ;
+    }
+  }
+}
+
+// direction 0: flat[off_t + i] = src_t[i] * s ; direction 1: dst_t[i] = flat[off_t + i] * s
+__global__ void __launch_bounds__(NTHR)
+flat_copy_kernel(MTList L, float* __restrict__ flat, float s, int direction) {
+  const int64_t total = L.chunk_off[L.n];
+  for (int64_t c = blockIdx.x; c < total; c += gridDim.x) {
+    const int t = find_tensor(L, c);
+    const int64_t base = (c - L.chunk_off[t]) * CHUNK;
+    const int64_t end = min(base + (int64_t)CHUNK, L.numel[t]);
+    float* ext = L.p0[t];
+    float* fl = flat + reinterpret_cast<int64_t>(L.p1[t]);  // p1 carries the element offset
+    if (direction == 0)
+      for (int64_t i = base + threadIdx.x; i < end; i += NTHR) fl[i] = ext[i] * s;
+    else
+      for (int64_t i = base + threadIdx.x; i < end; i += NTHR) ext[i] = fl[i] * s;
+  }
+}
+
+// Build MTList batches of <= MAXT tensors.
+template <typename F>
+static void for_batches(size_t n, F&& f) {
+  for (size_t s = 0; s < n; s += MAXT) f(s, std::min(n, s + MAXT));
+}
+
+static int grid_for(int64_t chunks) { return (int)std::max<int64_t>(1, std::min<int64_t>(chunks, 2048)); }
+
+static void check_f32(const at::Tensor& t) {
+  DPA_CHECK_INPUT(t);
+  TORCH_CHECK(t.scalar_type() == at::kFloat, "optimizer tensors must be f32");
+}
+
+void unscale_check(std::vector<at::Tensor> grads, at::Tensor scale, at::Tensor found_inf) {
+  check_f32(scale); check_f32(found_inf);
+  for_batches(grads.size(), [&](size_t s, size_t e) {
+    MTList L{};
+    L.n = (int)(e - s);
+    L.chunk_off[0] = 0;
+    for (size_t i = s; i < e; ++i) {
+      check_f32(grads[i]);
+      const int k = (int)(i - s);
+      L.numel[k] = grads[i].numel();
+      L.p0[k] = grads[i].data_ptr<float>();
+      L.chunk_off[k + 1] = L.chunk_off[k] + (L.numel[k] + CHUNK - 1) / CHUNK;
+    }
+    hipLaunchKernelGGL(unscale_check_kernel, dim3(grid_for(L.chunk_off[L.n])), dim3(NTHR), 0, cur_stream(), L,
+                       scale.data_ptr<float>(), found_inf.data_ptr<float>());
+    DPA_CHECK_LAUNCH();
+  });
+}
+
+void sgd_step(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std::vector<at::Tensor> bufs,
+              double lr, double momentum, double dampening, double wd, bool nesterov, bool maximize, bool first,
+              c10::optional<at::Tensor> found_inf, c10::optional<at::Tensor> grad_scale) {
+  TORCH_CHECK(params.size() == grads.size());
+  TORCH_CHECK(bufs.empty() || bufs.size() == params.size());
+  const float* fi = found_inf.has_value() ? found_inf->data_ptr<float>() : nullptr;
+  const float* gsp = grad_scale.has_value() ? grad_scale->data_ptr<float>() : nullptr;
+  for_batches(params.size(), [&](size_t s, size_t e) {
+    MTList L{};
+    L.n = (int)(e - s);
+    L.chunk_off[0] = 0;
+    for (size_t i = s; i < e; ++i) {
+      check_f32(params[i]); check_f32(grads[i]);
+      TORCH_CHECK(params[i].numel() == grads[i].numel());
+      const int k = (int)(i - s);
+      L.numel[k] = params[i].numel();
+      L.p0[k] = params[i].data_ptr<float>();
+      L.p1[k] = grads[i].data_ptr<float>();
+      L.p2[k] = bufs.empty() ? nullptr : bufs[i].data_ptr<float>();
+      L.chunk_off[k + 1] = L.chunk_off[k] + (L.numel[k] + CHUNK - 1) / CHUNK;
+    }
+    hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(L.chunk_off[L.n])), dim3(NTHR), 0, cur_stream(), L, (float)lr,
+                       (float)momentum, (float)dampening, (float)wd, (int)nesterov, (int)maximize, (int)first, fi,
+                       gsp);
+    DPA_CHECK_LAUNCH();
+  });
+}
+
+void update_scale(at::Tensor scale, at::Tensor tracker, at::Tensor found_inf, double growth, double backoff,
+                  int64_t interval) {
+  check_f32(scale); check_f32(found_inf);
+  TORCH_CHECK(tracker.scalar_type() == at::kInt);
+  hipLaunchKernelGGL(update_scale_kernel, dim3(1), dim3(64), 0, cur_stream(), scale.data_ptr<float>(),
+                     tracker.data_ptr<int>(), found_inf.data_ptr<float>(), (float)growth, (float)backoff,
+                     (int)interval);
+  DPA_CHECK_LAUNCH();
+}
+
+// Copy tensors into (direction 0) / out of (direction 1) a flat f32 buffer at
+// the given element offsets, multiplying by `s`.
+void flat_copy(std::vector<at::Tensor> tensors, std::vector<int64_t> offsets, at::Tensor flat, double s,
+               int64_t direction) {
+  check_f32(flat);
+  TORCH_CHECK(tensors.size() == offsets.size());
+  for_batches(tensors.size(), [&](size_t b, size_t e) {
+    MTList L{};
+    L.n = (int)(e - b);
+    L.chunk_off[0] = 0;
+    for (size_t i = b; i < e; ++i) {
+      check_f32(tensors[i]);
+      TORCH_CHECK(offsets[i] + tensors[i].numel() <= flat.numel());
+      const int k = (int)(i - b);
+      L.numel[k] = tensors[i].numel();
+      L.p0[k] = tensors[i].data_ptr<float>();
+      L.p1[k] = reinterpret_cast<float*>(offsets[i]);
+      L.chunk_off[k + 1] = L.chunk_off[k] + (L.numel[k] + CHUNK - 1) / CHUNK;
+    }
+    hipLaunchKernelGGL(flat_copy_kernel, dim3(grid_for(L.chunk_off[L.n])), dim3(NTHR), 0, cur_stream(), L,
+                       flat.data_ptr<float>(), (float)s, (int)direction);
+    DPA_CHECK_LAUNCH();
+  });
+}
+
+}  // namespace opt
+
+void register_optim(pybind11::module& m) {
+  auto s = m.def_submodule("optim", "multi-tensor SGD / AMP GradScaler kernels");
+  s.def("unscale_check", &opt::unscale_check);
+  s.def("sgd_step", &opt::sgd_step, pybind11::arg("params"), pybind11::arg("grads"), pybind11::arg("bufs"),
+        pybind11::arg("lr"), pybind11::arg("momentum"), pybind11::arg("dampening"), pybind11::arg("weight_decay"),
+        pybind11::arg("nesterov"), pybind11::arg("maximize"), pybind11::arg("first"),
+        pybind11::arg("found_inf") = pybind11::none(), pybind11::arg("grad_scale") = pybind11::none());
+  s.def("update_scale", &opt::update_scale);
+  s.def("flat_copy", &opt::flat_copy);
+}
+
+}  // namespace dpa

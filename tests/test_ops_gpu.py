@@ -1,0 +1,216 @@
+"""Numerics of the native HIP kernels vs plain PyTorch fp32 references."""
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _block(cin, cout, seed=0):
+    torch.manual_seed(seed)
+    conv = nn.Conv2d(cin, cout, 5, 1, 2)
+    bn = nn.BatchNorm2d(cout)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+        bn.running_mean.uniform_(-0.1, 0.1)
+        bn.running_var.uniform_(0.5, 1.5)
+    return conv.to(DEV), bn.to(DEV)
+
+
+def _ref_block(x, conv, bn):
+    y = F.conv2d(x, conv.weight, conv.bias, 1, 2)
+    return F.max_pool2d(F.relu(bn(y)), 2, 2)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("cin,cout,hw", [(1, 16, 28), (16, 32, 14)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B", [32, 12])
+def test_conv_block_fwd_bwd(C, cin, cout, hw, dtype, B):
+    """fp32: tight vs the fp32 reference.  bf16/fp16: error vs the fp32
+    reference must be within 2x of torch's own autocast error (+ floor)."""
+    from ddp_practice_amd.ops.convblock import conv_block
+
+    conv, bn = _block(cin, cout)
+    conv_r, bn_r = copy.deepcopy(conv), copy.deepcopy(bn)
+    conv_l, bn_l = copy.deepcopy(conv), copy.deepcopy(bn)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    x = torch.rand(B, cin, hw, hw, generator=g).to(DEV)
+    xr = x.clone().requires_grad_(cin > 1)
+    xl = x.clone().requires_grad_(cin > 1)
+    xn = x.clone().to(dtype).requires_grad_(cin > 1)
+    out = conv_block(xn, conv, bn, cdtype=dtype)
+    ref = _ref_block(xr, conv_r, bn_r)
+    lp = dtype != torch.float32
+    if lp:
+        with torch.autocast("cuda", dtype=dtype):
+            ref_l = _ref_block(xl, conv_l, bn_l)
+
+    def bound(a, r, l, floor):
+        e = _rel(a, r)
+        lim = max(2.0 * _rel(l, r), floor) if lp else floor
+        assert e < lim, (e, lim)
+
+    assert out.dtype == dtype
+    bound(out, ref, ref_l if lp else None, 2e-5 if not lp else 5e-3)
+    st = 1e-4 if dtype == torch.float32 else 1e-2
+    torch.testing.assert_close(bn.running_mean, bn_r.running_mean, rtol=st, atol=st)
+    torch.testing.assert_close(bn.running_var, bn_r.running_var, rtol=st, atol=st)
+    assert int(bn.num_batches_tracked) == int(bn_r.num_batches_tracked) == 1
+    go = torch.randn(ref.shape, generator=g).to(DEV)
+    ref.backward(go)
+    out.backward(go.to(dtype))
+    if lp:
+        ref_l.backward(go.to(ref_l.dtype))
+    fl = 1e-4 if not lp else 5e-3
+    bound(conv.weight.grad, conv_r.weight.grad, conv_l.weight.grad if lp else None, fl)
+    bound(bn.weight.grad, bn_r.weight.grad, bn_l.weight.grad if lp else None, fl)
+    bound(bn.bias.grad, bn_r.bias.grad, bn_l.bias.grad if lp else None, fl)
+    # conv bias grad is ~0 analytically (BN follows); compare absolutely
+    db_err = (conv.bias.grad - conv_r.bias.grad).abs().max().item()
+    db_lim = 2.0 * (conv_l.bias.grad - conv_r.bias.grad).abs().max().item() + 1e-2 if lp else 2e-3
+    assert db_err < db_lim, (db_err, db_lim)
+    if cin > 1:
+        bound(xn.grad, xr.grad, xl.grad if lp else None, fl)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv_block_eval(C, dtype):
+    from ddp_practice_amd.ops.convblock import conv_block
+
+    conv, bn = _block(16, 32)
+    bn.eval()
+    x = torch.rand(8, 16, 14, 14, device=DEV)
+    with torch.no_grad():
+        out = conv_block(x.to(dtype), conv, bn, cdtype=dtype)
+        ref = _ref_block(x, conv, bn)
+    assert _rel(out, ref) < (2e-5 if dtype == torch.float32 else 2e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(32, 10, 1568), (7, 10, 1568), (40, 33, 100)])
+def test_linear(C, dtype, M, N, K):
+    from ddp_practice_amd.ops.head import linear
+
+    torch.manual_seed(0)
+    lin = nn.Linear(K, N).to(DEV)
+    x = torch.randn(M, K, device=DEV)
+    xr = x.clone().requires_grad_()
+    xn = x.clone().to(dtype).requires_grad_()
+    w = lin.weight.detach().clone().requires_grad_()
+    b = lin.bias.detach().clone().requires_grad_()
+    out = linear(xn, w, b, cdtype=dtype)
+    ref = F.linear(xr, lin.weight, lin.bias)
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert _rel(out, ref) < tol
+    go = torch.randn(M, N, device=DEV)
+    out.backward(go.to(dtype))
+    ref.backward(go)
+    assert _rel(w.grad, lin.weight.grad) < tol * 2
+    assert _rel(b.grad, lin.bias.grad) < tol * 2
+    assert _rel(xn.grad, xr.grad) < tol * 2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+def test_cross_entropy(C, dtype):
+    from ddp_practice_amd.ops.head import cross_entropy
+
+    torch.manual_seed(0)
+    logits = (torch.randn(32, 10, device=DEV) * 3).to(dtype)
+    tgt = torch.randint(0, 10, (32,), device=DEV)
+    tgt[3] = -100
+    a = logits.clone().requires_grad_()
+    r = logits.float().clone().requires_grad_()
+    loss = cross_entropy(a, tgt)
+    ref = F.cross_entropy(r, tgt)
+    torch.testing.assert_close(loss, ref, rtol=1e-5, atol=1e-5)
+    (loss * 3).backward()
+    (ref * 3).backward()
+    torch.testing.assert_close(a.grad.float(), r.grad, rtol=1e-2, atol=1e-3)
+
+
+def test_accuracy(C):
+    from ddp_practice_amd.ops.head import accuracy_
+
+    logits = torch.randn(37, 10, device=DEV)
+    tgt = torch.randint(0, 10, (37,), device=DEV)
+    cnt = torch.zeros(2, device=DEV)
+    accuracy_(logits, tgt, cnt)
+    assert cnt[0].item() == 37
+    assert cnt[1].item() == (logits.argmax(1) == tgt).sum().item()
+
+
+def test_sgd_and_scaler_kernels(C):
+    torch.manual_seed(0)
+    ps = [torch.randn(n, device=DEV) for n in (5, 5000, 29034)]
+    gs = [torch.randn_like(p) * 1024 for p in ps]
+    scale = torch.tensor([1024.0], device=DEV)
+    fi = torch.zeros(1, device=DEV)
+    ref_p = [p.clone() for p in ps]
+    ref_g = [g.clone() / 1024 for g in gs]
+    C.optim.unscale_check(gs, scale, fi)
+    assert fi.item() == 0
+    for g, r in zip(gs, ref_g):
+        torch.testing.assert_close(g, r)
+    bufs = [torch.zeros_like(p) for p in ps]
+    C.optim.sgd_step(ps, gs, bufs, 0.1, 0.9, 0.0, 1e-4, False, False, True, fi, None)
+    opt = torch.optim.SGD([torch.nn.Parameter(p) for p in ref_p], lr=0.1, momentum=0.9, weight_decay=1e-4)
+    for p, g in zip(opt.param_groups[0]["params"], ref_g):
+        p.grad = g
+    opt.step()
+    for p, r in zip(ps, opt.param_groups[0]["params"]):
+        torch.testing.assert_close(p, r.detach())
+    # inf -> found_inf set, step skipped
+    gs[1][7] = float("inf")
+    before = [p.clone() for p in ps]
+    fi.zero_()
+    C.optim.unscale_check(gs, scale, fi)
+    assert fi.item() == 1
+    C.optim.sgd_step(ps, gs, bufs, 0.1, 0.9, 0.0, 0.0, False, False, False, fi, None)
+    for p, b in zip(ps, before):
+        assert torch.equal(p, b)
+    # update_scale semantics
+    tr = torch.zeros(1, dtype=torch.int32, device=DEV)
+    C.optim.update_scale(scale, tr, fi, 2.0, 0.5, 3)
+    assert scale.item() == 512 and tr.item() == 0
+    fi.zero_()
+    for i in range(3):
+        C.optim.update_scale(scale, tr, fi, 2.0, 0.5, 3)
+    assert scale.item() == 1024 and tr.item() == 0
+
+
+def test_flat_copy(C):
+    ts = [torch.randn(n, device=DEV) for n in (3, 4097, 10)]
+    offs = [0, 3, 4100]
+    flat = torch.zeros(4110, device=DEV)
+    C.optim.flat_copy(ts, offs, flat, 0.5, 0)
+    torch.testing.assert_close(flat, torch.cat(ts) * 0.5)
+    outs = [torch.empty_like(t) for t in ts]
+    C.optim.flat_copy(outs, offs, flat, 2.0, 1)
+    for o, t in zip(outs, ts):
+        torch.testing.assert_close(o, t)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gather(C, dtype):
+    imgs = torch.randint(0, 256, (100, 28, 28), dtype=torch.uint8, device=DEV)
+    labels = torch.randint(0, 10, (100,), device=DEV)
+    order = torch.randperm(100, device=DEV)
+    ctr = torch.zeros(2, dtype=torch.int32, device=DEV)
+    out = torch.empty(32, 1, 28, 28, dtype=dtype, device=DEV)
+    lab = torch.empty(32, dtype=torch.long, device=DEV)
+    for step in range(3):
+        C.data.gather(imgs, labels, order, ctr, -1, out, lab, 1 / 255.0, 0.0)
+        sel = order[step * 32:(step + 1) * 32]
+        torch.testing.assert_close(out.float(), (imgs[sel].float() / 255).unsqueeze(1).to(dtype).float())
+        assert torch.equal(lab, labels[sel])
+    assert ctr.tolist() == [3, 0]
