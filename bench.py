@@ -1,0 +1,159 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: ConvNet DDP + AMP training step, images/s for the whole node.
+
+Config (BASELINE.json): the reference's ddp_main.py training step — ConvNet
+(29,034 params), batch 32 per rank (weak scaling), SGD(lr=1e-4), SyncBN,
+AMP autocast + GradScaler (bf16 here), DistributedSampler order, synthetic
+1x28x28 MNIST-shaped data, random-init weights.  One process per GPU over
+RCCL.  Each timed step = data gather + forward + loss + backward (+ SyncBN /
+DDP all-reduces) + unscale/inf-check + SGD + scale update, replayed from a
+captured hipGraph.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+BASELINE_IMG_S = {1: 7923.0, 2: 5840.0}  # BASELINE.md (derived from README.md:201 / :466)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--batch-size", type=int, default=32)
+    ap.add_argument("--amp-dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--steps-per-graph", type=int, default=16)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-sync-bn", action="store_true")
+    args = ap.parse_args(argv)
+
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import ddp_practice_amd as dpa
+    from ddp_practice_amd import distributed as ddist
+    from ddp_practice_amd.amp import GradScaler
+    from ddp_practice_amd.data import DeviceLoader, DistributedSampler, synthetic
+    from ddp_practice_amd.models import ConvNet
+    from ddp_practice_amd.ops.head import cross_entropy
+    from ddp_practice_amd.optim import SGD
+    from ddp_practice_amd.parallel import DistributedDataParallel, convert_sync_batchnorm
+    from ddp_practice_amd.runtime import CapturedStep
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("for --gpus N>1 launch with torchrun --nproc-per-node N")
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        ddist.init_process_group(backend="nccl")
+    rank = ddist.get_rank()
+
+    amp = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": None}[args.amp_dtype]
+    torch.manual_seed(0)
+    model = ConvNet(amp_dtype=amp).to(dev)
+    if world > 1:
+        if not args.no_sync_bn:
+            model = convert_sync_batchnorm(model)
+        model = DistributedDataParallel(model, device_ids=[local_rank])
+    optimizer = SGD(model.parameters(), lr=1e-4)
+    scaler = GradScaler(enabled=amp is not None)
+
+    ds = synthetic(60000, seed=1)
+    sampler = DistributedSampler(ds, num_replicas=world, rank=rank)
+    loader = DeviceLoader(ds, batch_size=args.batch_size, sampler=sampler, device=dev,
+                          dtype=amp if amp is not None else torch.float32)
+    images, labels = loader.static_batch()
+    loader.start_epoch()
+    nfull = len(sampler) // args.batch_size
+
+    def step():
+        loader.fill_(images, labels)
+        out = model(images)
+        loss = cross_entropy(out, labels)
+        optimizer.zero_grad(set_to_none=True)
+        scaler.scale(loss).backward()
+        scaler.step(optimizer)
+        scaler.update()
+
+    spg = 1 if args.no_graph else args.steps_per_graph
+    runner = CapturedStep(step, warmup=3, steps_per_graph=spg, enabled=not args.no_graph,
+                          pre_capture=lambda: loader.set_step(0))
+    captured = runner.capture() if not args.no_graph else False
+    if not args.no_graph and not captured and rank == 0:
+        print(f"[bench] graph capture failed, eager fallback: {runner.capture_error!r}", file=sys.stderr)
+
+    # keep the device step counter inside the epoch: restart the order when needed
+    state = {"pos": 0}
+
+    def run_chunk():
+        if state["pos"] + spg > nfull:
+            loader.set_step(0)
+            state["pos"] = 0
+        runner.run()
+        state["pos"] += spg
+
+    n_warm = max(1, args.warmup // spg)
+    for _ in range(n_warm):
+        run_chunk()
+    n_iter = max(1, args.steps // spg)
+    steps = n_iter * spg
+    ddist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n_iter):
+        run_chunk()
+    torch.cuda.synchronize()
+    ddist.barrier()
+    t1 = time.perf_counter()
+    dt = t1 - t0
+    dt_max = ddist.max_over_ranks(dt)
+    ms = dt_max / steps * 1e3
+    img_s = args.batch_size * world * steps / dt_max
+    if rank == 0:
+        base = BASELINE_IMG_S.get(world, BASELINE_IMG_S[1])
+        print(json.dumps({
+            "metric": "images/sec (whole node) + 3-epoch wall-clock, MNIST ConvNet at 1/2/4/8 MI355X",
+            "value": round(img_s, 1),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": n_warm * spg,
+            "ms_per_step": round(ms, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(img_s / base, 3),
+            "dtype": args.amp_dtype,
+            "data": "synthetic 1x28x28 MNIST-shaped uint8 (60k), random-init weights",
+            "config": {
+                "model": "ConvNet (2x[Conv5x5-BN-ReLU-MaxPool2] + Linear(1568,10), 29,034 params)",
+                "global_batch": args.batch_size * world,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "per_rank_batch": args.batch_size,
+                "sync_bn": world > 1 and not args.no_sync_bn,
+                "amp": f"autocast {args.amp_dtype} + GradScaler",
+                "optimizer": "SGD(lr=1e-4)",
+                "hipgraph": bool(captured),
+                "steps_per_graph": spg,
+                "est_3epoch_train_s": round(3 * len(loader) * ms / 1e3, 3),
+                "baseline_img_s": base,
+            },
+        }), flush=True)
+    ddist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -8,6 +8,8 @@ void register_convblock(pybind11::module& m);
 void register_head(pybind11::module& m);
 void register_optim(pybind11::module& m);
 void register_data(pybind11::module& m);
+void register_comm(pybind11::module& m);
+void register_reducer(pybind11::module& m);
 }
 
 PYBIND11_MODULE(_C, m) {
@@ -17,4 +19,6 @@ PYBIND11_MODULE(_C, m) {
   dpa::register_head(m);
   dpa::register_optim(m);
   dpa::register_data(m);
+  dpa::register_comm(m);
+  dpa::register_reducer(m);
 }

@@ -1,0 +1,263 @@
+// DDP gradient reducer: buckets, autograd post-hooks, in-order async
+// all-reduce overlapped with the rest of backward.
+//
+// Semantics of torch's C++ Reducer (torch/csrc/distributed/c10d/reducer.cpp,
+// driven from torch/nn/parallel/distributed.py:1199-1248,1521-1617) re-designed
+// for one process per MI355X:
+//  * Buckets are flat f32/bf16/f16 device buffers; the bucket plan (reverse
+//    parameter order, first bucket small, then a cap) is computed in Python and
+//    re-planned after the first iteration in actual grad-ready order.
+//  * A post-hook on each parameter's AccumulateGrad node marks it ready.  When
+//    a bucket's last gradient arrives it is packed with ONE multi-tensor kernel
+//    (grad * 1/W into the bucket) and its all-reduce is launched on the
+//    communicator's stream; buckets launch strictly in index order so every
+//    rank issues identical collective sequences.
+//  * After the last bucket launches, the compute stream is fenced on all of
+//    them and every param.grad becomes a view of its bucket (the
+//    gradient_as_bucket_view=True layout: no copy-back kernel).
+//  * Everything is enqueue-only (kernels, events, RCCL), so a whole DDP step
+//    can be captured into a hipGraph.
+#include <torch/csrc/autograd/engine.h>
+#include <torch/csrc/autograd/function.h>
+#include <torch/csrc/autograd/utils/lambda_post_hook.h>
+#include <torch/csrc/autograd/variable.h>
+
+#include <mutex>
+
+#include "comm/collective.h"
+#include "common.h"
+
+namespace dpa {
+namespace ddp {
+
+using torch::autograd::variable_list;
+
+class Reducer : public std::enable_shared_from_this<Reducer> {
+ public:
+  Reducer(std::vector<at::Tensor> params, std::vector<std::vector<int64_t>> buckets,
+          std::shared_ptr<Collective> comm, bool find_unused)
+      : params_(std::move(params)), comm_(std::move(comm)), find_unused_(find_unused) {
+    TORCH_CHECK(comm_ != nullptr);
+    ready_.assign(params_.size(), 0);
+    set_buckets(buckets);
+  }
+
+  // Register hooks (needs shared_from_this, so after construction).
+  void install_hooks() {
+    std::weak_ptr<Reducer> self = shared_from_this();
+    for (size_t i = 0; i < params_.size(); ++i) {
+      auto& p = params_[i];
+      TORCH_CHECK(p.requires_grad(), "DDP parameter ", i, " does not require grad");
+      auto acc = torch::autograd::impl::grad_accumulator(p);
+      TORCH_CHECK(acc != nullptr, "parameter ", i, " has no grad accumulator (not a leaf?)");
+      acc->add_post_hook(std::make_unique<torch::autograd::utils::LambdaPostHook>(
+          [self, i](const variable_list& outputs, const variable_list&) {
+            if (auto r = self.lock()) r->mark_ready(i);
+            return outputs;
+          }));
+      accs_.push_back(std::move(acc));
+    }
+  }
+
+  void set_buckets(const std::vector<std::vector<int64_t>>& buckets) {
+    std::lock_guard<std::mutex> g(mu_);
+    buckets_.clear();
+    param_bucket_.assign(params_.size(), -1);
+    param_offset_.assign(params_.size(), 0);
+    for (size_t b = 0; b < buckets.size(); ++b) {
+      Bucket bk;
+      int64_t off = 0;
+      at::ScalarType dt = at::kFloat;
+      for (size_t j = 0; j < buckets[b].size(); ++j) {
+        const int64_t i = buckets[b][j];
+        TORCH_CHECK(i >= 0 && i < (int64_t)params_.size(), "bad param index in bucket");
+        TORCH_CHECK(param_bucket_[i] < 0, "param ", i, " in two buckets");
+        if (j == 0) dt = params_[i].scalar_type();
+        TORCH_CHECK(params_[i].scalar_type() == dt, "bucket mixes dtypes");
+        param_bucket_[i] = (int)b;
+        param_offset_[i] = off;
+        bk.params.push_back(i);
+        bk.offsets.push_back(off);
+        off += params_[i].numel();
+      }
+      bk.flat = at::zeros({off}, params_[buckets[b].empty() ? 0 : buckets[b][0]].options().requires_grad(false));
+      buckets_.push_back(std::move(bk));
+    }
+    for (size_t i = 0; i < params_.size(); ++i)
+      TORCH_CHECK(param_bucket_[i] >= 0, "param ", i, " not assigned to a bucket");
+    reset_locked();
+  }
+
+  // Called by DDP.forward (train mode, grad enabled) before the graph is built.
+  void prepare_for_backward(bool sync) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (expect_ && !finalized_ && any_ready_)
+      TORCH_CHECK(false,
+                  "DDP: the previous iteration's reduction did not finish (some parameters received no "
+                  "gradient). Use find_unused_parameters=True if parameters can be unused.");
+    reset_locked();
+    sync_ = sync;
+    expect_ = true;
+  }
+
+  void mark_ready(size_t i) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!expect_ || !sync_) return;  // no_sync() or backward outside a DDP forward
+    if (ready_[i]) return;           // reentrant backward hits the same hook twice: ignore
+    if (!any_ready_) {
+      any_ready_ = true;
+      // finalize at the end of this backward even if some params never get a grad
+      std::weak_ptr<Reducer> self = shared_from_this();
+      torch::autograd::Engine::get_default_engine().queue_callback([self]() {
+        if (auto r = self.lock()) r->finalize();
+      });
+    }
+    ready_[i] = 1;
+    if (record_order_) order_.push_back((int64_t)i);
+    Bucket& bk = buckets_[param_bucket_[i]];
+    bk.pending -= 1;
+    launch_ready_locked();
+  }
+
+  void finalize() {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!expect_ || finalized_) return;
+    if (find_unused_) {
+      for (size_t i = 0; i < params_.size(); ++i) {
+        if (!ready_[i]) {
+          ready_[i] = 1;
+          Bucket& bk = buckets_[param_bucket_[i]];
+          bk.unused.push_back(i);
+          bk.pending -= 1;
+        }
+      }
+      launch_ready_locked();
+    }
+    for (auto& bk : buckets_)
+      TORCH_CHECK(bk.launched, "DDP: bucket not reduced at end of backward (unused parameters? set "
+                               "find_unused_parameters=True)");
+    for (size_t b = 0; b < buckets_.size(); ++b) comm_->wait((int)b);
+    // grads become views of the all-reduced buckets
+    for (auto& bk : buckets_) {
+      for (size_t j = 0; j < bk.params.size(); ++j) {
+        auto& p = params_[bk.params[j]];
+        at::Tensor view = bk.flat.narrow(0, bk.offsets[j], p.numel()).view(p.sizes());
+        p.mutable_grad() = view;
+      }
+    }
+    finalized_ = true;
+    record_order_ = false;
+  }
+
+  std::vector<int64_t> ready_order() const { return order_; }
+  int64_t num_buckets() const { return (int64_t)buckets_.size(); }
+  std::vector<at::Tensor> bucket_tensors() const {
+    std::vector<at::Tensor> v;
+    for (auto& b : buckets_) v.push_back(b.flat);
+    return v;
+  }
+  std::vector<std::vector<int64_t>> bucket_indices() const {
+    std::vector<std::vector<int64_t>> v;
+    for (auto& b : buckets_) v.push_back(b.params);
+    return v;
+  }
+  void set_record_order(bool on) {
+    record_order_ = on;
+    if (on) order_.clear();
+  }
+
+ private:
+  struct Bucket {
+    std::vector<int64_t> params, offsets;
+    std::vector<int64_t> unused;
+    at::Tensor flat;
+    int64_t pending = 0;
+    bool launched = false;
+  };
+
+  void reset_locked() {
+    std::fill(ready_.begin(), ready_.end(), 0);
+    for (auto& bk : buckets_) {
+      bk.pending = (int64_t)bk.params.size();
+      bk.launched = false;
+      bk.unused.clear();
+    }
+    next_launch_ = 0;
+    any_ready_ = false;
+    finalized_ = false;
+    expect_ = false;
+  }
+
+  // launch every complete bucket whose predecessors have launched
+  void launch_ready_locked() {
+    while (next_launch_ < buckets_.size() && buckets_[next_launch_].pending == 0) {
+      Bucket& bk = buckets_[next_launch_];
+      std::vector<at::Tensor> srcs;
+      std::vector<int64_t> offs;
+      const double inv_w = 1.0 / (double)comm_->world();
+      for (size_t j = 0; j < bk.params.size(); ++j) {
+        const int64_t i = bk.params[j];
+        at::Tensor gr = params_[i].grad();
+        const bool unused = std::find(bk.unused.begin(), bk.unused.end(), i) != bk.unused.end();
+        if (unused || !gr.defined()) {
+          bk.flat.narrow(0, bk.offsets[j], params_[i].numel()).zero_();
+          continue;
+        }
+        TORCH_CHECK(gr.numel() == params_[i].numel());
+        srcs.push_back(gr.is_contiguous() ? gr.view({-1}) : gr.contiguous().view({-1}));
+        offs.push_back(bk.offsets[j]);
+      }
+      if (!srcs.empty()) {
+        if (bk.flat.is_cuda() && bk.flat.scalar_type() == at::kFloat) {
+          opt::flat_copy(srcs, offs, bk.flat, inv_w, 0);
+        } else {
+          for (size_t k = 0; k < srcs.size(); ++k)
+            bk.flat.narrow(0, offs[k], srcs[k].numel()).copy_(srcs[k]).mul_(inv_w);
+        }
+      }
+      comm_->all_reduce_async(bk.flat, RedOp::SUM, (int)next_launch_);
+      bk.launched = true;
+      ++next_launch_;
+    }
+  }
+
+  std::vector<at::Tensor> params_;
+  std::vector<std::shared_ptr<torch::autograd::Node>> accs_;
+  std::shared_ptr<Collective> comm_;
+  bool find_unused_;
+  std::vector<Bucket> buckets_;
+  std::vector<int> param_bucket_;
+  std::vector<int64_t> param_offset_;
+  std::vector<char> ready_;
+  size_t next_launch_ = 0;
+  bool any_ready_ = false, finalized_ = false, expect_ = false, sync_ = true;
+  bool record_order_ = true;
+  std::vector<int64_t> order_;
+  std::mutex mu_;
+};
+
+}  // namespace ddp
+
+void register_reducer(pybind11::module& m) {
+  namespace py = pybind11;
+  auto s = m.def_submodule("ddp", "DDP gradient reducer");
+  py::class_<ddp::Reducer, std::shared_ptr<ddp::Reducer>>(s, "Reducer")
+      .def(py::init([](std::vector<at::Tensor> params, std::vector<std::vector<int64_t>> buckets,
+                       std::shared_ptr<Collective> comm, bool find_unused) {
+             auto r = std::make_shared<ddp::Reducer>(std::move(params), std::move(buckets), std::move(comm),
+                                                     find_unused);
+             r->install_hooks();
+             return r;
+           }),
+           py::arg("params"), py::arg("buckets"), py::arg("comm"), py::arg("find_unused") = false)
+      .def("prepare_for_backward", &ddp::Reducer::prepare_for_backward, py::arg("sync") = true)
+      .def("finalize", &ddp::Reducer::finalize)
+      .def("set_buckets", &ddp::Reducer::set_buckets)
+      .def("ready_order", &ddp::Reducer::ready_order)
+      .def("num_buckets", &ddp::Reducer::num_buckets)
+      .def("bucket_tensors", &ddp::Reducer::bucket_tensors)
+      .def("bucket_indices", &ddp::Reducer::bucket_indices)
+      .def("set_record_order", &ddp::Reducer::set_record_order);
+}
+
+}  // namespace dpa

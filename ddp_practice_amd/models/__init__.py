@@ -1,0 +1,2 @@
+"""Model zoo: the reference ConvNet and the ResNet-50 stress config."""
+from .convnet import ConvNet  # noqa: F401

@@ -1,0 +1,94 @@
+"""The reference ConvNet, with the same module tree / state_dict keys.
+
+reference: /root/reference/origin_main.py:9-31 and ddp_main.py:13-36:
+    layer1 = Conv2d(1,16,5,p=2) -> BatchNorm2d(16) -> ReLU -> MaxPool2d(2,2)
+    layer2 = Conv2d(16,32,5,p=2) -> BatchNorm2d(32) -> ReLU -> MaxPool2d(2,2)
+    fc     = Linear(7*7*32, num_classes)
+29,034 parameters, 16 state_dict entries ("layer1.0.weight" ... "fc.bias").
+
+On a HIP device each ``layerN`` runs as ONE fused op (2 launches forward,
+4-5 backward: ops/convblock.py) and ``fc`` on the MFMA head kernel; when a
+``SyncBatchNorm`` from this package replaces the BatchNorm (see
+``parallel.sync_bn.convert_sync_batchnorm``) the fused op all-reduces its
+statistics through that module's communicator.  On CPU the plain PyTorch
+modules run (the reference's semantics; used by the plumbing config and the
+CPU test tier).
+
+``amp_dtype`` reproduces the reference's ``autocast`` *inside* ``forward``
+(ddp_main.py:31): ``None`` = fp32 (origin_main.py), ``torch.float16`` = the
+reference's AMP default, ``torch.bfloat16`` = this framework's AMP default.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ..amp import autocast, compute_dtype
+
+
+class ConvNet(nn.Module):
+    def __init__(self, num_classes: int = 10, amp_dtype: torch.dtype | None = None, fused: bool = True):
+        super().__init__()
+        self.layer1 = nn.Sequential(
+            nn.Conv2d(1, 16, kernel_size=5, stride=1, padding=2),
+            nn.BatchNorm2d(16),
+            nn.ReLU(),
+            nn.MaxPool2d(kernel_size=2, stride=2),
+        )
+        self.layer2 = nn.Sequential(
+            nn.Conv2d(16, 32, kernel_size=5, stride=1, padding=2),
+            nn.BatchNorm2d(32),
+            nn.ReLU(),
+            nn.MaxPool2d(kernel_size=2, stride=2),
+        )
+        self.fc = nn.Linear(7 * 7 * 32, num_classes)
+        self.amp_dtype = amp_dtype
+        self.fused = fused
+
+    # ---------------------------------------------------------------- native
+    def _native_ok(self, x: torch.Tensor) -> bool:
+        if not (self.fused and x.is_cuda):
+            return False
+        from ..ops.convblock import supported
+
+        return supported(x, self.layer1[0]) and self.layer1[1].track_running_stats \
+            and self.layer2[1].track_running_stats
+
+    @staticmethod
+    def _block(seq: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
+        from ..ops.convblock import conv_block
+
+        bn = seq[1]
+        comm = None
+        if bn.training:
+            if isinstance(bn, nn.SyncBatchNorm):  # torch's SyncBN: use the package communicator
+                from ..parallel.comm import default_comm
+
+                comm = default_comm()
+            else:
+                comm = getattr(bn, "comm", None)
+        return conv_block(x, seq[0], bn, comm=comm)
+
+    def _forward_native(self, x: torch.Tensor) -> torch.Tensor:
+        from ..ops.head import linear
+
+        out = self._block(self.layer1, x)
+        out = self._block(self.layer2, out)
+        out = out.reshape(out.size(0), -1)
+        return linear(out, self.fc.weight, self.fc.bias)
+
+    def _forward_torch(self, x: torch.Tensor) -> torch.Tensor:
+        out = self.layer1(x)
+        out = self.layer2(out)
+        out = out.reshape(out.size(0), -1)
+        return self.fc(out)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        native = self._native_ok(x)
+        fwd = self._forward_native if native else self._forward_torch
+        if self.amp_dtype is not None:
+            with autocast(dtype=self.amp_dtype, device_type="cuda" if x.is_cuda else "cpu"):
+                if native and x.dtype != compute_dtype(x):
+                    x = x.to(compute_dtype(x))
+                return fwd(x)
+        return fwd(x)

@@ -1,0 +1,84 @@
+"""SGD on the multi-tensor HIP kernel (one launch per <= 36 tensors).
+
+Same hyper-parameters and update rule as ``torch.optim.SGD``
+(torch/optim/sgd.py:29-42, foreach path :471), plus ``found_inf`` so that
+``GradScaler.step`` can predicate the update on device (no host sync).
+
+reference: /root/reference/origin_main.py:87, ddp_main.py:125 —
+``torch.optim.SGD(model.parameters(), 1e-4)``.
+"""
+from __future__ import annotations
+
+import torch
+from torch.optim import Optimizer
+
+from .._ext import load as _load_ext
+
+
+class SGD(Optimizer):
+    supports_device_found_inf = True
+
+    def __init__(self, params, lr: float = 1e-3, momentum: float = 0.0, dampening: float = 0.0,
+                 weight_decay: float = 0.0, nesterov: bool = False, *, maximize: bool = False):
+        if lr < 0.0:
+            raise ValueError(f"Invalid learning rate: {lr}")
+        if momentum < 0.0:
+            raise ValueError(f"Invalid momentum value: {momentum}")
+        if weight_decay < 0.0:
+            raise ValueError(f"Invalid weight_decay value: {weight_decay}")
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                        nesterov=nesterov, maximize=maximize)
+        super().__init__(params, defaults)
+
+    @torch.no_grad()
+    def step(self, closure=None, found_inf: torch.Tensor | None = None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            params, grads, bufs = [], [], []
+            first = False
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                params.append(p)
+                grads.append(p.grad)
+                if group["momentum"] != 0:
+                    st = self.state[p]
+                    if "momentum_buffer" not in st or st["momentum_buffer"] is None:
+                        st["momentum_buffer"] = torch.zeros_like(p)
+                        first = True
+                    bufs.append(st["momentum_buffer"])
+            if not params:
+                continue
+            native = params[0].is_cuda and all(
+                p.dtype == torch.float32 and p.is_contiguous() and g.dtype == torch.float32 and g.is_contiguous()
+                for p, g in zip(params, grads))
+            if native:
+                _load_ext().optim.sgd_step(params, grads, bufs, group["lr"], group["momentum"], group["dampening"],
+                                           group["weight_decay"], group["nesterov"], group["maximize"], first,
+                                           found_inf, None)
+            else:
+                if found_inf is not None and bool(found_inf.item()):
+                    continue
+                self._torch_step(group, params, grads, bufs, first)
+        return loss
+
+    @staticmethod
+    def _torch_step(group, params, grads, bufs, first):
+        lr, mom, damp, wd = group["lr"], group["momentum"], group["dampening"], group["weight_decay"]
+        for i, (p, g) in enumerate(zip(params, grads)):
+            d = -g if group["maximize"] else g
+            if wd != 0:
+                d = d.add(p, alpha=wd)
+            if mom != 0:
+                b = bufs[i]
+                if first:
+                    b.copy_(d)
+                else:
+                    b.mul_(mom).add_(d, alpha=1 - damp)
+                d = d.add(b, alpha=mom) if group["nesterov"] else b
+            p.add_(d, alpha=-lr)

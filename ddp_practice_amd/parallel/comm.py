@@ -1,0 +1,329 @@
+"""Process group + communicator.
+
+``init_process_group`` keeps the reference's contract (backend "nccl" and
+``init_method="env://"``: MASTER_ADDR / MASTER_PORT / RANK / WORLD_SIZE, as set
+by /root/reference/ddp_main.py:61-65,72-73 or by torchrun,
+ddp_main_torchrun.py:102-104).  torch.distributed does the rendezvous (TCPStore)
+so ``torch.distributed.get_rank()`` etc. keep working in user code; on a HIP
+device this package then builds its OWN RCCL communicator (C++,
+csrc/comm/rccl_comm.cpp) whose unique id travels through that store, and
+every collective of the framework (DDP buckets, SyncBN statistics, buffer
+broadcast, metric reduce, barrier) goes through it.  On CPU (tests, the
+plumbing config) the same interface is served by torch.distributed/gloo.
+
+Communicator interface (all tensor ops are stream-ordered and
+hipGraph-capturable on the RCCL path):
+    all_reduce_(t, op)            in place
+    all_reduce(t, op) -> Tensor   out of place
+    broadcast_(t, src), reduce_(t, dst, op), all_gather_into_tensor(out, inp),
+    reduce_scatter_tensor(out, inp, op), all_to_all_single(out, inp), barrier()
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+from .._ext import load as _load_ext
+
+_DEFAULT = None
+_GEN = 0
+
+_TORCH_OPS = {
+    "sum": dist.ReduceOp.SUM, "prod": dist.ReduceOp.PRODUCT, "max": dist.ReduceOp.MAX,
+    "min": dist.ReduceOp.MIN,
+}
+
+
+def _op_name(op) -> str:
+    if isinstance(op, str):
+        return op.lower()
+    for k, v in _TORCH_OPS.items():
+        if op == v:
+            return k
+    if op == getattr(dist.ReduceOp, "AVG", object()):
+        return "avg"
+    raise ValueError(f"unsupported reduce op {op}")
+
+
+class Communicator:
+    rank: int = 0
+    world_size: int = 1
+    device: torch.device = torch.device("cpu")
+
+    # -- in-place / out-of-place all-reduce
+    def all_reduce_(self, t: torch.Tensor, op="sum") -> torch.Tensor:
+        raise NotImplementedError
+
+    def all_reduce(self, t: torch.Tensor, op="sum") -> torch.Tensor:
+        out = t.clone()
+        return self.all_reduce_(out, op)
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        raise NotImplementedError
+
+    def reduce_(self, t: torch.Tensor, dst: int = 0, op="sum") -> torch.Tensor:
+        raise NotImplementedError
+
+    def all_gather_into_tensor(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError
+
+    def reduce_scatter_tensor(self, out: torch.Tensor, inp: torch.Tensor, op="sum") -> torch.Tensor:
+        raise NotImplementedError
+
+    def all_to_all_single(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError
+
+    def barrier(self) -> None:
+        raise NotImplementedError
+
+    @property
+    def native(self):
+        """C++ Collective handle used by the DDP reducer."""
+        return _load_ext().comm.PyCollective(self)
+
+    def destroy(self) -> None:
+        pass
+
+
+class LocalCommunicator(Communicator):
+    """World of one: every collective is the identity."""
+
+    def __init__(self, device=None):
+        self.rank, self.world_size = 0, 1
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+
+    def all_reduce_(self, t, op="sum"):
+        return t
+
+    def all_reduce(self, t, op="sum"):
+        return t
+
+    def broadcast_(self, t, src=0):
+        return t
+
+    def reduce_(self, t, dst=0, op="sum"):
+        return t
+
+    def all_gather_into_tensor(self, out, inp):
+        out.view(-1).copy_(inp.view(-1))
+        return out
+
+    def reduce_scatter_tensor(self, out, inp, op="sum"):
+        out.view(-1).copy_(inp.view(-1))
+        return out
+
+    def all_to_all_single(self, out, inp):
+        out.copy_(inp)
+        return out
+
+    def barrier(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+
+class TorchCommunicator(Communicator):
+    """torch.distributed-backed communicator (gloo on CPU; any backend/group)."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world_size = dist.get_world_size(group)
+        self.device = torch.device("cpu")
+
+    def all_reduce_(self, t, op="sum"):
+        name = _op_name(op)
+        if name == "avg":
+            dist.all_reduce(t, dist.ReduceOp.SUM, group=self.group)
+            t.div_(self.world_size)
+        else:
+            dist.all_reduce(t, _TORCH_OPS[name], group=self.group)
+        return t
+
+    def broadcast_(self, t, src=0):
+        dist.broadcast(t, src, group=self.group)
+        return t
+
+    def reduce_(self, t, dst=0, op="sum"):
+        dist.reduce(t, dst, _TORCH_OPS[_op_name(op)], group=self.group)
+        return t
+
+    def all_gather_into_tensor(self, out, inp):
+        chunks = list(out.view(self.world_size, -1).unbind(0))
+        dist.all_gather(chunks, inp.reshape(-1).contiguous(), group=self.group)
+        return out
+
+    def reduce_scatter_tensor(self, out, inp, op="sum"):
+        tmp = inp.clone()
+        self.all_reduce_(tmp, op)
+        out.view(-1).copy_(tmp.view(self.world_size, -1)[self.rank])
+        return out
+
+    def all_to_all_single(self, out, inp):
+        ins = list(inp.view(self.world_size, -1).unbind(0))
+        outs = [torch.empty_like(x) for x in ins]
+        for r in range(self.world_size):
+            dist.scatter(outs[r], ins if r == self.rank else None, src=r, group=self.group)
+        out.view(self.world_size, -1).copy_(torch.stack(outs))
+        return out
+
+    def barrier(self):
+        dist.barrier(group=self.group)
+
+
+class RcclCommunicator(Communicator):
+    """The native RCCL communicator (one per process / GPU)."""
+
+    def __init__(self, rank: int, world_size: int, device: torch.device, store=None, key: str = "dpa_rccl"):
+        C = _load_ext()
+        self.rank, self.world_size = rank, world_size
+        self.device = torch.device(device)
+        if world_size > 1:
+            if store is None:
+                store = dist.distributed_c10d._get_default_store()
+            if rank == 0:
+                uid = C.comm.RcclComm.unique_id()
+                store.set(key, uid)
+            else:
+                store.wait([key], datetime.timedelta(seconds=600))
+                uid = store.get(key)
+        else:
+            uid = C.comm.RcclComm.unique_id()
+        self._c = C.comm.RcclComm(bytes(uid), rank, world_size, self.device.index)
+
+    @property
+    def native(self):
+        return self._c
+
+    def all_reduce_(self, t, op="sum"):
+        self._c.all_reduce(t, _op_name(op))
+        return t
+
+    def all_reduce(self, t, op="sum"):
+        out = torch.empty_like(t)
+        self._c.all_reduce(t, _op_name(op), out)
+        return out
+
+    def broadcast_(self, t, src=0):
+        self._c.broadcast(t, int(src))
+        return t
+
+    def reduce_(self, t, dst=0, op="sum"):
+        self._c.reduce(t, int(dst), _op_name(op))
+        return t
+
+    def all_gather_into_tensor(self, out, inp):
+        self._c.all_gather(out, inp.contiguous())
+        return out
+
+    def reduce_scatter_tensor(self, out, inp, op="sum"):
+        self._c.reduce_scatter(out, inp.contiguous(), _op_name(op))
+        return out
+
+    def all_to_all_single(self, out, inp):
+        self._c.all_to_all(out, inp.contiguous())
+        return out
+
+    def barrier(self):
+        self._c.barrier()
+
+    def async_error(self) -> str:
+        return self._c.async_error()
+
+    def abort(self):
+        self._c.abort()
+
+    def destroy(self):
+        self._c.destroy()
+
+
+# ------------------------------------------------------------------ process group
+def init_process_group(backend: str | None = None, init_method: str | None = "env://", world_size: int = -1,
+                       rank: int = -1, timeout: datetime.timedelta | None = None, device=None):
+    """Rendezvous (torch TCPStore, env://) + this package's communicator.
+
+    ``backend``: "nccl"/"rccl" (GPU; the framework's collectives use the native
+    RCCL communicator) or "gloo" (CPU).  Default: "nccl" if a GPU is present.
+    """
+    global _DEFAULT, _GEN
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    backend = backend.lower()
+    torch_backend = "nccl" if backend in ("nccl", "rccl") else backend
+    kw = {}
+    if timeout is not None:
+        kw["timeout"] = timeout
+    if not dist.is_initialized():
+        dist.init_process_group(torch_backend, init_method=init_method, world_size=world_size, rank=rank, **kw)
+    r, w = dist.get_rank(), dist.get_world_size()
+    if torch_backend == "nccl":
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        _GEN += 1
+        _DEFAULT = RcclCommunicator(r, w, device, key=f"dpa_rccl_uid_{_GEN}")
+    else:
+        _DEFAULT = TorchCommunicator() if w > 1 else LocalCommunicator()
+    return _DEFAULT
+
+
+def is_initialized() -> bool:
+    return _DEFAULT is not None or dist.is_initialized()
+
+
+def default_comm() -> Communicator:
+    global _DEFAULT
+    if _DEFAULT is None:
+        if dist.is_initialized():
+            _DEFAULT = TorchCommunicator() if dist.get_world_size() > 1 else LocalCommunicator()
+        else:
+            dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else None
+            _DEFAULT = LocalCommunicator(dev)
+    return _DEFAULT
+
+
+def set_default_comm(c: Communicator | None) -> None:
+    global _DEFAULT
+    _DEFAULT = c
+
+
+def get_rank() -> int:
+    if _DEFAULT is not None:
+        return _DEFAULT.rank
+    return dist.get_rank() if dist.is_initialized() else int(os.environ.get("RANK", "0"))
+
+
+def get_world_size() -> int:
+    if _DEFAULT is not None:
+        return _DEFAULT.world_size
+    return dist.get_world_size() if dist.is_initialized() else int(os.environ.get("WORLD_SIZE", "1"))
+
+
+def barrier() -> None:
+    if _DEFAULT is not None:
+        _DEFAULT.barrier()
+    elif dist.is_initialized():
+        dist.barrier()
+
+
+def max_over_ranks(x: float) -> float:
+    c = _DEFAULT
+    if c is None or c.world_size == 1:
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float32, device=c.device)
+    c.all_reduce_(t, "max")
+    return float(t.item())
+
+
+def destroy_process_group() -> None:
+    global _DEFAULT
+    if _DEFAULT is not None:
+        try:
+            if _DEFAULT.device.type == "cuda":
+                torch.cuda.synchronize(_DEFAULT.device)
+            _DEFAULT.destroy()
+        finally:
+            _DEFAULT = None
+    if dist.is_initialized():
+        dist.destroy_process_group()

@@ -1,0 +1,184 @@
+"""DistributedDataParallel over the native communicator + C++ reducer.
+
+Contract of torch.nn.parallel.DistributedDataParallel as the reference uses it
+(/root/reference/ddp_main.py:121-123: ``DDP(model, device_ids=[local_rank])``):
+  * construction: parameter-shape check across ranks, then rank 0's
+    parameters and buffers are broadcast (torch/nn/parallel/distributed.py:825,860-872);
+  * every training forward: buffers broadcast from rank 0 when
+    ``broadcast_buffers`` (distributed.py:1521-1558) — skipped when every buffer
+    belongs to a SyncBatchNorm, whose running stats are computed from globally
+    reduced statistics and are therefore already identical on all ranks;
+  * backward: gradients averaged over ranks by bucketed all-reduce overlapped
+    with the remaining backward (C++ Reducer, csrc/ddp/reducer.cpp);
+  * ``state_dict()`` keys carry the ``module.`` prefix; ``no_sync()``;
+    ``find_unused_parameters``.
+
+Bucket sizing for MI355X: RCCL over xGMI is latency-bound below ~1 MB and
+per-link-bandwidth bound above (7 x ~153 GB/s links per GPU, ring algorithms
+use one link per direction).  Fewer, larger buckets amortise the ~10-30 us
+per-collective latency; the first bucket stays small (1 MiB) so the
+all-reduce of the last layers' gradients starts while early layers are still
+in backward.  Default cap 32 MiB (HBM is 288 GB, memory is not the limit).
+"""
+from __future__ import annotations
+
+import contextlib
+import warnings
+
+import torch
+import torch.nn as nn
+
+from .._ext import load as _load_ext
+from . import comm as _comm
+from .sync_bn import SyncBatchNorm
+
+DEFAULT_FIRST_BUCKET_MB = 1.0
+DEFAULT_BUCKET_CAP_MB = 32.0
+
+
+def compute_bucket_assignment(params, cap_bytes: float, first_bytes: float, order=None) -> list[list[int]]:
+    """Greedy bucketing in `order` (default: reverse parameter order), per dtype/device.
+
+    Same algorithm as torch's _compute_bucket_assignment_by_size: a bucket closes
+    once its byte size reaches the current limit; limits are [first, cap, cap, ...].
+    """
+    if order is None:
+        order = list(range(len(params) - 1, -1, -1))
+    open_b: dict = {}
+    limits_idx: dict = {}
+    out: list[list[int]] = []
+    limits = [first_bytes, cap_bytes]
+    for i in order:
+        p = params[i]
+        key = (p.dtype, p.device)
+        b = open_b.setdefault(key, [[], 0])
+        b[0].append(i)
+        b[1] += p.numel() * p.element_size()
+        li = limits_idx.get(key, 0)
+        if b[1] >= limits[min(li, 1)]:
+            out.append(b[0])
+            open_b[key] = [[], 0]
+            limits_idx[key] = li + 1
+    for b in open_b.values():
+        if b[0]:
+            out.append(b[0])
+    return out
+
+
+class DistributedDataParallel(nn.Module):
+    def __init__(self, module: nn.Module, device_ids=None, output_device=None, dim: int = 0,
+                 broadcast_buffers: bool = True, process_group=None, bucket_cap_mb: float | None = None,
+                 find_unused_parameters: bool = False, check_reduction: bool = False,
+                 gradient_as_bucket_view: bool = True, static_graph: bool = False,
+                 first_bucket_mb: float | None = None):
+        super().__init__()
+        self.module = module
+        self.device_ids = device_ids
+        self.broadcast_buffers = broadcast_buffers
+        self.find_unused_parameters = find_unused_parameters
+        self.static_graph = static_graph
+        if not gradient_as_bucket_view:
+            warnings.warn("gradient_as_bucket_view=False is not supported; grads are bucket views")
+        self.comm = process_group if isinstance(process_group, _comm.Communicator) else _comm.default_comm()
+        self.bucket_cap_bytes = (bucket_cap_mb if bucket_cap_mb is not None else DEFAULT_BUCKET_CAP_MB) * 2 ** 20
+        self.first_bucket_bytes = (first_bucket_mb if first_bucket_mb is not None
+                                   else DEFAULT_FIRST_BUCKET_MB) * 2 ** 20
+        self._params = [p for p in module.parameters() if p.requires_grad]
+        if len({id(p) for p in self._params}) != len(self._params):
+            raise RuntimeError("DDP does not support shared parameters listed twice")
+        self._sync_enabled = True
+        self._iteration = 0
+        self._rebuilt = False
+        self.require_forward_param_sync = True
+        self._verify_param_shapes()
+        self._sync_module_states()
+        self._buffers_need_sync = broadcast_buffers and any(
+            not isinstance(self._owner_of_buffer(name), (SyncBatchNorm, nn.SyncBatchNorm))
+            for name, _ in module.named_buffers())
+        self.reducer = None
+        if self.comm.world_size > 1 and self._params:
+            buckets = compute_bucket_assignment(self._params, self.bucket_cap_bytes, self.first_bucket_bytes)
+            self.reducer = _load_ext().ddp.Reducer(self._params, buckets, self.comm.native, find_unused_parameters)
+
+    # ------------------------------------------------------------- init sync
+    def _owner_of_buffer(self, name: str):
+        mod = self.module
+        parts = name.split(".")
+        for p in parts[:-1]:
+            mod = getattr(mod, p)
+        return mod
+
+    def _verify_param_shapes(self):
+        if self.comm.world_size == 1:
+            return
+        sig = [float(len(self._params))] + [float(hash(tuple(p.shape)) % 1000003) for p in self._params]
+        t = torch.tensor(sig, dtype=torch.float64, device=self.comm.device)
+        if t.device.type == "cuda":
+            t = t.float()
+        lo, hi = t.clone(), t.clone()
+        self.comm.all_reduce_(lo, "min")
+        self.comm.all_reduce_(hi, "max")
+        if not torch.equal(lo, hi):
+            raise RuntimeError("DDP: parameter shapes/count differ across ranks")
+
+    def _flat_broadcast(self, tensors):
+        by_dtype: dict = {}
+        for t in tensors:
+            by_dtype.setdefault(t.dtype, []).append(t)
+        for ts in by_dtype.values():
+            flat = torch.cat([t.detach().reshape(-1) for t in ts])
+            self.comm.broadcast_(flat, 0)
+            off = 0
+            with torch.no_grad():
+                for t in ts:
+                    n = t.numel()
+                    t.copy_(flat[off:off + n].view_as(t))
+                    off += n
+
+    def _sync_module_states(self):
+        if self.comm.world_size == 1:
+            return
+        ts = [p.data for p in self.module.parameters()] + [b for b in self.module.buffers()]
+        if ts:
+            self._flat_broadcast(ts)
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, *inputs, **kwargs):
+        if self.reducer is not None and torch.is_grad_enabled() and self.module.training:
+            if self._iteration == 1 and not self._rebuilt:
+                self._rebuild_buckets()
+            self.reducer.prepare_for_backward(self._sync_enabled)
+            self._iteration += 1
+        if self._buffers_need_sync and self.comm.world_size > 1 and self.require_forward_param_sync:
+            bufs = [b for b in self.module.buffers()]
+            if bufs:
+                self._flat_broadcast(bufs)
+        out = self.module(*inputs, **kwargs)
+        if not self.module.training:
+            pass
+        return out
+
+    def _rebuild_buckets(self):
+        """Re-plan buckets in the order grads became ready during iteration 1."""
+        self._rebuilt = True
+        order = list(self.reducer.ready_order())
+        if len(order) != len(self._params) or self.find_unused_parameters:
+            return
+        buckets = compute_bucket_assignment(self._params, self.bucket_cap_bytes, self.first_bucket_bytes, order)
+        if buckets != [list(b) for b in self.reducer.bucket_indices()]:
+            self.reducer.set_buckets(buckets)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        old = self._sync_enabled
+        self._sync_enabled = False
+        try:
+            yield
+        finally:
+            self._sync_enabled = old
+
+    # -------------------------------------------------------------- utilities
+    def bucket_sizes_bytes(self) -> list[int]:
+        if self.reducer is None:
+            return []
+        return [t.numel() * t.element_size() for t in self.reducer.bucket_tensors()]
