@@ -41,6 +41,7 @@ class GradScaler:
         self._growth_tracker: torch.Tensor | None = None
         self._found_inf: torch.Tensor | None = None
         self._per_opt: dict[int, dict[str, Any]] = {}
+        self._armed = True  # device found_inf is known to be 0
 
     # ------------------------------------------------------------------ state
     def _lazy_init(self, dev: torch.device):
@@ -72,7 +73,8 @@ class GradScaler:
             return outputs
         if isinstance(outputs, torch.Tensor):
             self._lazy_init(outputs.device)
-            return outputs * self._scale.to(outputs.device, non_blocking=True)
+            # 0-d scale: a 0-d loss stays 0-d, so backward needs no sum-to-shape reduction
+            return outputs * self._scale.to(outputs.device, non_blocking=True).view(())
         if isinstance(outputs, (list, tuple)):
             return type(outputs)(self.scale(o) for o in outputs)
         raise ValueError("outputs must be a Tensor or an iterable of Tensors")
@@ -99,8 +101,12 @@ class GradScaler:
         grads = self._grads(optimizer)
         if self._scale is None:
             self._lazy_init(grads[0].device if grads else torch.device(self._device))
-        self._found_inf.zero_()
-        if grads and _native_ok(grads[0]) and all(g.dtype == torch.float32 and g.is_contiguous() for g in grads):
+        native = grads and _native_ok(grads[0]) and all(g.dtype == torch.float32 and g.is_contiguous()
+                                                           for g in grads)
+        if not (native and self._armed):
+            self._found_inf.zero_()
+        self._armed = False
+        if native:
             _load_ext().optim.unscale_check(grads, self._scale, self._found_inf)
         else:
             inv = self._scale.double().reciprocal().float()
@@ -141,8 +147,10 @@ class GradScaler:
                 self._scale.copy_(new_scale)
         else:
             if self._scale.is_cuda:
+                # also re-arms found_inf to 0 on device (no separate fill launch)
                 _load_ext().optim.update_scale(self._scale, self._growth_tracker, self._found_inf,
                                                self._growth_factor, self._backoff_factor, self._growth_interval)
+                self._armed = True
             else:
                 torch._amp_update_scale_(self._scale, self._growth_tracker, self._found_inf,
                                          self._growth_factor, self._backoff_factor, self._growth_interval)

@@ -2,29 +2,34 @@
 //     Conv2d(CIN->COUT, 5x5, stride 1, pad 2) -> BatchNorm2d -> ReLU -> MaxPool2d(2,2)
 // (reference: /root/reference/origin_main.py:12-23, ddp_main.py:16-27).
 //
-// Forward (train):  [conv_fwd: implicit-GEMM MFMA + bias + BN partial stats]
-//                   -> (optional SyncBN all-reduce of the 2C+1 stats, host side)
-//                   -> [bn_relu_pool: finalize stats, running-stat update,
+// Forward (train):  [conv_fwd: implicit-GEMM MFMA + bias + per-workgroup BN partial sums -> fslab]
+//                   -> (SyncBN: one all-reduce of fslab, host side)
+//                   -> [bn_relu_pool: reduce fslab, running-stat update,
 //                       normalise, ReLU, 2x2 max-pool, argmax index]
-// Backward:         [bwd_reduce: pool/ReLU routing + per-channel sum(dy), sum(dy*xhat)]
-//                   -> (optional SyncBN all-reduce of 2C sums)
+// Backward:         [bwd_reduce: pool/ReLU routing + per-channel partial sum(dy), sum(dy*xhat) -> bslab]
+//                   -> (SyncBN: one all-reduce of bslab)
 //                   -> [bwd_elemt: BN input-grad at full resolution]
-//                   -> [conv_wgrad: MFMA, split over images, f32 atomics into dW, db]
+//                   -> [conv_wgrad: MFMA per image chunk -> wslab]
+//                   -> [grad_reduce: wslab -> dW, db ; bslab -> dgamma, dbeta]
 //                   -> [conv_fwd<DGRAD>: input grad = conv of dy with flipped W^T]
 //
 // Design notes (MI355X):
-//  * Everything here is latency-bound (per-step GEMMs are 20-160 MFLOP), so the
-//    goal is few launches, one LDS round trip per operand, and enough
-//    workgroups (B x splits >= 64) to spread over XCDs.
+//  * Everything here is latency-bound (per-step GEMMs are 20-160 MFLOP): few
+//    launches, one LDS round trip per operand, >= 64 workgroups per launch.
+//  * No float atomics and no zero-fill launches: every cross-workgroup sum is
+//    a per-workgroup partial row ("slab") reduced by its consumer kernel.
+//    (Contended atomics — every workgroup adding into the same few hundred
+//    addresses — serialise at the memory side; the first version of this file
+//    spent 32 us per wgrad on them.)  Deterministic as a bonus.
 //  * im2col never touches HBM: the input image (with halo) sits in LDS in
 //    HWC order so that 8 K-consecutive elements (8 input channels of one tap)
 //    are one 16-B ds_read; conv1 (CIN=1) gathers its 25 taps element-wise.
 //  * wgrad keeps 5 kw-shifted copies of the input in LDS so that the B operand
 //    (8 consecutive output columns of one tap) is again one aligned 16-B read.
-//  * BN statistics are accumulated around a per-channel shift (the running
-//    mean, identical on every rank) to avoid E[x^2]-E[x]^2 cancellation; the
-//    sums are plain sums, so SyncBN needs one all-reduce of 2C+1 floats and
-//    no device->host mask sync (cf. torch/nn/modules/_functions.py:74-101).
+//  * BN statistics are sums around a per-channel shift (the running mean,
+//    identical on every rank) to avoid E[x^2]-E[x]^2 cancellation; partial
+//    sums + counts make SyncBN ONE all-reduce with no device->host mask sync
+//    (cf. torch/nn/modules/_functions.py:74-101).
 #include "common.h"
 
 namespace dpa {
@@ -32,14 +37,81 @@ namespace cb {
 
 constexpr int NTHR = 256;
 
-// stats buffer layout (floats): [0,C) sum(y-shift) | [C,2C) sum((y-shift)^2) |
-// [2C] count | [2C+1, 3C+1) shift copy.  First 2C+1 entries are all-reduced.
+// Final statistics buffer written by bn_relu_pool (read by the backward):
+// [0,C) sum(y-shift) | [C,2C) sum((y-shift)^2) | [2C] count | [2C+1,3C+1) shift
 __host__ __device__ constexpr int stats_len(int C) { return 3 * C + 1; }
+// forward partial-sum row per conv workgroup: [sum(C) | sumsq(C) | count]
+__host__ __device__ constexpr int fslab_row(int C) { return 2 * C + 1; }
+
+template <int I> struct SH;
+template <> struct SH<0> { static constexpr int CIN = 1, COUT = 16, H = 28, W = 28, SPLIT = 4, WROWS = 28; };
+template <> struct SH<1> { static constexpr int CIN = 16, COUT = 32, H = 14, W = 14, SPLIT = 2, WROWS = 14; };
+constexpr int kBwdSplit = 8;  // batch split of bwd_reduce
+
+// ---------------------------------------------------------------------------
+// Staging helpers.  Every global->LDS staging loop is split into "issue every
+// load into registers" then "convert + scatter into LDS", with compile-time
+// trip counts so all of a thread's loads are in flight together: one L2
+// round trip per staging phase instead of one per loop iteration (the loop
+// form cost 20+ us per kernel in the first profile).
+// ---------------------------------------------------------------------------
+// f32 array of N elements (N % 4 == 0, 16-B aligned) -> sink(e, v) per element
+template <int N, typename Sink>
+__device__ __forceinline__ void stage_f32(const float* __restrict__ src, Sink&& sink) {
+  static_assert(N % 4 == 0, "N must be a multiple of 4");
+  constexpr int N4 = N / 4;
+  constexpr int IT = (N4 + NTHR - 1) / NTHR;
+  f32x4 v[IT];
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int e = threadIdx.x + i * NTHR;
+    if (e < N4) v[i] = s4[e];
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int e = threadIdx.x + i * NTHR;
+    if (e < N4) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sink(4 * e + j, v[i][j]);
+    }
+  }
+}
+
+// [C][H][W] image of T (W even) -> sink(c, h, w, v_w, v_w+1) per element pair
+template <typename T> struct Pair2 { typedef uint32_t type; };
+template <> struct Pair2<float> { typedef uint64_t type; };
+template <typename T, int C, int H, int W, typename Sink>
+__device__ __forceinline__ void stage_chw(const T* __restrict__ src, Sink&& sink) {
+  static_assert(W % 2 == 0, "W must be even");
+  typedef typename Pair2<T>::type P;
+  constexpr int NP = C * H * W / 2;
+  constexpr int IT = (NP + NTHR - 1) / NTHR;
+  P v[IT];
+  const P* s2 = reinterpret_cast<const P*>(src);
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int e = threadIdx.x + i * NTHR;
+    if (e < NP) v[i] = s2[e];
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int e = threadIdx.x + i * NTHR;
+    if (e < NP) {
+      const int pe = 2 * e;
+      const int c = pe / (H * W), rem = pe % (H * W);
+      T a, b;
+      __builtin_memcpy(&a, &v[i], sizeof(T));
+      __builtin_memcpy(&b, reinterpret_cast<const char*>(&v[i]) + sizeof(T), sizeof(T));
+      sink(c, rem / W, rem % W, a, b);
+    }
+  }
+}
 
 // ---------------------------------------------------------------------------
 // Implicit-GEMM 5x5 convolution, one (image, m-range) per workgroup.
-//   MODE 0: forward + bias + BN partial stats      (train)
-//   MODE 1: forward + bias                         (eval / no BN stats)
+//   MODE 0: forward + bias + BN partial sums        (train)
+//   MODE 1: forward + bias                          (eval)
 //   MODE 2: data-grad: input = dy (CIN = COUT_orig), output = dx,
 //           W_eff[co][ci][kh][kw] = W[ci][co][4-kh][4-kw], no bias
 // GEMM view: rows = output pixels of one image, cols = output channels,
@@ -48,8 +120,8 @@ __host__ __device__ constexpr int stats_len(int C) { return 3 * C + 1; }
 template <typename T, int CIN, int COUT, int H, int W, int MODE>
 __global__ void __launch_bounds__(NTHR)
 conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
-               T* __restrict__ y, float* __restrict__ stats, const float* __restrict__ shift,
-               int nsplit) {
+               T* __restrict__ y, float* __restrict__ fslab, float* __restrict__ fstats,
+               const float* __restrict__ shift, int nsplit) {
   static_assert(CIN == 1 || CIN % 8 == 0, "CIN must be 1 or a multiple of 8");
   static_assert(COUT % 16 == 0, "COUT must be a multiple of 16");
   static_assert((H * W) % 4 == 0, "H*W must be a multiple of 4");
@@ -72,29 +144,34 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
   const int sp = blockIdx.x % nsplit;
   const T* xb = x + (size_t)b * CIN * HW;
 
-  // --- stage weights: wl[co][k], k = (kh*5+kw)*CIN + ci, zero for k >= K
-  for (int e = tid; e < COUT * KP; e += NTHR) {
-    const int co = e / KP, k = e % KP;
-    float v = 0.f;
-    if (k < K) {
-      const int tap = k / CIN, ci = k % CIN;
-      const int kh = tap / 5, kw = tap % 5;
-      if (MODE == 2)
-        v = w[((ci * COUT + co) * 5 + (4 - kh)) * 5 + (4 - kw)];
-      else
-        v = w[((co * CIN + ci) * 5 + kh) * 5 + kw];
-    }
-    wl[co * KPW + k] = Cvt<T>::from_f(v);
+  // --- stage weights (batched float4 reads in natural [co][ci][kh][kw] order,
+  //     scattered LDS writes to wl[co][(kh*5+kw)*CIN + ci])
+  const T zero = Cvt<T>::from_f(0.f);
+  if constexpr (KP > K) {
+    for (int e = tid; e < COUT * (KP - K); e += NTHR) wl[(e / (KP - K)) * KPW + K + e % (KP - K)] = zero;
   }
+  // natural W index e = (o * WIN + i) * 25 + tap, WIN = in-channels of W
+  // (= CIN here, = COUT for the data-grad where W is [CIN][COUT][5][5])
+  constexpr int KO = 25 * (MODE == 2 ? COUT : CIN);
+  stage_f32<COUT * K>(w, [&](int e, float v) {
+    const int o = e / KO, rem = e % KO;      // o: out-ch of W
+    const int i = rem / 25, tap = rem % 25;  // i: in-ch of W
+    if (MODE == 2)  // W_eff[co=i][ci=o][tap'] with tap' = 24 - tap
+      wl[i * KPW + (24 - tap) * CIN + o] = Cvt<T>::from_f(v);
+    else
+      wl[o * KPW + tap * CIN + i] = Cvt<T>::from_f(v);
+  });
   // --- stage the zero-padded image in HWC order
-  for (int e = tid; e < HP * WPD * CIN; e += NTHR) img[e] = Cvt<T>::from_f(0.f);
-  if (MODE == 0 && tid < 2 * COUT) lstat[tid] = 0.f;
-  __syncthreads();
-  for (int e = tid; e < CIN * HW; e += NTHR) {
-    const int ci = e / HW, pix = e % HW;
-    const int h = pix / W, ww = pix % W;
-    img[((h + 2) * WPD + (ww + 2)) * CIN + ci] = xb[e];
+  for (int e = tid; e < HP * WPD * CIN; e += NTHR) {
+    const int hp = e / (WPD * CIN), rem = e % (WPD * CIN);
+    const int wp = rem / CIN;
+    if (hp < 2 || hp >= H + 2 || wp < 2 || wp >= W + 2) img[e] = zero;
   }
+  if (MODE == 0 && tid < 2 * COUT) lstat[tid] = 0.f;
+  stage_chw<T, CIN, H, W>(xb, [&](int ci, int h, int ww, T a, T bb) {
+    img[((h + 2) * WPD + (ww + 2)) * CIN + ci] = a;
+    img[((h + 2) * WPD + (ww + 3)) * CIN + ci] = bb;
+  });
   __syncthreads();
 
   const int lane = tid & 63, wv = tid >> 6;
@@ -167,59 +244,99 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
       a2 += __shfl_xor(a2, 16, 64);
       a2 += __shfl_xor(a2, 32, 64);
       if (q == 0) {
-        atomicAdd(&lstat[nt * 16 + r], a1);
+        atomicAdd(&lstat[nt * 16 + r], a1);  // LDS atomics: 4 waves per address
         atomicAdd(&lstat[COUT + nt * 16 + r], a2);
       }
     }
     __syncthreads();
-    if (tid < 2 * COUT) atomicAdd(&stats[tid], lstat[tid]);
-    if (blockIdx.x == 0) {
-      if (tid < COUT) stats[2 * COUT + 1 + tid] = shift[tid];
+    float* row = fslab + (size_t)blockIdx.x * fslab_row(COUT);
+    if (tid < 2 * COUT) row[tid] = lstat[tid];
+    if (tid == 0) {
+      const int p0 = mt0 * 16, p1 = min(mt1 * 16, HW);
+      row[2 * COUT] = (float)(p1 - p0);
     }
-    if (sp == 0 && tid == 0) atomicAdd(&stats[2 * COUT], (float)HW);
+    if (blockIdx.x == 0 && tid < COUT) fstats[2 * COUT + 1 + tid] = shift[tid];
   }
 }
 
 // ---------------------------------------------------------------------------
 // BN finalize + normalise + ReLU + 2x2/2 max-pool (+ argmax index, first max
 // wins in (dy,dx) scan order as ATen's max_pool2d).  One thread per pooled
-// output.  Block 0 updates running stats (momentum<0 => cumulative average).
+// output.  Each workgroup first reduces the conv's per-workgroup partial sums
+// (nrows x (2C+1) floats, L2-resident); workgroup 0 publishes the final sums to
+// fstats and updates the running stats (momentum<0 => cumulative average).
 // ---------------------------------------------------------------------------
 template <typename T, int C, int H, int W>
 __global__ void __launch_bounds__(NTHR)
-bn_relu_pool_kernel(const T* __restrict__ y, const float* __restrict__ stats,
-                    const float* __restrict__ gamma, const float* __restrict__ beta,
+bn_relu_pool_kernel(const T* __restrict__ y, const float* __restrict__ fslab, int nrows,
+                    float* __restrict__ fstats, const float* __restrict__ gamma, const float* __restrict__ beta,
                     float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
-                    float momentum, float eps, int train, T* __restrict__ p,
-                    uint8_t* __restrict__ idx, int total) {
+                    float momentum, float eps, int train, T* __restrict__ p, uint8_t* __restrict__ idx,
+                    int total) {
   constexpr int HO = H / 2, WO = W / 2;
-  const int e = blockIdx.x * NTHR + threadIdx.x;
-  if (train && blockIdx.x == 0 && threadIdx.x < C) {
-    const int c = threadIdx.x;
-    const float n = stats[2 * C];
-    const float m1 = stats[c] / n;
-    const float mean = stats[2 * C + 1 + c] + m1;
-    const float var = fmaxf(stats[C + c] / n - m1 * m1, 0.f);
-    const int64_t nb = nbt[0] + 1;
-    const float mom = momentum >= 0.f ? momentum : 1.f / (float)nb;
-    rmean[c] = (1.f - mom) * rmean[c] + mom * mean;
-    rvar[c] = (1.f - mom) * rvar[c] + mom * var * (n / fmaxf(n - 1.f, 1.f));
-    if (c == 0) nbt[0] = nb;
+  constexpr int RL = 2 * C + 1;
+  __shared__ float part[NTHR];
+  __shared__ float sc_s[C], sh_s[C];
+  const int tid = threadIdx.x;
+  if (train) {
+    // column j of the slab summed over rows; NTHR/RL row-groups in parallel
+    constexpr int G = NTHR / RL;  // >= 3 for C <= 32
+    static_assert(G >= 1, "C too large");
+    const int j = tid % RL, g = tid / RL;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    if (g < G) {
+      int rr = g;
+      for (; rr + 3 * G < nrows; rr += 4 * G) {
+        a0 += fslab[(size_t)rr * RL + j];
+        a1 += fslab[(size_t)(rr + G) * RL + j];
+        a2 += fslab[(size_t)(rr + 2 * G) * RL + j];
+        a3 += fslab[(size_t)(rr + 3 * G) * RL + j];
+      }
+      for (; rr < nrows; rr += G) a0 += fslab[(size_t)rr * RL + j];
+    }
+    part[tid] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (tid < RL) {
+      float t = 0.f;
+      for (int gg = 0; gg < G; ++gg) t += part[gg * RL + tid];
+      part[tid] = t;  // each tid < RL only touches its own column's slots (gg*RL + tid)
+    }
+    __syncthreads();
+    if (tid < C) {
+      const float n = part[2 * C];
+      const float m1 = part[tid] / n;
+      const float shv = fstats[2 * C + 1 + tid];
+      const float mean = shv + m1;
+      const float var = fmaxf(part[C + tid] / n - m1 * m1, 0.f);
+      const float invstd = rsqrtf(var + eps);
+      const float s = gamma[tid] * invstd;
+      sc_s[tid] = s;
+      sh_s[tid] = beta[tid] - mean * s;
+      if (blockIdx.x == 0) {
+        fstats[tid] = part[tid];
+        fstats[C + tid] = part[C + tid];
+        if (tid == 0) fstats[2 * C] = n;
+        const int64_t nb = nbt[0] + 1;
+        const float mom = momentum >= 0.f ? momentum : 1.f / (float)nb;
+        rmean[tid] = (1.f - mom) * rmean[tid] + mom * mean;
+        rvar[tid] = (1.f - mom) * rvar[tid] + mom * var * (n / fmaxf(n - 1.f, 1.f));
+      }
+    }
+    __syncthreads();
+    if (blockIdx.x == 0 && tid == 0) nbt[0] = nbt[0] + 1;
+  } else {
+    if (tid < C) {
+      const float invstd = rsqrtf(rvar[tid] + eps);
+      const float s = gamma[tid] * invstd;
+      sc_s[tid] = s;
+      sh_s[tid] = beta[tid] - rmean[tid] * s;
+    }
+    __syncthreads();
   }
+  const int e = blockIdx.x * NTHR + tid;
   if (e >= total) return;
   const int c = (e / (HO * WO)) % C;
-  float mean, invstd;
-  if (train) {
-    const float n = stats[2 * C];
-    const float m1 = stats[c] / n;
-    mean = stats[2 * C + 1 + c] + m1;
-    invstd = rsqrtf(fmaxf(stats[C + c] / n - m1 * m1, 0.f) + eps);
-  } else {
-    mean = rmean[c];
-    invstd = rsqrtf(rvar[c] + eps);
-  }
-  const float sc = gamma[c] * invstd;
-  const float sh = beta[c] - mean * sc;
+  const float sc = sc_s[c], sh = sh_s[c];
   const int bc = e / (HO * WO), pix = e % (HO * WO);
   const int ho = pix / WO, wo = pix % WO;
   const T* src = y + (size_t)bc * H * W + (2 * ho) * W + 2 * wo;
@@ -235,35 +352,35 @@ bn_relu_pool_kernel(const T* __restrict__ y, const float* __restrict__ stats,
   idx[e] = (uint8_t)bi;
 }
 
-// mean / invstd of channel c from a (possibly all-reduced) stats buffer.
+// mean / invstd of channel c from the final stats buffer.
 template <int C>
-__device__ __forceinline__ void stats_mean_invstd(const float* stats, int c, float eps, float& mean,
+__device__ __forceinline__ void stats_mean_invstd(const float* fstats, int c, float eps, float& mean,
                                                   float& invstd, float& n) {
-  n = stats[2 * C];
-  const float m1 = stats[c] / n;
-  mean = stats[2 * C + 1 + c] + m1;
-  invstd = rsqrtf(fmaxf(stats[C + c] / n - m1 * m1, 0.f) + eps);
+  n = fstats[2 * C];
+  const float m1 = fstats[c] / n;
+  mean = fstats[2 * C + 1 + c] + m1;
+  invstd = rsqrtf(fmaxf(fstats[C + c] / n - m1 * m1, 0.f) + eps);
 }
 
 // ---------------------------------------------------------------------------
 // Backward part 1: route the pooled grad through max-pool (argmax) and ReLU
-// (pooled output > 0), and reduce per channel
-//   sums[c]     += sum dy          (= grad of BN bias)
-//   sums[C + c] += sum dy * xhat   (= grad of BN weight)
-// grid = (C, nsplit over the batch).
+// (pooled output > 0), and reduce per channel into bslab[split][2C]:
+//   [c]     sum dy          (-> grad of BN bias)
+//   [C + c] sum dy * xhat   (-> grad of BN weight)
+// grid = (C, kBwdSplit over the batch).
 // ---------------------------------------------------------------------------
 template <typename T, int C, int H, int W>
 __global__ void __launch_bounds__(NTHR)
 bwd_reduce_kernel(const T* __restrict__ dp, const T* __restrict__ p, const uint8_t* __restrict__ idx,
-                  const T* __restrict__ y, const float* __restrict__ stats, float eps,
-                  float* __restrict__ sums, int B) {
+                  const T* __restrict__ y, const float* __restrict__ fstats, float eps,
+                  float* __restrict__ bslab, int B) {
   constexpr int HO = H / 2, WO = W / 2, PP = HO * WO;
   __shared__ float red[2 * NTHR / 64];
   const int c = blockIdx.x;
   const int nsplit = gridDim.y;
   const int b0 = (B * blockIdx.y) / nsplit, b1 = (B * (blockIdx.y + 1)) / nsplit;
   float mean, invstd, n;
-  stats_mean_invstd<C>(stats, c, eps, mean, invstd, n);
+  stats_mean_invstd<C>(fstats, c, eps, mean, invstd, n);
   float a1 = 0.f, a2 = 0.f;
   const int cnt = (b1 - b0) * PP;
   for (int t = threadIdx.x; t < cnt; t += NTHR) {
@@ -288,8 +405,8 @@ bwd_reduce_kernel(const T* __restrict__ dp, const T* __restrict__ p, const uint8
   if (threadIdx.x == 0) {
     float t1 = 0.f, t2 = 0.f;
     for (int i = 0; i < NTHR / 64; ++i) { t1 += red[i]; t2 += red[NTHR / 64 + i]; }
-    atomicAdd(&sums[c], t1);
-    atomicAdd(&sums[C + c], t2);
+    bslab[blockIdx.y * 2 * C + c] = t1;
+    bslab[blockIdx.y * 2 * C + C + c] = t2;
   }
 }
 
@@ -297,22 +414,39 @@ bwd_reduce_kernel(const T* __restrict__ dp, const T* __restrict__ p, const uint8
 // Backward part 2: BN input gradient at full resolution, one thread per
 // pooled element (its 2x2 window):
 //   dx = gamma*invstd*(dy - S1/n - xhat*S2/n),  dy = routed pooled grad or 0
+// S1, S2 = column sums of the (all-reduced) bslab.
 // ---------------------------------------------------------------------------
 template <typename T, int C, int H, int W>
 __global__ void __launch_bounds__(NTHR)
 bwd_elemt_kernel(const T* __restrict__ dp, const T* __restrict__ p, const uint8_t* __restrict__ idx,
-                 const T* __restrict__ y, const float* __restrict__ stats,
-                 const float* __restrict__ gsums, const float* __restrict__ gamma, float eps,
+                 const T* __restrict__ y, const float* __restrict__ fstats,
+                 const float* __restrict__ gslab, int nsplit, const float* __restrict__ gamma, float eps,
                  T* __restrict__ dx, int total) {
   constexpr int HO = H / 2, WO = W / 2, PP = HO * WO;
-  const int e = blockIdx.x * NTHR + threadIdx.x;
+  __shared__ float k_s[3 * C];
+  __shared__ float m_s[2 * C];
+  const int tid = threadIdx.x;
+  if (tid < C) {
+    float s1 = 0.f, s2 = 0.f;
+    for (int s = 0; s < nsplit; ++s) {
+      s1 += gslab[s * 2 * C + tid];
+      s2 += gslab[s * 2 * C + C + tid];
+    }
+    float mean, invstd, n;
+    stats_mean_invstd<C>(fstats, tid, eps, mean, invstd, n);
+    k_s[tid] = s1 / n;
+    k_s[C + tid] = s2 / n;
+    k_s[2 * C + tid] = gamma[tid] * invstd;
+    m_s[tid] = mean;
+    m_s[C + tid] = invstd;
+  }
+  __syncthreads();
+  const int e = blockIdx.x * NTHR + tid;
   if (e >= total) return;
   const int bc = e / PP, pix = e % PP;
   const int c = bc % C;
-  float mean, invstd, n;
-  stats_mean_invstd<C>(stats, c, eps, mean, invstd, n);
-  const float k1 = gsums[c] / n, k2 = gsums[C + c] / n;
-  const float gi = gamma[c] * invstd;
+  const float k1 = k_s[c], k2 = k_s[C + c], gi = k_s[2 * C + c];
+  const float mean = m_s[c], invstd = m_s[C + c];
   const float pv = Cvt<T>::to_f(p[e]);
   const float g = pv > 0.f ? Cvt<T>::to_f(dp[e]) : 0.f;
   const int kk = idx[e];
@@ -328,84 +462,175 @@ bwd_elemt_kernel(const T* __restrict__ dp, const T* __restrict__ p, const uint8_
 }
 
 // ---------------------------------------------------------------------------
-// Weight/bias gradient of the 5x5 conv.  One workgroup per (image, row-chunk).
+// Weight/bias gradient partials of the 5x5 conv.  One workgroup per
+// (image, row-chunk); writes wslab[blk][COUT*N + COUT] (dW partial | db partial).
 // GEMM: rows = COUT, cols = (ci, kh, kw) natural order, K = pixels of the chunk
 // with the row padded to WP = ceil8(W) (dy is zero in the pad columns).
 // LDS: dy[COUT][ROWS][WP] and 5 kw-shifted copies xs[kw][CIN][ROWS+4][WP] of
 // the zero-padded input so both operands are aligned 16-B LDS reads.
-// Partial sums go to dW/db with f32 atomics (buffers zeroed by the caller).
+// When there are fewer (m,n) tile pairs than waves, waves split K instead
+// and combine through LDS.
 // ---------------------------------------------------------------------------
 template <typename T, int CIN, int COUT, int H, int W, int ROWS>
 __global__ void __launch_bounds__(NTHR)
-conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* __restrict__ dw,
-                     float* __restrict__ db, int nsplit) {
+conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* __restrict__ wslab,
+                     int nsplit) {
   constexpr int WP = ceil_to(W, 8);
   static_assert((ROWS * WP) % 32 == 0, "ROWS*WP must be a multiple of 32");
   constexpr int KSTEPS = ROWS * WP / 32;
   constexpr int N = CIN * 25;
   constexpr int NTL = (N + 15) / 16;
   constexpr int MTL = COUT / 16;
+  constexpr int PAIRS = MTL * NTL;
+  constexpr int NW = NTHR / 64;
+  constexpr int KSPLIT = PAIRS >= NW ? 1 : NW / PAIRS;  // waves per pair
   constexpr int XR = ROWS + 4;
+  constexpr int ROWLEN = COUT * N + COUT;
   typedef MM<T> mm;
   __shared__ __attribute__((aligned(16))) T dyl[COUT * ROWS * WP];
+  constexpr int WX = WP + 4;  // padded input row (2 halo columns each side, room for the kw shift)
   __shared__ __attribute__((aligned(16))) T xs[5 * CIN * XR * WP];
+  __shared__ __attribute__((aligned(16))) T xpad[CIN * XR * WX];
+  __shared__ f32x4 kred[KSPLIT > 1 ? NW : 1][64];
 
   const int tid = threadIdx.x;
   const int b = blockIdx.x / nsplit, sp = blockIdx.x % nsplit;
   const int r0 = sp * ROWS;
   const T* xb = x + (size_t)b * CIN * H * W;
   const T* dyb = dy + (size_t)b * COUT * H * W;
+  const T zero = Cvt<T>::from_f(0.f);
 
-  for (int e = tid; e < COUT * ROWS * WP; e += NTHR) {
-    const int co = e / (ROWS * WP), rem = e % (ROWS * WP);
-    const int rr = rem / WP, cc = rem % WP;
-    const int row = r0 + rr;
-    dyl[e] = (row < H && cc < W) ? dyb[(co * H + row) * W + cc] : Cvt<T>::from_f(0.f);
+  // dy chunk -> dyl[co][rr][0..WP) (pad columns zero)
+  for (int e = tid; e < COUT * ROWS * (WP - W); e += NTHR) {
+    const int cr = e / (WP - W), cc = W + e % (WP - W);
+    dyl[cr * WP + cc] = zero;
   }
-  for (int e = tid; e < 5 * CIN * XR * WP; e += NTHR) {
-    const int kw = e / (CIN * XR * WP);
-    int rem = e % (CIN * XR * WP);
-    const int ci = rem / (XR * WP);
-    rem %= XR * WP;
-    const int rr = rem / WP, cc = rem % WP;
-    const int ih = r0 + rr - 2, iw = cc + kw - 2;
-    xs[e] = (ih >= 0 && ih < H && iw >= 0 && iw < W) ? xb[(ci * H + ih) * W + iw]
-                                                     : Cvt<T>::from_f(0.f);
+  if (r0 + ROWS > H) {  // rows past the image (last chunk): zero
+    for (int e = tid; e < COUT * ROWS * WP; e += NTHR)
+      if (r0 + (e / WP) % ROWS >= H) dyl[e] = zero;
+  }
+  // input rows r0-2 .. r0+ROWS+1 -> xpad[ci][XR][WX], columns shifted by 2 (zero halo)
+  for (int e = tid; e < CIN * XR * WX; e += NTHR) {
+    const int cc = e % WX, rr = (e / WX) % XR;
+    const int ih = r0 + rr - 2;
+    if (cc < 2 || cc >= W + 2 || ih < 0 || ih >= H) xpad[e] = zero;
+  }
+  if (ROWS == H) {  // whole image per workgroup: both operands are full [C][H][W] images
+    stage_chw<T, COUT, H, W>(dyb, [&](int co, int h, int ww, T a, T bb) {
+      dyl[(co * ROWS + h) * WP + ww] = a;
+      dyl[(co * ROWS + h) * WP + ww + 1] = bb;
+    });
+    stage_chw<T, CIN, H, W>(xb, [&](int ci, int h, int ww, T a, T bb) {
+      xpad[(ci * XR + h + 2) * WX + ww + 2] = a;
+      xpad[(ci * XR + h + 2) * WX + ww + 3] = bb;
+    });
+  } else {
+    for (int e = tid; e < COUT * ROWS * W; e += NTHR) {
+      const int co = e / (ROWS * W), rem = e % (ROWS * W);
+      const int rr = rem / W, cc = rem % W;
+      if (r0 + rr < H) dyl[(co * ROWS + rr) * WP + cc] = dyb[(co * H + r0 + rr) * W + cc];
+    }
+    for (int e = tid; e < CIN * XR * W; e += NTHR) {
+      const int ci = e / (XR * W), rem = e % (XR * W);
+      const int rr = rem / W, cc = rem % W;
+      const int ih = r0 + rr - 2;
+      if (ih >= 0 && ih < H) xpad[(ci * XR + rr) * WX + cc + 2] = xb[(ci * H + ih) * W + cc];
+    }
+  }
+  __syncthreads();
+  // 5 kw-shifted copies, LDS -> LDS: xs[kw][ci][rr][c] = xpad[ci][rr][c + kw]
+  for (int e = tid; e < 5 * CIN * XR * (WP / 8); e += NTHR) {
+    const int c8 = e % (WP / 8);
+    const int rowid = e / (WP / 8);  // (kw, ci, rr)
+    const int kw = rowid / (CIN * XR), cr = rowid % (CIN * XR);
+    const T* srcp = &xpad[cr * WX + 8 * c8 + kw];
+    T* dstp = &xs[rowid * WP + 8 * c8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dstp[j] = srcp[j];
   }
   __syncthreads();
 
+  float* row_out = wslab + (size_t)blockIdx.x * ROWLEN;
   const int lane = tid & 63, wv = tid >> 6;
   const int r = lane & 15, q = lane >> 4;
-  // bias grad: per output channel sum of dy over this chunk
-  for (int co = wv; co < COUT; co += NTHR / 64) {
+  // bias grad partial: per output channel sum of dy over this chunk
+  for (int co = wv; co < COUT; co += NW) {
     float a = 0.f;
     for (int i = lane; i < ROWS * WP; i += 64) a += Cvt<T>::to_f(dyl[co * ROWS * WP + i]);
     a = wave_sum(a);
-    if (lane == 0) atomicAdd(&db[co], a);
+    if (lane == 0) row_out[COUT * N + co] = a;
   }
-  for (int pr = wv; pr < MTL * NTL; pr += NTHR / 64) {
+  const int ks = KSPLIT > 1 ? wv % KSPLIT : 0;
+  const int pstart = KSPLIT > 1 ? wv / KSPLIT : wv;
+  const int pstep = KSPLIT > 1 ? NW / KSPLIT : NW;
+  for (int pr = pstart; pr < PAIRS; pr += pstep) {
     const int mt = pr / NTL, nt = pr % NTL;
     int n = nt * 16 + r;
-    const bool nvalid = n < N;
-    n = nvalid ? n : 0;
+    n = n < N ? n : 0;
     const int ci = n / 25, kh = (n % 25) / 5, kw = n % 5;
     const T* brow = &xs[((kw * CIN + ci) * XR + kh) * WP];
     const T* arow = &dyl[(mt * 16 + r) * ROWS * WP];
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < KSTEPS; ++s) {
+    for (int s = ks; s < KSTEPS; s += KSPLIT) {
       const int P = 32 * s + 8 * q;  // pixel index within the chunk
       const int row = P / WP, col0 = P % WP;
       const typename mm::frag a = mm::ld(arow + P);
       const typename mm::frag bf = mm::ld(brow + row * WP + col0);
       acc = mm::mma(a, bf, acc);
     }
+    if constexpr (KSPLIT > 1) {
+      kred[wv][lane] = acc;
+      __syncthreads();
+      if (ks != 0) continue;
+      for (int k2 = 1; k2 < KSPLIT; ++k2) acc += kred[wv + k2][lane];
+    }
     // D[row = 4q+i][col = r]: dW[co = mt*16+4q+i][n]
     const int col = nt * 16 + r;
     if (col < N) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) atomicAdd(&dw[(mt * 16 + 4 * q + i) * N + col], acc[i]);
+      for (int i = 0; i < 4; ++i) row_out[(mt * 16 + 4 * q + i) * N + col] = acc[i];
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Column sums of up to two slabs in one launch:
+//   out1[i] = sum_r slab1[r*n1 + i]  (i < n1),  out2[j] = sum_r slab2[r*n2 + j]  (j < n2)
+// A workgroup owns 16 columns; its 16 row-groups each sum every 16th row
+// (independent loads in flight), then combine through LDS.
+// ---------------------------------------------------------------------------
+constexpr int SR_COLS = 16, SR_GROUPS = NTHR / SR_COLS;
+__global__ void __launch_bounds__(NTHR)
+slab_reduce_kernel(const float* __restrict__ slab1, int rows1, int n1, float* __restrict__ out1,
+                   const float* __restrict__ slab2, int rows2, int n2, float* __restrict__ out2) {
+  __shared__ float part[SR_GROUPS][SR_COLS + 1];
+  const int nb1 = (n1 + SR_COLS - 1) / SR_COLS;
+  const bool first = (int)blockIdx.x < nb1;
+  const float* slab = first ? slab1 : slab2;
+  const int rows = first ? rows1 : rows2;
+  const int n = first ? n1 : n2;
+  float* out = first ? out1 : out2;
+  const int c0 = (first ? blockIdx.x : blockIdx.x - nb1) * SR_COLS;
+  const int col = c0 + (threadIdx.x % SR_COLS), g = threadIdx.x / SR_COLS;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (col < n) {
+    int rr = g;
+    for (; rr + 3 * SR_GROUPS < rows; rr += 4 * SR_GROUPS) {
+      a0 += slab[(size_t)rr * n + col];
+      a1 += slab[(size_t)(rr + SR_GROUPS) * n + col];
+      a2 += slab[(size_t)(rr + 2 * SR_GROUPS) * n + col];
+      a3 += slab[(size_t)(rr + 3 * SR_GROUPS) * n + col];
+    }
+    for (; rr < rows; rr += SR_GROUPS) a0 += slab[(size_t)rr * n + col];
+  }
+  part[g][threadIdx.x % SR_COLS] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (threadIdx.x < SR_COLS && c0 + (int)threadIdx.x < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int gg = 0; gg < SR_GROUPS; ++gg) t += part[gg][threadIdx.x];
+    out[c0 + threadIdx.x] = t;
   }
 }
 
@@ -419,21 +644,22 @@ struct Shape {
   }
 };
 
-// Compile-time instantiations (the ConvNet blocks).  Other shapes are routed
-// to the generic layer kernels by the Python side.
+// Compile-time instantiations (the ConvNet blocks).
 static const Shape kShapes[] = {{1, 16, 28, 28}, {16, 32, 14, 14}};
 
-// Call f(std::integral_constant<int, i>) for the instantiated shape index that
-// matches (cin, cout, h, w); returns false if none does.
 template <typename F>
 static bool with_shape(const Shape& s, F&& f) {
   if (s == kShapes[0]) { f(std::integral_constant<int, 0>{}); return true; }
   if (s == kShapes[1]) { f(std::integral_constant<int, 1>{}); return true; }
   return false;
 }
-template <int I> struct SH;
-template <> struct SH<0> { static constexpr int CIN = 1, COUT = 16, H = 28, W = 28, SPLIT = 4, WROWS = 7; };
-template <> struct SH<1> { static constexpr int CIN = 16, COUT = 32, H = 14, W = 14, SPLIT = 2, WROWS = 14; };
+// The per-channel kernels only depend on (C, H, W).
+template <typename F>
+static bool with_chw(int C, int H, int W, F&& f) {
+  if (C == 16 && H == 28 && W == 28) { f(std::integral_constant<int, 0>{}); return true; }
+  if (C == 32 && H == 14 && W == 14) { f(std::integral_constant<int, 1>{}); return true; }
+  return false;
+}
 
 template <typename F>
 static void with_t(DT dt, F&& f) {
@@ -448,24 +674,40 @@ bool supported(int cin, int cout, int h, int w) {
   return with_shape(Shape{cin, cout, h, w}, [](auto) {});
 }
 
-static Shape shape_of(const at::Tensor& x, const at::Tensor& w) {
-  return Shape{(int)x.size(1), (int)w.size(0), (int)x.size(2), (int)x.size(3)};
+// number of conv-forward workgroups (= rows of the forward stats slab)
+int64_t fwd_rows(int cin, int cout, int h, int w, int64_t B) {
+  int64_t r = -1;
+  with_shape(Shape{cin, cout, h, w}, [&](auto I) { r = B * SH<decltype(I)::value>::SPLIT; });
+  TORCH_CHECK(r >= 0, "conv block shape not instantiated");
+  return r;
 }
+// number of wgrad workgroups (= rows of the wgrad slab)
+int64_t wgrad_rows(int cin, int cout, int h, int w, int64_t B) {
+  int64_t r = -1;
+  with_shape(Shape{cin, cout, h, w}, [&](auto I) {
+    typedef SH<decltype(I)::value> S;
+    r = B * ((S::H + S::WROWS - 1) / S::WROWS);
+  });
+  TORCH_CHECK(r >= 0, "conv block shape not instantiated");
+  return r;
+}
+int64_t bwd_split(int64_t B) { return B >= kBwdSplit ? kBwdSplit : std::max<int64_t>(B, 1); }
 
-// Forward conv (+bias) [+ BN partial stats into `stats` (zeroed, len 3C+1)].
-void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor bias, at::Tensor y, c10::optional<at::Tensor> stats,
-              c10::optional<at::Tensor> shift) {
+// Forward conv (+bias) [+ BN partial sums into fslab, shift copy into fstats].
+void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor bias, at::Tensor y, c10::optional<at::Tensor> fslab,
+              c10::optional<at::Tensor> fstats, c10::optional<at::Tensor> shift) {
   DPA_CHECK_INPUT(x); DPA_CHECK_INPUT(w); DPA_CHECK_INPUT(bias); DPA_CHECK_INPUT(y);
   TORCH_CHECK(w.scalar_type() == at::kFloat && bias.scalar_type() == at::kFloat);
   TORCH_CHECK(y.scalar_type() == x.scalar_type());
-  const Shape s = shape_of(x, w);
+  const Shape s{(int)x.size(1), (int)w.size(0), (int)x.size(2), (int)x.size(3)};
   TORCH_CHECK(w.size(1) == s.cin && w.size(2) == 5 && w.size(3) == 5, "weight must be [COUT][CIN][5][5]");
   TORCH_CHECK(y.size(0) == x.size(0) && y.size(1) == s.cout && y.size(2) == s.h && y.size(3) == s.w);
   const int B = (int)x.size(0);
-  const bool st = stats.has_value();
+  const bool st = fslab.has_value();
   if (st) {
-    DPA_CHECK_INPUT((*stats)); DPA_CHECK_INPUT((*shift));
-    TORCH_CHECK(stats->numel() == stats_len(s.cout) && shift->numel() == s.cout);
+    DPA_CHECK_INPUT((*fslab)); DPA_CHECK_INPUT((*fstats)); DPA_CHECK_INPUT((*shift));
+    TORCH_CHECK(fstats->numel() == stats_len(s.cout) && shift->numel() == s.cout);
+    TORCH_CHECK(fslab->numel() == fwd_rows(s.cin, s.cout, s.h, s.w, B) * fslab_row(s.cout), "fslab size");
   }
   if (B == 0) return;
   hipStream_t stream = cur_stream();
@@ -476,11 +718,12 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor bias, at::Tensor y, c10::op
       typedef decltype(tag) T;
       if (st)
         hipLaunchKernelGGL((conv5x5_kernel<T, S::CIN, S::COUT, S::H, S::W, 0>), grid, blk, 0, stream, dptr<T>(x),
-                           w.data_ptr<float>(), bias.data_ptr<float>(), dptr<T>(y), stats->data_ptr<float>(),
-                           shift->data_ptr<float>(), S::SPLIT);
+                           w.data_ptr<float>(), bias.data_ptr<float>(), dptr<T>(y), fslab->data_ptr<float>(),
+                           fstats->data_ptr<float>(), shift->data_ptr<float>(), S::SPLIT);
       else
         hipLaunchKernelGGL((conv5x5_kernel<T, S::CIN, S::COUT, S::H, S::W, 1>), grid, blk, 0, stream, dptr<T>(x),
-                           w.data_ptr<float>(), bias.data_ptr<float>(), dptr<T>(y), nullptr, nullptr, S::SPLIT);
+                           w.data_ptr<float>(), bias.data_ptr<float>(), dptr<T>(y), nullptr, nullptr, nullptr,
+                           S::SPLIT);
     });
   });
   TORCH_CHECK(ok, "conv block shape not instantiated");
@@ -494,43 +737,38 @@ void conv_dgrad(at::Tensor dy, at::Tensor w, at::Tensor dx) {
   const int H = (int)dy.size(2), W = (int)dy.size(3);
   TORCH_CHECK(dy.size(1) == cout && dx.size(1) == cin && dx.scalar_type() == dy.scalar_type());
   const int B = (int)dy.size(0);
-  const bool ok = (cin == 16 && cout == 32 && H == 14 && W == 14);
-  TORCH_CHECK(ok, "dgrad shape not instantiated: ", cout, "->", cin, " ", H, "x", W);
+  TORCH_CHECK(cin == 16 && cout == 32 && H == 14 && W == 14, "dgrad shape not instantiated: ", cout, "->", cin, " ",
+              H, "x", W);
   if (B == 0) return;
   constexpr int ns = 2;
   hipStream_t stream = cur_stream();
   with_t(dt_of(dy), [&](auto tag) {
     typedef decltype(tag) T;
     hipLaunchKernelGGL((conv5x5_kernel<T, 32, 16, 14, 14, 2>), dim3(B * ns), dim3(NTHR), 0, stream, dptr<T>(dy),
-                       w.data_ptr<float>(), nullptr, dptr<T>(dx), nullptr, nullptr, ns);
+                       w.data_ptr<float>(), nullptr, dptr<T>(dx), nullptr, nullptr, nullptr, ns);
   });
   DPA_CHECK_LAUNCH();
 }
 
-// The per-channel kernels only depend on (C, H, W); find the instantiation.
-template <typename F>
-static bool with_chw(int C, int H, int W, F&& f) {
-  if (C == 16 && H == 28 && W == 28) { f(std::integral_constant<int, 0>{}); return true; }
-  if (C == 32 && H == 14 && W == 14) { f(std::integral_constant<int, 1>{}); return true; }
-  return false;
-}
-
-void bn_relu_pool(at::Tensor y, at::Tensor stats, at::Tensor gamma, at::Tensor beta, at::Tensor rmean,
-                  at::Tensor rvar, at::Tensor nbt, double momentum, double eps, bool train, at::Tensor p,
-                  at::Tensor idx) {
+void bn_relu_pool(at::Tensor y, c10::optional<at::Tensor> fslab, at::Tensor fstats, at::Tensor gamma, at::Tensor beta,
+                  at::Tensor rmean, at::Tensor rvar, at::Tensor nbt, double momentum, double eps, bool train,
+                  at::Tensor p, at::Tensor idx) {
   DPA_CHECK_INPUT(y); DPA_CHECK_INPUT(p); DPA_CHECK_INPUT(idx);
   const int B = (int)y.size(0), C = (int)y.size(1), H = (int)y.size(2), W = (int)y.size(3);
   TORCH_CHECK(idx.scalar_type() == at::kByte && p.scalar_type() == y.scalar_type());
   TORCH_CHECK(nbt.scalar_type() == at::kLong);
+  TORCH_CHECK(!train || fslab.has_value(), "train mode needs the forward slab");
   const int total = B * C * (H / 2) * (W / 2);
+  const int nrows = fslab.has_value() ? (int)(fslab->numel() / fslab_row(C)) : 0;
   hipStream_t stream = cur_stream();
   const bool ok = with_chw(C, H, W, [&](auto I) {
     typedef SH<decltype(I)::value> S;
     if (total == 0) return;
     with_t(dt_of(y), [&](auto tag) {
       typedef decltype(tag) T;
-      hipLaunchKernelGGL((bn_relu_pool_kernel<T, S::COUT, S::H, S::W>), dim3((total + NTHR - 1) / NTHR), dim3(NTHR), 0,
-                         stream, dptr<T>(y), stats.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
+      hipLaunchKernelGGL((bn_relu_pool_kernel<T, S::COUT, S::H, S::W>), dim3((total + NTHR - 1) / NTHR), dim3(NTHR),
+                         0, stream, dptr<T>(y), fslab.has_value() ? fslab->data_ptr<float>() : nullptr, nrows,
+                         fstats.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
                          rmean.data_ptr<float>(), rvar.data_ptr<float>(), nbt.data_ptr<int64_t>(), (float)momentum,
                          (float)eps, (int)train, dptr<T>(p), idx.data_ptr<uint8_t>(), total);
     });
@@ -539,32 +777,34 @@ void bn_relu_pool(at::Tensor y, at::Tensor stats, at::Tensor gamma, at::Tensor b
   DPA_CHECK_LAUNCH();
 }
 
-void bwd_reduce(at::Tensor dp, at::Tensor p, at::Tensor idx, at::Tensor y, at::Tensor stats, double eps,
-                at::Tensor sums) {
-  DPA_CHECK_INPUT(dp); DPA_CHECK_INPUT(y); DPA_CHECK_INPUT(sums);
+void bwd_reduce(at::Tensor dp, at::Tensor p, at::Tensor idx, at::Tensor y, at::Tensor fstats, double eps,
+                at::Tensor bslab) {
+  DPA_CHECK_INPUT(dp); DPA_CHECK_INPUT(y); DPA_CHECK_INPUT(bslab);
   TORCH_CHECK(dp.scalar_type() == y.scalar_type() && p.scalar_type() == y.scalar_type());
   const int B = (int)y.size(0), C = (int)y.size(1), H = (int)y.size(2), W = (int)y.size(3);
+  const int nsplit = (int)bwd_split(B);
+  TORCH_CHECK(bslab.numel() == (int64_t)nsplit * 2 * C, "bslab size");
   hipStream_t stream = cur_stream();
   const bool ok = with_chw(C, H, W, [&](auto I) {
     typedef SH<decltype(I)::value> S;
-    if (B == 0) return;
-    const int nsplit = B >= 8 ? 8 : B;
+    if (B == 0) { bslab.zero_(); return; }
     with_t(dt_of(y), [&](auto tag) {
       typedef decltype(tag) T;
       hipLaunchKernelGGL((bwd_reduce_kernel<T, S::COUT, S::H, S::W>), dim3(C, nsplit), dim3(NTHR), 0, stream,
-                         dptr<T>(dp), dptr<T>(p), idx.data_ptr<uint8_t>(), dptr<T>(y), stats.data_ptr<float>(),
-                         (float)eps, sums.data_ptr<float>(), B);
+                         dptr<T>(dp), dptr<T>(p), idx.data_ptr<uint8_t>(), dptr<T>(y), fstats.data_ptr<float>(),
+                         (float)eps, bslab.data_ptr<float>(), B);
     });
   });
   TORCH_CHECK(ok, "bwd_reduce shape not instantiated");
   DPA_CHECK_LAUNCH();
 }
 
-void bwd_elemt(at::Tensor dp, at::Tensor p, at::Tensor idx, at::Tensor y, at::Tensor stats, at::Tensor gsums,
+void bwd_elemt(at::Tensor dp, at::Tensor p, at::Tensor idx, at::Tensor y, at::Tensor fstats, at::Tensor gslab,
                at::Tensor gamma, double eps, at::Tensor dx) {
-  DPA_CHECK_INPUT(dp); DPA_CHECK_INPUT(y); DPA_CHECK_INPUT(dx);
+  DPA_CHECK_INPUT(dp); DPA_CHECK_INPUT(y); DPA_CHECK_INPUT(dx); DPA_CHECK_INPUT(gslab);
   const int B = (int)y.size(0), C = (int)y.size(1), H = (int)y.size(2), W = (int)y.size(3);
   const int total = B * C * (H / 2) * (W / 2);
+  const int nsplit = (int)(gslab.numel() / (2 * C));
   hipStream_t stream = cur_stream();
   const bool ok = with_chw(C, H, W, [&](auto I) {
     typedef SH<decltype(I)::value> S;
@@ -572,19 +812,21 @@ void bwd_elemt(at::Tensor dp, at::Tensor p, at::Tensor idx, at::Tensor y, at::Te
     with_t(dt_of(y), [&](auto tag) {
       typedef decltype(tag) T;
       hipLaunchKernelGGL((bwd_elemt_kernel<T, S::COUT, S::H, S::W>), dim3((total + NTHR - 1) / NTHR), dim3(NTHR), 0,
-                         stream, dptr<T>(dp), dptr<T>(p), idx.data_ptr<uint8_t>(), dptr<T>(y), stats.data_ptr<float>(),
-                         gsums.data_ptr<float>(), gamma.data_ptr<float>(), (float)eps, dptr<T>(dx), total);
+                         stream, dptr<T>(dp), dptr<T>(p), idx.data_ptr<uint8_t>(), dptr<T>(y), fstats.data_ptr<float>(),
+                         gslab.data_ptr<float>(), nsplit, gamma.data_ptr<float>(), (float)eps, dptr<T>(dx), total);
     });
   });
   TORCH_CHECK(ok, "bwd_elemt shape not instantiated");
   DPA_CHECK_LAUNCH();
 }
 
-void conv_wgrad(at::Tensor x, at::Tensor dy, at::Tensor dw, at::Tensor db) {
-  DPA_CHECK_INPUT(x); DPA_CHECK_INPUT(dy); DPA_CHECK_INPUT(dw); DPA_CHECK_INPUT(db);
-  TORCH_CHECK(dw.scalar_type() == at::kFloat && db.scalar_type() == at::kFloat);
+void conv_wgrad(at::Tensor x, at::Tensor dy, at::Tensor wslab) {
+  DPA_CHECK_INPUT(x); DPA_CHECK_INPUT(dy); DPA_CHECK_INPUT(wslab);
+  TORCH_CHECK(wslab.scalar_type() == at::kFloat);
   const int B = (int)x.size(0);
   const Shape s{(int)x.size(1), (int)dy.size(1), (int)x.size(2), (int)x.size(3)};
+  TORCH_CHECK(wslab.numel() == wgrad_rows(s.cin, s.cout, s.h, s.w, B) * (s.cout * s.cin * 25 + s.cout),
+              "wslab size");
   hipStream_t stream = cur_stream();
   const bool ok = with_shape(s, [&](auto I) {
     typedef SH<decltype(I)::value> S;
@@ -593,26 +835,56 @@ void conv_wgrad(at::Tensor x, at::Tensor dy, at::Tensor dw, at::Tensor db) {
     with_t(dt_of(x), [&](auto tag) {
       typedef decltype(tag) T;
       hipLaunchKernelGGL((conv5x5_wgrad_kernel<T, S::CIN, S::COUT, S::H, S::W, S::WROWS>), dim3(B * ns), dim3(NTHR),
-                         0, stream, dptr<T>(x), dptr<T>(dy), dw.data_ptr<float>(), db.data_ptr<float>(), ns);
+                         0, stream, dptr<T>(x), dptr<T>(dy), wslab.data_ptr<float>(), ns);
     });
   });
   TORCH_CHECK(ok, "wgrad shape not instantiated");
   DPA_CHECK_LAUNCH();
 }
 
+// out1 = column sums of slab1 [rows1][n1]; out2 = column sums of slab2 [rows2][n2]
+void slab_reduce(at::Tensor slab1, int64_t n1, at::Tensor out1, c10::optional<at::Tensor> slab2, int64_t n2,
+                 c10::optional<at::Tensor> out2) {
+  DPA_CHECK_INPUT(slab1); DPA_CHECK_INPUT(out1);
+  TORCH_CHECK(slab1.numel() % n1 == 0 && out1.numel() == n1);
+  const int rows1 = (int)(slab1.numel() / n1);
+  int rows2 = 0;
+  if (slab2.has_value()) {
+    DPA_CHECK_INPUT((*slab2)); DPA_CHECK_INPUT((*out2));
+    TORCH_CHECK(slab2->numel() % n2 == 0 && out2->numel() == n2);
+    rows2 = (int)(slab2->numel() / n2);
+  } else {
+    n2 = 0;
+  }
+  const int64_t nblk = (n1 + SR_COLS - 1) / SR_COLS + (n2 + SR_COLS - 1) / SR_COLS;
+  if (nblk == 0) return;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(nblk), dim3(NTHR), 0, cur_stream(),
+                     slab1.data_ptr<float>(), rows1, (int)n1, out1.data_ptr<float>(),
+                     slab2.has_value() ? slab2->data_ptr<float>() : nullptr, rows2, (int)n2,
+                     out2.has_value() ? out2->data_ptr<float>() : nullptr);
+  DPA_CHECK_LAUNCH();
+}
+
 }  // namespace cb
 
 void register_convblock(pybind11::module& m) {
+  namespace py = pybind11;
   auto s = m.def_submodule("convblock", "fused Conv5x5-BN-ReLU-MaxPool block kernels");
   s.def("supported", &cb::supported);
   s.def("stats_len", [](int C) { return cb::stats_len(C); });
-  s.def("conv_fwd", &cb::conv_fwd, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("bias"),
-        pybind11::arg("y"), pybind11::arg("stats") = pybind11::none(), pybind11::arg("shift") = pybind11::none());
+  s.def("fslab_row", [](int C) { return cb::fslab_row(C); });
+  s.def("fwd_rows", &cb::fwd_rows);
+  s.def("wgrad_rows", &cb::wgrad_rows);
+  s.def("bwd_split", &cb::bwd_split);
+  s.def("conv_fwd", &cb::conv_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"),
+        py::arg("fslab") = py::none(), py::arg("fstats") = py::none(), py::arg("shift") = py::none());
   s.def("conv_dgrad", &cb::conv_dgrad);
   s.def("conv_wgrad", &cb::conv_wgrad);
   s.def("bn_relu_pool", &cb::bn_relu_pool);
   s.def("bwd_reduce", &cb::bwd_reduce);
   s.def("bwd_elemt", &cb::bwd_elemt);
+  s.def("slab_reduce", &cb::slab_reduce, py::arg("slab1"), py::arg("n1"), py::arg("out1"),
+        py::arg("slab2") = py::none(), py::arg("n2") = 0, py::arg("out2") = py::none());
 }
 
 }  // namespace dpa

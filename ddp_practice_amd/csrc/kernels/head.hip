@@ -39,22 +39,51 @@ __device__ __forceinline__ typename MM<T>::frag load_col8(const S* base, int col
   return f;
 }
 
-// out[M][N] = x[M][K] . w[N][K]^T + b ; one 16x16 tile per block, K split over
-// the 4 waves, partials reduced through LDS.
+// Vector fast path: 8 elements of a row that is 16-B aligned when K % 8 == 0.
+template <typename T, typename S>
+__device__ __forceinline__ typename MM<T>::frag load_row8v(const S* base, int row, int rows, int k0, int K) {
+  if (row < rows && k0 + 8 <= K && (K & 7) == 0) {
+    const S* p = base + (size_t)row * K + k0;
+    typename MM<T>::frag f;
+    if constexpr (sizeof(S) == 4) {
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(p);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { f[j] = MM<T>::cv(lo[j]); f[4 + j] = MM<T>::cv(hi[j]); }
+    } else {
+      const u16x8 v = *reinterpret_cast<const u16x8*>(p);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const unsigned short bits = v[j];
+        S sv;
+        __builtin_memcpy(&sv, &bits, 2);
+        f[j] = MM<T>::cv(Cvt<S>::to_f(sv));
+      }
+    }
+    return f;
+  }
+  return load_row8<T, S>(base, row, rows, k0, K);
+}
+
+// out[M][N] = x[M][K] . w[N][K]^T + b ; one 16x16 tile per workgroup, K split
+// over 16 waves (vector loads straight to registers: every element is read
+// once, so no LDS staging), partials combined through LDS.
+constexpr int LIN_THR = 1024;
 template <typename T>
-__global__ void __launch_bounds__(NTHR)
+__global__ void __launch_bounds__(LIN_THR)
 linear_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w, const float* __restrict__ b,
                   T* __restrict__ out, int M, int N, int K) {
-  __shared__ f32x4 part[NTHR / 64][64];
+  constexpr int NW = LIN_THR / 64;
+  __shared__ f32x4 part[NW][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = lane & 15, q = lane >> 4;
   const int mt = blockIdx.x, nt = blockIdx.y;
   const int KS = (K + 31) / 32;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int s = wv; s < KS; s += NTHR / 64) {
+  for (int s = wv; s < KS; s += NW) {
     const int k0 = 32 * s + 8 * q;
-    const auto a = load_row8<T, T>(x, mt * 16 + r, M, k0, K);
-    const auto bf = load_row8<T, float>(w, nt * 16 + r, N, k0, K);
+    const auto a = load_row8v<T, T>(x, mt * 16 + r, M, k0, K);
+    const auto bf = load_row8v<T, float>(w, nt * 16 + r, N, k0, K);
     acc = MM<T>::mma(a, bf, acc);
   }
   part[wv][lane] = acc;
@@ -62,7 +91,7 @@ linear_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w, const fl
   if (wv == 0) {
     f32x4 t = part[0][lane];
 #pragma unroll
-    for (int i = 1; i < NTHR / 64; ++i) t += part[i][lane];
+    for (int i = 1; i < NW; ++i) t += part[i][lane];
     const int col = nt * 16 + r;
     if (col < N) {
       const float bb = b ? b[col] : 0.f;
@@ -239,7 +268,7 @@ void linear_fwd(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> b, at::Ten
   const float* bp = b.has_value() ? b->data_ptr<float>() : nullptr;
   const dim3 grid((M + 15) / 16, (N + 15) / 16);
   DPA_DISPATCH_T(dt_of(x), {
-    hipLaunchKernelGGL(linear_fwd_kernel<T>, grid, dim3(NTHR), 0, cur_stream(), dptr<T>(x),
+    hipLaunchKernelGGL(linear_fwd_kernel<T>, grid, dim3(LIN_THR), 0, cur_stream(), dptr<T>(x),
                        w.data_ptr<float>(), bp, dptr<T>(out), M, N, K);
   });
   DPA_CHECK_LAUNCH();

@@ -83,10 +83,12 @@ sgd_kernel(MTList L, float lr, float momentum, float dampening, float wd, int ne
   }
 }
 
-__global__ void update_scale_kernel(float* scale, int* tracker, const float* found_inf, float growth,
+__global__ void update_scale_kernel(float* scale, int* tracker, float* found_inf, float growth,
                                     float backoff, int interval) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  if (found_inf[0] != 0.f) {
+  const bool inf = found_inf[0] != 0.f;
+  found_inf[0] = 0.f;  // re-arm for the next step: unscale_check only ever sets it
+  if (inf) {
     scale[0] = scale[0] * backoff;
     tracker[0] = 0;
   } else {

@@ -3,6 +3,8 @@
 // Used by tests/test_kernels_gpu.py to pin the lane maps common.h documents.
 #include "common.h"
 
+#include <chrono>
+
 namespace dpa {
 
 __global__ void __launch_bounds__(64) mfma_selftest_kernel(const float* __restrict__ A,
@@ -42,7 +44,47 @@ std::vector<at::Tensor> mfma_selftest(at::Tensor A, at::Tensor B) {
   return {Dbf, Df};
 }
 
+__global__ void noop_kernel(float* p) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) p[0] += 1.f;
+}
+
+// Launch-floor microbenchmark: n dependent no-op launches on the current
+// stream, either eagerly or captured once into a hipGraph and replayed `reps`
+// times.  Returns microseconds per kernel (host wall clock, stream-synced).
+double launch_floor(at::Tensor buf, int64_t n, int64_t reps, bool graph, int64_t blocks) {
+  hipStream_t s = cur_stream();
+  float* p = buf.data_ptr<float>();
+  DPA_CHECK_HIP(hipStreamSynchronize(s));
+  if (!graph) {
+    auto t0 = std::chrono::high_resolution_clock::now();
+    for (int64_t r = 0; r < reps; ++r)
+      for (int64_t i = 0; i < n; ++i) hipLaunchKernelGGL(noop_kernel, dim3(blocks), dim3(64), 0, s, p);
+    DPA_CHECK_HIP(hipStreamSynchronize(s));
+    auto t1 = std::chrono::high_resolution_clock::now();
+    return std::chrono::duration<double, std::micro>(t1 - t0).count() / (double)(n * reps);
+  }
+  hipStream_t cs;
+  DPA_CHECK_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  hipGraph_t g;
+  hipGraphExec_t ge;
+  DPA_CHECK_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+  for (int64_t i = 0; i < n; ++i) hipLaunchKernelGGL(noop_kernel, dim3(blocks), dim3(64), 0, cs, p);
+  DPA_CHECK_HIP(hipStreamEndCapture(cs, &g));
+  DPA_CHECK_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  DPA_CHECK_HIP(hipGraphLaunch(ge, cs));
+  DPA_CHECK_HIP(hipStreamSynchronize(cs));
+  auto t0 = std::chrono::high_resolution_clock::now();
+  for (int64_t r = 0; r < reps; ++r) DPA_CHECK_HIP(hipGraphLaunch(ge, cs));
+  DPA_CHECK_HIP(hipStreamSynchronize(cs));
+  auto t1 = std::chrono::high_resolution_clock::now();
+  hipGraphExecDestroy(ge);
+  hipGraphDestroy(g);
+  hipStreamDestroy(cs);
+  return std::chrono::duration<double, std::micro>(t1 - t0).count() / (double)(n * reps);
+}
+
 void register_selftest(pybind11::module& m) {
+  m.def("launch_floor", &launch_floor, "us per dependent no-op kernel (eager or hipGraph)");
   m.def("mfma_selftest", &mfma_selftest, "16x16x32 bf16 and 16x16x4 f32 MFMA lane-map test");
 }
 
