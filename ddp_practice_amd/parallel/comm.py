@@ -258,6 +258,9 @@ def init_process_group(backend: str | None = None, init_method: str | None = "en
     if not dist.is_initialized():
         dist.init_process_group(torch_backend, init_method=init_method, world_size=world_size, rank=rank, **kw)
     r, w = dist.get_rank(), dist.get_world_size()
+    if torch_backend == "gloo" and w > 1 and "OMP_NUM_THREADS" not in os.environ:
+        # several CPU ranks on one host: do not oversubscribe the cores (torchrun's default too)
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // w))
     if torch_backend == "nccl":
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())

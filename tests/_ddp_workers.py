@@ -1,0 +1,114 @@
+"""Worker bodies for tests/test_ddp_cpu.py (run under tests/_dist.run)."""
+import copy
+
+import torch
+import torch.nn as nn
+
+
+def _batch(seed, n):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(n, 1, 28, 28, generator=g), torch.randint(0, 10, (n,), generator=g)
+
+
+def ddp_syncbn_equivalence(rank, world, per_rank):
+    """DDP(SyncBN ConvNet) on per-rank shards == single-process ConvNet on the full batch."""
+    import ddp_practice_amd.distributed as dist
+    from ddp_practice_amd.models import ConvNet
+    from ddp_practice_amd.optim import SGD
+    from ddp_practice_amd.parallel import DistributedDataParallel, convert_sync_batchnorm
+
+    torch.manual_seed(0)
+    ref = ConvNet()
+    torch.manual_seed(123 + rank)  # different init per rank: DDP must broadcast rank 0's
+    model = ConvNet()
+    if rank == 0:
+        model.load_state_dict(ref.state_dict())
+    model = DistributedDataParallel(convert_sync_batchnorm(model))
+    opt = SGD(model.parameters(), lr=0.1)
+    ref_opt = torch.optim.SGD(ref.parameters(), lr=0.1)
+    out = {}
+    for step in range(3):
+        x, y = _batch(step, per_rank * world)
+        xs, ys = x[rank * per_rank:(rank + 1) * per_rank], y[rank * per_rank:(rank + 1) * per_rank]
+        loss = nn.functional.cross_entropy(model(xs), ys)
+        opt.zero_grad()
+        loss.backward()
+        ref_loss = nn.functional.cross_entropy(ref(x), y)
+        ref_opt.zero_grad()
+        ref_loss.backward()
+        for (n, p), (_, q) in zip(model.module.named_parameters(), ref.named_parameters()):
+            torch.testing.assert_close(p.grad, q.grad, rtol=1e-4, atol=1e-5, msg=f"grad {n} step {step}")
+        opt.step()
+        ref_opt.step()
+    for (n, b), (_, rb) in zip(model.module.named_buffers(), ref.named_buffers()):
+        torch.testing.assert_close(b.float(), rb.float(), rtol=1e-4, atol=1e-5, msg=f"buffer {n}")
+    # all ranks hold identical parameters
+    flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    lo, hi = flat.clone(), flat.clone()
+    c = dist.default_comm()
+    c.all_reduce_(lo, "min")
+    c.all_reduce_(hi, "max")
+    assert torch.equal(lo, hi)
+    out["keys"] = list(model.state_dict().keys())
+    out["buckets"] = model.bucket_sizes_bytes()
+    return out
+
+
+def ddp_no_sync_and_unused(rank, world):
+    import ddp_practice_amd.distributed as dist
+    from ddp_practice_amd.parallel import DistributedDataParallel
+
+    class Net(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = nn.Linear(4, 3)
+            self.unused = nn.Linear(4, 3)
+
+        def forward(self, x):
+            return self.a(x)
+
+    torch.manual_seed(0)
+    net = DistributedDataParallel(Net(), find_unused_parameters=True)
+    x = torch.full((2, 4), float(rank + 1))
+    # no_sync: local accumulation, no all-reduce
+    with net.no_sync():
+        net(x).sum().backward()
+    g_local = net.module.a.weight.grad.clone()
+    # synced step accumulates on top and averages: (local + local)/world summed over ranks
+    net(x).sum().backward()
+    g = net.module.a.weight.grad
+    exp = torch.zeros_like(g)
+    for r in range(world):
+        exp += 2 * torch.full((3, 4), 2.0 * (r + 1)) / world
+    torch.testing.assert_close(g, exp)
+    assert torch.count_nonzero(net.module.unused.weight.grad) == 0
+    assert g_local.abs().sum() > 0
+    return True
+
+
+def comm_collectives(rank, world):
+    import ddp_practice_amd.distributed as dist
+
+    c = dist.default_comm()
+    t = torch.tensor([float(rank + 1)])
+    dist.all_reduce(t)
+    assert t.item() == sum(range(1, world + 1))
+    t = torch.tensor([float(rank)])
+    dist.reduce(t, 0)
+    if rank == 0:
+        assert t.item() == sum(range(world))
+    t = torch.tensor([float(rank + 5)])
+    dist.broadcast(t, 0)
+    assert t.item() == 5.0
+    out = torch.zeros(world * 2)
+    dist.all_gather_into_tensor(out, torch.tensor([float(rank), float(rank) * 10]))
+    assert out.tolist() == sum([[float(r), float(r) * 10] for r in range(world)], [])
+    rs = torch.zeros(1)
+    dist.reduce_scatter_tensor(rs, torch.arange(world, dtype=torch.float32))
+    assert rs.item() == rank * world
+    a2a = torch.zeros(world)
+    c.all_to_all_single(a2a, torch.full((world,), float(rank)))
+    assert a2a.tolist() == [float(r) for r in range(world)]
+    assert abs(dist.max_over_ranks(float(rank)) - (world - 1)) < 1e-6
+    dist.barrier()
+    return True

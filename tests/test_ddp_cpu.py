@@ -1,0 +1,47 @@
+"""DDP / SyncBN / communicator semantics on 2 CPU ranks (gloo)."""
+import pytest
+import torch
+
+from ddp_practice_amd.parallel import compute_bucket_assignment
+
+from . import _ddp_workers as W
+from ._dist import run
+
+pytestmark = pytest.mark.slow
+
+
+def test_ddp_syncbn_matches_single_process_full_batch():
+    outs = run(W.ddp_syncbn_equivalence, world=2, args=(8,))
+    keys = outs[0]["keys"]
+    assert keys[0] == "module.layer1.0.weight" and len(keys) == 16
+    assert "module.layer2.1.running_var" in keys and "module.fc.bias" in keys
+    assert outs[0]["buckets"] == [29034 * 4]
+
+
+def test_ddp_no_sync_and_find_unused():
+    assert run(W.ddp_no_sync_and_unused, world=2) == [True, True]
+
+
+def test_comm_collectives_gloo():
+    assert run(W.comm_collectives, world=3) == [True] * 3
+
+
+def _torch_buckets(params, first, cap):
+    import torch.distributed as dist
+
+    idx, _ = dist._compute_bucket_assignment_by_size(
+        params[::-1], [first, cap], [False] * len(params))
+    n = len(params)
+    return [[n - 1 - i for i in b] for b in idx]
+
+
+@pytest.mark.parametrize("shapes", [
+    [(16, 1, 5, 5), (16,), (16,), (16,), (32, 16, 5, 5), (32,), (32,), (32,), (10, 1568), (10,)],
+    [(2048, 2048), (2048,), (512, 512), (1000, 2048), (1000,), (64, 3, 7, 7)],
+])
+def test_bucket_assignment_matches_torch(shapes):
+    params = [torch.empty(s) for s in shapes]
+    first, cap = 1 << 20, 25 << 20
+    ours = compute_bucket_assignment(params, cap, first)
+    ref = _torch_buckets(params, first, cap)
+    assert sorted(map(sorted, ours)) == sorted(map(sorted, ref))
