@@ -2,6 +2,12 @@
 // Each translation unit exposes a register_* function; nothing here but glue.
 #include <torch/extension.h>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
+#include <cstdlib>
+
 namespace dpa {
 void register_selftest(pybind11::module& m);
 void register_convblock(pybind11::module& m);
@@ -12,7 +18,24 @@ void register_comm(pybind11::module& m);
 void register_reducer(pybind11::module& m);
 }
 
+// Opt-in (DPA_NATIVE_BACKTRACE=1) host-side SIGSEGV handler printing the native
+// stack: diagnostics for crashes inside the HIP runtime / RCCL / torch.
+static void dpa_segv_handler(int sig) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  const char msg[] = "\n[ddp_practice_amd] native backtrace:\n";
+  ssize_t w = write(2, msg, sizeof(msg) - 1);
+  (void)w;
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 PYBIND11_MODULE(_C, m) {
+  if (const char* e = std::getenv("DPA_NATIVE_BACKTRACE"); e && e[0] == '1') {
+    signal(SIGSEGV, dpa_segv_handler);
+    signal(SIGABRT, dpa_segv_handler);
+  }
   m.doc() = "ddp_practice_amd native extension (gfx950 HIP kernels, RCCL communicator, DDP reducer)";
   dpa::register_selftest(m);
   dpa::register_convblock(m);

@@ -1,6 +1,7 @@
 // Collective interface shared by the RCCL communicator and the DDP reducer.
 #pragma once
 
+#include <hip/hip_runtime.h>
 #include <torch/extension.h>
 
 #include <memory>
@@ -20,7 +21,8 @@ struct Collective {
   virtual int rank() const = 0;
   virtual int world() const = 0;
   virtual void all_reduce_async(at::Tensor t, RedOp op, int slot) = 0;
-  virtual void wait(int slot) = 0;
+  // stream == nullptr: the caller's current stream
+  virtual void wait(int slot, hipStream_t stream) = 0;
 };
 
 // Flat multi-tensor copy (csrc/kernels/optim.hip): direction 0 = pack into flat.

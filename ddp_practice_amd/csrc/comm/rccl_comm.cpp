@@ -226,9 +226,9 @@ class RcclComm : public Collective {
     DPA_CHECK_HIP(hipEventRecord(slot_[slot], stream_.stream()));
   }
 
-  void wait(int slot) override {
+  void wait(int slot, hipStream_t stream) override {
     TORCH_CHECK(slot >= 0 && slot < kSlots, "slot out of range");
-    DPA_CHECK_HIP(hipStreamWaitEvent(cur_stream(), slot_[slot], 0));
+    DPA_CHECK_HIP(hipStreamWaitEvent(stream ? stream : cur_stream(), slot_[slot], 0));
   }
 
  private:
@@ -281,7 +281,7 @@ class PyCollective : public Collective {
     const char* names[] = {"sum", "prod", "max", "min", "avg"};
     obj_.attr("all_reduce_")(t, names[(int)op]);
   }
-  void wait(int) override {}
+  void wait(int, hipStream_t) override {}
 
  private:
   pybind11::object obj_;
@@ -314,7 +314,7 @@ void register_comm(pybind11::module& m) {
       .def("all_reduce_async", [](comm::RcclComm& c, at::Tensor t, const std::string& op, int slot) {
         c.all_reduce_async(t, parse_op(op), slot);
       })
-      .def("wait", &comm::RcclComm::wait)
+      .def("wait", [](comm::RcclComm& c, int slot) { c.wait(slot, nullptr); })
       .def("async_error", &comm::RcclComm::async_error)
       .def("abort", &comm::RcclComm::abort)
       .def("destroy", &comm::RcclComm::destroy);

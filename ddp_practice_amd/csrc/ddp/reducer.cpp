@@ -22,10 +22,14 @@
 #include <torch/csrc/autograd/utils/lambda_post_hook.h>
 #include <torch/csrc/autograd/variable.h>
 
+#include <cstdlib>
 #include <mutex>
 
 #include "comm/collective.h"
 #include "common.h"
+
+#include <c10/hip/HIPGuard.h>
+#include <algorithm>
 
 namespace dpa {
 namespace ddp {
@@ -38,25 +42,46 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
           std::shared_ptr<Collective> comm, bool find_unused)
       : params_(std::move(params)), comm_(std::move(comm)), find_unused_(find_unused) {
     TORCH_CHECK(comm_ != nullptr);
+    if (const char* e = std::getenv("DPA_REDUCER_JOIN_EACH")) join_each_ = e[0] == '1';
     ready_.assign(params_.size(), 0);
     set_buckets(buckets);
   }
 
-  // Register hooks (needs shared_from_this, so after construction).
-  void install_hooks() {
+  // (Re)bind the post-hooks to the parameters' AccumulateGrad nodes.
+  //
+  // An AccumulateGrad node records the stream that was current when it was
+  // created, and the autograd engine syncs that "leaf stream" with the caller's
+  // stream at the end of every backward.  Nodes created on the legacy default
+  // stream therefore poison a hipGraph capture (an event record on the null
+  // stream while another stream captures).  So the nodes are (re)created lazily
+  // on the stream of the forward that will produce the backward — first
+  // training forward, and again at the forward of a graph capture — after
+  // dropping this reducer's strong references to the old ones.
+  void refresh_hooks_locked() {
     std::weak_ptr<Reducer> self = shared_from_this();
+    accs_.clear();
     for (size_t i = 0; i < params_.size(); ++i) {
       auto& p = params_[i];
       TORCH_CHECK(p.requires_grad(), "DDP parameter ", i, " does not require grad");
       auto acc = torch::autograd::impl::grad_accumulator(p);
       TORCH_CHECK(acc != nullptr, "parameter ", i, " has no grad accumulator (not a leaf?)");
-      acc->add_post_hook(std::make_unique<torch::autograd::utils::LambdaPostHook>(
-          [self, i](const variable_list& outputs, const variable_list&) {
-            if (auto r = self.lock()) r->mark_ready(i);
-            return outputs;
-          }));
+      bool hooked = false;
+      for (auto& w : hooked_)
+        if (auto n = w.lock(); n && n.get() == acc.get()) hooked = true;
+      if (!hooked) {
+        acc->add_post_hook(std::make_unique<torch::autograd::utils::LambdaPostHook>(
+            [self, i](const variable_list& outputs, const variable_list&) {
+              if (auto r = self.lock()) r->mark_ready(i);
+              return outputs;
+            }));
+        hooked_.push_back(acc);
+      }
       accs_.push_back(std::move(acc));
     }
+    // forget expired nodes
+    hooked_.erase(std::remove_if(hooked_.begin(), hooked_.end(), [](auto& w) { return w.expired(); }),
+                  hooked_.end());
+    hooks_ready_ = true;
   }
 
   void set_buckets(const std::vector<std::vector<int64_t>>& buckets) {
@@ -98,6 +123,21 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     reset_locked();
     sync_ = sync;
     expect_ = true;
+    // all reducer work (pack, collective fork/join) goes to the forward's stream,
+    // which is the stream the backward kernels run on (the capture stream when
+    // capturing), whatever stream the AccumulateGrad hooks happen to run under
+    on_cuda_ = !params_.empty() && params_[0].is_cuda();
+    if (on_cuda_) {
+      device_ = params_[0].get_device();
+      work_stream_ = cur_stream();
+    }
+    bool capturing = false;
+    if (on_cuda_) {
+      hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+      DPA_CHECK_HIP(hipStreamIsCapturing(work_stream_, &st));
+      capturing = st == hipStreamCaptureStatusActive;
+    }
+    if (!hooks_ready_ || capturing) refresh_hooks_locked();
   }
 
   void mark_ready(size_t i) {
@@ -106,22 +146,34 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     if (ready_[i]) return;           // reentrant backward hits the same hook twice: ignore
     if (!any_ready_) {
       any_ready_ = true;
-      // finalize at the end of this backward even if some params never get a grad
-      std::weak_ptr<Reducer> self = shared_from_this();
-      torch::autograd::Engine::get_default_engine().queue_callback([self]() {
-        if (auto r = self.lock()) r->finalize();
-      });
+      if (find_unused_) {
+        // params that never get a grad must still be reduced: finalize at the end
+        // of this backward (engine final callback)
+        std::weak_ptr<Reducer> self = shared_from_this();
+        torch::autograd::Engine::get_default_engine().queue_callback([self]() {
+          if (auto r = self.lock()) r->finalize();
+        });
+      }
     }
     ready_[i] = 1;
+    ++n_ready_;
     if (record_order_) order_.push_back((int64_t)i);
     Bucket& bk = buckets_[param_bucket_[i]];
     bk.pending -= 1;
     launch_ready_locked();
+    // every parameter reported: finalize right here, on the backward's stream
+    if (!find_unused_ && n_ready_ == params_.size()) finalize_locked();
   }
 
   void finalize() {
     std::lock_guard<std::mutex> g(mu_);
+    finalize_locked();
+  }
+
+  void finalize_locked() {
     if (!expect_ || finalized_) return;
+    c10::optional<c10::hip::HIPStreamGuard> guard;
+    bind_stream(guard);
     if (find_unused_) {
       for (size_t i = 0; i < params_.size(); ++i) {
         if (!ready_[i]) {
@@ -136,7 +188,10 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     for (auto& bk : buckets_)
       TORCH_CHECK(bk.launched, "DDP: bucket not reduced at end of backward (unused parameters? set "
                                "find_unused_parameters=True)");
-    for (size_t b = 0; b < buckets_.size(); ++b) comm_->wait((int)b);
+    // join on the stream the buckets were launched from (the backward's stream,
+    // i.e. the capture stream under hipGraph capture) — not whatever stream is
+    // current on the thread that runs the engine's final callback
+    for (size_t b = 0; b < buckets_.size(); ++b) comm_->wait((int)b, on_cuda_ ? work_stream_ : nullptr);
     // grads become views of the all-reduced buckets
     for (auto& bk : buckets_) {
       for (size_t j = 0; j < bk.params.size(); ++j) {
@@ -183,13 +238,21 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
       bk.unused.clear();
     }
     next_launch_ = 0;
+    n_ready_ = 0;
     any_ready_ = false;
     finalized_ = false;
     expect_ = false;
   }
 
   // launch every complete bucket whose predecessors have launched
+  void bind_stream(c10::optional<c10::hip::HIPStreamGuard>& g) {
+    if (on_cuda_ && work_stream_ != nullptr)
+      g.emplace(c10::hip::getStreamFromExternal(work_stream_, (c10::DeviceIndex)device_));
+  }
+
   void launch_ready_locked() {
+    c10::optional<c10::hip::HIPStreamGuard> guard;
+    bind_stream(guard);
     while (next_launch_ < buckets_.size() && buckets_[next_launch_].pending == 0) {
       Bucket& bk = buckets_[next_launch_];
       std::vector<at::Tensor> srcs;
@@ -216,6 +279,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
         }
       }
       comm_->all_reduce_async(bk.flat, RedOp::SUM, (int)next_launch_);
+      if (join_each_) comm_->wait((int)next_launch_, nullptr);
       bk.launched = true;
       ++next_launch_;
     }
@@ -230,8 +294,15 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   std::vector<int64_t> param_offset_;
   std::vector<char> ready_;
   size_t next_launch_ = 0;
+  size_t n_ready_ = 0;
   bool any_ready_ = false, finalized_ = false, expect_ = false, sync_ = true;
   bool record_order_ = true;
+  hipStream_t work_stream_ = nullptr;
+  int device_ = 0;
+  bool on_cuda_ = false;
+  bool hooks_ready_ = false;
+  std::vector<std::weak_ptr<torch::autograd::Node>> hooked_;
+  bool join_each_ = false;  // join every bucket immediately (no overlap)
   std::vector<int64_t> order_;
   std::mutex mu_;
 };
@@ -244,10 +315,8 @@ void register_reducer(pybind11::module& m) {
   py::class_<ddp::Reducer, std::shared_ptr<ddp::Reducer>>(s, "Reducer")
       .def(py::init([](std::vector<at::Tensor> params, std::vector<std::vector<int64_t>> buckets,
                        std::shared_ptr<Collective> comm, bool find_unused) {
-             auto r = std::make_shared<ddp::Reducer>(std::move(params), std::move(buckets), std::move(comm),
-                                                     find_unused);
-             r->install_hooks();
-             return r;
+             return std::make_shared<ddp::Reducer>(std::move(params), std::move(buckets), std::move(comm),
+                                                   find_unused);
            }),
            py::arg("params"), py::arg("buckets"), py::arg("comm"), py::arg("find_unused") = false)
       .def("prepare_for_backward", &ddp::Reducer::prepare_for_backward, py::arg("sync") = true)

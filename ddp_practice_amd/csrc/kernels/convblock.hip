@@ -137,7 +137,7 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
 
   __shared__ __attribute__((aligned(16))) T img[HP * WPD * CIN];
   __shared__ __attribute__((aligned(16))) T wl[COUT * KPW];
-  __shared__ float lstat[2 * COUT];
+  __shared__ float lstat[(NTHR / 64) * 2 * COUT];
 
   const int tid = threadIdx.x;
   const int b = blockIdx.x / nsplit;
@@ -167,7 +167,6 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
     const int wp = rem / CIN;
     if (hp < 2 || hp >= H + 2 || wp < 2 || wp >= W + 2) img[e] = zero;
   }
-  if (MODE == 0 && tid < 2 * COUT) lstat[tid] = 0.f;
   stage_chw<T, CIN, H, W>(xb, [&](int ci, int h, int ww, T a, T bb) {
     img[((h + 2) * WPD + (ww + 2)) * CIN + ci] = a;
     img[((h + 2) * WPD + (ww + 3)) * CIN + ci] = bb;
@@ -243,14 +242,19 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
       a1 += __shfl_xor(a1, 32, 64);
       a2 += __shfl_xor(a2, 16, 64);
       a2 += __shfl_xor(a2, 32, 64);
-      if (q == 0) {
-        atomicAdd(&lstat[nt * 16 + r], a1);  // LDS atomics: 4 waves per address
-        atomicAdd(&lstat[COUT + nt * 16 + r], a2);
+      if (q == 0) {  // per-wave partials, summed below in a fixed order (deterministic)
+        lstat[wv * 2 * COUT + nt * 16 + r] = a1;
+        lstat[wv * 2 * COUT + COUT + nt * 16 + r] = a2;
       }
     }
     __syncthreads();
     float* row = fslab + (size_t)blockIdx.x * fslab_row(COUT);
-    if (tid < 2 * COUT) row[tid] = lstat[tid];
+    if (tid < 2 * COUT) {
+      float t = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < NTHR / 64; ++w2) t += lstat[w2 * 2 * COUT + tid];
+      row[tid] = t;
+    }
     if (tid == 0) {
       const int p0 = mt0 * 16, p1 = min(mt1 * 16, HW);
       row[2 * COUT] = (float)(p1 - p0);

@@ -161,7 +161,7 @@ def evaluate(model, loader: DeviceLoader, comm=None, dst: int = 0):
         else:
             counters[0] += images.shape[0]
             counters[1] += (out.argmax(1) == labels).float().sum()
-    if comm is not None and comm.world_size > 1:
+    if comm is not None and comm.active:
         comm.reduce_(counters, dst, "sum")
     size, correct = counters.tolist()
     return correct, size

@@ -48,7 +48,7 @@ class ConvBlockFn(torch.autograd.Function):
         if training:
             fslab = torch.empty(C.fwd_rows(cin, cout, H, W, B) * C.fslab_row(cout), dtype=torch.float32, device=dev)
             C.conv_fwd(x, w, b, y, fslab, fstats, running_mean)
-            if comm is not None and comm.world_size > 1:
+            if comm is not None and comm.active:
                 comm.all_reduce_(fslab)
             C.bn_relu_pool(y, fslab, fstats, gamma, beta, running_mean, running_var, nbt, mom, float(eps), True, p,
                            idx)
@@ -78,7 +78,7 @@ class ConvBlockFn(torch.autograd.Function):
         bslab = torch.empty(nsplit * 2 * cout, dtype=torch.float32, device=dev)
         C.bwd_reduce(dp, p, idx, y, fstats, ctx.eps, bslab)
         comm = ctx.comm
-        if comm is not None and comm.world_size > 1:
+        if comm is not None and comm.active:
             gslab = comm.all_reduce(bslab)  # out of place: local sums stay the BN param grads
         else:
             gslab = bslab

@@ -52,6 +52,14 @@ class Communicator:
     rank: int = 0
     world_size: int = 1
     device: torch.device = torch.device("cpu")
+    # DPA_FORCE_COLLECTIVES=1 runs every collective code path even in a world of
+    # one (single-GPU tests of the RCCL / reducer / SyncBN paths under capture)
+    force_active: bool = os.environ.get("DPA_FORCE_COLLECTIVES", "0") == "1"
+
+    @property
+    def active(self) -> bool:
+        """True when collectives must actually run (world > 1, or forced)."""
+        return self.world_size > 1 or self.force_active
 
     # -- in-place / out-of-place all-reduce
     def all_reduce_(self, t: torch.Tensor, op="sum") -> torch.Tensor:

@@ -96,7 +96,7 @@ class DistributedDataParallel(nn.Module):
             not isinstance(self._owner_of_buffer(name), (SyncBatchNorm, nn.SyncBatchNorm))
             for name, _ in module.named_buffers())
         self.reducer = None
-        if self.comm.world_size > 1 and self._params:
+        if self.comm.active and self._params:
             buckets = compute_bucket_assignment(self._params, self.bucket_cap_bytes, self.first_bucket_bytes)
             self.reducer = _load_ext().ddp.Reducer(self._params, buckets, self.comm.native, find_unused_parameters)
 
@@ -149,7 +149,7 @@ class DistributedDataParallel(nn.Module):
                 self._rebuild_buckets()
             self.reducer.prepare_for_backward(self._sync_enabled)
             self._iteration += 1
-        if self._buffers_need_sync and self.comm.world_size > 1 and self.require_forward_param_sync:
+        if self._buffers_need_sync and self.comm.active and self.require_forward_param_sync:
             bufs = [b for b in self.module.buffers()]
             if bufs:
                 self._flat_broadcast(bufs)

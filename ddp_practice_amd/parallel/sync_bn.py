@@ -35,7 +35,7 @@ class _SyncBNFn(torch.autograd.Function):
         d = xf - shift
         n_local = float(x.numel() // C)
         stats = torch.cat([d.sum(red), (d * d).sum(red), torch.full((1,), n_local, device=x.device)])
-        if comm is not None and comm.world_size > 1:
+        if comm is not None and comm.active:
             comm.all_reduce_(stats)
         n = stats[2 * C]
         m1 = stats[:C] / n
@@ -69,7 +69,7 @@ class _SyncBNFn(torch.autograd.Function):
         s2 = (dyf * xhat).sum(red)
         sums = torch.cat([s1, s2])
         comm = ctx.comm
-        g = comm.all_reduce(sums) if (comm is not None and comm.world_size > 1) else sums
+        g = comm.all_reduce(sums) if (comm is not None and comm.active) else sums
         w = weight.float() if weight is not None else torch.ones(C, device=dy.device)
         k1 = (g[:C] / n).view(shp)
         k2 = (g[C:] / n).view(shp)
@@ -100,7 +100,7 @@ class SyncBatchNorm(_BatchNorm):
     def forward(self, x):
         self._check_input_dim(x)
         comm = self.comm
-        if not self.training or not self.track_running_stats or comm.world_size == 1:
+        if not self.training or not self.track_running_stats or not comm.active:
             if self.training and self.track_running_stats:
                 # the same shifted-sum path, world of one
                 return _SyncBNFn.apply(x, self.weight, self.bias, self.running_mean, self.running_var,

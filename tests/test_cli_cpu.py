@@ -1,0 +1,70 @@
+"""End-to-end CLI runs on CPU (BASELINE config 1 plumbing + gloo DDP), small synthetic sets."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from ._dist import free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.slow
+
+REF_KEYS = ["layer1.0.weight", "layer1.0.bias", "layer1.1.weight", "layer1.1.bias", "layer1.1.running_mean",
+            "layer1.1.running_var", "layer1.1.num_batches_tracked", "layer2.0.weight", "layer2.0.bias",
+            "layer2.1.weight", "layer2.1.bias", "layer2.1.running_mean", "layer2.1.running_var",
+            "layer2.1.num_batches_tracked", "fc.weight", "fc.bias"]
+
+
+def _run(args, cwd, env_extra=None, timeout=600):
+    env = dict(os.environ)
+    env.pop("CUDA_VISIBLE_DEVICES", None)
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, *args], cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def _check_stdout(out, epochs):
+    lines = [ln for ln in out.splitlines() if ln.strip()]
+    for e in range(epochs):
+        assert f"begin training of epoch {e + 1}/{epochs}" in lines
+    assert "begin testing" in lines
+    acc = [ln for ln in lines if ln.startswith("Accuracy is ")]
+    assert len(acc) == 1 and acc[0].endswith("%")
+    assert any(ln.startswith("time elapsed: ") and ln.endswith(" seconds") for ln in lines)
+    return float(acc[0][len("Accuracy is "):-1])
+
+
+def test_origin_main_cpu(tmp_path):
+    out = _run([os.path.join(ROOT, "origin_main.py"), "-e", "2", "--synthetic", "--train-samples", "2048",
+                "--test-samples", "512", "--seed", "0"], tmp_path)
+    acc = _check_stdout(out, 2)
+    assert acc > 20.0  # learns something in 128 tiny steps at lr 1e-4
+    ck = torch.load(tmp_path / "origin_checkpoint.pt", weights_only=True)
+    assert list(ck) == ["model"] and list(ck["model"]) == REF_KEYS
+    from ddp_practice_amd.models import ConvNet
+
+    m = ConvNet()
+    m.load_state_dict(ck["model"])
+
+
+def test_ddp_main_spawn_cpu(tmp_path):
+    out = _run([os.path.join(ROOT, "ddp_main.py"), "-e", "1", "--synthetic", "--train-samples", "1024",
+                "--test-samples", "256", "--cpu-procs", "2", "--amp-dtype", "fp32"], tmp_path,
+               {"MASTER_PORT": str(free_port()), "DPA_MASTER_ADDR": "127.0.0.1"})
+    _check_stdout(out, 1)
+    ck = torch.load(tmp_path / "ddp_checkpoint.pt", weights_only=True)
+    assert list(ck["model"]) == ["module." + k for k in REF_KEYS]
+
+
+def test_ddp_main_torchrun_cpu(tmp_path):
+    port = free_port()
+    out = _run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr=127.0.0.1",
+                f"--master-port={port}", os.path.join(ROOT, "ddp_main_torchrun.py"), "--gpu", "", "-e", "1",
+                "--synthetic", "--train-samples", "1024", "--test-samples", "256", "--amp-dtype", "bf16"], tmp_path)
+    _check_stdout(out, 1)
+    ck = torch.load(tmp_path / "ddp_checkpoint.pt", weights_only=True)
+    assert list(ck["model"]) == ["module." + k for k in REF_KEYS]
+    assert set(ck["scaler"]) == {"scale", "growth_factor", "backoff_factor", "growth_interval", "_growth_tracker"}

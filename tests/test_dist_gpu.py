@@ -1,0 +1,115 @@
+"""Single-GPU checks of the distributed stack: native RCCL communicator, DDP
+reducer, SyncBN-in-fused-block, all under hipGraph capture.
+
+World size is 1 on the test box; ``Communicator.force_active`` makes every
+collective code path run anyway (RCCL all-reduce of a world of one is the
+identity, so results must equal the non-distributed run).
+"""
+import copy
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rccl(C):
+    import ddp_practice_amd.distributed as dist
+    from ddp_practice_amd.parallel import comm as comm_mod
+
+    from ._dist import free_port
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1",
+                      LOCAL_RANK="0")
+    torch.cuda.set_device(0)
+    c = dist.init_process_group("nccl")
+    assert isinstance(c, comm_mod.RcclCommunicator)
+    old = comm_mod.Communicator.force_active
+    comm_mod.Communicator.force_active = True
+    yield c
+    comm_mod.Communicator.force_active = old
+    dist.destroy_process_group()
+
+
+def test_rccl_collectives_world1(rccl):
+    t = torch.arange(8, dtype=torch.float32, device="cuda")
+    rccl.all_reduce_(t)
+    assert t.tolist() == list(range(8))
+    o = rccl.all_reduce(t, "max")
+    assert torch.equal(o, t) and o.data_ptr() != t.data_ptr()
+    rccl.broadcast_(t, 0)
+    rccl.reduce_(t, 0)
+    out = torch.empty(8, device="cuda")
+    rccl.all_gather_into_tensor(out, t)
+    assert torch.equal(out, t)
+    rccl.reduce_scatter_tensor(out, t)
+    rccl.all_to_all_single(out, t)
+    assert torch.equal(out, t)
+    for dt in (torch.bfloat16, torch.float16, torch.int64):
+        x = torch.ones(5, dtype=dt, device="cuda")
+        rccl.all_reduce_(x)
+        assert x.float().sum().item() == 5
+    rccl.barrier()
+    assert rccl.async_error() == ""
+
+
+def test_rccl_under_graph_capture(rccl):
+    x = torch.ones(1024, device="cuda")
+    y = torch.empty_like(x)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        rccl.all_reduce_(x)
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(g):
+        x.mul_(2)
+        rccl.all_reduce_(x)
+        y.copy_(x)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert y[0].item() == 8.0
+
+
+def _train(model, steps, images, labels, scaler_on, use_graph):
+    from ddp_practice_amd.amp import GradScaler
+    from ddp_practice_amd.data import DeviceLoader, ImageDataset
+    from ddp_practice_amd.engine import TrainLoop
+    from ddp_practice_amd.nn import CrossEntropyLoss
+    from ddp_practice_amd.optim import SGD
+
+    ds = ImageDataset(images, labels)
+    loader = DeviceLoader(ds, batch_size=32, shuffle=False, device="cuda",
+                          dtype=torch.bfloat16 if scaler_on else torch.float32)
+    opt = SGD(model.parameters(), lr=0.05)
+    scaler = GradScaler() if scaler_on else None
+    loop = TrainLoop(model, CrossEntropyLoss(), opt, loader, scaler, use_graph=use_graph, steps_per_graph=4)
+    for _ in range(steps):
+        loop.run_epoch()
+    assert loop.graph_error is None, loop.graph_error
+    return model
+
+
+@pytest.mark.parametrize("graph", [False, True])
+@pytest.mark.parametrize("amp", [False, True])
+def test_ddp_syncbn_fused_graph_matches_plain(rccl, amp, graph):
+    """DDP(SyncBN ConvNet) with forced collectives, graph-captured, == plain ConvNet eager."""
+    from ddp_practice_amd.data import synthetic
+    from ddp_practice_amd.models import ConvNet
+    from ddp_practice_amd.parallel import DistributedDataParallel, convert_sync_batchnorm
+
+    ds = synthetic(32 * 9 + 5, seed=11)  # 9 full batches (2 graph replays + 1-step graph) + a tail of 5
+    torch.manual_seed(0)
+    dt = torch.bfloat16 if amp else None
+    plain = ConvNet(amp_dtype=dt).cuda()
+    ddp = DistributedDataParallel(convert_sync_batchnorm(copy.deepcopy(plain)), device_ids=[0])
+    assert ddp.reducer is not None
+    _train(plain, 2, ds.images, ds.labels, amp, use_graph=False)
+    _train(ddp, 2, ds.images, ds.labels, amp, use_graph=graph)
+    tol = 1e-5 if not amp else 2e-3
+    for (n, p), (_, q) in zip(ddp.module.state_dict().items(), plain.state_dict().items()):
+        torch.testing.assert_close(p.float(), q.float(), rtol=tol, atol=tol, msg=n)
+    assert int(ddp.module.layer1[1].num_batches_tracked) == 2 * 10
