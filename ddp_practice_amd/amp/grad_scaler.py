@@ -26,7 +26,8 @@ def _native_ok(t: torch.Tensor) -> bool:
 
 class GradScaler:
     def __init__(self, device: str = "cuda", init_scale: float = 2.0 ** 16, growth_factor: float = 2.0,
-                 backoff_factor: float = 0.5, growth_interval: int = 2000, enabled: bool = True):
+                 backoff_factor: float = 0.5, growth_interval: int = 2000, enabled: bool = True,
+                 fuse_step: bool = True):
         if growth_factor <= 1.0:
             raise ValueError("growth_factor should be > 1")
         if not (0.0 < backoff_factor < 1.0):
@@ -42,6 +43,11 @@ class GradScaler:
         self._found_inf: torch.Tensor | None = None
         self._per_opt: dict[int, dict[str, Any]] = {}
         self._armed = True  # device found_inf is known to be 0
+        # fused single-launch step: enabled once an iteration with exactly one
+        # optimizer has been seen (the fused kernel also performs update())
+        self._fuse_step = fuse_step
+        self._single_opt_iters = 0
+        self._fused_done = False
 
     # ------------------------------------------------------------------ state
     def _lazy_init(self, dev: torch.device):
@@ -74,7 +80,25 @@ class GradScaler:
         if isinstance(outputs, torch.Tensor):
             self._lazy_init(outputs.device)
             # 0-d scale: a 0-d loss stays 0-d, so backward needs no sum-to-shape reduction
-            return outputs * self._scale.to(outputs.device, non_blocking=True).view(())
+            s0 = self._scale.to(outputs.device, non_blocking=True).view(())
+            scaled = outputs * s0
+            if outputs.requires_grad and outputs.dim() == 0 and outputs.is_cuda:
+                # d(scale*loss)/dθ = scale * dloss/dθ: seed the loss's own backward
+                # with the scale tensor instead of a ones() fill + MulBackward kernel
+                # pair (2 fewer launches per step); any other use of `scaled`
+                # (extra terms, retain/create_graph, explicit gradient) goes
+                # through normal autograd.
+                base = outputs
+                seed = s0 if base.dtype == torch.float32 else s0.to(base.dtype)
+
+                def _backward(gradient=None, retain_graph=None, create_graph=False, inputs=None):
+                    if gradient is None and not create_graph:
+                        torch.autograd.backward(base, grad_tensors=seed, retain_graph=retain_graph, inputs=inputs)
+                    else:
+                        torch.Tensor.backward(scaled, gradient, retain_graph, create_graph, inputs)
+
+                scaled.backward = _backward
+            return scaled
         if isinstance(outputs, (list, tuple)):
             return type(outputs)(self.scale(o) for o in outputs)
         raise ValueError("outputs must be a Tensor or an iterable of Tensors")
@@ -123,6 +147,17 @@ class GradScaler:
         st = self._per_opt.setdefault(id(optimizer), {"stage": "ready"})
         if st["stage"] == "stepped":
             raise RuntimeError("step() has already been called since the last update().")
+        if self._fused_done:
+            raise RuntimeError("GradScaler: a fused AMP step already updated the scale in this iteration; "
+                               "use GradScaler(fuse_step=False) with several optimizers")
+        if (st["stage"] == "ready" and self._fuse_step and self._single_opt_iters >= 1 and self._scale is not None
+                and self._scale.is_cuda and getattr(optimizer, "can_fuse_amp", lambda: False)()):
+            # unscale + inf-check + SGD + scale update in one launch (update() becomes bookkeeping)
+            optimizer.fused_amp_step(self._scale, self._growth_tracker, self._found_inf, self._growth_factor,
+                                     self._backoff_factor, self._growth_interval)
+            self._fused_done = True
+            st["stage"] = "stepped"
+            return None
         if st["stage"] == "ready":
             self.unscale_(optimizer)
         ret = None
@@ -139,6 +174,15 @@ class GradScaler:
         if not self._enabled:
             return
         if self._scale is None:
+            return
+        self._single_opt_iters = self._single_opt_iters + 1 if len(self._per_opt) == 1 else 0
+        if self._fused_done:
+            # the fused step kernel already updated scale / tracker and re-armed found_inf
+            self._fused_done = False
+            self._armed = True
+            if new_scale is not None:
+                self._scale.fill_(new_scale) if isinstance(new_scale, float) else self._scale.copy_(new_scale)
+            self._per_opt = {}
             return
         if new_scale is not None:
             if isinstance(new_scale, float):

@@ -103,6 +103,61 @@ __global__ void update_scale_kernel(float* scale, int* tracker, float* found_inf
   }
 }
 
+// GradScaler.step + SGD + GradScaler.update in ONE single-workgroup launch, for
+// parameter sets small enough that one CU streams them twice in a few us
+// (the ConvNet: 29,034 floats).  Phase 1 decides found_inf for the whole set
+// (a block-wide OR, so no cross-workgroup protocol is needed), phase 2 writes
+// the unscaled grads back (torch semantics) and applies the update only if all
+// grads are finite, phase 3 updates scale / growth tracker and re-arms
+// found_inf.  p0 = param, p1 = grad, p2 = momentum buffer (or null).
+constexpr int FUSED_THR = 1024;
+__global__ void __launch_bounds__(FUSED_THR)
+amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ tracker, float* __restrict__ found_inf,
+                     float lr, float momentum, float dampening, float wd, int nesterov, int maximize, int first,
+                     float growth, float backoff, int interval) {
+  const float inv = 1.f / scale[0];
+  bool bad = false;
+  for (int t = 0; t < L.n; ++t) {
+    const float* g = L.p1[t];
+    for (int64_t i = threadIdx.x; i < L.numel[t]; i += FUSED_THR) bad |= !isfinite(g[i]);
+  }
+  bad = __syncthreads_or(bad);
+  for (int t = 0; t < L.n; ++t) {
+    float* p = L.p0[t];
+    float* g = L.p1[t];
+    float* buf = L.p2[t];
+    for (int64_t i = threadIdx.x; i < L.numel[t]; i += FUSED_THR) {
+      const float gv = g[i] * inv;
+      g[i] = gv;
+      if (bad) continue;
+      float d = maximize ? -gv : gv;
+      if (wd != 0.f) d += wd * p[i];
+      if (momentum != 0.f) {
+        const float bv = first ? d : momentum * buf[i] + (1.f - dampening) * d;
+        buf[i] = bv;
+        d = nesterov ? d + momentum * bv : bv;
+      }
+      p[i] -= lr * d;
+    }
+  }
+  if (threadIdx.x == 0) {
+    found_inf[0] = 0.f;
+    if (bad) {
+      scale[0] = scale[0] * backoff;
+      tracker[0] = 0;
+    } else {
+      const int succ = tracker[0] + 1;
+      if (succ == interval) {
+        const float ns = scale[0] * growth;
+        if (isfinite(ns)) scale[0] = ns;
+        tracker[0] = 0;
+      } else {
+        tracker[0] = succ;
+      }
+    }
+  }
+}
+
 // direction 0: flat[off_t + i] = src_t[i] * s ; direction 1: dst_t[i] = flat[off_t + i] * s
 __global__ void __launch_bounds__(NTHR)
 flat_copy_kernel(MTList L, float* __restrict__ flat, float s, int direction) {
@@ -180,6 +235,32 @@ void sgd_step(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std
   });
 }
 
+void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std::vector<at::Tensor> bufs,
+                   double lr, double momentum, double dampening, double wd, bool nesterov, bool maximize, bool first,
+                   at::Tensor scale, at::Tensor tracker, at::Tensor found_inf, double growth, double backoff,
+                   int64_t interval) {
+  TORCH_CHECK(params.size() == grads.size() && params.size() <= (size_t)MAXT, "fused AMP-SGD: <= ", MAXT,
+              " tensors");
+  TORCH_CHECK(bufs.empty() || bufs.size() == params.size());
+  check_f32(scale); check_f32(found_inf);
+  TORCH_CHECK(tracker.scalar_type() == at::kInt);
+  MTList L{};
+  L.n = (int)params.size();
+  for (size_t i = 0; i < params.size(); ++i) {
+    check_f32(params[i]); check_f32(grads[i]);
+    TORCH_CHECK(params[i].numel() == grads[i].numel());
+    L.numel[i] = params[i].numel();
+    L.p0[i] = params[i].data_ptr<float>();
+    L.p1[i] = grads[i].data_ptr<float>();
+    L.p2[i] = bufs.empty() ? nullptr : bufs[i].data_ptr<float>();
+  }
+  hipLaunchKernelGGL(amp_sgd_fused_kernel, dim3(1), dim3(FUSED_THR), 0, cur_stream(), L, scale.data_ptr<float>(),
+                     tracker.data_ptr<int>(), found_inf.data_ptr<float>(), (float)lr, (float)momentum,
+                     (float)dampening, (float)wd, (int)nesterov, (int)maximize, (int)first, (float)growth,
+                     (float)backoff, (int)interval);
+  DPA_CHECK_LAUNCH();
+}
+
 void update_scale(at::Tensor scale, at::Tensor tracker, at::Tensor found_inf, double growth, double backoff,
                   int64_t interval) {
   check_f32(scale); check_f32(found_inf);
@@ -225,6 +306,8 @@ void register_optim(pybind11::module& m) {
         pybind11::arg("nesterov"), pybind11::arg("maximize"), pybind11::arg("first"),
         pybind11::arg("found_inf") = pybind11::none(), pybind11::arg("grad_scale") = pybind11::none());
   s.def("update_scale", &opt::update_scale);
+  s.def("amp_sgd_fused", &opt::amp_sgd_fused);
+  s.attr("MAXT") = opt::MAXT;
   s.def("flat_copy", &opt::flat_copy);
 }
 

@@ -67,6 +67,47 @@ class SGD(Optimizer):
                 self._torch_step(group, params, grads, bufs, first)
         return loss
 
+    # ------------------------------------------------------------------ AMP
+    FUSED_AMP_MAX_NUMEL = 1 << 18
+
+    def _collect(self):
+        out = []
+        for group in self.param_groups:
+            params, grads, bufs, first = [], [], [], False
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                params.append(p)
+                grads.append(p.grad)
+                if group["momentum"] != 0:
+                    st = self.state[p]
+                    if st.get("momentum_buffer") is None:
+                        st["momentum_buffer"] = torch.zeros_like(p)
+                        first = True
+                    bufs.append(st["momentum_buffer"])
+            out.append((group, params, grads, bufs, first))
+        return out
+
+    def can_fuse_amp(self) -> bool:
+        """One parameter group of small f32 device tensors: unscale + inf-check +
+        SGD + scale update fit one single-workgroup launch."""
+        if len(self.param_groups) != 1:
+            return False
+        ps = [p for p in self.param_groups[0]["params"] if p.grad is not None]
+        if not ps or len(ps) > _load_ext().optim.MAXT:
+            return False
+        if sum(p.numel() for p in ps) > self.FUSED_AMP_MAX_NUMEL:
+            return False
+        return all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and p.grad.dtype == torch.float32
+                   and p.grad.is_contiguous() for p in ps)
+
+    @torch.no_grad()
+    def fused_amp_step(self, scale, tracker, found_inf, growth, backoff, interval):
+        (group, params, grads, bufs, first), = self._collect()
+        _load_ext().optim.amp_sgd_fused(params, grads, bufs, group["lr"], group["momentum"], group["dampening"],
+                                        group["weight_decay"], group["nesterov"], group["maximize"], first,
+                                        scale, tracker, found_inf, growth, backoff, interval)
+
     @staticmethod
     def _torch_step(group, params, grads, bufs, first):
         lr, mom, damp, wd = group["lr"], group["momentum"], group["dampening"], group["weight_decay"]

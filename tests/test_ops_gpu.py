@@ -214,3 +214,59 @@ def test_gather(C, dtype):
         torch.testing.assert_close(out.float(), (imgs[sel].float() / 255).unsqueeze(1).to(dtype).float())
         assert torch.equal(lab, labels[sel])
     assert ctr.tolist() == [3, 0]
+
+
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+def test_fused_amp_sgd_matches_unfused(C, momentum):
+    torch.manual_seed(0)
+    ps = [torch.randn(n, device=DEV) for n in (7, 3000, 29034)]
+    for inject_inf in (False, True):
+        gs = [torch.randn_like(p) * 512 for p in ps]
+        if inject_inf:
+            gs[2][5] = float("nan")
+        pa, pb = [p.clone() for p in ps], [p.clone() for p in ps]
+        ga, gb = [g.clone() for g in gs], [g.clone() for g in gs]
+        ba, bb = [torch.zeros_like(p) for p in ps], [torch.zeros_like(p) for p in ps]
+        sa, sb = torch.tensor([512.0], device=DEV), torch.tensor([512.0], device=DEV)
+        ta, tb = torch.zeros(1, dtype=torch.int32, device=DEV), torch.zeros(1, dtype=torch.int32, device=DEV)
+        fa, fb = torch.zeros(1, device=DEV), torch.zeros(1, device=DEV)
+        C.optim.amp_sgd_fused(pa, ga, ba, 0.1, momentum, 0.0, 1e-4, False, False, True, sa, ta, fa, 2.0, 0.5, 1)
+        C.optim.unscale_check(gb, sb, fb)
+        C.optim.sgd_step(pb, gb, bb, 0.1, momentum, 0.0, 1e-4, False, False, True, fb, None)
+        C.optim.update_scale(sb, tb, fb, 2.0, 0.5, 1)
+        for x, y in zip(pa + ga, pb + gb):
+            torch.testing.assert_close(x, y, equal_nan=True)
+        assert sa.item() == sb.item() == (256.0 if inject_inf else 1024.0)
+        assert ta.item() == tb.item() and fa.item() == fb.item() == 0.0
+
+
+def test_grad_scaler_fast_backward_and_fused_step(C):
+    """scaler.scale(loss).backward() seeds with the scale; fused step == torch GradScaler + SGD."""
+    from ddp_practice_amd.amp import GradScaler
+    from ddp_practice_amd.ops.head import cross_entropy
+    from ddp_practice_amd.optim import SGD
+
+    torch.manual_seed(0)
+    w0 = torch.randn(10, 20, device=DEV)
+    x = torch.randn(8, 20, device=DEV)
+    y = torch.randint(0, 10, (8,), device=DEV)
+    wa = torch.nn.Parameter(w0.clone())
+    wb = torch.nn.Parameter(w0.clone())
+    sa = GradScaler(init_scale=1024.0, growth_interval=2)
+    sb = torch.amp.GradScaler("cuda", init_scale=1024.0, growth_interval=2)
+    oa, ob = SGD([wa], lr=0.1), torch.optim.SGD([wb], lr=0.1)
+    for it in range(4):
+        la = cross_entropy(x @ wa.t(), y)
+        lb = torch.nn.functional.cross_entropy(x @ wb.t(), y)
+        oa.zero_grad()
+        ob.zero_grad()
+        sa.scale(la).backward()
+        sb.scale(lb).backward()
+        sa.step(oa)
+        sb.step(ob)
+        sa.update()
+        sb.update()
+        assert sa._fused_done is False
+        torch.testing.assert_close(wa, wb, rtol=1e-5, atol=1e-6)
+        assert sa.get_scale() == sb.get_scale()
+    assert sa._single_opt_iters >= 3  # the fused path was taken from iteration 2 on
