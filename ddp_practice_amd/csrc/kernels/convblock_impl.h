@@ -1,0 +1,788 @@
+// Fused "conv block" kernels for the ConvNet hot path:
+//     Conv2d(CIN->COUT, 5x5, stride 1, pad 2) -> BatchNorm2d -> ReLU -> MaxPool2d(2,2)
+// (reference: /root/reference/origin_main.py:12-23, ddp_main.py:16-27).
+//
+// Forward (train):  [conv_fwd: implicit-GEMM MFMA + bias + per-workgroup BN partial sums -> fslab]
+//                   -> (SyncBN: one all-reduce of fslab, host side)
+//                   -> [bn_relu_pool: reduce fslab, running-stat update,
+//                       normalise, ReLU, 2x2 max-pool, argmax index]
+// Backward:         [bwd_reduce: pool/ReLU routing + per-channel partial sum(dy), sum(dy*xhat) -> bslab]
+//                   -> (SyncBN: one all-reduce of bslab)
+//                   -> [bwd_elemt: BN input-grad at full resolution]
+//                   -> [conv_wgrad: MFMA per image chunk -> wslab]
+//                   -> [grad_reduce: wslab -> dW, db ; bslab -> dgamma, dbeta]
+//                   -> [conv_fwd<DGRAD>: input grad = conv of dy with flipped W^T]
+//
+// Design notes (MI355X):
+//  * Everything here is latency-bound (per-step GEMMs are 20-160 MFLOP): few
+//    launches, one LDS round trip per operand, >= 64 workgroups per launch.
+//  * No float atomics and no zero-fill launches: every cross-workgroup sum is
+//    a per-workgroup partial row ("slab") reduced by its consumer kernel.
+//    (Contended atomics — every workgroup adding into the same few hundred
+//    addresses — serialise at the memory side; the first version of this file
+//    spent 32 us per wgrad on them.)  Deterministic as a bonus.
+//  * im2col never touches HBM: the input image (with halo) sits in LDS in
+//    HWC order so that 8 K-consecutive elements (8 input channels of one tap)
+//    are one 16-B ds_read; conv1 (CIN=1) gathers its 25 taps element-wise.
+//  * wgrad keeps 5 kw-shifted copies of the input in LDS so that the B operand
+//    (8 consecutive output columns of one tap) is again one aligned 16-B read.
+//  * BN statistics are sums around a per-channel shift (the running mean,
+//    identical on every rank) to avoid E[x^2]-E[x]^2 cancellation; partial
+//    sums + counts make SyncBN ONE all-reduce with no device->host mask sync
+//    (cf. torch/nn/modules/_functions.py:74-101).
+#pragma once
+#include "common.h"
+
+namespace dpa {
+namespace cb {
+
+constexpr int NTHR = 256;
+
+// Final statistics buffer written by bn_relu_pool (read by the backward):
+// [0,C) sum(y-shift) | [C,2C) sum((y-shift)^2) | [2C] count | [2C+1,3C+1) shift
+__host__ __device__ constexpr int stats_len(int C) { return 3 * C + 1; }
+// forward partial-sum row per conv workgroup: [sum(C) | sumsq(C) | count]
+__host__ __device__ constexpr int fslab_row(int C) { return 2 * C + 1; }
+
+template <int I> struct SH;
+template <> struct SH<0> { static constexpr int CIN = 1, COUT = 16, H = 28, W = 28, SPLIT = 4, WROWS = 28; };
+template <> struct SH<1> { static constexpr int CIN = 16, COUT = 32, H = 14, W = 14, SPLIT = 2, WROWS = 14; };
+constexpr int kBwdSplit = 8;  // batch split of bwd_reduce
+
+// ---------------------------------------------------------------------------
+// Staging helpers.  Every global->LDS staging loop is split into "issue every
+// load into registers" then "convert + scatter into LDS", with compile-time
+// trip counts so all of a thread's loads are in flight together: one L2
+// round trip per staging phase instead of one per loop iteration (the loop
+// form cost 20+ us per kernel in the first profile).
+// ---------------------------------------------------------------------------
+// f32 array of N elements (N % 4 == 0, 16-B aligned) -> sink(e, v) per element
+template <int N, typename Sink>
+__device__ __forceinline__ void stage_f32(const float* __restrict__ src, Sink&& sink) {
+  static_assert(N % 4 == 0, "N must be a multiple of 4");
+  constexpr int N4 = N / 4;
+  constexpr int IT = (N4 + NTHR - 1) / NTHR;
+  f32x4 v[IT];
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int e = threadIdx.x + i * NTHR;
+    if (e < N4) v[i] = s4[e];
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int e = threadIdx.x + i * NTHR;
+    if (e < N4) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sink(4 * e + j, v[i][j]);
+    }
+  }
+}
+
+// [C][H][W] image of T (W even) -> sink(c, h, w, v_w, v_w+1) per element pair
+template <typename T> struct Pair2 { typedef uint32_t type; };
+template <> struct Pair2<float> { typedef uint64_t type; };
+template <typename T, int C, int H, int W, typename Sink>
+__device__ __forceinline__ void stage_chw(const T* __restrict__ src, Sink&& sink) {
+  static_assert(W % 2 == 0, "W must be even");
+  typedef typename Pair2<T>::type P;
+  constexpr int NP = C * H * W / 2;
+  constexpr int IT = (NP + NTHR - 1) / NTHR;
+  P v[IT];
+  const P* s2 = reinterpret_cast<const P*>(src);
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int e = threadIdx.x + i * NTHR;
+    if (e < NP) v[i] = s2[e];
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int e = threadIdx.x + i * NTHR;
+    if (e < NP) {
+      const int pe = 2 * e;
+      const int c = pe / (H * W), rem = pe % (H * W);
+      T a, b;
+      __builtin_memcpy(&a, &v[i], sizeof(T));
+      __builtin_memcpy(&b, reinterpret_cast<const char*>(&v[i]) + sizeof(T), sizeof(T));
+      sink(c, rem / W, rem % W, a, b);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// BatchNorm finalize, shared by bn_relu_pool and the fused prologues of the
+// next layer's kernel (ops/convnet_fused.py).  train: reduce the conv's
+// per-workgroup partial sums (nrows x (2C+1), L2-resident), publish the final
+// sums to fstats and update running stats on the leader workgroup; eval: use
+// the running stats.  Leaves per-channel y*sc + sh coefficients in LDS.
+// ---------------------------------------------------------------------------
+struct BNParams {
+  const float* fslab;
+  int nrows;
+  float* fstats;
+  const float* gamma;
+  const float* beta;
+  float* rmean;
+  float* rvar;
+  int64_t* nbt;
+  float momentum;
+  float eps;
+  int train;
+};
+
+// part: >= blockDim.x floats of LDS; ends with __syncthreads().
+template <int C>
+__device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, float* sh_s, float* part, bool leader) {
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  if (bp.train) {
+    constexpr int RL = 2 * C + 1;
+    const int G = nthr / RL;
+    const int j = tid % RL, g = tid / RL;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    if (g < G) {
+      int rr = g;
+      for (; rr + 3 * G < bp.nrows; rr += 4 * G) {
+        a0 += bp.fslab[(size_t)rr * RL + j];
+        a1 += bp.fslab[(size_t)(rr + G) * RL + j];
+        a2 += bp.fslab[(size_t)(rr + 2 * G) * RL + j];
+        a3 += bp.fslab[(size_t)(rr + 3 * G) * RL + j];
+      }
+      for (; rr < bp.nrows; rr += G) a0 += bp.fslab[(size_t)rr * RL + j];
+    }
+    part[tid] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (tid < RL) {
+      float t = 0.f;
+      for (int gg = 0; gg < G; ++gg) t += part[gg * RL + tid];
+      part[tid] = t;  // only this thread reads slot tid (its gg = 0 term) before the write
+    }
+    __syncthreads();
+    if (tid < C) {
+      const float n = part[2 * C];
+      const float m1 = part[tid] / n;
+      const float mean = bp.fstats[2 * C + 1 + tid] + m1;
+      const float var = fmaxf(part[C + tid] / n - m1 * m1, 0.f);
+      const float s = bp.gamma[tid] * rsqrtf(var + bp.eps);
+      sc_s[tid] = s;
+      sh_s[tid] = bp.beta[tid] - mean * s;
+      if (leader) {
+        bp.fstats[tid] = part[tid];
+        bp.fstats[C + tid] = part[C + tid];
+        if (tid == 0) bp.fstats[2 * C] = n;
+        const int64_t nb = bp.nbt[0] + 1;
+        const float mom = bp.momentum >= 0.f ? bp.momentum : 1.f / (float)nb;
+        bp.rmean[tid] = (1.f - mom) * bp.rmean[tid] + mom * mean;
+        bp.rvar[tid] = (1.f - mom) * bp.rvar[tid] + mom * var * (n / fmaxf(n - 1.f, 1.f));
+      }
+    }
+    __syncthreads();
+    if (leader && tid == 0) bp.nbt[0] = bp.nbt[0] + 1;
+  } else {
+    if (tid < C) {
+      const float s = bp.gamma[tid] * rsqrtf(bp.rvar[tid] + bp.eps);
+      sc_s[tid] = s;
+      sh_s[tid] = bp.beta[tid] - bp.rmean[tid] * s;
+    }
+    __syncthreads();
+  }
+}
+
+// BN -> ReLU -> 2x2 max (first max wins) of one window given as two row pairs.
+template <typename T>
+__device__ __forceinline__ void bn_relu_max4(const typename Pair2<T>::type top, const typename Pair2<T>::type bot,
+                                             float sc, float sh, float& best, int& bi) {
+  T v[4];
+  __builtin_memcpy(&v[0], &top, 2 * sizeof(T));
+  __builtin_memcpy(&v[2], &bot, 2 * sizeof(T));
+  best = -1.f;
+  bi = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float z = fmaxf(rnd_t<T>(Cvt<T>::to_f(v[k]) * sc + sh), 0.f);
+    if (z > best) { best = z; bi = k; }
+  }
+}
+
+// Input of a conv that starts with the previous block's BN -> ReLU -> MaxPool.
+template <typename T>
+struct PoolIn {
+  const T* y;          // previous conv output (pre-BN) [B][CIN][2H][2W]
+  BNParams bn;         // its BatchNorm
+  T* p_out;            // pooled output written for the backward (or null)
+  uint8_t* idx_out;    // argmax index written for the backward
+};
+
+// ---------------------------------------------------------------------------
+// Implicit-GEMM 5x5 convolution, one (image, m-range) per workgroup.
+//   MODE 0: forward + bias + BN partial sums        (train)
+//   MODE 1: forward + bias                          (eval)
+//   MODE 2: data-grad: input = dy (CIN = COUT_orig), output = dx,
+//           W_eff[co][ci][kh][kw] = W[ci][co][4-kh][4-kw], no bias
+// GEMM view: rows = output pixels of one image, cols = output channels,
+// K = 25*CIN ordered (kh, kw, ci) with ci fastest.
+// ---------------------------------------------------------------------------
+//   PRO 0: the input image is read from x;
+//   PRO 1: the input is produced in the staging pass from the previous block's
+//          pre-BN output (pin: BN finalize -> normalise -> ReLU -> 2x2 max-pool),
+//          which also writes the pooled map + argmax for the backward (split 0).
+template <typename T, int CIN, int COUT, int H, int W, int MODE, int PRO = 0>
+__global__ void __launch_bounds__(NTHR)
+conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+               T* __restrict__ y, float* __restrict__ fslab, float* __restrict__ fstats,
+               const float* __restrict__ shift, int nsplit, PoolIn<T> pin = PoolIn<T>{}) {
+  static_assert(CIN == 1 || CIN % 8 == 0, "CIN must be 1 or a multiple of 8");
+  static_assert(COUT % 16 == 0, "COUT must be a multiple of 16");
+  static_assert((H * W) % 4 == 0, "H*W must be a multiple of 4");
+  constexpr int HP = H + 4, WPD = W + 4;
+  constexpr int K = 25 * CIN;
+  constexpr int KP = ceil_to(K, 32);
+  constexpr int KS = KP / 32;
+  constexpr int KPW = KP + 8;  // LDS row pitch of the weight tile (breaks bank aliasing)
+  constexpr int NT = COUT / 16;
+  constexpr int HW = H * W;
+  constexpr int MT = (HW + 15) / 16;
+  typedef MM<T> mm;
+
+  __shared__ __attribute__((aligned(16))) T img[HP * WPD * CIN];
+  __shared__ __attribute__((aligned(16))) T wl[COUT * KPW];
+  __shared__ float lstat[(NTHR / 64) * 2 * COUT];
+
+  const int tid = threadIdx.x;
+  const int b = blockIdx.x / nsplit;
+  const int sp = blockIdx.x % nsplit;
+  const T* xb = x + (size_t)b * CIN * HW;
+
+  // --- stage weights (batched float4 reads in natural [co][ci][kh][kw] order,
+  //     scattered LDS writes to wl[co][(kh*5+kw)*CIN + ci])
+  const T zero = Cvt<T>::from_f(0.f);
+  if constexpr (KP > K) {
+    for (int e = tid; e < COUT * (KP - K); e += NTHR) wl[(e / (KP - K)) * KPW + K + e % (KP - K)] = zero;
+  }
+  // natural W index e = (o * WIN + i) * 25 + tap, WIN = in-channels of W
+  // (= CIN here, = COUT for the data-grad where W is [CIN][COUT][5][5])
+  constexpr int KO = 25 * (MODE == 2 ? COUT : CIN);
+  stage_f32<COUT * K>(w, [&](int e, float v) {
+    const int o = e / KO, rem = e % KO;      // o: out-ch of W
+    const int i = rem / 25, tap = rem % 25;  // i: in-ch of W
+    if (MODE == 2)  // W_eff[co=i][ci=o][tap'] with tap' = 24 - tap
+      wl[i * KPW + (24 - tap) * CIN + o] = Cvt<T>::from_f(v);
+    else
+      wl[o * KPW + tap * CIN + i] = Cvt<T>::from_f(v);
+  });
+  // --- stage the zero-padded image in HWC order
+  for (int e = tid; e < HP * WPD * CIN; e += NTHR) {
+    const int hp = e / (WPD * CIN), rem = e % (WPD * CIN);
+    const int wp = rem / CIN;
+    if (hp < 2 || hp >= H + 2 || wp < 2 || wp >= W + 2) img[e] = zero;
+  }
+  if constexpr (PRO == 0) {
+    stage_chw<T, CIN, H, W>(xb, [&](int ci, int h, int ww, T a, T bb) {
+      img[((h + 2) * WPD + (ww + 2)) * CIN + ci] = a;
+      img[((h + 2) * WPD + (ww + 3)) * CIN + ci] = bb;
+    });
+  } else {
+    __shared__ float sc_s[CIN], sh_s[CIN];
+    __shared__ float part[NTHR];
+    bn_finalize<CIN>(pin.bn, sc_s, sh_s, part, blockIdx.x == 0);
+    typedef typename Pair2<T>::type P;
+    constexpr int NPO = CIN * HW;  // pooled outputs of one image = this conv's input
+    constexpr int IT = (NPO + NTHR - 1) / NTHR;
+    const T* yb = pin.y + (size_t)b * CIN * 4 * HW;
+    P top[IT], bot[IT];
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = tid + i * NTHR;
+      if (e < NPO) {
+        const int ci = e / HW, pix = e % HW, ho = pix / W, wo = pix % W;
+        const P* src = reinterpret_cast<const P*>(yb + ((size_t)ci * 2 * H + 2 * ho) * 2 * W + 2 * wo);
+        top[i] = src[0];
+        bot[i] = src[W];  // next input row (2W elements = W pairs)
+      }
+    }
+    const bool wr = pin.p_out != nullptr && sp == 0;
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = tid + i * NTHR;
+      if (e < NPO) {
+        const int ci = e / HW, pix = e % HW, ho = pix / W, wo = pix % W;
+        float best;
+        int bi;
+        bn_relu_max4<T>(top[i], bot[i], sc_s[ci], sh_s[ci], best, bi);
+        const T pv = Cvt<T>::from_f(best);
+        img[((ho + 2) * WPD + (wo + 2)) * CIN + ci] = pv;
+        if (wr) {
+          pin.p_out[(size_t)b * NPO + e] = pv;
+          pin.idx_out[(size_t)b * NPO + e] = (uint8_t)bi;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  const int lane = tid & 63, wv = tid >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int mt0 = (MT * sp) / nsplit, mt1 = (MT * (sp + 1)) / nsplit;
+
+  float s1[NT], s2[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) s1[nt] = s2[nt] = 0.f;
+
+  for (int mt = mt0 + wv; mt < mt1; mt += NTHR / 64) {
+    const int m = mt * 16 + r;
+    const int mm_ = m < HW ? m : HW - 1;
+    const int oh = mm_ / W, ow = mm_ % W;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      typename mm::frag a;
+      if constexpr (CIN == 1) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int tap = 32 * s + 8 * q + j;
+          float v = 0.f;
+          if (tap < 25) v = Cvt<T>::to_f(img[(oh + tap / 5) * WPD + ow + tap % 5]);
+          a[j] = mm::cv(v);
+        }
+      } else {
+        const int kb = 32 * s + 8 * q;
+        int tap = kb / CIN;
+        const int ci0 = kb % CIN;
+        tap = tap < 25 ? tap : 24;  // K padding: weights are zero there
+        a = mm::ld(&img[((oh + tap / 5) * WPD + ow + tap % 5) * CIN + ci0]);
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const typename mm::frag bf = mm::ld(&wl[(nt * 16 + r) * KPW + 32 * s + 8 * q]);
+        acc[nt] = mm::mma(a, bf, acc[nt]);
+      }
+    }
+    // --- epilogue: D[row = 4q+i][col = r] -> pixel mt*16+4q+i, channel nt*16+r
+    const int pix0 = mt * 16 + 4 * q;
+    if (pix0 < HW) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int co = nt * 16 + r;
+        const float bs = (MODE == 2) ? 0.f : bias[co];
+        T* dst = y + ((size_t)b * COUT + co) * HW + pix0;
+        const float sh = (MODE == 0) ? shift[co] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v = acc[nt][i] + bs;
+          dst[i] = Cvt<T>::from_f(v);
+          if (MODE == 0) {
+            const float d = rnd_t<T>(v) - sh;
+            s1[nt] += d;
+            s2[nt] += d * d;
+          }
+        }
+      }
+    }
+  }
+  if constexpr (MODE == 0) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      float a1 = s1[nt], a2 = s2[nt];
+      a1 += __shfl_xor(a1, 16, 64);
+      a1 += __shfl_xor(a1, 32, 64);
+      a2 += __shfl_xor(a2, 16, 64);
+      a2 += __shfl_xor(a2, 32, 64);
+      if (q == 0) {  // per-wave partials, summed below in a fixed order (deterministic)
+        lstat[wv * 2 * COUT + nt * 16 + r] = a1;
+        lstat[wv * 2 * COUT + COUT + nt * 16 + r] = a2;
+      }
+    }
+    __syncthreads();
+    float* row = fslab + (size_t)blockIdx.x * fslab_row(COUT);
+    if (tid < 2 * COUT) {
+      float t = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < NTHR / 64; ++w2) t += lstat[w2 * 2 * COUT + tid];
+      row[tid] = t;
+    }
+    if (tid == 0) {
+      const int p0 = mt0 * 16, p1 = min(mt1 * 16, HW);
+      row[2 * COUT] = (float)(p1 - p0);
+    }
+    if (blockIdx.x == 0 && tid < COUT) fstats[2 * COUT + 1 + tid] = shift[tid];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// BN finalize + normalise + ReLU + 2x2/2 max-pool (+ argmax index, first max
+// wins in (dy,dx) scan order as ATen's max_pool2d).  One thread per pooled
+// output.  Each workgroup first reduces the conv's per-workgroup partial sums
+// (nrows x (2C+1) floats, L2-resident); workgroup 0 publishes the final sums to
+// fstats and updates the running stats (momentum<0 => cumulative average).
+// ---------------------------------------------------------------------------
+template <typename T, int C, int H, int W>
+__global__ void __launch_bounds__(NTHR)
+bn_relu_pool_kernel(const T* __restrict__ y, const float* __restrict__ fslab, int nrows,
+                    float* __restrict__ fstats, const float* __restrict__ gamma, const float* __restrict__ beta,
+                    float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
+                    float momentum, float eps, int train, T* __restrict__ p, uint8_t* __restrict__ idx,
+                    int total) {
+  constexpr int HO = H / 2, WO = W / 2;
+  constexpr int RL = 2 * C + 1;
+  __shared__ float part[NTHR];
+  __shared__ float sc_s[C], sh_s[C];
+  const int tid = threadIdx.x;
+  if (train) {
+    // column j of the slab summed over rows; NTHR/RL row-groups in parallel
+    constexpr int G = NTHR / RL;  // >= 3 for C <= 32
+    static_assert(G >= 1, "C too large");
+    const int j = tid % RL, g = tid / RL;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    if (g < G) {
+      int rr = g;
+      for (; rr + 3 * G < nrows; rr += 4 * G) {
+        a0 += fslab[(size_t)rr * RL + j];
+        a1 += fslab[(size_t)(rr + G) * RL + j];
+        a2 += fslab[(size_t)(rr + 2 * G) * RL + j];
+        a3 += fslab[(size_t)(rr + 3 * G) * RL + j];
+      }
+      for (; rr < nrows; rr += G) a0 += fslab[(size_t)rr * RL + j];
+    }
+    part[tid] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (tid < RL) {
+      float t = 0.f;
+      for (int gg = 0; gg < G; ++gg) t += part[gg * RL + tid];
+      part[tid] = t;  // each tid < RL only touches its own column's slots (gg*RL + tid)
+    }
+    __syncthreads();
+    if (tid < C) {
+      const float n = part[2 * C];
+      const float m1 = part[tid] / n;
+      const float shv = fstats[2 * C + 1 + tid];
+      const float mean = shv + m1;
+      const float var = fmaxf(part[C + tid] / n - m1 * m1, 0.f);
+      const float invstd = rsqrtf(var + eps);
+      const float s = gamma[tid] * invstd;
+      sc_s[tid] = s;
+      sh_s[tid] = beta[tid] - mean * s;
+      if (blockIdx.x == 0) {
+        fstats[tid] = part[tid];
+        fstats[C + tid] = part[C + tid];
+        if (tid == 0) fstats[2 * C] = n;
+        const int64_t nb = nbt[0] + 1;
+        const float mom = momentum >= 0.f ? momentum : 1.f / (float)nb;
+        rmean[tid] = (1.f - mom) * rmean[tid] + mom * mean;
+        rvar[tid] = (1.f - mom) * rvar[tid] + mom * var * (n / fmaxf(n - 1.f, 1.f));
+      }
+    }
+    __syncthreads();
+    if (blockIdx.x == 0 && tid == 0) nbt[0] = nbt[0] + 1;
+  } else {
+    if (tid < C) {
+      const float invstd = rsqrtf(rvar[tid] + eps);
+      const float s = gamma[tid] * invstd;
+      sc_s[tid] = s;
+      sh_s[tid] = beta[tid] - rmean[tid] * s;
+    }
+    __syncthreads();
+  }
+  const int e = blockIdx.x * NTHR + tid;
+  if (e >= total) return;
+  const int c = (e / (HO * WO)) % C;
+  const float sc = sc_s[c], sh = sh_s[c];
+  const int bc = e / (HO * WO), pix = e % (HO * WO);
+  const int ho = pix / WO, wo = pix % WO;
+  const T* src = y + (size_t)bc * H * W + (2 * ho) * W + 2 * wo;
+  float best = -1.f;
+  int bi = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float v = Cvt<T>::to_f(src[(k >> 1) * W + (k & 1)]);
+    const float z = fmaxf(rnd_t<T>(v * sc + sh), 0.f);
+    if (z > best) { best = z; bi = k; }
+  }
+  p[e] = Cvt<T>::from_f(best);
+  idx[e] = (uint8_t)bi;
+}
+
+// mean / invstd of channel c from the final stats buffer.
+template <int C>
+__device__ __forceinline__ void stats_mean_invstd(const float* fstats, int c, float eps, float& mean,
+                                                  float& invstd, float& n) {
+  n = fstats[2 * C];
+  const float m1 = fstats[c] / n;
+  mean = fstats[2 * C + 1 + c] + m1;
+  invstd = rsqrtf(fmaxf(fstats[C + c] / n - m1 * m1, 0.f) + eps);
+}
+
+// ---------------------------------------------------------------------------
+// Backward part 1: route the pooled grad through max-pool (argmax) and ReLU
+// (pooled output > 0), and reduce per channel into bslab[split][2C]:
+//   [c]     sum dy          (-> grad of BN bias)
+//   [C + c] sum dy * xhat   (-> grad of BN weight)
+// grid = (C, kBwdSplit over the batch).
+// ---------------------------------------------------------------------------
+template <typename T, int C, int H, int W>
+__global__ void __launch_bounds__(NTHR)
+bwd_reduce_kernel(const T* __restrict__ dp, const T* __restrict__ p, const uint8_t* __restrict__ idx,
+                  const T* __restrict__ y, const float* __restrict__ fstats, float eps,
+                  float* __restrict__ bslab, int B) {
+  constexpr int HO = H / 2, WO = W / 2, PP = HO * WO;
+  __shared__ float red[2 * NTHR / 64];
+  const int c = blockIdx.x;
+  const int nsplit = gridDim.y;
+  const int b0 = (B * blockIdx.y) / nsplit, b1 = (B * (blockIdx.y + 1)) / nsplit;
+  float mean, invstd, n;
+  stats_mean_invstd<C>(fstats, c, eps, mean, invstd, n);
+  float a1 = 0.f, a2 = 0.f;
+  const int cnt = (b1 - b0) * PP;
+  for (int t = threadIdx.x; t < cnt; t += NTHR) {
+    const int b = b0 + t / PP, pix = t % PP;
+    const size_t e = ((size_t)b * C + c) * PP + pix;
+    const float pv = Cvt<T>::to_f(p[e]);
+    if (pv > 0.f) {
+      const float g = Cvt<T>::to_f(dp[e]);
+      const int k = idx[e];
+      const int ho = pix / WO, wo = pix % WO;
+      const float yv = Cvt<T>::to_f(
+          y[((size_t)b * C + c) * H * W + (2 * ho + (k >> 1)) * W + 2 * wo + (k & 1)]);
+      a1 += g;
+      a2 += g * (yv - mean) * invstd;
+    }
+  }
+  a1 = wave_sum(a1);
+  a2 = wave_sum(a2);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) { red[wv] = a1; red[NTHR / 64 + wv] = a2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t1 = 0.f, t2 = 0.f;
+    for (int i = 0; i < NTHR / 64; ++i) { t1 += red[i]; t2 += red[NTHR / 64 + i]; }
+    bslab[blockIdx.y * 2 * C + c] = t1;
+    bslab[blockIdx.y * 2 * C + C + c] = t2;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward part 2: BN input gradient at full resolution, one thread per
+// pooled element (its 2x2 window):
+//   dx = gamma*invstd*(dy - S1/n - xhat*S2/n),  dy = routed pooled grad or 0
+// S1, S2 = column sums of the (all-reduced) bslab.
+// ---------------------------------------------------------------------------
+template <typename T, int C, int H, int W>
+__global__ void __launch_bounds__(NTHR)
+bwd_elemt_kernel(const T* __restrict__ dp, const T* __restrict__ p, const uint8_t* __restrict__ idx,
+                 const T* __restrict__ y, const float* __restrict__ fstats,
+                 const float* __restrict__ gslab, int nsplit, const float* __restrict__ gamma, float eps,
+                 T* __restrict__ dx, int total) {
+  constexpr int HO = H / 2, WO = W / 2, PP = HO * WO;
+  __shared__ float k_s[3 * C];
+  __shared__ float m_s[2 * C];
+  const int tid = threadIdx.x;
+  if (tid < C) {
+    float s1 = 0.f, s2 = 0.f;
+    for (int s = 0; s < nsplit; ++s) {
+      s1 += gslab[s * 2 * C + tid];
+      s2 += gslab[s * 2 * C + C + tid];
+    }
+    float mean, invstd, n;
+    stats_mean_invstd<C>(fstats, tid, eps, mean, invstd, n);
+    k_s[tid] = s1 / n;
+    k_s[C + tid] = s2 / n;
+    k_s[2 * C + tid] = gamma[tid] * invstd;
+    m_s[tid] = mean;
+    m_s[C + tid] = invstd;
+  }
+  __syncthreads();
+  const int e = blockIdx.x * NTHR + tid;
+  if (e >= total) return;
+  const int bc = e / PP, pix = e % PP;
+  const int c = bc % C;
+  const float k1 = k_s[c], k2 = k_s[C + c], gi = k_s[2 * C + c];
+  const float mean = m_s[c], invstd = m_s[C + c];
+  const float pv = Cvt<T>::to_f(p[e]);
+  const float g = pv > 0.f ? Cvt<T>::to_f(dp[e]) : 0.f;
+  const int kk = idx[e];
+  const int ho = pix / WO, wo = pix % WO;
+  const size_t base = (size_t)bc * H * W + (2 * ho) * W + 2 * wo;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const size_t o = base + (k >> 1) * W + (k & 1);
+    const float xh = (Cvt<T>::to_f(y[o]) - mean) * invstd;
+    const float dy = (k == kk) ? g : 0.f;
+    dx[o] = Cvt<T>::from_f(gi * (dy - k1 - xh * k2));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Weight/bias gradient partials of the 5x5 conv.  One workgroup per
+// (image, row-chunk); writes wslab[blk][COUT*N + COUT] (dW partial | db partial).
+// GEMM: rows = COUT, cols = (ci, kh, kw) natural order, K = pixels of the chunk
+// with the row padded to WP = ceil8(W) (dy is zero in the pad columns).
+// LDS: dy[COUT][ROWS][WP] and 5 kw-shifted copies xs[kw][CIN][ROWS+4][WP] of
+// the zero-padded input so both operands are aligned 16-B LDS reads.
+// When there are fewer (m,n) tile pairs than waves, waves split K instead
+// and combine through LDS.
+// ---------------------------------------------------------------------------
+template <typename T, int CIN, int COUT, int H, int W, int ROWS>
+__global__ void __launch_bounds__(NTHR)
+conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* __restrict__ wslab,
+                     int nsplit) {
+  constexpr int WP = ceil_to(W, 8);
+  static_assert((ROWS * WP) % 32 == 0, "ROWS*WP must be a multiple of 32");
+  constexpr int KSTEPS = ROWS * WP / 32;
+  constexpr int N = CIN * 25;
+  constexpr int NTL = (N + 15) / 16;
+  constexpr int MTL = COUT / 16;
+  constexpr int PAIRS = MTL * NTL;
+  constexpr int NW = NTHR / 64;
+  constexpr int KSPLIT = PAIRS >= NW ? 1 : NW / PAIRS;  // waves per pair
+  constexpr int XR = ROWS + 4;
+  constexpr int ROWLEN = COUT * N + COUT;
+  typedef MM<T> mm;
+  __shared__ __attribute__((aligned(16))) T dyl[COUT * ROWS * WP];
+  constexpr int WX = WP + 4;  // padded input row (2 halo columns each side, room for the kw shift)
+  __shared__ __attribute__((aligned(16))) T xs[5 * CIN * XR * WP];
+  __shared__ __attribute__((aligned(16))) T xpad[CIN * XR * WX];
+  __shared__ f32x4 kred[KSPLIT > 1 ? NW : 1][64];
+
+  const int tid = threadIdx.x;
+  const int b = blockIdx.x / nsplit, sp = blockIdx.x % nsplit;
+  const int r0 = sp * ROWS;
+  const T* xb = x + (size_t)b * CIN * H * W;
+  const T* dyb = dy + (size_t)b * COUT * H * W;
+  const T zero = Cvt<T>::from_f(0.f);
+
+  // dy chunk -> dyl[co][rr][0..WP) (pad columns zero)
+  for (int e = tid; e < COUT * ROWS * (WP - W); e += NTHR) {
+    const int cr = e / (WP - W), cc = W + e % (WP - W);
+    dyl[cr * WP + cc] = zero;
+  }
+  if (r0 + ROWS > H) {  // rows past the image (last chunk): zero
+    for (int e = tid; e < COUT * ROWS * WP; e += NTHR)
+      if (r0 + (e / WP) % ROWS >= H) dyl[e] = zero;
+  }
+  // input rows r0-2 .. r0+ROWS+1 -> xpad[ci][XR][WX], columns shifted by 2 (zero halo)
+  for (int e = tid; e < CIN * XR * WX; e += NTHR) {
+    const int cc = e % WX, rr = (e / WX) % XR;
+    const int ih = r0 + rr - 2;
+    if (cc < 2 || cc >= W + 2 || ih < 0 || ih >= H) xpad[e] = zero;
+  }
+  if (ROWS == H) {  // whole image per workgroup: both operands are full [C][H][W] images
+    stage_chw<T, COUT, H, W>(dyb, [&](int co, int h, int ww, T a, T bb) {
+      dyl[(co * ROWS + h) * WP + ww] = a;
+      dyl[(co * ROWS + h) * WP + ww + 1] = bb;
+    });
+    stage_chw<T, CIN, H, W>(xb, [&](int ci, int h, int ww, T a, T bb) {
+      xpad[(ci * XR + h + 2) * WX + ww + 2] = a;
+      xpad[(ci * XR + h + 2) * WX + ww + 3] = bb;
+    });
+  } else {
+    for (int e = tid; e < COUT * ROWS * W; e += NTHR) {
+      const int co = e / (ROWS * W), rem = e % (ROWS * W);
+      const int rr = rem / W, cc = rem % W;
+      if (r0 + rr < H) dyl[(co * ROWS + rr) * WP + cc] = dyb[(co * H + r0 + rr) * W + cc];
+    }
+    for (int e = tid; e < CIN * XR * W; e += NTHR) {
+      const int ci = e / (XR * W), rem = e % (XR * W);
+      const int rr = rem / W, cc = rem % W;
+      const int ih = r0 + rr - 2;
+      if (ih >= 0 && ih < H) xpad[(ci * XR + rr) * WX + cc + 2] = xb[(ci * H + ih) * W + cc];
+    }
+  }
+  __syncthreads();
+  // 5 kw-shifted copies, LDS -> LDS: xs[kw][ci][rr][c] = xpad[ci][rr][c + kw]
+  for (int e = tid; e < 5 * CIN * XR * (WP / 8); e += NTHR) {
+    const int c8 = e % (WP / 8);
+    const int rowid = e / (WP / 8);  // (kw, ci, rr)
+    const int kw = rowid / (CIN * XR), cr = rowid % (CIN * XR);
+    const T* srcp = &xpad[cr * WX + 8 * c8 + kw];
+    T* dstp = &xs[rowid * WP + 8 * c8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dstp[j] = srcp[j];
+  }
+  __syncthreads();
+
+  float* row_out = wslab + (size_t)blockIdx.x * ROWLEN;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  // bias grad partial: per output channel sum of dy over this chunk
+  for (int co = wv; co < COUT; co += NW) {
+    float a = 0.f;
+    for (int i = lane; i < ROWS * WP; i += 64) a += Cvt<T>::to_f(dyl[co * ROWS * WP + i]);
+    a = wave_sum(a);
+    if (lane == 0) row_out[COUT * N + co] = a;
+  }
+  const int ks = KSPLIT > 1 ? wv % KSPLIT : 0;
+  const int pstart = KSPLIT > 1 ? wv / KSPLIT : wv;
+  const int pstep = KSPLIT > 1 ? NW / KSPLIT : NW;
+  for (int pr = pstart; pr < PAIRS; pr += pstep) {
+    const int mt = pr / NTL, nt = pr % NTL;
+    int n = nt * 16 + r;
+    n = n < N ? n : 0;
+    const int ci = n / 25, kh = (n % 25) / 5, kw = n % 5;
+    const T* brow = &xs[((kw * CIN + ci) * XR + kh) * WP];
+    const T* arow = &dyl[(mt * 16 + r) * ROWS * WP];
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = ks; s < KSTEPS; s += KSPLIT) {
+      const int P = 32 * s + 8 * q;  // pixel index within the chunk
+      const int row = P / WP, col0 = P % WP;
+      const typename mm::frag a = mm::ld(arow + P);
+      const typename mm::frag bf = mm::ld(brow + row * WP + col0);
+      acc = mm::mma(a, bf, acc);
+    }
+    if constexpr (KSPLIT > 1) {
+      kred[wv][lane] = acc;
+      __syncthreads();
+      if (ks != 0) continue;
+      for (int k2 = 1; k2 < KSPLIT; ++k2) acc += kred[wv + k2][lane];
+    }
+    // D[row = 4q+i][col = r]: dW[co = mt*16+4q+i][n]
+    const int col = nt * 16 + r;
+    if (col < N) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) row_out[(mt * 16 + 4 * q + i) * N + col] = acc[i];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Column sums of up to two slabs in one launch:
+//   out1[i] = sum_r slab1[r*n1 + i]  (i < n1),  out2[j] = sum_r slab2[r*n2 + j]  (j < n2)
+// A workgroup owns 16 columns; its 16 row-groups each sum every 16th row
+// (independent loads in flight), then combine through LDS.
+// ---------------------------------------------------------------------------
+constexpr int SR_COLS = 16, SR_GROUPS = NTHR / SR_COLS;
+static __global__ void __launch_bounds__(NTHR)
+slab_reduce_kernel(const float* __restrict__ slab1, int rows1, int n1, float* __restrict__ out1,
+                   const float* __restrict__ slab2, int rows2, int n2, float* __restrict__ out2) {
+  __shared__ float part[SR_GROUPS][SR_COLS + 1];
+  const int nb1 = (n1 + SR_COLS - 1) / SR_COLS;
+  const bool first = (int)blockIdx.x < nb1;
+  const float* slab = first ? slab1 : slab2;
+  const int rows = first ? rows1 : rows2;
+  const int n = first ? n1 : n2;
+  float* out = first ? out1 : out2;
+  const int c0 = (first ? blockIdx.x : blockIdx.x - nb1) * SR_COLS;
+  const int col = c0 + (threadIdx.x % SR_COLS), g = threadIdx.x / SR_COLS;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (col < n) {
+    int rr = g;
+    for (; rr + 3 * SR_GROUPS < rows; rr += 4 * SR_GROUPS) {
+      a0 += slab[(size_t)rr * n + col];
+      a1 += slab[(size_t)(rr + SR_GROUPS) * n + col];
+      a2 += slab[(size_t)(rr + 2 * SR_GROUPS) * n + col];
+      a3 += slab[(size_t)(rr + 3 * SR_GROUPS) * n + col];
+    }
+    for (; rr < rows; rr += SR_GROUPS) a0 += slab[(size_t)rr * n + col];
+  }
+  part[g][threadIdx.x % SR_COLS] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (threadIdx.x < SR_COLS && c0 + (int)threadIdx.x < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int gg = 0; gg < SR_GROUPS; ++gg) t += part[gg][threadIdx.x];
+    out[c0 + threadIdx.x] = t;
+  }
+}
+
+}  // namespace cb
+}  // namespace dpa

@@ -46,10 +46,17 @@ unscale_check_kernel(MTList L, const float* __restrict__ scale, float* __restric
     const int64_t base = (c - L.chunk_off[t]) * CHUNK;
     const int64_t end = min(base + (int64_t)CHUNK, L.numel[t]);
     float* g = L.p0[t];
-    for (int64_t i = base + threadIdx.x; i < end; i += NTHR) {
-      const float v = g[i];
-      bad |= !isfinite(v);
-      g[i] = v * inv;
+    float v[CHUNK / NTHR];
+#pragma unroll
+    for (int k = 0; k < CHUNK / NTHR; ++k) {
+      const int64_t i = base + k * NTHR + threadIdx.x;
+      v[k] = i < end ? g[i] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < CHUNK / NTHR; ++k) {
+      const int64_t i = base + k * NTHR + threadIdx.x;
+      bad |= !isfinite(v[k]);
+      if (i < end) g[i] = v[k] * inv;
     }
   }
   if (__any(bad) && (threadIdx.x & 63) == 0) found_inf[0] = 1.f;
@@ -69,16 +76,28 @@ sgd_kernel(MTList L, float lr, float momentum, float dampening, float wd, int ne
     float* p = L.p0[t];
     const float* g = L.p1[t];
     float* buf = L.p2[t];
-    for (int64_t i = base + threadIdx.x; i < end; i += NTHR) {
-      float d = g[i] * gs;
+    float gv[CHUNK / NTHR], pv[CHUNK / NTHR], bv0[CHUNK / NTHR];
+#pragma unroll
+    for (int k = 0; k < CHUNK / NTHR; ++k) {
+      const int64_t i = base + k * NTHR + threadIdx.x;
+      const bool in = i < end;
+      gv[k] = in ? g[i] : 0.f;
+      pv[k] = in ? p[i] : 0.f;
+      bv0[k] = (in && momentum != 0.f && !first) ? buf[i] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < CHUNK / NTHR; ++k) {
+      const int64_t i = base + k * NTHR + threadIdx.x;
+      if (i >= end) continue;
+      float d = gv[k] * gs;
       if (maximize) d = -d;
-      if (wd != 0.f) d += wd * p[i];
+      if (wd != 0.f) d += wd * pv[k];
       if (momentum != 0.f) {
-        float bv = first ? d : momentum * buf[i] + (1.f - dampening) * d;
-        buf[i] = bv;
-        d = nesterov ? d + momentum * bv : bv;
+        const float b = first ? d : momentum * bv0[k] + (1.f - dampening) * d;
+        buf[i] = b;
+        d = nesterov ? d + momentum * b : b;
       }
-      p[i] -= lr * d;
+      p[i] = pv[k] - lr * d;
     }
   }
 }
@@ -111,33 +130,74 @@ __global__ void update_scale_kernel(float* scale, int* tracker, float* found_inf
 // grads are finite, phase 3 updates scale / growth tracker and re-arms
 // found_inf.  p0 = param, p1 = grad, p2 = momentum buffer (or null).
 constexpr int FUSED_THR = 1024;
+constexpr int FUSED_U = 16;  // elements per thread per batch: 16 independent loads in flight
+
+// element prefix table in L.chunk_off (chunk_off[t] = first virtual index of tensor t)
+__device__ __forceinline__ int locate(const MTList& L, int64_t gi) {
+  int lo = 0, hi = L.n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (L.chunk_off[mid] <= gi) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
 __global__ void __launch_bounds__(FUSED_THR)
 amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ tracker, float* __restrict__ found_inf,
                      float lr, float momentum, float dampening, float wd, int nesterov, int maximize, int first,
                      float growth, float backoff, int interval) {
   const float inv = 1.f / scale[0];
+  const int64_t total = L.chunk_off[L.n];
   bool bad = false;
-  for (int t = 0; t < L.n; ++t) {
-    const float* g = L.p1[t];
-    for (int64_t i = threadIdx.x; i < L.numel[t]; i += FUSED_THR) bad |= !isfinite(g[i]);
+  for (int64_t base = 0; base < total; base += (int64_t)FUSED_U * FUSED_THR) {
+    float v[FUSED_U];
+#pragma unroll
+    for (int k = 0; k < FUSED_U; ++k) {
+      const int64_t gi = base + (int64_t)k * FUSED_THR + threadIdx.x;
+      v[k] = 0.f;
+      if (gi < total) {
+        const int t = locate(L, gi);
+        v[k] = L.p1[t][gi - L.chunk_off[t]];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < FUSED_U; ++k) bad |= !isfinite(v[k]);
   }
   bad = __syncthreads_or(bad);
-  for (int t = 0; t < L.n; ++t) {
-    float* p = L.p0[t];
-    float* g = L.p1[t];
-    float* buf = L.p2[t];
-    for (int64_t i = threadIdx.x; i < L.numel[t]; i += FUSED_THR) {
-      const float gv = g[i] * inv;
-      g[i] = gv;
-      if (bad) continue;
-      float d = maximize ? -gv : gv;
-      if (wd != 0.f) d += wd * p[i];
-      if (momentum != 0.f) {
-        const float bv = first ? d : momentum * buf[i] + (1.f - dampening) * d;
-        buf[i] = bv;
-        d = nesterov ? d + momentum * bv : bv;
+  for (int64_t base = 0; base < total; base += (int64_t)FUSED_U * FUSED_THR) {
+    float gv[FUSED_U], pv[FUSED_U], bv[FUSED_U];
+    int tt[FUSED_U];
+    int64_t oo[FUSED_U];
+#pragma unroll
+    for (int k = 0; k < FUSED_U; ++k) {
+      const int64_t gi = base + (int64_t)k * FUSED_THR + threadIdx.x;
+      tt[k] = -1;
+      if (gi < total) {
+        const int t = locate(L, gi);
+        const int64_t o = gi - L.chunk_off[t];
+        tt[k] = t;
+        oo[k] = o;
+        gv[k] = L.p1[t][o];
+        pv[k] = L.p0[t][o];
+        bv[k] = (momentum != 0.f && !first) ? L.p2[t][o] : 0.f;
       }
-      p[i] -= lr * d;
+    }
+#pragma unroll
+    for (int k = 0; k < FUSED_U; ++k) {
+      if (tt[k] < 0) continue;
+      const int t = tt[k];
+      const int64_t o = oo[k];
+      const float g = gv[k] * inv;
+      L.p1[t][o] = g;
+      if (bad) continue;
+      float d = maximize ? -g : g;
+      if (wd != 0.f) d += wd * pv[k];
+      if (momentum != 0.f) {
+        const float b = first ? d : momentum * bv[k] + (1.f - dampening) * d;
+        L.p2[t][o] = b;
+        d = nesterov ? d + momentum * b : b;
+      }
+      L.p0[t][o] = pv[k] - lr * d;
     }
   }
   if (threadIdx.x == 0) {
@@ -246,6 +306,7 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
   TORCH_CHECK(tracker.scalar_type() == at::kInt);
   MTList L{};
   L.n = (int)params.size();
+  L.chunk_off[0] = 0;
   for (size_t i = 0; i < params.size(); ++i) {
     check_f32(params[i]); check_f32(grads[i]);
     TORCH_CHECK(params[i].numel() == grads[i].numel());
@@ -253,6 +314,7 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
     L.p0[i] = params[i].data_ptr<float>();
     L.p1[i] = grads[i].data_ptr<float>();
     L.p2[i] = bufs.empty() ? nullptr : bufs[i].data_ptr<float>();
+    L.chunk_off[i + 1] = L.chunk_off[i] + L.numel[i];  // element prefix (not chunks) for this kernel
   }
   hipLaunchKernelGGL(amp_sgd_fused_kernel, dim3(1), dim3(FUSED_THR), 0, cur_stream(), L, scale.data_ptr<float>(),
                      tracker.data_ptr<int>(), found_inf.data_ptr<float>(), (float)lr, (float)momentum,

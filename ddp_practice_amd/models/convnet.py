@@ -6,8 +6,10 @@ reference: /root/reference/origin_main.py:9-31 and ddp_main.py:13-36:
     fc     = Linear(7*7*32, num_classes)
 29,034 parameters, 16 state_dict entries ("layer1.0.weight" ... "fc.bias").
 
-On a HIP device each ``layerN`` runs as ONE fused op (2 launches forward,
-4-5 backward: ops/convblock.py) and ``fc`` on the MFMA head kernel; when a
+On a HIP device the whole network runs as ONE fused op (3 launches forward,
+7 backward: ops/convnet_fused.py); ``fused="layer"`` runs each ``layerN`` as
+one op (2 launches forward, 4-5 backward: ops/convblock.py) and ``fc`` on the
+MFMA head kernel; ``fused=False`` runs the torch modules.  When a
 ``SyncBatchNorm`` from this package replaces the BatchNorm (see
 ``parallel.sync_bn.convert_sync_batchnorm``) the fused op all-reduces its
 statistics through that module's communicator.  On CPU the plain PyTorch
@@ -27,7 +29,7 @@ from ..amp import autocast, compute_dtype
 
 
 class ConvNet(nn.Module):
-    def __init__(self, num_classes: int = 10, amp_dtype: torch.dtype | None = None, fused: bool = True):
+    def __init__(self, num_classes: int = 10, amp_dtype: torch.dtype | None = None, fused: bool | str = True):
         super().__init__()
         self.layer1 = nn.Sequential(
             nn.Conv2d(1, 16, kernel_size=5, stride=1, padding=2),
@@ -55,23 +57,29 @@ class ConvNet(nn.Module):
             and self.layer2[1].track_running_stats
 
     @staticmethod
-    def _block(seq: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
+    def _comm_of(bn: nn.Module):
+        if not bn.training:
+            return None
+        if isinstance(bn, nn.SyncBatchNorm):  # torch's SyncBN: use the package communicator
+            from ..parallel.comm import default_comm
+
+            return default_comm()
+        return getattr(bn, "comm", None)
+
+    @classmethod
+    def _block(cls, seq: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
         from ..ops.convblock import conv_block
 
-        bn = seq[1]
-        comm = None
-        if bn.training:
-            if isinstance(bn, nn.SyncBatchNorm):  # torch's SyncBN: use the package communicator
-                from ..parallel.comm import default_comm
-
-                comm = default_comm()
-            else:
-                comm = getattr(bn, "comm", None)
-        return conv_block(x, seq[0], bn, comm=comm)
+        return conv_block(x, seq[0], seq[1], comm=cls._comm_of(seq[1]))
 
     def _forward_native(self, x: torch.Tensor) -> torch.Tensor:
+        from ..ops import convnet_fused
         from ..ops.head import linear
 
+        if self.fused != "layer" and convnet_fused.supported(self, x):
+            c1, c2 = self._comm_of(self.layer1[1]), self._comm_of(self.layer2[1])
+            if c1 is c2:
+                return convnet_fused.convnet_forward(self, x, comm=c1)
         out = self._block(self.layer1, x)
         out = self._block(self.layer2, out)
         out = out.reshape(out.size(0), -1)

@@ -1,0 +1,160 @@
+"""The whole ConvNet forward/backward as ONE autograd op (csrc/kernels/convnet_fused.hip).
+
+Fusing across the layer boundaries of /root/reference/origin_main.py:9-31
+removes launches that exist only because torch runs one module at a time:
+
+  forward  (train): conv1(+BN1 sums) | BN1-ReLU-pool1 -> conv2 (+BN2 sums) | BN2-ReLU-pool2 -> fc
+                    = 3 launches for the model (per-layer ops: 6, torch: ~14 + host syncs)
+  backward:         fc-bwd + pool2/ReLU2 routing + BN2 sums + BN2 input grad | conv2 wgrad | conv2 dgrad
+                    | conv2 grad sums | pool1/ReLU1 routing + BN1 sums + BN1 input grad | conv1 wgrad
+                    | conv1 grad sums = 7 launches
+
+With SyncBN (``comm`` active) the per-workgroup forward partial sums and the
+per-channel backward sums are all-reduced between the kernels (one
+collective each), and the BN input-gradient steps run as their own launches
+after the all-reduce.  Parameter gradients are views of one output buffer.
+"""
+from __future__ import annotations
+
+import torch
+
+from .._ext import load as _load_ext
+
+
+def _mods():
+    C = _load_ext()
+    return C.convblock, C.convnet
+
+
+def supported(model, x: torch.Tensor) -> bool:
+    if not x.is_cuda or x.dim() != 4 or tuple(x.shape[1:]) != (1, 28, 28):
+        return False
+    l1, l2, fc = model.layer1, model.layer2, model.fc
+    for seq, cin, cout in ((l1, 1, 16), (l2, 16, 32)):
+        conv, bn = seq[0], seq[1]
+        if (conv.in_channels, conv.out_channels, conv.kernel_size, conv.stride, conv.padding) != \
+                (cin, cout, (5, 5), (1, 1), (2, 2)) or conv.bias is None or conv.groups != 1:
+            return False
+        if not (bn.track_running_stats and bn.affine):
+            return False
+        if not isinstance(seq[2], torch.nn.ReLU) or not isinstance(seq[3], torch.nn.MaxPool2d):
+            return False
+    n, b = fc.out_features, x.shape[0]
+    # head backward keeps dlogits, one channel of fc.weight and of the pooled features in LDS (64 KB)
+    return fc.in_features == 32 * 49 and fc.bias is not None and 1 <= n <= 64 and b * (n + 49) + n * 49 <= 16384
+
+
+class ConvNetFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, b1, g1, be1, w2, b2, g2, be2, wfc, bfc, bufs, training, moms, epss, comm, cdtype):
+        cb, cn = _mods()
+        rm1, rv1, nbt1, rm2, rv2, nbt2 = bufs
+        m1, m2 = (-1.0 if m is None else float(m) for m in moms)
+        e1, e2 = (float(e) for e in epss)
+        x = x.to(cdtype).contiguous()
+        B = x.shape[0]
+        dev = x.device
+        N = wfc.shape[0]
+        sync = comm is not None and comm.active and training
+        y1 = torch.empty((B, 16, 28, 28), dtype=cdtype, device=dev)
+        y2 = torch.empty((B, 32, 14, 14), dtype=cdtype, device=dev)
+        logits = torch.empty((B, N), dtype=cdtype, device=dev)
+        fstats1 = torch.empty(cb.stats_len(16), dtype=torch.float32, device=dev)
+        fstats2 = torch.empty(cb.stats_len(32), dtype=torch.float32, device=dev)
+        if training:
+            fslab1 = torch.empty(cb.fwd_rows(1, 16, 28, 28, B) * cb.fslab_row(16), dtype=torch.float32, device=dev)
+            fslab2 = torch.empty(cb.fwd_rows(16, 32, 14, 14, B) * cb.fslab_row(32), dtype=torch.float32, device=dev)
+            p1 = torch.empty((B, 16, 14, 14), dtype=cdtype, device=dev)
+            idx1 = torch.empty((B, 16, 14, 14), dtype=torch.uint8, device=dev)
+            p2 = torch.empty((B, 32 * 49), dtype=cdtype, device=dev)
+            idx2 = torch.empty((B, 32 * 49), dtype=torch.uint8, device=dev)
+            cb.conv_fwd(x, w1, b1, y1, fslab1, fstats1, rm1)
+            if sync:
+                comm.all_reduce_(fslab1)
+            cn.conv2_fwd(y1, fslab1, fstats1, g1, be1, rm1, rv1, nbt1, m1, e1, True, w2, b2, y2, fslab2, fstats2,
+                         rm2, p1, idx1)
+            if sync:
+                comm.all_reduce_(fslab2)
+            cn.head_fwd(y2, fslab2, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, True, wfc, bfc, logits, p2, idx2)
+            ctx.save_for_backward(x, w2, wfc, g1, g2, y1, p1, idx1, fstats1, y2, p2, idx2, fstats2)
+        else:
+            cb.conv_fwd(x, w1, b1, y1)
+            cn.conv2_fwd(y1, None, fstats1, g1, be1, rm1, rv1, nbt1, m1, e1, False, w2, b2, y2, None, fstats2, rm2,
+                         None, None)
+            cn.head_fwd(y2, None, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, False, wfc, bfc, logits, None, None)
+        ctx.training = training
+        ctx.sync = sync
+        ctx.comm = comm
+        ctx.eps = (e1, e2)
+        ctx.shapes = (w1.shape, w2.shape, wfc.shape)
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        if not ctx.training:
+            raise RuntimeError("ConvNetFn: backward through an eval-mode forward is not supported")
+        cb, cn = _mods()
+        x, w2, wfc, g1, g2, y1, p1, idx1, fstats1, y2, p2, idx2, fstats2 = ctx.saved_tensors
+        e1, e2 = ctx.eps
+        comm, sync = ctx.comm, ctx.sync
+        dl = dlogits.to(y2.dtype).contiguous()
+        B = y2.shape[0]
+        dev = y2.device
+        s_w1, s_w2, s_wfc = ctx.shapes
+        n_w1, n_w2, n_wfc = s_w1.numel(), s_w2.numel(), s_wfc.numel()
+        N = s_wfc[0]
+        # one output buffer for every parameter gradient (views handed to autograd)
+        sizes = [n_w1, 16, 16, 16, n_w2, 32, 32, 32, n_wfc, N]
+        out = torch.empty(sum(sizes), dtype=torch.float32, device=dev)
+        views = list(out.split(sizes))
+        dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, dwfc, dbfc = views
+        # --- fc + pool2/ReLU2 + BN2
+        bslab2 = torch.empty(2 * 32, dtype=torch.float32, device=dev)
+        dy2 = torch.empty_like(y2)
+        if not sync:
+            cn.head_bwd(dl, wfc, p2, idx2, y2, fstats2, g2, e2, dwfc, dbfc, dg2, dbe2, bslab2, None, dy2)
+        else:
+            dp2 = torch.empty_like(p2)
+            cn.head_bwd(dl, wfc, p2, idx2, y2, fstats2, g2, e2, dwfc, dbfc, dg2, dbe2, bslab2, dp2, None)
+            gslab2 = comm.all_reduce(bslab2)
+            cb.bwd_elemt(dp2.view(B, 32, 7, 7), p2.view(B, 32, 7, 7), idx2.view(B, 32, 7, 7), y2, fstats2, gslab2,
+                         g2, e2, dy2)
+        # --- conv2: weight grad (per-image partials) and data grad
+        wslab2 = torch.empty(cb.wgrad_rows(16, 32, 14, 14, B) * (n_w2 + 32), dtype=torch.float32, device=dev)
+        cb.conv_wgrad(p1, dy2, wslab2)
+        dp1 = torch.empty((B, 16, 14, 14), dtype=y1.dtype, device=dev)
+        cb.conv_dgrad(dy2, w2, dp1)
+        cb.slab_reduce(wslab2, n_w2 + 32, out.narrow(0, n_w1 + 48, n_w2 + 32))
+        # --- pool1/ReLU1 + BN1
+        bslab1 = torch.empty(2 * 16, dtype=torch.float32, device=dev)
+        dy1 = torch.empty_like(y1)
+        if not sync:
+            cn.pool1_bwd(dp1, p1, idx1, y1, fstats1, g1, e1, dg1, dbe1, bslab1, dy1)
+        else:
+            cn.pool1_bwd(dp1, p1, idx1, y1, fstats1, g1, e1, dg1, dbe1, bslab1, None)
+            gslab1 = comm.all_reduce(bslab1)
+            cb.bwd_elemt(dp1, p1, idx1, y1, fstats1, gslab1, g1, e1, dy1)
+        # --- conv1 weight grad
+        wslab1 = torch.empty(cb.wgrad_rows(1, 16, 28, 28, B) * (n_w1 + 16), dtype=torch.float32, device=dev)
+        cb.conv_wgrad(x, dy1, wslab1)
+        cb.slab_reduce(wslab1, n_w1 + 16, out.narrow(0, 0, n_w1 + 16))
+        return (None, dw1.view(s_w1), db1, dg1, dbe1, dw2.view(s_w2), db2, dg2, dbe2, dwfc.view(s_wfc), dbfc,
+                None, None, None, None, None, None)
+
+
+def convnet_forward(model, x, comm=None, cdtype=None):
+    """Run the reference ConvNet module tree through the fused op."""
+    if cdtype is None:
+        from ..amp import compute_dtype
+
+        cdtype = compute_dtype(x)
+    l1, l2, fc = model.layer1, model.layer2, model.fc
+    c1, bn1, c2, bn2 = l1[0], l1[1], l2[0], l2[1]
+    training = bn1.training
+    if bn1.training != bn2.training:
+        raise RuntimeError("fused ConvNet: both BatchNorms must be in the same mode")
+    bufs = (bn1.running_mean, bn1.running_var, bn1.num_batches_tracked,
+            bn2.running_mean, bn2.running_var, bn2.num_batches_tracked)
+    return ConvNetFn.apply(x, c1.weight, c1.bias, bn1.weight, bn1.bias, c2.weight, c2.bias, bn2.weight, bn2.bias,
+                           fc.weight, fc.bias, bufs, training, (bn1.momentum, bn2.momentum), (bn1.eps, bn2.eps),
+                           comm, cdtype)

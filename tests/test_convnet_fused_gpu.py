@@ -1,0 +1,127 @@
+"""Whole-ConvNet fused op (ops/convnet_fused.py) vs the torch module tree (fp32 reference)."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _model(seed=0, n=10):
+    from ddp_practice_amd.models import ConvNet
+
+    torch.manual_seed(seed)
+    m = ConvNet(num_classes=n)
+    with torch.no_grad():
+        for bn in (m.layer1[1], m.layer2[1]):
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.2, 0.2)
+            bn.running_mean.uniform_(-0.1, 0.1)
+            bn.running_var.uniform_(0.5, 1.5)
+    return m.to(DEV)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def _torch_fwd(m, x):
+    out = m.layer2(m.layer1(x))
+    return m.fc(out.reshape(out.size(0), -1))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,N", [(32, 10), (7, 10), (100, 10), (16, 64)])
+def test_convnet_fused_fwd_bwd(C, dtype, B, N):
+    from ddp_practice_amd.ops import convnet_fused
+
+    m = _model(n=N)
+    mr, ml = copy.deepcopy(m), copy.deepcopy(m)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = torch.rand(B, 1, 28, 28, generator=g).to(DEV)
+    assert convnet_fused.supported(m, x)
+    out = convnet_fused.convnet_forward(m, x, cdtype=dtype)
+    ref = _torch_fwd(mr, x)
+    lp = dtype != torch.float32
+    if lp:
+        with torch.autocast("cuda", dtype=dtype):
+            ref_l = _torch_fwd(ml, x)
+
+    def bound(a, r, l, floor):
+        e = _rel(a, r)
+        lim = max(2.0 * _rel(l, r), floor) if lp else floor
+        assert e < lim, (e, lim)
+
+    assert out.dtype == dtype and out.shape == (B, N)
+    bound(out, ref, ref_l if lp else None, 3e-5 if not lp else 5e-3)
+    st = 1e-4 if not lp else 1e-2
+    for bn, bnr in ((m.layer1[1], mr.layer1[1]), (m.layer2[1], mr.layer2[1])):
+        torch.testing.assert_close(bn.running_mean, bnr.running_mean, rtol=st, atol=st)
+        torch.testing.assert_close(bn.running_var, bnr.running_var, rtol=st, atol=st)
+        assert int(bn.num_batches_tracked) == 1
+    go = torch.randn(ref.shape, generator=g).to(DEV)
+    ref.backward(go)
+    out.backward(go.to(dtype))
+    if lp:
+        ref_l.backward(go.to(ref_l.dtype))
+    fl = 1e-4 if not lp else 5e-3
+    named_l = dict(ml.named_parameters()) if lp else {}
+    for (n, p), (_, q) in zip(m.named_parameters(), mr.named_parameters()):
+        assert p.grad is not None and p.grad.shape == p.shape, n
+        if n.endswith("0.bias"):  # conv bias grad is ~0 analytically (BN follows)
+            lim = 2.0 * (named_l[n].grad - q.grad).abs().max().item() + 1e-2 if lp else 2e-3
+            assert (p.grad - q.grad).abs().max().item() < lim, n
+            continue
+        e = _rel(p.grad, q.grad)
+        lim = max(2.0 * _rel(named_l[n].grad, q.grad), fl) if lp else fl
+        assert e < lim, (n, e, lim)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_convnet_fused_eval(C, dtype):
+    from ddp_practice_amd.ops import convnet_fused
+
+    m = _model().eval()
+    x = torch.rand(24, 1, 28, 28, device=DEV)
+    with torch.no_grad():
+        out = convnet_fused.convnet_forward(m, x, cdtype=dtype)
+        ref = _torch_fwd(m, x)
+    assert _rel(out, ref) < (3e-5 if dtype == torch.float32 else 2e-2)
+
+
+def test_convnet_fused_matches_layer_path(C):
+    """fp32: whole-model op == per-layer ops (same kernels, same reduction order)."""
+    m = _model()
+    ml = copy.deepcopy(m)
+    ml.fused = "layer"
+    x = torch.rand(32, 1, 28, 28, device=DEV)
+    for _ in range(3):
+        for mod in (m, ml):
+            mod.zero_grad(set_to_none=True)
+            mod(x).square().mean().backward()
+            with torch.no_grad():
+                for p in mod.parameters():
+                    p.add_(p.grad, alpha=-0.1)
+    for (n, p), (_, q) in zip(m.state_dict().items(), ml.state_dict().items()):
+        torch.testing.assert_close(p.float(), q.float(), rtol=2e-5, atol=2e-5, msg=n)
+
+
+def test_convnet_model_dispatches_fused(C):
+    from ddp_practice_amd.ops import convnet_fused
+
+    m = _model()
+    calls = []
+    orig = convnet_fused.ConvNetFn.apply
+
+    def spy(*a):
+        calls.append(1)
+        return orig(*a)
+
+    convnet_fused.ConvNetFn.apply = spy
+    try:
+        m(torch.rand(8, 1, 28, 28, device=DEV)).sum().backward()
+    finally:
+        convnet_fused.ConvNetFn.apply = orig
+    assert calls == [1]
