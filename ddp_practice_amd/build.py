@@ -27,6 +27,7 @@ CSRC = PKG / "csrc"
 BUILD = PKG.parent / "build" / "native"
 TARGET = PKG / "_C.so"
 ARCH = "gfx950"
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 
 def _torch_dirs():
@@ -115,7 +116,9 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = True) ->
                *map(str, objs), "-o", str(TARGET),
                f"-L{torch_lib}", f"-Wl,-rpath,{torch_lib}",
                "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
-               "-ltorch_python", "-lamdhip64", "-lrccl"]
+               "-ltorch_python", "-lamdhip64", "-lrccl",
+               # roctx markers (rocprofv3 --marker-trace); ships with the ROCm image
+               f"-L{ROCM}/lib", f"-Wl,-rpath,{ROCM}/lib", "-lrocprofiler-sdk-roctx"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

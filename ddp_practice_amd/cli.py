@@ -1,0 +1,193 @@
+"""Shared body of the three entry points (origin_main.py, ddp_main.py,
+ddp_main_torchrun.py).
+
+The reference repeats the same ~50-line ``main`` in every script
+(/root/reference/origin_main.py:84-113, ddp_main.py:115-170,
+ddp_main_torchrun.py:101-158); here the scripts keep the reference's
+``prepare()`` / launch / timer contract and call ``run()``.
+
+Stdout contract (rank 0 only): ``begin training of epoch e/E``,
+``begin testing``, ``Accuracy is xx.xx%`` (the scripts print ``time elapsed``).
+
+Additive flags (all optional; defaults reproduce the reference):
+  --synthetic / --data-root / --train-samples / --test-samples   data
+  --amp-dtype {fp16,bf16,fp32}        precision (reference: fp32 origin, fp16 DDP)
+  --no-graph                          run every step eagerly (no hipGraph replay)
+  --no-sync-bn / --bucket-cap-mb      DDP knobs
+  --seed N                            model-init seed
+  --resume PATH [--start-epoch N]     load {"model"[, "scaler"]} before training
+  --watchdog-timeout S                abort + exit when no progress for S seconds
+  --profile                           roctx ranges (rocprofv3 --marker-trace)
+  --metrics-file PATH                 per-epoch JSONL (img/s, scale, ...) on rank 0
+  --checkpoint PATH                   output file name
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+
+def add_run_args(parser, amp_default: str, checkpoint: str, distributed: bool) -> None:
+    parser.add_argument("--data-root", default="./data")
+    parser.add_argument("--synthetic", action="store_true", help="use the synthetic MNIST-shaped dataset")
+    parser.add_argument("--train-samples", type=int, default=None, help="synthetic train-set size (tests)")
+    parser.add_argument("--test-samples", type=int, default=None, help="synthetic test-set size (tests)")
+    parser.add_argument("--amp-dtype", default=amp_default, choices=["fp16", "bf16", "fp32"])
+    parser.add_argument("--no-graph", action="store_true", help="run the training step eagerly")
+    parser.add_argument("--seed", type=int, default=None)
+    parser.add_argument("--checkpoint", default=checkpoint)
+    parser.add_argument("--resume", default=None, help="checkpoint to load before training")
+    parser.add_argument("--start-epoch", type=int, default=0, help="first epoch index (sampler seed) when resuming")
+    parser.add_argument("--watchdog-timeout", type=float, default=None,
+                        help="seconds without progress before aborting (env DPA_WATCHDOG_TIMEOUT; 0 = off)")
+    parser.add_argument("--profile", action="store_true", help="emit roctx ranges for rocprofv3 --marker-trace")
+    parser.add_argument("--metrics-file", default=None, help="per-epoch JSONL metrics (rank 0)")
+    if distributed:
+        parser.add_argument("--no-sync-bn", action="store_true")
+        parser.add_argument("--bucket-cap-mb", type=float, default=None)
+
+
+def load_checkpoint(path: str, model, scaler=None) -> None:
+    """Load a reference-format checkpoint ({"model": sd[, "scaler": sd]}) without unpickling code.
+
+    Accepts both key styles (``layer1.0.weight`` and DDP's ``module.layer1.0.weight``).
+    """
+    import torch
+
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    sd = ck["model"]
+    if all(k.startswith("module.") for k in sd):
+        sd = {k[len("module."):]: v for k, v in sd.items()}
+    model.load_state_dict(sd)
+    if scaler is not None and "scaler" in ck and ck["scaler"]:
+        scaler.load_state_dict(ck["scaler"])
+
+
+class _Metrics:
+    def __init__(self, path: str | None, rank: int, world: int, device):
+        self.path = path if rank == 0 else None
+        self.world = world
+        self.device = device
+        self.t0 = None
+
+    def start(self):
+        if self.path is None:
+            return
+        self._sync()
+        self.t0 = time.perf_counter()
+
+    def _sync(self):
+        import torch
+
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def epoch(self, epoch: int, images: int, steps: int, scaler=None):
+        if self.path is None:
+            return
+        self._sync()
+        dt = time.perf_counter() - self.t0
+        rec = {"epoch": epoch, "steps_per_rank": steps, "images": images, "seconds": round(dt, 4),
+               "images_per_s": round(images / dt, 1) if dt > 0 else None, "world_size": self.world}
+        if scaler is not None and scaler.is_enabled():
+            rec["loss_scale"] = scaler.get_scale()
+        with open(self.path, "a") as f:
+            f.write(json.dumps(rec) + "\n")
+        self.t0 = time.perf_counter()
+
+
+def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None = None) -> None:
+    """Build model/data/optimizer, train ``args.epochs`` epochs, test, save (rank 0)."""
+    import torch
+
+    import ddp_practice_amd.distributed as dist
+    from ddp_practice_amd.amp import GradScaler
+    from ddp_practice_amd.data import MNIST, DeviceLoader, DistributedSampler
+    from ddp_practice_amd.engine import TrainLoop, evaluate
+    from ddp_practice_amd.models import ConvNet
+    from ddp_practice_amd.nn import CrossEntropyLoss
+    from ddp_practice_amd.optim import SGD
+    from ddp_practice_amd.utils import FaultInjector, Watchdog, set_tracing, trace_range
+
+    if args.profile:
+        set_tracing(True)
+    if args.seed is not None:
+        torch.manual_seed(args.seed)
+    gpu = torch.cuda.is_available()
+    dev = torch.device("cuda", local_rank if distributed else 0) if gpu else torch.device("cpu")
+    rank = dist.get_rank() if distributed else 0
+    world = dist.get_world_size() if distributed else 1
+    comm = dist.default_comm() if distributed else None
+    amp = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": None}[args.amp_dtype]
+
+    model = ConvNet(amp_dtype=amp).to(dev)  # autocast inside forward, as the reference
+    scaler = GradScaler(enabled=True) if amp is not None else None
+    if args.resume:
+        load_checkpoint(args.resume, model, scaler)
+    if distributed:
+        from ddp_practice_amd.parallel import DistributedDataParallel, convert_sync_batchnorm
+
+        if not args.no_sync_bn:
+            model = convert_sync_batchnorm(model)
+        model = DistributedDataParallel(model, device_ids=[local_rank] if gpu else None,
+                                        bucket_cap_mb=args.bucket_cap_mb)
+    criterion = CrossEntropyLoss().to(dev)
+    optimizer = SGD(model.parameters(), 1e-4)
+
+    act_dtype = amp if (amp is not None and gpu) else torch.float32
+    train_dataset = MNIST(root=args.data_root, train=True, force_synthetic=args.synthetic, n=args.train_samples)
+    test_dataset = MNIST(root=args.data_root, train=False, force_synthetic=args.synthetic, n=args.test_samples)
+    if distributed:
+        g = torch.Generator()
+        g.manual_seed(generator_seed if generator_seed is not None else 3407 + rank)
+        train_dloader = DeviceLoader(train_dataset, batch_size=args.batch_size, shuffle=False, num_workers=4,
+                                     pin_memory=True, sampler=DistributedSampler(train_dataset), generator=g,
+                                     device=dev, dtype=act_dtype)
+        test_dloader = DeviceLoader(test_dataset, batch_size=args.batch_size, shuffle=False, num_workers=2,
+                                    pin_memory=True, sampler=DistributedSampler(test_dataset), device=dev,
+                                    dtype=act_dtype)
+    else:
+        train_dloader = DeviceLoader(train_dataset, batch_size=args.batch_size, shuffle=True, device=dev,
+                                     dtype=act_dtype, num_workers=4, pin_memory=True)
+        test_dloader = DeviceLoader(test_dataset, batch_size=args.batch_size, shuffle=True, device=dev,
+                                    dtype=act_dtype, num_workers=2, pin_memory=True)
+
+    timeout = args.watchdog_timeout
+    if timeout is None and "DPA_WATCHDOG_TIMEOUT" in os.environ:
+        timeout = float(os.environ["DPA_WATCHDOG_TIMEOUT"])
+    watchdog = Watchdog(comm, timeout=timeout, tag=f"rank{rank}") if timeout else None
+    faults = FaultInjector(rank)
+    loop = TrainLoop(model, criterion, optimizer, train_dloader, scaler, use_graph=not args.no_graph,
+                     watchdog=watchdog, faults=faults)
+    metrics = _Metrics(args.metrics_file, rank, world, dev)
+    metrics.start()
+    try:
+        for epoch in range(args.start_epoch, args.start_epoch + args.epochs):
+            if rank == 0:
+                print(f"begin training of epoch {epoch - args.start_epoch + 1}/{args.epochs}", flush=True)
+            if distributed:
+                train_dloader.sampler.set_epoch(epoch)
+            loop.run_epoch()
+            metrics.epoch(epoch, len(train_dataset), len(train_dloader), scaler)
+        if loop.graph_error is not None and rank == 0:
+            print(f"[ddp_practice_amd] hipGraph capture failed, ran eagerly: {loop.graph_error!r}", file=sys.stderr)
+        if rank == 0:
+            print("begin testing", flush=True)
+        with trace_range("evaluate"):
+            correct, size = evaluate(model, test_dloader, comm=comm, dst=0)
+        if watchdog is not None:
+            watchdog.tick()
+        if rank == 0:
+            print(f"Accuracy is {correct / size:.2%}", flush=True)
+            with trace_range("checkpoint"):
+                state = {"model": model.state_dict()}
+                if scaler is not None and distributed:
+                    state["scaler"] = scaler.state_dict()
+                torch.save(state, args.checkpoint)
+    finally:
+        if watchdog is not None:
+            watchdog.stop()
+    if distributed:
+        dist.destroy_process_group()

@@ -23,6 +23,9 @@ struct Collective {
   virtual void all_reduce_async(at::Tensor t, RedOp op, int slot) = 0;
   // stream == nullptr: the caller's current stream
   virtual void wait(int slot, hipStream_t stream) = 0;
+  // failure handling (watchdog thread): may be called concurrently with other calls
+  virtual std::string async_error() { return std::string(); }
+  virtual void abort_now() {}
 };
 
 // Flat multi-tensor copy (csrc/kernels/optim.hip): direction 0 = pack into flat.

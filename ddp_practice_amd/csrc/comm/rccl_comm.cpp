@@ -93,7 +93,9 @@ class RcclComm : public Collective {
     c10::hip::HIPGuard guard(device);
     {
       pybind11::gil_scoped_release nogil;  // init rendezvous blocks until every rank arrives
-      DPA_NCCL(ncclCommInitRank(&comm_, world, id, rank));
+      ncclComm_t c = nullptr;
+      DPA_NCCL(ncclCommInitRank(&c, world, id, rank));
+      comm_ = c;
     }
     for (int i = 0; i < kRing; ++i) {
       DPA_CHECK_HIP(hipEventCreateWithFlags(&fork_[i], hipEventDisableTiming));
@@ -105,10 +107,10 @@ class RcclComm : public Collective {
   ~RcclComm() override { destroy(); }
 
   void destroy() {
-    if (comm_ != nullptr) {
+    ncclComm_t c = comm_.exchange(nullptr);
+    if (c != nullptr) {
       hipStreamSynchronize(stream_.stream());
-      ncclCommDestroy(comm_);
-      comm_ = nullptr;
+      ncclCommDestroy(c);
     }
     for (int i = 0; i < kRing; ++i) {
       if (fork_[i]) hipEventDestroy(fork_[i]);
@@ -123,16 +125,16 @@ class RcclComm : public Collective {
 
   // Abort outstanding work (failure handling / watchdog path).
   void abort() {
-    if (comm_ != nullptr) {
-      ncclCommAbort(comm_);
-      comm_ = nullptr;
-    }
+    ncclComm_t c = comm_.exchange(nullptr);
+    if (c != nullptr) ncclCommAbort(c);
   }
+  void abort_now() override { abort(); }
 
-  std::string async_error() {
-    if (comm_ == nullptr) return "destroyed";
+  std::string async_error() override {
+    ncclComm_t c = comm_.load();
+    if (c == nullptr) return "destroyed";
     ncclResult_t st = ncclSuccess;
-    ncclCommGetAsyncError(comm_, &st);
+    ncclCommGetAsyncError(c, &st);
     return st == ncclSuccess ? std::string() : std::string(ncclGetErrorString(st));
   }
 
@@ -151,7 +153,7 @@ class RcclComm : public Collective {
     }
     fenced([&](hipStream_t s) {
       DPA_NCCL(ncclAllReduce(t.data_ptr(), dst.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(parse_op(op)),
-                             comm_, s));
+                             comm_.load(), s));
     });
     return dst;
   }
@@ -160,7 +162,7 @@ class RcclComm : public Collective {
     check(in); check(out);
     TORCH_CHECK(out.numel() == in.numel() * world_ && out.scalar_type() == in.scalar_type());
     fenced([&](hipStream_t s) {
-      DPA_NCCL(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), nccl_dtype(in), comm_, s));
+      DPA_NCCL(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), nccl_dtype(in), comm_.load(), s));
     });
   }
 
@@ -169,14 +171,14 @@ class RcclComm : public Collective {
     TORCH_CHECK(in.numel() == out.numel() * world_ && out.scalar_type() == in.scalar_type());
     fenced([&](hipStream_t s) {
       DPA_NCCL(ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(), nccl_dtype(in),
-                                 nccl_op(parse_op(op)), comm_, s));
+                                 nccl_op(parse_op(op)), comm_.load(), s));
     });
   }
 
   void broadcast(at::Tensor t, int root) {
     check(t);
     fenced([&](hipStream_t s) {
-      DPA_NCCL(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), root, comm_, s));
+      DPA_NCCL(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), root, comm_.load(), s));
     });
   }
 
@@ -184,7 +186,7 @@ class RcclComm : public Collective {
     check(t);
     fenced([&](hipStream_t s) {
       DPA_NCCL(ncclReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(parse_op(op)), root,
-                          comm_, s));
+                          comm_.load(), s));
     });
   }
 
@@ -197,8 +199,8 @@ class RcclComm : public Collective {
     fenced([&](hipStream_t s) {
       DPA_NCCL(ncclGroupStart());
       for (int r = 0; r < world_; ++r) {
-        DPA_NCCL(ncclSend(static_cast<char*>(in.data_ptr()) + r * chunk * esz, chunk, nccl_dtype(in), r, comm_, s));
-        DPA_NCCL(ncclRecv(static_cast<char*>(out.data_ptr()) + r * chunk * esz, chunk, nccl_dtype(in), r, comm_, s));
+        DPA_NCCL(ncclSend(static_cast<char*>(in.data_ptr()) + r * chunk * esz, chunk, nccl_dtype(in), r, comm_.load(), s));
+        DPA_NCCL(ncclRecv(static_cast<char*>(out.data_ptr()) + r * chunk * esz, chunk, nccl_dtype(in), r, comm_.load(), s));
       }
       DPA_NCCL(ncclGroupEnd());
     });
@@ -221,7 +223,7 @@ class RcclComm : public Collective {
     const int i = next_++ % kRing;
     DPA_CHECK_HIP(hipEventRecord(fork_[i], cur));
     DPA_CHECK_HIP(hipStreamWaitEvent(stream_.stream(), fork_[i], 0));
-    DPA_NCCL(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), comm_,
+    DPA_NCCL(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), comm_.load(),
                            stream_.stream()));
     DPA_CHECK_HIP(hipEventRecord(slot_[slot], stream_.stream()));
   }
@@ -236,7 +238,7 @@ class RcclComm : public Collective {
   static constexpr int kSlots = 256;
 
   void check(const at::Tensor& t) const {
-    TORCH_CHECK(comm_ != nullptr, "communicator destroyed or aborted");
+    TORCH_CHECK(comm_.load() != nullptr, "communicator destroyed or aborted");
     TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "RCCL tensors must be contiguous device tensors");
     TORCH_CHECK(t.get_device() == device_, "tensor on device ", t.get_device(), ", communicator on ", device_);
   }
@@ -252,7 +254,7 @@ class RcclComm : public Collective {
     DPA_CHECK_HIP(hipStreamWaitEvent(cur, join_[i], 0));
   }
 
-  ncclComm_t comm_ = nullptr;
+  std::atomic<ncclComm_t> comm_{nullptr};
   int rank_, world_, device_;
   c10::hip::HIPStream stream_;
   hipEvent_t fork_[kRing] = {};

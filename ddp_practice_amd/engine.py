@@ -23,6 +23,7 @@ import torch
 
 from .data.loader import DeviceLoader
 from .runtime.graph import CapturedStep
+from .utils.trace import trace_range
 
 
 def _snapshot(model, optimizer, scaler):
@@ -63,7 +64,7 @@ class TrainLoop:
     """Epoch runner: graph-replayed full batches + eager tail batch."""
 
     def __init__(self, model, criterion, optimizer, loader: DeviceLoader, scaler=None, use_graph: bool = True,
-                 steps_per_graph: int = 16):
+                 steps_per_graph: int = 16, watchdog=None, faults=None):
         self.model = model
         self.criterion = criterion
         self.optimizer = optimizer
@@ -75,24 +76,52 @@ class TrainLoop:
         self.images, self.labels = loader.static_batch()
         self._graphs: dict[int, CapturedStep] = {}
         self.graph_error = None
+        self.watchdog = watchdog  # utils.Watchdog: ticked after every chunk of steps
+        self.faults = faults if faults else None  # utils.FaultInjector (DPA_FAULT)
+        self.global_step = 0
 
     # -- one step on the static buffers (what gets captured)
-    def _step(self, images=None, labels=None, fill=True):
+    def _step(self, images=None, labels=None, fill=True, before_update=None):
         if fill:
             self.loader.fill_(self.images, self.labels)
         images = self.images if images is None else images
         labels = self.labels if labels is None else labels
-        outputs = self.model(images)
-        loss = self.criterion(outputs, labels)
+        with trace_range("forward"):
+            outputs = self.model(images)
+            loss = self.criterion(outputs, labels)
         self.optimizer.zero_grad(set_to_none=True)
         if self.scaler is not None:
-            self.scaler.scale(loss).backward()
-            self.scaler.step(self.optimizer)
-            self.scaler.update()
+            with trace_range("backward"):
+                self.scaler.scale(loss).backward()
+            if before_update is not None:
+                before_update()
+            with trace_range("optimizer"):
+                self.scaler.step(self.optimizer)
+                self.scaler.update()
         else:
-            loss.backward()
-            self.optimizer.step()
+            with trace_range("backward"):
+                loss.backward()
+            if before_update is not None:
+                before_update()
+            with trace_range("optimizer"):
+                self.optimizer.step()
         return loss
+
+    def _eager_step(self, images=None, labels=None, fill=True):
+        """One un-captured step (CPU, tail batches, steps with an injected fault)."""
+        step = self.global_step
+        hook = None
+        if self.faults is not None:
+            self.faults.before_step(step)
+            params = [p for g in self.optimizer.param_groups for p in g["params"]]
+            hook = lambda: self.faults.corrupt_grads(step, params)  # noqa: E731
+        self._step(images, labels, fill=fill, before_update=hook)
+        self.global_step += 1
+        self._tick()
+
+    def _tick(self):
+        if self.watchdog is not None:
+            self.watchdog.tick()
 
     def _graph(self, k: int) -> CapturedStep | None:
         if not self.use_graph:
@@ -123,23 +152,34 @@ class TrainLoop:
         tail = [b for b in sizes if b != B]
         self.loader.start_epoch()
         done = 0
-        if self.use_graph and nfull > 0:
-            big = self._graph(self.spg) if nfull >= self.spg else None
-            while big is not None and nfull - done >= self.spg:
-                big.run()
-                done += self.spg
-            if nfull - done > 0:
-                one = self._graph(1)
-                while one is not None and done < nfull:
-                    one.run()
-                    done += 1
-        while done < nfull:  # eager fallback (CPU, or capture failed)
-            self._step()
-            done += 1
-        for i, b in enumerate(tail):
-            imgs, labels = self.loader.static_batch(b)
-            self.loader._fill_tail(imgs, labels, nfull + i)
-            self._step(imgs, labels, fill=False)
+        faults = self.faults
+        with trace_range("train_epoch"):
+            if self.use_graph and nfull > 0:
+                big = self._graph(self.spg) if nfull >= self.spg else None
+                while big is not None and nfull - done >= self.spg:
+                    if faults is not None and faults.pending_in(self.global_step, self.global_step + self.spg):
+                        break  # run the chunk holding the fault step by step
+                    big.run()
+                    done += self.spg
+                    self.global_step += self.spg
+                    self._tick()
+                if nfull - done > 0:
+                    one = self._graph(1)
+                    while one is not None and done < nfull:
+                        if faults is not None and faults.pending_in(self.global_step, self.global_step + 1):
+                            self._eager_step()
+                        else:
+                            one.run()
+                            self.global_step += 1
+                            self._tick()
+                        done += 1
+            while done < nfull:  # eager fallback (CPU, or capture failed)
+                self._eager_step()
+                done += 1
+            for i, b in enumerate(tail):
+                imgs, labels = self.loader.static_batch(b)
+                self.loader._fill_tail(imgs, labels, nfull + i)
+                self._eager_step(imgs, labels, fill=False)
 
 
 @torch.no_grad()

@@ -276,6 +276,10 @@ def init_process_group(backend: str | None = None, init_method: str | None = "en
         _DEFAULT = RcclCommunicator(r, w, device, key=f"dpa_rccl_uid_{_GEN}")
     else:
         _DEFAULT = TorchCommunicator() if w > 1 else LocalCommunicator()
+    if os.environ.get("DPA_DEBUG_COLLECTIVES", "0") == "1":
+        from ..utils.debug import CheckedCommunicator
+
+        _DEFAULT = CheckedCommunicator(_DEFAULT)
     return _DEFAULT
 
 

@@ -1,0 +1,171 @@
+"""Auxiliary subsystems on CPU: watchdog, fault injection, collective-mismatch
+detection, resume, metrics."""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+import torch
+
+from . import _dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_fault_spec_parsing():
+    from ddp_practice_amd.utils.fault import FaultInjector, parse
+
+    fs = parse("1:5:exit:3, *:2:slow:0.01,0:7:inf")
+    assert [(f.rank, f.step, f.kind, f.arg) for f in fs] == [(1, 5, "exit", "3"), (None, 2, "slow", "0.01"),
+                                                              (0, 7, "inf", None)]
+    inj = FaultInjector(0, "1:5:exit,*:2:slow:0.01,0:7:inf")
+    assert [f.kind for f in inj.faults] == ["slow", "inf"]
+    assert inj.pending_in(0, 3) and not inj.pending_in(3, 7) and inj.pending_in(7, 8)
+    with pytest.raises(ValueError):
+        parse("0:1:explode")
+    inj = FaultInjector(0, "0:1:raise")
+    inj.before_step(0)
+    with pytest.raises(RuntimeError, match="injected fault"):
+        inj.before_step(1)
+
+
+def test_watchdog_host_heartbeat_fires_without_exit():
+    from ddp_practice_amd.utils import Watchdog
+
+    wd = Watchdog(None, timeout=0.3, poll=0.02, exit_on_fire=False)
+    for _ in range(5):  # regular heartbeats: no fire
+        wd.heartbeat()
+        time.sleep(0.1)
+    assert not wd.fired
+    time.sleep(0.6)
+    assert wd.fired and "heartbeat" in wd.reason
+    wd.stop()
+
+
+def test_watchdog_disarmed_does_not_fire():
+    from ddp_practice_amd.utils import Watchdog
+
+    with Watchdog(None, timeout=0.1, poll=0.02, exit_on_fire=False) as wd:
+        time.sleep(0.3)  # never armed
+        assert not wd.fired
+        wd.heartbeat()
+        wd.disarm()
+        time.sleep(0.3)
+        assert not wd.fired
+
+
+def _cli(args, env_extra, timeout=300):
+    env = dict(os.environ)
+    env.pop("CUDA_VISIBLE_DEVICES", None)
+    env.update(env_extra)
+    t0 = time.time()
+    r = subprocess.run([sys.executable, *args], cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    return r, time.time() - t0
+
+
+@pytest.mark.slow
+def test_hung_rank_is_detected_by_watchdog(tmp_path):
+    """Rank 1 stops entering collectives at step 3: every rank exits non-zero within the timeout
+    (without the watchdog the gloo collective would block for 30 min)."""
+    r, dt = _cli([os.path.join(ROOT, "ddp_main.py"), "-e", "1", "--synthetic", "--train-samples", "512",
+                  "--test-samples", "64", "--cpu-procs", "2", "--amp-dtype", "fp32", "--watchdog-timeout", "4",
+                  "--checkpoint", str(tmp_path / "ck.pt")],
+                 {"MASTER_PORT": str(_dist.free_port()), "DPA_MASTER_ADDR": "127.0.0.1", "DPA_FAULT": "1:3:hang"})
+    assert r.returncode != 0
+    assert "[dpa watchdog]" in r.stderr, r.stderr[-2000:]
+    assert dt < 120
+    assert not (tmp_path / "ck.pt").exists()
+
+
+@pytest.mark.slow
+def test_dead_rank_tears_down_group(tmp_path):
+    r, dt = _cli([os.path.join(ROOT, "ddp_main.py"), "-e", "1", "--synthetic", "--train-samples", "512",
+                  "--test-samples", "64", "--cpu-procs", "2", "--amp-dtype", "fp32",
+                  "--checkpoint", str(tmp_path / "ck.pt")],
+                 {"MASTER_PORT": str(_dist.free_port()), "DPA_MASTER_ADDR": "127.0.0.1", "DPA_FAULT": "1:2:exit:7"})
+    assert r.returncode != 0
+    assert "injecting exit" in r.stdout
+    assert dt < 120
+
+
+def _mismatch_worker(rank, world):
+    import ddp_practice_amd.distributed as dist
+    from ddp_practice_amd.parallel.comm import set_default_comm
+    from ddp_practice_amd.utils.debug import CheckedCommunicator, CollectiveMismatch
+
+    c = CheckedCommunicator(dist.default_comm())
+    set_default_comm(c)
+    t = torch.ones(4)
+    c.all_reduce_(t)  # matching call passes
+    assert t.tolist() == [2.0] * 4
+    bad = torch.ones(4 if rank == 0 else 5)
+    try:
+        c.all_reduce_(bad)
+    except CollectiveMismatch as e:
+        msg = str(e)
+    else:
+        msg = ""
+    c.broadcast_(torch.zeros(3), 0)  # still usable afterwards
+    return msg, c.history
+
+
+def test_collective_mismatch_is_reported():
+    out = _dist.run(_mismatch_worker, world=2)
+    for msg, hist in out:
+        assert "collective mismatch" in msg
+        assert "all_reduce(float32[4]" in msg and "all_reduce(float32[5]" in msg
+        assert len(hist) == 3
+
+
+def test_inf_fault_skips_step_and_backs_off_scale():
+    from ddp_practice_amd.amp import GradScaler
+    from ddp_practice_amd.data import DeviceLoader, synthetic
+    from ddp_practice_amd.engine import TrainLoop
+    from ddp_practice_amd.models import ConvNet
+    from ddp_practice_amd.nn import CrossEntropyLoss
+    from ddp_practice_amd.optim import SGD
+    from ddp_practice_amd.utils import FaultInjector
+
+    torch.manual_seed(0)
+    ds = synthetic(4 * 8, seed=1)
+    model = ConvNet()
+    opt = SGD(model.parameters(), 0.1)
+    scaler = GradScaler(device="cpu")
+    loader = DeviceLoader(ds, batch_size=8, shuffle=False, device=torch.device("cpu"))
+    snaps = []
+
+    class Spy(FaultInjector):
+        def before_step(self, step):
+            snaps.append((scaler.get_scale(), [p.detach().clone() for p in model.parameters()]))
+            super().before_step(step)
+
+    loop = TrainLoop(model, CrossEntropyLoss(), opt, loader, scaler, use_graph=False, faults=Spy(0, "0:2:inf"))
+    loop.run_epoch()
+    snaps.append((scaler.get_scale(), [p.detach().clone() for p in model.parameters()]))
+    scales = [s for s, _ in snaps]
+    assert scales == [65536.0, 65536.0, 65536.0, 32768.0, 32768.0]
+    # step 2 (the one with +inf) left every parameter untouched
+    for a, b in zip(snaps[2][1], snaps[3][1]):
+        assert torch.equal(a, b)
+    assert not all(torch.equal(a, b) for a, b in zip(snaps[1][1], snaps[2][1]))
+
+
+@pytest.mark.slow
+def test_resume_and_metrics(tmp_path):
+    from .test_cli_cpu import _check_stdout
+
+    ck = tmp_path / "origin_checkpoint.pt"
+    base = [os.path.join(ROOT, "origin_main.py"), "-e", "1", "--synthetic", "--train-samples", "512",
+            "--test-samples", "128", "--seed", "0", "--checkpoint", str(ck)]
+    r, _ = _cli(base + ["--metrics-file", str(tmp_path / "m.jsonl")], {})
+    assert r.returncode == 0, r.stderr
+    _check_stdout(r.stdout, 1)
+    recs = [json.loads(ln) for ln in open(tmp_path / "m.jsonl")]
+    assert len(recs) == 1 and recs[0]["images"] == 512 and recs[0]["images_per_s"] > 0
+    first = torch.load(ck, weights_only=True)["model"]
+    r, _ = _cli(base + ["--resume", str(ck), "--start-epoch", "1", "--checkpoint", str(tmp_path / "b.pt")], {})
+    assert r.returncode == 0, r.stderr
+    second = torch.load(tmp_path / "b.pt", weights_only=True)["model"]
+    assert int(second["layer1.1.num_batches_tracked"]) == 2 * int(first["layer1.1.num_batches_tracked"])
