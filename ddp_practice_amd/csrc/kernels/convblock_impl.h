@@ -132,7 +132,8 @@ struct BNParams {
 
 // part: >= blockDim.x floats of LDS; ends with __syncthreads().
 template <int C>
-__device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, float* sh_s, float* part, bool leader) {
+__device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, float* sh_s, float* part, bool leader,
+                                            float* mean_s = nullptr, float* istd_s = nullptr) {
   const int tid = threadIdx.x, nthr = blockDim.x;
   if (bp.train) {
     constexpr int RL = 2 * C + 1;
@@ -162,9 +163,11 @@ __device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, flo
       const float m1 = part[tid] / n;
       const float mean = bp.fstats[2 * C + 1 + tid] + m1;
       const float var = fmaxf(part[C + tid] / n - m1 * m1, 0.f);
-      const float s = bp.gamma[tid] * rsqrtf(var + bp.eps);
+      const float istd = rsqrtf(var + bp.eps);
+      const float s = bp.gamma[tid] * istd;
       sc_s[tid] = s;
       sh_s[tid] = bp.beta[tid] - mean * s;
+      if (mean_s != nullptr) { mean_s[tid] = mean; istd_s[tid] = istd; }
       if (leader) {
         bp.fstats[tid] = part[tid];
         bp.fstats[C + tid] = part[C + tid];
@@ -179,9 +182,11 @@ __device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, flo
     if (leader && tid == 0) bp.nbt[0] = bp.nbt[0] + 1;
   } else {
     if (tid < C) {
-      const float s = bp.gamma[tid] * rsqrtf(bp.rvar[tid] + bp.eps);
+      const float istd = rsqrtf(bp.rvar[tid] + bp.eps);
+      const float s = bp.gamma[tid] * istd;
       sc_s[tid] = s;
       sh_s[tid] = bp.beta[tid] - bp.rmean[tid] * s;
+      if (mean_s != nullptr) { mean_s[tid] = bp.rmean[tid]; istd_s[tid] = istd; }
     }
     __syncthreads();
   }
@@ -203,13 +208,187 @@ __device__ __forceinline__ void bn_relu_max4(const typename Pair2<T>::type top, 
   }
 }
 
+// Same, also returning xhat = (y - mean) * invstd at the argmax.
+template <typename T>
+__device__ __forceinline__ void bn_relu_max4x(const typename Pair2<T>::type top, const typename Pair2<T>::type bot,
+                                              float sc, float sh, float mean, float istd, float& best, int& bi,
+                                              float& xh) {
+  T v[4];
+  __builtin_memcpy(&v[0], &top, 2 * sizeof(T));
+  __builtin_memcpy(&v[2], &bot, 2 * sizeof(T));
+  best = -1.f;
+  bi = 0;
+  float yb = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float yv = Cvt<T>::to_f(v[k]);
+    const float z = fmaxf(rnd_t<T>(yv * sc + sh), 0.f);
+    if (z > best) { best = z; bi = k; yb = yv; }
+  }
+  xh = (yb - mean) * istd;
+}
+
+// Pooled-index byte of the fused path: bits 0-1 argmax in the 2x2 window
+// (dy * 2 + dx), bit 2 set when the ReLU passed the value (pooled output > 0).
+constexpr int IDX_POS = 3, IDX_RELU = 4;
+
 // Input of a conv that starts with the previous block's BN -> ReLU -> MaxPool.
 template <typename T>
 struct PoolIn {
   const T* y;          // previous conv output (pre-BN) [B][CIN][2H][2W]
   BNParams bn;         // its BatchNorm
   T* p_out;            // pooled output written for the backward (or null)
-  uint8_t* idx_out;    // argmax index written for the backward
+  uint8_t* idx_out;    // argmax index | relu bit, written for the backward
+  T* xh_out;           // normalised value at the argmax (BN backward sums)
+};
+
+// ---------------------------------------------------------------------------
+// Backward through [BN -> ReLU -> MaxPool2d(2,2)] fused into the staging of the
+// next backward kernel: the conv-output gradient is produced on the fly as
+//   dy = gi * (g - k1 - xhat * k2),  g = pooled grad at the window's argmax if
+//   the ReLU passed it, else 0;  k1 = S1/n, k2 = S2/n, gi = gamma * invstd,
+// with S1 = sum g, S2 = sum g * xhat over the (global) batch.
+// ---------------------------------------------------------------------------
+template <typename T>
+struct BwdIn {
+  const T* dp;            // pooled grad [B][C][H/2][W/2]
+  const uint8_t* idx;     // argmax | relu bit
+  const T* y;             // pre-BN conv output [B][C][H][W]
+  const float* fstats;    // forward statistics (stats_len(C))
+  const float* gsum;      // rows x [S1(C) | S2(C)], all-reduced under SyncBN
+  int grows;
+  const float* lsum;      // this rank's rows (dgamma / dbeta); may alias gsum
+  int lrows;
+  const float* gamma;
+  float eps;
+  float* dgamma;          // written by workgroup 0 when non-null
+  float* dbeta;
+};
+
+// Column sums of rows x RL floats (row-major) -> out[0..RL) in LDS, using the
+// whole workgroup; part: >= blockDim.x floats of LDS.  Ends with a barrier.
+__device__ __forceinline__ void colsum_rows(const float* __restrict__ src, int rows, int RL, float* part,
+                                            float* out) {
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int G = nthr / RL;
+  const int j = tid % RL, g = tid / RL;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (g < G) {
+    int rr = g;
+    for (; rr + 3 * G < rows; rr += 4 * G) {
+      a0 += src[(size_t)rr * RL + j];
+      a1 += src[(size_t)(rr + G) * RL + j];
+      a2 += src[(size_t)(rr + 2 * G) * RL + j];
+      a3 += src[(size_t)(rr + 3 * G) * RL + j];
+    }
+    for (; rr < rows; rr += G) a0 += src[(size_t)rr * RL + j];
+  }
+  part[tid] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  float t = 0.f;
+  if (tid < RL)
+    for (int gg = 0; gg < G; ++gg) t += part[gg * RL + tid];
+  __syncthreads();
+  if (tid < RL) out[tid] = t;
+  __syncthreads();
+}
+
+// coef (LDS, 5C floats): [k1 | k2 | gi | mean | invstd]; part: >= blockDim.x
+// floats of LDS, sums: >= 2C floats of LDS.  Workgroup `leader` also writes
+// dgamma / dbeta from the local rows.  Ends with a barrier.
+template <int C, typename T>
+__device__ __forceinline__ void bn_bwd_coef(const BwdIn<T>& bi, float* coef, float* part, float* sums, bool leader) {
+  const int tid = threadIdx.x;
+  colsum_rows(bi.gsum, bi.grows, 2 * C, part, sums);
+  if (tid < C) {
+    const float n = bi.fstats[2 * C];
+    const float m1 = bi.fstats[tid] / n;
+    const float mean = bi.fstats[2 * C + 1 + tid] + m1;
+    const float istd = rsqrtf(fmaxf(bi.fstats[C + tid] / n - m1 * m1, 0.f) + bi.eps);
+    coef[tid] = sums[tid] / n;
+    coef[C + tid] = sums[C + tid] / n;
+    coef[2 * C + tid] = bi.gamma[tid] * istd;
+    coef[3 * C + tid] = mean;
+    coef[4 * C + tid] = istd;
+    if (leader && bi.dgamma != nullptr && bi.lsum == bi.gsum) {
+      bi.dgamma[tid] = sums[C + tid];
+      bi.dbeta[tid] = sums[tid];
+    }
+  }
+  __syncthreads();
+  if (leader && bi.dgamma != nullptr && bi.lsum != bi.gsum) {
+    colsum_rows(bi.lsum, bi.lrows, 2 * C, part, sums);
+    if (tid < C) {
+      bi.dgamma[tid] = sums[C + tid];
+      bi.dbeta[tid] = sums[tid];
+    }
+  }
+}
+
+// Produce dy[c][h][w] of image b for every 2x2 window.  Two phases so that the
+// loads can be issued before the coefficient reduction (their latencies
+// overlap): load(bi, b) ... bn_bwd_coef(...) ... emit(coef, sink) with
+// sink(c, h, w, v00, v01, v10, v11), (h, w) = the window's top-left pixel.
+template <typename T, int C, int H, int W, int NT_>
+struct BnBwdStage {
+  typedef typename Pair2<T>::type P;
+  static constexpr int HO = H / 2, WO = W / 2, PP = HO * WO, NWIN = C * PP;
+  static constexpr int IT = (NWIN + NT_ - 1) / NT_;
+  P top[IT], bot[IT];
+  T g[IT];
+  uint8_t ix[IT];
+
+  __device__ __forceinline__ void load(const BwdIn<T>& bi, int b) {
+    const T* yb = bi.y + (size_t)b * C * H * W;
+    const T* dpb = bi.dp + (size_t)b * NWIN;
+    const uint8_t* ib = bi.idx + (size_t)b * NWIN;
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = threadIdx.x + i * NT_;
+      if (e < NWIN) {
+        const int c = e / PP, pix = e % PP, ho = pix / WO, wo = pix % WO;
+        const P* src = reinterpret_cast<const P*>(yb + ((size_t)c * H + 2 * ho) * W + 2 * wo);
+        top[i] = src[0];
+        bot[i] = src[W / 2];
+        g[i] = dpb[e];
+        ix[i] = ib[e];
+      }
+    }
+  }
+
+  template <typename Sink>
+  __device__ __forceinline__ void emit(const float* coef, Sink&& sink) {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = threadIdx.x + i * NT_;
+      if (e < NWIN) {
+        const int c = e / PP, pix = e % PP, ho = pix / WO, wo = pix % WO;
+        const float k1 = coef[c], k2 = coef[C + c], gi = coef[2 * C + c], mean = coef[3 * C + c],
+                    istd = coef[4 * C + c];
+        T v[4];
+        __builtin_memcpy(&v[0], &top[i], 2 * sizeof(T));
+        __builtin_memcpy(&v[2], &bot[i], 2 * sizeof(T));
+        const int k = ix[i] & IDX_POS;
+        const float gg = (ix[i] & IDX_RELU) ? Cvt<T>::to_f(g[i]) : 0.f;
+        T o[4];
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const float xh = (Cvt<T>::to_f(v[qq]) - mean) * istd;
+          o[qq] = Cvt<T>::from_f(gi * ((qq == k ? gg : 0.f) - k1 - xh * k2));
+        }
+        sink(c, 2 * ho, 2 * wo, o[0], o[1], o[2], o[3]);
+      }
+    }
+  }
+};
+
+// Epilogue of the data-grad kernel that produces a pooled grad: per-workgroup
+// BN partial sums of the block below ([S1 | S2] per channel -> one slab row).
+template <typename T>
+struct BwdEpi {
+  const uint8_t* idx;  // that block's pooled index (relu bit)
+  const T* xh;         // that block's xhat at the argmax
+  float* bslab;        // rows = workgroups, row = [S1(COUT) | S2(COUT)]
 };
 
 // ---------------------------------------------------------------------------
@@ -224,15 +403,23 @@ struct PoolIn {
 //   PRO 0: the input image is read from x;
 //   PRO 1: the input is produced in the staging pass from the previous block's
 //          pre-BN output (pin: BN finalize -> normalise -> ReLU -> 2x2 max-pool),
-//          which also writes the pooled map + argmax for the backward (split 0).
-template <typename T, int CIN, int COUT, int H, int W, int MODE, int PRO = 0>
+//          which also writes the pooled map + argmax|relu index + xhat at the
+//          argmax for the backward (split 0);
+//   PRO 2: (MODE 2) the input dy is produced from the pooled grad of the next
+//          block (bin: backward through MaxPool -> ReLU -> BN, see BwdIn).
+//   EPI 1: (MODE 2) the output is a pooled grad: also write this workgroup's
+//          BN partial sums [S1 | S2] of the block below (epi).
+template <typename T, int CIN, int COUT, int H, int W, int MODE, int PRO = 0, int EPI = 0>
 __global__ void __launch_bounds__(NTHR)
 conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
                T* __restrict__ y, float* __restrict__ fslab, float* __restrict__ fstats,
-               const float* __restrict__ shift, int nsplit, PoolIn<T> pin = PoolIn<T>{}) {
+               const float* __restrict__ shift, int nsplit, PoolIn<T> pin = PoolIn<T>{},
+               BwdIn<T> bin = BwdIn<T>{}, BwdEpi<T> epi = BwdEpi<T>{}) {
   static_assert(CIN == 1 || CIN % 8 == 0, "CIN must be 1 or a multiple of 8");
   static_assert(COUT % 16 == 0, "COUT must be a multiple of 16");
   static_assert((H * W) % 4 == 0, "H*W must be a multiple of 4");
+  static_assert(PRO != 2 || MODE == 2, "PRO 2 is a data-grad prologue");
+  static_assert(EPI == 0 || MODE == 2, "EPI 1 is a data-grad epilogue");
   constexpr int HP = H + 4, WPD = W + 4;
   constexpr int K = 25 * CIN;
   constexpr int KP = ceil_to(K, 32);
@@ -251,6 +438,7 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
   const int b = blockIdx.x / nsplit;
   const int sp = blockIdx.x % nsplit;
   const T* xb = x + (size_t)b * CIN * HW;
+  const int mt0 = (MT * sp) / nsplit, mt1 = (MT * (sp + 1)) / nsplit;
 
   // --- stage weights (batched float4 reads in natural [co][ci][kh][kw] order,
   //     scattered LDS writes to wl[co][(kh*5+kw)*CIN + ci])
@@ -275,22 +463,34 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
     const int wp = rem / CIN;
     if (hp < 2 || hp >= H + 2 || wp < 2 || wp >= W + 2) img[e] = zero;
   }
+  // EPI: this workgroup's output range of the pooled index / xhat of the block below
+  constexpr int EPIX = EPI ? MT * 16 : 1;
+  __shared__ uint8_t eidx[EPI ? COUT * EPIX : 1];
+  __shared__ T exh[EPI ? COUT * EPIX : 1];
+  if constexpr (EPI == 1) {
+    const int p0 = mt0 * 16, np = min(mt1 * 16, HW) - p0;
+    for (int e = tid; e < COUT * np; e += NTHR) {
+      const int co = e / np, pp = e % np;
+      const size_t o = ((size_t)b * COUT + co) * HW + p0 + pp;
+      eidx[co * EPIX + pp] = epi.idx[o];
+      exh[co * EPIX + pp] = epi.xh[o];
+    }
+  }
   if constexpr (PRO == 0) {
     stage_chw<T, CIN, H, W>(xb, [&](int ci, int h, int ww, T a, T bb) {
       img[((h + 2) * WPD + (ww + 2)) * CIN + ci] = a;
       img[((h + 2) * WPD + (ww + 3)) * CIN + ci] = bb;
     });
-  } else {
-    __shared__ float sc_s[CIN], sh_s[CIN];
+  } else if constexpr (PRO == 1) {
+    __shared__ float sc_s[CIN], sh_s[CIN], mean_s[CIN], istd_s[CIN];
     __shared__ float part[NTHR];
-    bn_finalize<CIN>(pin.bn, sc_s, sh_s, part, blockIdx.x == 0);
     typedef typename Pair2<T>::type P;
     constexpr int NPO = CIN * HW;  // pooled outputs of one image = this conv's input
     constexpr int IT = (NPO + NTHR - 1) / NTHR;
     const T* yb = pin.y + (size_t)b * CIN * 4 * HW;
     P top[IT], bot[IT];
 #pragma unroll
-    for (int i = 0; i < IT; ++i) {
+    for (int i = 0; i < IT; ++i) {  // issued before the statistics reduction: the latencies overlap
       const int e = tid + i * NTHR;
       if (e < NPO) {
         const int ci = e / HW, pix = e % HW, ho = pix / W, wo = pix % W;
@@ -299,29 +499,42 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
         bot[i] = src[W];  // next input row (2W elements = W pairs)
       }
     }
+    bn_finalize<CIN>(pin.bn, sc_s, sh_s, part, blockIdx.x == 0, mean_s, istd_s);
     const bool wr = pin.p_out != nullptr && sp == 0;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int e = tid + i * NTHR;
       if (e < NPO) {
         const int ci = e / HW, pix = e % HW, ho = pix / W, wo = pix % W;
-        float best;
+        float best, xh;
         int bi;
-        bn_relu_max4<T>(top[i], bot[i], sc_s[ci], sh_s[ci], best, bi);
+        bn_relu_max4x<T>(top[i], bot[i], sc_s[ci], sh_s[ci], mean_s[ci], istd_s[ci], best, bi, xh);
         const T pv = Cvt<T>::from_f(best);
         img[((ho + 2) * WPD + (wo + 2)) * CIN + ci] = pv;
         if (wr) {
           pin.p_out[(size_t)b * NPO + e] = pv;
-          pin.idx_out[(size_t)b * NPO + e] = (uint8_t)bi;
+          pin.idx_out[(size_t)b * NPO + e] = (uint8_t)(bi | (best > 0.f ? IDX_RELU : 0));
+          pin.xh_out[(size_t)b * NPO + e] = Cvt<T>::from_f(xh);
         }
       }
     }
+  } else {
+    __shared__ float coef[5 * CIN], sums[2 * CIN];
+    __shared__ float part[NTHR];
+    BnBwdStage<T, CIN, H, W, NTHR> st;
+    st.load(bin, b);
+    bn_bwd_coef<CIN, T>(bin, coef, part, sums, blockIdx.x == 0);
+    st.emit(coef, [&](int c, int h, int ww, T v00, T v01, T v10, T v11) {
+      img[((h + 2) * WPD + (ww + 2)) * CIN + c] = v00;
+      img[((h + 2) * WPD + (ww + 3)) * CIN + c] = v01;
+      img[((h + 3) * WPD + (ww + 2)) * CIN + c] = v10;
+      img[((h + 3) * WPD + (ww + 3)) * CIN + c] = v11;
+    });
   }
   __syncthreads();
 
   const int lane = tid & 63, wv = tid >> 6;
   const int r = lane & 15, q = lane >> 4;
-  const int mt0 = (MT * sp) / nsplit, mt1 = (MT * (sp + 1)) / nsplit;
 
   float s1[NT], s2[NT];
 #pragma unroll
@@ -376,11 +589,17 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
             s1[nt] += d;
             s2[nt] += d * d;
           }
+          if (EPI == 1) {
+            const int le = co * EPIX + pix0 - mt0 * 16 + i;
+            const float g = (eidx[le] & IDX_RELU) ? rnd_t<T>(v) : 0.f;
+            s1[nt] += g;
+            s2[nt] += g * Cvt<T>::to_f(exh[le]);
+          }
         }
       }
     }
   }
-  if constexpr (MODE == 0) {
+  if constexpr (MODE == 0 || EPI == 1) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       float a1 = s1[nt], a2 = s2[nt];
@@ -394,18 +613,21 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
       }
     }
     __syncthreads();
-    float* row = fslab + (size_t)blockIdx.x * fslab_row(COUT);
+    float* row = (MODE == 0 ? fslab + (size_t)blockIdx.x * fslab_row(COUT)
+                            : epi.bslab + (size_t)blockIdx.x * 2 * COUT);
     if (tid < 2 * COUT) {
       float t = 0.f;
 #pragma unroll
       for (int w2 = 0; w2 < NTHR / 64; ++w2) t += lstat[w2 * 2 * COUT + tid];
       row[tid] = t;
     }
-    if (tid == 0) {
-      const int p0 = mt0 * 16, p1 = min(mt1 * 16, HW);
-      row[2 * COUT] = (float)(p1 - p0);
+    if constexpr (MODE == 0) {
+      if (tid == 0) {
+        const int p0 = mt0 * 16, p1 = min(mt1 * 16, HW);
+        row[2 * COUT] = (float)(p1 - p0);
+      }
+      if (blockIdx.x == 0 && tid < COUT) fstats[2 * COUT + 1 + tid] = shift[tid];
     }
-    if (blockIdx.x == 0 && tid < COUT) fstats[2 * COUT + 1 + tid] = shift[tid];
   }
 }
 
@@ -621,10 +843,13 @@ bwd_elemt_kernel(const T* __restrict__ dp, const T* __restrict__ p, const uint8_
 // When there are fewer (m,n) tile pairs than waves, waves split K instead
 // and combine through LDS.
 // ---------------------------------------------------------------------------
-template <typename T, int CIN, int COUT, int H, int W, int ROWS>
+// PRO 2: dy is produced on the fly from the pooled grad of the next block
+// (bin: backward through MaxPool -> ReLU -> BN); needs ROWS == H.
+template <typename T, int CIN, int COUT, int H, int W, int ROWS, int PRO = 0>
 __global__ void __launch_bounds__(NTHR)
 conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* __restrict__ wslab,
-                     int nsplit) {
+                     int nsplit, BwdIn<T> bin = BwdIn<T>{}) {
+  static_assert(PRO == 0 || (PRO == 2 && ROWS == H), "PRO 2 needs whole images per workgroup");
   constexpr int WP = ceil_to(W, 8);
   static_assert((ROWS * WP) % 32 == 0, "ROWS*WP must be a multiple of 32");
   constexpr int KSTEPS = ROWS * WP / 32;
@@ -665,7 +890,23 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
     const int ih = r0 + rr - 2;
     if (cc < 2 || cc >= W + 2 || ih < 0 || ih >= H) xpad[e] = zero;
   }
-  if (ROWS == H) {  // whole image per workgroup: both operands are full [C][H][W] images
+  if constexpr (PRO == 2) {
+    __shared__ float coef[5 * COUT], sums[2 * COUT];
+    __shared__ float part[NTHR];
+    BnBwdStage<T, COUT, H, W, NTHR> st;
+    st.load(bin, b);
+    stage_chw<T, CIN, H, W>(xb, [&](int ci, int h, int ww, T a, T bb) {
+      xpad[(ci * XR + h + 2) * WX + ww + 2] = a;
+      xpad[(ci * XR + h + 2) * WX + ww + 3] = bb;
+    });
+    bn_bwd_coef<COUT, T>(bin, coef, part, sums, blockIdx.x == 0);
+    st.emit(coef, [&](int co, int h, int ww, T v00, T v01, T v10, T v11) {
+      dyl[(co * ROWS + h) * WP + ww] = v00;
+      dyl[(co * ROWS + h) * WP + ww + 1] = v01;
+      dyl[(co * ROWS + h + 1) * WP + ww] = v10;
+      dyl[(co * ROWS + h + 1) * WP + ww + 1] = v11;
+    });
+  } else if (ROWS == H) {  // whole image per workgroup: both operands are full [C][H][W] images
     stage_chw<T, COUT, H, W>(dyb, [&](int co, int h, int ww, T a, T bb) {
       dyl[(co * ROWS + h) * WP + ww] = a;
       dyl[(co * ROWS + h) * WP + ww + 1] = bb;

@@ -1,15 +1,20 @@
 // Whole-ConvNet fused kernels (ops/convnet_fused.py).  Layer boundaries are
-// fused where the data dependence allows it:
+// fused where the data dependence allows it; every BatchNorm reduction is
+// produced as per-workgroup partial sums in the epilogue of the kernel that
+// computes its operand and reduced in the prologue of the kernel that needs
+// the result, so no launch exists only to reduce or to apply a BatchNorm:
 //
-//   forward   gather | conv1(+BN1 partial sums) | [BN1-ReLU-pool1 -> conv2 (+BN2 sums)]
-//             | [BN2-ReLU-pool2 -> fc] -> logits
-//   backward  [fc bwd + pool2/ReLU2 routing + BN2 reduce (+ BN2 input grad)]
-//             | conv2 wgrad | conv2 dgrad | [pool1/ReLU1 routing + BN1 reduce (+ BN1 input grad)]
-//             | conv1 wgrad | slab sums
+//   forward   gather | conv1 (+BN1 sums) | [BN1-ReLU-pool1 -> conv2 (+BN2 sums)]
+//             | [BN2-ReLU-pool2 -> fc] -> logits                          (3 launches)
+//   backward  [fc bwd -> dp2 (+BN2 sums: complete per channel)]
+//             | [BN2/ReLU2/pool2 bwd -> conv2 dgrad -> dp1 (+BN1 partial sums)]
+//             | [BN2/ReLU2/pool2 bwd -> conv2 wgrad]        (independent of dgrad)
+//             | [BN1/ReLU1/pool1 bwd -> conv1 wgrad]
+//             | weight-grad sums                                        (5 launches)
 //
-// (reference model: /root/reference/origin_main.py:9-31.)  With SyncBN the BN
-// input-grad steps run as separate launches after an all-reduce of the
-// per-channel sums.  Everything stays deterministic (no float atomics).
+// (reference model: /root/reference/origin_main.py:9-31.)  With SyncBN the
+// partial sums are all-reduced between the launches (host side).  Everything
+// is deterministic (no float atomics).
 #include "convblock_impl.h"
 
 namespace dpa {
@@ -17,214 +22,109 @@ namespace cnf {
 
 using cb::BNParams;
 using cb::bn_finalize;
-using cb::bn_relu_max4;
+using cb::bn_relu_max4x;
+using cb::BwdEpi;
+using cb::BwdIn;
+using cb::IDX_POS;
+using cb::IDX_RELU;
 using cb::Pair2;
 using cb::PoolIn;
 
-constexpr int HT = 1024;       // head forward: one big workgroup per 16-row tile
+constexpr int HF = 256;        // head forward: one workgroup per image
 constexpr int NTHR_HB = 256;   // head backward: one workgroup per BN2 channel
-constexpr int NTHR_PB = 1024;  // pool1/BN1 backward: one workgroup per BN1 channel
 
 // ---------------------------------------------------------------------------
-// [BN2 finalize -> BN -> ReLU -> 2x2 max-pool -> flatten -> Linear] for 16
-// batch rows per workgroup.  The pooled features of the 16 rows are staged in
-// LDS as the MFMA A operand; fc weights (f32, row-major [N][K]) are read once
-// per workgroup straight to registers.  NTL = ceil(N / 16) output tiles.
+// [BN2 finalize -> BN -> ReLU -> 2x2 max-pool -> flatten -> Linear] for one
+// image per workgroup (B workgroups: the whole chip works on the head instead
+// of B/16 tiles).  The fc is a 1 x K x N GEMV per image: every thread owns K/HF
+// pooled features, multiplies them against the fc rows and the N partial dot
+// products are reduced across the workgroup.  The y2 loads are issued before
+// the BN statistics reduction so the two latencies overlap.
 // ---------------------------------------------------------------------------
-template <typename T, int C, int H, int W, int NTL>
-__global__ void __launch_bounds__(HT)
-head_fwd_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__ wfc,
-                const float* __restrict__ bfc, T* __restrict__ logits, T* __restrict__ p_out,
-                uint8_t* __restrict__ idx_out, int B, int N) {
+template <typename T, int C, int H, int W, int NMAX>
+__global__ void __launch_bounds__(HF)
+head_fwd_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__ wfc, const float* __restrict__ bfc,
+                T* __restrict__ logits, T* __restrict__ p_out, uint8_t* __restrict__ idx_out, T* __restrict__ xh_out,
+                int N) {
   constexpr int HO = H / 2, WO = W / 2, PP = HO * WO, K = C * PP;
-  constexpr int KPAD = ceil_to(K, 32) + 8;  // zero K-padding + 16 B row skew
-  constexpr int KS = (K + 31) / 32;
-  constexpr int NW = HT / 64;
-  typedef MM<T> mm;
+  constexpr int IT = (K + HF - 1) / HF;
   typedef typename Pair2<T>::type P;
-  __shared__ __attribute__((aligned(16))) T pimg[16 * KPAD];
-  __shared__ float sc_s[C], sh_s[C];
-  __shared__ float part[HT];
-  __shared__ f32x4 red[NW][64];
-
-  const int tid = threadIdx.x;
-  const int row0 = blockIdx.x * 16;
-  const int rows = min(16, B - row0);
-  bn_finalize<C>(bn, sc_s, sh_s, part, blockIdx.x == 0);
-
-  // zero the K padding columns and the rows past the batch
-  for (int e = tid; e < 16 * (KPAD - K); e += HT) pimg[(e / (KPAD - K)) * KPAD + K + e % (KPAD - K)] = Cvt<T>::from_f(0.f);
-  // pooled features: 16 rows x K, 8 windows per thread in flight per batch
-  constexpr int TOT = 16 * K;
-  constexpr int U = 8;
-  for (int base = 0; base < TOT; base += U * HT) {
-    P top[U], bot[U];
+  __shared__ float sc_s[C], sh_s[C], mean_s[C], istd_s[C];
+  __shared__ float part[HF];
+  __shared__ float red[HF / 64][NMAX];
+  const int tid = threadIdx.x, b = blockIdx.x;
+  const T* yb = y + (size_t)b * C * H * W;
+  P top[IT], bot[IT];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = base + u * HT + tid;
-      const int r = e / K, f = e % K;
-      if (e < TOT && r < rows) {
-        const int c = f / PP, pix = f % PP, ho = pix / WO, wo = pix % WO;
-        const P* src = reinterpret_cast<const P*>(y + (((size_t)(row0 + r) * C + c) * H + 2 * ho) * W + 2 * wo);
-        top[u] = src[0];
-        bot[u] = src[W / 2];
+  for (int i = 0; i < IT; ++i) {
+    const int k = tid + i * HF;
+    if (k < K) {
+      const int c = k / PP, pix = k % PP, ho = pix / WO, wo = pix % WO;
+      const P* src = reinterpret_cast<const P*>(yb + ((size_t)c * H + 2 * ho) * W + 2 * wo);
+      top[i] = src[0];
+      bot[i] = src[W / 2];
+    }
+  }
+  bn_finalize<C>(bn, sc_s, sh_s, part, b == 0, mean_s, istd_s);
+  float pf[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int k = tid + i * HF;
+    pf[i] = 0.f;
+    if (k < K) {
+      const int c = k / PP;
+      float best, xh;
+      int bi;
+      bn_relu_max4x<T>(top[i], bot[i], sc_s[c], sh_s[c], mean_s[c], istd_s[c], best, bi, xh);
+      const T pv = Cvt<T>::from_f(best);
+      pf[i] = Cvt<T>::to_f(pv);
+      if (p_out != nullptr) {
+        p_out[(size_t)b * K + k] = pv;
+        idx_out[(size_t)b * K + k] = (uint8_t)(bi | (best > 0.f ? IDX_RELU : 0));
+        xh_out[(size_t)b * K + k] = Cvt<T>::from_f(xh);
       }
     }
+  }
+  const int lane = tid & 63, wv = tid >> 6;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = base + u * HT + tid;
-      if (e >= TOT) continue;
-      const int r = e / K, f = e % K;
-      if (r < rows) {
-        float best;
-        int bi;
-        bn_relu_max4<T>(top[u], bot[u], sc_s[f / PP], sh_s[f / PP], best, bi);
-        const T pv = Cvt<T>::from_f(best);
-        pimg[r * KPAD + f] = pv;
-        if (p_out != nullptr) {
-          p_out[(size_t)(row0 + r) * K + f] = pv;
-          idx_out[(size_t)(row0 + r) * K + f] = (uint8_t)bi;
-        }
-      } else {
-        pimg[r * KPAD + f] = Cvt<T>::from_f(0.f);
+  for (int n = 0; n < NMAX; ++n) {
+    if (n < N) {  // uniform
+      float a = 0.f;
+#pragma unroll
+      for (int i = 0; i < IT; ++i) {
+        const int k = tid + i * HF;
+        if (k < K) a += pf[i] * wfc[(size_t)n * K + k];
       }
+      a = wave_sum(a);
+      if (lane == 0) red[wv][n] = a;
     }
   }
   __syncthreads();
-
-  const int lane = tid & 63, wv = tid >> 6;
-  const int r = lane & 15, q = lane >> 4;
-  f32x4 acc[NTL];
+  if (tid < N) {
+    float t = bfc[tid];
 #pragma unroll
-  for (int nt = 0; nt < NTL; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int s = wv; s < KS; s += NW) {
-    const int k0 = 32 * s + 8 * q;
-    const typename mm::frag a = mm::ld(&pimg[r * KPAD + k0]);
-#pragma unroll
-    for (int nt = 0; nt < NTL; ++nt) {
-      const int n = nt * 16 + r;
-      typename mm::frag bf;
-      if (n < N && k0 + 8 <= K) {
-        const f32x4 lo = *reinterpret_cast<const f32x4*>(wfc + (size_t)n * K + k0);
-        const f32x4 hi = *reinterpret_cast<const f32x4*>(wfc + (size_t)n * K + k0 + 4);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { bf[j] = mm::cv(lo[j]); bf[4 + j] = mm::cv(hi[j]); }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) bf[j] = mm::cv((n < N && k0 + j < K) ? wfc[(size_t)n * K + k0 + j] : 0.f);
-      }
-      acc[nt] = mm::mma(a, bf, acc[nt]);
-    }
-  }
-#pragma unroll
-  for (int nt = 0; nt < NTL; ++nt) {
-    __syncthreads();
-    red[wv][lane] = acc[nt];
-    __syncthreads();
-    if (wv == 0) {
-      f32x4 t = red[0][lane];
-#pragma unroll
-      for (int i = 1; i < NW; ++i) t += red[i][lane];
-      const int col = nt * 16 + r;
-      if (col < N) {
-        const float bb = bfc[col];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = 4 * q + i;
-          if (row < rows) logits[(size_t)(row0 + row) * N + col] = Cvt<T>::from_f(t[i] + bb);
-        }
-      }
-    }
-  }
-}
-
-// mean / invstd / count of channel c from the final stats buffer.
-template <int C>
-__device__ __forceinline__ void mean_invstd(const float* fstats, int c, float eps, float& mean, float& invstd,
-                                            float& n) {
-  n = fstats[2 * C];
-  const float m1 = fstats[c] / n;
-  mean = fstats[2 * C + 1 + c] + m1;
-  invstd = rsqrtf(fmaxf(fstats[C + c] / n - m1 * m1, 0.f) + eps);
-}
-
-// Per-channel BN backward over one pooled layer, one workgroup per channel.
-// `gp(b, j)` returns the (un-routed) gradient of pooled output j of image b.
-// Phase 1 routes it through ReLU (pooled value > 0) and the argmax and sums
-// dy and dy*xhat; phase 2 (non-sync) writes the BN input gradient dx at full
-// resolution, recomputing the routing.
-template <typename T, int C, int H, int W, int THR, typename GP>
-__device__ __forceinline__ void pool_bn_bwd_channel(GP&& gp, const T* __restrict__ p, const uint8_t* __restrict__ idx,
-                                                    const T* __restrict__ y, const float* __restrict__ fstats,
-                                                    const float* __restrict__ gamma, float eps, int B, int c,
-                                                    float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                    float* __restrict__ bslab, T* __restrict__ dx, float* red) {
-  constexpr int HO = H / 2, WO = W / 2, PP = HO * WO;
-  const int tid = threadIdx.x;
-  float mean, invstd, n;
-  mean_invstd<C>(fstats, c, eps, mean, invstd, n);
-  float a1 = 0.f, a2 = 0.f;
-  const int cnt = B * PP;
-  for (int t = tid; t < cnt; t += THR) {
-    const int b = t / PP, j = t % PP;
-    const size_t e = ((size_t)b * C + c) * PP + j;
-    if (Cvt<T>::to_f(p[e]) > 0.f) {
-      const float g = gp(b, j);
-      const int k = idx[e];
-      const int ho = j / WO, wo = j % WO;
-      const float yv = Cvt<T>::to_f(y[((size_t)b * C + c) * H * W + (2 * ho + (k >> 1)) * W + 2 * wo + (k & 1)]);
-      a1 += g;
-      a2 += g * (yv - mean) * invstd;
-    }
-  }
-  a1 = wave_sum(a1);
-  a2 = wave_sum(a2);
-  const int lane = tid & 63, wv = tid >> 6;
-  if (lane == 0) { red[wv] = a1; red[THR / 64 + wv] = a2; }
-  __syncthreads();
-  float s1 = 0.f, s2 = 0.f;
-  for (int i = 0; i < THR / 64; ++i) { s1 += red[i]; s2 += red[THR / 64 + i]; }
-  if (tid == 0) {
-    dbeta[c] = s1;
-    dgamma[c] = s2;
-    bslab[c] = s1;
-    bslab[C + c] = s2;
-  }
-  if (dx == nullptr) return;
-  const float k1 = s1 / n, k2 = s2 / n, gi = gamma[c] * invstd;
-  for (int t = tid; t < cnt; t += THR) {
-    const int b = t / PP, j = t % PP;
-    const size_t e = ((size_t)b * C + c) * PP + j;
-    const float g = Cvt<T>::to_f(p[e]) > 0.f ? gp(b, j) : 0.f;
-    const int kk = idx[e];
-    const int ho = j / WO, wo = j % WO;
-    const size_t base = ((size_t)b * C + c) * H * W + (2 * ho) * W + 2 * wo;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const size_t o = base + (k >> 1) * W + (k & 1);
-      const float xh = (Cvt<T>::to_f(y[o]) - mean) * invstd;
-      dx[o] = Cvt<T>::from_f(gi * (((k == kk) ? g : 0.f) - k1 - xh * k2));
-    }
+    for (int i = 0; i < HF / 64; ++i) t += red[i][tid];
+    logits[(size_t)b * N + tid] = Cvt<T>::from_f(t);
   }
 }
 
 // ---------------------------------------------------------------------------
-// fc backward + pool2/ReLU2 routing + BN2 reduce (+ BN2 input grad), one
-// workgroup per BN2 channel c (its PP = 7*7 pooled features).
-//   dW_fc[:, cPP..] = dlogits^T . p2[:, cPP..]     (complete: all batch rows)
-//   dp2[b, cPP + j] = sum_n dlogits[b, n] W[n, cPP + j]
-// dynamic LDS: dlogits [B][N] f32 + W columns [N][PP] f32 + p2 slice [B][PP] f32.
+// fc backward + the BN2 backward sums, one workgroup per BN2 channel c (its
+// PP = 7*7 pooled features; the sums are complete, no partial rows):
+//   dp2[b, cPP + j]   = sum_n dlogits[b, n] W[n, cPP + j]          (stored in T)
+//   dW_fc[n, cPP + j] = sum_b dlogits[b, n] p2[b, cPP + j]
+//   S1[c] = sum g, S2[c] = sum g * xhat, g = dp2 where the ReLU passed it
+// dynamic LDS: dlogits [B][N] + W columns [N][PP] + p2 slice [B][PP] (f32).
 // ---------------------------------------------------------------------------
 template <typename T, int C, int H, int W>
 __global__ void __launch_bounds__(NTHR_HB)
 head_bwd_kernel(const T* __restrict__ dlogits, const float* __restrict__ wfc, const T* __restrict__ p2,
-                const uint8_t* __restrict__ idx2, const T* __restrict__ y2, const float* __restrict__ fstats2,
-                const float* __restrict__ gamma2, float eps, int B, int N, float* __restrict__ dwfc,
+                const uint8_t* __restrict__ idx2, const T* __restrict__ xh2, int B, int N, float* __restrict__ dwfc,
                 float* __restrict__ dbfc, float* __restrict__ dgamma, float* __restrict__ dbeta,
-                float* __restrict__ bslab, T* __restrict__ dp2_out, T* __restrict__ dy2) {
+                float* __restrict__ bsum, T* __restrict__ dp2) {
   constexpr int HO = H / 2, WO = W / 2, PP = HO * WO, K = C * PP;
   extern __shared__ __attribute__((aligned(16))) float hsm[];
-  __shared__ float red[2 * NTHR_HB / 64];
+  __shared__ float red[2][NTHR_HB / 64];
   float* dl = hsm;               // [B][N]
   float* wc = dl + B * N;        // [N][PP]
   float* pc = wc + N * PP;       // [B][PP]
@@ -233,6 +133,23 @@ head_bwd_kernel(const T* __restrict__ dlogits, const float* __restrict__ wfc, co
   for (int e = tid; e < N * PP; e += NTHR_HB) wc[e] = wfc[(size_t)(e / PP) * K + f0 + e % PP];
   for (int e = tid; e < B * PP; e += NTHR_HB) pc[e] = Cvt<T>::to_f(p2[(size_t)(e / PP) * K + f0 + e % PP]);
   __syncthreads();
+  // pooled-map grad + BN2 sums
+  float s1 = 0.f, s2 = 0.f;
+  for (int e = tid; e < B * PP; e += NTHR_HB) {
+    const int b = e / PP, j = e % PP;
+    const size_t o = (size_t)b * K + f0 + j;
+    const uint8_t ix = idx2[o];
+    const float xh = Cvt<T>::to_f(xh2[o]);
+    float a = 0.f;
+    for (int nn = 0; nn < N; ++nn) a += dl[b * N + nn] * wc[nn * PP + j];
+    const T gt = Cvt<T>::from_f(a);
+    dp2[o] = gt;
+    if (ix & IDX_RELU) {
+      const float g = Cvt<T>::to_f(gt);
+      s1 += g;
+      s2 += g * xh;
+    }
+  }
   // fc weight grad for this channel's columns, fc bias grad on workgroup 0
   for (int e = tid; e < N * PP; e += NTHR_HB) {
     const int nn = e / PP, j = e % PP;
@@ -247,33 +164,21 @@ head_bwd_kernel(const T* __restrict__ dlogits, const float* __restrict__ wfc, co
       dbfc[nn] = a;
     }
   }
-  auto gp = [&](int b, int j) {
-    float a = 0.f;
-    for (int nn = 0; nn < N; ++nn) a += dl[b * N + nn] * wc[nn * PP + j];
-    return Cvt<T>::to_f(Cvt<T>::from_f(a));  // the pooled-map grad as stored in T (autocast semantics)
-  };
-  if (dp2_out != nullptr) {  // SyncBN path: materialise dp2 for the separate BN input-grad launch
-    for (int e = tid; e < B * PP; e += NTHR_HB)
-      dp2_out[(size_t)(e / PP) * K + f0 + e % PP] = Cvt<T>::from_f(gp(e / PP, e % PP));
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  const int lane = tid & 63, wv = tid >> 6;
+  if (lane == 0) { red[0][wv] = s1; red[1][wv] = s2; }
+  __syncthreads();
+  if (tid == 0) {
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NTHR_HB / 64; ++i) { t1 += red[0][i]; t2 += red[1][i]; }
+    dbeta[c] = t1;
+    dgamma[c] = t2;
+    bsum[c] = t1;
+    bsum[C + c] = t2;
   }
-  pool_bn_bwd_channel<T, C, H, W, NTHR_HB>(gp, p2, idx2, y2, fstats2, gamma2, eps, B, c, dgamma, dbeta, bslab, dy2,
-                                           red);
 }
-
-// pool1/ReLU1 routing + BN1 reduce (+ BN1 input grad), one workgroup per channel.
-template <typename T, int C, int H, int W>
-__global__ void __launch_bounds__(NTHR_PB)
-pool_bn_bwd_kernel(const T* __restrict__ dp, const T* __restrict__ p, const uint8_t* __restrict__ idx,
-                   const T* __restrict__ y, const float* __restrict__ fstats, const float* __restrict__ gamma,
-                   float eps, int B, float* __restrict__ dgamma, float* __restrict__ dbeta,
-                   float* __restrict__ bslab, T* __restrict__ dx) {
-  constexpr int PP = (H / 2) * (W / 2);
-  __shared__ float red[2 * NTHR_PB / 64];
-  const int c = blockIdx.x;
-  auto gp = [&](int b, int j) { return Cvt<T>::to_f(dp[((size_t)b * C + c) * PP + j]); };
-  pool_bn_bwd_channel<T, C, H, W, NTHR_PB>(gp, p, idx, y, fstats, gamma, eps, B, c, dgamma, dbeta, bslab, dx, red);
-}
-
 
 // ===========================================================================
 // Host side
@@ -306,16 +211,46 @@ static BNParams bn_params(c10::optional<at::Tensor> fslab, at::Tensor fstats, at
   return bp;
 }
 
+template <typename T>
+static BwdIn<T> bwd_in(at::Tensor dp, at::Tensor idx, at::Tensor y, at::Tensor fstats, at::Tensor gsum,
+                       c10::optional<at::Tensor> lsum, at::Tensor gamma, double eps, int C,
+                       c10::optional<at::Tensor> dgamma, c10::optional<at::Tensor> dbeta) {
+  TORCH_CHECK(gsum.numel() % (2 * C) == 0, "BN backward sums: rows of 2C floats expected");
+  TORCH_CHECK(dp.scalar_type() == y.scalar_type() && idx.scalar_type() == at::kByte);
+  TORCH_CHECK(fstats.numel() == cb::stats_len(C) && gamma.numel() == C);
+  BwdIn<T> bi;
+  bi.dp = dptr<T>(dp);
+  bi.idx = idx.data_ptr<uint8_t>();
+  bi.y = dptr<T>(y);
+  bi.fstats = fstats.data_ptr<float>();
+  bi.gsum = gsum.data_ptr<float>();
+  bi.grows = (int)(gsum.numel() / (2 * C));
+  at::Tensor ls = lsum.has_value() ? *lsum : gsum;
+  TORCH_CHECK(ls.numel() % (2 * C) == 0);
+  bi.lsum = ls.data_ptr<float>();
+  bi.lrows = (int)(ls.numel() / (2 * C));
+  bi.gamma = gamma.data_ptr<float>();
+  bi.eps = (float)eps;
+  bi.dgamma = dgamma.has_value() ? dgamma->data_ptr<float>() : nullptr;
+  bi.dbeta = dbeta.has_value() ? dbeta->data_ptr<float>() : nullptr;
+  return bi;
+}
+
 // [BN1 -> ReLU -> pool1] -> conv2 (+ BN2 partial sums when training).
 void conv2_fwd(at::Tensor y1, c10::optional<at::Tensor> fslab1, at::Tensor fstats1, at::Tensor g1, at::Tensor b1,
                at::Tensor rm1, at::Tensor rv1, at::Tensor nbt1, double momentum, double eps, bool train, at::Tensor w2,
                at::Tensor bias2, at::Tensor y2, c10::optional<at::Tensor> fslab2, at::Tensor fstats2, at::Tensor rm2,
-               c10::optional<at::Tensor> p1_out, c10::optional<at::Tensor> idx1_out) {
+               c10::optional<at::Tensor> p1_out, c10::optional<at::Tensor> idx1_out,
+               c10::optional<at::Tensor> xh1_out) {
   DPA_CHECK_INPUT(y1); DPA_CHECK_INPUT(w2); DPA_CHECK_INPUT(y2);
   const int B = (int)y1.size(0);
   TORCH_CHECK(y1.size(1) == 16 && y1.size(2) == 28 && y1.size(3) == 28 && w2.size(0) == 32 && w2.size(1) == 16,
               "fused conv2 expects the ConvNet shapes");
   TORCH_CHECK(y2.scalar_type() == y1.scalar_type());
+  TORCH_CHECK(p1_out.has_value() == idx1_out.has_value() && p1_out.has_value() == xh1_out.has_value());
+  if (p1_out.has_value())
+    TORCH_CHECK(p1_out->numel() == (int64_t)B * 16 * 196 && idx1_out->numel() == p1_out->numel() &&
+                xh1_out->numel() == p1_out->numel());
   if (train) TORCH_CHECK(fslab2.has_value() && fslab2->numel() == (int64_t)B * 2 * cb::fslab_row(32));
   if (B == 0) return;
   const BNParams bp = bn_params(fslab1, fstats1, g1, b1, rm1, rv1, nbt1, momentum, eps, train, 16);
@@ -323,8 +258,9 @@ void conv2_fwd(at::Tensor y1, c10::optional<at::Tensor> fslab1, at::Tensor fstat
   hipStream_t stream = cur_stream();
   with_t(dt_of(y1), [&](auto tag) {
     typedef decltype(tag) T;
-    cb::PoolIn<T> pin{dptr<T>(y1), bp, p1_out.has_value() ? dptr<T>(*p1_out) : nullptr,
-                      idx1_out.has_value() ? idx1_out->data_ptr<uint8_t>() : nullptr};
+    PoolIn<T> pin{dptr<T>(y1), bp, p1_out.has_value() ? dptr<T>(*p1_out) : nullptr,
+                  idx1_out.has_value() ? idx1_out->data_ptr<uint8_t>() : nullptr,
+                  xh1_out.has_value() ? dptr<T>(*xh1_out) : nullptr};
     if (train)
       hipLaunchKernelGGL((cb::conv5x5_kernel<T, 16, 32, 14, 14, 0, 1>), dim3(B * ns), dim3(cb::NTHR), 0, stream,
                          nullptr, w2.data_ptr<float>(), bias2.data_ptr<float>(), dptr<T>(y2),
@@ -340,64 +276,108 @@ void conv2_fwd(at::Tensor y1, c10::optional<at::Tensor> fslab1, at::Tensor fstat
 // [BN2 -> ReLU -> pool2] -> flatten -> fc.
 void head_fwd(at::Tensor y2, c10::optional<at::Tensor> fslab2, at::Tensor fstats2, at::Tensor g2, at::Tensor b2,
               at::Tensor rm2, at::Tensor rv2, at::Tensor nbt2, double momentum, double eps, bool train, at::Tensor wfc,
-              at::Tensor bfc, at::Tensor logits, c10::optional<at::Tensor> p2_out, c10::optional<at::Tensor> idx2_out) {
+              at::Tensor bfc, at::Tensor logits, c10::optional<at::Tensor> p2_out, c10::optional<at::Tensor> idx2_out,
+              c10::optional<at::Tensor> xh2_out) {
   DPA_CHECK_INPUT(y2); DPA_CHECK_INPUT(wfc); DPA_CHECK_INPUT(logits);
   const int B = (int)y2.size(0), N = (int)wfc.size(0);
   TORCH_CHECK(y2.size(1) == 32 && y2.size(2) == 14 && y2.size(3) == 14 && wfc.size(1) == 32 * 49,
               "fused head expects the ConvNet shapes");
   TORCH_CHECK(N >= 1 && N <= 64, "fused head supports up to 64 classes");
+  TORCH_CHECK(logits.numel() == (int64_t)B * N && logits.scalar_type() == y2.scalar_type());
+  TORCH_CHECK(p2_out.has_value() == idx2_out.has_value() && p2_out.has_value() == xh2_out.has_value());
+  if (p2_out.has_value())
+    TORCH_CHECK(p2_out->numel() == (int64_t)B * 1568 && idx2_out->numel() == p2_out->numel() &&
+                xh2_out->numel() == p2_out->numel());
   if (B == 0) return;
   const BNParams bp = bn_params(fslab2, fstats2, g2, b2, rm2, rv2, nbt2, momentum, eps, train, 32);
-  const dim3 grid((B + 15) / 16);
   hipStream_t stream = cur_stream();
   with_t(dt_of(y2), [&](auto tag) {
     typedef decltype(tag) T;
     T* po = p2_out.has_value() ? dptr<T>(*p2_out) : nullptr;
     uint8_t* io = idx2_out.has_value() ? idx2_out->data_ptr<uint8_t>() : nullptr;
-    auto go = [&](auto ntl) {
-      hipLaunchKernelGGL((head_fwd_kernel<T, 32, 14, 14, decltype(ntl)::value>), grid, dim3(HT), 0, stream,
-                         dptr<T>(y2), bp, wfc.data_ptr<float>(), bfc.data_ptr<float>(), dptr<T>(logits), po, io, B, N);
+    T* xo = xh2_out.has_value() ? dptr<T>(*xh2_out) : nullptr;
+    auto go = [&](auto nmax) {
+      hipLaunchKernelGGL((head_fwd_kernel<T, 32, 14, 14, decltype(nmax)::value>), dim3(B), dim3(HF), 0, stream,
+                         dptr<T>(y2), bp, wfc.data_ptr<float>(), bfc.data_ptr<float>(), dptr<T>(logits), po, io, xo,
+                         N);
     };
-    if (N <= 16) go(std::integral_constant<int, 1>{});
-    else if (N <= 32) go(std::integral_constant<int, 2>{});
-    else go(std::integral_constant<int, 4>{});
+    if (N <= 16) go(std::integral_constant<int, 16>{});
+    else go(std::integral_constant<int, 64>{});
   });
   DPA_CHECK_LAUNCH();
 }
 
-// fc backward + pool2/ReLU2 routing + BN2 reduce (+ BN2 input grad when dy2 given).
-void head_bwd(at::Tensor dlogits, at::Tensor wfc, at::Tensor p2, at::Tensor idx2, at::Tensor y2, at::Tensor fstats2,
-              at::Tensor g2, double eps, at::Tensor dwfc, at::Tensor dbfc, at::Tensor dgamma2, at::Tensor dbeta2,
-              at::Tensor bslab2, c10::optional<at::Tensor> dp2_out, c10::optional<at::Tensor> dy2) {
-  DPA_CHECK_INPUT(dlogits); DPA_CHECK_INPUT(p2); DPA_CHECK_INPUT(y2);
-  const int B = (int)y2.size(0), N = (int)wfc.size(0);
-  TORCH_CHECK(dlogits.scalar_type() == y2.scalar_type() && p2.scalar_type() == y2.scalar_type());
-  const size_t lds = sizeof(float) * ((size_t)B * N + (size_t)N * 49 + (size_t)B * 49);
+size_t head_bwd_lds(int64_t B, int64_t N) { return sizeof(float) * (size_t)(B * N + N * 49 + B * 49); }
+
+// fc backward + BN2 backward sums (local, complete per channel).
+void head_bwd(at::Tensor dlogits, at::Tensor wfc, at::Tensor p2, at::Tensor idx2, at::Tensor xh2, at::Tensor dwfc,
+              at::Tensor dbfc, at::Tensor dgamma2, at::Tensor dbeta2, at::Tensor bsum2, at::Tensor dp2) {
+  DPA_CHECK_INPUT(dlogits); DPA_CHECK_INPUT(p2); DPA_CHECK_INPUT(dp2);
+  const int B = (int)p2.size(0), N = (int)wfc.size(0);
+  TORCH_CHECK(p2.numel() == (int64_t)B * 1568 && dp2.numel() == p2.numel() && xh2.numel() == p2.numel());
+  TORCH_CHECK(dlogits.numel() == (int64_t)B * N);
+  TORCH_CHECK(dlogits.scalar_type() == p2.scalar_type() && dp2.scalar_type() == p2.scalar_type());
+  TORCH_CHECK(bsum2.numel() == 64 && dwfc.numel() == wfc.numel() && dbfc.numel() == N);
+  const size_t lds = head_bwd_lds(B, N);
   TORCH_CHECK(lds <= 64 * 1024, "fused head backward: batch too large for LDS (B*N)");
-  with_t(dt_of(y2), [&](auto tag) {
+  if (B == 0) return;
+  with_t(dt_of(p2), [&](auto tag) {
     typedef decltype(tag) T;
     hipLaunchKernelGGL((head_bwd_kernel<T, 32, 14, 14>), dim3(32), dim3(NTHR_HB), lds, cur_stream(),
-                       dptr<T>(dlogits), wfc.data_ptr<float>(), dptr<T>(p2), idx2.data_ptr<uint8_t>(), dptr<T>(y2),
-                       fstats2.data_ptr<float>(), g2.data_ptr<float>(), (float)eps, B, N, dwfc.data_ptr<float>(),
-                       dbfc.data_ptr<float>(), dgamma2.data_ptr<float>(), dbeta2.data_ptr<float>(),
-                       bslab2.data_ptr<float>(), dp2_out.has_value() ? dptr<T>(*dp2_out) : nullptr,
-                       dy2.has_value() ? dptr<T>(*dy2) : nullptr);
+                       dptr<T>(dlogits), wfc.data_ptr<float>(), dptr<T>(p2), idx2.data_ptr<uint8_t>(), dptr<T>(xh2), B,
+                       N, dwfc.data_ptr<float>(), dbfc.data_ptr<float>(), dgamma2.data_ptr<float>(),
+                       dbeta2.data_ptr<float>(), bsum2.data_ptr<float>(), dptr<T>(dp2));
   });
   DPA_CHECK_LAUNCH();
 }
 
-// pool1/ReLU1 routing + BN1 reduce (+ BN1 input grad when dy1 given).
-void pool1_bwd(at::Tensor dp1, at::Tensor p1, at::Tensor idx1, at::Tensor y1, at::Tensor fstats1, at::Tensor g1,
-               double eps, at::Tensor dgamma1, at::Tensor dbeta1, at::Tensor bslab1, c10::optional<at::Tensor> dy1) {
-  DPA_CHECK_INPUT(dp1); DPA_CHECK_INPUT(p1); DPA_CHECK_INPUT(y1);
-  const int B = (int)y1.size(0);
-  TORCH_CHECK(y1.size(1) == 16 && y1.size(2) == 28 && y1.size(3) == 28);
-  with_t(dt_of(y1), [&](auto tag) {
+constexpr int kDgradSplit = 2;
+int64_t dgrad2_rows(int64_t B) { return B * kDgradSplit; }
+
+// [pool2/ReLU2/BN2 backward] -> conv2 data grad -> dp1 (+ BN1 partial sums rows).
+void conv2_dgrad(at::Tensor w2, at::Tensor y2, at::Tensor dp2, at::Tensor idx2, at::Tensor fstats2, at::Tensor gsum2,
+                 at::Tensor g2, double eps2, at::Tensor dp1, at::Tensor idx1, at::Tensor xh1, at::Tensor bslab1) {
+  DPA_CHECK_INPUT(y2); DPA_CHECK_INPUT(dp1);
+  const int B = (int)y2.size(0);
+  TORCH_CHECK(y2.size(1) == 32 && y2.size(2) == 14 && dp2.numel() == (int64_t)B * 32 * 49);
+  TORCH_CHECK(dp1.numel() == (int64_t)B * 16 * 196 && idx1.numel() == dp1.numel() && xh1.numel() == dp1.numel());
+  TORCH_CHECK(bslab1.numel() == dgrad2_rows(B) * 32, "BN1 partial-sum slab size");
+  if (B == 0) return;
+  with_t(dt_of(y2), [&](auto tag) {
     typedef decltype(tag) T;
-    hipLaunchKernelGGL((pool_bn_bwd_kernel<T, 16, 28, 28>), dim3(16), dim3(NTHR_PB), 0, cur_stream(), dptr<T>(dp1),
-                       dptr<T>(p1), idx1.data_ptr<uint8_t>(), dptr<T>(y1), fstats1.data_ptr<float>(),
-                       g1.data_ptr<float>(), (float)eps, B, dgamma1.data_ptr<float>(), dbeta1.data_ptr<float>(),
-                       bslab1.data_ptr<float>(), dy1.has_value() ? dptr<T>(*dy1) : nullptr);
+    BwdIn<T> bi = bwd_in<T>(dp2, idx2, y2, fstats2, gsum2, c10::nullopt, g2, eps2, 32, c10::nullopt, c10::nullopt);
+    BwdEpi<T> ep{idx1.data_ptr<uint8_t>(), dptr<T>(xh1), bslab1.data_ptr<float>()};
+    hipLaunchKernelGGL((cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1>), dim3(B * kDgradSplit), dim3(cb::NTHR), 0,
+                       cur_stream(), nullptr, w2.data_ptr<float>(), nullptr, dptr<T>(dp1), nullptr, nullptr, nullptr,
+                       kDgradSplit, PoolIn<T>{}, bi, ep);
+  });
+  DPA_CHECK_LAUNCH();
+}
+
+// [pool/ReLU/BN backward of the block whose conv is (CIN->COUT, HxW)] -> weight-grad partials.
+// layer 2: x = p1 [B,16,14,14], (y, dp, idx) = layer-2 tensors; layer 1: x = images, layer-1 tensors.
+void conv_wgrad_bn(at::Tensor x, at::Tensor y, at::Tensor dp, at::Tensor idx, at::Tensor fstats, at::Tensor gsum,
+                   c10::optional<at::Tensor> lsum, at::Tensor gamma, double eps, c10::optional<at::Tensor> dgamma,
+                   c10::optional<at::Tensor> dbeta, at::Tensor wslab) {
+  DPA_CHECK_INPUT(x); DPA_CHECK_INPUT(y);
+  const int B = (int)y.size(0);
+  const int cin = (int)x.size(1), cout = (int)y.size(1), H = (int)y.size(2);
+  TORCH_CHECK(x.scalar_type() == y.scalar_type());
+  if (B == 0) return;
+  with_t(dt_of(y), [&](auto tag) {
+    typedef decltype(tag) T;
+    BwdIn<T> bi = bwd_in<T>(dp, idx, y, fstats, gsum, lsum, gamma, eps, cout, dgamma, dbeta);
+    if (cin == 16 && cout == 32 && H == 14) {
+      TORCH_CHECK(wslab.numel() == (int64_t)B * (32 * 400 + 32), "wgrad slab size");
+      hipLaunchKernelGGL((cb::conv5x5_wgrad_kernel<T, 16, 32, 14, 14, 14, 2>), dim3(B), dim3(cb::NTHR), 0,
+                         cur_stream(), dptr<T>(x), nullptr, wslab.data_ptr<float>(), 1, bi);
+    } else if (cin == 1 && cout == 16 && H == 28) {
+      TORCH_CHECK(wslab.numel() == (int64_t)B * (16 * 25 + 16), "wgrad slab size");
+      hipLaunchKernelGGL((cb::conv5x5_wgrad_kernel<T, 1, 16, 28, 28, 28, 2>), dim3(B), dim3(cb::NTHR), 0,
+                         cur_stream(), dptr<T>(x), nullptr, wslab.data_ptr<float>(), 1, bi);
+    } else {
+      TORCH_CHECK(false, "fused wgrad: shape not instantiated");
+    }
   });
   DPA_CHECK_LAUNCH();
 }
@@ -410,7 +390,10 @@ void register_convnet_fused(pybind11::module& m) {
   s.def("conv2_fwd", &cnf::conv2_fwd);
   s.def("head_fwd", &cnf::head_fwd);
   s.def("head_bwd", &cnf::head_bwd);
-  s.def("pool1_bwd", &cnf::pool1_bwd);
+  s.def("head_bwd_lds", &cnf::head_bwd_lds);
+  s.def("dgrad2_rows", &cnf::dgrad2_rows);
+  s.def("conv2_dgrad", &cnf::conv2_dgrad);
+  s.def("conv_wgrad_bn", &cnf::conv_wgrad_bn);
 }
 
 }  // namespace dpa

@@ -132,75 +132,104 @@ __global__ void update_scale_kernel(float* scale, int* tracker, float* found_inf
 constexpr int FUSED_THR = 1024;
 constexpr int FUSED_U = 16;  // elements per thread per batch: 16 independent loads in flight
 
-// element prefix table in L.chunk_off (chunk_off[t] = first virtual index of tensor t)
-__device__ __forceinline__ int locate(const MTList& L, int64_t gi) {
-  int lo = 0, hi = L.n - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (L.chunk_off[mid] <= gi) lo = mid; else hi = mid - 1;
-  }
-  return lo;
-}
+constexpr int SEG_SHIFT = 6;                      // 64-element segments
+constexpr int64_t FUSED_MAX = (int64_t)1 << 18;   // elements handled by the single workgroup
+constexpr int MAX_SEG = (int)(FUSED_MAX >> SEG_SHIFT);
 
+// Tensor tables live in LDS: per-lane dynamic indexing of the by-value kernel
+// argument would be a chain of dependent global loads per element (measured:
+// 80 us for 29k elements); the segment map turns "which tensor holds flat
+// element gi" into one LDS read plus (rarely) a short forward scan.
 __global__ void __launch_bounds__(FUSED_THR)
 amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ tracker, float* __restrict__ found_inf,
                      float lr, float momentum, float dampening, float wd, int nesterov, int maximize, int first,
                      float growth, float backoff, int interval) {
+  __shared__ int64_t soff[MAXT + 1];
+  __shared__ float* sp0[MAXT];
+  __shared__ float* sp1[MAXT];
+  __shared__ float* sp2[MAXT];
+  __shared__ uint8_t seg[MAX_SEG];
+  const int tid = threadIdx.x;
+  const int n = L.n;
+  if (tid <= n) soff[tid] = L.chunk_off[tid];
+  if (tid < n) {
+    sp0[tid] = L.p0[tid];
+    sp1[tid] = L.p1[tid];
+    sp2[tid] = L.p2[tid];
+  }
+  __syncthreads();
+  const int64_t total = soff[n];
+  const int nseg = (int)((total + (1 << SEG_SHIFT) - 1) >> SEG_SHIFT);
+  for (int sg = tid; sg < nseg; sg += FUSED_THR) {
+    const int64_t e = (int64_t)sg << SEG_SHIFT;
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (soff[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    seg[sg] = (uint8_t)lo;
+  }
+  __syncthreads();
+  auto locate = [&](int64_t gi) {
+    int t = seg[gi >> SEG_SHIFT];
+    while (soff[t + 1] <= gi) ++t;
+    return t;
+  };
+
   const float inv = 1.f / scale[0];
-  const int64_t total = L.chunk_off[L.n];
   bool bad = false;
   for (int64_t base = 0; base < total; base += (int64_t)FUSED_U * FUSED_THR) {
     float v[FUSED_U];
 #pragma unroll
     for (int k = 0; k < FUSED_U; ++k) {
-      const int64_t gi = base + (int64_t)k * FUSED_THR + threadIdx.x;
+      const int64_t gi = base + (int64_t)k * FUSED_THR + tid;
       v[k] = 0.f;
       if (gi < total) {
-        const int t = locate(L, gi);
-        v[k] = L.p1[t][gi - L.chunk_off[t]];
+        const int t = locate(gi);
+        v[k] = sp1[t][gi - soff[t]];
       }
     }
 #pragma unroll
     for (int k = 0; k < FUSED_U; ++k) bad |= !isfinite(v[k]);
   }
   bad = __syncthreads_or(bad);
+  const bool use_buf = momentum != 0.f && !first;
   for (int64_t base = 0; base < total; base += (int64_t)FUSED_U * FUSED_THR) {
     float gv[FUSED_U], pv[FUSED_U], bv[FUSED_U];
-    int tt[FUSED_U];
-    int64_t oo[FUSED_U];
+    int tt[FUSED_U], oo[FUSED_U];
 #pragma unroll
     for (int k = 0; k < FUSED_U; ++k) {
-      const int64_t gi = base + (int64_t)k * FUSED_THR + threadIdx.x;
+      const int64_t gi = base + (int64_t)k * FUSED_THR + tid;
       tt[k] = -1;
       if (gi < total) {
-        const int t = locate(L, gi);
-        const int64_t o = gi - L.chunk_off[t];
+        const int t = locate(gi);
+        const int o = (int)(gi - soff[t]);
         tt[k] = t;
         oo[k] = o;
-        gv[k] = L.p1[t][o];
-        pv[k] = L.p0[t][o];
-        bv[k] = (momentum != 0.f && !first) ? L.p2[t][o] : 0.f;
+        gv[k] = sp1[t][o];
+        pv[k] = sp0[t][o];
+        bv[k] = use_buf ? sp2[t][o] : 0.f;
       }
     }
 #pragma unroll
     for (int k = 0; k < FUSED_U; ++k) {
-      if (tt[k] < 0) continue;
       const int t = tt[k];
-      const int64_t o = oo[k];
+      if (t < 0) continue;
+      const int o = oo[k];
       const float g = gv[k] * inv;
-      L.p1[t][o] = g;
+      sp1[t][o] = g;
       if (bad) continue;
       float d = maximize ? -g : g;
       if (wd != 0.f) d += wd * pv[k];
       if (momentum != 0.f) {
         const float b = first ? d : momentum * bv[k] + (1.f - dampening) * d;
-        L.p2[t][o] = b;
+        sp2[t][o] = b;
         d = nesterov ? d + momentum * b : b;
       }
-      L.p0[t][o] = pv[k] - lr * d;
+      sp0[t][o] = pv[k] - lr * d;
     }
   }
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
     found_inf[0] = 0.f;
     if (bad) {
       scale[0] = scale[0] * backoff;
@@ -315,7 +344,9 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
     L.p1[i] = grads[i].data_ptr<float>();
     L.p2[i] = bufs.empty() ? nullptr : bufs[i].data_ptr<float>();
     L.chunk_off[i + 1] = L.chunk_off[i] + L.numel[i];  // element prefix (not chunks) for this kernel
+    TORCH_CHECK(momentum == 0.0 || !bufs.empty(), "fused AMP-SGD: momentum needs buffers");
   }
+  TORCH_CHECK(L.chunk_off[L.n] <= FUSED_MAX, "fused AMP-SGD handles at most ", FUSED_MAX, " elements");
   hipLaunchKernelGGL(amp_sgd_fused_kernel, dim3(1), dim3(FUSED_THR), 0, cur_stream(), L, scale.data_ptr<float>(),
                      tracker.data_ptr<int>(), found_inf.data_ptr<float>(), (float)lr, (float)momentum,
                      (float)dampening, (float)wd, (int)nesterov, (int)maximize, (int)first, (float)growth,

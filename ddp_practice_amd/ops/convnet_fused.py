@@ -5,14 +5,16 @@ removes launches that exist only because torch runs one module at a time:
 
   forward  (train): conv1(+BN1 sums) | BN1-ReLU-pool1 -> conv2 (+BN2 sums) | BN2-ReLU-pool2 -> fc
                     = 3 launches for the model (per-layer ops: 6, torch: ~14 + host syncs)
-  backward:         fc-bwd + pool2/ReLU2 routing + BN2 sums + BN2 input grad | conv2 wgrad | conv2 dgrad
-                    | conv2 grad sums | pool1/ReLU1 routing + BN1 sums + BN1 input grad | conv1 wgrad
-                    | conv1 grad sums = 7 launches
+  backward:         fc bwd (+BN2 sums) | BN2 bwd -> conv2 dgrad (+BN1 sums) | BN2 bwd -> conv2 wgrad
+                    | BN1 bwd -> conv1 wgrad | weight-grad sums = 5 launches
+                    (per-layer ops: 10, torch: ~20)
 
-With SyncBN (``comm`` active) the per-workgroup forward partial sums and the
-per-channel backward sums are all-reduced between the kernels (one
-collective each), and the BN input-gradient steps run as their own launches
-after the all-reduce.  Parameter gradients are views of one output buffer.
+Every BatchNorm backward is applied while staging the operand of the next
+GEMM (the conv-output gradient never exists in HBM), and its reductions are
+emitted by the kernel that produced the pooled gradient.  With SyncBN
+(``comm`` active) the partial sums are all-reduced between the kernels (one
+small collective each: 2 forward, 2 backward).  Parameter gradients are views
+of one output buffer.
 """
 from __future__ import annotations
 
@@ -64,24 +66,28 @@ class ConvNetFn(torch.autograd.Function):
         if training:
             fslab1 = torch.empty(cb.fwd_rows(1, 16, 28, 28, B) * cb.fslab_row(16), dtype=torch.float32, device=dev)
             fslab2 = torch.empty(cb.fwd_rows(16, 32, 14, 14, B) * cb.fslab_row(32), dtype=torch.float32, device=dev)
+            # pooled maps, argmax|relu index and xhat at the argmax of both blocks (for the backward)
             p1 = torch.empty((B, 16, 14, 14), dtype=cdtype, device=dev)
             idx1 = torch.empty((B, 16, 14, 14), dtype=torch.uint8, device=dev)
+            xh1 = torch.empty((B, 16, 14, 14), dtype=cdtype, device=dev)
             p2 = torch.empty((B, 32 * 49), dtype=cdtype, device=dev)
             idx2 = torch.empty((B, 32 * 49), dtype=torch.uint8, device=dev)
+            xh2 = torch.empty((B, 32 * 49), dtype=cdtype, device=dev)
             cb.conv_fwd(x, w1, b1, y1, fslab1, fstats1, rm1)
             if sync:
                 comm.all_reduce_(fslab1)
             cn.conv2_fwd(y1, fslab1, fstats1, g1, be1, rm1, rv1, nbt1, m1, e1, True, w2, b2, y2, fslab2, fstats2,
-                         rm2, p1, idx1)
+                         rm2, p1, idx1, xh1)
             if sync:
                 comm.all_reduce_(fslab2)
-            cn.head_fwd(y2, fslab2, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, True, wfc, bfc, logits, p2, idx2)
-            ctx.save_for_backward(x, w2, wfc, g1, g2, y1, p1, idx1, fstats1, y2, p2, idx2, fstats2)
+            cn.head_fwd(y2, fslab2, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, True, wfc, bfc, logits, p2, idx2, xh2)
+            ctx.save_for_backward(x, w2, wfc, g1, g2, y1, p1, idx1, xh1, fstats1, y2, p2, idx2, xh2, fstats2)
         else:
             cb.conv_fwd(x, w1, b1, y1)
             cn.conv2_fwd(y1, None, fstats1, g1, be1, rm1, rv1, nbt1, m1, e1, False, w2, b2, y2, None, fstats2, rm2,
-                         None, None)
-            cn.head_fwd(y2, None, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, False, wfc, bfc, logits, None, None)
+                         None, None, None)
+            cn.head_fwd(y2, None, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, False, wfc, bfc, logits, None, None,
+                        None)
         ctx.training = training
         ctx.sync = sync
         ctx.comm = comm
@@ -94,7 +100,7 @@ class ConvNetFn(torch.autograd.Function):
         if not ctx.training:
             raise RuntimeError("ConvNetFn: backward through an eval-mode forward is not supported")
         cb, cn = _mods()
-        x, w2, wfc, g1, g2, y1, p1, idx1, fstats1, y2, p2, idx2, fstats2 = ctx.saved_tensors
+        x, w2, wfc, g1, g2, y1, p1, idx1, xh1, fstats1, y2, p2, idx2, xh2, fstats2 = ctx.saved_tensors
         e1, e2 = ctx.eps
         comm, sync = ctx.comm, ctx.sync
         dl = dlogits.to(y2.dtype).contiguous()
@@ -103,41 +109,31 @@ class ConvNetFn(torch.autograd.Function):
         s_w1, s_w2, s_wfc = ctx.shapes
         n_w1, n_w2, n_wfc = s_w1.numel(), s_w2.numel(), s_wfc.numel()
         N = s_wfc[0]
-        # one output buffer for every parameter gradient (views handed to autograd)
+        # one output buffer for every parameter gradient (views handed to autograd);
+        # [dW1 | db1] and [dW2 | db2] are the rows of the two weight-grad slabs
         sizes = [n_w1, 16, 16, 16, n_w2, 32, 32, 32, n_wfc, N]
         out = torch.empty(sum(sizes), dtype=torch.float32, device=dev)
-        views = list(out.split(sizes))
-        dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, dwfc, dbfc = views
-        # --- fc + pool2/ReLU2 + BN2
-        bslab2 = torch.empty(2 * 32, dtype=torch.float32, device=dev)
-        dy2 = torch.empty_like(y2)
-        if not sync:
-            cn.head_bwd(dl, wfc, p2, idx2, y2, fstats2, g2, e2, dwfc, dbfc, dg2, dbe2, bslab2, None, dy2)
-        else:
-            dp2 = torch.empty_like(p2)
-            cn.head_bwd(dl, wfc, p2, idx2, y2, fstats2, g2, e2, dwfc, dbfc, dg2, dbe2, bslab2, dp2, None)
-            gslab2 = comm.all_reduce(bslab2)
-            cb.bwd_elemt(dp2.view(B, 32, 7, 7), p2.view(B, 32, 7, 7), idx2.view(B, 32, 7, 7), y2, fstats2, gslab2,
-                         g2, e2, dy2)
-        # --- conv2: weight grad (per-image partials) and data grad
-        wslab2 = torch.empty(cb.wgrad_rows(16, 32, 14, 14, B) * (n_w2 + 32), dtype=torch.float32, device=dev)
-        cb.conv_wgrad(p1, dy2, wslab2)
+        dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, dwfc, dbfc = out.split(sizes)
+        f32 = dict(dtype=torch.float32, device=dev)
+        # 1. fc backward -> dp2, fc grads, BN2 sums (complete per channel on this rank)
+        bsum2 = torch.empty(64, **f32)
+        dp2 = torch.empty_like(p2)
+        cn.head_bwd(dl, wfc, p2, idx2, xh2, dwfc, dbfc, dg2, dbe2, bsum2, dp2)
+        gsum2 = comm.all_reduce(bsum2) if sync else bsum2
+        # 2. BN2 bwd -> conv2 dgrad -> dp1 (+ BN1 partial sums)
         dp1 = torch.empty((B, 16, 14, 14), dtype=y1.dtype, device=dev)
-        cb.conv_dgrad(dy2, w2, dp1)
-        cb.slab_reduce(wslab2, n_w2 + 32, out.narrow(0, n_w1 + 48, n_w2 + 32))
-        # --- pool1/ReLU1 + BN1
-        bslab1 = torch.empty(2 * 16, dtype=torch.float32, device=dev)
-        dy1 = torch.empty_like(y1)
-        if not sync:
-            cn.pool1_bwd(dp1, p1, idx1, y1, fstats1, g1, e1, dg1, dbe1, bslab1, dy1)
-        else:
-            cn.pool1_bwd(dp1, p1, idx1, y1, fstats1, g1, e1, dg1, dbe1, bslab1, None)
-            gslab1 = comm.all_reduce(bslab1)
-            cb.bwd_elemt(dp1, p1, idx1, y1, fstats1, gslab1, g1, e1, dy1)
-        # --- conv1 weight grad
-        wslab1 = torch.empty(cb.wgrad_rows(1, 16, 28, 28, B) * (n_w1 + 16), dtype=torch.float32, device=dev)
-        cb.conv_wgrad(x, dy1, wslab1)
-        cb.slab_reduce(wslab1, n_w1 + 16, out.narrow(0, 0, n_w1 + 16))
+        bslab1 = torch.empty(cn.dgrad2_rows(B) * 32, **f32)
+        cn.conv2_dgrad(w2, y2, dp2, idx2, fstats2, gsum2, g2, e2, dp1, idx1, xh1, bslab1)
+        # 3. BN2 bwd -> conv2 wgrad partials (independent of 2)
+        wslab2 = torch.empty(B * (n_w2 + 32), **f32)
+        cn.conv_wgrad_bn(p1, y2, dp2, idx2, fstats2, gsum2, None, g2, e2, None, None, wslab2)
+        # 4. BN1 bwd -> conv1 wgrad partials (+ dgamma1 / dbeta1 from the local sums)
+        gslab1 = comm.all_reduce(bslab1) if sync else bslab1
+        wslab1 = torch.empty(B * (n_w1 + 16), **f32)
+        cn.conv_wgrad_bn(x, y1, dp1, idx1, fstats1, gslab1, bslab1 if sync else None, g1, e1, dg1, dbe1, wslab1)
+        # 5. weight-grad partial sums -> [dW1 | db1], [dW2 | db2]
+        cb.slab_reduce(wslab1, n_w1 + 16, out.narrow(0, 0, n_w1 + 16), wslab2, n_w2 + 32,
+                       out.narrow(0, n_w1 + 48, n_w2 + 32))
         return (None, dw1.view(s_w1), db1, dg1, dbe1, dw2.view(s_w2), db2, dg2, dbe2, dwfc.view(s_wfc), dbfc,
                 None, None, None, None, None, None)
 
