@@ -103,7 +103,10 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
         param_offset_[i] = off;
         bk.params.push_back(i);
         bk.offsets.push_back(off);
-        off += params_[i].numel();
+        // 16-byte aligned views: the grads stay valid float4 operands for the
+        // vectorised optimizer kernels (the pad elements stay zero)
+        const int64_t al = std::max<int64_t>(1, 16 / (int64_t)params_[i].element_size());
+        off += (params_[i].numel() + al - 1) / al * al;
       }
       bk.flat = at::zeros({off}, params_[buckets[b].empty() ? 0 : buckets[b][0]].options().requires_grad(false));
       buckets_.push_back(std::move(bk));

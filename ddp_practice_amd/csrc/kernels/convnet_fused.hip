@@ -86,17 +86,27 @@ head_fwd_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__ 
     }
   }
   const int lane = tid & 63, wv = tid >> 6;
+  // fc rows in chunks of NC outputs: every load of a chunk is issued before
+  // its first FMA (rows past N are clamped to N-1 and discarded)
+  constexpr int NC = 8;
+  for (int n0 = 0; n0 < N; n0 += NC) {  // uniform
+    float wr[NC][IT];
 #pragma unroll
-  for (int n = 0; n < NMAX; ++n) {
-    if (n < N) {  // uniform
-      float a = 0.f;
+    for (int j = 0; j < NC; ++j) {
+      const int n = min(n0 + j, N - 1);
 #pragma unroll
       for (int i = 0; i < IT; ++i) {
-        const int k = tid + i * HF;
-        if (k < K) a += pf[i] * wfc[(size_t)n * K + k];
+        const int k = min(tid + i * HF, K - 1);
+        wr[j][i] = wfc[(size_t)n * K + k];
       }
+    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      float a = 0.f;
+#pragma unroll
+      for (int i = 0; i < IT; ++i) a += pf[i] * wr[j][i];  // pf = 0 past K
       a = wave_sum(a);
-      if (lane == 0) red[wv][n] = a;
+      if (lane == 0 && n0 + j < N) red[wv][n0 + j] = a;
     }
   }
   __syncthreads();

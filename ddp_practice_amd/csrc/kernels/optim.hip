@@ -130,38 +130,42 @@ __global__ void update_scale_kernel(float* scale, int* tracker, float* found_inf
 // grads are finite, phase 3 updates scale / growth tracker and re-arms
 // found_inf.  p0 = param, p1 = grad, p2 = momentum buffer (or null).
 constexpr int FUSED_THR = 1024;
-constexpr int FUSED_U = 16;  // elements per thread per batch: 16 independent loads in flight
-
-constexpr int SEG_SHIFT = 6;                      // 64-element segments
+constexpr int FUSED_U = 4;                        // float4 granules per thread per pass
+constexpr int SEG_SHIFT = 4;                      // 16-granule segments
 constexpr int64_t FUSED_MAX = (int64_t)1 << 18;   // elements handled by the single workgroup
-constexpr int MAX_SEG = (int)(FUSED_MAX >> SEG_SHIFT);
+constexpr int MAX_SEG = (int)((FUSED_MAX / 4) >> SEG_SHIFT) + MAXT;
 
-// Tensor tables live in LDS: per-lane dynamic indexing of the by-value kernel
-// argument would be a chain of dependent global loads per element (measured:
-// 80 us for 29k elements); the segment map turns "which tensor holds flat
-// element gi" into one LDS read plus (rarely) a short forward scan.
+// The flat index space is in float4 granules; tensor t owns ceil(numel/4)
+// granules starting at chunk_off[t] (every pointer 16-B aligned, checked on the
+// host), so a granule never straddles two tensors and the common case is one
+// 16-B load per operand.  Tensor tables live in LDS: per-lane dynamic indexing
+// of the by-value kernel argument is a chain of dependent global loads per
+// element (measured: 80 us for 29k elements); the segment map turns "which
+// tensor holds granule gi" into one LDS read plus (rarely) a short scan.
 __global__ void __launch_bounds__(FUSED_THR)
 amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ tracker, float* __restrict__ found_inf,
                      float lr, float momentum, float dampening, float wd, int nesterov, int maximize, int first,
                      float growth, float backoff, int interval) {
-  __shared__ int64_t soff[MAXT + 1];
+  __shared__ int soff[MAXT + 1];
+  __shared__ int snum[MAXT];
   __shared__ float* sp0[MAXT];
   __shared__ float* sp1[MAXT];
   __shared__ float* sp2[MAXT];
   __shared__ uint8_t seg[MAX_SEG];
   const int tid = threadIdx.x;
   const int n = L.n;
-  if (tid <= n) soff[tid] = L.chunk_off[tid];
+  if (tid <= n) soff[tid] = (int)L.chunk_off[tid];
   if (tid < n) {
+    snum[tid] = (int)L.numel[tid];
     sp0[tid] = L.p0[tid];
     sp1[tid] = L.p1[tid];
     sp2[tid] = L.p2[tid];
   }
   __syncthreads();
-  const int64_t total = soff[n];
-  const int nseg = (int)((total + (1 << SEG_SHIFT) - 1) >> SEG_SHIFT);
+  const int total = soff[n];
+  const int nseg = (total + (1 << SEG_SHIFT) - 1) >> SEG_SHIFT;
   for (int sg = tid; sg < nseg; sg += FUSED_THR) {
-    const int64_t e = (int64_t)sg << SEG_SHIFT;
+    const int e = sg << SEG_SHIFT;
     int lo = 0, hi = n - 1;
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
@@ -170,63 +174,76 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
     seg[sg] = (uint8_t)lo;
   }
   __syncthreads();
-  auto locate = [&](int64_t gi) {
+  auto locate = [&](int gi) {
     int t = seg[gi >> SEG_SHIFT];
     while (soff[t + 1] <= gi) ++t;
     return t;
   };
+  auto load4 = [](const float* p, int rem) {
+    if (rem >= 4) return *reinterpret_cast<const f32x4*>(p);
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < rem; ++j) v[j] = p[j];
+    return v;
+  };
+  auto store4 = [](float* p, int rem, f32x4 v) {
+    if (rem >= 4) { *reinterpret_cast<f32x4*>(p) = v; return; }
+    for (int j = 0; j < rem; ++j) p[j] = v[j];
+  };
 
   const float inv = 1.f / scale[0];
   bool bad = false;
-  for (int64_t base = 0; base < total; base += (int64_t)FUSED_U * FUSED_THR) {
-    float v[FUSED_U];
+  for (int base = 0; base < total; base += FUSED_U * FUSED_THR) {
+    f32x4 v[FUSED_U];
 #pragma unroll
     for (int k = 0; k < FUSED_U; ++k) {
-      const int64_t gi = base + (int64_t)k * FUSED_THR + tid;
-      v[k] = 0.f;
+      const int gi = base + k * FUSED_THR + tid;
+      v[k] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (gi < total) {
         const int t = locate(gi);
-        v[k] = sp1[t][gi - soff[t]];
+        const int o = (gi - soff[t]) * 4;
+        v[k] = load4(sp1[t] + o, snum[t] - o);
       }
     }
 #pragma unroll
-    for (int k = 0; k < FUSED_U; ++k) bad |= !isfinite(v[k]);
+    for (int k = 0; k < FUSED_U; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bad |= !isfinite(v[k][j]);
   }
   bad = __syncthreads_or(bad);
   const bool use_buf = momentum != 0.f && !first;
-  for (int64_t base = 0; base < total; base += (int64_t)FUSED_U * FUSED_THR) {
-    float gv[FUSED_U], pv[FUSED_U], bv[FUSED_U];
+  for (int base = 0; base < total; base += FUSED_U * FUSED_THR) {
+    f32x4 gv[FUSED_U], pv[FUSED_U], bv[FUSED_U];
     int tt[FUSED_U], oo[FUSED_U];
 #pragma unroll
     for (int k = 0; k < FUSED_U; ++k) {
-      const int64_t gi = base + (int64_t)k * FUSED_THR + tid;
+      const int gi = base + k * FUSED_THR + tid;
       tt[k] = -1;
       if (gi < total) {
         const int t = locate(gi);
-        const int o = (int)(gi - soff[t]);
+        const int o = (gi - soff[t]) * 4, rem = snum[t] - o;
         tt[k] = t;
         oo[k] = o;
-        gv[k] = sp1[t][o];
-        pv[k] = sp0[t][o];
-        bv[k] = use_buf ? sp2[t][o] : 0.f;
+        gv[k] = load4(sp1[t] + o, rem);
+        pv[k] = load4(sp0[t] + o, rem);
+        bv[k] = use_buf ? load4(sp2[t] + o, rem) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
 #pragma unroll
     for (int k = 0; k < FUSED_U; ++k) {
       const int t = tt[k];
       if (t < 0) continue;
-      const int o = oo[k];
-      const float g = gv[k] * inv;
-      sp1[t][o] = g;
+      const int o = oo[k], rem = snum[t] - o;
+      const f32x4 g = gv[k] * inv;
+      store4(sp1[t] + o, rem, g);
       if (bad) continue;
-      float d = maximize ? -g : g;
+      f32x4 d = maximize ? -g : g;
       if (wd != 0.f) d += wd * pv[k];
       if (momentum != 0.f) {
-        const float b = first ? d : momentum * bv[k] + (1.f - dampening) * d;
-        sp2[t][o] = b;
-        d = nesterov ? d + momentum * b : b;
+        const f32x4 bb = first ? d : momentum * bv[k] + (1.f - dampening) * d;
+        store4(sp2[t] + o, rem, bb);
+        d = nesterov ? d + momentum * bb : bb;
       }
-      sp0[t][o] = pv[k] - lr * d;
+      store4(sp0[t] + o, rem, pv[k] - lr * d);
     }
   }
   if (tid == 0) {
@@ -343,10 +360,12 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
     L.p0[i] = params[i].data_ptr<float>();
     L.p1[i] = grads[i].data_ptr<float>();
     L.p2[i] = bufs.empty() ? nullptr : bufs[i].data_ptr<float>();
-    L.chunk_off[i + 1] = L.chunk_off[i] + L.numel[i];  // element prefix (not chunks) for this kernel
+    L.chunk_off[i + 1] = L.chunk_off[i] + (L.numel[i] + 3) / 4;  // float4-granule prefix for this kernel
     TORCH_CHECK(momentum == 0.0 || !bufs.empty(), "fused AMP-SGD: momentum needs buffers");
+    auto al = [](const float* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    TORCH_CHECK(al(L.p0[i]) && al(L.p1[i]) && al(L.p2[i]), "fused AMP-SGD needs 16-byte aligned tensors");
   }
-  TORCH_CHECK(L.chunk_off[L.n] <= FUSED_MAX, "fused AMP-SGD handles at most ", FUSED_MAX, " elements");
+  TORCH_CHECK(L.chunk_off[L.n] * 4 <= FUSED_MAX, "fused AMP-SGD handles at most ", FUSED_MAX, " elements");
   hipLaunchKernelGGL(amp_sgd_fused_kernel, dim3(1), dim3(FUSED_THR), 0, cur_stream(), L, scale.data_ptr<float>(),
                      tracker.data_ptr<int>(), found_inf.data_ptr<float>(), (float)lr, (float)momentum,
                      (float)dampening, (float)wd, (int)nesterov, (int)maximize, (int)first, (float)growth,

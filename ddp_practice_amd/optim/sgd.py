@@ -98,8 +98,12 @@ class SGD(Optimizer):
             return False
         if sum(p.numel() for p in ps) > self.FUSED_AMP_MAX_NUMEL:
             return False
+        def aligned(t):  # the kernel moves float4 granules
+            return t is None or t.data_ptr() % 16 == 0
+
         return all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and p.grad.dtype == torch.float32
-                   and p.grad.is_contiguous() for p in ps)
+                   and p.grad.is_contiguous() and aligned(p) and aligned(p.grad)
+                   and aligned(self.state.get(p, {}).get("momentum_buffer")) for p in ps)
 
     @torch.no_grad()
     def fused_amp_step(self, scale, tracker, found_inf, growth, backoff, interval):

@@ -35,48 +35,48 @@ def _torch_fwd(m, x):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("B,N", [(32, 10), (7, 10), (100, 10), (16, 64)])
 def test_convnet_fused_fwd_bwd(C, dtype, B, N):
+    """Error of the fused op vs a float64 reference must be within 2x of torch's
+    own error at the same precision (fp32 eager, or autocast) plus a small floor."""
     from ddp_practice_amd.ops import convnet_fused
 
     m = _model(n=N)
-    mr, ml = copy.deepcopy(m), copy.deepcopy(m)
+    m64, mt = copy.deepcopy(m).double(), copy.deepcopy(m)
     g = torch.Generator(device="cpu").manual_seed(3)
     x = torch.rand(B, 1, 28, 28, generator=g).to(DEV)
     assert convnet_fused.supported(m, x)
     out = convnet_fused.convnet_forward(m, x, cdtype=dtype)
-    ref = _torch_fwd(mr, x)
-    lp = dtype != torch.float32
-    if lp:
+    ref = _torch_fwd(m64, x.double())
+    if dtype == torch.float32:
+        ref_t = _torch_fwd(mt, x)
+    else:
         with torch.autocast("cuda", dtype=dtype):
-            ref_l = _torch_fwd(ml, x)
+            ref_t = _torch_fwd(mt, x)
 
-    def bound(a, r, l, floor):
+    def bound(a, r, t, floor, what):
         e = _rel(a, r)
-        lim = max(2.0 * _rel(l, r), floor) if lp else floor
-        assert e < lim, (e, lim)
+        lim = max(2.0 * _rel(t, r), floor)
+        assert e < lim, (what, e, lim)
 
+    lp = dtype != torch.float32
     assert out.dtype == dtype and out.shape == (B, N)
-    bound(out, ref, ref_l if lp else None, 3e-5 if not lp else 5e-3)
-    st = 1e-4 if not lp else 1e-2
-    for bn, bnr in ((m.layer1[1], mr.layer1[1]), (m.layer2[1], mr.layer2[1])):
-        torch.testing.assert_close(bn.running_mean, bnr.running_mean, rtol=st, atol=st)
-        torch.testing.assert_close(bn.running_var, bnr.running_var, rtol=st, atol=st)
+    bound(out, ref, ref_t, 1e-5 if not lp else 2e-3, "logits")
+    for bn, bnr, bnt in ((m.layer1[1], m64.layer1[1], mt.layer1[1]), (m.layer2[1], m64.layer2[1], mt.layer2[1])):
+        bound(bn.running_mean, bnr.running_mean, bnt.running_mean, 1e-5 if not lp else 2e-3, "running_mean")
+        bound(bn.running_var, bnr.running_var, bnt.running_var, 1e-5 if not lp else 2e-3, "running_var")
         assert int(bn.num_batches_tracked) == 1
     go = torch.randn(ref.shape, generator=g).to(DEV)
-    ref.backward(go)
+    ref.backward(go.double())
     out.backward(go.to(dtype))
-    if lp:
-        ref_l.backward(go.to(ref_l.dtype))
-    fl = 1e-4 if not lp else 5e-3
-    named_l = dict(ml.named_parameters()) if lp else {}
-    for (n, p), (_, q) in zip(m.named_parameters(), mr.named_parameters()):
+    ref_t.backward(go.to(ref_t.dtype))
+    named_t = dict(mt.named_parameters())
+    for (n, p), (_, q) in zip(m.named_parameters(), m64.named_parameters()):
         assert p.grad is not None and p.grad.shape == p.shape, n
-        if n.endswith("0.bias"):  # conv bias grad is ~0 analytically (BN follows)
-            lim = 2.0 * (named_l[n].grad - q.grad).abs().max().item() + 1e-2 if lp else 2e-3
-            assert (p.grad - q.grad).abs().max().item() < lim, n
+        if n.endswith("0.bias"):  # conv bias grad is ~0 analytically (BN follows): absolute bound
+            e = (p.grad.double() - q.grad).abs().max().item()
+            lim = 2.0 * (named_t[n].grad.double() - q.grad).abs().max().item() + (1e-4 if not lp else 1e-2)
+            assert e < lim, (n, e, lim)
             continue
-        e = _rel(p.grad, q.grad)
-        lim = max(2.0 * _rel(named_l[n].grad, q.grad), fl) if lp else fl
-        assert e < lim, (n, e, lim)
+        bound(p.grad, q.grad, named_t[n].grad, 1e-5 if not lp else 2e-3, n)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
@@ -92,7 +92,7 @@ def test_convnet_fused_eval(C, dtype):
 
 
 def test_convnet_fused_matches_layer_path(C):
-    """fp32: whole-model op == per-layer ops (same kernels, same reduction order)."""
+    """fp32: whole-model op == per-layer ops (same math, different reduction order)."""
     m = _model()
     ml = copy.deepcopy(m)
     ml.fused = "layer"
@@ -105,7 +105,7 @@ def test_convnet_fused_matches_layer_path(C):
                 for p in mod.parameters():
                     p.add_(p.grad, alpha=-0.1)
     for (n, p), (_, q) in zip(m.state_dict().items(), ml.state_dict().items()):
-        torch.testing.assert_close(p.float(), q.float(), rtol=2e-5, atol=2e-5, msg=n)
+        torch.testing.assert_close(p.float(), q.float(), rtol=1e-4, atol=1e-4, msg=n)
 
 
 def test_convnet_model_dispatches_fused(C):

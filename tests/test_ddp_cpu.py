@@ -15,7 +15,10 @@ def test_ddp_syncbn_matches_single_process_full_batch():
     keys = outs[0]["keys"]
     assert keys[0] == "module.layer1.0.weight" and len(keys) == 16
     assert "module.layer2.1.running_var" in keys and "module.fc.bias" in keys
-    assert outs[0]["buckets"] == [29034 * 4]
+    # one bucket like torch's (29,034 floats); every param view starts 16-B aligned,
+    # which pads fc.bias (10 -> 12) and the 5x5 bias of 16/32 floats not at all
+    sizes = [10, 15680, 32, 32, 32, 12800, 16, 16, 16, 400]
+    assert outs[0]["buckets"] == [sum((n + 3) // 4 * 4 for n in sizes) * 4]
 
 
 def test_ddp_no_sync_and_find_unused():
