@@ -19,6 +19,36 @@ import torch
 
 from .._ext import load as _load_ext
 
+_ACTIVE = None  # weakref to the GradScaler whose scale native losses pre-apply
+
+
+def active_scale(device: torch.device):
+    """Scale tensor of the active GradScaler on ``device`` (or None).
+
+    Native losses (ops/head.py cross_entropy) use it to write the gradient of
+    the *scaled* loss in their forward kernel; ``GradScaler.scale`` then hands
+    out that pre-scaled loss and its fast backward needs neither the
+    ``loss * scale`` multiply nor the loss-backward launch.
+    """
+    sc = _ACTIVE() if _ACTIVE is not None else None
+    if sc is None or not sc._enabled or sc._scale is None or sc._scale.device != device:
+        return None
+    return sc._scale
+
+
+class _ScaledLossFn(torch.autograd.Function):
+    """scale * loss whose value the loss kernel already produced (no launch)."""
+
+    @staticmethod
+    def forward(ctx, loss, scale, ce_node):
+        ctx.save_for_backward(scale)
+        return ce_node.scaled  # a view of the loss kernel's output buffer: no launch
+
+    @staticmethod
+    def backward(ctx, g):
+        (scale,) = ctx.saved_tensors
+        return g * scale.view(()).to(g.dtype), None, None
+
 
 def _native_ok(t: torch.Tensor) -> bool:
     return t.is_cuda
@@ -51,6 +81,11 @@ class GradScaler:
 
     # ------------------------------------------------------------------ state
     def _lazy_init(self, dev: torch.device):
+        global _ACTIVE
+        if self._enabled and dev.type == "cuda":
+            import weakref
+
+            _ACTIVE = weakref.ref(self)
         if self._scale is None:
             self._scale = torch.full((1,), self._init_scale, dtype=torch.float32, device=dev)
             self._growth_tracker = torch.full((1,), getattr(self, "_pending_tracker", 0), dtype=torch.int32,
@@ -81,6 +116,25 @@ class GradScaler:
             self._lazy_init(outputs.device)
             # 0-d scale: a 0-d loss stays 0-d, so backward needs no sum-to-shape reduction
             s0 = self._scale.to(outputs.device, non_blocking=True).view(())
+            ce = getattr(outputs, "_dpa_ce", None)
+            if ce is not None and ce[1] is self._scale and outputs.requires_grad and outputs.dim() == 0:
+                # native CE loss: its kernel already wrote loss*scale and d(scale*loss)/dlogits
+                node = ce[0]
+                scaled = _ScaledLossFn.apply(outputs, self._scale, node)
+                base = outputs
+
+                def _backward_ce(gradient=None, retain_graph=None, create_graph=False, inputs=None):
+                    if gradient is None and not create_graph:
+                        node.token.seeded = True
+                        try:
+                            torch.autograd.backward(base, grad_tensors=s0, retain_graph=retain_graph, inputs=inputs)
+                        finally:
+                            node.token.seeded = False
+                    else:
+                        torch.Tensor.backward(scaled, gradient, retain_graph, create_graph, inputs)
+
+                scaled.backward = _backward_ce
+                return scaled
             scaled = outputs * s0
             if outputs.requires_grad and outputs.dim() == 0 and outputs.is_cuda:
                 # d(scale*loss)/dθ = scale * dloss/dθ: seed the loss's own backward

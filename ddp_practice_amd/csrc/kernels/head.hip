@@ -163,64 +163,94 @@ linear_bwd_kernel(const T* __restrict__ dout, const T* __restrict__ x, const flo
 }
 
 // Cross-entropy (mean over non-ignored rows) of logits [B][N] (storage T,
-// math f32).  Writes loss[0] and dlog[b][n] = (softmax - onehot)/count, f32.
-// One workgroup, one wave per row (rows strided over waves).
-template <typename T>
-__global__ void __launch_bounds__(1024)
+// math f32).  Writes loss[0] and dlog[b][n] = (softmax - onehot)/count (f32).
+// When `scale` is given (an active GradScaler) it also writes loss[1] =
+// loss * scale and dls[b][n] = dlog * scale in T: the gradient of the scaled
+// loss that the backward then returns without a launch (ops/head.py).
+// One workgroup; a GL-lane group per row (GL = 16 for N <= 16), so 64 rows
+// are processed per pass with group-local shuffles only.
+template <int GL>
+__device__ __forceinline__ float group_max(float v) {
+#pragma unroll
+  for (int o = GL / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+template <int GL>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = GL / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+constexpr int CE_THR = 1024;
+
+template <typename T, int GL>
+__global__ void __launch_bounds__(CE_THR)
 ce_fwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ target, float* __restrict__ loss,
-              float* __restrict__ dlog, int B, int N, int64_t ignore_index, float smoothing) {
-  __shared__ float red[2 * 16];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  float lsum = 0.f, cnt = 0.f;
-  for (int b = wv; b < B; b += nw) {
-    const T* row = logits + (size_t)b * N;
-    const int64_t t = target[b];
-    float mx = -INFINITY;
-    for (int n = lane; n < N; n += 64) mx = fmaxf(mx, Cvt<T>::to_f(row[n]));
-    mx = wave_max(mx);
-    float se = 0.f, sx = 0.f;
-    for (int n = lane; n < N; n += 64) {
+              float* __restrict__ dlog, int B, int N, int64_t ignore_index, float smoothing,
+              const float* __restrict__ scale, T* __restrict__ dls) {
+  constexpr int RPP = CE_THR / GL;  // rows per pass
+  __shared__ float red[CE_THR / 64];
+  __shared__ int cnt_s;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int gl = tid % GL, gr = tid / GL;
+  if (tid == 0) cnt_s = 0;
+  __syncthreads();
+  int c = 0;
+  for (int b = tid; b < B; b += CE_THR) c += target[b] != ignore_index;
+  if (c) atomicAdd(&cnt_s, c);  // integer: order-independent
+  __syncthreads();
+  const float cnt = (float)cnt_s;
+  const float inv = cnt > 0.f ? 1.f / cnt : 0.f;
+  const float sc = scale != nullptr ? scale[0] : 0.f;
+  float lsum = 0.f;
+  for (int r0 = 0; r0 < B; r0 += RPP) {
+    const int b = r0 + gr;
+    const bool rv = b < B;
+    const T* row = logits + (size_t)(rv ? b : 0) * N;
+    const int64_t t = rv ? target[b] : ignore_index;
+    float mx = -INFINITY, sx = 0.f;
+    for (int n = gl; n < N; n += GL) {
       const float v = Cvt<T>::to_f(row[n]);
-      se += __expf(v - mx);
+      mx = fmaxf(mx, v);
       sx += v;
     }
-    se = wave_sum(se);
-    sx = wave_sum(sx);
+    mx = group_max<GL>(mx);
+    sx = group_sum<GL>(sx);
+    float se = 0.f;
+    for (int n = gl; n < N; n += GL) se += __expf(Cvt<T>::to_f(row[n]) - mx);
+    se = group_sum<GL>(se);
     const float lse = mx + __logf(se);
-    if (t != ignore_index) {
-      const float xt = Cvt<T>::to_f(row[t]);
+    const bool use = rv && t != ignore_index;
+    if (use && gl == 0) {
+      const float xt = (t >= 0 && t < N) ? Cvt<T>::to_f(row[t]) : NAN;  // bad target -> NaN loss
       // (1-eps)*(lse - x_t) + eps*(lse - mean_n x_n)
       lsum += (1.f - smoothing) * (lse - xt) + smoothing * (lse - sx / (float)N);
-      cnt += 1.f;
     }
-    // stash lse in dlog[b][0] temporarily? no: recompute below (cheap)
+    if (rv) {
+      const float rs = 1.f / se;
+      for (int n = gl; n < N; n += GL) {
+        float d = 0.f;
+        if (use) {
+          const float sm = __expf(Cvt<T>::to_f(row[n]) - mx) * rs;
+          const float oh = (n == t ? 1.f - smoothing : 0.f) + smoothing / (float)N;
+          d = (sm - oh) * inv;
+        }
+        dlog[(size_t)b * N + n] = d;
+        if (dls != nullptr) dls[(size_t)b * N + n] = Cvt<T>::from_f(d * sc);
+      }
+    }
   }
-  if (lane == 0) { red[wv] = lsum; red[16 + wv] = cnt; }
+  lsum = wave_sum(lsum);
+  if (lane == 0) red[wv] = lsum;
   __syncthreads();
-  float tl = 0.f, tc = 0.f;
-  for (int i = 0; i < nw; ++i) { tl += red[i]; tc += red[16 + i]; }
-  if (threadIdx.x == 0) loss[0] = tc > 0.f ? tl / tc : NAN;
-  const float inv = tc > 0.f ? 1.f / tc : 0.f;
-  for (int b = wv; b < B; b += nw) {
-    const T* row = logits + (size_t)b * N;
-    const int64_t t = target[b];
-    float* drow = dlog + (size_t)b * N;
-    if (t == ignore_index) {
-      for (int n = lane; n < N; n += 64) drow[n] = 0.f;
-      continue;
-    }
-    float mx = -INFINITY;
-    for (int n = lane; n < N; n += 64) mx = fmaxf(mx, Cvt<T>::to_f(row[n]));
-    mx = wave_max(mx);
-    float se = 0.f;
-    for (int n = lane; n < N; n += 64) se += __expf(Cvt<T>::to_f(row[n]) - mx);
-    se = wave_sum(se);
-    const float rs = 1.f / se;
-    for (int n = lane; n < N; n += 64) {
-      const float sm = __expf(Cvt<T>::to_f(row[n]) - mx) * rs;
-      const float oh = (n == t ? 1.f - smoothing : 0.f) + smoothing / (float)N;
-      drow[n] = (sm - oh) * inv;
-    }
+  if (tid == 0) {
+    float tl = 0.f;
+#pragma unroll
+    for (int i = 0; i < CE_THR / 64; ++i) tl += red[i];
+    const float l = cnt > 0.f ? tl / cnt : NAN;
+    loss[0] = l;
+    if (scale != nullptr) loss[1] = l * sc;
   }
 }
 
@@ -290,15 +320,25 @@ void linear_bwd(at::Tensor dout, at::Tensor x, at::Tensor w, c10::optional<at::T
 }
 
 void ce_fwd(at::Tensor logits, at::Tensor target, at::Tensor loss, at::Tensor dlog, int64_t ignore_index,
-            double smoothing) {
+            double smoothing, c10::optional<at::Tensor> scale, c10::optional<at::Tensor> dls) {
   DPA_CHECK_INPUT(logits); DPA_CHECK_INPUT(target); DPA_CHECK_INPUT(loss); DPA_CHECK_INPUT(dlog);
   TORCH_CHECK(target.scalar_type() == at::kLong && dlog.scalar_type() == at::kFloat);
   const int B = (int)logits.size(0), N = (int)logits.size(1);
-  const int thr = B >= 16 ? 1024 : 256;
+  TORCH_CHECK(scale.has_value() == dls.has_value());
+  if (scale.has_value()) {
+    TORCH_CHECK(loss.numel() >= 2 && scale->scalar_type() == at::kFloat && dls->numel() == logits.numel() &&
+                dls->scalar_type() == logits.scalar_type());
+  }
   DPA_DISPATCH_T(dt_of(logits), {
-    hipLaunchKernelGGL(ce_fwd_kernel<T>, dim3(1), dim3(thr), 0, cur_stream(), dptr<T>(logits),
-                       target.data_ptr<int64_t>(), loss.data_ptr<float>(), dlog.data_ptr<float>(), B, N,
-                       ignore_index, (float)smoothing);
+    auto go = [&](auto gl) {
+      hipLaunchKernelGGL((ce_fwd_kernel<T, decltype(gl)::value>), dim3(1), dim3(CE_THR), 0, cur_stream(),
+                         dptr<T>(logits), target.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                         dlog.data_ptr<float>(), B, N, ignore_index, (float)smoothing,
+                         scale.has_value() ? scale->data_ptr<float>() : nullptr,
+                         dls.has_value() ? dptr<T>(*dls) : nullptr);
+    };
+    if (N <= 16) go(std::integral_constant<int, 16>{});
+    else go(std::integral_constant<int, 64>{});
   });
   DPA_CHECK_LAUNCH();
 }
@@ -333,7 +373,9 @@ void register_head(pybind11::module& m) {
   auto s = m.def_submodule("head", "Linear (MFMA) / CrossEntropy / accuracy kernels");
   s.def("linear_fwd", &head::linear_fwd);
   s.def("linear_bwd", &head::linear_bwd);
-  s.def("ce_fwd", &head::ce_fwd);
+  s.def("ce_fwd", &head::ce_fwd, pybind11::arg("logits"), pybind11::arg("target"), pybind11::arg("loss"),
+        pybind11::arg("dlog"), pybind11::arg("ignore_index"), pybind11::arg("smoothing"),
+        pybind11::arg("scale") = pybind11::none(), pybind11::arg("dls") = pybind11::none());
   s.def("ce_bwd", &head::ce_bwd);
   s.def("accuracy", &head::accuracy);
 }

@@ -56,33 +56,65 @@ def linear(x, weight, bias=None, cdtype=None):
     return LinearFn.apply(x, weight, bias, cdtype)
 
 
+class _ScaledSeed:
+    """Token shared by a native CE loss and the GradScaler that scales it.
+
+    When the scaler's fast backward seeds the loss with exactly its scale
+    tensor, the CE backward returns the gradient the forward kernel already
+    wrote for the scaled loss (d(scale*loss)/dlogits, in the logits dtype): the
+    ``loss * scale`` multiply and the CE backward launch disappear from the
+    step (amp/grad_scaler.py)."""
+
+    __slots__ = ("scale", "seeded")
+
+    def __init__(self, scale):
+        self.scale = scale
+        self.seeded = False
+
+
 class CrossEntropyFn(torch.autograd.Function):
     """mean-reduced cross entropy; forward also produces the analytic gradient."""
 
     @staticmethod
-    def forward(ctx, logits, target, ignore_index, smoothing):
+    def forward(ctx, logits, target, ignore_index, smoothing, scale):
         H = _H()
         lg = logits.contiguous()
-        loss = torch.empty((), dtype=torch.float32, device=logits.device)
+        buf = torch.empty(2, dtype=torch.float32, device=logits.device)
         dlog = torch.empty(lg.shape, dtype=torch.float32, device=logits.device)
-        H.ce_fwd(lg, target.contiguous(), loss.view(1), dlog, int(ignore_index), float(smoothing))
+        dls = torch.empty_like(lg) if scale is not None else None
+        H.ce_fwd(lg, target.contiguous(), buf, dlog, int(ignore_index), float(smoothing), scale, dls)
         ctx.save_for_backward(dlog)
         ctx.ldtype = lg.dtype
-        return loss
+        ctx.token = _ScaledSeed(scale) if scale is not None else None
+        ctx.dls = dls
+        ctx.scaled = buf[1] if scale is not None else None
+        return buf[0]
 
     @staticmethod
     def backward(ctx, grad):
+        tok = ctx.token
+        if tok is not None and tok.seeded:
+            # grad is the scaler's scale tensor: the forward already wrote dlog * scale
+            return ctx.dls, None, None, None, None
         (dlog,) = ctx.saved_tensors
         out = torch.empty(dlog.shape, dtype=ctx.ldtype, device=dlog.device)
         g = grad.reshape(1).to(torch.float32).contiguous()
         _H().ce_bwd(dlog, g, out)
-        return out, None, None, None
+        return out, None, None, None, None
 
 
 def cross_entropy(logits, target, ignore_index=-100, label_smoothing=0.0):
     if logits.dim() != 2:
         raise ValueError("native cross_entropy expects [B, C] logits")
-    return CrossEntropyFn.apply(logits, target, ignore_index, label_smoothing)
+    from ..amp.grad_scaler import active_scale
+
+    scale = active_scale(logits.device) if logits.requires_grad else None
+    loss = CrossEntropyFn.apply(logits, target, ignore_index, label_smoothing, scale)
+    if scale is not None and loss.grad_fn is not None:
+        node = loss.grad_fn
+        # the token / pre-scaled value travel with the loss tensor to GradScaler.scale
+        loss._dpa_ce = (node, scale)
+    return loss
 
 
 def accuracy_(logits, target, counters):

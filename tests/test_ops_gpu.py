@@ -270,3 +270,33 @@ def test_grad_scaler_fast_backward_and_fused_step(C):
         torch.testing.assert_close(wa, wb, rtol=1e-5, atol=1e-6)
         assert sa.get_scale() == sb.get_scale()
     assert sa._single_opt_iters >= 3  # the fused path was taken from iteration 2 on
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_cross_entropy_prescaled_by_active_scaler(C, dtype):
+    """With an active GradScaler the CE kernel writes loss*scale and d(scale*loss)/dlogits;
+    scaler.scale(loss).backward() then returns that gradient without a launch, and the
+    generic autograd path (scaled loss used in an expression) stays exact."""
+    from ddp_practice_amd.amp import GradScaler
+    from ddp_practice_amd.ops.head import cross_entropy
+
+    torch.manual_seed(0)
+    sc = GradScaler(init_scale=256.0)
+    sc._lazy_init(torch.device(DEV))
+    logits = (torch.randn(32, 10, device=DEV) * 3).to(dtype)
+    tgt = torch.randint(0, 10, (32,), device=DEV)
+    r = logits.float().clone().requires_grad_()
+    ref = torch.nn.functional.cross_entropy(r, tgt)
+    (ref * 256.0).backward()
+    for generic in (False, True):
+        a = logits.clone().requires_grad_()
+        loss = cross_entropy(a, tgt)
+        assert getattr(loss, "_dpa_ce", None) is not None
+        scaled = sc.scale(loss)
+        torch.testing.assert_close(scaled.float(), ref.detach() * 256.0, rtol=1e-5, atol=1e-3)
+        if generic:
+            (scaled * 1.0).backward()
+        else:
+            scaled.backward()
+        tol = 1e-5 if dtype == torch.float32 else 1e-2
+        torch.testing.assert_close(a.grad.float(), r.grad, rtol=tol, atol=tol * 256)
