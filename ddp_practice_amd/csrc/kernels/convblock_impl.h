@@ -865,7 +865,10 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
   __shared__ __attribute__((aligned(16))) T dyl[COUT * ROWS * WP];
   constexpr int WX = WP + 4;  // padded input row (2 halo columns each side, room for the kw shift)
   __shared__ __attribute__((aligned(16))) T xs[5 * CIN * XR * WP];
-  __shared__ __attribute__((aligned(16))) T xpad[CIN * XR * WX];
+  // whole image per workgroup: the 5 shifted copies are written straight from
+  // registers (no padded staging image, no LDS->LDS copy pass)
+  constexpr bool DIRECT = (ROWS == H);
+  __shared__ __attribute__((aligned(16))) T xpad[DIRECT ? 8 : CIN * XR * WX];
   __shared__ f32x4 kred[KSPLIT > 1 ? NW : 1][64];
 
   const int tid = threadIdx.x;
@@ -884,20 +887,36 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
     for (int e = tid; e < COUT * ROWS * WP; e += NTHR)
       if (r0 + (e / WP) % ROWS >= H) dyl[e] = zero;
   }
-  // input rows r0-2 .. r0+ROWS+1 -> xpad[ci][XR][WX], columns shifted by 2 (zero halo)
-  for (int e = tid; e < CIN * XR * WX; e += NTHR) {
-    const int cc = e % WX, rr = (e / WX) % XR;
-    const int ih = r0 + rr - 2;
-    if (cc < 2 || cc >= W + 2 || ih < 0 || ih >= H) xpad[e] = zero;
+  // xs[kw][ci][rr][c] = x[ci][r0 + rr - 2][c + kw - 2] (zero outside the image)
+  auto scatter5 = [&](int ci, int rr, int w, T v) {
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw) {
+      const int c = w + 2 - kw;
+      if (c >= 0 && c < WP) xs[((kw * CIN + ci) * XR + rr) * WP + c] = v;
+    }
+  };
+  if constexpr (DIRECT) {
+    constexpr int NZ = 5 * CIN * XR * WP * (int)sizeof(T) / 16;
+    static_assert((5 * CIN * XR * WP * sizeof(T)) % 16 == 0, "xs must be a whole number of 16-B chunks");
+    uint4* z = reinterpret_cast<uint4*>(xs);
+    for (int e = tid; e < NZ; e += NTHR) z[e] = make_uint4(0u, 0u, 0u, 0u);
+  } else {
+    // input rows r0-2 .. r0+ROWS+1 -> xpad[ci][XR][WX], columns shifted by 2 (zero halo)
+    for (int e = tid; e < CIN * XR * WX; e += NTHR) {
+      const int cc = e % WX, rr = (e / WX) % XR;
+      const int ih = r0 + rr - 2;
+      if (cc < 2 || cc >= W + 2 || ih < 0 || ih >= H) xpad[e] = zero;
+    }
   }
   if constexpr (PRO == 2) {
     __shared__ float coef[5 * COUT], sums[2 * COUT];
     __shared__ float part[NTHR];
     BnBwdStage<T, COUT, H, W, NTHR> st;
     st.load(bin, b);
+    __syncthreads();  // xs zero-fill before the scatter
     stage_chw<T, CIN, H, W>(xb, [&](int ci, int h, int ww, T a, T bb) {
-      xpad[(ci * XR + h + 2) * WX + ww + 2] = a;
-      xpad[(ci * XR + h + 2) * WX + ww + 3] = bb;
+      scatter5(ci, h + 2, ww, a);
+      scatter5(ci, h + 2, ww + 1, bb);
     });
     bn_bwd_coef<COUT, T>(bin, coef, part, sums, blockIdx.x == 0);
     st.emit(coef, [&](int co, int h, int ww, T v00, T v01, T v10, T v11) {
@@ -906,14 +925,15 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
       dyl[(co * ROWS + h + 1) * WP + ww] = v10;
       dyl[(co * ROWS + h + 1) * WP + ww + 1] = v11;
     });
-  } else if (ROWS == H) {  // whole image per workgroup: both operands are full [C][H][W] images
+  } else if constexpr (DIRECT) {  // both operands are full [C][H][W] images
     stage_chw<T, COUT, H, W>(dyb, [&](int co, int h, int ww, T a, T bb) {
       dyl[(co * ROWS + h) * WP + ww] = a;
       dyl[(co * ROWS + h) * WP + ww + 1] = bb;
     });
+    __syncthreads();  // xs zero-fill before the scatter
     stage_chw<T, CIN, H, W>(xb, [&](int ci, int h, int ww, T a, T bb) {
-      xpad[(ci * XR + h + 2) * WX + ww + 2] = a;
-      xpad[(ci * XR + h + 2) * WX + ww + 3] = bb;
+      scatter5(ci, h + 2, ww, a);
+      scatter5(ci, h + 2, ww + 1, bb);
     });
   } else {
     for (int e = tid; e < COUT * ROWS * W; e += NTHR) {
@@ -929,17 +949,19 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
     }
   }
   __syncthreads();
-  // 5 kw-shifted copies, LDS -> LDS: xs[kw][ci][rr][c] = xpad[ci][rr][c + kw]
-  for (int e = tid; e < 5 * CIN * XR * (WP / 8); e += NTHR) {
-    const int c8 = e % (WP / 8);
-    const int rowid = e / (WP / 8);  // (kw, ci, rr)
-    const int kw = rowid / (CIN * XR), cr = rowid % (CIN * XR);
-    const T* srcp = &xpad[cr * WX + 8 * c8 + kw];
-    T* dstp = &xs[rowid * WP + 8 * c8];
+  if constexpr (!DIRECT) {
+    // 5 kw-shifted copies, LDS -> LDS: xs[kw][ci][rr][c] = xpad[ci][rr][c + kw]
+    for (int e = tid; e < 5 * CIN * XR * (WP / 8); e += NTHR) {
+      const int c8 = e % (WP / 8);
+      const int rowid = e / (WP / 8);  // (kw, ci, rr)
+      const int kw = rowid / (CIN * XR), cr = rowid % (CIN * XR);
+      const T* srcp = &xpad[cr * WX + 8 * c8 + kw];
+      T* dstp = &xs[rowid * WP + 8 * c8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dstp[j] = srcp[j];
+      for (int j = 0; j < 8; ++j) dstp[j] = srcp[j];
+    }
+    __syncthreads();
   }
-  __syncthreads();
 
   float* row_out = wslab + (size_t)blockIdx.x * ROWLEN;
   const int lane = tid & 63, wv = tid >> 6;
