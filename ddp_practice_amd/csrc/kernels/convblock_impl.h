@@ -132,8 +132,8 @@ struct BNParams {
 
 // part: >= blockDim.x floats of LDS; ends with __syncthreads().
 template <int C>
-__device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, float* sh_s, float* part, bool leader,
-                                            float* mean_s = nullptr, float* istd_s = nullptr) {
+__device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, float* beta_s, float* mean_s,
+                                            float* istd_s, float* part, bool leader) {
   const int tid = threadIdx.x, nthr = blockDim.x;
   if (bp.train) {
     constexpr int RL = 2 * C + 1;
@@ -166,8 +166,9 @@ __device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, flo
       const float istd = rsqrtf(var + bp.eps);
       const float s = bp.gamma[tid] * istd;
       sc_s[tid] = s;
-      sh_s[tid] = bp.beta[tid] - mean * s;
-      if (mean_s != nullptr) { mean_s[tid] = mean; istd_s[tid] = istd; }
+      beta_s[tid] = bp.beta[tid];
+      mean_s[tid] = mean;
+      istd_s[tid] = istd;
       if (leader) {
         bp.fstats[tid] = part[tid];
         bp.fstats[C + tid] = part[C + tid];
@@ -185,33 +186,21 @@ __device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, flo
       const float istd = rsqrtf(bp.rvar[tid] + bp.eps);
       const float s = bp.gamma[tid] * istd;
       sc_s[tid] = s;
-      sh_s[tid] = bp.beta[tid] - bp.rmean[tid] * s;
-      if (mean_s != nullptr) { mean_s[tid] = bp.rmean[tid]; istd_s[tid] = istd; }
+      beta_s[tid] = bp.beta[tid];
+      mean_s[tid] = bp.rmean[tid];
+      istd_s[tid] = istd;
     }
     __syncthreads();
   }
 }
 
-// BN -> ReLU -> 2x2 max (first max wins) of one window given as two row pairs.
-template <typename T>
-__device__ __forceinline__ void bn_relu_max4(const typename Pair2<T>::type top, const typename Pair2<T>::type bot,
-                                             float sc, float sh, float& best, int& bi) {
-  T v[4];
-  __builtin_memcpy(&v[0], &top, 2 * sizeof(T));
-  __builtin_memcpy(&v[2], &bot, 2 * sizeof(T));
-  best = -1.f;
-  bi = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float z = fmaxf(rnd_t<T>(Cvt<T>::to_f(v[k]) * sc + sh), 0.f);
-    if (z > best) { best = z; bi = k; }
-  }
-}
-
-// Same, also returning xhat = (y - mean) * invstd at the argmax.
+// BN -> ReLU -> 2x2 max (first max wins, ATen's scan order) of one window given
+// as two row pairs; also returns xhat = (y - mean) * invstd at the argmax.
+// z = (y - mean) * (gamma * invstd) + beta: near the ReLU threshold this form
+// keeps the rounding error at the scale of beta instead of gamma*mean*invstd.
 template <typename T>
 __device__ __forceinline__ void bn_relu_max4x(const typename Pair2<T>::type top, const typename Pair2<T>::type bot,
-                                              float sc, float sh, float mean, float istd, float& best, int& bi,
+                                              float sc, float beta, float mean, float istd, float& best, int& bi,
                                               float& xh) {
   T v[4];
   __builtin_memcpy(&v[0], &top, 2 * sizeof(T));
@@ -222,7 +211,7 @@ __device__ __forceinline__ void bn_relu_max4x(const typename Pair2<T>::type top,
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const float yv = Cvt<T>::to_f(v[k]);
-    const float z = fmaxf(rnd_t<T>(yv * sc + sh), 0.f);
+    const float z = fmaxf(rnd_t<T>((yv - mean) * sc + beta), 0.f);
     if (z > best) { best = z; bi = k; yb = yv; }
   }
   xh = (yb - mean) * istd;
@@ -482,7 +471,7 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
       img[((h + 2) * WPD + (ww + 3)) * CIN + ci] = bb;
     });
   } else if constexpr (PRO == 1) {
-    __shared__ float sc_s[CIN], sh_s[CIN], mean_s[CIN], istd_s[CIN];
+    __shared__ float sc_s[CIN], beta_s[CIN], mean_s[CIN], istd_s[CIN];
     __shared__ float part[NTHR];
     typedef typename Pair2<T>::type P;
     constexpr int NPO = CIN * HW;  // pooled outputs of one image = this conv's input
@@ -499,7 +488,7 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
         bot[i] = src[W];  // next input row (2W elements = W pairs)
       }
     }
-    bn_finalize<CIN>(pin.bn, sc_s, sh_s, part, blockIdx.x == 0, mean_s, istd_s);
+    bn_finalize<CIN>(pin.bn, sc_s, beta_s, mean_s, istd_s, part, blockIdx.x == 0);
     const bool wr = pin.p_out != nullptr && sp == 0;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
@@ -508,7 +497,7 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
         const int ci = e / HW, pix = e % HW, ho = pix / W, wo = pix % W;
         float best, xh;
         int bi;
-        bn_relu_max4x<T>(top[i], bot[i], sc_s[ci], sh_s[ci], mean_s[ci], istd_s[ci], best, bi, xh);
+        bn_relu_max4x<T>(top[i], bot[i], sc_s[ci], beta_s[ci], mean_s[ci], istd_s[ci], best, bi, xh);
         const T pv = Cvt<T>::from_f(best);
         img[((ho + 2) * WPD + (wo + 2)) * CIN + ci] = pv;
         if (wr) {
@@ -648,7 +637,7 @@ bn_relu_pool_kernel(const T* __restrict__ y, const float* __restrict__ fslab, in
   constexpr int HO = H / 2, WO = W / 2;
   constexpr int RL = 2 * C + 1;
   __shared__ float part[NTHR];
-  __shared__ float sc_s[C], sh_s[C];
+  __shared__ float sc_s[C], beta_s[C], mean_s[C];
   const int tid = threadIdx.x;
   if (train) {
     // column j of the slab summed over rows; NTHR/RL row-groups in parallel
@@ -683,7 +672,8 @@ bn_relu_pool_kernel(const T* __restrict__ y, const float* __restrict__ fslab, in
       const float invstd = rsqrtf(var + eps);
       const float s = gamma[tid] * invstd;
       sc_s[tid] = s;
-      sh_s[tid] = beta[tid] - mean * s;
+      beta_s[tid] = beta[tid];
+      mean_s[tid] = mean;
       if (blockIdx.x == 0) {
         fstats[tid] = part[tid];
         fstats[C + tid] = part[C + tid];
@@ -701,14 +691,15 @@ bn_relu_pool_kernel(const T* __restrict__ y, const float* __restrict__ fslab, in
       const float invstd = rsqrtf(rvar[tid] + eps);
       const float s = gamma[tid] * invstd;
       sc_s[tid] = s;
-      sh_s[tid] = beta[tid] - rmean[tid] * s;
+      beta_s[tid] = beta[tid];
+      mean_s[tid] = rmean[tid];
     }
     __syncthreads();
   }
   const int e = blockIdx.x * NTHR + tid;
   if (e >= total) return;
   const int c = (e / (HO * WO)) % C;
-  const float sc = sc_s[c], sh = sh_s[c];
+  const float sc = sc_s[c], bt = beta_s[c], mn = mean_s[c];
   const int bc = e / (HO * WO), pix = e % (HO * WO);
   const int ho = pix / WO, wo = pix % WO;
   const T* src = y + (size_t)bc * H * W + (2 * ho) * W + 2 * wo;
@@ -717,7 +708,7 @@ bn_relu_pool_kernel(const T* __restrict__ y, const float* __restrict__ fslab, in
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const float v = Cvt<T>::to_f(src[(k >> 1) * W + (k & 1)]);
-    const float z = fmaxf(rnd_t<T>(v * sc + sh), 0.f);
+    const float z = fmaxf(rnd_t<T>((v - mn) * sc + bt), 0.f);
     if (z > best) { best = z; bi = k; }
   }
   p[e] = Cvt<T>::from_f(best);

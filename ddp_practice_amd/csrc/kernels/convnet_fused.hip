@@ -49,7 +49,7 @@ head_fwd_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__ 
   constexpr int HO = H / 2, WO = W / 2, PP = HO * WO, K = C * PP;
   constexpr int IT = (K + HF - 1) / HF;
   typedef typename Pair2<T>::type P;
-  __shared__ float sc_s[C], sh_s[C], mean_s[C], istd_s[C];
+  __shared__ float sc_s[C], beta_s[C], mean_s[C], istd_s[C];
   __shared__ float part[HF];
   __shared__ float red[HF / 64][NMAX];
   const int tid = threadIdx.x, b = blockIdx.x;
@@ -65,7 +65,7 @@ head_fwd_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__ 
       bot[i] = src[W / 2];
     }
   }
-  bn_finalize<C>(bn, sc_s, sh_s, part, b == 0, mean_s, istd_s);
+  bn_finalize<C>(bn, sc_s, beta_s, mean_s, istd_s, part, b == 0);
   float pf[IT];
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
@@ -75,7 +75,7 @@ head_fwd_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__ 
       const int c = k / PP;
       float best, xh;
       int bi;
-      bn_relu_max4x<T>(top[i], bot[i], sc_s[c], sh_s[c], mean_s[c], istd_s[c], best, bi, xh);
+      bn_relu_max4x<T>(top[i], bot[i], sc_s[c], beta_s[c], mean_s[c], istd_s[c], best, bi, xh);
       const T pv = Cvt<T>::from_f(best);
       pf[i] = Cvt<T>::to_f(pv);
       if (p_out != nullptr) {
