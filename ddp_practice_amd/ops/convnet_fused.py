@@ -23,16 +23,6 @@ import torch
 from .._ext import load as _load_ext
 
 
-_SIDE: dict = {}
-
-
-def _side_stream(dev: torch.device) -> torch.cuda.Stream:
-    s = _SIDE.get(dev.index)
-    if s is None:
-        s = _SIDE[dev.index] = torch.cuda.Stream(dev)
-    return s
-
-
 def _mods():
     C = _load_ext()
     return C.convblock, C.convnet
@@ -130,33 +120,20 @@ class ConvNetFn(torch.autograd.Function):
         dp2 = torch.empty_like(p2)
         cn.head_bwd(dl, wfc, p2, idx2, xh2, dwfc, dbfc, dg2, dbe2, bsum2, dp2)
         gsum2 = comm.all_reduce(bsum2) if sync else bsum2
-        # 3. (side stream) BN2 bwd -> conv2 wgrad partials -> [dW2 | db2]: independent of 2 and 4,
-        #    so it runs as a parallel branch (also inside a captured hipGraph)
-        cur = torch.cuda.current_stream(dev)
-        side = _side_stream(dev)
-        fork = torch.cuda.Event()
-        fork.record(cur)
-        wslab2 = torch.empty(B * (n_w2 + 32), **f32)
-        with torch.cuda.stream(side):
-            side.wait_event(fork)
-            cn.conv_wgrad_bn(p1, y2, dp2, idx2, fstats2, gsum2, None, g2, e2, None, None, wslab2)
-            cb.slab_reduce(wslab2, n_w2 + 32, out.narrow(0, n_w1 + 48, n_w2 + 32))
-            join = torch.cuda.Event()
-            join.record(side)
         # 2. BN2 bwd -> conv2 dgrad -> dp1 (+ BN1 partial sums)
         dp1 = torch.empty((B, 16, 14, 14), dtype=y1.dtype, device=dev)
         bslab1 = torch.empty(cn.dgrad2_rows(B) * 32, **f32)
         cn.conv2_dgrad(w2, y2, dp2, idx2, fstats2, gsum2, g2, e2, dp1, idx1, xh1, bslab1)
+        # 3. BN2 bwd -> conv2 wgrad partials (independent of 2)
+        wslab2 = torch.empty(B * (n_w2 + 32), **f32)
+        cn.conv_wgrad_bn(p1, y2, dp2, idx2, fstats2, gsum2, None, g2, e2, None, None, wslab2)
         # 4. BN1 bwd -> conv1 wgrad partials (+ dgamma1 / dbeta1 from the local sums)
         gslab1 = comm.all_reduce(bslab1) if sync else bslab1
         wslab1 = torch.empty(B * (n_w1 + 16), **f32)
         cn.conv_wgrad_bn(x, y1, dp1, idx1, fstats1, gslab1, bslab1 if sync else None, g1, e1, dg1, dbe1, wslab1)
-        # 5. weight-grad partial sums -> [dW1 | db1]; join the side branch
-        cb.slab_reduce(wslab1, n_w1 + 16, out.narrow(0, 0, n_w1 + 16))
-        cur.wait_event(join)
-        # every tensor the side branch touched is released after this join (program
-        # order on the current stream), so the caching allocator cannot hand its
-        # memory to later work on this stream while the branch still runs
+        # 5. weight-grad partial sums -> [dW1 | db1], [dW2 | db2]
+        cb.slab_reduce(wslab1, n_w1 + 16, out.narrow(0, 0, n_w1 + 16), wslab2, n_w2 + 32,
+                       out.narrow(0, n_w1 + 48, n_w2 + 32))
         return (None, dw1.view(s_w1), db1, dg1, dbe1, dw2.view(s_w2), db2, dg2, dbe2, dwfc.view(s_wfc), dbfc,
                 None, None, None, None, None, None)
 
