@@ -15,6 +15,7 @@ void register_head(pybind11::module& m);
 void register_optim(pybind11::module& m);
 void register_data(pybind11::module& m);
 void register_comm(pybind11::module& m);
+void register_xgmi(pybind11::module& m);
 void register_reducer(pybind11::module& m);
 void register_convnet_fused(pybind11::module& m);
 void register_runtime(pybind11::module& m);
@@ -44,6 +45,7 @@ PYBIND11_MODULE(_C, m) {
   dpa::register_head(m);
   dpa::register_optim(m);
   dpa::register_data(m);
+  dpa::register_xgmi(m);
   dpa::register_comm(m);
   dpa::register_reducer(m);
   dpa::register_convnet_fused(m);

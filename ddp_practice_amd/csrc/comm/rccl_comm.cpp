@@ -21,6 +21,7 @@
 #include <thread>
 
 #include "comm/collective.h"
+#include "comm/xgmi.h"
 #include "common.h"
 
 namespace dpa {
@@ -125,12 +126,14 @@ class RcclComm : public Collective {
 
   // Abort outstanding work (failure handling / watchdog path).
   void abort() {
+    if (auto x = xgmi_) x->abort();
     ncclComm_t c = comm_.exchange(nullptr);
     if (c != nullptr) ncclCommAbort(c);
   }
   void abort_now() override { abort(); }
 
   std::string async_error() override {
+    if (auto x = xgmi_; x && x->error() != 0) return x->error_string();
     ncclComm_t c = comm_.load();
     if (c == nullptr) return "destroyed";
     ncclResult_t st = ncclSuccess;
@@ -151,8 +154,13 @@ class RcclComm : public Collective {
       check(dst);
       TORCH_CHECK(dst.numel() == t.numel() && dst.scalar_type() == t.scalar_type());
     }
+    const RedOp rop = parse_op(op);
+    if (use_xgmi(t, dst, rop)) {  // one kernel on the caller's stream, no fork/join
+      xgmi_->all_reduce(t, dst, rop, cur_stream());
+      return dst;
+    }
     fenced([&](hipStream_t s) {
-      DPA_NCCL(ncclAllReduce(t.data_ptr(), dst.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(parse_op(op)),
+      DPA_NCCL(ncclAllReduce(t.data_ptr(), dst.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(rop),
                              comm_.load(), s));
     });
     return dst;
@@ -223,10 +231,25 @@ class RcclComm : public Collective {
     const int i = next_++ % kRing;
     DPA_CHECK_HIP(hipEventRecord(fork_[i], cur));
     DPA_CHECK_HIP(hipStreamWaitEvent(stream_.stream(), fork_[i], 0));
-    DPA_NCCL(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), comm_.load(),
-                           stream_.stream()));
+    if (use_xgmi(t, t, op))
+      xgmi_->all_reduce(t, t, op, stream_.stream());
+    else
+      DPA_NCCL(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), comm_.load(),
+                             stream_.stream()));
     DPA_CHECK_HIP(hipEventRecord(slot_[slot], stream_.stream()));
   }
+
+  // Route all-reduces of at most `max_bytes` to the one-shot xGMI engine
+  // (max_bytes <= 0: detach).  Every rank must attach the same way.
+  void attach_xgmi(std::shared_ptr<xgmi::XgmiComm> x, long long max_bytes) {
+    if (x) {
+      TORCH_CHECK(x->device() == device_ && x->world() == world_ && x->rank() == rank_,
+                  "xgmi engine does not match this communicator");
+    }
+    xgmi_ = max_bytes > 0 ? std::move(x) : nullptr;
+    xgmi_max_ = xgmi_ ? std::min(max_bytes, xgmi_->max_bytes()) : 0;
+  }
+  long long xgmi_max_bytes() const { return xgmi_ ? xgmi_max_ : 0; }
 
   void wait(int slot, hipStream_t stream) override {
     TORCH_CHECK(slot >= 0 && slot < kSlots, "slot out of range");
@@ -234,6 +257,11 @@ class RcclComm : public Collective {
   }
 
  private:
+  bool use_xgmi(const at::Tensor& in, const at::Tensor& out, RedOp op) const {
+    return xgmi_ && op != RedOp::PROD && (long long)in.nbytes() <= xgmi_max_ && xgmi_->supports(in) &&
+           xgmi_->supports(out);
+  }
+
   static constexpr int kRing = 64;
   static constexpr int kSlots = 256;
 
@@ -262,6 +290,8 @@ class RcclComm : public Collective {
   hipEvent_t slot_[kSlots] = {};
   int next_ = 0;
   at::Tensor barrier_buf_;
+  std::shared_ptr<xgmi::XgmiComm> xgmi_;
+  long long xgmi_max_ = 0;
 };
 
 // Python-implemented collective (torch.distributed / gloo on CPU; tests).
@@ -317,6 +347,8 @@ void register_comm(pybind11::module& m) {
         c.all_reduce_async(t, parse_op(op), slot);
       })
       .def("wait", [](comm::RcclComm& c, int slot) { c.wait(slot, nullptr); })
+      .def("attach_xgmi", &comm::RcclComm::attach_xgmi, py::arg("engine"), py::arg("max_bytes"))
+      .def_property_readonly("xgmi_max_bytes", &comm::RcclComm::xgmi_max_bytes)
       .def("async_error", &comm::RcclComm::async_error)
       .def("abort", &comm::RcclComm::abort)
       .def("destroy", &comm::RcclComm::destroy);

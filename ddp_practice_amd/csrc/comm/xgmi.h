@@ -1,0 +1,59 @@
+// One-shot xGMI all-reduce engine (implementation: comm/xgmi_allreduce.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <torch/extension.h>
+
+#include <string>
+#include <vector>
+
+#include "comm/collective.h"
+
+namespace dpa {
+namespace xgmi {
+
+constexpr int kMaxRanks = 8;
+
+struct Peers {
+  char* base[kMaxRanks];  // every rank's workspace, mapped into this process
+};
+
+class XgmiComm {
+ public:
+  // max_bytes: largest message this engine takes; timeout_s: bound on every wait
+  XgmiComm(int rank, int world, int device, long long max_bytes, double timeout_s);
+  ~XgmiComm();
+  XgmiComm(const XgmiComm&) = delete;
+  XgmiComm& operator=(const XgmiComm&) = delete;
+
+  pybind11::bytes handle() const;               // IPC handle of this rank's workspace
+  void open(std::vector<std::string> handles);  // map every peer's workspace
+  void close();
+
+  bool supports(const at::Tensor& t) const;
+  // out may alias in; stream == nullptr: the caller's current stream
+  void all_reduce(const at::Tensor& in, const at::Tensor& out, RedOp op, hipStream_t stream);
+
+  int error() const;  // 0 ok, 1 a peer never arrived (timeout), 2 aborted
+  std::string error_string() const;
+  void abort();       // every waiting block gives up (watchdog path)
+  void set_timeout(double s) { timeout_ticks_ = (long long)(s * 1e8); }
+  long long max_bytes() const { return slot_bytes_; }
+  long long workspace_bytes() const { return ws_bytes_; }
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  int device() const { return device_; }
+
+ private:
+  int rank_, world_, device_;
+  long long slot_bytes_ = 0, flags_off_ = 0, ctr_off_ = 0, ws_bytes_ = 0, timeout_ticks_ = 0;
+  int max_blocks_ = 0;
+  char* local_ = nullptr;
+  Peers peers_;
+  int* host_words_ = nullptr;  // [0] error, [1] abort (host-mapped, coherent)
+  int* dev_words_ = nullptr;
+  bool opened_ = false;
+};
+
+}  // namespace xgmi
+}  // namespace dpa

@@ -200,6 +200,10 @@ class RcclCommunicator(Communicator):
         else:
             uid = C.comm.RcclComm.unique_id()
         self._c = C.comm.RcclComm(bytes(uid), rank, world_size, self.device.index)
+        self.xgmi = None
+        self.xgmi_status = "off (world_size 1)" if world_size == 1 else "off"
+        if world_size > 1:
+            self.xgmi_status = setup_xgmi(self, store, key)
 
     @property
     def native(self):
@@ -240,11 +244,102 @@ class RcclCommunicator(Communicator):
     def async_error(self) -> str:
         return self._c.async_error()
 
+    @property
+    def xgmi_max_bytes(self) -> int:
+        return int(self._c.xgmi_max_bytes)
+
     def abort(self):
         self._c.abort()
 
     def destroy(self):
+        if self.xgmi is not None:
+            self._c.attach_xgmi(None, 0)
+            self.xgmi.close()
+            self.xgmi = None
         self._c.destroy()
+
+
+# ------------------------------------------------------------------ xGMI one-shot engine
+XGMI_DEFAULT_MAX_BYTES = 1 << 20  # every ConvNet collective (<= 116 KB); RCCL above
+
+
+def open_xgmi(rank: int, world: int, device: torch.device, store, key: str, max_bytes: int, timeout_s: float):
+    """Create this rank's xGMI workspace and map every peer's (handles via the store)."""
+    C = _load_ext()
+    x, err = None, ""
+    try:
+        x = C.xgmi.XgmiComm(rank, world, device.index, int(max_bytes), float(timeout_s))
+        h = x.handle()
+    except Exception as e:  # noqa: BLE001 - any failure here means "use RCCL"
+        x, h, err = None, b"", f"{type(e).__name__}: {e}"
+    store.set(f"{key}_xgmi_{rank}", h)
+    hs = [bytes(store.get(f"{key}_xgmi_{r}")) for r in range(world)]
+    if x is not None and all(len(v) > 0 for v in hs):
+        try:
+            x.open(hs)
+        except Exception as e:  # noqa: BLE001
+            x, err = None, f"{type(e).__name__}: {e}"
+    elif x is not None:
+        x, err = None, "a peer failed to create its workspace"
+    return x, err
+
+
+def setup_xgmi(rc: "RcclCommunicator", store, key: str) -> str:
+    """Attach the one-shot xGMI all-reduce (csrc/comm/xgmi_allreduce.hip) to ``rc``.
+
+    DPA_XGMI=0 disables it; DPA_XGMI_MAX_BYTES sets the size up to which it is
+    used (default 1 MiB).  Before attaching, every rank runs a self-test
+    against RCCL (values within fp32 tolerance, results bit-identical across
+    ranks, bounded by a short timeout); any failure on any rank keeps every
+    rank on RCCL.  Returns a status string.
+    """
+    if os.environ.get("DPA_XGMI", "1") == "0":
+        return "off (DPA_XGMI=0)"
+    if store is None:
+        store = dist.distributed_c10d._get_default_store()
+    max_bytes = int(float(os.environ.get("DPA_XGMI_MAX_BYTES", XGMI_DEFAULT_MAX_BYTES)))
+    timeout = float(os.environ.get("DPA_XGMI_TIMEOUT", "600"))
+    if max_bytes <= 0 or rc.world_size > 8:
+        return "off"
+    x, err = open_xgmi(rc.rank, rc.world_size, rc.device, store, key, max_bytes, 20.0)
+    ok = torch.tensor([1.0 if x is not None else 0.0], device=rc.device)
+    rc.native.all_reduce(ok, "min")
+    if ok.item() != 1.0:
+        return f"off (setup failed: {err or 'on a peer'})"
+    try:
+        good = _xgmi_selftest(rc, x)
+    except Exception as e:  # noqa: BLE001
+        good, err = False, f"{type(e).__name__}: {e}"
+    ok.fill_(1.0 if good and x.error() == 0 else 0.0)
+    rc.native.all_reduce(ok, "min")
+    if ok.item() != 1.0:
+        return f"off (self-test failed: {err or x.error_string() or 'on a peer'})"
+    x.set_timeout(timeout)
+    rc.native.attach_xgmi(x, max_bytes)
+    rc.xgmi = x
+    return f"on (<= {max_bytes} B)"
+
+
+def _xgmi_selftest(rc: "RcclCommunicator", x) -> bool:
+    g = torch.Generator(device="cpu").manual_seed(1234 + rc.rank)
+    for n, dt, op in ((33, torch.float32, "sum"), (4099, torch.float32, "sum"), (29034, torch.float32, "sum"),
+                      (8195, torch.bfloat16, "sum"), (1000, torch.float32, "max")):
+        t = torch.randn(n, generator=g).to(device=rc.device, dtype=dt)
+        mine = x.all_reduce(t, op, torch.empty_like(t))
+        ref = torch.empty_like(t)
+        rc.native.all_reduce(t, op, ref)
+        torch.cuda.synchronize(rc.device)
+        if x.error() != 0:
+            return False
+        tol = 1e-5 if dt == torch.float32 else 2e-2
+        if not torch.allclose(mine.float(), ref.float(), rtol=tol, atol=tol * rc.world_size):
+            return False
+        every = torch.empty(rc.world_size * n, dtype=dt, device=rc.device)
+        rc.native.all_gather(every, mine)
+        every = every.view(rc.world_size, n)
+        if not bool((every == every[0:1]).all()):
+            return False
+    return True
 
 
 # ------------------------------------------------------------------ process group

@@ -1,0 +1,121 @@
+"""Worker for tests/test_xgmi_gpu.py: W processes sharing ONE GPU run the
+one-shot xGMI all-reduce against each other (IPC-mapped workspaces on the same
+device exercise the whole protocol: peer stores, flags, epochs, parity reuse,
+graph replay, bounded waits)."""
+import os
+import traceback
+from datetime import timedelta
+
+import torch
+import torch.distributed  # noqa: F401  (TCPStore)
+
+DTYPES = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}
+
+
+def _data(rank, n, dt, it):
+    g = torch.Generator(device="cpu").manual_seed(1000 * it + 17 * rank + n)
+    return torch.randn(n, generator=g).to(dt)
+
+
+def _expect(world, n, dt, it, op):
+    xs = [_data(r, n, dt, it).float() for r in range(world)]
+    acc = xs[0].clone()
+    for x in xs[1:]:
+        acc = torch.maximum(acc, x) if op == "max" else torch.minimum(acc, x) if op == "min" else acc + x
+    if op == "avg":
+        acc = acc / world
+    return acc
+
+
+def _check(got, exp, dt, what):
+    tol = {torch.float32: 1e-5, torch.bfloat16: 1e-2, torch.float16: 2e-3}[dt]
+    got = got.float().cpu()
+    assert got.shape == exp.shape, what
+    err = ((got - exp).abs() / (exp.abs() + 1.0)).max().item()
+    assert err <= tol, (what, err)
+
+
+def worker(rank, world, port, mode, q):
+    try:
+        from ddp_practice_amd import _ext
+
+        C = _ext.load()
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        store = torch.distributed.TCPStore("127.0.0.1", port, world, rank == 0, timedelta(seconds=60))
+        from ddp_practice_amd.parallel.comm import open_xgmi
+
+        x, err = open_xgmi(rank, world, dev, store, "t", 1 << 20, 20.0)
+        assert x is not None, err
+        store.set(f"ready{rank}", "1")
+        store.wait([f"ready{r}" for r in range(world)])
+        if mode == "timeout":
+            # rank 0 waits for a peer that never comes: must return with error 1, not hang
+            if rank == 0:
+                x.set_timeout(0.5)
+                t = torch.ones(100, device=dev)
+                x.all_reduce(t)
+                torch.cuda.synchronize()
+                assert x.error() == 1, x.error()
+            store.set(f"done{rank}", "1")
+            store.wait([f"done{r}" for r in range(world)])
+            q.put((rank, "ok", None))
+            return
+        out = {}
+        it = 0
+        # eager: sizes across the chunk boundaries, ragged tails, every dtype and op
+        cases = [(33, "f32", "sum"), (2048, "f32", "sum"), (2049, "f32", "sum"), (29034, "f32", "sum"),
+                 (262144, "f32", "sum"), (5, "bf16", "sum"), (8195, "bf16", "sum"), (4097, "f16", "sum"),
+                 (1000, "f32", "max"), (1000, "f32", "min"), (3001, "f32", "avg")]
+        for n, dn, op in cases:
+            dt = DTYPES[dn]
+            t = _data(rank, n, dt, it).to(dev)
+            x.all_reduce(t, op)
+            torch.cuda.synchronize()
+            assert x.error() == 0, x.error_string()
+            _check(t, _expect(world, n, dt, it, op), dt, (n, dn, op))
+            out[f"{n}{dn}{op}"] = t.float().cpu()
+            it += 1
+        # back-to-back reuse of the same slots (parity flips, epochs advance), out of place
+        for k in range(40):
+            n = (k * 977) % 5000 + 1
+            t = _data(rank, n, torch.float32, it).to(dev)
+            o = torch.empty_like(t)
+            x.all_reduce(t, "sum", o)
+            _check(o.cpu() if k % 7 else o, _expect(world, n, torch.float32, it, "sum"), torch.float32, ("loop", k))
+            it += 1
+        torch.cuda.synchronize()
+        assert x.error() == 0, x.error_string()
+        # hipGraph: capture two collectives, replay with fresh inputs each time
+        a = torch.zeros(4099, device=dev)
+        b = torch.zeros(70000, device=dev)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            x.all_reduce(a)  # warm-up on the capture stream
+            x.all_reduce(b)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            x.all_reduce(a)
+            x.all_reduce(b, "max")
+        for r in range(12):
+            a.copy_(_data(rank, 4099, torch.float32, it).to(dev))
+            b.copy_(_data(rank, 70000, torch.float32, it + 1).to(dev))
+            g.replay()
+            torch.cuda.synchronize()
+            assert x.error() == 0, x.error_string()
+            _check(a, _expect(world, 4099, torch.float32, it, "sum"), torch.float32, ("graph a", r))
+            _check(b, _expect(world, 70000, torch.float32, it + 1, "max"), torch.float32, ("graph b", r))
+            it += 2
+        store.set(f"done{rank}", "1")
+        store.wait([f"done{r}" for r in range(world)])
+        x.close()
+        q.put((rank, "ok", out))
+    except Exception:  # pragma: no cover - reported to the parent
+        q.put((rank, "err", traceback.format_exc()))
+    finally:
+        q.close()
+        q.join_thread()
+        os._exit(0)
