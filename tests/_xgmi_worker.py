@@ -74,7 +74,7 @@ def worker(rank, world, port, mode, q):
             torch.cuda.synchronize()
             assert x.error() == 0, x.error_string()
             _check(t, _expect(world, n, dt, it, op), dt, (n, dn, op))
-            out[f"{n}{dn}{op}"] = t.float().cpu()
+            out[f"{n}{dn}{op}"] = t.float().cpu().numpy().tobytes()
             it += 1
         # back-to-back reuse of the same slots (parity flips, epochs advance), out of place
         for k in range(40):

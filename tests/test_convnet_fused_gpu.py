@@ -45,7 +45,17 @@ def test_convnet_fused_fwd_bwd(C, dtype, B, N):
     x = torch.rand(B, 1, 28, 28, generator=g).to(DEV)
     assert convnet_fused.supported(m, x)
     out = convnet_fused.convnet_forward(m, x, cdtype=dtype)
+    bn_out = {}  # float64 BN outputs (pre-ReLU) and their grads: the size of one routing flip
+    def keep(k):
+        def hook(mod, inp, o):
+            o.retain_grad()
+            bn_out[k] = (inp[0], o)
+        return hook
+
+    hooks = [bnm.register_forward_hook(keep(k)) for k, bnm in (("layer1", m64.layer1[1]), ("layer2", m64.layer2[1]))]
     ref = _torch_fwd(m64, x.double())
+    for h in hooks:
+        h.remove()
     if dtype == torch.float32:
         ref_t = _torch_fwd(mt, x)
     else:
@@ -76,16 +86,40 @@ def test_convnet_fused_fwd_bwd(C, dtype, B, N):
     named_t = dict(mt.named_parameters())
     for (n, p), (_, q) in zip(m.named_parameters(), m64.named_parameters()):
         assert p.grad is not None and p.grad.shape == p.shape, n
-        if n.endswith("0.bias"):  # conv bias grad is ~0 analytically (BN follows): absolute bound
+        if n.endswith("0.bias"):
+            # conv bias grad is 0 analytically (BN follows), so only noise is compared.
+            # In low precision the fused op normalises the stored (rounded) conv output
+            # with statistics of the unrounded fp32 accumulators, so its sum(xhat) over
+            # the batch is a random walk of rounding errors rather than ~0: allow 4x
+            # torch's noise (which normalises with statistics of the rounded values)
             e = (p.grad.double() - q.grad).abs().max().item()
-            lim = 2.0 * (named_t[n].grad.double() - q.grad).abs().max().item() + (1e-4 if not lp else 1e-2)
+            lim = (2.0 if not lp else 4.0) * (named_t[n].grad.double() - q.grad).abs().max().item() + \
+                (1e-4 if not lp else 1e-2)
             assert e < lim, (n, e, lim)
             continue
-        # fp32 at B=100: a pooled value within an ulp of the ReLU threshold / of its
-        # window neighbour can route differently from the float64 reference (for
-        # either implementation); one such flip moves a BN1 grad by ~1e-4
-        floor = (1e-5 if B <= 32 else 2e-4) if not lp else 2e-3
-        bound(p.grad, q.grad, named_t[n].grad, floor, n)
+        if not lp and n.split(".")[1] == "1":
+            # BN affine grads in fp32: a value within an ulp of the ReLU threshold or of
+            # its pool-window neighbour can route differently from the float64
+            # reference (for either implementation: ~1 such element per 1e6 at these
+            # sizes).  One flip moves d(beta) by one |dy| and d(gamma) by one |dy*xhat|,
+            # so allow up to 2 flips per channel on top of torch's own error.
+            _, o = bn_out[n.split(".")[0]]
+            dy = o.grad
+            xhat = (o.detach() - bn_out_beta(m64, n)) / bn_out_gamma(m64, n)
+            step = (dy * xhat if n.endswith("weight") else dy).abs().amax(dim=(0, 2, 3))
+            e = (p.grad.double() - q.grad).abs()
+            lim = 2.0 * (named_t[n].grad.double() - q.grad).abs() + 2.0 * step + 1e-6
+            assert bool((e <= lim).all()), (n, e.max().item(), (e / lim).max().item())
+            continue
+        bound(p.grad, q.grad, named_t[n].grad, 1e-5 if not lp else 2e-3, n)
+
+
+def bn_out_gamma(m, name):
+    return getattr(m, name.split(".")[0])[1].weight.detach().view(1, -1, 1, 1)
+
+
+def bn_out_beta(m, name):
+    return getattr(m, name.split(".")[0])[1].bias.detach().view(1, -1, 1, 1)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
