@@ -45,8 +45,8 @@ PYBIND11_MODULE(_C, m) {
   dpa::register_head(m);
   dpa::register_optim(m);
   dpa::register_data(m);
-  dpa::register_xgmi(m);
   dpa::register_comm(m);
+  dpa::register_xgmi(m);
   dpa::register_reducer(m);
   dpa::register_convnet_fused(m);
   dpa::register_runtime(m);

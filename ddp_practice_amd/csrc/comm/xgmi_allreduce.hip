@@ -304,6 +304,47 @@ void XgmiComm::abort() {
 
 }  // namespace xgmi
 
+// The engine as the reducer's Collective (csrc/ddp/reducer.cpp): async
+// all-reduces on a side stream fenced by events, like the RCCL communicator.
+// Used when every all-reduce of a run fits the engine (multi-process runs on
+// one GPU in the test tier, where RCCL refuses duplicate devices).
+class XgmiCollective : public Collective {
+ public:
+  explicit XgmiCollective(std::shared_ptr<xgmi::XgmiComm> x)
+      : x_(std::move(x)), stream_(c10::hip::getStreamFromPool(/*isHighPriority=*/true, x_->device())) {
+    for (int i = 0; i < kSlots; ++i) DPA_CHECK_HIP(hipEventCreateWithFlags(&slot_[i], hipEventDisableTiming));
+    for (int i = 0; i < kRing; ++i) DPA_CHECK_HIP(hipEventCreateWithFlags(&fork_[i], hipEventDisableTiming));
+  }
+  ~XgmiCollective() override {
+    for (auto& e : slot_) if (e) (void)hipEventDestroy(e);
+    for (auto& e : fork_) if (e) (void)hipEventDestroy(e);
+  }
+  int rank() const override { return x_->rank(); }
+  int world() const override { return x_->world(); }
+  void all_reduce_async(at::Tensor t, RedOp op, int slot) override {
+    TORCH_CHECK(slot >= 0 && slot < kSlots, "slot out of range");
+    const int i = next_++ % kRing;
+    DPA_CHECK_HIP(hipEventRecord(fork_[i], cur_stream()));
+    DPA_CHECK_HIP(hipStreamWaitEvent(stream_.stream(), fork_[i], 0));
+    x_->all_reduce(t, t, op, stream_.stream());
+    DPA_CHECK_HIP(hipEventRecord(slot_[slot], stream_.stream()));
+  }
+  void wait(int slot, hipStream_t stream) override {
+    TORCH_CHECK(slot >= 0 && slot < kSlots, "slot out of range");
+    DPA_CHECK_HIP(hipStreamWaitEvent(stream ? stream : cur_stream(), slot_[slot], 0));
+  }
+  std::string async_error() override { return x_->error_string(); }
+  void abort_now() override { x_->abort(); }
+
+ private:
+  static constexpr int kSlots = 256, kRing = 64;
+  std::shared_ptr<xgmi::XgmiComm> x_;
+  c10::hip::HIPStream stream_;
+  hipEvent_t slot_[kSlots] = {};
+  hipEvent_t fork_[kRing] = {};
+  int next_ = 0;
+};
+
 void register_xgmi(pybind11::module& m) {
   namespace py = pybind11;
   auto s = m.def_submodule("xgmi", "one-shot all-reduce over xGMI peer-mapped workspaces");
@@ -329,6 +370,9 @@ void register_xgmi(pybind11::module& m) {
       .def_property_readonly("workspace_bytes", &xgmi::XgmiComm::workspace_bytes)
       .def_property_readonly("rank", &xgmi::XgmiComm::rank)
       .def_property_readonly("world_size", &xgmi::XgmiComm::world);
+  // registered after comm.Collective (bind.cpp registers comm first)
+  py::class_<XgmiCollective, Collective, std::shared_ptr<XgmiCollective>>(s, "XgmiCollective")
+      .def(py::init<std::shared_ptr<xgmi::XgmiComm>>());
 }
 
 }  // namespace dpa

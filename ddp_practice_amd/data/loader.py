@@ -84,8 +84,13 @@ class DeviceLoader:
     # --------------------------------------------------------- device path
     def start_epoch(self) -> torch.Tensor:
         """Upload this epoch's order and reset the device step counter."""
-        order = self.epoch_order().to(self.device, non_blocking=False)
-        self._order = order
+        order = self.epoch_order()
+        if self._order is None or self._order.shape != order.shape:
+            self._order = order.to(self.device)
+        else:
+            # in place: captured hipGraphs hold this buffer's address
+            self._order.copy_(order)
+        order = self._order
         if self._ctr is None:
             self._ctr = torch.zeros(2, dtype=torch.int32, device=self.device)
         else:

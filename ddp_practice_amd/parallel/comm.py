@@ -259,6 +259,78 @@ class RcclCommunicator(Communicator):
         self._c.destroy()
 
 
+class XgmiCommunicator(Communicator):
+    """All-reduce-only communicator on the one-shot xGMI engine.
+
+    Every all-reduce (DDP buckets through the C++ reducer, SyncBN statistics)
+    runs on the engine; the rare host-side collectives (broadcast at DDP
+    construction, metric reduce, barrier) go through the torch process group
+    (gloo).  This is what lets several processes share ONE GPU in the test tier
+    (RCCL refuses duplicate devices); on a node, ``RcclCommunicator`` attaches
+    the same engine for its small all-reduces.
+    """
+
+    def __init__(self, rank: int, world_size: int, device: torch.device, store=None, key: str = "dpa_xgmi",
+                 max_bytes: int = 4 << 20, group=None):
+        C = _load_ext()
+        self.rank, self.world_size = rank, world_size
+        self.device = torch.device(device)
+        self.group = group
+        if store is None:
+            store = dist.distributed_c10d._get_default_store()
+        x, err = open_xgmi(rank, world_size, self.device, store, key, max_bytes,
+                           float(os.environ.get("DPA_XGMI_TIMEOUT", "600")))
+        if x is None:
+            raise RuntimeError(f"xgmi communicator: {err}")
+        self.xgmi = x
+        self._c = C.xgmi.XgmiCollective(x)
+
+    @property
+    def native(self):
+        return self._c
+
+    def all_reduce_(self, t, op="sum"):
+        self.xgmi.all_reduce(t, _op_name(op))
+        return t
+
+    def all_reduce(self, t, op="sum"):
+        out = torch.empty_like(t)
+        self.xgmi.all_reduce(t.contiguous(), _op_name(op), out)
+        return out
+
+    def _host(self, fn, t):
+        h = t.detach().cpu()
+        fn(h)
+        t.copy_(h)
+        return t
+
+    def broadcast_(self, t, src=0):
+        return self._host(lambda h: dist.broadcast(h, src, group=self.group), t)
+
+    def reduce_(self, t, dst=0, op="sum"):
+        return self._host(lambda h: dist.reduce(h, dst, _TORCH_OPS[_op_name(op)], group=self.group), t)
+
+    def all_gather_into_tensor(self, out, inp):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(h, inp.detach().cpu().contiguous(), group=self.group)
+        out.copy_(h)
+        return out
+
+    def barrier(self):
+        torch.cuda.synchronize(self.device)
+        dist.barrier(group=self.group)
+
+    def async_error(self) -> str:
+        return self.xgmi.error_string()
+
+    def abort(self):
+        self.xgmi.abort()
+
+    def destroy(self):
+        torch.cuda.synchronize(self.device)
+        self.xgmi.close()
+
+
 # ------------------------------------------------------------------ xGMI one-shot engine
 XGMI_DEFAULT_MAX_BYTES = 1 << 20  # every ConvNet collective (<= 116 KB); RCCL above
 
@@ -354,7 +426,7 @@ def init_process_group(backend: str | None = None, init_method: str | None = "en
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     backend = backend.lower()
-    torch_backend = "nccl" if backend in ("nccl", "rccl") else backend
+    torch_backend = "nccl" if backend in ("nccl", "rccl") else "gloo" if backend == "xgmi" else backend
     kw = {}
     if timeout is not None:
         kw["timeout"] = timeout
@@ -364,7 +436,12 @@ def init_process_group(backend: str | None = None, init_method: str | None = "en
     if torch_backend == "gloo" and w > 1 and "OMP_NUM_THREADS" not in os.environ:
         # several CPU ranks on one host: do not oversubscribe the cores (torchrun's default too)
         torch.set_num_threads(max(1, (os.cpu_count() or 1) // w))
-    if torch_backend == "nccl":
+    if backend == "xgmi":  # all-reduces on the xGMI engine, host collectives on gloo (see XgmiCommunicator)
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        _GEN += 1
+        _DEFAULT = XgmiCommunicator(r, w, device, key=f"dpa_xgmi_{_GEN}")
+    elif torch_backend == "nccl":
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         _GEN += 1

@@ -1,0 +1,130 @@
+"""Worker for tests/test_xgmi_ddp_gpu.py: DDP + SyncBN ConvNet training with W
+processes on ONE GPU, every all-reduce (SyncBN statistics, DDP bucket) on the
+xGMI engine, compared with a single-process run on the global batch."""
+import copy
+import hashlib
+import os
+import traceback
+
+import torch
+
+
+def _train(model, ds, batch, scaler_on, use_graph, sampler=None, epochs=2):
+    from ddp_practice_amd.amp import GradScaler
+    from ddp_practice_amd.data import DeviceLoader
+    from ddp_practice_amd.engine import TrainLoop
+    from ddp_practice_amd.nn import CrossEntropyLoss
+    from ddp_practice_amd.optim import SGD
+
+    loader = DeviceLoader(ds, batch_size=batch, shuffle=False, sampler=sampler, device="cuda",
+                          dtype=torch.bfloat16 if scaler_on else torch.float32)
+    opt = SGD(model.parameters(), lr=0.05)
+    scaler = GradScaler() if scaler_on else None
+    loop = TrainLoop(model, CrossEntropyLoss(), opt, loader, scaler, use_graph=use_graph, steps_per_graph=4)
+    for e in range(epochs):
+        if sampler is not None:
+            sampler.set_epoch(e)
+        loop.run_epoch()
+    assert loop.graph_error is None, loop.graph_error
+    return model
+
+
+def _digest(sd):
+    h = hashlib.sha1()
+    for k, v in sd.items():
+        h.update(k.encode())
+        h.update(v.detach().float().cpu().numpy().tobytes())
+    return h.hexdigest()
+
+
+def worker(rank, world, port, amp, graph, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK=str(rank))
+        torch.cuda.set_device(0)
+        import ddp_practice_amd.distributed as dist
+        from ddp_practice_amd.data import DistributedSampler, synthetic
+        from ddp_practice_amd.models import ConvNet
+        from ddp_practice_amd.parallel import DistributedDataParallel, XgmiCommunicator, convert_sync_batchnorm
+
+        c = dist.init_process_group("xgmi")
+        assert isinstance(c, XgmiCommunicator)
+        per_rank = 16
+        ds = synthetic(per_rank * world * 9 + 3 * world, seed=11)  # 9 full steps + a partial step per epoch
+        torch.manual_seed(rank)  # different init per rank: DDP must broadcast rank 0's
+        dt = torch.bfloat16 if amp else None
+        ddp = DistributedDataParallel(convert_sync_batchnorm(ConvNet(amp_dtype=dt).cuda()), device_ids=[0])
+        assert ddp.reducer is not None
+        init = copy.deepcopy(ddp.module.state_dict())
+        # one step, gradients: DDP-averaged grads of the rank batches == grads of the global batch
+        from ddp_practice_amd.ops.head import cross_entropy
+
+        g = torch.Generator().manual_seed(99)
+        gx = torch.rand(per_rank * world, 1, 28, 28, generator=g).cuda()
+        gy = torch.randint(0, 10, (per_rank * world,), generator=g).cuda()
+        one = copy.deepcopy(ddp.module)
+        ddp1 = DistributedDataParallel(one, device_ids=[0])
+        sl = slice(rank * per_rank, (rank + 1) * per_rank)
+        cross_entropy(ddp1(gx[sl].to(dt or torch.float32)), gy[sl]).backward()
+        grads = {k: p.grad.detach().clone() for k, p in one.named_parameters()}
+        del ddp1
+        sampler = DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=True, seed=5)
+        _train(ddp, ds, per_rank, amp, graph, sampler=sampler)
+        torch.cuda.synchronize()
+        assert c.async_error() == "", c.async_error()
+        res = {"digest": _digest(ddp.module.state_dict())}
+        if rank == 0:
+            # the same optimisation on ONE process over the global batch, in the
+            # order the distributed sampler interleaves the ranks' samples
+            from ddp_practice_amd.data import ImageDataset
+
+            plain = ConvNet(amp_dtype=dt).cuda()
+            plain.load_state_dict(init)
+            plain1 = copy.deepcopy(plain)
+            cross_entropy(plain1(gx.to(dt or torch.float32)), gy).backward()
+            gtol = 2e-5 if not amp else 2e-2
+            gerrs = {}
+            for k, p in plain1.named_parameters():
+                if k.endswith("0.bias"):  # analytically 0 (BN follows): noise only
+                    continue
+                gerrs[k] = ((grads[k] - p.grad).norm() / (p.grad.norm() + 1e-12)).item()
+            res["grad_errs"] = gerrs
+            assert all(e < gtol for e in gerrs.values()), gerrs
+            n = len(ds)
+            imgs, labels = [], []
+            for e in range(2):
+                order = torch.randperm(n, generator=torch.Generator().manual_seed(5 + e))
+                shards = [order[r::world] for r in range(world)]
+                for s0 in range(0, n // world, per_rank):
+                    idx = torch.cat([sh[s0:s0 + per_rank] for sh in shards])
+                    imgs.append(ds.images[idx])
+                    labels.append(ds.labels[idx])
+            # one global batch per step: the rank-major concatenation above
+            steps_ds = ImageDataset(torch.cat(imgs), torch.cat(labels))
+            sizes = [len(x) for x in labels]
+            from ddp_practice_amd.engine import TrainLoop  # noqa: F401
+            pos = 0
+            ref = plain
+            for sz in sizes:
+                sub = ImageDataset(steps_ds.images[pos:pos + sz], steps_ds.labels[pos:pos + sz])
+                _train(ref, sub, sz, amp, False, epochs=1)
+                pos += sz
+            # 20 SGD steps at lr 0.05 amplify reduction-order differences (the conv1
+            # weight grad is a sum of ~B*784 cancelling terms): a loose trajectory check
+            tol = 2e-3 if not amp else 6e-2
+            errs = {}
+            for (k, p), (_, r) in zip(ddp.module.state_dict().items(), ref.state_dict().items()):
+                if p.dtype.is_floating_point:
+                    errs[k] = ((p.float() - r.float()).norm() / (r.float().norm() + 1e-6)).item()
+                else:
+                    assert torch.equal(p, r), (k, p, r)
+            res["errs"] = errs
+            assert all(e < tol for e in errs.values()), errs
+        dist.destroy_process_group()
+        q.put((rank, "ok", res))
+    except Exception:  # pragma: no cover - reported to the parent
+        q.put((rank, "err", traceback.format_exc()))
+    finally:
+        q.close()
+        q.join_thread()
+        os._exit(0)
