@@ -155,13 +155,13 @@ class RcclComm : public Collective {
       TORCH_CHECK(dst.numel() == t.numel() && dst.scalar_type() == t.scalar_type());
     }
     const RedOp rop = parse_op(op);
-    if (use_xgmi(t, dst, rop)) {  // one kernel on the caller's stream, no fork/join
-      xgmi_->all_reduce(t, dst, rop, cur_stream());
-      return dst;
-    }
+    // on the comm stream like every collective: one total order per rank = issue order
     fenced([&](hipStream_t s) {
-      DPA_NCCL(ncclAllReduce(t.data_ptr(), dst.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(rop),
-                             comm_.load(), s));
+      if (use_xgmi(t, dst, rop))
+        xgmi_->all_reduce(t, dst, rop, s);
+      else
+        DPA_NCCL(ncclAllReduce(t.data_ptr(), dst.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(rop),
+                               comm_.load(), s));
     });
     return dst;
   }

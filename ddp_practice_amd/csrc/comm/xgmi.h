@@ -38,7 +38,7 @@ class XgmiComm {
   std::string error_string() const;
   void abort();       // every waiting block gives up (watchdog path)
   void set_timeout(double s) { timeout_ticks_ = (long long)(s * 1e8); }
-  long long max_bytes() const { return slot_bytes_; }
+  long long max_bytes() const { return max_elems_ * 4; }  // as fp32
   long long workspace_bytes() const { return ws_bytes_; }
   int rank() const { return rank_; }
   int world() const { return world_; }
@@ -46,7 +46,7 @@ class XgmiComm {
 
  private:
   int rank_, world_, device_;
-  long long slot_bytes_ = 0, flags_off_ = 0, ctr_off_ = 0, ws_bytes_ = 0, timeout_ticks_ = 0;
+  long long max_elems_ = 0, slot_bytes_ = 0, ctr_off_ = 0, ws_bytes_ = 0, timeout_ticks_ = 0;
   int max_blocks_ = 0;
   char* local_ = nullptr;
   Peers peers_;

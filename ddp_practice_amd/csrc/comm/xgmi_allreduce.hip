@@ -13,25 +13,28 @@
 // (ProcessGroupNCCL in the reference: /root/reference/ddp_main.py:73, and the
 // all-reduces inside DDP / SyncBatchNorm, SURVEY.md §2.2 U-PG / U-RED / U-SBN).
 //
-// Protocol (per block b of the grid; blocks are independent, no grid sync):
-//   ep  = ctr[b] + 1                      ctr[b]: this rank's count of collectives
-//                                          that had a block b (same on every rank:
-//                                          every rank issues the same sequence)
-//   par = ep & 1                           double-buffered slots/flags
-//   1. store my chunk b into slot[par][me] of EVERY rank (incl. me)
-//   2. system-scope release; flag[par][me][b] = ep on every rank
-//   3. poll my flags[par][p][b] == ep for all p (bounded: timeout/abort -> error word)
-//   4. system-scope acquire; out[chunk b] = op over p = 0..W-1 of slot[par][p]
-//      (same order on every rank -> bit-identical results everywhere)
-//   5. ctr[b] = ep
-// Reuse safety: a rank writes slot parity par of epoch ep+2 only after it saw
-// every peer's flag for ep+1, which each peer raised after finishing ep.
+// Protocol (per block b of the grid, 2048 elements per block; blocks are
+// independent, no grid sync):
+//   ep  = ctr[b] + 1      ctr[b]: this rank's count of collectives that had a
+//                         block b (equal on every rank: every rank issues the
+//                         same sequence of collectives, stream-ordered)
+//   par = ep & 1          double-buffered slots
+//   1. each lane turns its 8 elements into 8-byte granules {fp32 value, ep} and
+//      stores them into slot[par][me] of EVERY rank (incl. me) over xGMI
+//   2. each lane polls its granules in slot[par][p] for p = 0..W-1 until their
+//      tag is ep (bounded: timeout/abort -> host-visible error word), and
+//      reduces them in rank order (bit-identical results on every rank)
+//   3. ctr[b] = ep
+// A granule is written by one naturally aligned 8-byte store, so value and tag
+// arrive together: no flag, no release/acquire fence, one xGMI hop of latency
+// (MI355X_MICROARCH.md "handoff-1to1" vs "handoff-flag").  Reuse safety: a rank
+// writes parity par of epoch ep+2 only after reading every peer's ep+1
+// granules, which each peer wrote after its kernel for ep had completed.
 //
-// Workspaces are hipExtMallocWithFlags(hipDeviceMallocUncached): neither side
-// caches them in its XCD L2, so the only ordering needed is the system-scope
-// release/acquire pair around the flag.  Everything is enqueue-only (a kernel
-// launch), so a collective can be captured into a hipGraph and replayed: the
-// epoch lives in device memory and advances on replay.
+// Workspaces are hipExtMallocWithFlags(hipDeviceMallocUncached): no XCD L2
+// holds a stale line of them; polls are sc0 sc1 (L1-bypassing) loads.
+// Everything is enqueue-only (one kernel launch), so a collective can be
+// captured into a hipGraph and replayed: the epoch lives in device memory.
 #include <c10/hip/HIPGuard.h>
 
 #include <atomic>
@@ -44,29 +47,27 @@ namespace dpa {
 namespace xgmi {
 
 constexpr int kThreads = 256;
-constexpr int kVecBytes = 16;                         // one 16-B store per lane per rank
-constexpr int kChunkBytes = kThreads * kVecBytes * 2;  // 8 KB of payload per block
+constexpr int kPerThread = 8;                        // elements per lane
+constexpr int kChunkElems = kThreads * kPerThread;   // 2048 elements per block
+
+typedef __attribute__((ext_vector_type(2))) unsigned long long u64x2;
 
 struct Args {
   Peers peers;
-  const char* in;
-  char* out;
-  long long nbytes;         // payload bytes (multiple of the element size)
-  long long slot_bytes;     // per-rank slot size in the workspace
-  long long flags_off;      // byte offset of the flag array in every workspace
-  long long ctr_off;        // byte offset of this rank's epoch counters
-  int rank, world, max_blocks;
+  const void* in;
+  void* out;
+  long long n;              // elements
+  long long slot_bytes;     // per-rank slot (granules) in the workspace
+  long long ctr_off;        // byte offset of this rank's per-block epoch counters
+  int rank, world;
   int* err;                 // host-mapped: 0 ok, 1 timeout, 2 aborted
   const int* abort_flag;    // host-mapped: non-zero -> stop waiting
   long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
 };
 
-__device__ __forceinline__ uint32_t* flag_ptr(char* ws, const Args& a, int par, int src, int b) {
-  return reinterpret_cast<uint32_t*>(ws + a.flags_off) + ((size_t)(par * kMaxRanks + src) * a.max_blocks + b);
+__device__ __forceinline__ unsigned long long granule(float v, uint32_t ep) {
+  return ((unsigned long long)ep << 32) | (unsigned long long)__float_as_uint(v);
 }
-
-template <typename T>
-__device__ __forceinline__ float to_f(T v) { return Cvt<T>::to_f(v); }
 
 // op: 0 sum, 1 avg, 2 max, 3 min
 template <typename T, int OP>
@@ -74,120 +75,103 @@ __global__ __launch_bounds__(kThreads) void oneshot_kernel(Args a) {
   const int b = blockIdx.x, tid = threadIdx.x;
   char* mine = a.peers.base[a.rank];
   uint32_t* ctr = reinterpret_cast<uint32_t*>(mine + a.ctr_off) + b;
-  __shared__ uint32_t s_ep;
-  __shared__ int s_fail;
-  if (tid == 0) {
-    s_ep = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-    s_fail = 0;
-  }
-  __syncthreads();
-  const uint32_t ep = s_ep;
-  const int par = ep & 1;
-  const long long c0 = (long long)b * kChunkBytes;
-  const long long cb = min((long long)kChunkBytes, a.nbytes - c0);
-  const long long slot0 = (long long)par * kMaxRanks * a.slot_bytes;
+  const uint32_t ep = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const long long par_off = (long long)(ep & 1) * kMaxRanks * a.slot_bytes;
+  const long long e0 = (long long)b * kChunkElems + (long long)tid * kPerThread;
+  const int ne = (int)max(0LL, min((long long)kPerThread, a.n - e0));
 
-  // 1. push my chunk into slot[par][me] of every rank
-  f32x4 v[2];
-  int have[2];
+  // 1. my elements -> {value, epoch} granules in slot[parity][me] of every rank
+  float v[kPerThread];
+  const T* in = static_cast<const T*>(a.in) + e0;
+  if (ne == kPerThread) {
+    if constexpr (sizeof(T) == 4) {
+      const f32x4 x0 = reinterpret_cast<const f32x4*>(in)[0], x1 = reinterpret_cast<const f32x4*>(in)[1];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const long long o = (long long)(k * kThreads + tid) * kVecBytes;
-    have[k] = o < cb;
-    if (cb - o >= kVecBytes) {
-      v[k] = *reinterpret_cast<const f32x4*>(a.in + c0 + o);
-    } else if (have[k]) {  // ragged tail: never read past the tensor
-      v[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const uint16_t* src = reinterpret_cast<const uint16_t*>(a.in + c0 + o);
-      uint16_t* d = reinterpret_cast<uint16_t*>(&v[k]);
-      for (int j = 0; j < (int)((cb - o) >> 1); ++j) d[j] = src[j];
+      for (int j = 0; j < 4; ++j) { v[j] = x0[j]; v[4 + j] = x1[j]; }
+    } else {
+      const f32x4 raw = *reinterpret_cast<const f32x4*>(in);
+      const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+      for (int j = 0; j < kPerThread; ++j) v[j] = Cvt<T>::to_f(e[j]);
     }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kPerThread; ++j) v[j] = j < ne ? Cvt<T>::to_f(in[j]) : 0.f;
   }
   for (int p = 0; p < a.world; ++p) {
-    char* dst = a.peers.base[p] + slot0 + (long long)a.rank * a.slot_bytes + c0;
+    unsigned long long* dst =
+        reinterpret_cast<unsigned long long*>(a.peers.base[p] + par_off + (long long)a.rank * a.slot_bytes) + e0;
+    if (ne == kPerThread) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k)
-      if (have[k]) *reinterpret_cast<f32x4*>(dst + (long long)(k * kThreads + tid) * kVecBytes) = v[k];
+      for (int j = 0; j < kPerThread; j += 2)
+        *reinterpret_cast<u64x2*>(dst + j) = u64x2{granule(v[j], ep), granule(v[j + 1], ep)};
+    } else {
+      for (int j = 0; j < ne; ++j) dst[j] = granule(v[j], ep);
+    }
   }
-  // 2. release (every storing lane), then one lane per destination raises the flag
-  __threadfence_system();
-  __syncthreads();
-  if (tid < a.world) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(flag_ptr(a.peers.base[tid], a, par, a.rank, b), ep, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  // 3. wait for every rank's chunk b: one lane of wave 0 per source rank, bounded;
-  //    wave 0 then acquires (invalidates this CU's caches) before the barrier
-  if (tid < 64) {
-    if (tid < a.world) {
-      const uint32_t* f = flag_ptr(mine, a, par, tid, b);
-      const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-      unsigned polls = 0;
-      while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != ep) {
+
+  // 2. every rank's granules for my elements, in rank order (identical result on
+  //    every rank); each granule carries its own epoch tag: no flag, no fence
+  float acc[kPerThread];
+  bool fail = false;
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  unsigned polls = 0;
+  for (int p = 0; p < a.world && !fail; ++p) {
+    const unsigned long long* src =
+        reinterpret_cast<const unsigned long long*>(mine + par_off + (long long)p * a.slot_bytes) + e0;
+    for (int j = 0; j < ne; ++j) {
+      unsigned long long g;
+      while (((g = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) >> 32) != ep) {
         __builtin_amdgcn_s_sleep(1);
-        if ((++polls & 1023u) == 0) {
+        if ((++polls & 255u) == 0) {
           int why = 0;
           if (__hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) why = 2;
           else if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) why = 1;
           if (why) {
             __hip_atomic_store(a.err, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            s_fail = 1;
+            fail = true;
             break;
           }
         }
       }
+      if (fail) break;
+      const float x = __uint_as_float((uint32_t)g);
+      if (p == 0) acc[j] = x;
+      else if (OP == 2) acc[j] = fmaxf(acc[j], x);
+      else if (OP == 3) acc[j] = fminf(acc[j], x);
+      else acc[j] += x;
     }
-    __threadfence_system();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  __syncthreads();
-  if (s_fail) return;  // fatal: the host sees the error word; epochs are no longer consistent
-
-  // 4. reduce the W slots in rank order (identical on every rank)
-  constexpr int E = kVecBytes / sizeof(T);
+  if (!fail) {
+    T* out = static_cast<T*>(a.out) + e0;
+    const float s = OP == 1 ? 1.f / (float)a.world : 1.f;
+    if (ne == kPerThread && sizeof(T) == 2) {
+      f32x4 raw;
+      T* r = reinterpret_cast<T*>(&raw);
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    if (!have[k]) continue;
-    const long long o = c0 + (long long)(k * kThreads + tid) * kVecBytes;
-    const int ne = (int)min((long long)E, (cb - (long long)(k * kThreads + tid) * kVecBytes) / (long long)sizeof(T));
-    float acc[E];
-    for (int p = 0; p < a.world; ++p) {
-      const f32x4 raw = *reinterpret_cast<const f32x4*>(mine + slot0 + (long long)p * a.slot_bytes + o);
-      const T* e = reinterpret_cast<const T*>(&raw);
-#pragma unroll
-      for (int j = 0; j < E; ++j) {
-        const float x = to_f<T>(e[j]);
-        if (p == 0) acc[j] = x;
-        else if (OP == 2) acc[j] = fmaxf(acc[j], x);
-        else if (OP == 3) acc[j] = fminf(acc[j], x);
-        else acc[j] += x;
-      }
-    }
-    T* dst = reinterpret_cast<T*>(a.out + o);
-    if (ne == E) {
-      f32x4 res;
-      T* r = reinterpret_cast<T*>(&res);
-#pragma unroll
-      for (int j = 0; j < E; ++j) r[j] = Cvt<T>::from_f(OP == 1 ? acc[j] / (float)a.world : acc[j]);
-      *reinterpret_cast<f32x4*>(dst) = res;
+      for (int j = 0; j < kPerThread; ++j) r[j] = Cvt<T>::from_f(acc[j] * s);
+      *reinterpret_cast<f32x4*>(out) = raw;
+    } else if (ne == kPerThread) {
+      reinterpret_cast<f32x4*>(out)[0] = f32x4{acc[0] * s, acc[1] * s, acc[2] * s, acc[3] * s};
+      reinterpret_cast<f32x4*>(out)[1] = f32x4{acc[4] * s, acc[5] * s, acc[6] * s, acc[7] * s};
     } else {
-      for (int j = 0; j < ne; ++j) dst[j] = Cvt<T>::from_f(OP == 1 ? acc[j] / (float)a.world : acc[j]);
+      for (int j = 0; j < ne; ++j) out[j] = Cvt<T>::from_f(acc[j] * s);
     }
   }
-  // 5. this block's epoch is done
+  // 3. this block's epoch is done (after every lane read the counter)
   __syncthreads();
-  if (tid == 0) __hip_atomic_store(ctr, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0 && !fail) __hip_atomic_store(ctr, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 XgmiComm::XgmiComm(int rank, int world, int device, long long slot_bytes, double timeout_s)
     : rank_(rank), world_(world), device_(device) {
   TORCH_CHECK(world >= 1 && world <= kMaxRanks, "xgmi: 1..", kMaxRanks, " ranks");
   TORCH_CHECK(rank >= 0 && rank < world);
-  slot_bytes_ = ((std::max(slot_bytes, 1LL) + kChunkBytes - 1) / kChunkBytes) * kChunkBytes;
-  max_blocks_ = (int)(slot_bytes_ / kChunkBytes);
-  flags_off_ = 2LL * kMaxRanks * slot_bytes_;
-  ctr_off_ = flags_off_ + 2LL * kMaxRanks * max_blocks_ * 4;
+  // max_bytes is counted as fp32 elements; every element travels as an 8-B granule
+  max_elems_ = ((std::max(slot_bytes, 4LL) / 4 + kChunkElems - 1) / kChunkElems) * kChunkElems;
+  max_blocks_ = (int)(max_elems_ / kChunkElems);
+  slot_bytes_ = max_elems_ * 8;
+  ctr_off_ = 2LL * kMaxRanks * slot_bytes_;
   ws_bytes_ = ((ctr_off_ + (long long)max_blocks_ * 4 + 4095) / 4096) * 4096;
   timeout_ticks_ = (long long)(timeout_s * 1e8);
   c10::hip::HIPGuard guard(device_);
@@ -247,30 +231,28 @@ void XgmiComm::open(std::vector<std::string> handles) {
 bool XgmiComm::supports(const at::Tensor& t) const {
   const auto st = t.scalar_type();
   return opened_ && t.is_cuda() && t.get_device() == device_ && t.is_contiguous() &&
-         (st == at::kFloat || st == at::kBFloat16 || st == at::kHalf) && t.nbytes() > 0 &&
-         (long long)t.nbytes() <= slot_bytes_ && (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0;
+         (st == at::kFloat || st == at::kBFloat16 || st == at::kHalf) && t.numel() > 0 &&
+         (long long)t.numel() <= max_elems_ && (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0;
 }
 
 void XgmiComm::all_reduce(const at::Tensor& in, const at::Tensor& out, RedOp op, hipStream_t stream) {
-  TORCH_CHECK(supports(in) && supports(out) && in.nbytes() == out.nbytes() &&
+  TORCH_CHECK(supports(in) && supports(out) && in.numel() == out.numel() &&
                   in.scalar_type() == out.scalar_type(),
               "xgmi all_reduce: unsupported tensor (device/dtype/size/alignment)");
   TORCH_CHECK(op != RedOp::PROD, "xgmi all_reduce: prod is not supported");
   Args a;
   a.peers = peers_;
-  a.in = static_cast<const char*>(in.data_ptr());
-  a.out = static_cast<char*>(out.data_ptr());
-  a.nbytes = (long long)in.nbytes();
+  a.in = in.data_ptr();
+  a.out = out.data_ptr();
+  a.n = in.numel();
   a.slot_bytes = slot_bytes_;
-  a.flags_off = flags_off_;
   a.ctr_off = ctr_off_;
   a.rank = rank_;
   a.world = world_;
-  a.max_blocks = max_blocks_;
   a.err = dev_words_;
   a.abort_flag = dev_words_ + 1;
   a.timeout_ticks = timeout_ticks_;
-  const int grid = (int)((a.nbytes + kChunkBytes - 1) / kChunkBytes);
+  const int grid = (int)((a.n + kChunkElems - 1) / kChunkElems);
   hipStream_t s = stream ? stream : cur_stream();
   const int o = op == RedOp::SUM ? 0 : op == RedOp::AVG ? 1 : op == RedOp::MAX ? 2 : 3;
   auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, s, a); };
@@ -313,11 +295,15 @@ class XgmiCollective : public Collective {
   explicit XgmiCollective(std::shared_ptr<xgmi::XgmiComm> x)
       : x_(std::move(x)), stream_(c10::hip::getStreamFromPool(/*isHighPriority=*/true, x_->device())) {
     for (int i = 0; i < kSlots; ++i) DPA_CHECK_HIP(hipEventCreateWithFlags(&slot_[i], hipEventDisableTiming));
-    for (int i = 0; i < kRing; ++i) DPA_CHECK_HIP(hipEventCreateWithFlags(&fork_[i], hipEventDisableTiming));
+    for (int i = 0; i < kRing; ++i) {
+      DPA_CHECK_HIP(hipEventCreateWithFlags(&fork_[i], hipEventDisableTiming));
+      DPA_CHECK_HIP(hipEventCreateWithFlags(&join_[i], hipEventDisableTiming));
+    }
   }
   ~XgmiCollective() override {
     for (auto& e : slot_) if (e) (void)hipEventDestroy(e);
     for (auto& e : fork_) if (e) (void)hipEventDestroy(e);
+    for (auto& e : join_) if (e) (void)hipEventDestroy(e);
   }
   int rank() const override { return x_->rank(); }
   int world() const override { return x_->world(); }
@@ -333,6 +319,17 @@ class XgmiCollective : public Collective {
     TORCH_CHECK(slot >= 0 && slot < kSlots, "slot out of range");
     DPA_CHECK_HIP(hipStreamWaitEvent(stream ? stream : cur_stream(), slot_[slot], 0));
   }
+  // stream-synchronous form: on the same side stream as the async ones, so all
+  // collectives of this rank run in issue order
+  void all_reduce(const at::Tensor& in, const at::Tensor& out, RedOp op) {
+    hipStream_t cur = cur_stream();
+    const int i = next_++ % kRing;
+    DPA_CHECK_HIP(hipEventRecord(fork_[i], cur));
+    DPA_CHECK_HIP(hipStreamWaitEvent(stream_.stream(), fork_[i], 0));
+    x_->all_reduce(in, out, op, stream_.stream());
+    DPA_CHECK_HIP(hipEventRecord(join_[i], stream_.stream()));
+    DPA_CHECK_HIP(hipStreamWaitEvent(cur, join_[i], 0));
+  }
   std::string async_error() override { return x_->error_string(); }
   void abort_now() override { x_->abort(); }
 
@@ -342,6 +339,7 @@ class XgmiCollective : public Collective {
   c10::hip::HIPStream stream_;
   hipEvent_t slot_[kSlots] = {};
   hipEvent_t fork_[kRing] = {};
+  hipEvent_t join_[kRing] = {};
   int next_ = 0;
 };
 
@@ -372,7 +370,14 @@ void register_xgmi(pybind11::module& m) {
       .def_property_readonly("world_size", &xgmi::XgmiComm::world);
   // registered after comm.Collective (bind.cpp registers comm first)
   py::class_<XgmiCollective, Collective, std::shared_ptr<XgmiCollective>>(s, "XgmiCollective")
-      .def(py::init<std::shared_ptr<xgmi::XgmiComm>>());
+      .def(py::init<std::shared_ptr<xgmi::XgmiComm>>())
+      .def("all_reduce",
+           [](XgmiCollective& c, at::Tensor t, const std::string& op, c10::optional<at::Tensor> out) {
+             at::Tensor dst = out.has_value() ? *out : t;
+             c.all_reduce(t, dst, parse_op(op));
+             return dst;
+           },
+           py::arg("t"), py::arg("op") = "sum", py::arg("out") = py::none());
 }
 
 }  // namespace dpa

@@ -202,7 +202,7 @@ class RcclCommunicator(Communicator):
         self._c = C.comm.RcclComm(bytes(uid), rank, world_size, self.device.index)
         self.xgmi = None
         self.xgmi_status = "off (world_size 1)" if world_size == 1 else "off"
-        if world_size > 1:
+        if world_size > 1 or self.force_active:
             self.xgmi_status = setup_xgmi(self, store, key)
 
     @property
@@ -290,12 +290,12 @@ class XgmiCommunicator(Communicator):
         return self._c
 
     def all_reduce_(self, t, op="sum"):
-        self.xgmi.all_reduce(t, _op_name(op))
+        self._c.all_reduce(t, _op_name(op))
         return t
 
     def all_reduce(self, t, op="sum"):
         out = torch.empty_like(t)
-        self.xgmi.all_reduce(t.contiguous(), _op_name(op), out)
+        self._c.all_reduce(t.contiguous(), _op_name(op), out)
         return out
 
     def _host(self, fn, t):
