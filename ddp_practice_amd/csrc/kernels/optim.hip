@@ -122,36 +122,43 @@ __global__ void update_scale_kernel(float* scale, int* tracker, float* found_inf
   }
 }
 
-// GradScaler.step + SGD + GradScaler.update in ONE single-workgroup launch, for
-// parameter sets small enough that one CU streams them twice in a few us
-// (the ConvNet: 29,034 floats).  Phase 1 decides found_inf for the whole set
-// (a block-wide OR, so no cross-workgroup protocol is needed), phase 2 writes
-// the unscaled grads back (torch semantics) and applies the update only if all
-// grads are finite, phase 3 updates scale / growth tracker and re-arms
-// found_inf.  p0 = param, p1 = grad, p2 = momentum buffer (or null).
-constexpr int FUSED_THR = 1024;
-constexpr int FUSED_U = 4;                        // float4 granules per thread per pass
-constexpr int SEG_SHIFT = 4;                      // 16-granule segments
-constexpr int64_t FUSED_MAX = (int64_t)1 << 18;   // elements handled by the single workgroup
-constexpr int MAX_SEG = (int)((FUSED_MAX / 4) >> SEG_SHIFT) + MAXT;
+// GradScaler.step + SGD + GradScaler.update in ONE launch over a small grid
+// (the ConvNet: 29,034 floats -> 8 workgroups).  Every lane loads its grads,
+// params (and momentum buffers) into registers, the workgroups agree on
+// found_inf through ONE 64-bit device-scope atomic per generation
+// ({arrivals, non-finite workgroups} in one word: no fence, no flag), and then
+// each applies its own slice: unscaled grads written back (torch semantics),
+// the update applied only if every grad is finite, scale / growth tracker
+// updated and found_inf re-armed by workgroup 0.  p0 = param, p1 = grad,
+// p2 = momentum buffer (or null).
+//
+// Grid barrier state `sync` (int64[3], zero-initialised, one per optimizer and
+// grid size): [0] launch counter g, [1 + (g & 1)] this launch's word.  Block 0
+// resets the other parity's word and bumps g after the barrier; the next launch
+// is stream-ordered after this one, so it always finds its word at zero.  The
+// grid (<= FUSED_MAX_BLOCKS of 256 lanes, one per CU at most) is co-resident.
+constexpr int FUSED_THR = 256;
+constexpr int FUSED_U = 4;                                  // float4 granules per lane
+constexpr int FUSED_BLOCK_GRAN = FUSED_THR * FUSED_U;       // 4096 floats per workgroup
+constexpr int FUSED_MAX_BLOCKS = 128;
+constexpr int64_t FUSED_MAX = (int64_t)FUSED_MAX_BLOCKS * FUSED_BLOCK_GRAN * 4;
 
 // The flat index space is in float4 granules; tensor t owns ceil(numel/4)
 // granules starting at chunk_off[t] (every pointer 16-B aligned, checked on the
-// host), so a granule never straddles two tensors and the common case is one
-// 16-B load per operand.  Tensor tables live in LDS: per-lane dynamic indexing
-// of the by-value kernel argument is a chain of dependent global loads per
-// element (measured: 80 us for 29k elements); the segment map turns "which
-// tensor holds granule gi" into one LDS read plus (rarely) a short scan.
+// host), so a granule never straddles two tensors.  Tensor tables live in LDS
+// (per-lane dynamic indexing of the by-value kernel argument is a chain of
+// dependent scalar loads).
 __global__ void __launch_bounds__(FUSED_THR)
 amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ tracker, float* __restrict__ found_inf,
-                     float lr, float momentum, float dampening, float wd, int nesterov, int maximize, int first,
-                     float growth, float backoff, int interval) {
+                     unsigned long long* __restrict__ sync, float lr, float momentum, float dampening, float wd,
+                     int nesterov, int maximize, int first, float growth, float backoff, int interval) {
   __shared__ int soff[MAXT + 1];
   __shared__ int snum[MAXT];
   __shared__ float* sp0[MAXT];
   __shared__ float* sp1[MAXT];
   __shared__ float* sp2[MAXT];
-  __shared__ uint8_t seg[MAX_SEG];
+  __shared__ unsigned long long s_gen;
+  __shared__ int s_bad;
   const int tid = threadIdx.x;
   const int n = L.n;
   if (tid <= n) soff[tid] = (int)L.chunk_off[tid];
@@ -161,24 +168,10 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
     sp1[tid] = L.p1[tid];
     sp2[tid] = L.p2[tid];
   }
+  if (tid == 0) s_gen = __hip_atomic_fetch_add(&sync[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   const int total = soff[n];
-  const int nseg = (total + (1 << SEG_SHIFT) - 1) >> SEG_SHIFT;
-  for (int sg = tid; sg < nseg; sg += FUSED_THR) {
-    const int e = sg << SEG_SHIFT;
-    int lo = 0, hi = n - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (soff[mid] <= e) lo = mid; else hi = mid - 1;
-    }
-    seg[sg] = (uint8_t)lo;
-  }
-  __syncthreads();
-  auto locate = [&](int gi) {
-    int t = seg[gi >> SEG_SHIFT];
-    while (soff[t + 1] <= gi) ++t;
-    return t;
-  };
+  const unsigned long long gen = s_gen;
   auto load4 = [](const float* p, int rem) {
     if (rem >= 4) return *reinterpret_cast<const f32x4*>(p);
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -189,66 +182,70 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
     if (rem >= 4) { *reinterpret_cast<f32x4*>(p) = v; return; }
     for (int j = 0; j < rem; ++j) p[j] = v[j];
   };
-
-  const float inv = 1.f / scale[0];
-  bool bad = false;
-  for (int base = 0; base < total; base += FUSED_U * FUSED_THR) {
-    f32x4 v[FUSED_U];
-#pragma unroll
-    for (int k = 0; k < FUSED_U; ++k) {
-      const int gi = base + k * FUSED_THR + tid;
-      v[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (gi < total) {
-        const int t = locate(gi);
-        const int o = (gi - soff[t]) * 4;
-        v[k] = load4(sp1[t] + o, snum[t] - o);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < FUSED_U; ++k)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bad |= !isfinite(v[k][j]);
-  }
-  bad = __syncthreads_or(bad);
   const bool use_buf = momentum != 0.f && !first;
-  for (int base = 0; base < total; base += FUSED_U * FUSED_THR) {
-    f32x4 gv[FUSED_U], pv[FUSED_U], bv[FUSED_U];
-    int tt[FUSED_U], oo[FUSED_U];
+  f32x4 gv[FUSED_U], pv[FUSED_U], bv[FUSED_U];
+  int tt[FUSED_U], oo[FUSED_U];
+  bool bad = false;
 #pragma unroll
-    for (int k = 0; k < FUSED_U; ++k) {
-      const int gi = base + k * FUSED_THR + tid;
-      tt[k] = -1;
-      if (gi < total) {
-        const int t = locate(gi);
-        const int o = (gi - soff[t]) * 4, rem = snum[t] - o;
-        tt[k] = t;
-        oo[k] = o;
-        gv[k] = load4(sp1[t] + o, rem);
-        pv[k] = load4(sp0[t] + o, rem);
-        bv[k] = use_buf ? load4(sp2[t] + o, rem) : f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < FUSED_U; ++k) {
+    const int gi = blockIdx.x * FUSED_BLOCK_GRAN + k * FUSED_THR + tid;
+    tt[k] = -1;
+    if (gi < total) {
+      int lo = 0, hi = n - 1;  // tensor holding granule gi
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (soff[mid] <= gi) lo = mid; else hi = mid - 1;
       }
-    }
+      const int o = (gi - soff[lo]) * 4, rem = snum[lo] - o;
+      tt[k] = lo;
+      oo[k] = o;
+      gv[k] = load4(sp1[lo] + o, rem);
+      pv[k] = load4(sp0[lo] + o, rem);
+      bv[k] = use_buf ? load4(sp2[lo] + o, rem) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < FUSED_U; ++k) {
-      const int t = tt[k];
-      if (t < 0) continue;
-      const int o = oo[k], rem = snum[t] - o;
-      const f32x4 g = gv[k] * inv;
-      store4(sp1[t] + o, rem, g);
-      if (bad) continue;
-      f32x4 d = maximize ? -g : g;
-      if (wd != 0.f) d += wd * pv[k];
-      if (momentum != 0.f) {
-        const f32x4 bb = first ? d : momentum * bv[k] + (1.f - dampening) * d;
-        store4(sp2[t] + o, rem, bb);
-        d = nesterov ? d + momentum * bb : bb;
-      }
-      store4(sp0[t] + o, rem, pv[k] - lr * d);
+      for (int j = 0; j < 4; ++j) bad |= !isfinite(gv[k][j]);
     }
   }
+  const bool block_bad = __syncthreads_or(bad);
   if (tid == 0) {
+    unsigned long long* word = &sync[1 + (gen & 1)];
+    const unsigned long long G = gridDim.x;
+    __hip_atomic_fetch_add(word, 1ull | ((unsigned long long)block_bad << 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long v;
+    while (((v = __hip_atomic_fetch_add(word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & 0xffffffffull) <
+           G)
+      __builtin_amdgcn_s_sleep(1);
+    s_bad = (v >> 32) != 0;
+    if (blockIdx.x == 0) {
+      __hip_atomic_exchange(&sync[1 + ((gen + 1) & 1)], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&sync[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  const bool any_bad = s_bad;
+  const float inv = 1.f / scale[0];
+#pragma unroll
+  for (int k = 0; k < FUSED_U; ++k) {
+    const int t = tt[k];
+    if (t < 0) continue;
+    const int o = oo[k], rem = snum[t] - o;
+    const f32x4 g = gv[k] * inv;
+    store4(sp1[t] + o, rem, g);
+    if (any_bad) continue;
+    f32x4 d = maximize ? -g : g;
+    if (wd != 0.f) d += wd * pv[k];
+    if (momentum != 0.f) {
+      const f32x4 bb = first ? d : momentum * bv[k] + (1.f - dampening) * d;
+      store4(sp2[t] + o, rem, bb);
+      d = nesterov ? d + momentum * bb : bb;
+    }
+    store4(sp0[t] + o, rem, pv[k] - lr * d);
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    // every workgroup read scale[0] before arriving, and block 0 passed the barrier
     found_inf[0] = 0.f;
-    if (bad) {
+    if (any_bad) {
       scale[0] = scale[0] * backoff;
       tracker[0] = 0;
     } else {
@@ -344,12 +341,14 @@ void sgd_step(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std
 void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std::vector<at::Tensor> bufs,
                    double lr, double momentum, double dampening, double wd, bool nesterov, bool maximize, bool first,
                    at::Tensor scale, at::Tensor tracker, at::Tensor found_inf, double growth, double backoff,
-                   int64_t interval) {
+                   int64_t interval, at::Tensor sync) {
   TORCH_CHECK(params.size() == grads.size() && params.size() <= (size_t)MAXT, "fused AMP-SGD: <= ", MAXT,
               " tensors");
   TORCH_CHECK(bufs.empty() || bufs.size() == params.size());
   check_f32(scale); check_f32(found_inf);
   TORCH_CHECK(tracker.scalar_type() == at::kInt);
+  TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == at::kLong && sync.numel() >= 3 && sync.is_contiguous(),
+              "fused AMP-SGD: sync must be a zero-initialised int64[3] device tensor");
   MTList L{};
   L.n = (int)params.size();
   L.chunk_off[0] = 0;
@@ -366,8 +365,10 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
     TORCH_CHECK(al(L.p0[i]) && al(L.p1[i]) && al(L.p2[i]), "fused AMP-SGD needs 16-byte aligned tensors");
   }
   TORCH_CHECK(L.chunk_off[L.n] * 4 <= FUSED_MAX, "fused AMP-SGD handles at most ", FUSED_MAX, " elements");
-  hipLaunchKernelGGL(amp_sgd_fused_kernel, dim3(1), dim3(FUSED_THR), 0, cur_stream(), L, scale.data_ptr<float>(),
-                     tracker.data_ptr<int>(), found_inf.data_ptr<float>(), (float)lr, (float)momentum,
+  const int grid = (int)std::max<int64_t>(1, (L.chunk_off[L.n] + FUSED_BLOCK_GRAN - 1) / FUSED_BLOCK_GRAN);
+  hipLaunchKernelGGL(amp_sgd_fused_kernel, dim3(grid), dim3(FUSED_THR), 0, cur_stream(), L, scale.data_ptr<float>(),
+                     tracker.data_ptr<int>(), found_inf.data_ptr<float>(),
+                     reinterpret_cast<unsigned long long*>(sync.data_ptr<int64_t>()), (float)lr, (float)momentum,
                      (float)dampening, (float)wd, (int)nesterov, (int)maximize, (int)first, (float)growth,
                      (float)backoff, (int)interval);
   DPA_CHECK_LAUNCH();
@@ -419,6 +420,7 @@ void register_optim(pybind11::module& m) {
         pybind11::arg("found_inf") = pybind11::none(), pybind11::arg("grad_scale") = pybind11::none());
   s.def("update_scale", &opt::update_scale);
   s.def("amp_sgd_fused", &opt::amp_sgd_fused);
+  s.attr("FUSED_MAX") = opt::FUSED_MAX;
   s.attr("MAXT") = opt::MAXT;
   s.def("flat_copy", &opt::flat_copy);
 }

@@ -68,7 +68,7 @@ class SGD(Optimizer):
         return loss
 
     # ------------------------------------------------------------------ AMP
-    FUSED_AMP_MAX_NUMEL = 1 << 18
+    FUSED_AMP_MAX_NUMEL = 1 << 19  # csrc/kernels/optim.hip FUSED_MAX
 
     def _collect(self):
         out = []
@@ -90,7 +90,7 @@ class SGD(Optimizer):
 
     def can_fuse_amp(self) -> bool:
         """One parameter group of small f32 device tensors: unscale + inf-check +
-        SGD + scale update fit one single-workgroup launch."""
+        SGD + scale update fit one launch of <= 128 co-resident workgroups."""
         if len(self.param_groups) != 1:
             return False
         ps = [p for p in self.param_groups[0]["params"] if p.grad is not None]
@@ -108,9 +108,14 @@ class SGD(Optimizer):
     @torch.no_grad()
     def fused_amp_step(self, scale, tracker, found_inf, growth, backoff, interval):
         (group, params, grads, bufs, first), = self._collect()
+        sync = getattr(self, "_amp_sync", None)
+        if sync is None or sync.device != params[0].device:
+            # grid-barrier state of the fused kernel (allocated before any graph capture:
+            # the first step runs eagerly)
+            sync = self._amp_sync = torch.zeros(3, dtype=torch.int64, device=params[0].device)
         _load_ext().optim.amp_sgd_fused(params, grads, bufs, group["lr"], group["momentum"], group["dampening"],
                                         group["weight_decay"], group["nesterov"], group["maximize"], first,
-                                        scale, tracker, found_inf, growth, backoff, interval)
+                                        scale, tracker, found_inf, growth, backoff, interval, sync)
 
     @staticmethod
     def _torch_step(group, params, grads, bufs, first):

@@ -217,27 +217,50 @@ def test_gather(C, dtype):
 
 
 @pytest.mark.parametrize("momentum", [0.0, 0.9])
-def test_fused_amp_sgd_matches_unfused(C, momentum):
+@pytest.mark.parametrize("sizes", [(7, 3000, 29034), (5, 200001, 33)])
+def test_fused_amp_sgd_matches_unfused(C, momentum, sizes):
+    """Grid-barrier fused unscale+check+SGD+update == the three unfused kernels, over
+    several launches sharing one barrier state (generations / parity reuse), with
+    non-finite grads injected on some of them, eager and graph-replayed."""
     torch.manual_seed(0)
-    ps = [torch.randn(n, device=DEV) for n in (7, 3000, 29034)]
-    for inject_inf in (False, True):
+    ps = [torch.randn(n, device=DEV) for n in sizes]
+    pa, pb = [p.clone() for p in ps], [p.clone() for p in ps]
+    ba, bb = [torch.zeros_like(p) for p in ps], [torch.zeros_like(p) for p in ps]
+    sa, sb = torch.tensor([512.0], device=DEV), torch.tensor([512.0], device=DEV)
+    ta, tb = torch.zeros(1, dtype=torch.int32, device=DEV), torch.zeros(1, dtype=torch.int32, device=DEV)
+    fa, fb = torch.zeros(1, device=DEV), torch.zeros(1, device=DEV)
+    sync = torch.zeros(3, dtype=torch.int64, device=DEV)
+    ga = [torch.empty_like(p) for p in ps]
+
+    def fused(first):
+        C.optim.amp_sgd_fused(pa, ga, ba, 0.1, momentum, 0.0, 1e-4, False, False, first, sa, ta, fa, 2.0, 0.5, 2,
+                              sync)
+
+    graph = None
+    for it in range(8):
         gs = [torch.randn_like(p) * 512 for p in ps]
-        if inject_inf:
-            gs[2][5] = float("nan")
-        pa, pb = [p.clone() for p in ps], [p.clone() for p in ps]
-        ga, gb = [g.clone() for g in gs], [g.clone() for g in gs]
-        ba, bb = [torch.zeros_like(p) for p in ps], [torch.zeros_like(p) for p in ps]
-        sa, sb = torch.tensor([512.0], device=DEV), torch.tensor([512.0], device=DEV)
-        ta, tb = torch.zeros(1, dtype=torch.int32, device=DEV), torch.zeros(1, dtype=torch.int32, device=DEV)
-        fa, fb = torch.zeros(1, device=DEV), torch.zeros(1, device=DEV)
-        C.optim.amp_sgd_fused(pa, ga, ba, 0.1, momentum, 0.0, 1e-4, False, False, True, sa, ta, fa, 2.0, 0.5, 1)
+        if it in (1, 4, 6):
+            gs[it % len(gs)][it] = float("nan") if it != 4 else float("inf")
+        for x, g in zip(ga, gs):
+            x.copy_(g)
+        gb = [g.clone() for g in gs]
+        first = it == 0
+        if it < 4:
+            fused(first)
+        else:  # graph replay of the same launch (not first: momentum buffers exist)
+            if graph is None:
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    fused(False)
+            graph.replay()
         C.optim.unscale_check(gb, sb, fb)
-        C.optim.sgd_step(pb, gb, bb, 0.1, momentum, 0.0, 1e-4, False, False, True, fb, None)
-        C.optim.update_scale(sb, tb, fb, 2.0, 0.5, 1)
-        for x, y in zip(pa + ga, pb + gb):
+        C.optim.sgd_step(pb, gb, bb, 0.1, momentum, 0.0, 1e-4, False, False, first, fb, None)
+        C.optim.update_scale(sb, tb, fb, 2.0, 0.5, 2)
+        torch.cuda.synchronize()
+        for x, y in zip(pa + ga + ba, pb + gb + bb):
             torch.testing.assert_close(x, y, equal_nan=True)
-        assert sa.item() == sb.item() == (256.0 if inject_inf else 1024.0)
-        assert ta.item() == tb.item() and fa.item() == fb.item() == 0.0
+        assert sa.item() == sb.item() and ta.item() == tb.item() and fa.item() == fb.item() == 0.0, it
+    assert int(sync[0]) == 8  # one generation per launch: 4 eager + 4 graph replays (capture runs nothing)
 
 
 def test_grad_scaler_fast_backward_and_fused_step(C):
