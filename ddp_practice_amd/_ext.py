@@ -9,6 +9,9 @@ the CPU test tier and the ``origin_main.py`` plumbing config use.
 from __future__ import annotations
 
 import importlib
+import importlib.util
+import os
+import sys
 
 _C = None
 _ERR: Exception | None = None
@@ -22,7 +25,14 @@ def load():
     try:
         import torch  # noqa: F401  (loads libamdhip64 / librccl from the torch wheel first)
 
-        _C = importlib.import_module("ddp_practice_amd._C")
+        so = os.environ.get("DPA_EXT_SO")
+        if so:  # experiment build (ddp_practice_amd/build.py DPA_BUILD_TAG), loaded under the same name
+            spec = importlib.util.spec_from_file_location("ddp_practice_amd._C", so)
+            _C = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(_C)
+            sys.modules["ddp_practice_amd._C"] = _C
+        else:
+            _C = importlib.import_module("ddp_practice_amd._C")
     except Exception as e:  # pragma: no cover - exercised only when the build is missing
         _ERR = e
         raise RuntimeError(

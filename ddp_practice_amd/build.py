@@ -24,8 +24,11 @@ from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
-BUILD = PKG.parent / "build" / "native"
-TARGET = PKG / "_C.so"
+# experiment builds: DPA_BUILD_TAG=x [DPA_EXTRA_CFLAGS="-DFOO"] -> ddp_practice_amd/_C_x.so
+# (load it with DPA_EXT_SO=ddp_practice_amd/_C_x.so); the default build is untouched
+_TAG = os.environ.get("DPA_BUILD_TAG", "")
+BUILD = PKG.parent / "build" / ("native" + (f"_{_TAG}" if _TAG else ""))
+TARGET = PKG / (f"_C_{_TAG}.so" if _TAG else "_C.so")
 ARCH = "gfx950"
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
@@ -61,6 +64,7 @@ def _flags():
         "-fno-gpu-rdc", "-munsafe-fp-atomics",
         f"-I{CSRC}", f"-I{sysconfig.get_paths()['include']}",
     ]
+    f += os.environ.get("DPA_EXTRA_CFLAGS", "").split()
     f += [f"-I{d}" for d in inc]
     return f
 

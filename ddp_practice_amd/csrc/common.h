@@ -39,6 +39,23 @@ inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(
 
 #define DPA_CHECK_LAUNCH() DPA_CHECK_HIP(hipGetLastError())
 
+// Phase timestamps for kernel tuning (experiment builds with -DDPA_TIMING only):
+// DPA_STAMP(i) records s_memrealtime (100 MHz) of wave 0 of every workgroup in
+// dpa_stamps[block][i]; read back with runtime.read_stamps().
+#ifdef DPA_TIMING
+#define DPA_MAX_STAMP_BLOCKS 512
+#define DPA_NSTAMPS 16
+// one copy per translation unit (-fno-gpu-rdc): read back from the TU that owns the kernels
+static __device__ unsigned long long dpa_stamps[DPA_MAX_STAMP_BLOCKS * DPA_NSTAMPS];
+#define DPA_STAMP(i)                                                                                     \
+  do {                                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < DPA_MAX_STAMP_BLOCKS)                                           \
+      dpa_stamps[blockIdx.x * DPA_NSTAMPS + (i)] = __builtin_amdgcn_s_memrealtime();                     \
+  } while (0)
+#else
+#define DPA_STAMP(i) do {} while (0)
+#endif
+
 #define DPA_CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a HIP device tensor")
 #define DPA_CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
 #define DPA_CHECK_INPUT(t) \

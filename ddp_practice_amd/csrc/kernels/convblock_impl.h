@@ -130,6 +130,27 @@ struct BNParams {
   int train;
 };
 
+// Sum of src[r * RL + j] over rows r = g, g + G, ...: up to RSUM_U rows per
+// lane are loaded in ONE batch (all loads in flight before the first add), so
+// a slab of up to RSUM_U * G rows costs one L2 round trip instead of one per
+// 4 rows (the partial-sum slabs are 64-256 rows: this was 3-5 serial trips).
+constexpr int RSUM_U = 24;
+__device__ __forceinline__ float strided_rowsum(const float* __restrict__ src, int rows, int RL, int j, int g,
+                                                int G) {
+  float acc = 0.f;
+  for (int base = g; base < rows; base += RSUM_U * G) {
+    float v[RSUM_U];
+#pragma unroll
+    for (int u = 0; u < RSUM_U; ++u) {
+      const int rr = base + u * G;
+      v[u] = rr < rows ? src[(size_t)rr * RL + j] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < RSUM_U; ++u) acc += v[u];
+  }
+  return acc;
+}
+
 // part: >= blockDim.x floats of LDS; ends with __syncthreads().
 template <int C>
 __device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, float* beta_s, float* mean_s,
@@ -139,18 +160,19 @@ __device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, flo
     constexpr int RL = 2 * C + 1;
     const int G = nthr / RL;
     const int j = tid % RL, g = tid / RL;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    if (g < G) {
-      int rr = g;
-      for (; rr + 3 * G < bp.nrows; rr += 4 * G) {
-        a0 += bp.fslab[(size_t)rr * RL + j];
-        a1 += bp.fslab[(size_t)(rr + G) * RL + j];
-        a2 += bp.fslab[(size_t)(rr + 2 * G) * RL + j];
-        a3 += bp.fslab[(size_t)(rr + 3 * G) * RL + j];
+    // per-channel parameters first: their loads overlap the slab reduction's
+    float gam = 0.f, bet = 0.f, shf = 0.f, rm = 0.f, rv = 0.f;
+    if (tid < C) {
+      gam = bp.gamma[tid];
+      bet = bp.beta[tid];
+      shf = bp.fstats[2 * C + 1 + tid];
+      if (leader) {
+        rm = bp.rmean[tid];
+        rv = bp.rvar[tid];
       }
-      for (; rr < bp.nrows; rr += G) a0 += bp.fslab[(size_t)rr * RL + j];
     }
-    part[tid] = (a0 + a1) + (a2 + a3);
+    const int64_t nb0 = leader ? bp.nbt[0] : 0;
+    part[tid] = g < G ? strided_rowsum(bp.fslab, bp.nrows, RL, j, g, G) : 0.f;
     __syncthreads();
     if (tid < RL) {
       float t = 0.f;
@@ -161,26 +183,26 @@ __device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, flo
     if (tid < C) {
       const float n = part[2 * C];
       const float m1 = part[tid] / n;
-      const float mean = bp.fstats[2 * C + 1 + tid] + m1;
+      const float mean = shf + m1;
       const float var = fmaxf(part[C + tid] / n - m1 * m1, 0.f);
       const float istd = rsqrtf(var + bp.eps);
-      const float s = bp.gamma[tid] * istd;
+      const float s = gam * istd;
       sc_s[tid] = s;
-      beta_s[tid] = bp.beta[tid];
+      beta_s[tid] = bet;
       mean_s[tid] = mean;
       istd_s[tid] = istd;
       if (leader) {
         bp.fstats[tid] = part[tid];
         bp.fstats[C + tid] = part[C + tid];
         if (tid == 0) bp.fstats[2 * C] = n;
-        const int64_t nb = bp.nbt[0] + 1;
+        const int64_t nb = nb0 + 1;
         const float mom = bp.momentum >= 0.f ? bp.momentum : 1.f / (float)nb;
-        bp.rmean[tid] = (1.f - mom) * bp.rmean[tid] + mom * mean;
-        bp.rvar[tid] = (1.f - mom) * bp.rvar[tid] + mom * var * (n / fmaxf(n - 1.f, 1.f));
+        bp.rmean[tid] = (1.f - mom) * rm + mom * mean;
+        bp.rvar[tid] = (1.f - mom) * rv + mom * var * (n / fmaxf(n - 1.f, 1.f));
       }
     }
     __syncthreads();
-    if (leader && tid == 0) bp.nbt[0] = bp.nbt[0] + 1;
+    if (leader && tid == 0) bp.nbt[0] = nb0 + 1;
   } else {
     if (tid < C) {
       const float istd = rsqrtf(bp.rvar[tid] + bp.eps);
@@ -261,18 +283,7 @@ __device__ __forceinline__ void colsum_rows(const float* __restrict__ src, int r
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int G = nthr / RL;
   const int j = tid % RL, g = tid / RL;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  if (g < G) {
-    int rr = g;
-    for (; rr + 3 * G < rows; rr += 4 * G) {
-      a0 += src[(size_t)rr * RL + j];
-      a1 += src[(size_t)(rr + G) * RL + j];
-      a2 += src[(size_t)(rr + 2 * G) * RL + j];
-      a3 += src[(size_t)(rr + 3 * G) * RL + j];
-    }
-    for (; rr < rows; rr += G) a0 += src[(size_t)rr * RL + j];
-  }
-  part[tid] = (a0 + a1) + (a2 + a3);
+  part[tid] = g < G ? strided_rowsum(src, rows, RL, j, g, G) : 0.f;
   __syncthreads();
   float t = 0.f;
   if (tid < RL)
@@ -288,15 +299,22 @@ __device__ __forceinline__ void colsum_rows(const float* __restrict__ src, int r
 template <int C, typename T>
 __device__ __forceinline__ void bn_bwd_coef(const BwdIn<T>& bi, float* coef, float* part, float* sums, bool leader) {
   const int tid = threadIdx.x;
+  float n = 0.f, f0 = 0.f, f1 = 0.f, shf = 0.f, gam = 0.f;
+  if (tid < C) {  // issued before the reduction: latencies overlap
+    n = bi.fstats[2 * C];
+    f0 = bi.fstats[tid];
+    f1 = bi.fstats[C + tid];
+    shf = bi.fstats[2 * C + 1 + tid];
+    gam = bi.gamma[tid];
+  }
   colsum_rows(bi.gsum, bi.grows, 2 * C, part, sums);
   if (tid < C) {
-    const float n = bi.fstats[2 * C];
-    const float m1 = bi.fstats[tid] / n;
-    const float mean = bi.fstats[2 * C + 1 + tid] + m1;
-    const float istd = rsqrtf(fmaxf(bi.fstats[C + tid] / n - m1 * m1, 0.f) + bi.eps);
+    const float m1 = f0 / n;
+    const float mean = shf + m1;
+    const float istd = rsqrtf(fmaxf(f1 / n - m1 * m1, 0.f) + bi.eps);
     coef[tid] = sums[tid] / n;
     coef[C + tid] = sums[C + tid] / n;
-    coef[2 * C + tid] = bi.gamma[tid] * istd;
+    coef[2 * C + tid] = gam * istd;
     coef[3 * C + tid] = mean;
     coef[4 * C + tid] = istd;
     if (leader && bi.dgamma != nullptr && bi.lsum == bi.gsum) {
@@ -381,6 +399,42 @@ struct BwdEpi {
 };
 
 // ---------------------------------------------------------------------------
+// Pre-packed low-precision weights of the 16->32 conv (ConvNet layer 2), in
+// exactly the LDS tile layout conv5x5_kernel uses (rows padded to KPW, K
+// padding zeroed): the forward tile [32][424] (k = tap*16 + ci) and the
+// data-grad tile [16][808] (k = (24-tap)*32 + co, the flipped transpose).
+// The layer-1 forward kernel writes them as a side job (its workgroups are
+// idle for most of the chip anyway), so the layer-2 kernels stage their weight
+// tile with straight 16-B copies instead of 12,800 converted, scattered
+// element stores per workgroup (the VALU-heaviest part of their staging).
+// ---------------------------------------------------------------------------
+constexpr int W2F_ROWS = 32, W2F_PITCH = 424;   // ceil_to(25*16, 32) + 8
+constexpr int W2D_ROWS = 16, W2D_PITCH = 808;   // ceil_to(25*32, 32) + 8
+constexpr int W2F_LEN = W2F_ROWS * W2F_PITCH, W2D_LEN = W2D_ROWS * W2D_PITCH;
+template <typename T>
+struct WPack {
+  const float* w2 = nullptr;  // [32][16][5][5] f32 master weights
+  T* fwd = nullptr;           // [W2F_LEN]
+  T* dgrad = nullptr;         // [W2D_LEN]
+};
+template <typename T>
+__device__ __forceinline__ void pack_w2(const WPack<T>& pk) {
+  const int total = W2F_LEN + W2D_LEN;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    if (e < W2F_LEN) {
+      const int co = e / W2F_PITCH, k = e % W2F_PITCH;
+      const float v = k < 400 ? pk.w2[(co * 16 + (k & 15)) * 25 + (k >> 4)] : 0.f;
+      pk.fwd[e] = Cvt<T>::from_f(v);
+    } else {
+      const int e2 = e - W2F_LEN;
+      const int ci = e2 / W2D_PITCH, k = e2 % W2D_PITCH;
+      const float v = k < 800 ? pk.w2[((k & 31) * 16 + ci) * 25 + (24 - (k >> 5))] : 0.f;
+      pk.dgrad[e2] = Cvt<T>::from_f(v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Implicit-GEMM 5x5 convolution, one (image, m-range) per workgroup.
 //   MODE 0: forward + bias + BN partial sums        (train)
 //   MODE 1: forward + bias                          (eval)
@@ -398,12 +452,16 @@ struct BwdEpi {
 //          block (bin: backward through MaxPool -> ReLU -> BN, see BwdIn).
 //   EPI 1: (MODE 2) the output is a pooled grad: also write this workgroup's
 //          BN partial sums [S1 | S2] of the block below (epi).
-template <typename T, int CIN, int COUT, int H, int W, int MODE, int PRO = 0, int EPI = 0>
+//   WPK 0: stage the weight tile from the f32 master weights w;
+//   WPK 1: w is ignored, the tile is copied from the pre-packed wpk (pack_w2);
+//   WPK 2: as 0, and this launch also writes the layer-2 packs (pk).
+template <typename T, int CIN, int COUT, int H, int W, int MODE, int PRO = 0, int EPI = 0, int WPK = 0>
 __global__ void __launch_bounds__(NTHR)
 conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
                T* __restrict__ y, float* __restrict__ fslab, float* __restrict__ fstats,
                const float* __restrict__ shift, int nsplit, PoolIn<T> pin = PoolIn<T>{},
-               BwdIn<T> bin = BwdIn<T>{}, BwdEpi<T> epi = BwdEpi<T>{}) {
+               BwdIn<T> bin = BwdIn<T>{}, BwdEpi<T> epi = BwdEpi<T>{}, const T* __restrict__ wpk = nullptr,
+               WPack<T> pk = WPack<T>{}) {
   static_assert(CIN == 1 || CIN % 8 == 0, "CIN must be 1 or a multiple of 8");
   static_assert(COUT % 16 == 0, "COUT must be a multiple of 16");
   static_assert((H * W) % 4 == 0, "H*W must be a multiple of 4");
@@ -425,27 +483,52 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
 
   const int tid = threadIdx.x;
   const int b = blockIdx.x / nsplit;
+  DPA_STAMP(0);
   const int sp = blockIdx.x % nsplit;
   const T* xb = x + (size_t)b * CIN * HW;
   const int mt0 = (MT * sp) / nsplit, mt1 = (MT * (sp + 1)) / nsplit;
+  // epilogue operands of this lane's channels (co = nt*16 + lane%16), loaded up front
+  float pre_bias[NT], pre_shift[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int co = nt * 16 + (tid & 15);
+    pre_bias[nt] = (MODE == 2) ? 0.f : bias[co];
+    pre_shift[nt] = (MODE == 0) ? shift[co] : 0.f;
+  }
 
   // --- stage weights (batched float4 reads in natural [co][ci][kh][kw] order,
   //     scattered LDS writes to wl[co][(kh*5+kw)*CIN + ci])
   const T zero = Cvt<T>::from_f(0.f);
-  if constexpr (KP > K) {
-    for (int e = tid; e < COUT * (KP - K); e += NTHR) wl[(e / (KP - K)) * KPW + K + e % (KP - K)] = zero;
+  // WPK 1: the packed tile's loads are issued here and land in LDS just before
+  // the compute barrier, so their latency overlaps the prologue's own loads
+  constexpr int WN16 = WPK == 1 ? COUT * KPW * (int)sizeof(T) / 16 : 1;
+  constexpr int WIT = (WN16 + NTHR - 1) / NTHR;
+  uint4 wreg[WPK == 1 ? WIT : 1];
+  if constexpr (WPK == 1) {
+    static_assert((COUT * KPW * sizeof(T)) % 16 == 0, "packed weight tile must be whole 16-B chunks");
+    static_assert(COUT * KPW == (MODE == 2 ? W2D_LEN : W2F_LEN), "pre-packed weights exist for layer 2 only");
+    const uint4* src = reinterpret_cast<const uint4*>(wpk);
+#pragma unroll
+    for (int i = 0; i < WIT; ++i)
+      if (tid + i * NTHR < WN16) wreg[i] = src[tid + i * NTHR];
+  } else {
+    if constexpr (KP > K) {
+      for (int e = tid; e < COUT * (KP - K); e += NTHR) wl[(e / (KP - K)) * KPW + K + e % (KP - K)] = zero;
+    }
+    // natural W index e = (o * WIN + i) * 25 + tap, WIN = in-channels of W
+    // (= CIN here, = COUT for the data-grad where W is [CIN][COUT][5][5])
+    constexpr int KO = 25 * (MODE == 2 ? COUT : CIN);
+    stage_f32<COUT * K>(w, [&](int e, float v) {
+      const int o = e / KO, rem = e % KO;      // o: out-ch of W
+      const int i = rem / 25, tap = rem % 25;  // i: in-ch of W
+      if (MODE == 2)  // W_eff[co=i][ci=o][tap'] with tap' = 24 - tap
+        wl[i * KPW + (24 - tap) * CIN + o] = Cvt<T>::from_f(v);
+      else
+        wl[o * KPW + tap * CIN + i] = Cvt<T>::from_f(v);
+    });
   }
-  // natural W index e = (o * WIN + i) * 25 + tap, WIN = in-channels of W
-  // (= CIN here, = COUT for the data-grad where W is [CIN][COUT][5][5])
-  constexpr int KO = 25 * (MODE == 2 ? COUT : CIN);
-  stage_f32<COUT * K>(w, [&](int e, float v) {
-    const int o = e / KO, rem = e % KO;      // o: out-ch of W
-    const int i = rem / 25, tap = rem % 25;  // i: in-ch of W
-    if (MODE == 2)  // W_eff[co=i][ci=o][tap'] with tap' = 24 - tap
-      wl[i * KPW + (24 - tap) * CIN + o] = Cvt<T>::from_f(v);
-    else
-      wl[o * KPW + tap * CIN + i] = Cvt<T>::from_f(v);
-  });
+  if constexpr (WPK == 2) pack_w2<T>(pk);
+  DPA_STAMP(1);
   // --- stage the zero-padded image in HWC order
   for (int e = tid; e < HP * WPD * CIN; e += NTHR) {
     const int hp = e / (WPD * CIN), rem = e % (WPD * CIN);
@@ -489,6 +572,7 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
       }
     }
     bn_finalize<CIN>(pin.bn, sc_s, beta_s, mean_s, istd_s, part, blockIdx.x == 0);
+    DPA_STAMP(3);
     const bool wr = pin.p_out != nullptr && sp == 0;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
@@ -513,6 +597,7 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
     BnBwdStage<T, CIN, H, W, NTHR> st;
     st.load(bin, b);
     bn_bwd_coef<CIN, T>(bin, coef, part, sums, blockIdx.x == 0);
+    DPA_STAMP(3);
     st.emit(coef, [&](int c, int h, int ww, T v00, T v01, T v10, T v11) {
       img[((h + 2) * WPD + (ww + 2)) * CIN + c] = v00;
       img[((h + 2) * WPD + (ww + 3)) * CIN + c] = v01;
@@ -520,7 +605,15 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
       img[((h + 3) * WPD + (ww + 3)) * CIN + c] = v11;
     });
   }
+  if constexpr (WPK == 1) {
+    uint4* dst = reinterpret_cast<uint4*>(wl);
+#pragma unroll
+    for (int i = 0; i < WIT; ++i)
+      if (tid + i * NTHR < WN16) dst[tid + i * NTHR] = wreg[i];
+  }
+  DPA_STAMP(4);
   __syncthreads();
+  DPA_STAMP(5);
 
   const int lane = tid & 63, wv = tid >> 6;
   const int r = lane & 15, q = lane >> 4;
@@ -566,9 +659,9 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const int co = nt * 16 + r;
-        const float bs = (MODE == 2) ? 0.f : bias[co];
+        const float bs = pre_bias[nt];
         T* dst = y + ((size_t)b * COUT + co) * HW + pix0;
-        const float sh = (MODE == 0) ? shift[co] : 0.f;
+        const float sh = pre_shift[nt];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float v = acc[nt][i] + bs;
@@ -588,6 +681,7 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
       }
     }
   }
+  DPA_STAMP(6);
   if constexpr (MODE == 0 || EPI == 1) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
@@ -618,6 +712,7 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
       if (blockIdx.x == 0 && tid < COUT) fstats[2 * COUT + 1 + tid] = shift[tid];
     }
   }
+  DPA_STAMP(7);
 }
 
 // ---------------------------------------------------------------------------
@@ -864,6 +959,7 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
 
   const int tid = threadIdx.x;
   const int b = blockIdx.x / nsplit, sp = blockIdx.x % nsplit;
+  DPA_STAMP(0);
   const int r0 = sp * ROWS;
   const T* xb = x + (size_t)b * CIN * H * W;
   const T* dyb = dy + (size_t)b * COUT * H * W;
@@ -910,6 +1006,7 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
       scatter5(ci, h + 2, ww + 1, bb);
     });
     bn_bwd_coef<COUT, T>(bin, coef, part, sums, blockIdx.x == 0);
+    DPA_STAMP(3);
     st.emit(coef, [&](int co, int h, int ww, T v00, T v01, T v10, T v11) {
       dyl[(co * ROWS + h) * WP + ww] = v00;
       dyl[(co * ROWS + h) * WP + ww + 1] = v01;
@@ -939,6 +1036,7 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
       if (ih >= 0 && ih < H) xpad[(ci * XR + rr) * WX + cc + 2] = xb[(ci * H + ih) * W + cc];
     }
   }
+  DPA_STAMP(4);
   __syncthreads();
   if constexpr (!DIRECT) {
     // 5 kw-shifted copies, LDS -> LDS: xs[kw][ci][rr][c] = xpad[ci][rr][c + kw]
@@ -955,6 +1053,7 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
   }
 
   float* row_out = wslab + (size_t)blockIdx.x * ROWLEN;
+  DPA_STAMP(5);
   const int lane = tid & 63, wv = tid >> 6;
   const int r = lane & 15, q = lane >> 4;
   // bias grad partial: per output channel sum of dy over this chunk
@@ -964,6 +1063,7 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
     a = wave_sum(a);
     if (lane == 0) row_out[COUT * N + co] = a;
   }
+  DPA_STAMP(6);
   const int ks = KSPLIT > 1 ? wv % KSPLIT : 0;
   const int pstart = KSPLIT > 1 ? wv / KSPLIT : wv;
   const int pstep = KSPLIT > 1 ? NW / KSPLIT : NW;
@@ -996,6 +1096,7 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
       for (int i = 0; i < 4; ++i) row_out[(mt * 16 + 4 * q + i) * N + col] = acc[i];
     }
   }
+  DPA_STAMP(7);
 }
 
 // ---------------------------------------------------------------------------

@@ -251,8 +251,9 @@ void conv2_fwd(at::Tensor y1, c10::optional<at::Tensor> fslab1, at::Tensor fstat
                at::Tensor rm1, at::Tensor rv1, at::Tensor nbt1, double momentum, double eps, bool train, at::Tensor w2,
                at::Tensor bias2, at::Tensor y2, c10::optional<at::Tensor> fslab2, at::Tensor fstats2, at::Tensor rm2,
                c10::optional<at::Tensor> p1_out, c10::optional<at::Tensor> idx1_out,
-               c10::optional<at::Tensor> xh1_out) {
-  DPA_CHECK_INPUT(y1); DPA_CHECK_INPUT(w2); DPA_CHECK_INPUT(y2);
+               c10::optional<at::Tensor> xh1_out, at::Tensor wpk) {
+  DPA_CHECK_INPUT(y1); DPA_CHECK_INPUT(w2); DPA_CHECK_INPUT(y2); DPA_CHECK_INPUT(wpk);
+  TORCH_CHECK(wpk.numel() == cb::W2F_LEN && wpk.scalar_type() == y1.scalar_type(), "packed conv2 weights");
   const int B = (int)y1.size(0);
   TORCH_CHECK(y1.size(1) == 16 && y1.size(2) == 28 && y1.size(3) == 28 && w2.size(0) == 32 && w2.size(1) == 16,
               "fused conv2 expects the ConvNet shapes");
@@ -272,13 +273,14 @@ void conv2_fwd(at::Tensor y1, c10::optional<at::Tensor> fslab1, at::Tensor fstat
                   idx1_out.has_value() ? idx1_out->data_ptr<uint8_t>() : nullptr,
                   xh1_out.has_value() ? dptr<T>(*xh1_out) : nullptr};
     if (train)
-      hipLaunchKernelGGL((cb::conv5x5_kernel<T, 16, 32, 14, 14, 0, 1>), dim3(B * ns), dim3(cb::NTHR), 0, stream,
-                         nullptr, w2.data_ptr<float>(), bias2.data_ptr<float>(), dptr<T>(y2),
-                         fslab2->data_ptr<float>(), fstats2.data_ptr<float>(), rm2.data_ptr<float>(), ns, pin);
+      hipLaunchKernelGGL((cb::conv5x5_kernel<T, 16, 32, 14, 14, 0, 1, 0, 1>), dim3(B * ns), dim3(cb::NTHR), 0,
+                         stream, nullptr, nullptr, bias2.data_ptr<float>(), dptr<T>(y2), fslab2->data_ptr<float>(),
+                         fstats2.data_ptr<float>(), rm2.data_ptr<float>(), ns, pin, BwdIn<T>{}, BwdEpi<T>{},
+                         dptr<T>(wpk), cb::WPack<T>{});
     else
-      hipLaunchKernelGGL((cb::conv5x5_kernel<T, 16, 32, 14, 14, 1, 1>), dim3(B * ns), dim3(cb::NTHR), 0, stream,
-                         nullptr, w2.data_ptr<float>(), bias2.data_ptr<float>(), dptr<T>(y2), nullptr, nullptr,
-                         nullptr, ns, pin);
+      hipLaunchKernelGGL((cb::conv5x5_kernel<T, 16, 32, 14, 14, 1, 1, 0, 1>), dim3(B * ns), dim3(cb::NTHR), 0,
+                         stream, nullptr, nullptr, bias2.data_ptr<float>(), dptr<T>(y2), nullptr, nullptr, nullptr,
+                         ns, pin, BwdIn<T>{}, BwdEpi<T>{}, dptr<T>(wpk), cb::WPack<T>{});
   });
   DPA_CHECK_LAUNCH();
 }
@@ -341,13 +343,52 @@ void head_bwd(at::Tensor dlogits, at::Tensor wfc, at::Tensor p2, at::Tensor idx2
   DPA_CHECK_LAUNCH();
 }
 
+// Layer-1 conv (+BN1 sums when training) that also packs the layer-2 weights
+// into their low-precision LDS tile layouts (cb::pack_w2).
+void conv1_fwd_pack(at::Tensor x, at::Tensor w1, at::Tensor b1, at::Tensor y1, c10::optional<at::Tensor> fslab1,
+                    c10::optional<at::Tensor> fstats1, c10::optional<at::Tensor> shift1, at::Tensor w2,
+                    at::Tensor wpk_f, at::Tensor wpk_d) {
+  DPA_CHECK_INPUT(x); DPA_CHECK_INPUT(w1); DPA_CHECK_INPUT(b1); DPA_CHECK_INPUT(y1); DPA_CHECK_INPUT(w2);
+  DPA_CHECK_INPUT(wpk_f); DPA_CHECK_INPUT(wpk_d);
+  const int B = (int)x.size(0);
+  typedef cb::SH<0> S;
+  TORCH_CHECK(x.size(1) == 1 && x.size(2) == 28 && x.size(3) == 28 && w1.numel() == 16 * 25 && b1.numel() == 16,
+              "fused conv1 expects the ConvNet shapes");
+  TORCH_CHECK(w2.numel() == 32 * 16 * 25 && w2.scalar_type() == at::kFloat && w1.scalar_type() == at::kFloat);
+  TORCH_CHECK(y1.numel() == (int64_t)B * 16 * 784 && y1.scalar_type() == x.scalar_type());
+  TORCH_CHECK(wpk_f.numel() == cb::W2F_LEN && wpk_d.numel() == cb::W2D_LEN &&
+              wpk_f.scalar_type() == x.scalar_type() && wpk_d.scalar_type() == x.scalar_type());
+  const bool st = fslab1.has_value();
+  if (st)
+    TORCH_CHECK(fslab1->numel() == (int64_t)B * S::SPLIT * cb::fslab_row(16) && fstats1->numel() == cb::stats_len(16) &&
+                shift1->numel() == 16);
+  if (B == 0) return;
+  with_t(dt_of(x), [&](auto tag) {
+    typedef decltype(tag) T;
+    cb::WPack<T> pk{w2.data_ptr<float>(), dptr<T>(wpk_f), dptr<T>(wpk_d)};
+    if (st)
+      hipLaunchKernelGGL((cb::conv5x5_kernel<T, 1, 16, 28, 28, 0, 0, 0, 2>), dim3(B * S::SPLIT), dim3(cb::NTHR), 0,
+                         cur_stream(), dptr<T>(x), w1.data_ptr<float>(), b1.data_ptr<float>(), dptr<T>(y1),
+                         fslab1->data_ptr<float>(), fstats1->data_ptr<float>(), shift1->data_ptr<float>(), S::SPLIT,
+                         PoolIn<T>{}, BwdIn<T>{}, BwdEpi<T>{}, nullptr, pk);
+    else
+      hipLaunchKernelGGL((cb::conv5x5_kernel<T, 1, 16, 28, 28, 1, 0, 0, 2>), dim3(B * S::SPLIT), dim3(cb::NTHR), 0,
+                         cur_stream(), dptr<T>(x), w1.data_ptr<float>(), b1.data_ptr<float>(), dptr<T>(y1), nullptr,
+                         nullptr, nullptr, S::SPLIT, PoolIn<T>{}, BwdIn<T>{}, BwdEpi<T>{}, nullptr, pk);
+  });
+  DPA_CHECK_LAUNCH();
+}
+
 constexpr int kDgradSplit = 2;
 int64_t dgrad2_rows(int64_t B) { return B * kDgradSplit; }
 
 // [pool2/ReLU2/BN2 backward] -> conv2 data grad -> dp1 (+ BN1 partial sums rows).
-void conv2_dgrad(at::Tensor w2, at::Tensor y2, at::Tensor dp2, at::Tensor idx2, at::Tensor fstats2, at::Tensor gsum2,
-                 at::Tensor g2, double eps2, at::Tensor dp1, at::Tensor idx1, at::Tensor xh1, at::Tensor bslab1) {
-  DPA_CHECK_INPUT(y2); DPA_CHECK_INPUT(dp1);
+void conv2_dgrad(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx2, at::Tensor fstats2,
+                 at::Tensor gsum2, at::Tensor g2, double eps2, at::Tensor dp1, at::Tensor idx1, at::Tensor xh1,
+                 at::Tensor bslab1) {
+  DPA_CHECK_INPUT(y2); DPA_CHECK_INPUT(dp1); DPA_CHECK_INPUT(wpk_d);
+  TORCH_CHECK(wpk_d.numel() == cb::W2D_LEN && wpk_d.scalar_type() == y2.scalar_type(),
+              "packed conv2 data-grad weights");
   const int B = (int)y2.size(0);
   TORCH_CHECK(y2.size(1) == 32 && y2.size(2) == 14 && dp2.numel() == (int64_t)B * 32 * 49);
   TORCH_CHECK(dp1.numel() == (int64_t)B * 16 * 196 && idx1.numel() == dp1.numel() && xh1.numel() == dp1.numel());
@@ -357,9 +398,9 @@ void conv2_dgrad(at::Tensor w2, at::Tensor y2, at::Tensor dp2, at::Tensor idx2, 
     typedef decltype(tag) T;
     BwdIn<T> bi = bwd_in<T>(dp2, idx2, y2, fstats2, gsum2, c10::nullopt, g2, eps2, 32, c10::nullopt, c10::nullopt);
     BwdEpi<T> ep{idx1.data_ptr<uint8_t>(), dptr<T>(xh1), bslab1.data_ptr<float>()};
-    hipLaunchKernelGGL((cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1>), dim3(B * kDgradSplit), dim3(cb::NTHR), 0,
-                       cur_stream(), nullptr, w2.data_ptr<float>(), nullptr, dptr<T>(dp1), nullptr, nullptr, nullptr,
-                       kDgradSplit, PoolIn<T>{}, bi, ep);
+    hipLaunchKernelGGL((cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1, 1>), dim3(B * kDgradSplit), dim3(cb::NTHR),
+                       0, cur_stream(), nullptr, nullptr, nullptr, dptr<T>(dp1), nullptr, nullptr, nullptr,
+                       kDgradSplit, PoolIn<T>{}, bi, ep, dptr<T>(wpk_d), cb::WPack<T>{});
   });
   DPA_CHECK_LAUNCH();
 }
@@ -402,6 +443,23 @@ void register_convnet_fused(pybind11::module& m) {
   s.def("head_bwd", &cnf::head_bwd);
   s.def("head_bwd_lds", &cnf::head_bwd_lds);
   s.def("dgrad2_rows", &cnf::dgrad2_rows);
+  s.def("conv1_fwd_pack", &cnf::conv1_fwd_pack);
+#ifdef DPA_TIMING
+  s.def("read_stamps", []() {
+    auto out = at::empty({DPA_MAX_STAMP_BLOCKS, DPA_NSTAMPS}, at::TensorOptions().dtype(at::kLong));
+    DPA_CHECK_HIP(hipDeviceSynchronize());
+    DPA_CHECK_HIP(hipMemcpyFromSymbol(out.data_ptr(), HIP_SYMBOL(dpa_stamps), sizeof(unsigned long long) *
+                                      DPA_MAX_STAMP_BLOCKS * DPA_NSTAMPS));
+    return out;
+  });
+  s.def("clear_stamps", []() {
+    DPA_CHECK_HIP(hipDeviceSynchronize());
+    std::vector<unsigned long long> z(DPA_MAX_STAMP_BLOCKS * DPA_NSTAMPS, 0ull);
+    DPA_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dpa_stamps), z.data(), z.size() * sizeof(unsigned long long)));
+  });
+#endif
+  s.attr("W2F_LEN") = cb::W2F_LEN;
+  s.attr("W2D_LEN") = cb::W2D_LEN;
   s.def("conv2_dgrad", &cnf::conv2_dgrad);
   s.def("conv_wgrad_bn", &cnf::conv_wgrad_bn);
 }

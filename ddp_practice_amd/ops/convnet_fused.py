@@ -3,7 +3,8 @@
 Fusing across the layer boundaries of /root/reference/origin_main.py:9-31
 removes launches that exist only because torch runs one module at a time:
 
-  forward  (train): conv1(+BN1 sums) | BN1-ReLU-pool1 -> conv2 (+BN2 sums) | BN2-ReLU-pool2 -> fc
+  forward  (train): conv1(+BN1 sums, packs conv2's bf16 weight tiles) | BN1-ReLU-pool1 -> conv2 (+BN2 sums)
+                    | BN2-ReLU-pool2 -> fc
                     = 3 launches for the model (per-layer ops: 6, torch: ~14 + host syncs)
   backward:         fc bwd (+BN2 sums) | BN2 bwd -> conv2 dgrad (+BN1 sums) | BN2 bwd -> conv2 wgrad
                     | BN1 bwd -> conv1 wgrad | weight-grad sums = 5 launches
@@ -61,6 +62,9 @@ class ConvNetFn(torch.autograd.Function):
         y1 = torch.empty((B, 16, 28, 28), dtype=cdtype, device=dev)
         y2 = torch.empty((B, 32, 14, 14), dtype=cdtype, device=dev)
         logits = torch.empty((B, N), dtype=cdtype, device=dev)
+        # layer-2 weights pre-packed (low precision, LDS tile layouts) by the conv1 launch
+        wpk_f = torch.empty(cn.W2F_LEN, dtype=cdtype, device=dev)
+        wpk_d = torch.empty(cn.W2D_LEN, dtype=cdtype, device=dev)
         fstats1 = torch.empty(cb.stats_len(16), dtype=torch.float32, device=dev)
         fstats2 = torch.empty(cb.stats_len(32), dtype=torch.float32, device=dev)
         if training:
@@ -73,19 +77,19 @@ class ConvNetFn(torch.autograd.Function):
             p2 = torch.empty((B, 32 * 49), dtype=cdtype, device=dev)
             idx2 = torch.empty((B, 32 * 49), dtype=torch.uint8, device=dev)
             xh2 = torch.empty((B, 32 * 49), dtype=cdtype, device=dev)
-            cb.conv_fwd(x, w1, b1, y1, fslab1, fstats1, rm1)
+            cn.conv1_fwd_pack(x, w1, b1, y1, fslab1, fstats1, rm1, w2, wpk_f, wpk_d)
             if sync:
                 comm.all_reduce_(fslab1)
             cn.conv2_fwd(y1, fslab1, fstats1, g1, be1, rm1, rv1, nbt1, m1, e1, True, w2, b2, y2, fslab2, fstats2,
-                         rm2, p1, idx1, xh1)
+                         rm2, p1, idx1, xh1, wpk_f)
             if sync:
                 comm.all_reduce_(fslab2)
             cn.head_fwd(y2, fslab2, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, True, wfc, bfc, logits, p2, idx2, xh2)
-            ctx.save_for_backward(x, w2, wfc, g1, g2, y1, p1, idx1, xh1, fstats1, y2, p2, idx2, xh2, fstats2)
+            ctx.save_for_backward(x, wpk_d, wfc, g1, g2, y1, p1, idx1, xh1, fstats1, y2, p2, idx2, xh2, fstats2)
         else:
-            cb.conv_fwd(x, w1, b1, y1)
+            cn.conv1_fwd_pack(x, w1, b1, y1, None, None, None, w2, wpk_f, wpk_d)
             cn.conv2_fwd(y1, None, fstats1, g1, be1, rm1, rv1, nbt1, m1, e1, False, w2, b2, y2, None, fstats2, rm2,
-                         None, None, None)
+                         None, None, None, wpk_f)
             cn.head_fwd(y2, None, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, False, wfc, bfc, logits, None, None,
                         None)
         ctx.training = training
@@ -100,7 +104,7 @@ class ConvNetFn(torch.autograd.Function):
         if not ctx.training:
             raise RuntimeError("ConvNetFn: backward through an eval-mode forward is not supported")
         cb, cn = _mods()
-        x, w2, wfc, g1, g2, y1, p1, idx1, xh1, fstats1, y2, p2, idx2, xh2, fstats2 = ctx.saved_tensors
+        x, wpk_d, wfc, g1, g2, y1, p1, idx1, xh1, fstats1, y2, p2, idx2, xh2, fstats2 = ctx.saved_tensors
         e1, e2 = ctx.eps
         comm, sync = ctx.comm, ctx.sync
         dl = dlogits.to(y2.dtype).contiguous()
@@ -123,7 +127,7 @@ class ConvNetFn(torch.autograd.Function):
         # 2. BN2 bwd -> conv2 dgrad -> dp1 (+ BN1 partial sums)
         dp1 = torch.empty((B, 16, 14, 14), dtype=y1.dtype, device=dev)
         bslab1 = torch.empty(cn.dgrad2_rows(B) * 32, **f32)
-        cn.conv2_dgrad(w2, y2, dp2, idx2, fstats2, gsum2, g2, e2, dp1, idx1, xh1, bslab1)
+        cn.conv2_dgrad(wpk_d, y2, dp2, idx2, fstats2, gsum2, g2, e2, dp1, idx1, xh1, bslab1)
         # 3. BN2 bwd -> conv2 wgrad partials (independent of 2)
         wslab2 = torch.empty(B * (n_w2 + 32), **f32)
         cn.conv_wgrad_bn(p1, y2, dp2, idx2, fstats2, gsum2, None, g2, e2, None, None, wslab2)

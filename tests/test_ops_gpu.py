@@ -240,7 +240,8 @@ def test_fused_amp_sgd_matches_unfused(C, momentum, sizes):
     for it in range(8):
         gs = [torch.randn_like(p) * 512 for p in ps]
         if it in (1, 4, 6):
-            gs[it % len(gs)][it] = float("nan") if it != 4 else float("inf")
+            g = gs[it % len(gs)]
+            g[it % g.numel()] = float("nan") if it != 4 else float("inf")
         for x, g in zip(ga, gs):
             x.copy_(g)
         gb = [g.clone() for g in gs]
