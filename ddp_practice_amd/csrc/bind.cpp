@@ -19,6 +19,7 @@ void register_xgmi(pybind11::module& m);
 void register_reducer(pybind11::module& m);
 void register_convnet_fused(pybind11::module& m);
 void register_runtime(pybind11::module& m);
+void register_bn_nhwc(pybind11::module& m);
 }
 
 // Opt-in (DPA_NATIVE_BACKTRACE=1) host-side SIGSEGV handler printing the native
@@ -50,4 +51,5 @@ PYBIND11_MODULE(_C, m) {
   dpa::register_reducer(m);
   dpa::register_convnet_fused(m);
   dpa::register_runtime(m);
+  dpa::register_bn_nhwc(m);
 }

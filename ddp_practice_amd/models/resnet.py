@@ -1,0 +1,169 @@
+"""ResNet-50 (torchvision layout: same module tree, parameter names and
+state_dict keys, 25,557,032 parameters) for the BASELINE.json stress config
+"ResNet-50 on synthetic 3x224x224, world_size=8 AMP bf16 (stress MFMA conv +
+all-reduce bucket fusion)".  The reference repository has no ResNet; the
+architecture is He et al. 2015 with the v1.5 stride placement (stride on the
+3x3 conv of each stage's first bottleneck), the variant torchvision ships.
+
+Execution on a HIP device (``fused=True``): activations are bf16/f16/f32
+``channels_last`` (NHWC in memory) end to end;
+  * 1x1 convolutions are GEMMs on the NHWC rows ([N*H*W, Cin] x [Cin, Cout],
+    hipBLASLt through ``torch.matmul``; stride-2 projections subsample first);
+  * 3x3 / 7x7 convolutions go to MIOpen's NHWC kernels (``F.conv2d``);
+  * every BatchNorm runs on the native NHWC kernels with its ReLU and, for the
+    last BN of a bottleneck, the residual add fused in (ops/bn_nhwc.py), as
+    SyncBatchNorm when the module was converted (one small all-reduce each way);
+  * max-pool 3x3/2 and the global average pool are native kernels; fc is a
+    hipBLASLt GEMM.
+On CPU the plain torch modules run (the same math; the CPU test tier).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..amp import autocast, compute_dtype
+
+
+def _conv_gemm_1x1(x: torch.Tensor, w: torch.Tensor, stride: int) -> torch.Tensor:
+    """1x1 conv of a channels_last activation as a GEMM over its NHWC rows."""
+    if stride != 1:
+        x = x[:, :, ::stride, ::stride]
+    N, C, H, W = x.shape
+    rows = x.permute(0, 2, 3, 1)
+    if not rows.is_contiguous():
+        rows = rows.contiguous()
+    out = torch.matmul(rows.reshape(N * H * W, C), w.reshape(w.shape[0], C).t())
+    return out.reshape(N, H, W, -1).permute(0, 3, 1, 2)
+
+
+def _conv(x: torch.Tensor, conv: nn.Conv2d, cdtype: torch.dtype) -> torch.Tensor:
+    w = conv.weight.to(cdtype)
+    if conv.kernel_size == (1, 1) and conv.padding == (0, 0) and conv.groups == 1 and conv.bias is None:
+        return _conv_gemm_1x1(x, w, conv.stride[0])
+    out = F.conv2d(x, w, None if conv.bias is None else conv.bias.to(cdtype), conv.stride, conv.padding,
+                   conv.dilation, conv.groups)
+    return out if out.is_contiguous(memory_format=torch.channels_last) else \
+        out.contiguous(memory_format=torch.channels_last)
+
+
+def _comm_of(bn: nn.Module):
+    if not bn.training:
+        return None
+    if isinstance(bn, nn.SyncBatchNorm):
+        from ..parallel.comm import default_comm
+
+        return default_comm()
+    return getattr(bn, "comm", None)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: nn.Module | None = None):
+        super().__init__()
+        width = planes
+        self.conv1 = nn.Conv2d(inplanes, width, kernel_size=1, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = nn.Conv2d(width, width, kernel_size=3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = nn.Conv2d(width, planes * self.expansion, kernel_size=1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * self.expansion)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        identity = x
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        if self.downsample is not None:
+            identity = self.downsample(x)
+        return self.relu(out + identity)
+
+    def forward_native(self, x: torch.Tensor, cdtype: torch.dtype) -> torch.Tensor:
+        from ..ops.bn_nhwc import bn_act
+
+        out = bn_act(_conv(x, self.conv1, cdtype), self.bn1, relu=True, comm=_comm_of(self.bn1))
+        out = bn_act(_conv(out, self.conv2, cdtype), self.bn2, relu=True, comm=_comm_of(self.bn2))
+        identity = x
+        if self.downsample is not None:
+            conv, bn = self.downsample[0], self.downsample[1]
+            identity = bn_act(_conv(x, conv, cdtype), bn, relu=False, comm=_comm_of(bn))
+        return bn_act(_conv(out, self.conv3, cdtype), self.bn3, res=identity, relu=True, comm=_comm_of(self.bn3))
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes: int = 1000, amp_dtype: torch.dtype | None = None,
+                 fused: bool = True):
+        super().__init__()
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.layer1 = self._make_layer(64, layers[0])
+        self.layer2 = self._make_layer(128, layers[1], stride=2)
+        self.layer3 = self._make_layer(256, layers[2], stride=2)
+        self.layer4 = self._make_layer(512, layers[3], stride=2)
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(512 * Bottleneck.expansion, num_classes)
+        for m in self.modules():  # torchvision's initialisation
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.constant_(m.weight, 1)
+                nn.init.constant_(m.bias, 0)
+        self.amp_dtype = amp_dtype
+        self.fused = fused
+
+    def _make_layer(self, planes: int, blocks: int, stride: int = 1) -> nn.Sequential:
+        downsample = None
+        if stride != 1 or self.inplanes != planes * Bottleneck.expansion:
+            downsample = nn.Sequential(
+                nn.Conv2d(self.inplanes, planes * Bottleneck.expansion, kernel_size=1, stride=stride, bias=False),
+                nn.BatchNorm2d(planes * Bottleneck.expansion),
+            )
+        layers = [Bottleneck(self.inplanes, planes, stride, downsample)]
+        self.inplanes = planes * Bottleneck.expansion
+        layers += [Bottleneck(self.inplanes, planes) for _ in range(1, blocks)]
+        return nn.Sequential(*layers)
+
+    # ------------------------------------------------------------------ paths
+    def _native_ok(self, x: torch.Tensor) -> bool:
+        if not (self.fused and x.is_cuda and x.dim() == 4):
+            return False
+        return all(m.affine and m.track_running_stats for m in self.modules()
+                   if isinstance(m, nn.modules.batchnorm._BatchNorm))
+
+    def _forward_torch(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        return self.fc(torch.flatten(self.avgpool(x), 1))
+
+    def _forward_native(self, x: torch.Tensor) -> torch.Tensor:
+        from ..ops.bn_nhwc import bn_act, global_avg_pool, max_pool_3x3s2
+
+        cdtype = compute_dtype(x) if self.amp_dtype is not None else torch.float32
+        x = x.to(dtype=cdtype, memory_format=torch.channels_last)
+        x = bn_act(_conv(x, self.conv1, cdtype), self.bn1, relu=True, comm=_comm_of(self.bn1))
+        x = max_pool_3x3s2(x)
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            for blk in layer:
+                x = blk.forward_native(x, cdtype)
+        feat = global_avg_pool(x)
+        return F.linear(feat, self.fc.weight.to(cdtype), self.fc.bias.to(cdtype))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        native = self._native_ok(x)
+        fwd = self._forward_native if native else self._forward_torch
+        if self.amp_dtype is not None:
+            with autocast(dtype=self.amp_dtype, device_type="cuda" if x.is_cuda else "cpu"):
+                return fwd(x)
+        return fwd(x)
+
+
+def resnet50(num_classes: int = 1000, amp_dtype: torch.dtype | None = None, fused: bool = True) -> ResNet:
+    return ResNet((3, 4, 6, 3), num_classes=num_classes, amp_dtype=amp_dtype, fused=fused)

@@ -1,0 +1,154 @@
+"""Channels-last BatchNorm (+ residual add) (+ ReLU), max-pool 3x3/2 and global
+average pool on the native kernels of csrc/kernels/bn_nhwc.hip.
+
+Used by the ResNet-50 stress model (models/resnet.py, BASELINE.json config 5).
+Activations are NCHW-shaped ``torch.channels_last`` tensors (NHWC in memory),
+the layout MIOpen / hipBLASLt consume for the convolutions.  BatchNorm follows
+torch semantics (batch stats, biased var for normalisation, unbiased var into
+running_var, momentum / cumulative average) and SyncBatchNorm semantics when a
+communicator is active: ONE all-reduce of [sum, sum_sq, count] (2C+1 floats)
+forward and of [sum dz, sum dz*xhat] (2C) backward, d(gamma) / d(beta) from the
+local sums (torch/nn/modules/_functions.py:10-205).
+"""
+from __future__ import annotations
+
+import torch
+
+from .._ext import load as _load_ext
+
+_CL = torch.channels_last
+
+
+def _K():
+    return _load_ext().bn_nhwc
+
+
+class _Workspace:
+    """Per-device partial-sum rows + the stats kernels' ticket (stream-ordered reuse)."""
+
+    _by_dev: dict = {}
+
+    @classmethod
+    def get(cls, dev: torch.device, C: int):
+        ws = cls._by_dev.get(dev)
+        need = 512 * 2 * C
+        if ws is None or ws[0].numel() < need:
+            part = torch.empty(max(need, 512 * 2 * 2048), dtype=torch.float32, device=dev)
+            ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+            ws = cls._by_dev[dev] = (part, ticket)
+        return ws
+
+
+def _cl(t: torch.Tensor) -> torch.Tensor:
+    return t if t.is_contiguous(memory_format=_CL) else t.contiguous(memory_format=_CL)
+
+
+class BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, res, running_mean, running_var, nbt, momentum, eps, training, relu, comm):
+        K = _K()
+        x = _cl(x)
+        C = x.shape[1]
+        dev = x.device
+        y = torch.empty_like(x, memory_format=_CL)
+        resc = _cl(res) if res is not None else None
+        mom = -1.0 if momentum is None else float(momentum)
+        f32 = dict(dtype=torch.float32, device=dev)
+        if training:
+            part, ticket = _Workspace.get(dev, C)
+            stats = torch.empty(3 * C + 1, **f32)
+            K.fwd_stats(x, C, running_mean, part, ticket, stats)
+            sync = comm is not None and comm.active
+            if sync:
+                comm.all_reduce_(stats.narrow(0, 0, 2 * C + 1))
+            save = torch.empty(2 * C, **f32)
+            K.apply(x, resc, y, C, stats, weight, bias, running_mean, running_var, nbt, mom, float(eps), True,
+                    relu, save)
+            ctx.save_for_backward(x, y if relu else None, weight, save, stats)
+            ctx.sync, ctx.comm, ctx.has_res = sync, comm, res is not None
+        else:
+            dummy = torch.empty(2 * C + 1, **f32)
+            K.apply(x, resc, y, C, dummy, weight, bias, running_mean, running_var, nbt, mom, float(eps), False,
+                    relu, dummy)
+            ctx.sync = None
+        ctx.relu = relu
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        if ctx.sync is None:
+            raise RuntimeError("BNActFn: backward through an eval-mode BatchNorm is not supported")
+        K = _K()
+        x, y, weight, save, stats = ctx.saved_tensors
+        C = x.shape[1]
+        dy = _cl(dy)
+        part, ticket = _Workspace.get(x.device, C)
+        f32 = dict(dtype=torch.float32, device=x.device)
+        out = torch.empty(2 * C, **f32)
+        dgamma = torch.empty(C, **f32)
+        dbeta = torch.empty(C, **f32)
+        K.bwd_stats(dy, y, x, C, save, part, ticket, out, dgamma, dbeta)
+        sums = ctx.comm.all_reduce(out) if ctx.sync else out
+        dx = torch.empty_like(x, memory_format=_CL)
+        dres = torch.empty_like(x, memory_format=_CL) if ctx.has_res else None
+        K.bwd_elemt(dy, y, x, C, save, sums, stats, weight, dx, dres)
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
+
+
+def bn_act(x, bn, res=None, relu=True, comm=None):
+    """BatchNorm module ``bn`` applied to channels_last ``x`` (+ res) (+ ReLU)."""
+    return BNActFn.apply(x, bn.weight, bn.bias, res, bn.running_mean, bn.running_var, bn.num_batches_tracked,
+                         bn.momentum, bn.eps, bn.training, relu, comm if bn.training else None)
+
+
+class MaxPoolFn(torch.autograd.Function):
+    """MaxPool2d(kernel 3, stride 2, padding 1) on channels_last."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x = _cl(x)
+        N, C, H, W = x.shape
+        OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        y = torch.empty((N, C, OH, OW), dtype=x.dtype, device=x.device, memory_format=_CL)
+        idx = torch.empty((N, OH, OW, C), dtype=torch.uint8, device=x.device)
+        _K().maxpool_fwd(x.permute(0, 2, 3, 1), y.permute(0, 2, 3, 1), idx)
+        ctx.save_for_backward(idx)
+        ctx.shape = (N, C, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        N, C, H, W = ctx.shape
+        dy = _cl(dy)
+        dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device, memory_format=_CL)
+        _K().maxpool_bwd(dy.permute(0, 2, 3, 1), idx, dx.permute(0, 2, 3, 1))
+        return dx
+
+
+class GlobalAvgPoolFn(torch.autograd.Function):
+    """AdaptiveAvgPool2d(1) + flatten on channels_last: [N, C, H, W] -> [N, C]."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x = _cl(x)
+        N, C, H, W = x.shape
+        y = torch.empty((N, C), dtype=x.dtype, device=x.device)
+        _K().avgpool_fwd(x.permute(0, 2, 3, 1), y, H * W)
+        ctx.shape = (N, C, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, C, H, W = ctx.shape
+        dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device, memory_format=_CL)
+        _K().avgpool_bwd(dy.contiguous(), dx.permute(0, 2, 3, 1), H * W)
+        return dx
+
+
+def max_pool_3x3s2(x):
+    return MaxPoolFn.apply(x)
+
+
+def global_avg_pool(x):
+    return GlobalAvgPoolFn.apply(x)

@@ -1,0 +1,34 @@
+"""ResNet-50 stress model (BASELINE.json config 5) on CPU: torchvision layout,
+parameter count, DDP bucket plan vs torch's planner."""
+import torch
+import torch.distributed as tdist
+
+from ddp_practice_amd.models import resnet50
+from ddp_practice_amd.parallel import compute_bucket_assignment
+
+
+def test_resnet50_layout_and_forward():
+    m = resnet50()
+    assert sum(p.numel() for p in m.parameters()) == 25_557_032
+    sd = m.state_dict()
+    assert len(sd) == 320
+    for k in ("conv1.weight", "bn1.running_var", "layer1.0.downsample.0.weight", "layer1.0.downsample.1.bias",
+              "layer2.3.conv3.weight", "layer3.5.bn2.num_batches_tracked", "layer4.2.bn3.weight", "fc.bias"):
+        assert k in sd, k
+    assert tuple(sd["layer4.0.conv2.weight"].shape) == (512, 512, 3, 3)
+    assert m.layer2[0].conv2.stride == (2, 2) and m.layer2[0].conv1.stride == (1, 1)  # v1.5 stride placement
+    out = m(torch.rand(2, 3, 64, 64))
+    assert out.shape == (2, 1000)
+    out.sum().backward()
+    assert all(p.grad is not None for p in m.parameters())
+
+
+def test_resnet50_bucket_plan_matches_torch():
+    """Reverse-order greedy buckets with [1 MiB, 25 MiB] limits: 5 buckets."""
+    params = list(resnet50().parameters())
+    ours = compute_bucket_assignment(params, 25 * 2 ** 20, 2 ** 20)
+    theirs, _ = tdist._compute_bucket_assignment_by_size(params[::-1], [2 ** 20, 25 * 2 ** 20])
+    n = len(params)
+    assert [sorted(b) for b in ours] == [sorted(n - 1 - i for i in b) for b in theirs]
+    sizes = [sum(params[i].numel() * 4 for i in b) / 2 ** 20 for b in ours]
+    assert [round(s, 2) for s in sizes] == [7.82, 30.04, 25.04, 25.32, 9.27]

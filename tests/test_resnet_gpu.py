@@ -1,0 +1,108 @@
+"""Native channels-last kernels (csrc/kernels/bn_nhwc.hip) vs torch fp32 / float64
+references, and the native ResNet-50 path vs the torch module path."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    return ((a.double() - b.double()).norm() / (b.double().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C,res,relu", [(64, False, True), (256, True, True), (2048, False, False),
+                                        (512, True, False)])
+def test_bn_act_fwd_bwd(C, res, relu, dtype):
+    from ddp_practice_amd.ops.bn_nhwc import bn_act
+
+    torch.manual_seed(0)
+    N, H, W = 3, 7, 9
+    x = (torch.randn(N, C, H, W, device=DEV) * 2 + 0.5).to(dtype).contiguous(memory_format=torch.channels_last)
+    r = torch.randn(N, C, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last) if res else None
+    bn = torch.nn.BatchNorm2d(C).to(DEV)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.3, 0.3)
+        bn.running_mean.uniform_(-0.2, 0.2)
+    ref = copy.deepcopy(bn).double()
+    xs = x.detach().clone().requires_grad_()
+    rs = r.detach().clone().requires_grad_() if res else None
+    y = bn_act(xs, bn, res=rs, relu=relu)
+    x64 = x.double().detach().requires_grad_()
+    r64 = r.double().detach().requires_grad_() if res else None
+    y64 = ref(x64) + (r64 if res else 0)
+    if relu:
+        y64 = y64.relu()
+    assert y.is_contiguous(memory_format=torch.channels_last) and y.dtype == dtype
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert _rel(y, y64) < tol
+    assert _rel(bn.running_mean, ref.running_mean) < 1e-5 and _rel(bn.running_var, ref.running_var) < 1e-5
+    assert int(bn.num_batches_tracked) == 1
+    g = torch.randn_like(y64)
+    (y.double() * g).sum().backward()
+    (y64 * g).sum().backward()
+    gtol = 1e-4 if dtype == torch.float32 else 3e-2
+    assert _rel(xs.grad, x64.grad) < gtol
+    assert _rel(bn.weight.grad, ref.weight.grad) < gtol and _rel(bn.bias.grad, ref.bias.grad) < gtol
+    if res:
+        assert _rel(rs.grad, r64.grad) < gtol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_pools(dtype):
+    from ddp_practice_amd.ops.bn_nhwc import global_avg_pool, max_pool_3x3s2
+
+    torch.manual_seed(1)
+    x = torch.randn(2, 64, 15, 12, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    xa = x.detach().clone().requires_grad_()
+    xb = x.detach().float().clone().requires_grad_()
+    y = max_pool_3x3s2(xa)
+    yr = F.max_pool2d(xb, 3, 2, 1)
+    assert torch.equal(y.float(), yr)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g)
+    assert _rel(xa.grad, xb.grad) < (1e-6 if dtype == torch.float32 else 1e-2)
+    x2 = torch.randn(3, 256, 7, 7, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    a = x2.detach().clone().requires_grad_()
+    b = x2.detach().float().clone().requires_grad_()
+    p = global_avg_pool(a)
+    pr = b.mean((2, 3))
+    assert _rel(p, pr) < (1e-6 if dtype == torch.float32 else 1e-2)
+    gp = torch.randn_like(pr)
+    p.backward(gp.to(dtype))
+    pr.backward(gp)
+    assert _rel(a.grad, b.grad) < (1e-6 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("amp", [None, torch.bfloat16])
+def test_resnet50_native_matches_torch_path(C, amp):
+    from ddp_practice_amd.models import resnet50
+
+    torch.manual_seed(0)
+    m = resnet50(num_classes=10, amp_dtype=amp).to(DEV)
+    t = copy.deepcopy(m)
+    t.fused = False
+    x = torch.rand(4, 3, 64, 64, device=DEV)
+    y = torch.randint(0, 10, (4,), device=DEV)
+    out = m(x)
+    ref = t(x)
+    tol = 2e-3 if amp is None else 5e-2
+    assert _rel(out, ref) < tol, _rel(out, ref)
+    F.cross_entropy(out.float(), y).backward()
+    F.cross_entropy(ref.float(), y).backward()
+    gt = dict(t.named_parameters())
+    worst = max((_rel(p.grad, gt[n].grad), n) for n, p in m.named_parameters()
+                if not n.endswith("bias") or n == "fc.bias")
+    assert worst[0] < (5e-3 if amp is None else 1e-1), worst
+    for (n, b), (_, r) in zip(m.named_buffers(), t.named_buffers()):
+        assert _rel(b.float(), r.float()) < 1e-3, n
+    m.eval()
+    t.eval()
+    with torch.no_grad():
+        assert _rel(m(x), t(x)) < tol
