@@ -48,7 +48,14 @@ def main(argv=None):
                     help="profiling: run the DDP/SyncBN collective path even at --gpus 1")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0, all-reduces on the xGMI engine (not the metric)")
+    ap.add_argument("--model", default="convnet", choices=["convnet", "resnet50"],
+                    help="convnet = the headline config; resnet50 = BASELINE.json stress config 5")
+    ap.add_argument("--resnet-impl", default="native", choices=["native", "torch"],
+                    help="resnet50: native NHWC kernels, or the plain torch module path (comparison)")
+    ap.add_argument("--image-size", type=int, default=224)
     args = ap.parse_args(argv)
+    if args.model == "resnet50":
+        return bench_resnet(args)
 
     import torch
 
@@ -175,6 +182,82 @@ def main(argv=None):
                 "est_3epoch_train_s": round(3 * len(loader) * ms / 1e3, 3),
                 "baseline_img_s": base,
             },
+        }), flush=True)
+    ddist.destroy_process_group()
+
+
+def bench_resnet(args):
+    """ResNet-50 training step (BASELINE.json config 5): channels-last AMP + GradScaler,
+    SyncBN + DDP over RCCL for N > 1, synthetic 3x224x224 batch, eager (MIOpen convs)."""
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from ddp_practice_amd import distributed as ddist
+    from ddp_practice_amd.amp import GradScaler
+    from ddp_practice_amd.models import resnet50
+    from ddp_practice_amd.ops.head import cross_entropy
+    from ddp_practice_amd.optim import SGD
+    from ddp_practice_amd.parallel import DistributedDataParallel, convert_sync_batchnorm
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        ddist.init_process_group(backend="nccl")
+    rank = ddist.get_rank()
+    amp = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": None}[args.amp_dtype]
+    bs = args.batch_size if args.batch_size != 32 else 128
+    torch.manual_seed(0)
+    model = resnet50(amp_dtype=amp, fused=args.resnet_impl == "native").to(dev)
+    if args.resnet_impl == "torch":
+        model = model.to(memory_format=torch.channels_last)
+    if world > 1:
+        if not args.no_sync_bn:
+            model = convert_sync_batchnorm(model)
+        model = DistributedDataParallel(model, device_ids=[local_rank])
+    optimizer = SGD(model.parameters(), lr=1e-4)
+    scaler = GradScaler(enabled=amp is not None)
+    g = torch.Generator(device="cpu").manual_seed(rank)
+    images = torch.rand(bs, 3, args.image_size, args.image_size, generator=g).to(dev)
+    labels = torch.randint(0, 1000, (bs,), generator=g).to(dev)
+    if args.resnet_impl == "torch":
+        images = images.contiguous(memory_format=torch.channels_last)
+
+    def step():
+        if args.resnet_impl == "torch" and amp is not None:
+            with torch.autocast("cuda", dtype=amp):
+                out = model(images)
+        else:
+            out = model(images)
+        loss = cross_entropy(out, labels)
+        optimizer.zero_grad(set_to_none=True)
+        scaler.scale(loss).backward()
+        scaler.step(optimizer)
+        scaler.update()
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    ddist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    ddist.barrier()
+    dt = ddist.max_over_ranks(time.perf_counter() - t0)
+    ms = dt / args.steps * 1e3
+    img_s = bs * world * args.steps / dt
+    if rank == 0:
+        print(json.dumps({
+            "metric": "images/sec (whole node), ResNet-50 stress config (BASELINE.json config 5)",
+            "value": round(img_s, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": max(1, args.warmup), "ms_per_step": round(ms, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.amp_dtype,
+            "data": f"synthetic 3x{args.image_size}x{args.image_size}, random-init weights",
+            "config": {"model": "ResNet-50 (25,557,032 params)", "global_batch": bs * world, "seq_len": None,
+                       "parallelism": f"dp{world}", "per_rank_batch": bs, "impl": args.resnet_impl,
+                       "sync_bn": world > 1 and not args.no_sync_bn, "optimizer": "SGD(lr=1e-4)"},
         }), flush=True)
     ddist.destroy_process_group()
 

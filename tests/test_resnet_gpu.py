@@ -82,27 +82,54 @@ def test_pools(dtype):
 
 @pytest.mark.parametrize("amp", [None, torch.bfloat16])
 def test_resnet50_native_matches_torch_path(C, amp):
+    """Native path vs a float64 run of the torch module path: the native error must
+    stay within a small factor of the torch path's own error at the same precision
+    (fp32 eager, or torch autocast) -- BatchNorm over few elements per channel
+    (batch 8, 3x3 maps in layer4) amplifies every rounding difference."""
     from ddp_practice_amd.models import resnet50
 
     torch.manual_seed(0)
     m = resnet50(num_classes=10, amp_dtype=amp).to(DEV)
     t = copy.deepcopy(m)
     t.fused = False
-    x = torch.rand(4, 3, 64, 64, device=DEV)
-    y = torch.randint(0, 10, (4,), device=DEV)
+    t.amp_dtype = None
+    r64 = copy.deepcopy(t).double()
+    x = torch.rand(8, 3, 96, 96, device=DEV)
+    y = torch.randint(0, 10, (8,), device=DEV)
     out = m(x)
-    ref = t(x)
-    tol = 2e-3 if amp is None else 5e-2
-    assert _rel(out, ref) < tol, _rel(out, ref)
+    if amp is None:
+        ref_t = t(x)
+    else:
+        with torch.autocast("cuda", dtype=amp):
+            ref_t = t(x)
+    ref = r64(x.double())
+    fac, floor = (4.0, 1e-4) if amp is None else (3.0, 2e-2)
+    assert _rel(out, ref) < max(fac * _rel(ref_t, ref), floor), (_rel(out, ref), _rel(ref_t, ref))
     F.cross_entropy(out.float(), y).backward()
-    F.cross_entropy(ref.float(), y).backward()
-    gt = dict(t.named_parameters())
-    worst = max((_rel(p.grad, gt[n].grad), n) for n, p in m.named_parameters()
-                if not n.endswith("bias") or n == "fc.bias")
-    assert worst[0] < (5e-3 if amp is None else 1e-1), worst
-    for (n, b), (_, r) in zip(m.named_buffers(), t.named_buffers()):
-        assert _rel(b.float(), r.float()) < 1e-3, n
+    F.cross_entropy(ref_t.float(), y).backward()
+    F.cross_entropy(ref, y).backward()
+    gt, g64 = dict(t.named_parameters()), dict(r64.named_parameters())
+    bad = []
+    for n, p in m.named_parameters():
+        if n.endswith("bias") and n != "fc.bias" and "bn" not in n and "downsample.1" not in n:
+            continue
+        e, et = _rel(p.grad, g64[n].grad), _rel(gt[n].grad, g64[n].grad)
+        if e > max(fac * et, floor):
+            bad.append((n, e, et))
+    # one value within an ulp of a ReLU threshold routes differently from float64 and
+    # moves every tensor its gradient passes through (that BN's affine grads, the conv
+    # below, the BN below that): allow a few such tensors, each within 10x torch's error
+    assert len(bad) <= 6 and all(e < 10 * et + 1e-3 for _, e, et in bad), bad[:8]
+    for (n, b), (_, bt), (_, r) in zip(m.named_buffers(), t.named_buffers(), r64.named_buffers()):
+        if b.dtype.is_floating_point:
+            assert _rel(b, r) < max(fac * _rel(bt, r), 1e-3), (n, _rel(b, r), _rel(bt, r))
+        else:
+            assert torch.equal(b, r.to(b.dtype)), n
     m.eval()
     t.eval()
+    r64.eval()
+    with torch.no_grad(), torch.autocast("cuda", dtype=amp or torch.bfloat16, enabled=amp is not None):
+        e_ref = _rel(t(x), r64(x.double()))
     with torch.no_grad():
-        assert _rel(m(x), t(x)) < tol
+        e = _rel(m(x), r64(x.double()))
+    assert e < max(fac * e_ref, floor), (e, e_ref)
