@@ -1,22 +1,32 @@
 // Channels-last (NHWC) BatchNorm (+ residual add) (+ ReLU), max-pool 3x3/2 and
 // global average pool for the ResNet-50 stress config (BASELINE.json config 5;
 // SURVEY.md §7.3 step 8).  Activations are [M = N*H*W][C] rows with C
-// contiguous, so one lane moves 16 B = 8 channels of one pixel per access and a
-// wave covers whole cache lines.
+// contiguous.
 //
-//   forward (train)  stats:  per-channel sum(x - shift), sum((x - shift)^2) over
-//                            the rows: per-workgroup partial rows, the LAST
-//                            workgroup to finish (device-scope ticket) reduces them
-//                            -> stats[2C+1] (+ shift copy); SyncBN all-reduces the
-//                            first 2C+1 entries between the launches
+// Geometry (every BN kernel): the channels are cut into column chunks of
+// CC = Lr*VEC channels (Lr <= 32 lanes x 16 B = up to 512 B of a row,
+// blockIdx.y = chunk); a lane owns one 16-B channel vector of its chunk for the
+// whole kernel (its per-channel coefficients live in registers) and walks rows
+// with stride RP = 256/Lr, U = 4 rows in flight per lane.
+//
+//   forward (train)  stats:  per-channel sum(x - shift), sum((x - shift)^2);
+//                            per-workgroup partial rows, combined by a
+//                            two-level ticket tree (groups of 16 workgroups,
+//                            then the groups) -> stats[2C+1] (+ shift copy);
+//                            the final reducer of chunk 0 bumps
+//                            num_batches_tracked.  SyncBN all-reduces the first
+//                            2C+1 entries between the launches.
 //                    apply:  y = relu?((x - mean) * gamma*invstd + beta (+ res));
-//                            workgroup 0 updates running stats (momentum, unbiased
-//                            var) and saves mean / invstd for the backward
-//   backward         stats:  dz = dy * [y > 0] (ReLU) ; sum(dz), sum(dz * xhat)
-//                            -> the same ticket reduction; d(gamma), d(beta) from
-//                            the local sums (torch SyncBN semantics); all-reduce
+//                            row-block 0 of each chunk updates running stats
+//                            (momentum, unbiased var) and saves mean / invstd
+//   backward         stats:  dz = dy * relu'(.) ; sum(dz), sum(dz * xhat) -> the
+//                            same tree; d(gamma), d(beta) from the local sums
+//                            (torch SyncBN semantics); all-reduce between
 //                    elemt:  dx = gamma*invstd * (dz - S1/n - xhat * S2/n),
 //                            d(res) = dz when the block had a residual input
+// ReLU derivative: from the saved output y when a residual was added; without
+// one it is recomputed from x with the forward's exact fma sequence
+// (y > 0  <=>  fma(x, s, b) > 0), so y is neither kept nor re-read.
 // The per-channel statistics are sums around a shift (the running mean, equal
 // on every rank) to avoid E[x^2] - E[x]^2 cancellation.  Deterministic: every
 // reduction has a fixed order (no float atomics).
@@ -26,7 +36,11 @@ namespace dpa {
 namespace bnh {
 
 constexpr int THR = 256;
-constexpr int MAXNV = 2;  // channel vectors per lane when C / VEC > THR (f32, C = 2048)
+constexpr int LR_MAX = 32;   // lanes per row segment of a chunk
+constexpr int G1 = 16;       // level-1 group size of the ticket tree
+constexpr int MAXGR = 512;   // row blocks per chunk in the statistics kernels
+constexpr int U = 4;         // rows in flight per lane
+constexpr int MAXTICKETS = 1024;
 
 template <typename T> struct V16 { static constexpr int N = 16 / sizeof(T); };
 
@@ -46,69 +60,110 @@ __device__ __forceinline__ void store_vec(T* p, const float* f) {
   *reinterpret_cast<f32x4*>(p) = raw;
 }
 
-// Lane geometry over a [rows][C] matrix: L = C/VEC vector columns; if L <= THR a
-// pass covers RP = THR/L rows, lane -> (row offset, column); else one row per
-// pass and each lane owns NV = L/THR columns.
-struct Geo {
-  int L, RP, roff, nv;
+__host__ __device__ inline int chunk_lanes(int C, int vec) { return C / vec < LR_MAX ? C / vec : LR_MAX; }
+
+// lane -> (row offset ro in [0, RP), channel c0 of its 16-B vector)
+template <int VEC>
+struct Chunk {
+  int Lr, CC, RP, ro, c0;
   bool active;
-  __device__ Geo(int C, int vec) {
-    L = C / vec;
-    if (L <= THR) {
-      RP = THR / L;
-      roff = threadIdx.x / L;
-      nv = 1;
-      active = roff < RP;
-    } else {
-      RP = 1;
-      roff = 0;
-      nv = L / THR;
-      active = true;
-    }
+  __device__ explicit Chunk(int C) {
+    Lr = chunk_lanes(C, VEC);
+    CC = Lr * VEC;
+    RP = THR / Lr;
+    ro = (int)threadIdx.x / Lr;
+    active = ro < RP;
+    c0 = (int)blockIdx.y * CC + ((int)threadIdx.x % Lr) * VEC;
   }
-  __device__ int col(int k) const { return L <= THR ? (int)threadIdx.x % L : (int)threadIdx.x + k * THR; }
 };
 
-// Last-workgroup reduction of G partial rows of width W -> out[W] (fixed order).
-__device__ __forceinline__ bool ticket_last(unsigned* ticket, int G) {
-  __shared__ int s_last;
+// rows [r0, r1) of this row block
+__device__ __forceinline__ void row_range(long long M, long long& r0, long long& r1) {
+  const long long per = (M + gridDim.x - 1) / gridDim.x;
+  r0 = (long long)blockIdx.x * per;
+  r1 = r0 + per < M ? r0 + per : M;
+}
+
+// Last-arriver election over `n` workgroups (agent-scope release / acquire).
+__device__ __forceinline__ bool ticket_last(unsigned* ticket, int n, int* s_flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its partial-row stores are done
   __syncthreads();
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (t == (unsigned)G - 1);
-    if (s_last) {
+    const int last = t == (unsigned)n - 1;
+    *s_flag = last;
+    if (last) {
       __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm for the next launch
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
   __syncthreads();
-  return s_last != 0;
+  return *s_flag != 0;
 }
 
-// (lo / hi non-null: also lo = out[0, W/2) and hi = out[W/2, W))
-__device__ __forceinline__ void reduce_partials(const float* __restrict__ part, int G, int W, float* __restrict__ out,
-                                                float* __restrict__ lo = nullptr, float* __restrict__ hi = nullptr) {
-  for (int j = threadIdx.x; j < W; j += THR) {
+// dst[t] = sum_{g < n} src[g*W + t] (n <= 2*G1), fixed order; the loads of a
+// batch of G1 rows are issued before the first add.
+__device__ __noinline__ void sum_rows(const float* __restrict__ src, int n, int W, float* __restrict__ dst) {
+  for (int t = threadIdx.x; t < W; t += THR) {
     float acc = 0.f;
-    int g = 0;
-    for (; g + 8 <= G; g += 8) {
-      float v[8];
+    for (int g0 = 0; g0 < n; g0 += G1) {
+      float v[G1];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(g + u) * W + j];
+      for (int u = 0; u < G1; ++u) v[u] = src[(size_t)(g0 + u < n ? g0 + u : n - 1) * W + t];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc += v[u];
+      for (int u = 0; u < G1; ++u) acc += g0 + u < n ? v[u] : 0.f;
     }
-    for (; g < G; ++g) acc += part[(size_t)g * W + j];
-    out[j] = acc;
-    if (lo != nullptr) {
-      if (j < W / 2) lo[j] = acc;
-      else hi[j - W / 2] = acc;
-    }
+    dst[t] = acc;
   }
+}
+
+// Block partial -> part, then the two-level ticket tree of this chunk.  Returns
+// true in the single workgroup per chunk that ends with the chunk's W totals in
+// red[0, W).  part: [Gc*Gr + Gc*NG][W] floats; tickets: [Gc*NG + Gc].
+__device__ bool chunk_reduce(float* __restrict__ part, unsigned* __restrict__ tickets, int W, float* red,
+                             int* s_flag) {
+  const int Gr = gridDim.x, Gc = gridDim.y, y = blockIdx.y;
+  const int NG = (Gr + G1 - 1) / G1;
+  float* p1 = part + (size_t)y * Gr * W;
+  float* p2 = part + (size_t)Gc * Gr * W + (size_t)y * NG * W;
+  for (int t = threadIdx.x; t < W; t += THR) p1[(size_t)blockIdx.x * W + t] = red[t];
+  const int grp = blockIdx.x / G1;
+  const int gsz = min(G1, Gr - grp * G1);
+  if (!ticket_last(tickets + y * NG + grp, gsz, s_flag)) return false;
+  if (NG == 1) {
+    sum_rows(p1, gsz, W, red);
+    __syncthreads();
+    return true;
+  }
+  sum_rows(p1 + (size_t)grp * G1 * W, gsz, W, p2 + (size_t)grp * W);
+  if (!ticket_last(tickets + Gc * NG + y, NG, s_flag)) return false;
+  sum_rows(p2, NG, W, red);
+  __syncthreads();
+  return true;
+}
+
+// Combine the RP row-lanes of the block: red[h*CC + c] = sum_ro acc_h (fixed order).
+template <int VEC>
+__device__ __forceinline__ void block_combine(const Chunk<VEC>& g, const float* s1, const float* s2, float* red,
+                                              float* scratch) {
+  const int cl = g.c0 - (int)blockIdx.y * g.CC;  // column within the chunk
+  if (g.active)
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      scratch[(size_t)g.ro * g.CC + cl + j] = s1[j];
+      scratch[(size_t)(g.RP + g.ro) * g.CC + cl + j] = s2[j];
+    }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 2 * g.CC; t += THR) {
+    const int h = t / g.CC, c = t % g.CC;
+    float acc = 0.f;
+    for (int rr = 0; rr < g.RP; ++rr) acc += scratch[(size_t)(h * g.RP + rr) * g.CC + c];
+    red[t] = acc;
+  }
+  __syncthreads();
 }
 
 // ----------------------------------------------------------------------------
@@ -117,82 +172,75 @@ __device__ __forceinline__ void reduce_partials(const float* __restrict__ part, 
 template <typename T>
 __global__ void __launch_bounds__(THR)
 fwd_stats_kernel(const T* __restrict__ x, long long M, int C, const float* __restrict__ shift,
-                 float* __restrict__ part, unsigned* __restrict__ ticket, float* __restrict__ stats) {
+                 float* __restrict__ part, unsigned* __restrict__ tickets, float* __restrict__ stats,
+                 int64_t* __restrict__ nbt) {
   constexpr int VEC = V16<T>::N;
-  const Geo g(C, VEC);
-  float s1[MAXNV][VEC], s2[MAXNV][VEC], sh[MAXNV][VEC];
-  for (int k = 0; k < MAXNV; ++k)
+  __shared__ float scratch[2 * THR * VEC];
+  __shared__ float red[2 * LR_MAX * VEC];
+  __shared__ int s_flag;
+  const Chunk<VEC> g(C);
+  float s1[VEC], s2[VEC], sh[VEC];
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) s1[k][j] = s2[k][j] = sh[k][j] = 0.f;
-  const long long rows_per = (M + gridDim.x - 1) / gridDim.x;
-  const long long r0 = (long long)blockIdx.x * rows_per, r1 = min(M, r0 + rows_per);
+  for (int j = 0; j < VEC; ++j) s1[j] = s2[j] = sh[j] = 0.f;
+  long long r0, r1;
+  row_range(M, r0, r1);
   if (g.active) {
-    for (int k = 0; k < g.nv; ++k)
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) sh[k][j] = shift[g.col(k) * VEC + j];
-    for (long long r = r0 + g.roff; r < r1; r += 2 * g.RP) {
-      const bool two = r + g.RP < r1;  // two rows in flight per iteration
-      for (int k = 0; k < g.nv; ++k) {
-        const int c0 = g.col(k) * VEC;
-        float a[VEC], b[VEC];
-        load_vec<T>(x + r * C + c0, a);
-        if (two) load_vec<T>(x + (r + g.RP) * C + c0, b);
+    for (int j = 0; j < VEC; ++j) sh[j] = shift[g.c0 + j];
+    long long r = r0 + g.ro;
+    for (; r + (U - 1) * g.RP < r1; r += U * g.RP) {
+      float a[U][VEC];
+#pragma unroll
+      for (int u = 0; u < U; ++u) load_vec<T>(x + (r + u * g.RP) * C + g.c0, a[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
-          const float d = a[j] - sh[k][j];
-          s1[k][j] += d;
-          s2[k][j] += d * d;
-          if (two) {
-            const float e = b[j] - sh[k][j];
-            s1[k][j] += e;
-            s2[k][j] += e * e;
-          }
+          const float d = a[u][j] - sh[j];
+          s1[j] += d;
+          s2[j] = fmaf(d, d, s2[j]);
         }
+    }
+    for (; r < r1; r += g.RP) {
+      float a[VEC];
+      load_vec<T>(x + r * C + g.c0, a);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float d = a[j] - sh[j];
+        s1[j] += d;
+        s2[j] = fmaf(d, d, s2[j]);
       }
     }
   }
-  // combine the RP row-lanes of each column through LDS (fixed order)
-  __shared__ float red[THR * 8];  // >= RP * VEC per column group, reused per k
-  float* prow = part + (size_t)blockIdx.x * 2 * C;
-  for (int k = 0; k < g.nv; ++k) {
-    const int c0 = g.col(k) * VEC;
-    for (int h = 0; h < 2; ++h) {
-      __syncthreads();
-      if (g.active)
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) red[(g.roff * g.L + (g.L <= THR ? c0 / VEC : 0)) * VEC + j] =
-            h == 0 ? s1[k][j] : s2[k][j];
-      __syncthreads();
-      if (g.L <= THR) {
-        for (int cj = threadIdx.x; cj < C; cj += THR) {
-          float t = 0.f;
-          for (int rr = 0; rr < g.RP; ++rr) t += red[(rr * g.L + cj / VEC) * VEC + cj % VEC];
-          prow[h * C + cj] = t;
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) prow[h * C + c0 + j] = h == 0 ? s1[k][j] : s2[k][j];
-      }
-    }
-    if (g.L <= THR) break;
+  block_combine<VEC>(g, s1, s2, red, scratch);
+  if (!chunk_reduce(part, tickets, 2 * g.CC, red, &s_flag)) return;
+  const int cb = (int)blockIdx.y * g.CC;
+  for (int t = threadIdx.x; t < g.CC; t += THR) {
+    stats[cb + t] = red[t];
+    stats[C + cb + t] = red[g.CC + t];
+    stats[2 * C + 1 + cb + t] = shift[cb + t];
   }
-  if (ticket_last(ticket, gridDim.x)) {
-    reduce_partials(part, gridDim.x, 2 * C, stats);
-    if (threadIdx.x == 0) stats[2 * C] = (float)M;
-    for (int c = threadIdx.x; c < C; c += THR) stats[2 * C + 1 + c] = shift[c];
+  if (blockIdx.y == 0 && threadIdx.x == 0) {
+    stats[2 * C] = (float)M;
+    if (nbt != nullptr) nbt[0] = nbt[0] + 1;
   }
 }
 
-// y = act((x - mean) * gamma*invstd + beta (+ res)); block 0: running stats + save
+// y = act((x - mean) * gamma*invstd + beta (+ res)) as fma(x, s, b) (+ res);
+// row block 0 of each chunk: running stats + save
 template <typename T, bool RES, bool RELU>
 __global__ void __launch_bounds__(THR)
 apply_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y, long long M, int C,
              const float* __restrict__ stats, const float* __restrict__ gamma, const float* __restrict__ beta,
-             float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt, float momentum,
+             float* __restrict__ rmean, float* __restrict__ rvar, const int64_t* __restrict__ nbt, float momentum,
              float eps, int train, float* __restrict__ save) {
   constexpr int VEC = V16<T>::N;
-  extern __shared__ float coef[];  // [C] scale, [C] shift-term
-  for (int c = threadIdx.x; c < C; c += THR) {
+  const Chunk<VEC> g(C);
+  if (!g.active) return;
+  float s[VEC], b[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    const int c = g.c0 + j;
     float mean, istd;
     if (train) {
       const float n = stats[2 * C];
@@ -200,11 +248,10 @@ apply_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__
       const float var = fmaxf(stats[C + c] / n - m1 * m1, 0.f);
       mean = stats[2 * C + 1 + c] + m1;
       istd = rsqrtf(var + eps);
-      if (blockIdx.x == 0) {
+      if (blockIdx.x == 0 && g.ro == 0) {
         save[c] = mean;
         save[C + c] = istd;
-        const int64_t nb = nbt[0] + 1;
-        const float mom = momentum >= 0.f ? momentum : 1.f / (float)nb;
+        const float mom = momentum >= 0.f ? momentum : 1.f / (float)nbt[0];  // nbt bumped by the stats kernel
         rmean[c] = (1.f - mom) * rmean[c] + mom * mean;
         rvar[c] = (1.f - mom) * rvar[c] + mom * var * (n / fmaxf(n - 1.f, 1.f));
       }
@@ -212,132 +259,178 @@ apply_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__
       mean = rmean[c];
       istd = rsqrtf(rvar[c] + eps);
     }
-    const float s = gamma[c] * istd;
-    coef[c] = s;
-    coef[C + c] = beta[c] - mean * s;
+    s[j] = gamma[c] * istd;
+    b[j] = fmaf(-mean, s[j], beta[c]);
   }
-  __syncthreads();
-  if (train && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] = nbt[0] + 1;
-  const long long nvec = M * (C / VEC);
-  for (long long v = (long long)blockIdx.x * THR + threadIdx.x; v < nvec; v += (long long)gridDim.x * THR) {
-    const long long e = v * VEC;
-    const int c0 = (int)(e % C);
-    float a[VEC], r[VEC];
-    load_vec<T>(x + e, a);
-    if (RES) load_vec<T>(res + e, r);
+  long long r0, r1;
+  row_range(M, r0, r1);
+  auto row = [&](long long r, float* a, const float* rr) {
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
-      float o = a[j] * coef[c0 + j] + coef[C + c0 + j];
-      if (RES) o += r[j];
+      float o = fmaf(a[j], s[j], b[j]);
+      if (RES) o += rr[j];
       if (RELU) o = fmaxf(o, 0.f);
       a[j] = o;
     }
-    store_vec<T>(y + e, a);
+    store_vec<T>(y + r * C + g.c0, a);
+  };
+  long long r = r0 + g.ro;
+  for (; r + (U - 1) * g.RP < r1; r += U * g.RP) {
+    float a[U][VEC], q[U][VEC];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      load_vec<T>(x + (r + u * g.RP) * C + g.c0, a[u]);
+      if (RES) load_vec<T>(res + (r + u * g.RP) * C + g.c0, q[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) row(r + u * g.RP, a[u], q[u]);
+  }
+  for (; r < r1; r += g.RP) {
+    float a[VEC], q[VEC];
+    load_vec<T>(x + r * C + g.c0, a);
+    if (RES) load_vec<T>(res + r * C + g.c0, q);
+    row(r, a, q);
   }
 }
 
-// backward statistics: S1 = sum dz, S2 = sum dz*xhat; dz = dy * [y > 0] if RELU.
-// out[0..C) = S1, [C..2C) = S2; dgamma = S2, dbeta = S1 (local, f32).
-template <typename T, bool RELU>
+// ReLU-derivative source of the backward kernels
+enum { ACT_NONE = 0, ACT_Y = 1, ACT_RECOMPUTE = 2 };
+
+template <int VEC, int ACT>
+struct BwdLane {
+  float mu[VEC], is[VEC], s[VEC], b[VEC];
+  __device__ void init(int c0, int C, const float* save, const float* gamma, const float* beta) {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      mu[j] = save[c0 + j];
+      is[j] = save[C + c0 + j];
+      if (ACT == ACT_RECOMPUTE) {
+        s[j] = gamma[c0 + j] * is[j];
+        b[j] = fmaf(-mu[j], s[j], beta[c0 + j]);
+      }
+    }
+  }
+  // dz = dy * relu'(.)
+  __device__ __forceinline__ float dz(int j, float d, float xv, float yv) const {
+    if (ACT == ACT_Y) return yv > 0.f ? d : 0.f;
+    if (ACT == ACT_RECOMPUTE) return fmaf(xv, s[j], b[j]) > 0.f ? d : 0.f;
+    return d;
+  }
+};
+
+// backward statistics: S1 = sum dz, S2 = sum dz*xhat.
+// out[0..C) = S1, [C..2C) = S2; dbeta = S1, dgamma = S2 (local, f32).
+template <typename T, int ACT>
 __global__ void __launch_bounds__(THR)
 bwd_stats_kernel(const T* __restrict__ dy, const T* __restrict__ y, const T* __restrict__ x, long long M, int C,
-                 const float* __restrict__ save, float* __restrict__ part, unsigned* __restrict__ ticket,
-                 float* __restrict__ out, float* __restrict__ dgamma, float* __restrict__ dbeta) {
+                 const float* __restrict__ save, const float* __restrict__ gamma, const float* __restrict__ beta,
+                 float* __restrict__ part, unsigned* __restrict__ tickets, float* __restrict__ out,
+                 float* __restrict__ dgamma, float* __restrict__ dbeta) {
   constexpr int VEC = V16<T>::N;
-  const Geo g(C, VEC);
-  float s1[MAXNV][VEC], s2[MAXNV][VEC], mu[MAXNV][VEC], is[MAXNV][VEC];
-  for (int k = 0; k < MAXNV; ++k)
+  __shared__ float scratch[2 * THR * VEC];
+  __shared__ float red[2 * LR_MAX * VEC];
+  __shared__ int s_flag;
+  const Chunk<VEC> g(C);
+  float s1[VEC], s2[VEC];
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) s1[k][j] = s2[k][j] = mu[k][j] = is[k][j] = 0.f;
-  const long long rows_per = (M + gridDim.x - 1) / gridDim.x;
-  const long long r0 = (long long)blockIdx.x * rows_per, r1 = min(M, r0 + rows_per);
+  for (int j = 0; j < VEC; ++j) s1[j] = s2[j] = 0.f;
+  long long r0, r1;
+  row_range(M, r0, r1);
   if (g.active) {
-    for (int k = 0; k < g.nv; ++k)
+    BwdLane<VEC, ACT> L;
+    L.init(g.c0, C, save, gamma, beta);
+    auto acc = [&](const float* d, const float* xv, const float* yv) {
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
-        mu[k][j] = save[g.col(k) * VEC + j];
-        is[k][j] = save[C + g.col(k) * VEC + j];
+        const float z = L.dz(j, d[j], xv[j], yv[j]);
+        s1[j] += z;
+        s2[j] = fmaf(z, (xv[j] - L.mu[j]) * L.is[j], s2[j]);
       }
-    for (long long r = r0 + g.roff; r < r1; r += g.RP) {
-      for (int k = 0; k < g.nv; ++k) {
-        const long long o = r * C + g.col(k) * VEC;
-        float d[VEC], xv[VEC], yv[VEC];
-        load_vec<T>(dy + o, d);
-        load_vec<T>(x + o, xv);
-        if (RELU) load_vec<T>(y + o, yv);
+    };
+    long long r = r0 + g.ro;
+    for (; r + (U - 1) * g.RP < r1; r += U * g.RP) {
+      float d[U][VEC], xv[U][VEC], yv[U][VEC];
 #pragma unroll
-        for (int j = 0; j < VEC; ++j) {
-          const float dz = (!RELU || yv[j] > 0.f) ? d[j] : 0.f;
-          s1[k][j] += dz;
-          s2[k][j] += dz * (xv[j] - mu[k][j]) * is[k][j];
-        }
+      for (int u = 0; u < U; ++u) {
+        const long long o = (r + u * g.RP) * C + g.c0;
+        load_vec<T>(dy + o, d[u]);
+        load_vec<T>(x + o, xv[u]);
+        if (ACT == ACT_Y) load_vec<T>(y + o, yv[u]);
       }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc(d[u], xv[u], yv[u]);
+    }
+    for (; r < r1; r += g.RP) {
+      float d[VEC], xv[VEC], yv[VEC];
+      const long long o = r * C + g.c0;
+      load_vec<T>(dy + o, d);
+      load_vec<T>(x + o, xv);
+      if (ACT == ACT_Y) load_vec<T>(y + o, yv);
+      acc(d, xv, yv);
     }
   }
-  __shared__ float red[THR * 8];
-  float* prow = part + (size_t)blockIdx.x * 2 * C;
-  for (int k = 0; k < g.nv; ++k) {
-    const int c0 = g.col(k) * VEC;
-    for (int h = 0; h < 2; ++h) {
-      __syncthreads();
-      if (g.active)
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) red[(g.roff * g.L + (g.L <= THR ? c0 / VEC : 0)) * VEC + j] =
-            h == 0 ? s1[k][j] : s2[k][j];
-      __syncthreads();
-      if (g.L <= THR) {
-        for (int cj = threadIdx.x; cj < C; cj += THR) {
-          float t = 0.f;
-          for (int rr = 0; rr < g.RP; ++rr) t += red[(rr * g.L + cj / VEC) * VEC + cj % VEC];
-          prow[h * C + cj] = t;
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) prow[h * C + c0 + j] = h == 0 ? s1[k][j] : s2[k][j];
-      }
-    }
-    if (g.L <= THR) break;
-  }
-  if (ticket_last(ticket, gridDim.x)) {
-    reduce_partials(part, gridDim.x, 2 * C, out, dbeta, dgamma);
+  block_combine<VEC>(g, s1, s2, red, scratch);
+  if (!chunk_reduce(part, tickets, 2 * g.CC, red, &s_flag)) return;
+  const int cb = (int)blockIdx.y * g.CC;
+  for (int t = threadIdx.x; t < g.CC; t += THR) {
+    out[cb + t] = dbeta[cb + t] = red[t];
+    out[C + cb + t] = dgamma[cb + t] = red[g.CC + t];
   }
 }
 
 // dx = gamma*invstd*(dz - S1/n - xhat*S2/n); dres = dz
-template <typename T, bool RELU, bool DRES>
+template <typename T, int ACT, bool DRES>
 __global__ void __launch_bounds__(THR)
 bwd_elemt_kernel(const T* __restrict__ dy, const T* __restrict__ y, const T* __restrict__ x, long long M, int C,
                  const float* __restrict__ save, const float* __restrict__ sums, const float* __restrict__ fstats,
-                 const float* __restrict__ gamma, T* __restrict__ dx, T* __restrict__ dres) {
+                 const float* __restrict__ gamma, const float* __restrict__ beta, T* __restrict__ dx,
+                 T* __restrict__ dres) {
   constexpr int VEC = V16<T>::N;
-  extern __shared__ float cf[];  // [C] gi, [C] k1, [C] k2, [C] mean, [C] istd
+  const Chunk<VEC> g(C);
+  if (!g.active) return;
+  BwdLane<VEC, ACT> L;
+  L.init(g.c0, C, save, gamma, beta);
+  float gi[VEC], k1[VEC], k2[VEC];
   const float n = fstats[2 * C];
-  for (int c = threadIdx.x; c < C; c += THR) {
-    const float istd = save[C + c];
-    cf[c] = gamma[c] * istd;
-    cf[C + c] = sums[c] / n;
-    cf[2 * C + c] = sums[C + c] / n;
-    cf[3 * C + c] = save[c];
-    cf[4 * C + c] = istd;
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    gi[j] = gamma[g.c0 + j] * L.is[j];
+    k1[j] = sums[g.c0 + j] / n;
+    k2[j] = sums[C + g.c0 + j] / n;
   }
-  __syncthreads();
-  const long long nvec = M * (C / VEC);
-  for (long long v = (long long)blockIdx.x * THR + threadIdx.x; v < nvec; v += (long long)gridDim.x * THR) {
-    const long long e = v * VEC;
-    const int c0 = (int)(e % C);
-    float d[VEC], xv[VEC], yv[VEC], o[VEC];
-    load_vec<T>(dy + e, d);
-    load_vec<T>(x + e, xv);
-    if (RELU) load_vec<T>(y + e, yv);
+  auto row = [&](long long o, const float* d, const float* xv, const float* yv) {
+    float z[VEC], e[VEC];
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
-      const int c = c0 + j;
-      d[j] = (!RELU || yv[j] > 0.f) ? d[j] : 0.f;
-      const float xh = (xv[j] - cf[3 * C + c]) * cf[4 * C + c];
-      o[j] = cf[c] * (d[j] - cf[C + c] - xh * cf[2 * C + c]);
+      z[j] = L.dz(j, d[j], xv[j], yv[j]);
+      const float xh = (xv[j] - L.mu[j]) * L.is[j];
+      e[j] = gi[j] * (z[j] - k1[j] - xh * k2[j]);
     }
-    store_vec<T>(dx + e, o);
-    if (DRES) store_vec<T>(dres + e, d);
+    store_vec<T>(dx + o, e);
+    if (DRES) store_vec<T>(dres + o, z);
+  };
+  long long r0, r1;
+  row_range(M, r0, r1);
+  long long r = r0 + g.ro;
+  for (; r + (U - 1) * g.RP < r1; r += U * g.RP) {
+    float d[U][VEC], xv[U][VEC], yv[U][VEC];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long o = (r + u * g.RP) * C + g.c0;
+      load_vec<T>(dy + o, d[u]);
+      load_vec<T>(x + o, xv[u]);
+      if (ACT == ACT_Y) load_vec<T>(y + o, yv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) row((r + u * g.RP) * C + g.c0, d[u], xv[u], yv[u]);
+  }
+  for (; r < r1; r += g.RP) {
+    float d[VEC], xv[VEC], yv[VEC];
+    const long long o = r * C + g.c0;
+    load_vec<T>(dy + o, d);
+    load_vec<T>(x + o, xv);
+    if (ACT == ACT_Y) load_vec<T>(y + o, yv);
+    row(o, d, xv, yv);
   }
 }
 
@@ -484,31 +577,52 @@ static void check_rows(const at::Tensor& t, long long M, int C) {
   TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, "bn_nhwc: 16-B aligned tensors");
 }
 
-static int stats_grid(long long M, int C, int vec) {
-  // enough workgroups to cover the chip, few enough that the last one's partial
-  // reduction (G x 2C floats) stays small
-  const long long work = M * (C / vec);
-  long long g = (work + THR * 16 - 1) / (THR * 16);
-  g = std::max<long long>(1, std::min<long long>(g, std::min<long long>(512, 262144 / (2 * C))));
-  return (int)g;
+
+// ----------------------------------------------------------------------------
+struct Grid2 {
+  int Gr, Gc;
+};
+template <typename T>
+static Grid2 chunk_grid(long long M, int C, int target) {
+  constexpr int VEC = V16<T>::N;
+  TORCH_CHECK(C % VEC == 0 && (C / VEC <= LR_MAX || (C / VEC) % LR_MAX == 0),
+              "bn_nhwc: channel count ", C, " (needs C % ", VEC, " == 0 and C/", VEC, " <= 32 or a multiple of 32)");
+  const int Lr = chunk_lanes(C, VEC);
+  const int RP = THR / Lr;
+  const int Gc = C / (Lr * VEC);
+  const long long by_rows = std::max<long long>(1, (M + (long long)RP * U - 1) / ((long long)RP * U));
+  const long long want = std::max<long long>(1, (target + Gc - 1) / Gc);
+  return {(int)std::min<long long>(by_rows, want), Gc};
+}
+template <typename T>
+static Grid2 stats_grid(long long M, int C) {
+  Grid2 g = chunk_grid<T>(M, C, 1024);
+  g.Gr = std::min(g.Gr, MAXGR);
+  return g;
 }
 static int elt_grid(long long nvec) {
   return (int)std::max<long long>(1, std::min<long long>((nvec + THR - 1) / THR, 4096));
 }
+static void check_workspace(const Grid2& g, int C, const at::Tensor& part, const at::Tensor& tickets) {
+  const int NG = (g.Gr + G1 - 1) / G1;
+  TORCH_CHECK(part.numel() >= (long long)2 * C * (g.Gr + NG), "bn_nhwc: partial-sum workspace too small");
+  TORCH_CHECK(tickets.numel() >= g.Gc * (NG + 1) && tickets.scalar_type() == at::kInt, "bn_nhwc: ticket workspace");
+}
 
-// part: >= 512*2C floats; ticket: one zero-initialised uint32 (re-armed by the kernel)
-void fwd_stats(at::Tensor x, int64_t C, at::Tensor shift, at::Tensor part, at::Tensor ticket, at::Tensor stats) {
+// part: >= 2C*(MAXGR + MAXGR/16) floats; tickets: >= MAXTICKETS zero-initialised int32 (re-armed by the kernels)
+void fwd_stats(at::Tensor x, int64_t C, at::Tensor shift, at::Tensor part, at::Tensor ticket, at::Tensor stats,
+               c10::optional<at::Tensor> nbt) {
   const long long M = x.numel() / C;
   check_rows(x, M, (int)C);
-  TORCH_CHECK(stats.numel() >= 3 * C + 1 && shift.numel() == C && part.numel() >= 512 * 2 * C);
+  TORCH_CHECK(stats.numel() >= 3 * C + 1 && shift.numel() == C);
   dispatch(x, [&](auto tag) {
     typedef decltype(tag) T;
-    TORCH_CHECK(C % V16<T>::N == 0 && C / V16<T>::N <= THR * MAXNV && (C / V16<T>::N <= THR || (C / V16<T>::N) % THR == 0),
-                "bn_nhwc: channel count");
-    const int G = stats_grid(M, (int)C, V16<T>::N);
-    hipLaunchKernelGGL(fwd_stats_kernel<T>, dim3(G), dim3(THR), 0, cur_stream(), dp<T>(x), M, (int)C,
+    const Grid2 g = stats_grid<T>(M, (int)C);
+    check_workspace(g, (int)C, part, ticket);
+    hipLaunchKernelGGL(fwd_stats_kernel<T>, dim3(g.Gr, g.Gc), dim3(THR), 0, cur_stream(), dp<T>(x), M, (int)C,
                        shift.data_ptr<float>(), part.data_ptr<float>(),
-                       reinterpret_cast<unsigned*>(ticket.data_ptr<int>()), stats.data_ptr<float>());
+                       reinterpret_cast<unsigned*>(ticket.data_ptr<int>()), stats.data_ptr<float>(),
+                       nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr);
   });
   DPA_CHECK_LAUNCH();
 }
@@ -522,10 +636,9 @@ void apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, int64_t C,
   if (res.has_value()) check_rows(*res, M, (int)C);
   dispatch(x, [&](auto tag) {
     typedef decltype(tag) T;
-    const int grid = elt_grid(M * C / V16<T>::N);
-    const size_t lds = 2 * C * sizeof(float);
+    const Grid2 g = chunk_grid<T>(M, (int)C, 2048);
     auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(THR), lds, cur_stream(), dp<T>(x),
+      hipLaunchKernelGGL(kern, dim3(g.Gr, g.Gc), dim3(THR), 0, cur_stream(), dp<T>(x),
                          res.has_value() ? dp<T>(*res) : nullptr, dp<T>(y), M, (int)C, stats.data_ptr<float>(),
                          gamma.data_ptr<float>(), beta.data_ptr<float>(), rmean.data_ptr<float>(),
                          rvar.data_ptr<float>(), nbt.data_ptr<int64_t>(), (float)momentum, (float)eps, (int)train,
@@ -540,50 +653,57 @@ void apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, int64_t C,
   DPA_CHECK_LAUNCH();
 }
 
-void bwd_stats(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, int64_t C, at::Tensor save, at::Tensor part,
-               at::Tensor ticket, at::Tensor out, at::Tensor dgamma, at::Tensor dbeta) {
+// act: 0 = no ReLU, 1 = ReLU derivative from y, 2 = recomputed from x (no residual)
+void bwd_stats(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, int64_t C, int64_t act, at::Tensor save,
+               at::Tensor gamma, at::Tensor beta, at::Tensor part, at::Tensor ticket, at::Tensor out,
+               at::Tensor dgamma, at::Tensor dbeta) {
   const long long M = x.numel() / C;
   check_rows(x, M, (int)C);
   check_rows(dy, M, (int)C);
-  if (y.has_value()) check_rows(*y, M, (int)C);
-  TORCH_CHECK(out.numel() >= 2 * C && part.numel() >= 512 * 2 * C && save.numel() >= 2 * C);
+  TORCH_CHECK(act >= 0 && act <= 2 && (act != ACT_Y || y.has_value()));
+  if (act == ACT_Y) check_rows(*y, M, (int)C);
+  TORCH_CHECK(out.numel() >= 2 * C && save.numel() >= 2 * C);
   dispatch(x, [&](auto tag) {
     typedef decltype(tag) T;
-    const int G = stats_grid(M, (int)C, V16<T>::N);
+    const Grid2 g = stats_grid<T>(M, (int)C);
+    check_workspace(g, (int)C, part, ticket);
     auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(G), dim3(THR), 0, cur_stream(), dp<T>(dy), y.has_value() ? dp<T>(*y) : nullptr,
-                         dp<T>(x), M, (int)C, save.data_ptr<float>(), part.data_ptr<float>(),
+      hipLaunchKernelGGL(kern, dim3(g.Gr, g.Gc), dim3(THR), 0, cur_stream(), dp<T>(dy),
+                         act == ACT_Y ? dp<T>(*y) : nullptr, dp<T>(x), M, (int)C, save.data_ptr<float>(),
+                         gamma.data_ptr<float>(), beta.data_ptr<float>(), part.data_ptr<float>(),
                          reinterpret_cast<unsigned*>(ticket.data_ptr<int>()), out.data_ptr<float>(),
                          dgamma.data_ptr<float>(), dbeta.data_ptr<float>());
     };
-    if (y.has_value()) go(bwd_stats_kernel<T, true>); else go(bwd_stats_kernel<T, false>);
+    if (act == ACT_Y) go(bwd_stats_kernel<T, ACT_Y>);
+    else if (act == ACT_RECOMPUTE) go(bwd_stats_kernel<T, ACT_RECOMPUTE>);
+    else go(bwd_stats_kernel<T, ACT_NONE>);
   });
   DPA_CHECK_LAUNCH();
 }
 
-void bwd_elemt(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, int64_t C, at::Tensor save, at::Tensor sums,
-               at::Tensor fstats, at::Tensor gamma, at::Tensor dx, c10::optional<at::Tensor> dres) {
+void bwd_elemt(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, int64_t C, int64_t act, at::Tensor save,
+               at::Tensor sums, at::Tensor fstats, at::Tensor gamma, at::Tensor beta, at::Tensor dx,
+               c10::optional<at::Tensor> dres) {
   const long long M = x.numel() / C;
   check_rows(x, M, (int)C);
   check_rows(dy, M, (int)C);
   check_rows(dx, M, (int)C);
-  if (y.has_value()) check_rows(*y, M, (int)C);
+  TORCH_CHECK(act >= 0 && act <= 2 && (act != ACT_Y || y.has_value()));
+  if (act == ACT_Y) check_rows(*y, M, (int)C);
   if (dres.has_value()) check_rows(*dres, M, (int)C);
   dispatch(x, [&](auto tag) {
     typedef decltype(tag) T;
-    const int grid = elt_grid(M * C / V16<T>::N);
-    const size_t lds = 5 * C * sizeof(float);
+    const Grid2 g = chunk_grid<T>(M, (int)C, 2048);
     auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(THR), lds, cur_stream(), dp<T>(dy),
-                         y.has_value() ? dp<T>(*y) : nullptr, dp<T>(x), M, (int)C, save.data_ptr<float>(),
-                         sums.data_ptr<float>(), fstats.data_ptr<float>(), gamma.data_ptr<float>(), dp<T>(dx),
-                         dres.has_value() ? dp<T>(*dres) : nullptr);
+      hipLaunchKernelGGL(kern, dim3(g.Gr, g.Gc), dim3(THR), 0, cur_stream(), dp<T>(dy),
+                         act == ACT_Y ? dp<T>(*y) : nullptr, dp<T>(x), M, (int)C, save.data_ptr<float>(),
+                         sums.data_ptr<float>(), fstats.data_ptr<float>(), gamma.data_ptr<float>(),
+                         beta.data_ptr<float>(), dp<T>(dx), dres.has_value() ? dp<T>(*dres) : nullptr);
     };
-    const bool r = y.has_value(), d = dres.has_value();
-    if (r && d) go(bwd_elemt_kernel<T, true, true>);
-    else if (r) go(bwd_elemt_kernel<T, true, false>);
-    else if (d) go(bwd_elemt_kernel<T, false, true>);
-    else go(bwd_elemt_kernel<T, false, false>);
+    const bool d = dres.has_value();
+    if (act == ACT_Y) { if (d) go(bwd_elemt_kernel<T, ACT_Y, true>); else go(bwd_elemt_kernel<T, ACT_Y, false>); }
+    else if (act == ACT_RECOMPUTE) { if (d) go(bwd_elemt_kernel<T, ACT_RECOMPUTE, true>); else go(bwd_elemt_kernel<T, ACT_RECOMPUTE, false>); }
+    else { if (d) go(bwd_elemt_kernel<T, ACT_NONE, true>); else go(bwd_elemt_kernel<T, ACT_NONE, false>); }
   });
   DPA_CHECK_LAUNCH();
 }
@@ -654,7 +774,8 @@ void register_bn_nhwc(pybind11::module& m) {
   s.def("maxpool_bwd", &bnh::maxpool_bwd);
   s.def("avgpool_fwd", &bnh::avgpool_fwd);
   s.def("avgpool_bwd", &bnh::avgpool_bwd);
-  s.attr("MAX_PARTIAL_ROWS") = 512;
+  s.attr("MAX_PARTIAL_ROWS") = bnh::MAXGR + bnh::MAXGR / bnh::G1;
+  s.attr("MAX_TICKETS") = bnh::MAXTICKETS;
 }
 
 }  // namespace dpa

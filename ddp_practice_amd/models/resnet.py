@@ -8,7 +8,8 @@ architecture is He et al. 2015 with the v1.5 stride placement (stride on the
 Execution on a HIP device (``fused=True``): activations are bf16/f16/f32
 ``channels_last`` (NHWC in memory) end to end;
   * 1x1 convolutions are GEMMs on the NHWC rows ([N*H*W, Cin] x [Cin, Cout],
-    hipBLASLt through ``torch.matmul``; stride-2 projections subsample first);
+    hipBLASLt; the weight gradient as a split-K batched GEMM with fp32
+    partials: ops/conv1x1.py; stride-2 projections subsample first);
   * 3x3 / 7x7 convolutions go to MIOpen's NHWC kernels (``F.conv2d``);
   * every BatchNorm runs on the native NHWC kernels with its ReLU and, for the
     last BN of a bottleneck, the residual add fused in (ops/bn_nhwc.py), as
@@ -24,24 +25,13 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..amp import autocast, compute_dtype
-
-
-def _conv_gemm_1x1(x: torch.Tensor, w: torch.Tensor, stride: int) -> torch.Tensor:
-    """1x1 conv of a channels_last activation as a GEMM over its NHWC rows."""
-    if stride != 1:
-        x = x[:, :, ::stride, ::stride]
-    N, C, H, W = x.shape
-    rows = x.permute(0, 2, 3, 1)
-    if not rows.is_contiguous():
-        rows = rows.contiguous()
-    out = torch.matmul(rows.reshape(N * H * W, C), w.reshape(w.shape[0], C).t())
-    return out.reshape(N, H, W, -1).permute(0, 3, 1, 2)
+from ..ops.conv1x1 import conv1x1
 
 
 def _conv(x: torch.Tensor, conv: nn.Conv2d, cdtype: torch.dtype) -> torch.Tensor:
-    w = conv.weight.to(cdtype)
     if conv.kernel_size == (1, 1) and conv.padding == (0, 0) and conv.groups == 1 and conv.bias is None:
-        return _conv_gemm_1x1(x, w, conv.stride[0])
+        return conv1x1(x, conv.weight, conv.stride[0], cdtype)
+    w = conv.weight.to(cdtype)
     out = F.conv2d(x, w, None if conv.bias is None else conv.bias.to(cdtype), conv.stride, conv.padding,
                    conv.dilation, conv.groups)
     return out if out.is_contiguous(memory_format=torch.channels_last) else \

@@ -24,18 +24,19 @@ def _K():
 
 
 class _Workspace:
-    """Per-device partial-sum rows + the stats kernels' ticket (stream-ordered reuse)."""
+    """Per-device partial-sum rows + the statistics kernels' tickets (stream-ordered reuse)."""
 
     _by_dev: dict = {}
 
     @classmethod
     def get(cls, dev: torch.device, C: int):
+        K = _K()
         ws = cls._by_dev.get(dev)
-        need = 512 * 2 * C
+        need = int(K.MAX_PARTIAL_ROWS) * 2 * C
         if ws is None or ws[0].numel() < need:
-            part = torch.empty(max(need, 512 * 2 * 2048), dtype=torch.float32, device=dev)
-            ticket = torch.zeros(1, dtype=torch.int32, device=dev)
-            ws = cls._by_dev[dev] = (part, ticket)
+            part = torch.empty(max(need, int(K.MAX_PARTIAL_ROWS) * 2 * 2048), dtype=torch.float32, device=dev)
+            tickets = torch.zeros(int(K.MAX_TICKETS), dtype=torch.int32, device=dev)
+            ws = cls._by_dev[dev] = (part, tickets)
         return ws
 
 
@@ -57,21 +58,22 @@ class BNActFn(torch.autograd.Function):
         if training:
             part, ticket = _Workspace.get(dev, C)
             stats = torch.empty(3 * C + 1, **f32)
-            K.fwd_stats(x, C, running_mean, part, ticket, stats)
+            K.fwd_stats(x, C, running_mean, part, ticket, stats, nbt)
             sync = comm is not None and comm.active
             if sync:
                 comm.all_reduce_(stats.narrow(0, 0, 2 * C + 1))
             save = torch.empty(2 * C, **f32)
             K.apply(x, resc, y, C, stats, weight, bias, running_mean, running_var, nbt, mom, float(eps), True,
                     relu, save)
-            ctx.save_for_backward(x, y if relu else None, weight, save, stats)
+            # ReLU derivative: from y after a residual add, else recomputed from x (y not kept)
+            ctx.act = (1 if res is not None else 2) if relu else 0
+            ctx.save_for_backward(x, y if ctx.act == 1 else None, weight, bias, save, stats)
             ctx.sync, ctx.comm, ctx.has_res = sync, comm, res is not None
         else:
             dummy = torch.empty(2 * C + 1, **f32)
             K.apply(x, resc, y, C, dummy, weight, bias, running_mean, running_var, nbt, mom, float(eps), False,
                     relu, dummy)
             ctx.sync = None
-        ctx.relu = relu
         return y
 
     @staticmethod
@@ -79,7 +81,7 @@ class BNActFn(torch.autograd.Function):
         if ctx.sync is None:
             raise RuntimeError("BNActFn: backward through an eval-mode BatchNorm is not supported")
         K = _K()
-        x, y, weight, save, stats = ctx.saved_tensors
+        x, y, weight, bias, save, stats = ctx.saved_tensors
         C = x.shape[1]
         dy = _cl(dy)
         part, ticket = _Workspace.get(x.device, C)
@@ -87,11 +89,11 @@ class BNActFn(torch.autograd.Function):
         out = torch.empty(2 * C, **f32)
         dgamma = torch.empty(C, **f32)
         dbeta = torch.empty(C, **f32)
-        K.bwd_stats(dy, y, x, C, save, part, ticket, out, dgamma, dbeta)
+        K.bwd_stats(dy, y, x, C, ctx.act, save, weight, bias, part, ticket, out, dgamma, dbeta)
         sums = ctx.comm.all_reduce(out) if ctx.sync else out
         dx = torch.empty_like(x, memory_format=_CL)
         dres = torch.empty_like(x, memory_format=_CL) if ctx.has_res else None
-        K.bwd_elemt(dy, y, x, C, save, sums, stats, weight, dx, dres)
+        K.bwd_elemt(dy, y, x, C, ctx.act, save, sums, stats, weight, bias, dx, dres)
         return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
 
 

@@ -1,0 +1,92 @@
+"""1x1 convolution of a channels_last activation as GEMMs over its NHWC rows.
+
+Used by the ResNet-50 stress model (models/resnet.py): 36 of its 53 convolutions
+are 1x1.  With the activation stored NHWC, a 1x1 conv is a plain GEMM on the
+[P = N*H*W, C] row matrix, so it runs on hipBLASLt with no layout work:
+
+  forward  out[P, Cout] = rows[P, Cin] @ W^T
+  dgrad    d_rows[P, Cin] = dY[P, Cout] @ W
+  wgrad    dW[Cout, Cin] = dY^T @ rows   -- K = P is huge (401,408 at 56x56, bs 128)
+           and the output tiny, so a single GEMM leaves the chip idle (hipBLASLt
+           picks a 16-workgroup tile: 650 us for a 13 GFLOP problem).  It runs as
+           a split-K batched GEMM instead: the rows are cut into S chunks of
+           ~2-4k rows, one fp32 [Cout, Cin] partial per chunk (bmm, fp32
+           output), summed in fp32 -- 7-13x faster at 56x56 / 28x28 (measured:
+           profiles/r1_gemm1x1_bs128.txt).
+The fp32 weight is cast to the compute dtype inside the op and its gradient
+comes back in fp32 straight from the fp32 partial sum (no bf16 round trip).
+"""
+from __future__ import annotations
+
+import torch
+
+WGRAD_CHUNK_ROWS = 2048
+WGRAD_MAX_SPLIT = 64
+
+
+def wgrad_split(P: int) -> int:
+    """Number of K chunks for a wgrad over P rows: the largest power of two
+    <= min(64, P // 2048) that divides P."""
+    s = 1
+    while s * 2 <= min(WGRAD_MAX_SPLIT, P // WGRAD_CHUNK_ROWS) and P % (s * 2) == 0:
+        s *= 2
+    return s
+
+
+def _wgrad(dyr: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
+    """fp32 dY^T @ rows for [P, Cout] / [P, Cin] row matrices."""
+    if not dyr.is_cuda:
+        return torch.mm(dyr.t().float(), rows.float())
+    P = rows.shape[0]
+    S = wgrad_split(P)
+    if S == 1:
+        return torch.mm(dyr.t(), rows, out_dtype=torch.float32)
+    part = torch.bmm(dyr.view(S, P // S, -1).transpose(1, 2), rows.view(S, P // S, -1), out_dtype=torch.float32)
+    return part.sum(0)
+
+
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] (any layout) -> contiguous [N*H*W, C] row matrix."""
+    r = t.permute(0, 2, 3, 1)
+    if not r.is_contiguous():
+        r = r.contiguous()
+    return r.reshape(-1, t.shape[1])
+
+
+class Conv1x1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stride: int, cdtype: torch.dtype):
+        in_shape = x.shape
+        if stride != 1:
+            x = x[:, :, ::stride, ::stride]
+        N, C, H, W = x.shape
+        rows = _rows(x.to(cdtype))
+        w = weight.reshape(weight.shape[0], C).to(cdtype)
+        out = torch.mm(rows, w.t())
+        ctx.save_for_backward(rows, w)
+        ctx.geom = (N, C, H, W, stride, in_shape)
+        ctx.wshape = weight.shape
+        return out.view(N, H, W, -1).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        rows, w = ctx.saved_tensors
+        N, C, H, W, stride, in_shape = ctx.geom
+        dyr = _rows(dy.to(rows.dtype))
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.mm(dyr, w).view(N, H, W, C).permute(0, 3, 1, 2)
+            if stride != 1:
+                n0, c0, h0, w0 = in_shape
+                full = torch.zeros((n0, h0, w0, c0), dtype=dx.dtype, device=dx.device).permute(0, 3, 1, 2)
+                full[:, :, ::stride, ::stride] = dx
+                dx = full
+        if ctx.needs_input_grad[1]:
+            dw = _wgrad(dyr, rows).view(ctx.wshape)
+        return dx, dw, None, None
+
+
+def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int, cdtype: torch.dtype) -> torch.Tensor:
+    """Bias-free 1x1 conv (stride 1 or 2) of ``x`` with the fp32 ``weight``; the
+    output is a channels_last [N, Cout, H', W'] tensor in ``cdtype``."""
+    return Conv1x1Fn.apply(x, weight, int(stride), cdtype)

@@ -1,0 +1,17 @@
+# Re-entry check: GPU tests, smoke, ConvNet bench, ResNet-50 native/torch benches
+set -o pipefail
+TAG=${1:-round}
+cd $GRAFT_REPO_ROOT
+OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
+mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests > $OUT/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; grep -E "FAIL|ERROR|passed|failed" $OUT/pytest.log | tail -20
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+timeout -k 10 200 python __graft_entry__.py > $OUT/smoke.log 2>&1 || { tail $OUT/smoke.log; exit 1; }
+tail -1 $OUT/smoke.log
+timeout -k 10 200 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
+timeout -k 10 300 python bench.py --model resnet50 --steps 20 --warmup 5 > $OUT/rn_native.json 2> $OUT/rn_native.err || { tail -20 $OUT/rn_native.err; exit 1; }
+cat $OUT/rn_native.json
+timeout -k 10 300 python bench.py --model resnet50 --resnet-impl torch --steps 20 --warmup 5 > $OUT/rn_torch.json 2> $OUT/rn_torch.err || { tail -20 $OUT/rn_torch.err; exit 1; }
+cat $OUT/rn_torch.json

@@ -32,3 +32,29 @@ def test_resnet50_bucket_plan_matches_torch():
     assert [sorted(b) for b in ours] == [sorted(n - 1 - i for i in b) for b in theirs]
     sizes = [sum(params[i].numel() * 4 for i in b) / 2 ** 20 for b in ours]
     assert [round(s, 2) for s in sizes] == [7.82, 30.04, 25.04, 25.32, 9.27]
+
+
+def test_conv1x1_op_matches_conv2d():
+    """ops/conv1x1.py (GEMMs on NHWC rows, split-K weight gradient) vs F.conv2d, stride 1 and 2."""
+    import torch.nn.functional as F
+
+    from ddp_practice_amd.ops.conv1x1 import conv1x1, wgrad_split
+
+    assert wgrad_split(128 * 56 * 56) == 64 and wgrad_split(128 * 14 * 14) == 8 and wgrad_split(6272) == 2
+    assert wgrad_split(1000) == 1
+    g = torch.Generator().manual_seed(0)
+    for stride in (1, 2):
+        x = torch.randn(2, 8, 6, 6, generator=g).contiguous(memory_format=torch.channels_last).requires_grad_()
+        w = torch.randn(12, 8, 1, 1, generator=g, requires_grad=True)
+        x2 = x.detach().clone().requires_grad_()
+        w2 = w.detach().clone().requires_grad_()
+        out = conv1x1(x, w, stride, torch.float32)
+        ref = F.conv2d(x2, w2, stride=stride)
+        assert out.is_contiguous(memory_format=torch.channels_last)
+        torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+        gy = torch.randn(ref.shape, generator=g)
+        out.backward(gy)
+        ref.backward(gy)
+        torch.testing.assert_close(x.grad, x2.grad, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(w.grad, w2.grad, rtol=1e-5, atol=1e-5)
+        assert w.grad.dtype == torch.float32

@@ -53,6 +53,47 @@ def test_bn_act_fwd_bwd(C, res, relu, dtype):
         assert _rel(rs.grad, r64.grad) < gtol
 
 
+@pytest.mark.parametrize("shape,res,relu,dtype", [((32, 64, 28, 28), False, True, torch.bfloat16),
+                                                  ((128, 2048, 7, 7), True, True, torch.bfloat16),
+                                                  ((16, 1024, 14, 14), False, False, torch.float32),
+                                                  ((8, 128, 56, 56), True, False, torch.float32)])
+def test_bn_act_large(shape, res, relu, dtype):
+    """Row counts that use the whole two-level ticket tree (up to 512 row blocks per
+    channel chunk, several chunks) and cumulative-average running stats
+    (momentum=None: num_batches_tracked bumped by the statistics kernel)."""
+    from ddp_practice_amd.ops.bn_nhwc import bn_act
+
+    torch.manual_seed(2)
+    N, C, H, W = shape
+    bn = torch.nn.BatchNorm2d(C, momentum=None).to(DEV)
+    ref = copy.deepcopy(bn).double()
+    for it in range(2):
+        x = (torch.randn(N, C, H, W, device=DEV) * 1.5 + 0.3 * it).to(dtype).contiguous(
+            memory_format=torch.channels_last)
+        r = torch.randn(N, C, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last) \
+            if res else None
+        xs = x.detach().clone().requires_grad_()
+        rs = r.detach().clone().requires_grad_() if res else None
+        y = bn_act(xs, bn, res=rs, relu=relu)
+        x64 = x.double().detach().requires_grad_()
+        r64 = r.double().detach().requires_grad_() if res else None
+        y64 = ref(x64) + (r64 if res else 0)
+        if relu:
+            y64 = y64.relu()
+        tol = 1e-5 if dtype == torch.float32 else 1e-2
+        assert _rel(y, y64) < tol
+        assert _rel(bn.running_mean, ref.running_mean) < 1e-5 and _rel(bn.running_var, ref.running_var) < 1e-5
+        assert int(bn.num_batches_tracked) == it + 1
+        g = torch.randn_like(y64)
+        (y.double() * g).sum().backward()
+        (y64 * g).sum().backward()
+        gtol = 1e-4 if dtype == torch.float32 else 3e-2
+        assert _rel(xs.grad, x64.grad) < gtol
+        if res:
+            assert _rel(rs.grad, r64.grad) < gtol
+    assert _rel(bn.weight.grad, ref.weight.grad) < gtol and _rel(bn.bias.grad, ref.bias.grad) < gtol
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_pools(dtype):
     from ddp_practice_amd.ops.bn_nhwc import global_avg_pool, max_pool_3x3s2
