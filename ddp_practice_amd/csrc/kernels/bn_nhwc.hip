@@ -38,9 +38,10 @@ namespace bnh {
 constexpr int THR = 256;
 constexpr int LR_MAX = 32;   // lanes per row segment of a chunk
 constexpr int G1 = 16;       // level-1 group size of the ticket tree
-constexpr int MAXGR = 512;   // row blocks per chunk in the statistics kernels
+constexpr int MAXGR = 1024;  // row blocks per chunk in the statistics kernels
 constexpr int U = 4;         // rows in flight per lane
-constexpr int MAXTICKETS = 1024;
+constexpr int UF = 8;        // rows in flight per lane, forward statistics (one input)
+constexpr int MAXTICKETS = 2048;
 
 template <typename T> struct V16 { static constexpr int N = 16 / sizeof(T); };
 
@@ -188,12 +189,12 @@ fwd_stats_kernel(const T* __restrict__ x, long long M, int C, const float* __res
 #pragma unroll
     for (int j = 0; j < VEC; ++j) sh[j] = shift[g.c0 + j];
     long long r = r0 + g.ro;
-    for (; r + (U - 1) * g.RP < r1; r += U * g.RP) {
-      float a[U][VEC];
+    for (; r + (UF - 1) * g.RP < r1; r += UF * g.RP) {
+      float a[UF][VEC];
 #pragma unroll
-      for (int u = 0; u < U; ++u) load_vec<T>(x + (r + u * g.RP) * C + g.c0, a[u]);
+      for (int u = 0; u < UF; ++u) load_vec<T>(x + (r + u * g.RP) * C + g.c0, a[u]);
 #pragma unroll
-      for (int u = 0; u < U; ++u)
+      for (int u = 0; u < UF; ++u)
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
           const float d = a[u][j] - sh[j];
@@ -582,6 +583,14 @@ static void check_rows(const at::Tensor& t, long long M, int C) {
 struct Grid2 {
   int Gr, Gc;
 };
+// workgroup-count targets (tunable: bn_nhwc.set_grid_targets; scripts/bn_sweep.py)
+static int g_stats_target = 1024;
+static int g_elt_target = 2048;
+void set_grid_targets(int64_t stats, int64_t elt) {
+  TORCH_CHECK(stats >= 1 && elt >= 1);
+  g_stats_target = (int)stats;
+  g_elt_target = (int)elt;
+}
 template <typename T>
 static Grid2 chunk_grid(long long M, int C, int target) {
   constexpr int VEC = V16<T>::N;
@@ -596,7 +605,7 @@ static Grid2 chunk_grid(long long M, int C, int target) {
 }
 template <typename T>
 static Grid2 stats_grid(long long M, int C) {
-  Grid2 g = chunk_grid<T>(M, C, 1024);
+  Grid2 g = chunk_grid<T>(M, C, g_stats_target);
   g.Gr = std::min(g.Gr, MAXGR);
   return g;
 }
@@ -636,7 +645,7 @@ void apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, int64_t C,
   if (res.has_value()) check_rows(*res, M, (int)C);
   dispatch(x, [&](auto tag) {
     typedef decltype(tag) T;
-    const Grid2 g = chunk_grid<T>(M, (int)C, 2048);
+    const Grid2 g = chunk_grid<T>(M, (int)C, g_elt_target);
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(g.Gr, g.Gc), dim3(THR), 0, cur_stream(), dp<T>(x),
                          res.has_value() ? dp<T>(*res) : nullptr, dp<T>(y), M, (int)C, stats.data_ptr<float>(),
@@ -693,7 +702,7 @@ void bwd_elemt(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, int64_t
   if (dres.has_value()) check_rows(*dres, M, (int)C);
   dispatch(x, [&](auto tag) {
     typedef decltype(tag) T;
-    const Grid2 g = chunk_grid<T>(M, (int)C, 2048);
+    const Grid2 g = chunk_grid<T>(M, (int)C, g_elt_target);
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(g.Gr, g.Gc), dim3(THR), 0, cur_stream(), dp<T>(dy),
                          act == ACT_Y ? dp<T>(*y) : nullptr, dp<T>(x), M, (int)C, save.data_ptr<float>(),
@@ -767,6 +776,7 @@ void avgpool_bwd(at::Tensor dy, at::Tensor dx, int64_t HW) {
 void register_bn_nhwc(pybind11::module& m) {
   auto s = m.def_submodule("bn_nhwc", "channels-last BatchNorm(+add)(+ReLU), max-pool 3x3/2, global avg-pool");
   s.def("fwd_stats", &bnh::fwd_stats);
+  s.def("set_grid_targets", &bnh::set_grid_targets);
   s.def("apply", &bnh::apply);
   s.def("bwd_stats", &bnh::bwd_stats);
   s.def("bwd_elemt", &bnh::bwd_elemt);
