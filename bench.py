@@ -34,6 +34,17 @@ def _comm_desc() -> str:
     return f"{name} (xgmi {st})" if st else name
 
 
+def _force_collectives():
+    """Profiling/rehearsal: run the DDP + SyncBN collective code path in a world of one."""
+    from ddp_practice_amd.parallel import comm as _comm
+
+    _comm.Communicator.force_active = True
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29571")
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -79,13 +90,7 @@ def main(argv=None):
     dev = torch.device("cuda", local_rank)
     dist_path = world > 1 or args.force_collectives
     if args.force_collectives:
-        from ddp_practice_amd.parallel import comm as _comm
-
-        _comm.Communicator.force_active = True
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29571")
-        os.environ.setdefault("RANK", "0")
-        os.environ.setdefault("WORLD_SIZE", "1")
+        _force_collectives()
     if dist_path:
         ddist.init_process_group(backend="xgmi" if args.share_gpu else "nccl")
     rank = ddist.get_rank()
@@ -203,7 +208,10 @@ def bench_resnet(args):
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    dist_path = world > 1 or args.force_collectives
+    if args.force_collectives:
+        _force_collectives()
+    if dist_path:
         ddist.init_process_group(backend="nccl")
     rank = ddist.get_rank()
     amp = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": None}[args.amp_dtype]
@@ -212,7 +220,7 @@ def bench_resnet(args):
     model = resnet50(amp_dtype=amp, fused=args.resnet_impl == "native").to(dev)
     if args.resnet_impl == "torch":
         model = model.to(memory_format=torch.channels_last)
-    if world > 1:
+    if dist_path:
         if not args.no_sync_bn:
             model = convert_sync_batchnorm(model)
         model = DistributedDataParallel(model, device_ids=[local_rank])
@@ -257,7 +265,8 @@ def bench_resnet(args):
             "data": f"synthetic 3x{args.image_size}x{args.image_size}, random-init weights",
             "config": {"model": "ResNet-50 (25,557,032 params)", "global_batch": bs * world, "seq_len": None,
                        "parallelism": f"dp{world}", "per_rank_batch": bs, "impl": args.resnet_impl,
-                       "sync_bn": world > 1 and not args.no_sync_bn, "optimizer": "SGD(lr=1e-4)"},
+                       "sync_bn": dist_path and not args.no_sync_bn, "optimizer": "SGD(lr=1e-4)",
+                       "comm": _comm_desc() if dist_path else "none"},
         }), flush=True)
     ddist.destroy_process_group()
 

@@ -37,8 +37,9 @@ namespace bnh {
 
 constexpr int THR = 256;
 constexpr int LR_MAX = 32;   // lanes per row segment of a chunk
-constexpr int G1 = 16;       // level-1 group size of the ticket tree
+constexpr int G1 = 32;       // level-1 group size of the ticket tree
 constexpr int MAXGR = 1024;  // row blocks per chunk in the statistics kernels
+constexpr int SHIFT_OFF = 4; // stats layout: [0,C) s1, [C,2C) s2, [2C] n, shift copy at 2C+SHIFT_OFF (16-B aligned)
 constexpr int U = 4;         // rows in flight per lane
 constexpr int UF = 8;        // rows in flight per lane, forward statistics (one input)
 constexpr int MAXTICKETS = 2048;
@@ -59,6 +60,27 @@ __device__ __forceinline__ void store_vec(T* p, const float* f) {
 #pragma unroll
   for (int j = 0; j < V16<T>::N; ++j) e[j] = Cvt<T>::from_f(f[j]);
   *reinterpret_cast<f32x4*>(p) = raw;
+}
+
+// VEC consecutive floats (VEC % 4 == 0, 16-B aligned) as 16-B loads
+template <int VEC>
+__device__ __forceinline__ void ldf(const float* __restrict__ p, float* d) {
+#pragma unroll
+  for (int k = 0; k < VEC / 4; ++k) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(p + 4 * k);
+    d[4 * k] = v[0];
+    d[4 * k + 1] = v[1];
+    d[4 * k + 2] = v[2];
+    d[4 * k + 3] = v[3];
+  }
+}
+template <int VEC>
+__device__ __forceinline__ void stf(float* __restrict__ p, const float* d) {
+#pragma unroll
+  for (int k = 0; k < VEC / 4; ++k) {
+    f32x4 v = {d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]};
+    *reinterpret_cast<f32x4*>(p + 4 * k) = v;
+  }
 }
 
 __host__ __device__ inline int chunk_lanes(int C, int vec) { return C / vec < LR_MAX ? C / vec : LR_MAX; }
@@ -105,19 +127,40 @@ __device__ __forceinline__ bool ticket_last(unsigned* ticket, int n, int* s_flag
   return *s_flag != 0;
 }
 
-// dst[t] = sum_{g < n} src[g*W + t] (n <= 2*G1), fixed order; the loads of a
-// batch of G1 rows are issued before the first add.
-__device__ __noinline__ void sum_rows(const float* __restrict__ src, int n, int W, float* __restrict__ dst) {
-  for (int t = threadIdx.x; t < W; t += THR) {
-    float acc = 0.f;
-    for (int g0 = 0; g0 < n; g0 += G1) {
-      float v[G1];
+// dst[t] = sum_{g < n} src[g*W + t], W % 4 == 0, fixed order.  Lanes load
+// 16-B column vectors; the RG = THR/(W/4) row groups of the block each sum
+// every RG-th row with up to 16 loads in flight per lane, then the RG partials
+// are added in group order through LDS (scr: >= THR*4 floats).
+__device__ __noinline__ void sum_rows(const float* __restrict__ src, int n, int W, float* __restrict__ dst,
+                                      float* scr) {
+  const int W4 = W / 4;
+  const int RG = W4 >= THR ? 1 : THR / W4;
+  for (int base = 0; base < W4; base += THR) {
+    const int col = base + (int)threadIdx.x % (W4 >= THR ? THR : W4);
+    const int rg = W4 >= THR ? 0 : (int)threadIdx.x / W4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (rg < RG && col < W4) {
+      for (int g0 = rg; g0 < n; g0 += 16 * RG) {
+        f32x4 v[16];
 #pragma unroll
-      for (int u = 0; u < G1; ++u) v[u] = src[(size_t)(g0 + u < n ? g0 + u : n - 1) * W + t];
+        for (int u = 0; u < 16; ++u) {
+          const int g = g0 + u * RG;
+          v[u] = *reinterpret_cast<const f32x4*>(src + (size_t)(g < n ? g : n - 1) * W + 4 * col);
+        }
 #pragma unroll
-      for (int u = 0; u < G1; ++u) acc += g0 + u < n ? v[u] : 0.f;
+        for (int u = 0; u < 16; ++u)
+          if (g0 + u * RG < n) acc += v[u];
+      }
     }
-    dst[t] = acc;
+    __syncthreads();
+    if (rg < RG && col < W4) *reinterpret_cast<f32x4*>(scr + 4 * ((size_t)rg * (W4 >= THR ? THR : W4) + (col - base))) = acc;
+    __syncthreads();
+    const int nc = W4 - base < THR ? W4 - base : THR;
+    if ((int)threadIdx.x < nc) {
+      f32x4 t = {0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < RG; ++r) t += *reinterpret_cast<const f32x4*>(scr + 4 * ((size_t)r * nc + threadIdx.x));
+      *reinterpret_cast<f32x4*>(dst + 4 * (base + threadIdx.x)) = t;
+    }
   }
 }
 
@@ -125,7 +168,7 @@ __device__ __noinline__ void sum_rows(const float* __restrict__ src, int n, int 
 // true in the single workgroup per chunk that ends with the chunk's W totals in
 // red[0, W).  part: [Gc*Gr + Gc*NG][W] floats; tickets: [Gc*NG + Gc].
 __device__ bool chunk_reduce(float* __restrict__ part, unsigned* __restrict__ tickets, int W, float* red,
-                             int* s_flag) {
+                             float* scr, int* s_flag) {
   const int Gr = gridDim.x, Gc = gridDim.y, y = blockIdx.y;
   const int NG = (Gr + G1 - 1) / G1;
   float* p1 = part + (size_t)y * Gr * W;
@@ -135,13 +178,13 @@ __device__ bool chunk_reduce(float* __restrict__ part, unsigned* __restrict__ ti
   const int gsz = min(G1, Gr - grp * G1);
   if (!ticket_last(tickets + y * NG + grp, gsz, s_flag)) return false;
   if (NG == 1) {
-    sum_rows(p1, gsz, W, red);
+    sum_rows(p1, gsz, W, red, scr);
     __syncthreads();
     return true;
   }
-  sum_rows(p1 + (size_t)grp * G1 * W, gsz, W, p2 + (size_t)grp * W);
+  sum_rows(p1 + (size_t)grp * G1 * W, gsz, W, p2 + (size_t)grp * W, scr);
   if (!ticket_last(tickets + Gc * NG + y, NG, s_flag)) return false;
-  sum_rows(p2, NG, W, red);
+  sum_rows(p2, NG, W, red, scr);
   __syncthreads();
   return true;
 }
@@ -169,7 +212,7 @@ __device__ __forceinline__ void block_combine(const Chunk<VEC>& g, const float* 
 
 // ----------------------------------------------------------------------------
 // forward statistics: stats[0..C) = sum(x-shift), [C..2C) = sum((x-shift)^2),
-// [2C] = rows, [2C+1 .. 3C+1) = shift (copied for the apply / backward)
+// [2C] = rows, [2C+4 .. 3C+4) = shift (copied for the apply / backward)
 template <typename T>
 __global__ void __launch_bounds__(THR)
 fwd_stats_kernel(const T* __restrict__ x, long long M, int C, const float* __restrict__ shift,
@@ -214,12 +257,12 @@ fwd_stats_kernel(const T* __restrict__ x, long long M, int C, const float* __res
     }
   }
   block_combine<VEC>(g, s1, s2, red, scratch);
-  if (!chunk_reduce(part, tickets, 2 * g.CC, red, &s_flag)) return;
+  if (!chunk_reduce(part, tickets, 2 * g.CC, red, scratch, &s_flag)) return;
   const int cb = (int)blockIdx.y * g.CC;
   for (int t = threadIdx.x; t < g.CC; t += THR) {
     stats[cb + t] = red[t];
     stats[C + cb + t] = red[g.CC + t];
-    stats[2 * C + 1 + cb + t] = shift[cb + t];
+    stats[2 * C + SHIFT_OFF + cb + t] = shift[cb + t];
   }
   if (blockIdx.y == 0 && threadIdx.x == 0) {
     stats[2 * C] = (float)M;
@@ -238,30 +281,48 @@ apply_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__
   constexpr int VEC = V16<T>::N;
   const Chunk<VEC> g(C);
   if (!g.active) return;
-  float s[VEC], b[VEC];
+  float s[VEC], b[VEC], mean[VEC], istd[VEC], ga[VEC], be[VEC];
+  ldf<VEC>(gamma + g.c0, ga);
+  ldf<VEC>(beta + g.c0, be);
+  if (train) {
+    float s1[VEC], s2[VEC], sh[VEC], var[VEC];
+    ldf<VEC>(stats + g.c0, s1);
+    ldf<VEC>(stats + C + g.c0, s2);
+    ldf<VEC>(stats + 2 * C + SHIFT_OFF + g.c0, sh);
+    const float n = stats[2 * C];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const float m1 = s1[j] / n;
+      var[j] = fmaxf(s2[j] / n - m1 * m1, 0.f);
+      mean[j] = sh[j] + m1;
+      istd[j] = rsqrtf(var[j] + eps);
+    }
+    if (blockIdx.x == 0 && g.ro == 0) {
+      stf<VEC>(save + g.c0, mean);
+      stf<VEC>(save + C + g.c0, istd);
+      const float mom = momentum >= 0.f ? momentum : 1.f / (float)nbt[0];  // nbt bumped by the stats kernel
+      float rm[VEC], rv[VEC];
+      ldf<VEC>(rmean + g.c0, rm);
+      ldf<VEC>(rvar + g.c0, rv);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        rm[j] = (1.f - mom) * rm[j] + mom * mean[j];
+        rv[j] = (1.f - mom) * rv[j] + mom * var[j] * (n / fmaxf(n - 1.f, 1.f));
+      }
+      stf<VEC>(rmean + g.c0, rm);
+      stf<VEC>(rvar + g.c0, rv);
+    }
+  } else {
+    float rv[VEC];
+    ldf<VEC>(rmean + g.c0, mean);
+    ldf<VEC>(rvar + g.c0, rv);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) istd[j] = rsqrtf(rv[j] + eps);
+  }
 #pragma unroll
   for (int j = 0; j < VEC; ++j) {
-    const int c = g.c0 + j;
-    float mean, istd;
-    if (train) {
-      const float n = stats[2 * C];
-      const float m1 = stats[c] / n;
-      const float var = fmaxf(stats[C + c] / n - m1 * m1, 0.f);
-      mean = stats[2 * C + 1 + c] + m1;
-      istd = rsqrtf(var + eps);
-      if (blockIdx.x == 0 && g.ro == 0) {
-        save[c] = mean;
-        save[C + c] = istd;
-        const float mom = momentum >= 0.f ? momentum : 1.f / (float)nbt[0];  // nbt bumped by the stats kernel
-        rmean[c] = (1.f - mom) * rmean[c] + mom * mean;
-        rvar[c] = (1.f - mom) * rvar[c] + mom * var * (n / fmaxf(n - 1.f, 1.f));
-      }
-    } else {
-      mean = rmean[c];
-      istd = rsqrtf(rvar[c] + eps);
-    }
-    s[j] = gamma[c] * istd;
-    b[j] = fmaf(-mean, s[j], beta[c]);
+    s[j] = ga[j] * istd[j];
+    b[j] = fmaf(-mean[j], s[j], be[j]);
   }
   long long r0, r1;
   row_range(M, r0, r1);
@@ -301,13 +362,16 @@ template <int VEC, int ACT>
 struct BwdLane {
   float mu[VEC], is[VEC], s[VEC], b[VEC];
   __device__ void init(int c0, int C, const float* save, const float* gamma, const float* beta) {
+    ldf<VEC>(save + c0, mu);
+    ldf<VEC>(save + C + c0, is);
+    if (ACT == ACT_RECOMPUTE) {
+      float ga[VEC], be[VEC];
+      ldf<VEC>(gamma + c0, ga);
+      ldf<VEC>(beta + c0, be);
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-      mu[j] = save[c0 + j];
-      is[j] = save[C + c0 + j];
-      if (ACT == ACT_RECOMPUTE) {
-        s[j] = gamma[c0 + j] * is[j];
-        b[j] = fmaf(-mu[j], s[j], beta[c0 + j]);
+      for (int j = 0; j < VEC; ++j) {
+        s[j] = ga[j] * is[j];
+        b[j] = fmaf(-mu[j], s[j], be[j]);
       }
     }
   }
@@ -371,7 +435,7 @@ bwd_stats_kernel(const T* __restrict__ dy, const T* __restrict__ y, const T* __r
     }
   }
   block_combine<VEC>(g, s1, s2, red, scratch);
-  if (!chunk_reduce(part, tickets, 2 * g.CC, red, &s_flag)) return;
+  if (!chunk_reduce(part, tickets, 2 * g.CC, red, scratch, &s_flag)) return;
   const int cb = (int)blockIdx.y * g.CC;
   for (int t = threadIdx.x; t < g.CC; t += THR) {
     out[cb + t] = dbeta[cb + t] = red[t];
@@ -393,11 +457,14 @@ bwd_elemt_kernel(const T* __restrict__ dy, const T* __restrict__ y, const T* __r
   L.init(g.c0, C, save, gamma, beta);
   float gi[VEC], k1[VEC], k2[VEC];
   const float n = fstats[2 * C];
+  ldf<VEC>(gamma + g.c0, gi);
+  ldf<VEC>(sums + g.c0, k1);
+  ldf<VEC>(sums + C + g.c0, k2);
 #pragma unroll
   for (int j = 0; j < VEC; ++j) {
-    gi[j] = gamma[g.c0 + j] * L.is[j];
-    k1[j] = sums[g.c0 + j] / n;
-    k2[j] = sums[C + g.c0 + j] / n;
+    gi[j] *= L.is[j];
+    k1[j] /= n;
+    k2[j] /= n;
   }
   auto row = [&](long long o, const float* d, const float* xv, const float* yv) {
     float z[VEC], e[VEC];
@@ -583,13 +650,18 @@ static void check_rows(const at::Tensor& t, long long M, int C) {
 struct Grid2 {
   int Gr, Gc;
 };
-// workgroup-count targets (tunable: bn_nhwc.set_grid_targets; scripts/bn_sweep.py)
-static int g_stats_target = 1024;
-static int g_elt_target = 2048;
-void set_grid_targets(int64_t stats, int64_t elt) {
-  TORCH_CHECK(stats >= 1 && elt >= 1);
+// workgroup-count targets (tunable: bn_nhwc.set_grid_targets; scripts/bn_sweep.py).
+// Statistics: fewer, longer workgroups win (the ticket tree's tail grows with the
+// row-block count): 128 below 64 MB of input, 256 above (measured on ResNet-50
+// shapes, profiles/r1_bn_sweep.txt).  0 = that rule.
+static int g_stats_target = 0;
+static int g_apply_target = 512;
+static int g_elemt_target = 1024;
+void set_grid_targets(int64_t stats, int64_t apply, int64_t elemt) {
+  TORCH_CHECK(stats >= 0 && apply >= 1 && elemt >= 1);
   g_stats_target = (int)stats;
-  g_elt_target = (int)elt;
+  g_apply_target = (int)apply;
+  g_elemt_target = (int)elemt;
 }
 template <typename T>
 static Grid2 chunk_grid(long long M, int C, int target) {
@@ -605,7 +677,8 @@ static Grid2 chunk_grid(long long M, int C, int target) {
 }
 template <typename T>
 static Grid2 stats_grid(long long M, int C) {
-  Grid2 g = chunk_grid<T>(M, C, g_stats_target);
+  const int target = g_stats_target > 0 ? g_stats_target : (M * C * (long long)sizeof(T) < (64ll << 20) ? 128 : 256);
+  Grid2 g = chunk_grid<T>(M, C, target);
   g.Gr = std::min(g.Gr, MAXGR);
   return g;
 }
@@ -623,7 +696,7 @@ void fwd_stats(at::Tensor x, int64_t C, at::Tensor shift, at::Tensor part, at::T
                c10::optional<at::Tensor> nbt) {
   const long long M = x.numel() / C;
   check_rows(x, M, (int)C);
-  TORCH_CHECK(stats.numel() >= 3 * C + 1 && shift.numel() == C);
+  TORCH_CHECK(stats.numel() >= 3 * C + SHIFT_OFF && shift.numel() == C);
   dispatch(x, [&](auto tag) {
     typedef decltype(tag) T;
     const Grid2 g = stats_grid<T>(M, (int)C);
@@ -645,7 +718,7 @@ void apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, int64_t C,
   if (res.has_value()) check_rows(*res, M, (int)C);
   dispatch(x, [&](auto tag) {
     typedef decltype(tag) T;
-    const Grid2 g = chunk_grid<T>(M, (int)C, g_elt_target);
+    const Grid2 g = chunk_grid<T>(M, (int)C, g_apply_target);
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(g.Gr, g.Gc), dim3(THR), 0, cur_stream(), dp<T>(x),
                          res.has_value() ? dp<T>(*res) : nullptr, dp<T>(y), M, (int)C, stats.data_ptr<float>(),
@@ -702,7 +775,7 @@ void bwd_elemt(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, int64_t
   if (dres.has_value()) check_rows(*dres, M, (int)C);
   dispatch(x, [&](auto tag) {
     typedef decltype(tag) T;
-    const Grid2 g = chunk_grid<T>(M, (int)C, g_elt_target);
+    const Grid2 g = chunk_grid<T>(M, (int)C, g_elemt_target);
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(g.Gr, g.Gc), dim3(THR), 0, cur_stream(), dp<T>(dy),
                          act == ACT_Y ? dp<T>(*y) : nullptr, dp<T>(x), M, (int)C, save.data_ptr<float>(),

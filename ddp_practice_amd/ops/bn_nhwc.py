@@ -57,7 +57,7 @@ class BNActFn(torch.autograd.Function):
         f32 = dict(dtype=torch.float32, device=dev)
         if training:
             part, ticket = _Workspace.get(dev, C)
-            stats = torch.empty(3 * C + 1, **f32)
+            stats = torch.empty(3 * C + 4, **f32)
             K.fwd_stats(x, C, running_mean, part, ticket, stats, nbt)
             sync = comm is not None and comm.active
             if sync:

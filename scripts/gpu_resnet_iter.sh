@@ -14,3 +14,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/prof -o r
 echo "prof rc=$?"
 f=$(find $OUT/prof -name "*kernel_trace.csv" | head -1)
 python3 $GRAFT_REPO_ROOT/scripts/trace_steady.py $f maxpool_fwd 5 > $OUT/steady.txt && head -45 $OUT/steady.txt
+cd $GRAFT_REPO_ROOT
+timeout -k 10 300 python bench.py --model resnet50 --batch-size $BS --steps 10 --warmup 3 --force-collectives > $OUT/forced.json 2> $OUT/forced.err || { tail -20 $OUT/forced.err; exit 1; }
+cat $OUT/forced.json
