@@ -10,7 +10,8 @@ Execution on a HIP device (``fused=True``): activations are bf16/f16/f32
   * 1x1 convolutions are GEMMs on the NHWC rows ([N*H*W, Cin] x [Cin, Cout],
     hipBLASLt; the weight gradient as a split-K batched GEMM with fp32
     partials: ops/conv1x1.py; stride-2 projections subsample first);
-  * 3x3 / 7x7 convolutions go to MIOpen's NHWC kernels (``F.conv2d``);
+  * 3x3 / 7x7 convolutions go to MIOpen's NHWC kernels (ops/conv_nhwc.py: one
+    cast+layout copy of the weight each way);
   * every BatchNorm runs on the native NHWC kernels with its ReLU and, for the
     last BN of a bottleneck, the residual add fused in (ops/bn_nhwc.py), as
     SyncBatchNorm when the module was converted (one small all-reduce each way);
@@ -25,12 +26,15 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..amp import autocast, compute_dtype
-from ..ops.conv1x1 import conv1x1
+from ..ops.conv1x1 import GradTap, conv1x1
+from ..ops.conv_nhwc import conv_nhwc
 
 
 def _conv(x: torch.Tensor, conv: nn.Conv2d, cdtype: torch.dtype) -> torch.Tensor:
     if conv.kernel_size == (1, 1) and conv.padding == (0, 0) and conv.groups == 1 and conv.bias is None:
         return conv1x1(x, conv.weight, conv.stride[0], cdtype)
+    if conv.bias is None and conv.groups == 1 and conv.dilation == (1, 1):
+        return conv_nhwc(x, conv.weight, conv.stride, conv.padding, cdtype)
     w = conv.weight.to(cdtype)
     out = F.conv2d(x, w, None if conv.bias is None else conv.bias.to(cdtype), conv.stride, conv.padding,
                    conv.dilation, conv.groups)
@@ -76,13 +80,18 @@ class Bottleneck(nn.Module):
     def forward_native(self, x: torch.Tensor, cdtype: torch.dtype) -> torch.Tensor:
         from ..ops.bn_nhwc import bn_act
 
-        out = bn_act(_conv(x, self.conv1, cdtype), self.bn1, relu=True, comm=_comm_of(self.bn1))
+        # identity blocks: conv1's dgrad GEMM accumulates the residual gradient (GradTap)
+        tap = GradTap() if (self.downsample is None and self.bn3.training and torch.is_grad_enabled()
+                            and x.requires_grad and x.is_contiguous(memory_format=torch.channels_last)) else None
+        c1 = conv1x1(x, self.conv1.weight, 1, cdtype, tap) if tap is not None else _conv(x, self.conv1, cdtype)
+        out = bn_act(c1, self.bn1, relu=True, comm=_comm_of(self.bn1))
         out = bn_act(_conv(out, self.conv2, cdtype), self.bn2, relu=True, comm=_comm_of(self.bn2))
         identity = x
         if self.downsample is not None:
             conv, bn = self.downsample[0], self.downsample[1]
             identity = bn_act(_conv(x, conv, cdtype), bn, relu=False, comm=_comm_of(bn))
-        return bn_act(_conv(out, self.conv3, cdtype), self.bn3, res=identity, relu=True, comm=_comm_of(self.bn3))
+        return bn_act(_conv(out, self.conv3, cdtype), self.bn3, res=identity, relu=True, comm=_comm_of(self.bn3),
+                      tap=tap)
 
 
 class ResNet(nn.Module):

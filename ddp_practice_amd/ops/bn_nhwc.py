@@ -46,7 +46,8 @@ def _cl(t: torch.Tensor) -> torch.Tensor:
 
 class BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, res, running_mean, running_var, nbt, momentum, eps, training, relu, comm):
+    def forward(ctx, x, weight, bias, res, running_mean, running_var, nbt, momentum, eps, training, relu, comm,
+                tap=None):
         K = _K()
         x = _cl(x)
         C = x.shape[1]
@@ -69,6 +70,7 @@ class BNActFn(torch.autograd.Function):
             ctx.act = (1 if res is not None else 2) if relu else 0
             ctx.save_for_backward(x, y if ctx.act == 1 else None, weight, bias, save, stats)
             ctx.sync, ctx.comm, ctx.has_res = sync, comm, res is not None
+            ctx.tap = tap if res is not None else None
         else:
             dummy = torch.empty(2 * C + 1, **f32)
             K.apply(x, resc, y, C, dummy, weight, bias, running_mean, running_var, nbt, mom, float(eps), False,
@@ -94,13 +96,16 @@ class BNActFn(torch.autograd.Function):
         dx = torch.empty_like(x, memory_format=_CL)
         dres = torch.empty_like(x, memory_format=_CL) if ctx.has_res else None
         K.bwd_elemt(dy, y, x, C, ctx.act, save, sums, stats, weight, bias, dx, dres)
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
+        if ctx.tap is not None:  # d(res) goes to the consumer's GEMM (ops/conv1x1.py GradTap)
+            ctx.tap.grad, dres = dres, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None
 
 
-def bn_act(x, bn, res=None, relu=True, comm=None):
-    """BatchNorm module ``bn`` applied to channels_last ``x`` (+ res) (+ ReLU)."""
+def bn_act(x, bn, res=None, relu=True, comm=None, tap=None):
+    """BatchNorm module ``bn`` applied to channels_last ``x`` (+ res) (+ ReLU).
+    ``tap``: hand d(res) to a GradTap instead of returning it (ops/conv1x1.py)."""
     return BNActFn.apply(x, bn.weight, bn.bias, res, bn.running_mean, bn.running_var, bn.num_batches_tracked,
-                         bn.momentum, bn.eps, bn.training, relu, comm if bn.training else None)
+                         bn.momentum, bn.eps, bn.training, relu, comm if bn.training else None, tap)
 
 
 class MaxPoolFn(torch.autograd.Function):

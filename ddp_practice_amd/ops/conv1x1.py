@@ -53,9 +53,27 @@ def _rows(t: torch.Tensor) -> torch.Tensor:
     return r.reshape(-1, t.shape[1])
 
 
+class GradTap:
+    """Hand-off of a residual gradient between two autograd nodes of one block.
+
+    A bottleneck without projection computes ``relu(bn3(...) + x)`` where ``x``
+    also feeds ``conv1``; autograd would add the two gradients of ``x`` with a
+    separate elementwise kernel.  With a tap, the BN (ops/bn_nhwc.py) stores
+    d(res) here instead of returning it, and ``conv1``'s dgrad GEMM accumulates
+    onto it in place (``addmm_``: C = C + dY @ W in the GEMM epilogue).  bn3's
+    backward always runs before conv1's (conv1 is upstream of bn3), so the
+    gradient is present when conv1 needs it.
+    """
+
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+
 class Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride: int, cdtype: torch.dtype):
+    def forward(ctx, x, weight, stride: int, cdtype: torch.dtype, tap: GradTap | None = None):
         in_shape = x.shape
         if stride != 1:
             x = x[:, :, ::stride, ::stride]
@@ -66,6 +84,9 @@ class Conv1x1Fn(torch.autograd.Function):
         ctx.save_for_backward(rows, w)
         ctx.geom = (N, C, H, W, stride, in_shape)
         ctx.wshape = weight.shape
+        ctx.tap = tap
+        if tap is not None and stride != 1:
+            raise ValueError("conv1x1: a gradient tap needs stride 1")
         return out.view(N, H, W, -1).permute(0, 3, 1, 2)
 
     @staticmethod
@@ -74,7 +95,15 @@ class Conv1x1Fn(torch.autograd.Function):
         N, C, H, W, stride, in_shape = ctx.geom
         dyr = _rows(dy.to(rows.dtype))
         dx = dw = None
-        if ctx.needs_input_grad[0]:
+        acc = None
+        if ctx.tap is not None:
+            acc, ctx.tap.grad = ctx.tap.grad, None
+        if ctx.needs_input_grad[0] and acc is not None:
+            if acc.shape != (N, C, H, W) or not acc.is_contiguous(memory_format=torch.channels_last):
+                raise RuntimeError("conv1x1: tapped gradient does not match the input")
+            _rows(acc).addmm_(dyr, w)  # acc <- acc + dY @ W (GEMM epilogue accumulate)
+            dx = acc
+        elif ctx.needs_input_grad[0]:
             dx = torch.mm(dyr, w).view(N, H, W, C).permute(0, 3, 1, 2)
             if stride != 1:
                 n0, c0, h0, w0 = in_shape
@@ -83,10 +112,12 @@ class Conv1x1Fn(torch.autograd.Function):
                 dx = full
         if ctx.needs_input_grad[1]:
             dw = _wgrad(dyr, rows).view(ctx.wshape)
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
-def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int, cdtype: torch.dtype) -> torch.Tensor:
+def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int, cdtype: torch.dtype,
+            tap: GradTap | None = None) -> torch.Tensor:
     """Bias-free 1x1 conv (stride 1 or 2) of ``x`` with the fp32 ``weight``; the
-    output is a channels_last [N, Cout, H', W'] tensor in ``cdtype``."""
-    return Conv1x1Fn.apply(x, weight, int(stride), cdtype)
+    output is a channels_last [N, Cout, H', W'] tensor in ``cdtype``.  ``tap``:
+    see :class:`GradTap`."""
+    return Conv1x1Fn.apply(x, weight, int(stride), cdtype, tap)

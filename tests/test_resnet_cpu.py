@@ -58,3 +58,46 @@ def test_conv1x1_op_matches_conv2d():
         torch.testing.assert_close(x.grad, x2.grad, rtol=1e-5, atol=1e-5)
         torch.testing.assert_close(w.grad, w2.grad, rtol=1e-5, atol=1e-5)
         assert w.grad.dtype == torch.float32
+
+
+def test_conv1x1_grad_tap_accumulates():
+    """A tapped residual gradient is accumulated by conv1x1's dgrad GEMM (in place)
+    and equals autograd's sum of the two gradient paths."""
+    from ddp_practice_amd.ops.conv1x1 import GradTap, conv1x1
+
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(2, 8, 5, 5, generator=g).contiguous(memory_format=torch.channels_last).requires_grad_()
+    w = torch.randn(6, 8, 1, 1, generator=g)
+    gy = torch.randn(2, 6, 5, 5, generator=g)
+    extra = torch.randn(2, 8, 5, 5, generator=g).contiguous(memory_format=torch.channels_last)
+    tap = GradTap()
+    out = conv1x1(x, w, 1, torch.float32, tap)
+    tap.grad = extra.clone()  # what the residual BN's backward would have stored
+    out.backward(gy)
+    x2 = x.detach().clone().requires_grad_()
+    (torch.nn.functional.conv2d(x2, w) * gy).sum().backward()
+    torch.testing.assert_close(x.grad, x2.grad + extra, rtol=1e-5, atol=1e-5)
+    assert tap.grad is None
+
+
+def test_conv_nhwc_op_matches_conv2d():
+    """ops/conv_nhwc.py (fp32 master weight, one cast+layout copy each way) vs F.conv2d."""
+    import torch.nn.functional as F
+
+    from ddp_practice_amd.ops.conv_nhwc import conv_nhwc
+
+    g = torch.Generator().manual_seed(3)
+    for stride, pad, k in ((1, 1, 3), (2, 1, 3), (2, 3, 7)):
+        x = torch.randn(2, 4, 11, 11, generator=g).contiguous(memory_format=torch.channels_last).requires_grad_()
+        w = torch.randn(5, 4, k, k, generator=g, requires_grad=True)
+        x2, w2 = x.detach().clone().requires_grad_(), w.detach().clone().requires_grad_()
+        out = conv_nhwc(x, w, (stride, stride), (pad, pad), torch.float32)
+        ref = F.conv2d(x2, w2, stride=stride, padding=pad)
+        assert out.is_contiguous(memory_format=torch.channels_last)
+        torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
+        gy = torch.randn(ref.shape, generator=g)
+        out.backward(gy)
+        ref.backward(gy)
+        torch.testing.assert_close(x.grad, x2.grad, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(w.grad, w2.grad, rtol=1e-4, atol=1e-4)
+        assert w.grad.is_contiguous() and w.grad.dtype == torch.float32
