@@ -111,35 +111,55 @@ __global__ __launch_bounds__(kThreads) void oneshot_kernel(Args a) {
   }
 
   // 2. every rank's granules for my elements, in rank order (identical result on
-  //    every rank); each granule carries its own epoch tag: no flag, no fence
+  //    every rank); each granule carries its own epoch tag: no flag, no fence.
+  //    The loads of PB ranks x 8 elements are all issued before the first tag
+  //    check (one memory round trip per batch, not one per granule); only a
+  //    granule that has not arrived yet is re-polled.
+  constexpr int PB = 4;
   float acc[kPerThread];
+#pragma unroll
+  for (int j = 0; j < kPerThread; ++j) acc[j] = 0.f;
   bool fail = false;
   const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
   unsigned polls = 0;
-  for (int p = 0; p < a.world && !fail; ++p) {
-    const unsigned long long* src =
-        reinterpret_cast<const unsigned long long*>(mine + par_off + (long long)p * a.slot_bytes) + e0;
-    for (int j = 0; j < ne; ++j) {
-      unsigned long long g;
-      while (((g = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) >> 32) != ep) {
-        __builtin_amdgcn_s_sleep(1);
-        if ((++polls & 255u) == 0) {
-          int why = 0;
-          if (__hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) why = 2;
-          else if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) why = 1;
-          if (why) {
-            __hip_atomic_store(a.err, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            fail = true;
-            break;
+  for (int p0 = 0; p0 < a.world && !fail; p0 += PB) {
+    unsigned long long g[PB][kPerThread];
+    const unsigned long long* src[PB];
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+      const int p = p0 + q < a.world ? p0 + q : p0;  // out-of-range batch slots re-read rank p0 (ignored)
+      src[q] = reinterpret_cast<const unsigned long long*>(mine + par_off + (long long)p * a.slot_bytes) + e0;
+#pragma unroll
+      for (int j = 0; j < kPerThread; ++j)  // slots hold whole chunks: j >= ne stays inside the slot
+        g[q][j] = __hip_atomic_load(src[q] + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+      if (p0 + q >= a.world || fail) continue;
+#pragma unroll
+      for (int j = 0; j < kPerThread; ++j) {
+        if (j >= ne || fail) continue;
+        while ((g[q][j] >> 32) != ep) {
+          __builtin_amdgcn_s_sleep(1);
+          g[q][j] = __hip_atomic_load(src[q] + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          if ((++polls & 255u) == 0) {
+            int why = 0;
+            if (__hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) why = 2;
+            else if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) why = 1;
+            if (why) {
+              __hip_atomic_store(a.err, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              fail = true;
+              break;
+            }
           }
         }
+        if (fail) continue;
+        const float x = __uint_as_float((uint32_t)g[q][j]);
+        if (p0 + q == 0) acc[j] = x;
+        else if (OP == 2) acc[j] = fmaxf(acc[j], x);
+        else if (OP == 3) acc[j] = fminf(acc[j], x);
+        else acc[j] += x;
       }
-      if (fail) break;
-      const float x = __uint_as_float((uint32_t)g);
-      if (p == 0) acc[j] = x;
-      else if (OP == 2) acc[j] = fmaxf(acc[j], x);
-      else if (OP == 3) acc[j] = fminf(acc[j], x);
-      else acc[j] += x;
     }
   }
   if (!fail) {

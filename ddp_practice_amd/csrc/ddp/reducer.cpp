@@ -12,6 +12,9 @@
 //    (grad * 1/W into the bucket) and its all-reduce is launched on the
 //    communicator's stream; buckets launch strictly in index order so every
 //    rank issues identical collective sequences.
+//  * Zero-copy buckets: when a bucket's gradients already tile one contiguous
+//    buffer (the fused ConvNet op writes all its parameter gradients into one
+//    output), that buffer is all-reduced in place with AVG: no pack kernel.
 //  * After the last bucket launches, the compute stream is fenced on all of
 //    them and every param.grad becomes a view of its bucket (the
 //    gradient_as_bucket_view=True layout: no copy-back kernel).
@@ -43,6 +46,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
       : params_(std::move(params)), comm_(std::move(comm)), find_unused_(find_unused) {
     TORCH_CHECK(comm_ != nullptr);
     if (const char* e = std::getenv("DPA_REDUCER_JOIN_EACH")) join_each_ = e[0] == '1';
+    if (const char* e = std::getenv("DPA_REDUCER_ZERO_COPY")) zero_copy_ = e[0] != '0';
     ready_.assign(params_.size(), 0);
     set_buckets(buckets);
   }
@@ -195,8 +199,9 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     // i.e. the capture stream under hipGraph capture) — not whatever stream is
     // current on the thread that runs the engine's final callback
     for (size_t b = 0; b < buckets_.size(); ++b) comm_->wait((int)b, on_cuda_ ? work_stream_ : nullptr);
-    // grads become views of the all-reduced buckets
+    // grads become views of the all-reduced buckets (in-place buckets: they already are)
     for (auto& bk : buckets_) {
+      if (bk.inplace) continue;
       for (size_t j = 0; j < bk.params.size(); ++j) {
         auto& p = params_[bk.params[j]];
         at::Tensor view = bk.flat.narrow(0, bk.offsets[j], p.numel()).view(p.sizes());
@@ -231,13 +236,39 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     at::Tensor flat;
     int64_t pending = 0;
     bool launched = false;
+    bool inplace = false;  // reduced where the grads live (no pack)
   };
+
+  // Zero-copy bucket: when every gradient of the bucket is a contiguous view and
+  // together they tile one contiguous region of one storage exactly (the fused
+  // ConvNet op hands autograd views of ONE gradient buffer), that region is
+  // all-reduced in place with AVG -- no pack kernel, no 1/W pass, grads stay put.
+  bool tiled_region_locked(const Bucket& bk, at::Tensor& region) {
+    if (!bk.unused.empty() || bk.params.empty()) return false;
+    std::vector<std::pair<int64_t, int64_t>> spans;
+    const at::Tensor g0 = params_[bk.params[0]].grad();
+    if (!g0.defined() || !g0.is_cuda() || g0.scalar_type() != bk.flat.scalar_type()) return false;
+    for (int64_t i : bk.params) {
+      const at::Tensor g = params_[i].grad();
+      if (!g.defined() || !g.is_contiguous() || g.scalar_type() != g0.scalar_type() ||
+          !g.storage().is_alias_of(g0.storage()) || g.numel() != params_[i].numel())
+        return false;
+      spans.emplace_back(g.storage_offset(), g.numel());
+    }
+    std::sort(spans.begin(), spans.end());
+    for (size_t k = 1; k < spans.size(); ++k)
+      if (spans[k].first != spans[k - 1].first + spans[k - 1].second) return false;
+    const int64_t lo = spans.front().first, n = spans.back().first + spans.back().second - lo;
+    region = at::empty({0}, g0.options()).set_(g0.storage(), lo, {n}, {1});
+    return true;
+  }
 
   void reset_locked() {
     std::fill(ready_.begin(), ready_.end(), 0);
     for (auto& bk : buckets_) {
       bk.pending = (int64_t)bk.params.size();
       bk.launched = false;
+      bk.inplace = false;
       bk.unused.clear();
     }
     next_launch_ = 0;
@@ -258,6 +289,15 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     bind_stream(guard);
     while (next_launch_ < buckets_.size() && buckets_[next_launch_].pending == 0) {
       Bucket& bk = buckets_[next_launch_];
+      at::Tensor region;
+      if (zero_copy_ && tiled_region_locked(bk, region)) {
+        comm_->all_reduce_async(region, RedOp::AVG, (int)next_launch_);
+        if (join_each_) comm_->wait((int)next_launch_, nullptr);
+        bk.inplace = bk.launched = true;
+        ++next_launch_;
+        continue;
+      }
+      bk.inplace = false;
       std::vector<at::Tensor> srcs;
       std::vector<int64_t> offs;
       const double inv_w = 1.0 / (double)comm_->world();
@@ -306,6 +346,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   bool hooks_ready_ = false;
   std::vector<std::weak_ptr<torch::autograd::Node>> hooked_;
   bool join_each_ = false;  // join every bucket immediately (no overlap)
+  bool zero_copy_ = true;   // reduce tiled gradient regions in place (DPA_REDUCER_ZERO_COPY=0: always pack)
   std::vector<int64_t> order_;
   std::mutex mu_;
 };
