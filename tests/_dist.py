@@ -8,6 +8,7 @@ import torch.multiprocessing as mp
 
 
 def free_port() -> int:
+    """A currently free port (for subprocess CLIs that bind their own store)."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     p = s.getsockname()[1]
@@ -15,29 +16,31 @@ def free_port() -> int:
     return p
 
 
-def _entry(rank, world, port, fn, args, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    os.environ["RANK"] = str(rank)
-    os.environ["LOCAL_RANK"] = str(rank)
-    os.environ["WORLD_SIZE"] = str(world)
-    torch.set_num_threads(2)
-    try:
-        import ddp_practice_amd.distributed as dist
+def parent_store():
+    """Rendezvous store served by the test process itself on an OS-chosen port.
 
-        dist.init_process_group("gloo")
-        out = fn(rank, world, *args)
-        dist.destroy_process_group()
-        q.put((rank, "ok", out))
-    except Exception:  # pragma: no cover - reported to the parent
-        q.put((rank, "err", traceback.format_exc()))
+    The workers connect as clients (``TORCHELASTIC_USE_AGENT_STORE=True`` makes
+    ``init_process_group(env://)`` do that, as under torchrun), so no worker has
+    to bind a port that another process could take first (EADDRINUSE races of
+    the free-port-then-bind pattern)."""
+    from datetime import timedelta
+
+    st = torch.distributed.TCPStore("127.0.0.1", 0, 1, True, timedelta(seconds=300), wait_for_workers=False)
+    return st, st.port
 
 
-def run(fn, world=2, args=(), timeout=240):
+def client_env(rank: int, world: int, port: int) -> dict:
+    return {"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank), "LOCAL_RANK": str(rank),
+            "WORLD_SIZE": str(world), "TORCHELASTIC_USE_AGENT_STORE": "True"}
+
+
+def launch(target, world, args=(), timeout=240):
+    """Run ``target(rank, world, port, *args, q)`` in ``world`` spawned processes
+    against a parent-held store; each must put (rank, "ok"|"err", payload) on q."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = free_port()
-    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q)) for r in range(world)]
+    store, port = parent_store()
+    procs = [ctx.Process(target=target, args=(r, world, port, *args, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -52,4 +55,23 @@ def run(fn, world=2, args=(), timeout=240):
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
+        del store
     return [res[r] for r in range(world)]
+
+
+def _entry(rank, world, port, fn, args, q):
+    os.environ.update(client_env(rank, world, port))
+    torch.set_num_threads(2)
+    try:
+        import ddp_practice_amd.distributed as dist
+
+        dist.init_process_group("gloo")
+        out = fn(rank, world, *args)
+        dist.destroy_process_group()
+        q.put((rank, "ok", out))
+    except Exception:  # pragma: no cover - reported to the parent
+        q.put((rank, "err", traceback.format_exc()))
+
+
+def run(fn, world=2, args=(), timeout=240):
+    return launch(_entry, world, (fn, args), timeout)

@@ -39,8 +39,9 @@ def _digest(sd):
 
 def worker(rank, world, port, amp, graph, q):
     try:
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                          LOCAL_RANK=str(rank))
+        from ._dist import client_env
+
+        os.environ.update(client_env(rank, world, port))
         torch.cuda.set_device(0)
         import ddp_practice_amd.distributed as dist
         from ddp_practice_amd.data import DistributedSampler, synthetic

@@ -42,7 +42,7 @@ def worker(rank, world, port, mode, q):
         C = _ext.load()
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
-        store = torch.distributed.TCPStore("127.0.0.1", port, world, rank == 0, timedelta(seconds=60))
+        store = torch.distributed.TCPStore("127.0.0.1", port, world, False, timedelta(seconds=60))  # parent serves
         from ddp_practice_amd.parallel.comm import open_xgmi
 
         x, err = open_xgmi(rank, world, dev, store, "t", 1 << 20, 20.0)

@@ -2,10 +2,8 @@
 sharing the single GPU of the test box: values vs a CPU fp32 reference,
 bit-identical results on every rank, graph replay, bounded waits."""
 import pytest
-import torch
-import torch.multiprocessing as mp
 
-from ._dist import free_port
+from ._dist import launch
 
 pytestmark = pytest.mark.gpu
 
@@ -13,24 +11,7 @@ pytestmark = pytest.mark.gpu
 def _run(world, mode, timeout=150):
     from ._xgmi_worker import worker
 
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = free_port()
-    procs = [ctx.Process(target=worker, args=(r, world, port, mode, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = {}
-    try:
-        for _ in range(world):
-            rank, st, out = q.get(timeout=timeout)
-            assert st == "ok", f"rank {rank} failed:\n{out}"
-            res[rank] = out
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
-    return [res[r] for r in range(world)]
+    return launch(worker, world, (mode,), timeout)
 
 
 @pytest.mark.parametrize("world", [2, 4])
