@@ -193,7 +193,8 @@ def main(argv=None):
 
 def bench_resnet(args):
     """ResNet-50 training step (BASELINE.json config 5): channels-last AMP + GradScaler,
-    SyncBN + DDP over RCCL for N > 1, synthetic 3x224x224 batch, eager (MIOpen convs)."""
+    SyncBN + DDP over RCCL for N > 1, synthetic 3x224x224 batch, replayed from a hipGraph
+    (--no-graph: eager)."""
     import torch
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -244,13 +245,22 @@ def bench_resnet(args):
         scaler.step(optimizer)
         scaler.update()
 
-    for _ in range(max(1, args.warmup)):
-        step()
+    # the step is ~600 launches: capture it (after warm-up, so MIOpen's algorithm
+    # search is done) and replay, or the host's per-op overhead becomes the bound
+    from ddp_practice_amd.runtime import CapturedStep
+
+    runner = CapturedStep(step, warmup=max(1, args.warmup), steps_per_graph=1, enabled=not args.no_graph)
+    captured = runner.capture() if not args.no_graph else False
+    if not captured:
+        if not args.no_graph and rank == 0:
+            print(f"[bench] graph capture failed, eager: {runner.capture_error!r}", file=sys.stderr)
+        for _ in range(max(1, args.warmup)):
+            step()
     ddist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        runner.run()
     torch.cuda.synchronize()
     ddist.barrier()
     dt = ddist.max_over_ranks(time.perf_counter() - t0)
@@ -266,7 +276,7 @@ def bench_resnet(args):
             "config": {"model": "ResNet-50 (25,557,032 params)", "global_batch": bs * world, "seq_len": None,
                        "parallelism": f"dp{world}", "per_rank_batch": bs, "impl": args.resnet_impl,
                        "sync_bn": dist_path and not args.no_sync_bn, "optimizer": "SGD(lr=1e-4)",
-                       "comm": _comm_desc() if dist_path else "none"},
+                       "comm": _comm_desc() if dist_path else "none", "hipgraph": bool(captured)},
         }), flush=True)
     ddist.destroy_process_group()
 

@@ -4,7 +4,7 @@
 // contiguous.
 //
 // Geometry (every BN kernel): the channels are cut into column chunks of
-// CC = Lr*VEC channels (Lr <= 32 lanes x 16 B = up to 512 B of a row,
+// CC = Lr*VEC <= 64 channels (8 lanes x 16 B bf16, 16 lanes fp32: 128 B of a row,
 // blockIdx.y = chunk); a lane owns one 16-B channel vector of its chunk for the
 // whole kernel (its per-channel coefficients live in registers) and walks rows
 // with stride RP = 256/Lr, U = 4 rows in flight per lane.
@@ -36,8 +36,9 @@ namespace dpa {
 namespace bnh {
 
 constexpr int THR = 256;
-constexpr int LR_MAX = 32;   // lanes per row segment of a chunk
-constexpr int G1 = 32;       // level-1 group size of the ticket tree
+constexpr int CC_MAX = 64;   // channels per column chunk, statistics kernels (128 B of a row)
+constexpr int CC_ELT = 256;  // channels per column chunk, elementwise kernels (512 B of a row)
+constexpr int G1 = 128;      // level-1 group size of the ticket tree (one level up to 128 row blocks)
 constexpr int MAXGR = 1024;  // row blocks per chunk in the statistics kernels
 constexpr int SHIFT_OFF = 4; // stats layout: [0,C) s1, [C,2C) s2, [2C] n, shift copy at 2C+SHIFT_OFF (16-B aligned)
 constexpr int U = 4;         // rows in flight per lane
@@ -83,7 +84,12 @@ __device__ __forceinline__ void stf(float* __restrict__ p, const float* d) {
   }
 }
 
-__host__ __device__ inline int chunk_lanes(int C, int vec) { return C / vec < LR_MAX ? C / vec : LR_MAX; }
+// Column-chunk width: the largest cc' = cc / 2^k (>= vec) with C <= cc' (one chunk)
+// or C % cc' == 0.  The kernels recover it as C / gridDim.y.
+inline int chunk_width(int C, int vec, int cc) {
+  while (cc > vec && !(C <= cc || C % cc == 0)) cc /= 2;
+  return C <= cc ? C : cc;
+}
 
 // lane -> (row offset ro in [0, RP), channel c0 of its 16-B vector)
 template <int VEC>
@@ -91,8 +97,8 @@ struct Chunk {
   int Lr, CC, RP, ro, c0;
   bool active;
   __device__ explicit Chunk(int C) {
-    Lr = chunk_lanes(C, VEC);
-    CC = Lr * VEC;
+    CC = C / (int)gridDim.y;  // chunk_width() on the host
+    Lr = CC / VEC;
     RP = THR / Lr;
     ro = (int)threadIdx.x / Lr;
     active = ro < RP;
@@ -220,7 +226,7 @@ fwd_stats_kernel(const T* __restrict__ x, long long M, int C, const float* __res
                  int64_t* __restrict__ nbt) {
   constexpr int VEC = V16<T>::N;
   __shared__ float scratch[2 * THR * VEC];
-  __shared__ float red[2 * LR_MAX * VEC];
+  __shared__ float red[2 * CC_MAX];
   __shared__ int s_flag;
   const Chunk<VEC> g(C);
   float s1[VEC], s2[VEC], sh[VEC];
@@ -393,7 +399,7 @@ bwd_stats_kernel(const T* __restrict__ dy, const T* __restrict__ y, const T* __r
                  float* __restrict__ dgamma, float* __restrict__ dbeta) {
   constexpr int VEC = V16<T>::N;
   __shared__ float scratch[2 * THR * VEC];
-  __shared__ float red[2 * LR_MAX * VEC];
+  __shared__ float red[2 * CC_MAX];
   __shared__ int s_flag;
   const Chunk<VEC> g(C);
   float s1[VEC], s2[VEC];
@@ -664,13 +670,13 @@ void set_grid_targets(int64_t stats, int64_t apply, int64_t elemt) {
   g_elemt_target = (int)elemt;
 }
 template <typename T>
-static Grid2 chunk_grid(long long M, int C, int target) {
+static Grid2 chunk_grid(long long M, int C, int target, int cc = CC_MAX) {
   constexpr int VEC = V16<T>::N;
-  TORCH_CHECK(C % VEC == 0 && (C / VEC <= LR_MAX || (C / VEC) % LR_MAX == 0),
-              "bn_nhwc: channel count ", C, " (needs C % ", VEC, " == 0 and C/", VEC, " <= 32 or a multiple of 32)");
-  const int Lr = chunk_lanes(C, VEC);
+  TORCH_CHECK(C % VEC == 0, "bn_nhwc: channel count ", C, " must be a multiple of ", VEC);
+  const int CCw = chunk_width(C, VEC, cc);
+  const int Lr = CCw / VEC;
   const int RP = THR / Lr;
-  const int Gc = C / (Lr * VEC);
+  const int Gc = C / CCw;
   const long long by_rows = std::max<long long>(1, (M + (long long)RP * U - 1) / ((long long)RP * U));
   const long long want = std::max<long long>(1, (target + Gc - 1) / Gc);
   return {(int)std::min<long long>(by_rows, want), Gc};
@@ -691,7 +697,7 @@ static void check_workspace(const Grid2& g, int C, const at::Tensor& part, const
   TORCH_CHECK(tickets.numel() >= g.Gc * (NG + 1) && tickets.scalar_type() == at::kInt, "bn_nhwc: ticket workspace");
 }
 
-// part: >= 2C*(MAXGR + MAXGR/16) floats; tickets: >= MAXTICKETS zero-initialised int32 (re-armed by the kernels)
+// part: >= 2C*(MAXGR + MAXGR/G1) floats; tickets: >= MAXTICKETS zero-initialised int32 (re-armed by the kernels)
 void fwd_stats(at::Tensor x, int64_t C, at::Tensor shift, at::Tensor part, at::Tensor ticket, at::Tensor stats,
                c10::optional<at::Tensor> nbt) {
   const long long M = x.numel() / C;
@@ -718,7 +724,7 @@ void apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, int64_t C,
   if (res.has_value()) check_rows(*res, M, (int)C);
   dispatch(x, [&](auto tag) {
     typedef decltype(tag) T;
-    const Grid2 g = chunk_grid<T>(M, (int)C, g_apply_target);
+    const Grid2 g = chunk_grid<T>(M, (int)C, g_apply_target, CC_ELT);
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(g.Gr, g.Gc), dim3(THR), 0, cur_stream(), dp<T>(x),
                          res.has_value() ? dp<T>(*res) : nullptr, dp<T>(y), M, (int)C, stats.data_ptr<float>(),
@@ -775,7 +781,7 @@ void bwd_elemt(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, int64_t
   if (dres.has_value()) check_rows(*dres, M, (int)C);
   dispatch(x, [&](auto tag) {
     typedef decltype(tag) T;
-    const Grid2 g = chunk_grid<T>(M, (int)C, g_elemt_target);
+    const Grid2 g = chunk_grid<T>(M, (int)C, g_elemt_target, CC_ELT);
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(g.Gr, g.Gc), dim3(THR), 0, cur_stream(), dp<T>(dy),
                          act == ACT_Y ? dp<T>(*y) : nullptr, dp<T>(x), M, (int)C, save.data_ptr<float>(),

@@ -50,7 +50,7 @@ for M, C in shapes:
     K.fwd_stats(x, C, shift, part, tick, stats, nbt)
     K.apply(x, None, yb, C, stats, gamma, beta, rm, rv, nbt, 0.1, 1e-5, True, True, save)
     best = {}
-    for st, el in itertools.product((0, 128, 256), (512, 1024, 2048)):
+    for st, el in itertools.product((64, 128, 256, 512), (256, 512, 1024, 2048)):
         K.set_grid_targets(st, el, el)
         r = {
             "fstats": (tm(lambda: K.fwd_stats(x, C, shift, part, tick, stats, None)), 1),

@@ -16,7 +16,7 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("C,res,relu", [(64, False, True), (256, True, True), (2048, False, False),
-                                        (512, True, False)])
+                                        (512, True, False), (24, True, True), (320, False, True)])
 def test_bn_act_fwd_bwd(C, res, relu, dtype):
     from ddp_practice_amd.ops.bn_nhwc import bn_act
 
