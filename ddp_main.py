@@ -64,9 +64,11 @@ def init_ddp(local_rank):
 
 
 def main(local_rank, args):
-    from ddp_practice_amd.cli import run
+    from ddp_practice_amd.cli import phase, run
 
+    phase("child start")
     init_ddp(local_rank)
+    phase("init_process_group")
     run(args, distributed=True, local_rank=local_rank, generator_seed=3407 + local_rank)
 
 

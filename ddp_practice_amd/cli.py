@@ -98,8 +98,18 @@ class _Metrics:
         self.t0 = time.perf_counter()
 
 
+_T0 = time.perf_counter()
+
+
+def phase(name: str) -> None:
+    """``DPA_PHASES=1``: print the time since this module was imported at each run phase (stderr)."""
+    if os.environ.get("DPA_PHASES") == "1":
+        print(f"[phase pid={os.getpid()}] {name} +{time.perf_counter() - _T0:.3f}s", file=sys.stderr, flush=True)
+
+
 def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None = None) -> None:
     """Build model/data/optimizer, train ``args.epochs`` epochs, test, save (rank 0)."""
+    phase("run")
     import torch
 
     import ddp_practice_amd.distributed as dist
@@ -111,6 +121,7 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
     from ddp_practice_amd.optim import SGD
     from ddp_practice_amd.utils import FaultInjector, Watchdog, set_tracing, trace_range
 
+    phase("imports")
     if args.profile:
         set_tracing(True)
     if args.seed is not None:
@@ -135,6 +146,7 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
                                         bucket_cap_mb=args.bucket_cap_mb)
     criterion = CrossEntropyLoss().to(dev)
     optimizer = SGD(model.parameters(), 1e-4)
+    phase("model")
 
     act_dtype = amp if (amp is not None and gpu) else torch.float32
     train_dataset = MNIST(root=args.data_root, train=True, force_synthetic=args.synthetic, n=args.train_samples)
@@ -154,6 +166,7 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
         test_dloader = DeviceLoader(test_dataset, batch_size=args.batch_size, shuffle=True, device=dev,
                                     dtype=act_dtype, num_workers=2, pin_memory=True)
 
+    phase("data")
     timeout = args.watchdog_timeout
     if timeout is None and "DPA_WATCHDOG_TIMEOUT" in os.environ:
         timeout = float(os.environ["DPA_WATCHDOG_TIMEOUT"])
@@ -171,6 +184,7 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
                 train_dloader.sampler.set_epoch(epoch)
             loop.run_epoch()
             metrics.epoch(epoch, len(train_dataset), len(train_dloader), scaler)
+            phase(f"epoch {epoch}")
         if loop.graph_error is not None and rank == 0:
             print(f"[ddp_practice_amd] hipGraph capture failed, ran eagerly: {loop.graph_error!r}", file=sys.stderr)
         if rank == 0:
@@ -179,6 +193,7 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
             correct, size = evaluate(model, test_dloader, comm=comm, dst=0)
         if watchdog is not None:
             watchdog.tick()
+        phase("evaluate")
         if rank == 0:
             print(f"Accuracy is {correct / size:.2%}", flush=True)
             with trace_range("checkpoint"):
@@ -189,5 +204,7 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
     finally:
         if watchdog is not None:
             watchdog.stop()
+    phase("saved")
     if distributed:
         dist.destroy_process_group()
+    phase("done")
