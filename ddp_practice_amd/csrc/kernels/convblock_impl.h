@@ -478,6 +478,20 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
   typedef MM<T> mm;
 
   __shared__ __attribute__((aligned(16))) T img[HP * WPD * CIN];
+  // img is [padded pixel][CIN] with the 8-channel (16-B) groups of each pixel
+  // XOR-swizzled by the pixel index: an A-fragment read takes 16 consecutive
+  // pixels x one 16-B group; with a 32/64-B pixel pitch those 16 addresses would
+  // share 8/4 bank groups (2/4-way conflicts), swizzled they hit 16 distinct ones
+  // (conv2 dgrad: SQ_LDS_BANK_CONFLICT -54 %)
+  constexpr int NCH = CIN >= 8 ? CIN / 8 : 1;              // 16-B groups per pixel
+  constexpr int PPB = NCH <= 16 ? 16 / NCH : 1;            // pixels per 256-B bank row
+  auto imo = [](int px, int c) -> int {
+    if constexpr (NCH <= 1) {
+      return px * CIN + c;
+    } else {
+      return px * CIN + ((((c >> 3) ^ ((px / PPB) & (NCH - 1)))) << 3) + (c & 7);
+    }
+  };
   __shared__ __attribute__((aligned(16))) T wl[COUT * KPW];
   __shared__ float lstat[(NTHR / 64) * 2 * COUT];
 
@@ -550,8 +564,8 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
   }
   if constexpr (PRO == 0) {
     stage_chw<T, CIN, H, W>(xb, [&](int ci, int h, int ww, T a, T bb) {
-      img[((h + 2) * WPD + (ww + 2)) * CIN + ci] = a;
-      img[((h + 2) * WPD + (ww + 3)) * CIN + ci] = bb;
+      img[imo((h + 2) * WPD + (ww + 2), ci)] = a;
+      img[imo((h + 2) * WPD + (ww + 3), ci)] = bb;
     });
   } else if constexpr (PRO == 1) {
     __shared__ float sc_s[CIN], beta_s[CIN], mean_s[CIN], istd_s[CIN];
@@ -583,7 +597,7 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
         int bi;
         bn_relu_max4x<T>(top[i], bot[i], sc_s[ci], beta_s[ci], mean_s[ci], istd_s[ci], best, bi, xh);
         const T pv = Cvt<T>::from_f(best);
-        img[((ho + 2) * WPD + (wo + 2)) * CIN + ci] = pv;
+        img[imo((ho + 2) * WPD + (wo + 2), ci)] = pv;
         if (wr) {
           pin.p_out[(size_t)b * NPO + e] = pv;
           pin.idx_out[(size_t)b * NPO + e] = (uint8_t)(bi | (best > 0.f ? IDX_RELU : 0));
@@ -599,10 +613,10 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
     bn_bwd_coef<CIN, T>(bin, coef, part, sums, blockIdx.x == 0);
     DPA_STAMP(3);
     st.emit(coef, [&](int c, int h, int ww, T v00, T v01, T v10, T v11) {
-      img[((h + 2) * WPD + (ww + 2)) * CIN + c] = v00;
-      img[((h + 2) * WPD + (ww + 3)) * CIN + c] = v01;
-      img[((h + 3) * WPD + (ww + 2)) * CIN + c] = v10;
-      img[((h + 3) * WPD + (ww + 3)) * CIN + c] = v11;
+      img[imo((h + 2) * WPD + (ww + 2), c)] = v00;
+      img[imo((h + 2) * WPD + (ww + 3), c)] = v01;
+      img[imo((h + 3) * WPD + (ww + 2), c)] = v10;
+      img[imo((h + 3) * WPD + (ww + 3), c)] = v11;
     });
   }
   if constexpr (WPK == 1) {
@@ -645,7 +659,7 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
         int tap = kb / CIN;
         const int ci0 = kb % CIN;
         tap = tap < 25 ? tap : 24;  // K padding: weights are zero there
-        a = mm::ld(&img[((oh + tap / 5) * WPD + ow + tap % 5) * CIN + ci0]);
+        a = mm::ld(&img[imo((oh + tap / 5) * WPD + ow + tap % 5, ci0)]);
       }
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
