@@ -336,29 +336,36 @@ __device__ __forceinline__ void bn_bwd_coef(const BwdIn<T>& bi, float* coef, flo
 // loads can be issued before the coefficient reduction (their latencies
 // overlap): load(bi, b) ... bn_bwd_coef(...) ... emit(coef, sink) with
 // sink(c, h, w, v00, v01, v10, v11), (h, w) = the window's top-left pixel.
-template <typename T, int C, int H, int W, int NT_>
+// ROWS (even): the conv-output rows [r0, r0 + ROWS) of one image (pooled rows
+// [r0/2, r0/2 + ROWS/2), clipped at the image); the sink gets chunk-relative rows.
+template <typename T, int C, int H, int W, int NT_, int ROWS = H>
 struct BnBwdStage {
   typedef typename Pair2<T>::type P;
-  static constexpr int HO = H / 2, WO = W / 2, PP = HO * WO, NWIN = C * PP;
+  static_assert(ROWS % 2 == 0 && ROWS <= H, "BN-backward staging works on whole 2x2 pooling windows");
+  static constexpr int HO = H / 2, WO = W / 2, PP = HO * WO;
+  static constexpr int CHO = ROWS / 2, CPP = CHO * WO, NWIN = C * CPP;  // windows of one chunk
   static constexpr int IT = (NWIN + NT_ - 1) / NT_;
   P top[IT], bot[IT];
   T g[IT];
   uint8_t ix[IT];
+  int ho0 = 0;
 
-  __device__ __forceinline__ void load(const BwdIn<T>& bi, int b) {
+  __device__ __forceinline__ void load(const BwdIn<T>& bi, int b, int r0 = 0) {
+    ho0 = r0 / 2;
     const T* yb = bi.y + (size_t)b * C * H * W;
-    const T* dpb = bi.dp + (size_t)b * NWIN;
-    const uint8_t* ib = bi.idx + (size_t)b * NWIN;
+    const T* dpb = bi.dp + (size_t)b * C * PP;
+    const uint8_t* ib = bi.idx + (size_t)b * C * PP;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int e = threadIdx.x + i * NT_;
-      if (e < NWIN) {
-        const int c = e / PP, pix = e % PP, ho = pix / WO, wo = pix % WO;
+      const int c = e / CPP, pix = e % CPP, ho = ho0 + pix / WO, wo = pix % WO;
+      if (e < NWIN && ho < HO) {
         const P* src = reinterpret_cast<const P*>(yb + ((size_t)c * H + 2 * ho) * W + 2 * wo);
         top[i] = src[0];
         bot[i] = src[W / 2];
-        g[i] = dpb[e];
-        ix[i] = ib[e];
+        const int ew = c * PP + ho * WO + wo;
+        g[i] = dpb[ew];
+        ix[i] = ib[ew];
       }
     }
   }
@@ -368,8 +375,9 @@ struct BnBwdStage {
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int e = threadIdx.x + i * NT_;
-      if (e < NWIN) {
-        const int c = e / PP, pix = e % PP, ho = pix / WO, wo = pix % WO;
+      const int c = e / CPP, pix = e % CPP, hl = pix / WO, wo = pix % WO;
+      if (e < NWIN && ho0 + hl < HO) {
+        const int ho = hl;  // chunk-relative pooled row
         const float k1 = coef[c], k2 = coef[C + c], gi = coef[2 * C + c], mean = coef[3 * C + c],
                     istd = coef[4 * C + c];
         T v[4];
@@ -949,7 +957,7 @@ template <typename T, int CIN, int COUT, int H, int W, int ROWS, int PRO = 0>
 __global__ void __launch_bounds__(NTHR)
 conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* __restrict__ wslab,
                      int nsplit, BwdIn<T> bin = BwdIn<T>{}) {
-  static_assert(PRO == 0 || (PRO == 2 && ROWS == H), "PRO 2 needs whole images per workgroup");
+  static_assert(PRO == 0 || (PRO == 2 && ROWS % 2 == 0), "PRO 2 works on whole 2x2 pooling windows");
   constexpr int WP = ceil_to(W, 8);
   static_assert((ROWS * WP) % 32 == 0, "ROWS*WP must be a multiple of 32");
   constexpr int KSTEPS = ROWS * WP / 32;
@@ -1012,13 +1020,22 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
   if constexpr (PRO == 2) {
     __shared__ float coef[5 * COUT], sums[2 * COUT];
     __shared__ float part[NTHR];
-    BnBwdStage<T, COUT, H, W, NTHR> st;
-    st.load(bin, b);
-    __syncthreads();  // xs zero-fill before the scatter
-    stage_chw<T, CIN, H, W>(xb, [&](int ci, int h, int ww, T a, T bb) {
-      scatter5(ci, h + 2, ww, a);
-      scatter5(ci, h + 2, ww + 1, bb);
-    });
+    BnBwdStage<T, COUT, H, W, NTHR, ROWS> st;
+    st.load(bin, b, r0);
+    if constexpr (DIRECT) {
+      __syncthreads();  // xs zero-fill before the scatter
+      stage_chw<T, CIN, H, W>(xb, [&](int ci, int h, int ww, T a, T bb) {
+        scatter5(ci, h + 2, ww, a);
+        scatter5(ci, h + 2, ww + 1, bb);
+      });
+    } else {  // input rows r0-2 .. r0+ROWS+1 -> xpad (kw copies after the barrier below)
+      for (int e = tid; e < CIN * XR * W; e += NTHR) {
+        const int ci = e / (XR * W), rem = e % (XR * W);
+        const int rr = rem / W, cc = rem % W;
+        const int ih = r0 + rr - 2;
+        if (ih >= 0 && ih < H) xpad[(ci * XR + rr) * WX + cc + 2] = xb[(ci * H + ih) * W + cc];
+      }
+    }
     bn_bwd_coef<COUT, T>(bin, coef, part, sums, blockIdx.x == 0);
     DPA_STAMP(3);
     st.emit(coef, [&](int co, int h, int ww, T v00, T v01, T v10, T v11) {
@@ -1070,12 +1087,26 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
   DPA_STAMP(5);
   const int lane = tid & 63, wv = tid >> 6;
   const int r = lane & 15, q = lane >> 4;
-  // bias grad partial: per output channel sum of dy over this chunk
-  for (int co = wv; co < COUT; co += NW) {
+  // bias grad partial: per output channel sum of dy over this chunk.  TPC lanes
+  // per channel, each summing 16-B groups (fixed order), then a TPC-lane
+  // butterfly: one pass for all channels (a wave-wide reduction per channel
+  // cost ~2 us here)
+  {
+    constexpr int TPC = NTHR / COUT;
+    static_assert(NTHR % COUT == 0 && TPC <= 64 && (TPC & (TPC - 1)) == 0, "bias-sum lane groups");
+    constexpr int E = ROWS * WP;
+    static_assert(E % 8 == 0, "dy rows are whole 16-B groups");
+    const int co = tid / TPC, sub = tid % TPC;
     float a = 0.f;
-    for (int i = lane; i < ROWS * WP; i += 64) a += Cvt<T>::to_f(dyl[co * ROWS * WP + i]);
-    a = wave_sum(a);
-    if (lane == 0) row_out[COUT * N + co] = a;
+    for (int i = sub * 8; i < E; i += TPC * 8) {
+      const typename mm::frag v = mm::ld(&dyl[co * ROWS * WP + i]);
+      const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a += Cvt<T>::to_f(e[j]);
+    }
+#pragma unroll
+    for (int o = TPC / 2; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    if (sub == 0) row_out[COUT * N + co] = a;
   }
   DPA_STAMP(6);
   const int ks = KSPLIT > 1 ? wv % KSPLIT : 0;

@@ -407,6 +407,15 @@ void conv2_dgrad(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx
 
 // [pool/ReLU/BN backward of the block whose conv is (CIN->COUT, HxW)] -> weight-grad partials.
 // layer 2: x = p1 [B,16,14,14], (y, dp, idx) = layer-2 tensors; layer 1: x = images, layer-1 tensors.
+// Weight-gradient row chunks (BN backward applied on the fly per chunk): more,
+// shorter workgroups than one image each (B = 32 -> 32 workgroups for 256 CUs).
+constexpr int WG1_ROWS = 4;  // layer 1 (28 rows): 7 chunks per image
+constexpr int WG2_ROWS = 4;  // layer 2 (14 rows): 4 chunks per image (last one 2 rows)
+int64_t wgrad_bn_rows(int64_t layer, int64_t B) {
+  TORCH_CHECK(layer == 1 || layer == 2);
+  return B * (layer == 1 ? (28 + WG1_ROWS - 1) / WG1_ROWS : (14 + WG2_ROWS - 1) / WG2_ROWS);
+}
+
 void conv_wgrad_bn(at::Tensor x, at::Tensor y, at::Tensor dp, at::Tensor idx, at::Tensor fstats, at::Tensor gsum,
                    c10::optional<at::Tensor> lsum, at::Tensor gamma, double eps, c10::optional<at::Tensor> dgamma,
                    c10::optional<at::Tensor> dbeta, at::Tensor wslab) {
@@ -419,13 +428,15 @@ void conv_wgrad_bn(at::Tensor x, at::Tensor y, at::Tensor dp, at::Tensor idx, at
     typedef decltype(tag) T;
     BwdIn<T> bi = bwd_in<T>(dp, idx, y, fstats, gsum, lsum, gamma, eps, cout, dgamma, dbeta);
     if (cin == 16 && cout == 32 && H == 14) {
-      TORCH_CHECK(wslab.numel() == (int64_t)B * (32 * 400 + 32), "wgrad slab size");
-      hipLaunchKernelGGL((cb::conv5x5_wgrad_kernel<T, 16, 32, 14, 14, 14, 2>), dim3(B), dim3(cb::NTHR), 0,
-                         cur_stream(), dptr<T>(x), nullptr, wslab.data_ptr<float>(), 1, bi);
+      constexpr int ns = (14 + WG2_ROWS - 1) / WG2_ROWS;
+      TORCH_CHECK(wslab.numel() == (int64_t)B * ns * (32 * 400 + 32), "wgrad slab size");
+      hipLaunchKernelGGL((cb::conv5x5_wgrad_kernel<T, 16, 32, 14, 14, WG2_ROWS, 2>), dim3(B * ns), dim3(cb::NTHR),
+                         0, cur_stream(), dptr<T>(x), nullptr, wslab.data_ptr<float>(), ns, bi);
     } else if (cin == 1 && cout == 16 && H == 28) {
-      TORCH_CHECK(wslab.numel() == (int64_t)B * (16 * 25 + 16), "wgrad slab size");
-      hipLaunchKernelGGL((cb::conv5x5_wgrad_kernel<T, 1, 16, 28, 28, 28, 2>), dim3(B), dim3(cb::NTHR), 0,
-                         cur_stream(), dptr<T>(x), nullptr, wslab.data_ptr<float>(), 1, bi);
+      constexpr int ns = (28 + WG1_ROWS - 1) / WG1_ROWS;
+      TORCH_CHECK(wslab.numel() == (int64_t)B * ns * (16 * 25 + 16), "wgrad slab size");
+      hipLaunchKernelGGL((cb::conv5x5_wgrad_kernel<T, 1, 16, 28, 28, WG1_ROWS, 2>), dim3(B * ns), dim3(cb::NTHR),
+                         0, cur_stream(), dptr<T>(x), nullptr, wslab.data_ptr<float>(), ns, bi);
     } else {
       TORCH_CHECK(false, "fused wgrad: shape not instantiated");
     }
@@ -462,6 +473,7 @@ void register_convnet_fused(pybind11::module& m) {
   s.attr("W2D_LEN") = cb::W2D_LEN;
   s.def("conv2_dgrad", &cnf::conv2_dgrad);
   s.def("conv_wgrad_bn", &cnf::conv_wgrad_bn);
+  s.def("wgrad_bn_rows", &cnf::wgrad_bn_rows);
 }
 
 }  // namespace dpa

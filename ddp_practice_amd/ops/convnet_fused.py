@@ -129,11 +129,11 @@ class ConvNetFn(torch.autograd.Function):
         bslab1 = torch.empty(cn.dgrad2_rows(B) * 32, **f32)
         cn.conv2_dgrad(wpk_d, y2, dp2, idx2, fstats2, gsum2, g2, e2, dp1, idx1, xh1, bslab1)
         # 3. BN2 bwd -> conv2 wgrad partials (independent of 2)
-        wslab2 = torch.empty(B * (n_w2 + 32), **f32)
+        wslab2 = torch.empty(cn.wgrad_bn_rows(2, B) * (n_w2 + 32), **f32)
         cn.conv_wgrad_bn(p1, y2, dp2, idx2, fstats2, gsum2, None, g2, e2, None, None, wslab2)
         # 4. BN1 bwd -> conv1 wgrad partials (+ dgamma1 / dbeta1 from the local sums)
         gslab1 = comm.all_reduce(bslab1) if sync else bslab1
-        wslab1 = torch.empty(B * (n_w1 + 16), **f32)
+        wslab1 = torch.empty(cn.wgrad_bn_rows(1, B) * (n_w1 + 16), **f32)
         cn.conv_wgrad_bn(x, y1, dp1, idx1, fstats1, gslab1, bslab1 if sync else None, g1, e1, dg1, dbe1, wslab1)
         # 5. weight-grad partial sums -> [dW1 | db1], [dW2 | db2]
         cb.slab_reduce(wslab1, n_w1 + 16, out.narrow(0, 0, n_w1 + 16), wslab2, n_w2 + 32,
