@@ -595,7 +595,10 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
     }
     bn_finalize<CIN>(pin.bn, sc_s, beta_s, mean_s, istd_s, part, blockIdx.x == 0);
     DPA_STAMP(3);
-    const bool wr = pin.p_out != nullptr && sp == 0;
+    // the pooled map / index / xhat outputs (for the backward) are written by all
+    // nsplit workgroups of the image, each its share (was: split 0 alone)
+    const bool wr = pin.p_out != nullptr;
+    const int e_lo = NPO * sp / nsplit, e_hi = NPO * (sp + 1) / nsplit;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int e = tid + i * NTHR;
@@ -606,7 +609,7 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
         bn_relu_max4x<T>(top[i], bot[i], sc_s[ci], beta_s[ci], mean_s[ci], istd_s[ci], best, bi, xh);
         const T pv = Cvt<T>::from_f(best);
         img[imo((ho + 2) * WPD + (wo + 2), ci)] = pv;
-        if (wr) {
+        if (wr && e >= e_lo && e < e_hi) {
           pin.p_out[(size_t)b * NPO + e] = pv;
           pin.idx_out[(size_t)b * NPO + e] = (uint8_t)(bi | (best > 0.f ? IDX_RELU : 0));
           pin.xh_out[(size_t)b * NPO + e] = Cvt<T>::from_f(xh);

@@ -157,7 +157,6 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
   __shared__ float* sp0[MAXT];
   __shared__ float* sp1[MAXT];
   __shared__ float* sp2[MAXT];
-  __shared__ unsigned long long s_gen;
   __shared__ int s_bad;
   const int tid = threadIdx.x;
   const int n = L.n;
@@ -168,10 +167,12 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
     sp1[tid] = L.p1[tid];
     sp2[tid] = L.p2[tid];
   }
-  if (tid == 0) s_gen = __hip_atomic_fetch_add(&sync[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   const int total = soff[n];
-  const unsigned long long gen = s_gen;
+  // the barrier generation is only used by lane 0: issued after the table
+  // barrier, its load stays in flight (no LDS round trip) with the gradients'
+  unsigned long long gen = 0;
+  if (tid == 0) gen = __hip_atomic_fetch_add(&sync[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   auto load4 = [](const float* p, int rem) {
     if (rem >= 4) return *reinterpret_cast<const f32x4*>(p);
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
