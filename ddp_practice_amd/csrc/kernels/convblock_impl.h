@@ -562,12 +562,29 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
   __shared__ uint8_t eidx[EPI ? COUT * EPIX : 1];
   __shared__ T exh[EPI ? COUT * EPIX : 1];
   if constexpr (EPI == 1) {
+    // every load of the range is issued before the first LDS store (a load ->
+    // store loop waits one memory round trip per iteration)
     const int p0 = mt0 * 16, np = min(mt1 * 16, HW) - p0;
-    for (int e = tid; e < COUT * np; e += NTHR) {
-      const int co = e / np, pp = e % np;
+    constexpr int EIT = (COUT * EPIX + NTHR - 1) / NTHR;
+    uint8_t ei[EIT];
+    T ex[EIT];
+#pragma unroll
+    for (int i = 0; i < EIT; ++i) {
+      const int e = tid + i * NTHR;
+      const int ec = e < COUT * np ? e : 0;  // clamped: the loads stay unconditional
+      const int co = ec / np, pp = ec % np;
       const size_t o = ((size_t)b * COUT + co) * HW + p0 + pp;
-      eidx[co * EPIX + pp] = epi.idx[o];
-      exh[co * EPIX + pp] = epi.xh[o];
+      ei[i] = epi.idx[o];
+      ex[i] = epi.xh[o];
+    }
+#pragma unroll
+    for (int i = 0; i < EIT; ++i) {
+      const int e = tid + i * NTHR;
+      if (e < COUT * np) {
+        const int co = e / np, pp = e % np;
+        eidx[co * EPIX + pp] = ei[i];
+        exh[co * EPIX + pp] = ex[i];
+      }
     }
   }
   if constexpr (PRO == 0) {
@@ -987,6 +1004,31 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
   DPA_STAMP(0);
   const int r0 = sp * ROWS;
   const T* xb = x + (size_t)b * CIN * H * W;
+  // input rows r0-2 .. r0+ROWS+1 -> xpad interior; all loads issued before the
+  // first LDS store (one memory round trip, not one per loop iteration)
+  auto stage_xpad = [&]() {
+    if constexpr (!DIRECT) {
+      constexpr int XN = CIN * XR * W, XIT = (XN + NTHR - 1) / NTHR;
+      T xv[XIT];
+#pragma unroll
+      for (int i = 0; i < XIT; ++i) {
+        const int e = threadIdx.x + i * NTHR;
+        const int ci = e / (XR * W), rem = e % (XR * W);
+        const int rr = rem / W, cc = rem % W;
+        const int ih = r0 + rr - 2;
+        const bool ok = e < XN && ih >= 0 && ih < H;
+        xv[i] = xb[ok ? (ci * H + ih) * W + cc : 0];
+      }
+#pragma unroll
+      for (int i = 0; i < XIT; ++i) {
+        const int e = threadIdx.x + i * NTHR;
+        const int ci = e / (XR * W), rem = e % (XR * W);
+        const int rr = rem / W, cc = rem % W;
+        const int ih = r0 + rr - 2;
+        if (e < XN && ih >= 0 && ih < H) xpad[(ci * XR + rr) * WX + cc + 2] = xv[i];
+      }
+    }
+  };
   const T* dyb = dy + (size_t)b * COUT * H * W;
   const T zero = Cvt<T>::from_f(0.f);
 
@@ -1032,12 +1074,7 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
         scatter5(ci, h + 2, ww + 1, bb);
       });
     } else {  // input rows r0-2 .. r0+ROWS+1 -> xpad (kw copies after the barrier below)
-      for (int e = tid; e < CIN * XR * W; e += NTHR) {
-        const int ci = e / (XR * W), rem = e % (XR * W);
-        const int rr = rem / W, cc = rem % W;
-        const int ih = r0 + rr - 2;
-        if (ih >= 0 && ih < H) xpad[(ci * XR + rr) * WX + cc + 2] = xb[(ci * H + ih) * W + cc];
-      }
+      stage_xpad();
     }
     bn_bwd_coef<COUT, T>(bin, coef, part, sums, blockIdx.x == 0);
     DPA_STAMP(3);
@@ -1063,12 +1100,7 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
       const int rr = rem / W, cc = rem % W;
       if (r0 + rr < H) dyl[(co * ROWS + rr) * WP + cc] = dyb[(co * H + r0 + rr) * W + cc];
     }
-    for (int e = tid; e < CIN * XR * W; e += NTHR) {
-      const int ci = e / (XR * W), rem = e % (XR * W);
-      const int rr = rem / W, cc = rem % W;
-      const int ih = r0 + rr - 2;
-      if (ih >= 0 && ih < H) xpad[(ci * XR + rr) * WX + cc + 2] = xb[(ci * H + ih) * W + cc];
-    }
+    stage_xpad();
   }
   DPA_STAMP(4);
   __syncthreads();
