@@ -526,13 +526,21 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
   constexpr int WN16 = WPK == 1 ? COUT * KPW * (int)sizeof(T) / 16 : 1;
   constexpr int WIT = (WN16 + NTHR - 1) / NTHR;
   uint4 wreg[WPK == 1 ? WIT : 1];
-  if constexpr (WPK == 1) {
-    static_assert((COUT * KPW * sizeof(T)) % 16 == 0, "packed weight tile must be whole 16-B chunks");
-    static_assert(COUT * KPW == (MODE == 2 ? W2D_LEN : W2F_LEN), "pre-packed weights exist for layer 2 only");
-    const uint4* src = reinterpret_cast<const uint4*>(wpk);
+  // with a BN prologue (PRO 1/2) the tile's loads are issued after the
+  // prologue's statistics barrier: a barrier waits for every outstanding load,
+  // and the tile is needed only at the MFMA loop
+  auto load_wpk = [&]() {
+    if constexpr (WPK == 1) {
+      static_assert((COUT * KPW * sizeof(T)) % 16 == 0, "packed weight tile must be whole 16-B chunks");
+      static_assert(COUT * KPW == (MODE == 2 ? W2D_LEN : W2F_LEN), "pre-packed weights exist for layer 2 only");
+      const uint4* src = reinterpret_cast<const uint4*>(wpk);
 #pragma unroll
-    for (int i = 0; i < WIT; ++i)
-      if (tid + i * NTHR < WN16) wreg[i] = src[tid + i * NTHR];
+      for (int i = 0; i < WIT; ++i)
+        if (tid + i * NTHR < WN16) wreg[i] = src[tid + i * NTHR];
+    }
+  };
+  if constexpr (WPK == 1) {
+    if constexpr (PRO == 0) load_wpk();
   } else {
     if constexpr (KP > K) {
       for (int e = tid; e < COUT * (KP - K); e += NTHR) wl[(e / (KP - K)) * KPW + K + e % (KP - K)] = zero;
@@ -551,42 +559,63 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
   }
   if constexpr (WPK == 2) pack_w2<T>(pk);
   DPA_STAMP(1);
-  // --- stage the zero-padded image in HWC order
-  for (int e = tid; e < HP * WPD * CIN; e += NTHR) {
-    const int hp = e / (WPD * CIN), rem = e % (WPD * CIN);
-    const int wp = rem / CIN;
-    if (hp < 2 || hp >= H + 2 || wp < 2 || wp >= W + 2) img[e] = zero;
+  // --- stage the zero-padded image in HWC order: zero the halo pixels
+  //     (whole 16-B groups when a pixel is, else element by element)
+  if constexpr ((CIN * sizeof(T)) % 16 == 0) {
+    constexpr int G = CIN * (int)sizeof(T) / 16;  // 16-B groups per pixel
+    uint4* img4 = reinterpret_cast<uint4*>(img);
+    for (int e = tid; e < HP * WPD * G; e += NTHR) {
+      const int px = e / G, hp = px / WPD, wp = px % WPD;
+      if (hp < 2 || hp >= H + 2 || wp < 2 || wp >= W + 2) img4[e] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  } else {
+    for (int e = tid; e < HP * WPD * CIN; e += NTHR) {
+      const int hp = e / (WPD * CIN), rem = e % (WPD * CIN);
+      const int wp = rem / CIN;
+      if (hp < 2 || hp >= H + 2 || wp < 2 || wp >= W + 2) img[e] = zero;
+    }
   }
   // EPI: this workgroup's output range of the pooled index / xhat of the block below
   constexpr int EPIX = EPI ? MT * 16 : 1;
   __shared__ uint8_t eidx[EPI ? COUT * EPIX : 1];
   __shared__ T exh[EPI ? COUT * EPIX : 1];
-  if constexpr (EPI == 1) {
-    // every load of the range is issued before the first LDS store (a load ->
-    // store loop waits one memory round trip per iteration)
-    const int p0 = mt0 * 16, np = min(mt1 * 16, HW) - p0;
-    constexpr int EIT = (COUT * EPIX + NTHR - 1) / NTHR;
-    uint8_t ei[EIT];
-    T ex[EIT];
+  // (the loads: issued after the BN prologue's barrier; the LDS stores: after
+  //  the emit, so the round trip overlaps it)
+  const int ep0 = mt0 * 16, enp = min(mt1 * 16, HW) - ep0;
+  constexpr int EIT = EPI ? (COUT * EPIX + NTHR - 1) / NTHR : 1;
+  uint8_t ei[EIT];
+  T ex[EIT];
+  auto load_epi = [&]() {
+    if constexpr (EPI == 1) {
 #pragma unroll
-    for (int i = 0; i < EIT; ++i) {
-      const int e = tid + i * NTHR;
-      const int ec = e < COUT * np ? e : 0;  // clamped: the loads stay unconditional
-      const int co = ec / np, pp = ec % np;
-      const size_t o = ((size_t)b * COUT + co) * HW + p0 + pp;
-      ei[i] = epi.idx[o];
-      ex[i] = epi.xh[o];
-    }
-#pragma unroll
-    for (int i = 0; i < EIT; ++i) {
-      const int e = tid + i * NTHR;
-      if (e < COUT * np) {
-        const int co = e / np, pp = e % np;
-        eidx[co * EPIX + pp] = ei[i];
-        exh[co * EPIX + pp] = ex[i];
+      for (int i = 0; i < EIT; ++i) {
+        const int e = tid + i * NTHR;
+        const int ec = e < COUT * enp ? e : 0;  // clamped: the loads stay unconditional
+        const int co = ec / enp, pp = ec % enp;
+        const size_t o = ((size_t)b * COUT + co) * HW + ep0 + pp;
+        ei[i] = epi.idx[o];
+        ex[i] = epi.xh[o];
       }
     }
+  };
+  auto store_epi = [&]() {
+    if constexpr (EPI == 1) {
+#pragma unroll
+      for (int i = 0; i < EIT; ++i) {
+        const int e = tid + i * NTHR;
+        if (e < COUT * enp) {
+          const int co = e / enp, pp = e % enp;
+          eidx[co * EPIX + pp] = ei[i];
+          exh[co * EPIX + pp] = ex[i];
+        }
+      }
+    }
+  };
+  if constexpr (PRO != 2) {
+    load_epi();
+    store_epi();
   }
+  DPA_STAMP(2);
   if constexpr (PRO == 0) {
     stage_chw<T, CIN, H, W>(xb, [&](int ci, int h, int ww, T a, T bb) {
       img[imo((h + 2) * WPD + (ww + 2), ci)] = a;
@@ -611,6 +640,7 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
       }
     }
     bn_finalize<CIN>(pin.bn, sc_s, beta_s, mean_s, istd_s, part, blockIdx.x == 0);
+    load_wpk();
     DPA_STAMP(3);
     // the pooled map / index / xhat outputs (for the backward) are written by all
     // nsplit workgroups of the image, each its share (was: split 0 alone)
@@ -638,7 +668,10 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
     __shared__ float part[NTHR];
     BnBwdStage<T, CIN, H, W, NTHR> st;
     st.load(bin, b);
+    DPA_STAMP(8);
     bn_bwd_coef<CIN, T>(bin, coef, part, sums, blockIdx.x == 0);
+    load_epi();
+    load_wpk();
     DPA_STAMP(3);
     st.emit(coef, [&](int c, int h, int ww, T v00, T v01, T v10, T v11) {
       img[imo((h + 2) * WPD + (ww + 2), c)] = v00;
@@ -646,6 +679,7 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
       img[imo((h + 3) * WPD + (ww + 2), c)] = v10;
       img[imo((h + 3) * WPD + (ww + 3), c)] = v11;
     });
+    store_epi();
   }
   if constexpr (WPK == 1) {
     uint4* dst = reinterpret_cast<uint4*>(wl);
