@@ -49,6 +49,7 @@ class XgmiComm {
   long long max_elems_ = 0, slot_bytes_ = 0, ctr_off_ = 0, ws_bytes_ = 0, timeout_ticks_ = 0;
   int max_blocks_ = 0;
   char* local_ = nullptr;
+  uint32_t* ctr_ = nullptr;  // per-block epoch counters: ordinary (cached) device memory
   Peers peers_;
   int* host_words_ = nullptr;  // [0] error, [1] abort (host-mapped, coherent)
   int* dev_words_ = nullptr;

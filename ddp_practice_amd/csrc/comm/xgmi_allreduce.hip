@@ -15,7 +15,7 @@
 //
 // Protocol (per block b of the grid, 2048 elements per block; blocks are
 // independent, no grid sync):
-//   ep  = ctr[b] + 1      ctr[b]: this rank's count of collectives that had a
+//   ep  = ctr[b] + 1      ctr[b]: this rank's count of collectives that had a  (ordinary device memory)
 //                         block b (equal on every rank: every rank issues the
 //                         same sequence of collectives, stream-ordered)
 //   par = ep & 1          double-buffered slots
@@ -58,7 +58,7 @@ struct Args {
   void* out;
   long long n;              // elements
   long long slot_bytes;     // per-rank slot (granules) in the workspace
-  long long ctr_off;        // byte offset of this rank's per-block epoch counters
+  uint32_t* ctr;            // this rank's per-block epoch counters
   int rank, world;
   int* err;                 // host-mapped: 0 ok, 1 timeout, 2 aborted
   const int* abort_flag;    // host-mapped: non-zero -> stop waiting
@@ -73,14 +73,15 @@ __device__ __forceinline__ unsigned long long granule(float v, uint32_t ep) {
 template <typename T, int OP>
 __global__ __launch_bounds__(kThreads) void oneshot_kernel(Args a) {
   const int b = blockIdx.x, tid = threadIdx.x;
+  DPA_STAMP(0);
   char* mine = a.peers.base[a.rank];
-  uint32_t* ctr = reinterpret_cast<uint32_t*>(mine + a.ctr_off) + b;
+  uint32_t* ctr = a.ctr + b;
   const uint32_t ep = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   const long long par_off = (long long)(ep & 1) * kMaxRanks * a.slot_bytes;
   const long long e0 = (long long)b * kChunkElems + (long long)tid * kPerThread;
   const int ne = (int)max(0LL, min((long long)kPerThread, a.n - e0));
 
-  // 1. my elements -> {value, epoch} granules in slot[parity][me] of every rank
+  // 1. my elements -> {value, epoch} granules in slot[parity][me] of every other rank
   float v[kPerThread];
   const T* in = static_cast<const T*>(a.in) + e0;
   if (ne == kPerThread) {
@@ -99,6 +100,7 @@ __global__ __launch_bounds__(kThreads) void oneshot_kernel(Args a) {
     for (int j = 0; j < kPerThread; ++j) v[j] = j < ne ? Cvt<T>::to_f(in[j]) : 0.f;
   }
   for (int p = 0; p < a.world; ++p) {
+    if (p == a.rank) continue;  // my own values stay in registers (v)
     unsigned long long* dst =
         reinterpret_cast<unsigned long long*>(a.peers.base[p] + par_off + (long long)a.rank * a.slot_bytes) + e0;
     if (ne == kPerThread) {
@@ -110,6 +112,7 @@ __global__ __launch_bounds__(kThreads) void oneshot_kernel(Args a) {
     }
   }
 
+  DPA_STAMP(1);
   // 2. every rank's granules for my elements, in rank order (identical result on
   //    every rank); each granule carries its own epoch tag: no flag, no fence.
   //    The loads of PB ranks x 8 elements are all issued before the first tag
@@ -139,6 +142,7 @@ __global__ __launch_bounds__(kThreads) void oneshot_kernel(Args a) {
 #pragma unroll
       for (int j = 0; j < kPerThread; ++j) {
         if (j >= ne || fail) continue;
+        if (p0 + q == a.rank) g[q][j] = granule(v[j], ep);  // own contribution: not written, not polled
         while ((g[q][j] >> 32) != ep) {
           __builtin_amdgcn_s_sleep(1);
           g[q][j] = __hip_atomic_load(src[q] + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -162,6 +166,7 @@ __global__ __launch_bounds__(kThreads) void oneshot_kernel(Args a) {
       }
     }
   }
+  DPA_STAMP(2);
   if (!fail) {
     T* out = static_cast<T*>(a.out) + e0;
     const float s = OP == 1 ? 1.f / (float)a.world : 1.f;
@@ -181,6 +186,7 @@ __global__ __launch_bounds__(kThreads) void oneshot_kernel(Args a) {
   // 3. this block's epoch is done (after every lane read the counter)
   __syncthreads();
   if (tid == 0 && !fail) __hip_atomic_store(ctr, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  DPA_STAMP(3);
 }
 
 XgmiComm::XgmiComm(int rank, int world, int device, long long slot_bytes, double timeout_s)
@@ -191,8 +197,11 @@ XgmiComm::XgmiComm(int rank, int world, int device, long long slot_bytes, double
   max_elems_ = ((std::max(slot_bytes, 4LL) / 4 + kChunkElems - 1) / kChunkElems) * kChunkElems;
   max_blocks_ = (int)(max_elems_ / kChunkElems);
   slot_bytes_ = max_elems_ * 8;
-  ctr_off_ = 2LL * kMaxRanks * slot_bytes_;
-  ws_bytes_ = ((ctr_off_ + (long long)max_blocks_ * 4 + 4095) / 4096) * 4096;
+  // the epoch counters are only ever touched by this rank, kernel after kernel
+  // on one stream: ordinary device memory (stream order makes each kernel's
+  // store visible to the next), read at L2 latency instead of an uncached trip
+  ctr_off_ = 0;
+  ws_bytes_ = ((2LL * kMaxRanks * slot_bytes_ + 4095) / 4096) * 4096;
   timeout_ticks_ = (long long)(timeout_s * 1e8);
   c10::hip::HIPGuard guard(device_);
   void* p = nullptr;
@@ -200,6 +209,11 @@ XgmiComm::XgmiComm(int rank, int world, int device, long long slot_bytes, double
   DPA_CHECK_HIP(hipMemset(p, 0, ws_bytes_));
   DPA_CHECK_HIP(hipDeviceSynchronize());
   local_ = static_cast<char*>(p);
+  void* c = nullptr;
+  DPA_CHECK_HIP(hipMalloc(&c, (size_t)max_blocks_ * sizeof(uint32_t)));
+  DPA_CHECK_HIP(hipMemset(c, 0, (size_t)max_blocks_ * sizeof(uint32_t)));
+  DPA_CHECK_HIP(hipDeviceSynchronize());
+  ctr_ = static_cast<uint32_t*>(c);
   for (int i = 0; i < kMaxRanks; ++i) peers_.base[i] = nullptr;
   peers_.base[rank_] = local_;
   void* h = nullptr;
@@ -220,6 +234,8 @@ void XgmiComm::close() {
   for (int p = 0; p < world_; ++p)
     if (p != rank_ && peers_.base[p] != nullptr) (void)hipIpcCloseMemHandle(peers_.base[p]);
   (void)hipFree(local_);
+  if (ctr_ != nullptr) (void)hipFree(ctr_);
+  ctr_ = nullptr;
   if (host_words_ != nullptr) (void)hipHostFree(host_words_);
   local_ = nullptr;
   host_words_ = dev_words_ = nullptr;
@@ -266,7 +282,7 @@ void XgmiComm::all_reduce(const at::Tensor& in, const at::Tensor& out, RedOp op,
   a.out = out.data_ptr();
   a.n = in.numel();
   a.slot_bytes = slot_bytes_;
-  a.ctr_off = ctr_off_;
+  a.ctr = ctr_;
   a.rank = rank_;
   a.world = world_;
   a.err = dev_words_;
@@ -366,6 +382,20 @@ class XgmiCollective : public Collective {
 void register_xgmi(pybind11::module& m) {
   namespace py = pybind11;
   auto s = m.def_submodule("xgmi", "one-shot all-reduce over xGMI peer-mapped workspaces");
+#ifdef DPA_TIMING
+  s.def("read_stamps", []() {
+    auto out = at::empty({DPA_MAX_STAMP_BLOCKS, DPA_NSTAMPS}, at::TensorOptions().dtype(at::kLong));
+    DPA_CHECK_HIP(hipDeviceSynchronize());
+    DPA_CHECK_HIP(hipMemcpyFromSymbol(out.data_ptr(), HIP_SYMBOL(dpa_stamps), sizeof(unsigned long long) *
+                                      DPA_MAX_STAMP_BLOCKS * DPA_NSTAMPS));
+    return out;
+  });
+  s.def("clear_stamps", []() {
+    DPA_CHECK_HIP(hipDeviceSynchronize());
+    std::vector<unsigned long long> z(DPA_MAX_STAMP_BLOCKS * DPA_NSTAMPS, 0ull);
+    DPA_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dpa_stamps), z.data(), z.size() * sizeof(unsigned long long)));
+  });
+#endif
   py::class_<xgmi::XgmiComm, std::shared_ptr<xgmi::XgmiComm>>(s, "XgmiComm")
       .def(py::init<int, int, int, long long, double>(), py::arg("rank"), py::arg("world"), py::arg("device"),
            py::arg("max_bytes") = 1 << 20, py::arg("timeout_s") = 600.0)
