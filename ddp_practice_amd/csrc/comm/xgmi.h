@@ -8,11 +8,10 @@
 #include <vector>
 
 #include "comm/collective.h"
+#include "comm/xsite.h"
 
 namespace dpa {
 namespace xgmi {
-
-constexpr int kMaxRanks = 8;
 
 struct Peers {
   char* base[kMaxRanks];  // every rank's workspace, mapped into this process
@@ -43,6 +42,8 @@ class XgmiComm {
   int rank() const { return rank_; }
   int world() const { return world_; }
   int device() const { return device_; }
+  // in-kernel SyncBN exchange site s (comm/xsite.h) for this rank's kernels
+  XSite site(int s) const;
 
  private:
   int rank_, world_, device_;
@@ -50,6 +51,8 @@ class XgmiComm {
   int max_blocks_ = 0;
   char* local_ = nullptr;
   uint32_t* ctr_ = nullptr;  // per-block epoch counters: ordinary (cached) device memory
+  unsigned long long* ticks_ = nullptr;  // per-site {epoch | tickets} words (ordinary device memory)
+  long long site_off_ = 0;               // byte offset of the fused-site regions in every workspace
   Peers peers_;
   int* host_words_ = nullptr;  // [0] error, [1] abort (host-mapped, coherent)
   int* dev_words_ = nullptr;

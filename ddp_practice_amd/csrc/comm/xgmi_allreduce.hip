@@ -201,7 +201,8 @@ XgmiComm::XgmiComm(int rank, int world, int device, long long slot_bytes, double
   // on one stream: ordinary device memory (stream order makes each kernel's
   // store visible to the next), read at L2 latency instead of an uncached trip
   ctr_off_ = 0;
-  ws_bytes_ = ((2LL * kMaxRanks * slot_bytes_ + 4095) / 4096) * 4096;
+  site_off_ = 2LL * kMaxRanks * slot_bytes_;  // then kSites fused-site regions (comm/xsite.h)
+  ws_bytes_ = ((site_off_ + kSites * kSiteBytes + 4095) / 4096) * 4096;
   timeout_ticks_ = (long long)(timeout_s * 1e8);
   c10::hip::HIPGuard guard(device_);
   void* p = nullptr;
@@ -214,6 +215,11 @@ XgmiComm::XgmiComm(int rank, int world, int device, long long slot_bytes, double
   DPA_CHECK_HIP(hipMemset(c, 0, (size_t)max_blocks_ * sizeof(uint32_t)));
   DPA_CHECK_HIP(hipDeviceSynchronize());
   ctr_ = static_cast<uint32_t*>(c);
+  void* tk = nullptr;
+  DPA_CHECK_HIP(hipMalloc(&tk, kSites * sizeof(unsigned long long)));
+  DPA_CHECK_HIP(hipMemset(tk, 0, kSites * sizeof(unsigned long long)));
+  DPA_CHECK_HIP(hipDeviceSynchronize());
+  ticks_ = static_cast<unsigned long long*>(tk);
   for (int i = 0; i < kMaxRanks; ++i) peers_.base[i] = nullptr;
   peers_.base[rank_] = local_;
   void* h = nullptr;
@@ -236,6 +242,8 @@ void XgmiComm::close() {
   (void)hipFree(local_);
   if (ctr_ != nullptr) (void)hipFree(ctr_);
   ctr_ = nullptr;
+  if (ticks_ != nullptr) (void)hipFree(ticks_);
+  ticks_ = nullptr;
   if (host_words_ != nullptr) (void)hipHostFree(host_words_);
   local_ = nullptr;
   host_words_ = dev_words_ = nullptr;
@@ -306,6 +314,20 @@ void XgmiComm::all_reduce(const at::Tensor& in, const at::Tensor& out, RedOp op,
   }
 #undef DPA_XG
   DPA_CHECK_LAUNCH();
+}
+
+XSite XgmiComm::site(int s) const {
+  TORCH_CHECK(opened_ && local_ != nullptr, "xgmi: site of a closed or unopened communicator");
+  TORCH_CHECK(s >= 0 && s < kSites, "xgmi: site id out of range");
+  XSite x;
+  for (int p = 0; p < world_; ++p) x.base[p] = peers_.base[p] + site_off_ + (long long)s * kSiteBytes;
+  x.tick = ticks_ + s;
+  x.rank = rank_;
+  x.world = world_;
+  x.err = dev_words_;
+  x.abort_flag = dev_words_ + 1;
+  x.timeout_ticks = timeout_ticks_;
+  return x;
 }
 
 int XgmiComm::error() const { return host_words_ ? __atomic_load_n(&host_words_[0], __ATOMIC_ACQUIRE) : 0; }

@@ -1,0 +1,127 @@
+// In-kernel SyncBN exchange over xGMI ("fused site"): the all-reduce of a
+// BatchNorm's per-channel sums runs inside the kernel that consumes them,
+// instead of as a collective kernel of its own between producer and consumer.
+//
+// Why: at W > 1 every SyncBN all-reduce (2C+1 floats forward,
+// 2C backward; /root/reference/ddp_main.py:120 convert_sync_batchnorm) is a
+// launch in the critical path that moves a few hundred bytes.  The consumer
+// kernel already reduces the producer's per-workgroup partial-sum slab to one
+// row of local sums in its prologue (cb::bn_finalize / cb::bn_bwd_coef); with
+// a site attached it then
+//   1. (workgroup 0 only) stores that row as {fp32 value, epoch} granules into
+//      slot[parity][me] of this site's region in EVERY peer's workspace,
+//   2. (every workgroup) polls the W rows of its own region and sums them in
+//      rank order -- bit-identical global sums on every rank and workgroup.
+// The granule protocol is the one-shot all-reduce's (comm/xgmi_allreduce.hip):
+// value and tag land in one 8-byte store, no flag, no fence.
+//
+// Epoch without host involvement (graph-replayable, any grid size): every
+// workgroup of a consumer launch takes one ticket from this rank's site word
+// {epoch:32 | tickets:32} with a device-scope atomic; the workgroup that takes
+// the last ticket of the launch returns tickets to 0 and bumps the epoch.  All
+// workgroups of one launch therefore see the same epoch (launches of a site
+// are stream-ordered), and every rank issues the same sequence of launches.
+// Reuse safety as for the one-shot kernel: a rank writes parity p of epoch e+2
+// only after its launch e+1 read every peer's e+1 row, which each peer wrote
+// after its own launch e had completed.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace dpa {
+namespace xgmi {
+
+constexpr int kMaxRanks = 8;
+constexpr int kSites = 8;                                             // sites per communicator
+constexpr int kSiteVals = 128;                                        // floats per rank row (>= 2C+1)
+constexpr long long kSiteSlotBytes = kSiteVals * 8LL;                 // granules
+constexpr long long kSiteBytes = 2LL * kMaxRanks * kSiteSlotBytes;   // both parities
+
+// site ids (ops/convnet_fused.py): one per consumer launch of a step
+enum : int { kSiteFwd1 = 0, kSiteFwd2 = 1, kSiteBwd2Dgrad = 2, kSiteBwd2Wgrad = 3, kSiteBwd1 = 4 };
+
+struct XSite {
+  char* base[kMaxRanks] = {};            // this site's region in every rank's workspace (peer-mapped)
+  unsigned long long* tick = nullptr;    // this rank's {epoch | tickets} word; nullptr: site inactive
+  int rank = 0, world = 1;
+  int* err = nullptr;                    // host-mapped: 1 timeout, 2 aborted
+  const int* abort_flag = nullptr;
+  long long timeout_ticks = 0;           // s_memrealtime ticks (100 MHz)
+  __host__ __device__ bool active() const { return tick != nullptr; }
+};
+
+// Lane 0 of every workgroup, once per launch, as early as possible (the
+// returned word is only needed by xsite_exchange: the atomic's latency hides
+// behind the caller's slab loads).
+__device__ __forceinline__ unsigned long long xsite_ticket(const XSite& xs) {
+  return __hip_atomic_fetch_add(xs.tick, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// vals: n (<= kSiteVals, <= blockDim.x) floats of LDS holding this rank's local
+// row; replaced by the rank-ordered sum over all ranks.  tk: lane 0's ticket.
+// pusher: exactly one workgroup of the launch (blockIdx 0).  Called by every
+// thread of the workgroup; ends with a barrier.
+__device__ __forceinline__ void xsite_exchange(const XSite& xs, float* vals, int n, unsigned long long tk,
+                                               bool pusher) {
+  __shared__ uint32_t ep_s;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    const uint32_t nblk = gridDim.x * gridDim.y * gridDim.z;
+    if ((uint32_t)tk == nblk - 1u)  // last ticket of this launch: next launch, next epoch
+      __hip_atomic_fetch_add(xs.tick, (1ull << 32) - (unsigned long long)nblk, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    ep_s = (uint32_t)(tk >> 32) + 1u;
+  }
+  __syncthreads();
+  if (tid < n) {
+    const uint32_t ep = ep_s;
+    const long long par = (long long)(ep & 1u) * kMaxRanks * kSiteSlotBytes;
+    const float mine = vals[tid];
+    const unsigned long long gm = ((unsigned long long)ep << 32) | (unsigned long long)__float_as_uint(mine);
+    if (pusher)
+      for (int p = 0; p < xs.world; ++p)
+        if (p != xs.rank)
+          *reinterpret_cast<unsigned long long*>(xs.base[p] + par + (long long)xs.rank * kSiteSlotBytes +
+                                                 (long long)tid * 8) = gm;
+    // every peer's granule loaded before the first tag check (one round trip)
+    unsigned long long g[kMaxRanks];
+    const unsigned long long* src[kMaxRanks];
+#pragma unroll
+    for (int p = 0; p < kMaxRanks; ++p) {
+      src[p] = reinterpret_cast<const unsigned long long*>(xs.base[xs.rank] + par + (long long)p * kSiteSlotBytes +
+                                                           (long long)tid * 8);
+      g[p] = (p < xs.world && p != xs.rank) ? __hip_atomic_load(src[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                            : gm;
+    }
+    float acc = 0.f;
+    bool fail = false;
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    unsigned polls = 0;
+#pragma unroll
+    for (int p = 0; p < kMaxRanks; ++p) {
+      if (p >= xs.world) continue;
+      while (!fail && (uint32_t)(g[p] >> 32) != ep) {
+        __builtin_amdgcn_s_sleep(1);
+        g[p] = __hip_atomic_load(src[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((++polls & 255u) == 0) {
+          int why = 0;
+          if (__hip_atomic_load(xs.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) why = 2;
+          else if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xs.timeout_ticks) why = 1;
+          if (why) {
+            __hip_atomic_store(xs.err, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            fail = true;
+          }
+        }
+      }
+      const float x = fail ? 0.f : __uint_as_float((uint32_t)g[p]);
+      acc = p == 0 ? x : acc + x;
+    }
+    vals[tid] = acc;  // only this lane reads or writes slot tid in here
+  }
+  __syncthreads();
+}
+
+}  // namespace xgmi
+}  // namespace dpa

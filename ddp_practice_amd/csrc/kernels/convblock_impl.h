@@ -32,6 +32,7 @@
 //    (cf. torch/nn/modules/_functions.py:74-101).
 #pragma once
 #include "common.h"
+#include "comm/xsite.h"
 
 namespace dpa {
 namespace cb {
@@ -128,6 +129,7 @@ struct BNParams {
   float momentum;
   float eps;
   int train;
+  xgmi::XSite xs;  // active: SyncBN sums exchanged in here (comm/xsite.h), fslab holds local rows
 };
 
 // Sum of src[r * RL + j] over rows r = g, g + G, ...: up to RSUM_U rows per
@@ -172,6 +174,9 @@ __device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, flo
       }
     }
     const int64_t nb0 = leader ? bp.nbt[0] : 0;
+    const bool xon = bp.xs.active();
+    unsigned long long tk = 0;
+    if (xon && tid == 0) tk = xgmi::xsite_ticket(bp.xs);  // latency hides behind the slab loads
     part[tid] = g < G ? strided_rowsum(bp.fslab, bp.nrows, RL, j, g, G) : 0.f;
     __syncthreads();
     if (tid < RL) {
@@ -180,6 +185,7 @@ __device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, flo
       part[tid] = t;  // only this thread reads slot tid (its gg = 0 term) before the write
     }
     __syncthreads();
+    if (xon) xgmi::xsite_exchange(bp.xs, part, RL, tk, leader);  // local -> global sums (SyncBN)
     if (tid < C) {
       const float n = part[2 * C];
       const float m1 = part[tid] / n;
@@ -274,6 +280,7 @@ struct BwdIn {
   float eps;
   float* dgamma;          // written by workgroup 0 when non-null
   float* dbeta;
+  xgmi::XSite xs;         // active: gsum holds local rows, exchanged in here (comm/xsite.h)
 };
 
 // Column sums of rows x RL floats (row-major) -> out[0..RL) in LDS, using the
@@ -307,7 +314,18 @@ __device__ __forceinline__ void bn_bwd_coef(const BwdIn<T>& bi, float* coef, flo
     shf = bi.fstats[2 * C + 1 + tid];
     gam = bi.gamma[tid];
   }
+  const bool xon = bi.xs.active();
+  unsigned long long tk = 0;
+  if (xon && tid == 0) tk = xgmi::xsite_ticket(bi.xs);  // latency hides behind the slab loads
   colsum_rows(bi.gsum, bi.grows, 2 * C, part, sums);
+  if (xon) {
+    // dgamma / dbeta are this rank's (DDP averages them); the coefficients use the global sums
+    if (leader && bi.dgamma != nullptr && tid < C) {
+      bi.dgamma[tid] = sums[C + tid];
+      bi.dbeta[tid] = sums[tid];
+    }
+    xgmi::xsite_exchange(bi.xs, sums, 2 * C, tk, leader);
+  }
   if (tid < C) {
     const float m1 = f0 / n;
     const float mean = shf + m1;
@@ -317,13 +335,13 @@ __device__ __forceinline__ void bn_bwd_coef(const BwdIn<T>& bi, float* coef, flo
     coef[2 * C + tid] = gam * istd;
     coef[3 * C + tid] = mean;
     coef[4 * C + tid] = istd;
-    if (leader && bi.dgamma != nullptr && bi.lsum == bi.gsum) {
+    if (leader && bi.dgamma != nullptr && bi.lsum == bi.gsum && !xon) {
       bi.dgamma[tid] = sums[C + tid];
       bi.dbeta[tid] = sums[tid];
     }
   }
   __syncthreads();
-  if (leader && bi.dgamma != nullptr && bi.lsum != bi.gsum) {
+  if (leader && bi.dgamma != nullptr && bi.lsum != bi.gsum && !xon) {
     colsum_rows(bi.lsum, bi.lrows, 2 * C, part, sums);
     if (tid < C) {
       bi.dgamma[tid] = sums[C + tid];

@@ -16,6 +16,7 @@
 // partial sums are all-reduced between the launches (host side).  Everything
 // is deterministic (no float atomics).
 #include "convblock_impl.h"
+#include "comm/xgmi.h"
 
 namespace dpa {
 namespace cnf {
@@ -246,12 +247,18 @@ static BwdIn<T> bwd_in(at::Tensor dp, at::Tensor idx, at::Tensor y, at::Tensor f
   return bi;
 }
 
+// xc (SyncBN over the xGMI engine, training only): the consumer kernel
+// exchanges the BN sums itself (comm/xsite.h); the slab arguments then hold
+// this rank's partial sums and no all-reduce runs between the launches.
+typedef std::shared_ptr<xgmi::XgmiComm> XcPtr;
+static xgmi::XSite site_of(const XcPtr& xc, int s) { return xc ? xc->site(s) : xgmi::XSite{}; }
+
 // [BN1 -> ReLU -> pool1] -> conv2 (+ BN2 partial sums when training).
 void conv2_fwd(at::Tensor y1, c10::optional<at::Tensor> fslab1, at::Tensor fstats1, at::Tensor g1, at::Tensor b1,
                at::Tensor rm1, at::Tensor rv1, at::Tensor nbt1, double momentum, double eps, bool train, at::Tensor w2,
                at::Tensor bias2, at::Tensor y2, c10::optional<at::Tensor> fslab2, at::Tensor fstats2, at::Tensor rm2,
                c10::optional<at::Tensor> p1_out, c10::optional<at::Tensor> idx1_out,
-               c10::optional<at::Tensor> xh1_out, at::Tensor wpk) {
+               c10::optional<at::Tensor> xh1_out, at::Tensor wpk, XcPtr xc) {
   DPA_CHECK_INPUT(y1); DPA_CHECK_INPUT(w2); DPA_CHECK_INPUT(y2); DPA_CHECK_INPUT(wpk);
   TORCH_CHECK(wpk.numel() == cb::W2F_LEN && wpk.scalar_type() == y1.scalar_type(), "packed conv2 weights");
   const int B = (int)y1.size(0);
@@ -264,7 +271,8 @@ void conv2_fwd(at::Tensor y1, c10::optional<at::Tensor> fslab1, at::Tensor fstat
                 xh1_out->numel() == p1_out->numel());
   if (train) TORCH_CHECK(fslab2.has_value() && fslab2->numel() == (int64_t)B * 2 * cb::fslab_row(32));
   if (B == 0) return;
-  const BNParams bp = bn_params(fslab1, fstats1, g1, b1, rm1, rv1, nbt1, momentum, eps, train, 16);
+  BNParams bp = bn_params(fslab1, fstats1, g1, b1, rm1, rv1, nbt1, momentum, eps, train, 16);
+  if (train) bp.xs = site_of(xc, xgmi::kSiteFwd1);
   constexpr int ns = 2;
   hipStream_t stream = cur_stream();
   with_t(dt_of(y1), [&](auto tag) {
@@ -289,7 +297,7 @@ void conv2_fwd(at::Tensor y1, c10::optional<at::Tensor> fslab1, at::Tensor fstat
 void head_fwd(at::Tensor y2, c10::optional<at::Tensor> fslab2, at::Tensor fstats2, at::Tensor g2, at::Tensor b2,
               at::Tensor rm2, at::Tensor rv2, at::Tensor nbt2, double momentum, double eps, bool train, at::Tensor wfc,
               at::Tensor bfc, at::Tensor logits, c10::optional<at::Tensor> p2_out, c10::optional<at::Tensor> idx2_out,
-              c10::optional<at::Tensor> xh2_out) {
+              c10::optional<at::Tensor> xh2_out, XcPtr xc) {
   DPA_CHECK_INPUT(y2); DPA_CHECK_INPUT(wfc); DPA_CHECK_INPUT(logits);
   const int B = (int)y2.size(0), N = (int)wfc.size(0);
   TORCH_CHECK(y2.size(1) == 32 && y2.size(2) == 14 && y2.size(3) == 14 && wfc.size(1) == 32 * 49,
@@ -301,7 +309,8 @@ void head_fwd(at::Tensor y2, c10::optional<at::Tensor> fslab2, at::Tensor fstats
     TORCH_CHECK(p2_out->numel() == (int64_t)B * 1568 && idx2_out->numel() == p2_out->numel() &&
                 xh2_out->numel() == p2_out->numel());
   if (B == 0) return;
-  const BNParams bp = bn_params(fslab2, fstats2, g2, b2, rm2, rv2, nbt2, momentum, eps, train, 32);
+  BNParams bp = bn_params(fslab2, fstats2, g2, b2, rm2, rv2, nbt2, momentum, eps, train, 32);
+  if (train) bp.xs = site_of(xc, xgmi::kSiteFwd2);
   hipStream_t stream = cur_stream();
   with_t(dt_of(y2), [&](auto tag) {
     typedef decltype(tag) T;
@@ -385,7 +394,7 @@ int64_t dgrad2_rows(int64_t B) { return B * kDgradSplit; }
 // [pool2/ReLU2/BN2 backward] -> conv2 data grad -> dp1 (+ BN1 partial sums rows).
 void conv2_dgrad(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx2, at::Tensor fstats2,
                  at::Tensor gsum2, at::Tensor g2, double eps2, at::Tensor dp1, at::Tensor idx1, at::Tensor xh1,
-                 at::Tensor bslab1) {
+                 at::Tensor bslab1, XcPtr xc) {
   DPA_CHECK_INPUT(y2); DPA_CHECK_INPUT(dp1); DPA_CHECK_INPUT(wpk_d);
   TORCH_CHECK(wpk_d.numel() == cb::W2D_LEN && wpk_d.scalar_type() == y2.scalar_type(),
               "packed conv2 data-grad weights");
@@ -397,6 +406,7 @@ void conv2_dgrad(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx
   with_t(dt_of(y2), [&](auto tag) {
     typedef decltype(tag) T;
     BwdIn<T> bi = bwd_in<T>(dp2, idx2, y2, fstats2, gsum2, c10::nullopt, g2, eps2, 32, c10::nullopt, c10::nullopt);
+    bi.xs = site_of(xc, xgmi::kSiteBwd2Dgrad);
     BwdEpi<T> ep{idx1.data_ptr<uint8_t>(), dptr<T>(xh1), bslab1.data_ptr<float>()};
     hipLaunchKernelGGL((cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1, 1>), dim3(B * kDgradSplit), dim3(cb::NTHR),
                        0, cur_stream(), nullptr, nullptr, nullptr, dptr<T>(dp1), nullptr, nullptr, nullptr,
@@ -418,7 +428,7 @@ int64_t wgrad_bn_rows(int64_t layer, int64_t B) {
 
 void conv_wgrad_bn(at::Tensor x, at::Tensor y, at::Tensor dp, at::Tensor idx, at::Tensor fstats, at::Tensor gsum,
                    c10::optional<at::Tensor> lsum, at::Tensor gamma, double eps, c10::optional<at::Tensor> dgamma,
-                   c10::optional<at::Tensor> dbeta, at::Tensor wslab) {
+                   c10::optional<at::Tensor> dbeta, at::Tensor wslab, XcPtr xc) {
   DPA_CHECK_INPUT(x); DPA_CHECK_INPUT(y);
   const int B = (int)y.size(0);
   const int cin = (int)x.size(1), cout = (int)y.size(1), H = (int)y.size(2);
@@ -427,6 +437,10 @@ void conv_wgrad_bn(at::Tensor x, at::Tensor y, at::Tensor dp, at::Tensor idx, at
   with_t(dt_of(y), [&](auto tag) {
     typedef decltype(tag) T;
     BwdIn<T> bi = bwd_in<T>(dp, idx, y, fstats, gsum, lsum, gamma, eps, cout, dgamma, dbeta);
+    if (xc) {
+      TORCH_CHECK(!lsum.has_value(), "fused SyncBN exchange: gsum must be this rank's rows (no lsum)");
+      bi.xs = site_of(xc, cout == 32 ? xgmi::kSiteBwd2Wgrad : xgmi::kSiteBwd1);
+    }
     if (cin == 16 && cout == 32 && H == 14) {
       constexpr int ns = (14 + WG2_ROWS - 1) / WG2_ROWS;
       TORCH_CHECK(wslab.numel() == (int64_t)B * ns * (32 * 400 + 32), "wgrad slab size");

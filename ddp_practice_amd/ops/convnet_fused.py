@@ -13,11 +13,15 @@ removes launches that exist only because torch runs one module at a time:
 Every BatchNorm backward is applied while staging the operand of the next
 GEMM (the conv-output gradient never exists in HBM), and its reductions are
 emitted by the kernel that produced the pooled gradient.  With SyncBN
-(``comm`` active) the partial sums are all-reduced between the kernels (one
-small collective each: 2 forward, 2 backward).  Parameter gradients are views
-of one output buffer.
+(``comm`` active) over the xGMI engine, each consuming kernel exchanges the
+per-channel sums with its peers itself (csrc/comm/xsite.h): no collective
+launch between the kernels.  Over any other communicator the partial sums are
+all-reduced between the kernels (one small collective each: 2 forward,
+2 backward).  Parameter gradients are views of one output buffer.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
@@ -47,6 +51,15 @@ def supported(model, x: torch.Tensor) -> bool:
     return fc.in_features == 32 * 49 and fc.bias is not None and 1 <= n <= 64 and b * (n + 49) + n * 49 <= 16384
 
 
+def _fused_site_engine(comm):
+    """The communicator's xGMI engine when SyncBN may exchange its sums inside the
+    kernels (csrc/comm/xsite.h), else None (all-reduces between the launches).
+    DPA_FUSED_SYNC=0 forces the launch-per-collective path (A/B runs)."""
+    if os.environ.get("DPA_FUSED_SYNC", "1") == "0":
+        return None
+    return getattr(comm, "xgmi", None)
+
+
 class ConvNetFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, b1, g1, be1, w2, b2, g2, be2, wfc, bfc, bufs, training, moms, epss, comm, cdtype):
@@ -59,6 +72,8 @@ class ConvNetFn(torch.autograd.Function):
         dev = x.device
         N = wfc.shape[0]
         sync = comm is not None and comm.active and training
+        # SyncBN sums exchanged inside the consuming kernels when the xGMI engine is up
+        xc = _fused_site_engine(comm) if sync else None
         y1 = torch.empty((B, 16, 28, 28), dtype=cdtype, device=dev)
         y2 = torch.empty((B, 32, 14, 14), dtype=cdtype, device=dev)
         logits = torch.empty((B, N), dtype=cdtype, device=dev)
@@ -78,23 +93,25 @@ class ConvNetFn(torch.autograd.Function):
             idx2 = torch.empty((B, 32 * 49), dtype=torch.uint8, device=dev)
             xh2 = torch.empty((B, 32 * 49), dtype=cdtype, device=dev)
             cn.conv1_fwd_pack(x, w1, b1, y1, fslab1, fstats1, rm1, w2, wpk_f, wpk_d)
-            if sync:
+            if sync and xc is None:
                 comm.all_reduce_(fslab1)
             cn.conv2_fwd(y1, fslab1, fstats1, g1, be1, rm1, rv1, nbt1, m1, e1, True, w2, b2, y2, fslab2, fstats2,
-                         rm2, p1, idx1, xh1, wpk_f)
-            if sync:
+                         rm2, p1, idx1, xh1, wpk_f, xc)
+            if sync and xc is None:
                 comm.all_reduce_(fslab2)
-            cn.head_fwd(y2, fslab2, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, True, wfc, bfc, logits, p2, idx2, xh2)
+            cn.head_fwd(y2, fslab2, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, True, wfc, bfc, logits, p2, idx2, xh2,
+                        xc)
             ctx.save_for_backward(x, wpk_d, wfc, g1, g2, y1, p1, idx1, xh1, fstats1, y2, p2, idx2, xh2, fstats2)
         else:
             cn.conv1_fwd_pack(x, w1, b1, y1, None, None, None, w2, wpk_f, wpk_d)
             cn.conv2_fwd(y1, None, fstats1, g1, be1, rm1, rv1, nbt1, m1, e1, False, w2, b2, y2, None, fstats2, rm2,
-                         None, None, None, wpk_f)
+                         None, None, None, wpk_f, None)
             cn.head_fwd(y2, None, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, False, wfc, bfc, logits, None, None,
-                        None)
+                        None, None)
         ctx.training = training
         ctx.sync = sync
         ctx.comm = comm
+        ctx.xc = xc
         ctx.eps = (e1, e2)
         ctx.shapes = (w1.shape, w2.shape, wfc.shape)
         return logits
@@ -106,7 +123,7 @@ class ConvNetFn(torch.autograd.Function):
         cb, cn = _mods()
         x, wpk_d, wfc, g1, g2, y1, p1, idx1, xh1, fstats1, y2, p2, idx2, xh2, fstats2 = ctx.saved_tensors
         e1, e2 = ctx.eps
-        comm, sync = ctx.comm, ctx.sync
+        comm, sync, xc = ctx.comm, ctx.sync, ctx.xc
         dl = dlogits.to(y2.dtype).contiguous()
         B = y2.shape[0]
         dev = y2.device
@@ -123,18 +140,21 @@ class ConvNetFn(torch.autograd.Function):
         bsum2 = torch.empty(64, **f32)
         dp2 = torch.empty_like(p2)
         cn.head_bwd(dl, wfc, p2, idx2, xh2, dwfc, dbfc, dg2, dbe2, bsum2, dp2)
-        gsum2 = comm.all_reduce(bsum2) if sync else bsum2
+        gsum2 = comm.all_reduce(bsum2) if sync and xc is None else bsum2
         # 2. BN2 bwd -> conv2 dgrad -> dp1 (+ BN1 partial sums)
         dp1 = torch.empty((B, 16, 14, 14), dtype=y1.dtype, device=dev)
         bslab1 = torch.empty(cn.dgrad2_rows(B) * 32, **f32)
-        cn.conv2_dgrad(wpk_d, y2, dp2, idx2, fstats2, gsum2, g2, e2, dp1, idx1, xh1, bslab1)
+        cn.conv2_dgrad(wpk_d, y2, dp2, idx2, fstats2, gsum2, g2, e2, dp1, idx1, xh1, bslab1, xc)
         # 3. BN2 bwd -> conv2 wgrad partials (independent of 2)
         wslab2 = torch.empty(cn.wgrad_bn_rows(2, B) * (n_w2 + 32), **f32)
-        cn.conv_wgrad_bn(p1, y2, dp2, idx2, fstats2, gsum2, None, g2, e2, None, None, wslab2)
+        cn.conv_wgrad_bn(p1, y2, dp2, idx2, fstats2, gsum2, None, g2, e2, None, None, wslab2, xc)
         # 4. BN1 bwd -> conv1 wgrad partials (+ dgamma1 / dbeta1 from the local sums)
-        gslab1 = comm.all_reduce(bslab1) if sync else bslab1
         wslab1 = torch.empty(cn.wgrad_bn_rows(1, B) * (n_w1 + 16), **f32)
-        cn.conv_wgrad_bn(x, y1, dp1, idx1, fstats1, gslab1, bslab1 if sync else None, g1, e1, dg1, dbe1, wslab1)
+        if sync and xc is None:
+            gslab1 = comm.all_reduce(bslab1)
+            cn.conv_wgrad_bn(x, y1, dp1, idx1, fstats1, gslab1, bslab1, g1, e1, dg1, dbe1, wslab1, None)
+        else:
+            cn.conv_wgrad_bn(x, y1, dp1, idx1, fstats1, bslab1, None, g1, e1, dg1, dbe1, wslab1, xc)
         # 5. weight-grad partial sums -> [dW1 | db1], [dW2 | db2]
         cb.slab_reduce(wslab1, n_w1 + 16, out.narrow(0, 0, n_w1 + 16), wslab2, n_w2 + 32,
                        out.narrow(0, n_w1 + 48, n_w2 + 32))
