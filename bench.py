@@ -104,6 +104,8 @@ def main(argv=None):
         model = DistributedDataParallel(model, device_ids=[local_rank])
     optimizer = SGD(model.parameters(), lr=1e-4)
     scaler = GradScaler(enabled=amp is not None)
+    # DDP gradient averaging inside the fused AMP-SGD kernel (xGMI engine only)
+    fused_grad = dist_path and amp is not None and model.defer_grad_sync_to(optimizer)
 
     ds = synthetic(60000, seed=1)
     sampler = DistributedSampler(ds, num_replicas=world, rank=rank)
@@ -182,6 +184,8 @@ def main(argv=None):
                 "optimizer": "SGD(lr=1e-4)",
                 "hipgraph": bool(captured),
                 "comm": _comm_desc(),
+                "grad_avg": ("in AMP-SGD kernel (xGMI)" if fused_grad else "reducer all-reduce") if dist_path
+                else "none (1 rank)",
                 "shared_gpu": bool(args.share_gpu),
                 "steps_per_graph": spg,
                 "est_3epoch_train_s": round(3 * len(loader) * ms / 1e3, 3),

@@ -176,6 +176,9 @@ class GradScaler:
             raise RuntimeError("unscale_() has already been called on this optimizer since the last update().")
         if st["stage"] == "stepped":
             raise RuntimeError("unscale_() is being called after step().")
+        flush = getattr(optimizer, "_flush_deferred", None)  # DDP.defer_grad_sync_to: average first
+        if flush is not None:
+            flush()
         grads = self._grads(optimizer)
         if self._scale is None:
             self._lazy_init(grads[0].device if grads else torch.device(self._device))

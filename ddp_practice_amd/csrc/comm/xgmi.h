@@ -44,6 +44,9 @@ class XgmiComm {
   int device() const { return device_; }
   // in-kernel SyncBN exchange site s (comm/xsite.h) for this rank's kernels
   XSite site(int s) const;
+  // the DDP gradient exchange of the fused AMP-SGD step (rows of max_bytes/4 floats)
+  XSite grad_site() const;
+  long long max_elems() const { return max_elems_; }
 
  private:
   int rank_, world_, device_;
@@ -53,6 +56,7 @@ class XgmiComm {
   uint32_t* ctr_ = nullptr;  // per-block epoch counters: ordinary (cached) device memory
   unsigned long long* ticks_ = nullptr;  // per-site {epoch | tickets} words (ordinary device memory)
   long long site_off_ = 0;               // byte offset of the fused-site regions in every workspace
+  long long grad_off_ = 0;               // byte offset of the gradient-exchange region
   Peers peers_;
   int* host_words_ = nullptr;  // [0] error, [1] abort (host-mapped, coherent)
   int* dev_words_ = nullptr;

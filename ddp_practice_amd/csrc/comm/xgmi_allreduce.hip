@@ -202,7 +202,8 @@ XgmiComm::XgmiComm(int rank, int world, int device, long long slot_bytes, double
   // store visible to the next), read at L2 latency instead of an uncached trip
   ctr_off_ = 0;
   site_off_ = 2LL * kMaxRanks * slot_bytes_;  // then kSites fused-site regions (comm/xsite.h)
-  ws_bytes_ = ((site_off_ + kSites * kSiteBytes + 4095) / 4096) * 4096;
+  grad_off_ = site_off_ + kSites * kSiteBytes;  // then the gradient-exchange slots [2][kMaxRanks]
+  ws_bytes_ = ((grad_off_ + 2LL * kMaxRanks * slot_bytes_ + 4095) / 4096) * 4096;
   timeout_ticks_ = (long long)(timeout_s * 1e8);
   c10::hip::HIPGuard guard(device_);
   void* p = nullptr;
@@ -327,6 +328,14 @@ XSite XgmiComm::site(int s) const {
   x.err = dev_words_;
   x.abort_flag = dev_words_ + 1;
   x.timeout_ticks = timeout_ticks_;
+  return x;
+}
+
+XSite XgmiComm::grad_site() const {
+  XSite x = site(kSiteGrad);
+  for (int p = 0; p < world_; ++p) x.base[p] = peers_.base[p] + grad_off_;
+  x.slot_bytes = slot_bytes_;
+  x.max_vals = max_elems_;
   return x;
 }
 

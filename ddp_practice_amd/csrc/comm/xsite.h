@@ -41,6 +41,9 @@ constexpr long long kSiteBytes = 2LL * kMaxRanks * kSiteSlotBytes;   // both par
 
 // site ids (ops/convnet_fused.py): one per consumer launch of a step
 enum : int { kSiteFwd1 = 0, kSiteFwd2 = 1, kSiteBwd2Dgrad = 2, kSiteBwd2Wgrad = 3, kSiteBwd1 = 4 };
+// the DDP gradient exchange inside the fused AMP-SGD kernel (XgmiComm::grad_site):
+// its own epoch word, slots of the engine's full message size
+constexpr int kSiteGrad = kSites - 1;
 
 struct XSite {
   char* base[kMaxRanks] = {};            // this site's region in every rank's workspace (peer-mapped)
@@ -49,6 +52,8 @@ struct XSite {
   int* err = nullptr;                    // host-mapped: 1 timeout, 2 aborted
   const int* abort_flag = nullptr;
   long long timeout_ticks = 0;           // s_memrealtime ticks (100 MHz)
+  long long slot_bytes = kSiteSlotBytes; // one rank's row of granules; a parity holds kMaxRanks rows
+  long long max_vals = kSiteVals;        // floats per row
   __host__ __device__ bool active() const { return tick != nullptr; }
 };
 
@@ -59,6 +64,36 @@ __device__ __forceinline__ unsigned long long xsite_ticket(const XSite& xs) {
   return __hip_atomic_fetch_add(xs.tick, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Lane 0: the launch's epoch from its ticket (the last ticket of the launch
+// re-arms the word for the next launch).
+__device__ __forceinline__ uint32_t xsite_epoch(const XSite& xs, unsigned long long tk) {
+  const uint32_t nblk = gridDim.x * gridDim.y * gridDim.z;
+  if ((uint32_t)tk == nblk - 1u)  // last ticket of this launch: next launch, next epoch
+    __hip_atomic_fetch_add(xs.tick, (1ull << 32) - (unsigned long long)nblk, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  return (uint32_t)(tk >> 32) + 1u;
+}
+
+// Spin until granule *src carries epoch ep (bounded: abort flag / timeout ->
+// error word, fail = true).  g: the granule already loaded.
+__device__ __forceinline__ float xsite_wait(const XSite& xs, const unsigned long long* src, unsigned long long g,
+                                            uint32_t ep, long long t0, unsigned& polls, bool& fail) {
+  while (!fail && (uint32_t)(g >> 32) != ep) {
+    __builtin_amdgcn_s_sleep(1);
+    g = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if ((++polls & 255u) == 0) {
+      int why = 0;
+      if (__hip_atomic_load(xs.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) why = 2;
+      else if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xs.timeout_ticks) why = 1;
+      if (why) {
+        __hip_atomic_store(xs.err, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        fail = true;
+      }
+    }
+  }
+  return fail ? 0.f : __uint_as_float((uint32_t)g);
+}
+
 // vals: n (<= kSiteVals, <= blockDim.x) floats of LDS holding this rank's local
 // row; replaced by the rank-ordered sum over all ranks.  tk: lane 0's ticket.
 // pusher: exactly one workgroup of the launch (blockIdx 0).  Called by every
@@ -67,30 +102,24 @@ __device__ __forceinline__ void xsite_exchange(const XSite& xs, float* vals, int
                                                bool pusher) {
   __shared__ uint32_t ep_s;
   const int tid = threadIdx.x;
-  if (tid == 0) {
-    const uint32_t nblk = gridDim.x * gridDim.y * gridDim.z;
-    if ((uint32_t)tk == nblk - 1u)  // last ticket of this launch: next launch, next epoch
-      __hip_atomic_fetch_add(xs.tick, (1ull << 32) - (unsigned long long)nblk, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-    ep_s = (uint32_t)(tk >> 32) + 1u;
-  }
+  if (tid == 0) ep_s = xsite_epoch(xs, tk);
   __syncthreads();
   if (tid < n) {
     const uint32_t ep = ep_s;
-    const long long par = (long long)(ep & 1u) * kMaxRanks * kSiteSlotBytes;
+    const long long par = (long long)(ep & 1u) * kMaxRanks * xs.slot_bytes;
     const float mine = vals[tid];
     const unsigned long long gm = ((unsigned long long)ep << 32) | (unsigned long long)__float_as_uint(mine);
     if (pusher)
       for (int p = 0; p < xs.world; ++p)
         if (p != xs.rank)
-          *reinterpret_cast<unsigned long long*>(xs.base[p] + par + (long long)xs.rank * kSiteSlotBytes +
+          *reinterpret_cast<unsigned long long*>(xs.base[p] + par + (long long)xs.rank * xs.slot_bytes +
                                                  (long long)tid * 8) = gm;
     // every peer's granule loaded before the first tag check (one round trip)
     unsigned long long g[kMaxRanks];
     const unsigned long long* src[kMaxRanks];
 #pragma unroll
     for (int p = 0; p < kMaxRanks; ++p) {
-      src[p] = reinterpret_cast<const unsigned long long*>(xs.base[xs.rank] + par + (long long)p * kSiteSlotBytes +
+      src[p] = reinterpret_cast<const unsigned long long*>(xs.base[xs.rank] + par + (long long)p * xs.slot_bytes +
                                                            (long long)tid * 8);
       g[p] = (p < xs.world && p != xs.rank) ? __hip_atomic_load(src[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                             : gm;
@@ -102,20 +131,7 @@ __device__ __forceinline__ void xsite_exchange(const XSite& xs, float* vals, int
 #pragma unroll
     for (int p = 0; p < kMaxRanks; ++p) {
       if (p >= xs.world) continue;
-      while (!fail && (uint32_t)(g[p] >> 32) != ep) {
-        __builtin_amdgcn_s_sleep(1);
-        g[p] = __hip_atomic_load(src[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if ((++polls & 255u) == 0) {
-          int why = 0;
-          if (__hip_atomic_load(xs.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) why = 2;
-          else if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xs.timeout_ticks) why = 1;
-          if (why) {
-            __hip_atomic_store(xs.err, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            fail = true;
-          }
-        }
-      }
-      const float x = fail ? 0.f : __uint_as_float((uint32_t)g[p]);
+      const float x = xsite_wait(xs, src[p], g[p], ep, t0, polls, fail);
       acc = p == 0 ? x : acc + x;
     }
     vals[tid] = acc;  // only this lane reads or writes slot tid in here

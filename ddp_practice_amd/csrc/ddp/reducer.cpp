@@ -198,7 +198,10 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     // join on the stream the buckets were launched from (the backward's stream,
     // i.e. the capture stream under hipGraph capture) — not whatever stream is
     // current on the thread that runs the engine's final callback
-    for (size_t b = 0; b < buckets_.size(); ++b) comm_->wait((int)b, on_cuda_ ? work_stream_ : nullptr);
+    if (defer_)
+      deferred_ = true;  // the buckets hold this rank's gradients until flush_deferred() / a fused consumer
+    else
+      for (size_t b = 0; b < buckets_.size(); ++b) comm_->wait((int)b, on_cuda_ ? work_stream_ : nullptr);
     // grads become views of the all-reduced buckets (in-place buckets: they already are)
     for (auto& bk : buckets_) {
       if (bk.inplace) continue;
@@ -210,6 +213,30 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     }
     finalized_ = true;
     record_order_ = false;
+  }
+
+  // Deferred gradient averaging (DistributedDataParallel.defer_grad_sync_to):
+  // buckets are not all-reduced at the end of backward; the gradient consumer
+  // either averages them itself (the fused AMP-SGD kernel over the xGMI engine:
+  // consume_deferred()) or calls flush_deferred(), which runs the bucket
+  // all-reduces now, on the caller's stream, and joins them.
+  void set_defer(bool on) {
+    std::lock_guard<std::mutex> g(mu_);
+    TORCH_CHECK(!(defer_ && !on && deferred_), "DDP: gradients still pending a deferred all-reduce");
+    defer_ = on;
+  }
+  bool deferred_pending() const { return deferred_; }
+  void consume_deferred() {
+    std::lock_guard<std::mutex> g(mu_);
+    deferred_ = false;
+  }
+  void flush_deferred() {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!deferred_) return;
+    for (size_t b = 0; b < buckets_.size(); ++b)
+      comm_->all_reduce_async(buckets_[b].red, RedOp::AVG, (int)b);
+    for (size_t b = 0; b < buckets_.size(); ++b) comm_->wait((int)b, nullptr);
+    deferred_ = false;
   }
 
   std::vector<int64_t> ready_order() const { return order_; }
@@ -234,6 +261,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     std::vector<int64_t> params, offsets;
     std::vector<int64_t> unused;
     at::Tensor flat;
+    at::Tensor red;  // what the all-reduce covers: the in-place gradient region or flat
     int64_t pending = 0;
     bool launched = false;
     bool inplace = false;  // reduced where the grads live (no pack)
@@ -291,8 +319,11 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
       Bucket& bk = buckets_[next_launch_];
       at::Tensor region;
       if (zero_copy_ && tiled_region_locked(bk, region)) {
-        comm_->all_reduce_async(region, RedOp::AVG, (int)next_launch_);
-        if (join_each_) comm_->wait((int)next_launch_, nullptr);
+        bk.red = region;
+        if (!defer_) {
+          comm_->all_reduce_async(region, RedOp::AVG, (int)next_launch_);
+          if (join_each_) comm_->wait((int)next_launch_, nullptr);
+        }
         bk.inplace = bk.launched = true;
         ++next_launch_;
         continue;
@@ -300,7 +331,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
       bk.inplace = false;
       std::vector<at::Tensor> srcs;
       std::vector<int64_t> offs;
-      const double inv_w = 1.0 / (double)comm_->world();
+      const double inv_w = defer_ ? 1.0 : 1.0 / (double)comm_->world();  // deferred: averaged by the consumer
       for (size_t j = 0; j < bk.params.size(); ++j) {
         const int64_t i = bk.params[j];
         at::Tensor gr = params_[i].grad();
@@ -321,8 +352,11 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
             bk.flat.narrow(0, offs[k], srcs[k].numel()).copy_(srcs[k]).mul_(inv_w);
         }
       }
-      comm_->all_reduce_async(bk.flat, RedOp::SUM, (int)next_launch_);
-      if (join_each_) comm_->wait((int)next_launch_, nullptr);
+      bk.red = bk.flat;
+      if (!defer_) {
+        comm_->all_reduce_async(bk.flat, RedOp::SUM, (int)next_launch_);
+        if (join_each_) comm_->wait((int)next_launch_, nullptr);
+      }
       bk.launched = true;
       ++next_launch_;
     }
@@ -345,6 +379,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   bool on_cuda_ = false;
   bool hooks_ready_ = false;
   std::vector<std::weak_ptr<torch::autograd::Node>> hooked_;
+  bool defer_ = false, deferred_ = false;  // see set_defer
   bool join_each_ = false;  // join every bucket immediately (no overlap)
   bool zero_copy_ = true;   // reduce tiled gradient regions in place (DPA_REDUCER_ZERO_COPY=0: always pack)
   std::vector<int64_t> order_;
@@ -370,7 +405,11 @@ void register_reducer(pybind11::module& m) {
       .def("num_buckets", &ddp::Reducer::num_buckets)
       .def("bucket_tensors", &ddp::Reducer::bucket_tensors)
       .def("bucket_indices", &ddp::Reducer::bucket_indices)
-      .def("set_record_order", &ddp::Reducer::set_record_order);
+      .def("set_record_order", &ddp::Reducer::set_record_order)
+      .def("set_defer", &ddp::Reducer::set_defer)
+      .def("deferred_pending", &ddp::Reducer::deferred_pending)
+      .def("consume_deferred", &ddp::Reducer::consume_deferred)
+      .def("flush_deferred", &ddp::Reducer::flush_deferred);
 }
 
 }  // namespace dpa

@@ -11,6 +11,7 @@
 // reference call sites: /root/reference/ddp_main.py:91-93 (scaler.scale/step/update),
 // origin_main.py:87 (SGD lr=1e-4).
 #include "common.h"
+#include "comm/xgmi.h"
 
 #include <vector>
 
@@ -148,10 +149,21 @@ constexpr int64_t FUSED_MAX = (int64_t)FUSED_MAX_BLOCKS * FUSED_BLOCK_GRAN * 4;
 // host), so a granule never straddles two tensors.  Tensor tables live in LDS
 // (per-lane dynamic indexing of the by-value kernel argument is a chain of
 // dependent scalar loads).
+//
+// XG (DDP over the xGMI engine, DistributedDataParallel.defer_grad_sync_to):
+// the gradient all-reduce is fused in as well.  Each lane pushes its local
+// gradient granules to every peer as {value, epoch} granules (the one-shot
+// protocol of comm/xgmi_allreduce.hip, epoch from comm/xsite.h tickets), then
+// sums the W ranks' values in rank order and divides by W before the inf check
+// -- the reducer launched no collective for these buckets.  U = 1 granule per
+// lane then (one poll round trip of W x 4 granules per lane, 4x the workgroups).
+template <int U, bool XG>
 __global__ void __launch_bounds__(FUSED_THR)
 amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ tracker, float* __restrict__ found_inf,
                      unsigned long long* __restrict__ sync, float lr, float momentum, float dampening, float wd,
-                     int nesterov, int maximize, int first, float growth, float backoff, int interval) {
+                     int nesterov, int maximize, int first, float growth, float backoff, int interval,
+                     xgmi::XSite xg) {
+  constexpr int BG = FUSED_THR * U;  // float4 granules per workgroup
   __shared__ int soff[MAXT + 1];
   __shared__ int snum[MAXT];
   __shared__ float* sp0[MAXT];
@@ -173,6 +185,8 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
   // barrier, its load stays in flight (no LDS round trip) with the gradients'
   unsigned long long gen = 0;
   if (tid == 0) gen = __hip_atomic_fetch_add(&sync[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long tk = 0;
+  if (XG && tid == 0) tk = xgmi::xsite_ticket(xg);
   auto load4 = [](const float* p, int rem) {
     if (rem >= 4) return *reinterpret_cast<const f32x4*>(p);
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -184,12 +198,12 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
     for (int j = 0; j < rem; ++j) p[j] = v[j];
   };
   const bool use_buf = momentum != 0.f && !first;
-  f32x4 gv[FUSED_U], pv[FUSED_U], bv[FUSED_U];
-  int tt[FUSED_U], oo[FUSED_U];
+  f32x4 gv[U], pv[U], bv[U];
+  int tt[U], oo[U];
   bool bad = false;
 #pragma unroll
-  for (int k = 0; k < FUSED_U; ++k) {
-    const int gi = blockIdx.x * FUSED_BLOCK_GRAN + k * FUSED_THR + tid;
+  for (int k = 0; k < U; ++k) {
+    const int gi = blockIdx.x * BG + k * FUSED_THR + tid;
     tt[k] = -1;
     if (gi < total) {
       int lo = 0, hi = n - 1;  // tensor holding granule gi
@@ -203,10 +217,66 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
       gv[k] = load4(sp1[lo] + o, rem);
       pv[k] = load4(sp0[lo] + o, rem);
       bv[k] = use_buf ? load4(sp2[lo] + o, rem) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bad |= !isfinite(gv[k][j]);
     }
   }
+  if constexpr (XG) {
+    __shared__ uint32_t ep_x;
+    if (tid == 0) ep_x = xgmi::xsite_epoch(xg, tk);
+    __syncthreads();
+    const uint32_t ep = ep_x;
+    const long long par = (long long)(ep & 1u) * xgmi::kMaxRanks * xg.slot_bytes;
+    auto gran = [ep](float v) { return ((unsigned long long)ep << 32) | (unsigned long long)__float_as_uint(v); };
+    typedef __attribute__((ext_vector_type(2))) unsigned long long u64x2;
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      if (tt[k] < 0) continue;
+      const long long fo = (long long)(blockIdx.x * BG + k * FUSED_THR + tid) * 32;  // 4 granules of 8 B
+      const u64x2 a = {gran(gv[k][0]), gran(gv[k][1])}, b = {gran(gv[k][2]), gran(gv[k][3])};
+      for (int p = 0; p < xg.world; ++p) {
+        if (p == xg.rank) continue;  // my own values stay in registers
+        u64x2* dst = reinterpret_cast<u64x2*>(xg.base[p] + par + (long long)xg.rank * xg.slot_bytes + fo);
+        dst[0] = a;
+        dst[1] = b;
+      }
+    }
+    const float invw = 1.f / (float)xg.world;
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    unsigned polls = 0;
+    bool fail = false;
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      if (tt[k] < 0) continue;
+      const long long fo = (long long)(blockIdx.x * BG + k * FUSED_THR + tid) * 32;
+      unsigned long long g[xgmi::kMaxRanks][4];
+      const unsigned long long* src[xgmi::kMaxRanks];
+#pragma unroll
+      for (int p = 0; p < xgmi::kMaxRanks; ++p) {  // every load issued before the first tag check
+        src[p] = reinterpret_cast<const unsigned long long*>(xg.base[xg.rank] + par + (long long)p * xg.slot_bytes +
+                                                             fo);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          g[p][j] = (p < xg.world && p != xg.rank)
+                        ? __hip_atomic_load(src[p] + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                        : 0ull;
+      }
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int p = 0; p < xgmi::kMaxRanks; ++p) {
+        if (p >= xg.world) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float x = p == xg.rank ? gv[k][j] : xgmi::xsite_wait(xg, src[p] + j, g[p][j], ep, t0, polls, fail);
+          acc[j] = p == 0 ? x : acc[j] + x;
+        }
+      }
+      gv[k] = acc * invw;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < U; ++k)
+    if (tt[k] >= 0)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bad |= !isfinite(gv[k][j]);
   const bool block_bad = __syncthreads_or(bad);
   if (tid == 0) {
     unsigned long long* word = &sync[1 + (gen & 1)];
@@ -227,7 +297,7 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
   const bool any_bad = s_bad;
   const float inv = 1.f / scale[0];
 #pragma unroll
-  for (int k = 0; k < FUSED_U; ++k) {
+  for (int k = 0; k < U; ++k) {
     const int t = tt[k];
     if (t < 0) continue;
     const int o = oo[k], rem = snum[t] - o;
@@ -339,10 +409,13 @@ void sgd_step(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std
   });
 }
 
+// elements the fused AMP-SGD kernel can exchange in one launch (U = 1 granule per lane)
+int64_t amp_sgd_xg_max() { return (int64_t)FUSED_MAX_BLOCKS * FUSED_THR * 4; }
+
 void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std::vector<at::Tensor> bufs,
                    double lr, double momentum, double dampening, double wd, bool nesterov, bool maximize, bool first,
                    at::Tensor scale, at::Tensor tracker, at::Tensor found_inf, double growth, double backoff,
-                   int64_t interval, at::Tensor sync) {
+                   int64_t interval, at::Tensor sync, std::shared_ptr<xgmi::XgmiComm> xc) {
   TORCH_CHECK(params.size() == grads.size() && params.size() <= (size_t)MAXT, "fused AMP-SGD: <= ", MAXT,
               " tensors");
   TORCH_CHECK(bufs.empty() || bufs.size() == params.size());
@@ -366,12 +439,23 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
     TORCH_CHECK(al(L.p0[i]) && al(L.p1[i]) && al(L.p2[i]), "fused AMP-SGD needs 16-byte aligned tensors");
   }
   TORCH_CHECK(L.chunk_off[L.n] * 4 <= FUSED_MAX, "fused AMP-SGD handles at most ", FUSED_MAX, " elements");
-  const int grid = (int)std::max<int64_t>(1, (L.chunk_off[L.n] + FUSED_BLOCK_GRAN - 1) / FUSED_BLOCK_GRAN);
-  hipLaunchKernelGGL(amp_sgd_fused_kernel, dim3(grid), dim3(FUSED_THR), 0, cur_stream(), L, scale.data_ptr<float>(),
-                     tracker.data_ptr<int>(), found_inf.data_ptr<float>(),
-                     reinterpret_cast<unsigned long long*>(sync.data_ptr<int64_t>()), (float)lr, (float)momentum,
-                     (float)dampening, (float)wd, (int)nesterov, (int)maximize, (int)first, (float)growth,
-                     (float)backoff, (int)interval);
+  auto launch = [&](auto kern, int bg, xgmi::XSite xg) {
+    const int grid = (int)std::max<int64_t>(1, (L.chunk_off[L.n] + bg - 1) / bg);
+    TORCH_CHECK(grid <= FUSED_MAX_BLOCKS, "fused AMP-SGD: grid exceeds the co-resident bound");
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(FUSED_THR), 0, cur_stream(), L, scale.data_ptr<float>(),
+                       tracker.data_ptr<int>(), found_inf.data_ptr<float>(),
+                       reinterpret_cast<unsigned long long*>(sync.data_ptr<int64_t>()), (float)lr, (float)momentum,
+                       (float)dampening, (float)wd, (int)nesterov, (int)maximize, (int)first, (float)growth,
+                       (float)backoff, (int)interval, xg);
+  };
+  if (xc) {
+    const xgmi::XSite xg = xc->grad_site();
+    TORCH_CHECK(L.chunk_off[L.n] * 4 <= std::min<int64_t>(xg.max_vals, amp_sgd_xg_max()),
+                "fused AMP-SGD gradient exchange: too many elements for the xGMI engine");
+    launch(amp_sgd_fused_kernel<1, true>, FUSED_THR, xg);
+  } else {
+    launch(amp_sgd_fused_kernel<FUSED_U, false>, FUSED_BLOCK_GRAN, xgmi::XSite{});
+  }
   DPA_CHECK_LAUNCH();
 }
 
@@ -421,6 +505,7 @@ void register_optim(pybind11::module& m) {
         pybind11::arg("found_inf") = pybind11::none(), pybind11::arg("grad_scale") = pybind11::none());
   s.def("update_scale", &opt::update_scale);
   s.def("amp_sgd_fused", &opt::amp_sgd_fused);
+  s.def("amp_sgd_xg_max", &opt::amp_sgd_xg_max);
   s.attr("FUSED_MAX") = opt::FUSED_MAX;
   s.attr("MAXT") = opt::MAXT;
   s.def("flat_copy", &opt::flat_copy);

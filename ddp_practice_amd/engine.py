@@ -78,6 +78,10 @@ class TrainLoop:
         self.graph_error = None
         self.watchdog = watchdog  # utils.Watchdog: ticked after every chunk of steps
         self.faults = faults if faults else None  # utils.FaultInjector (DPA_FAULT)
+        # DDP + fused AMP step: the optimizer kernel averages the gradients over xGMI
+        # (parallel/ddp.py defer_grad_sync_to; a no-op without the engine)
+        if scaler is not None and getattr(scaler, "_enabled", False) and hasattr(model, "defer_grad_sync_to"):
+            model.defer_grad_sync_to(optimizer)
         self.global_step = 0
 
     # -- one step on the static buffers (what gets captured)

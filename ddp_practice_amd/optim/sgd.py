@@ -32,8 +32,15 @@ class SGD(Optimizer):
                         nesterov=nesterov, maximize=maximize)
         super().__init__(params, defaults)
 
+    def _flush_deferred(self):
+        """Average gradients a DDP reducer left to this optimizer (DDP.defer_grad_sync_to)."""
+        d = getattr(self, "_deferred_ddp", None)
+        if d is not None:
+            d[0].flush_deferred()
+
     @torch.no_grad()
     def step(self, closure=None, found_inf: torch.Tensor | None = None):
+        self._flush_deferred()
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -113,9 +120,14 @@ class SGD(Optimizer):
             # grid-barrier state of the fused kernel (allocated before any graph capture:
             # the first step runs eagerly)
             sync = self._amp_sync = torch.zeros(3, dtype=torch.int64, device=params[0].device)
+        # gradients a DDP reducer deferred to this step are averaged inside the kernel
+        d = getattr(self, "_deferred_ddp", None)
+        xc = d[1] if d is not None and d[0].deferred_pending() else None
         _load_ext().optim.amp_sgd_fused(params, grads, bufs, group["lr"], group["momentum"], group["dampening"],
                                         group["weight_decay"], group["nesterov"], group["maximize"], first,
-                                        scale, tracker, found_inf, growth, backoff, interval, sync)
+                                        scale, tracker, found_inf, growth, backoff, interval, sync, xc)
+        if xc is not None:
+            d[0].consume_deferred()
 
     @staticmethod
     def _torch_step(group, params, grads, bufs, first):

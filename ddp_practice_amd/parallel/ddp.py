@@ -23,6 +23,7 @@ in backward.  Default cap 32 MiB (HBM is 288 GB, memory is not the limit).
 from __future__ import annotations
 
 import contextlib
+import os
 import warnings
 
 import torch
@@ -176,6 +177,38 @@ class DistributedDataParallel(nn.Module):
             yield
         finally:
             self._sync_enabled = old
+
+    # ------------------------------------------------ deferred grad averaging
+    def defer_grad_sync_to(self, optimizer) -> bool:
+        """Opt-in: let ``optimizer`` average the gradients instead of the reducer.
+
+        At the end of backward the buckets are left holding this rank's
+        gradients.  The fused AMP-SGD step (optim/sgd.py, GradScaler fast path)
+        then exchanges them with the peers inside its own kernel over the xGMI
+        engine (csrc/kernels/optim.hip, XG variant): no all-reduce launch.  Any
+        other gradient consumer of ``optimizer`` (``step()``, ``GradScaler.unscale_``)
+        first runs the bucket all-reduces (``reducer.flush_deferred``), so results
+        never change, only the launch count.  ``.grad`` read directly between
+        ``backward()`` and the optimizer step is therefore rank-local.
+
+        Enabled only when the communicator has the xGMI engine, every optimizer
+        parameter belongs to this module, and the gradients fit one exchange.
+        ``DPA_FUSED_GRAD=0`` disables it.  Returns whether it was enabled.
+        """
+        if os.environ.get("DPA_FUSED_GRAD", "1") == "0" or self.reducer is None:
+            return False
+        xc = getattr(self.comm, "xgmi", None)
+        if xc is None or not hasattr(optimizer, "fused_amp_step"):
+            return False
+        opt_params = [p for g in optimizer.param_groups for p in g["params"]]
+        if {id(p) for p in opt_params} != {id(p) for p in self._params}:
+            return False
+        n = sum(p.numel() for p in self._params)
+        if n > min(int(xc.max_bytes) // 4, int(_load_ext().optim.amp_sgd_xg_max())):
+            return False
+        self.reducer.set_defer(True)
+        optimizer._deferred_ddp = (self.reducer, xc)
+        return True
 
     # -------------------------------------------------------------- utilities
     def bucket_sizes_bytes(self) -> list[int]:
