@@ -48,3 +48,7 @@ def test_bucket_assignment_matches_torch(shapes):
     ours = compute_bucket_assignment(params, cap, first)
     ref = _torch_buckets(params, first, cap)
     assert sorted(map(sorted, ours)) == sorted(map(sorted, ref))
+
+
+def test_ddp_deferred_grad_sync_flush():
+    assert run(W.ddp_deferred_flush, world=2) == [True, True]
