@@ -234,7 +234,7 @@ def test_fused_amp_sgd_matches_unfused(C, momentum, sizes):
 
     def fused(first):
         C.optim.amp_sgd_fused(pa, ga, ba, 0.1, momentum, 0.0, 1e-4, False, False, first, sa, ta, fa, 2.0, 0.5, 2,
-                              sync)
+                              sync, None)
 
     graph = None
     for it in range(8):
