@@ -210,14 +210,14 @@ def bench_resnet(args):
     from ddp_practice_amd.parallel import DistributedDataParallel, convert_sync_batchnorm
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank = 0 if args.share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist_path = world > 1 or args.force_collectives
     if args.force_collectives:
         _force_collectives()
     if dist_path:
-        ddist.init_process_group(backend="nccl")
+        ddist.init_process_group(backend="xgmi" if args.share_gpu else "nccl")
     rank = ddist.get_rank()
     amp = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": None}[args.amp_dtype]
     bs = args.batch_size if args.batch_size != 32 else 128
@@ -280,7 +280,8 @@ def bench_resnet(args):
             "config": {"model": "ResNet-50 (25,557,032 params)", "global_batch": bs * world, "seq_len": None,
                        "parallelism": f"dp{world}", "per_rank_batch": bs, "impl": args.resnet_impl,
                        "sync_bn": dist_path and not args.no_sync_bn, "optimizer": "SGD(lr=1e-4)",
-                       "comm": _comm_desc() if dist_path else "none", "hipgraph": bool(captured)},
+                       "comm": _comm_desc() if dist_path else "none", "hipgraph": bool(captured),
+                       "shared_gpu": bool(args.share_gpu)},
         }), flush=True)
     ddist.destroy_process_group()
 

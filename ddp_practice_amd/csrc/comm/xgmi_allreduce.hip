@@ -379,7 +379,7 @@ class XgmiCollective : public Collective {
     const int i = next_++ % kRing;
     DPA_CHECK_HIP(hipEventRecord(fork_[i], cur_stream()));
     DPA_CHECK_HIP(hipStreamWaitEvent(stream_.stream(), fork_[i], 0));
-    x_->all_reduce(t, t, op, stream_.stream());
+    chunked(t, t, op);
     DPA_CHECK_HIP(hipEventRecord(slot_[slot], stream_.stream()));
   }
   void wait(int slot, hipStream_t stream) override {
@@ -393,7 +393,7 @@ class XgmiCollective : public Collective {
     const int i = next_++ % kRing;
     DPA_CHECK_HIP(hipEventRecord(fork_[i], cur));
     DPA_CHECK_HIP(hipStreamWaitEvent(stream_.stream(), fork_[i], 0));
-    x_->all_reduce(in, out, op, stream_.stream());
+    chunked(in, out, op);
     DPA_CHECK_HIP(hipEventRecord(join_[i], stream_.stream()));
     DPA_CHECK_HIP(hipStreamWaitEvent(cur, join_[i], 0));
   }
@@ -401,6 +401,24 @@ class XgmiCollective : public Collective {
   void abort_now() override { x_->abort(); }
 
  private:
+  // Tensors larger than the workspace slot (ResNet-50 DDP buckets) go as back-to-back
+  // one-shot launches over slot-sized views; max_elems() is a multiple of kChunkElems,
+  // so every view keeps the 16-B alignment of the base pointer.
+  void chunked(const at::Tensor& in, const at::Tensor& out, RedOp op) {
+    const int64_t n = in.numel(), m = x_->max_elems();
+    if (n <= m) {
+      x_->all_reduce(in, out, op, stream_.stream());
+      return;
+    }
+    TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && out.numel() == n,
+                "xgmi all_reduce: chunked path needs contiguous same-size tensors");
+    const auto fi = in.view(-1), fo = out.view(-1);
+    for (int64_t o = 0; o < n; o += m) {
+      const int64_t k = std::min(m, n - o);
+      x_->all_reduce(fi.narrow(0, o, k), fo.narrow(0, o, k), op, stream_.stream());
+    }
+  }
+
   static constexpr int kSlots = 256, kRing = 64;
   std::shared_ptr<xgmi::XgmiComm> x_;
   c10::hip::HIPStream stream_;

@@ -86,6 +86,18 @@ def worker(rank, world, port, mode, q):
             it += 1
         torch.cuda.synchronize()
         assert x.error() == 0, x.error_string()
+        # tensors larger than the workspace slot (1 MiB here): XgmiCollective splits them
+        # into back-to-back slot-sized launches (ResNet-50-sized DDP buckets)
+        xc = C.xgmi.XgmiCollective(x)
+        for n, dn, op in ((700001, "f32", "sum"), (600000, "bf16", "avg"), (524288, "f32", "max")):
+            dt = DTYPES[dn]
+            t = _data(rank, n, dt, it).to(dev)
+            xc.all_reduce(t, op)
+            torch.cuda.synchronize()
+            assert x.error() == 0, x.error_string()
+            _check(t, _expect(world, n, dt, it, op), dt, ("chunked", n, dn, op))
+            out[f"chunked{n}{dn}{op}"] = t.float().cpu().numpy().tobytes()
+            it += 1
         # hipGraph: capture two collectives, replay with fresh inputs each time
         a = torch.zeros(4099, device=dev)
         b = torch.zeros(70000, device=dev)
