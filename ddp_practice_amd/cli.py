@@ -26,6 +26,7 @@ from __future__ import annotations
 import json
 import os
 import sys
+import threading
 import time
 
 
@@ -122,6 +123,22 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
     from ddp_practice_amd.utils import FaultInjector, Watchdog, set_tracing, trace_range
 
     phase("imports")
+    # The datasets (IDX read or synthetic generation, numpy: releases the GIL in its bulk
+    # ops) are built on a side thread while this one brings up the HIP context, the native
+    # extension and the model; joined before the loaders need them.
+    ds_box: dict = {}
+
+    def _build_datasets():
+        try:
+            ds_box["train"] = MNIST(root=args.data_root, train=True, force_synthetic=args.synthetic,
+                                    n=args.train_samples)
+            ds_box["test"] = MNIST(root=args.data_root, train=False, force_synthetic=args.synthetic,
+                                   n=args.test_samples)
+        except BaseException as e:  # re-raised on the main thread
+            ds_box["error"] = e
+
+    ds_thread = threading.Thread(target=_build_datasets, name="dpa-datasets", daemon=True)
+    ds_thread.start()
     if args.profile:
         set_tracing(True)
     if args.seed is not None:
@@ -149,8 +166,10 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
     phase("model")
 
     act_dtype = amp if (amp is not None and gpu) else torch.float32
-    train_dataset = MNIST(root=args.data_root, train=True, force_synthetic=args.synthetic, n=args.train_samples)
-    test_dataset = MNIST(root=args.data_root, train=False, force_synthetic=args.synthetic, n=args.test_samples)
+    ds_thread.join()
+    if "error" in ds_box:
+        raise ds_box["error"]
+    train_dataset, test_dataset = ds_box["train"], ds_box["test"]
     if distributed:
         g = torch.Generator()
         g.manual_seed(generator_seed if generator_seed is not None else 3407 + rank)
