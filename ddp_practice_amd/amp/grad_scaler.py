@@ -54,6 +54,31 @@ def _native_ok(t: torch.Tensor) -> bool:
     return t.is_cuda
 
 
+
+def _seeded_backward(t: torch.Tensor, seed: torch.Tensor, retain_graph, inputs) -> None:
+    """``torch.autograd.backward(t, grad_tensors=seed)`` for a 0-d ``t`` and a 0-d floating
+    seed on its device, straight into the autograd engine (which casts the seed to ``t``'s
+    dtype, as torch's own path does).
+
+    torch's ``_make_grads`` only validates the seed's shape here, and doing so imports
+    ``torch.fx.experimental.symbolic_shapes`` (sympy) on first use: 1.35 s of the first
+    training step on a fresh box (measured with cProfile, ``scripts/prof_cli_ddp.sh``).
+    """
+    run = getattr(torch.autograd.graph, "_engine_run_backward", None)
+    if (run is None or seed.shape != t.shape or seed.device != t.device or not seed.is_floating_point()
+            or not t.is_floating_point()):
+        torch.autograd.backward(t, grad_tensors=seed, retain_graph=retain_graph, inputs=inputs)
+        return
+    if inputs is None:
+        inputs_t = ()
+    elif isinstance(inputs, (torch.Tensor, torch.autograd.graph.GradientEdge)):
+        inputs_t = (inputs,)
+    else:
+        inputs_t = tuple(inputs)
+        if not inputs_t:
+            raise RuntimeError("`inputs` argument to `backward()` cannot be empty.")
+    run((t,), (seed,), bool(retain_graph), False, inputs_t, allow_unreachable=True, accumulate_grad=True)
+
 class GradScaler:
     def __init__(self, device: str = "cuda", init_scale: float = 2.0 ** 16, growth_factor: float = 2.0,
                  backoff_factor: float = 0.5, growth_interval: int = 2000, enabled: bool = True,
@@ -127,7 +152,7 @@ class GradScaler:
                     if gradient is None and not create_graph:
                         node.token.seeded = True
                         try:
-                            torch.autograd.backward(base, grad_tensors=s0, retain_graph=retain_graph, inputs=inputs)
+                            _seeded_backward(base, s0, retain_graph, inputs)
                         finally:
                             node.token.seeded = False
                     else:
@@ -147,7 +172,7 @@ class GradScaler:
 
                 def _backward(gradient=None, retain_graph=None, create_graph=False, inputs=None):
                     if gradient is None and not create_graph:
-                        torch.autograd.backward(base, grad_tensors=seed, retain_graph=retain_graph, inputs=inputs)
+                        _seeded_backward(base, seed, retain_graph, inputs)
                     else:
                         torch.Tensor.backward(scaled, gradient, retain_graph, create_graph, inputs)
 

@@ -105,6 +105,9 @@ _T0 = time.perf_counter()
 def phase(name: str) -> None:
     """``DPA_PHASES=1``: print the time since this module was imported at each run phase (stderr)."""
     if os.environ.get("DPA_PHASES") == "1":
+        torch = sys.modules.get("torch")
+        if torch is not None and torch.cuda.is_initialized():
+            torch.cuda.synchronize()  # the mark covers the GPU work queued before it
         print(f"[phase pid={os.getpid()}] {name} +{time.perf_counter() - _T0:.3f}s", file=sys.stderr, flush=True)
 
 

@@ -24,10 +24,10 @@ def rccl(C):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1",
                       LOCAL_RANK="0")
     torch.cuda.set_device(0)
+    old = comm_mod.Communicator.force_active
+    comm_mod.Communicator.force_active = True  # W=1 without it gets the LocalCommunicator
     c = dist.init_process_group("nccl")
     assert isinstance(c, comm_mod.RcclCommunicator)
-    old = comm_mod.Communicator.force_active
-    comm_mod.Communicator.force_active = True
     yield c
     comm_mod.Communicator.force_active = old
     dist.destroy_process_group()
