@@ -91,3 +91,63 @@ def test_autocast_policy():
     with pytest.raises(ValueError):
         with autocast(dtype=torch.float32):
             pass
+
+
+def test_seeded_backward_matches_autograd_backward():
+    """GradScaler's engine-direct seeded backward == torch.autograd.backward(t, seed):
+    same grads, `inputs=` restricts accumulation, retain_graph allows a second pass,
+    a seed of another floating dtype is cast like torch does."""
+    from ddp_practice_amd.amp.grad_scaler import _seeded_backward
+
+    torch.manual_seed(0)
+    w = torch.randn(5, 3, requires_grad=True)
+    b = torch.randn(3, requires_grad=True)
+    x = torch.randn(4, 5)
+
+    def loss():
+        return ((x @ w + b).relu() ** 2).mean()
+
+    seed = torch.tensor(512.0)
+    torch.autograd.backward(loss(), grad_tensors=seed)
+    gw, gb = w.grad.clone(), b.grad.clone()
+    w.grad = b.grad = None
+    _seeded_backward(loss(), seed, None, None)
+    assert torch.equal(w.grad, gw) and torch.equal(b.grad, gb)
+    w.grad = b.grad = None
+    _seeded_backward(loss(), seed, None, [b])
+    assert w.grad is None and torch.equal(b.grad, gb)
+    b.grad = None
+    lv = loss()
+    _seeded_backward(lv, seed, True, None)
+    _seeded_backward(lv, seed, None, None)
+    assert torch.allclose(w.grad, 2 * gw)
+    w.grad = b.grad = None
+    lh = loss().to(torch.float64)
+    _seeded_backward(lh, seed, None, None)  # fp32 seed into an fp64 output
+    assert torch.allclose(w.grad, gw)
+    with pytest.raises(RuntimeError):
+        _seeded_backward(loss(), seed, None, [])
+
+
+def test_optimizer_and_scaler_do_not_import_dynamo_or_sympy():
+    """SGD construction/zero_grad/state_dict and a scaled backward stay clear of the lazy
+    torch._dynamo / sympy imports (~2.5 s on a fresh box), checked in a fresh interpreter."""
+    import subprocess
+    import sys
+
+    code = (
+        "import sys, torch\n"
+        "from ddp_practice_amd.optim import SGD\n"
+        "from ddp_practice_amd.amp.grad_scaler import _seeded_backward\n"
+        "p = torch.nn.Parameter(torch.randn(4))\n"
+        "o = SGD([p], lr=0.1)\n"
+        "_seeded_backward((p * p).sum(), torch.tensor(2.0), None, None)\n"
+        "o.step(); o.zero_grad(); o.load_state_dict(o.state_dict())\n"
+        "bad = [m for m in ('torch._dynamo', 'sympy') if m in sys.modules]\n"
+        "assert not bad, bad\n"
+    )
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
