@@ -143,6 +143,9 @@ constexpr int FUSED_U = 4;                                  // float4 granules p
 constexpr int FUSED_BLOCK_GRAN = FUSED_THR * FUSED_U;       // 4096 floats per workgroup
 constexpr int FUSED_MAX_BLOCKS = 128;
 constexpr int64_t FUSED_MAX = (int64_t)FUSED_MAX_BLOCKS * FUSED_BLOCK_GRAN * 4;
+// (A one-workgroup variant of 1024 lanes x 8 granules for the ConvNet measured 10.9 us
+// vs 8.6 us for 8 workgroups + grid barrier: one CU's bandwidth is the limit, not the
+// barrier.  A grid of one still skips the barrier, below.)
 
 // The flat index space is in float4 granules; tensor t owns ceil(numel/4)
 // granules starting at chunk_off[t] (every pointer 16-B aligned, checked on the
@@ -157,13 +160,13 @@ constexpr int64_t FUSED_MAX = (int64_t)FUSED_MAX_BLOCKS * FUSED_BLOCK_GRAN * 4;
 // sums the W ranks' values in rank order and divides by W before the inf check
 // -- the reducer launched no collective for these buckets.  U = 1 granule per
 // lane then (one poll round trip of W x 4 granules per lane, 4x the workgroups).
-template <int U, bool XG>
-__global__ void __launch_bounds__(FUSED_THR)
+template <int U, bool XG, int THR = FUSED_THR>
+__global__ void __launch_bounds__(THR)
 amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ tracker, float* __restrict__ found_inf,
                      unsigned long long* __restrict__ sync, float lr, float momentum, float dampening, float wd,
                      int nesterov, int maximize, int first, float growth, float backoff, int interval,
                      xgmi::XSite xg) {
-  constexpr int BG = FUSED_THR * U;  // float4 granules per workgroup
+  constexpr int BG = THR * U;  // float4 granules per workgroup
   __shared__ int soff[MAXT + 1];
   __shared__ int snum[MAXT];
   __shared__ float* sp0[MAXT];
@@ -184,7 +187,8 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
   // the barrier generation is only used by lane 0: issued after the table
   // barrier, its load stays in flight (no LDS round trip) with the gradients'
   unsigned long long gen = 0;
-  if (tid == 0) gen = __hip_atomic_fetch_add(&sync[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0 && gridDim.x > 1)
+    gen = __hip_atomic_fetch_add(&sync[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   unsigned long long tk = 0;
   if (XG && tid == 0) tk = xgmi::xsite_ticket(xg);
   auto load4 = [](const float* p, int rem) {
@@ -199,11 +203,11 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
   };
   const bool use_buf = momentum != 0.f && !first;
   f32x4 gv[U], pv[U], bv[U];
-  int tt[U], oo[U];
+  int tt[U];  // tensor of each granule (its offset is recomputed after the barrier)
   bool bad = false;
 #pragma unroll
   for (int k = 0; k < U; ++k) {
-    const int gi = blockIdx.x * BG + k * FUSED_THR + tid;
+    const int gi = blockIdx.x * BG + k * THR + tid;
     tt[k] = -1;
     if (gi < total) {
       int lo = 0, hi = n - 1;  // tensor holding granule gi
@@ -213,7 +217,6 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
       }
       const int o = (gi - soff[lo]) * 4, rem = snum[lo] - o;
       tt[k] = lo;
-      oo[k] = o;
       gv[k] = load4(sp1[lo] + o, rem);
       pv[k] = load4(sp0[lo] + o, rem);
       bv[k] = use_buf ? load4(sp2[lo] + o, rem) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -230,7 +233,7 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       if (tt[k] < 0) continue;
-      const long long fo = (long long)(blockIdx.x * BG + k * FUSED_THR + tid) * 32;  // 4 granules of 8 B
+      const long long fo = (long long)(blockIdx.x * BG + k * THR + tid) * 32;  // 4 granules of 8 B
       const u64x2 a = {gran(gv[k][0]), gran(gv[k][1])}, b = {gran(gv[k][2]), gran(gv[k][3])};
       for (int p = 0; p < xg.world; ++p) {
         if (p == xg.rank) continue;  // my own values stay in registers
@@ -246,7 +249,7 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       if (tt[k] < 0) continue;
-      const long long fo = (long long)(blockIdx.x * BG + k * FUSED_THR + tid) * 32;
+      const long long fo = (long long)(blockIdx.x * BG + k * THR + tid) * 32;
       unsigned long long g[xgmi::kMaxRanks][4];
       const unsigned long long* src[xgmi::kMaxRanks];
 #pragma unroll
@@ -277,8 +280,13 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
     if (tt[k] >= 0)
 #pragma unroll
       for (int j = 0; j < 4; ++j) bad |= !isfinite(gv[k][j]);
+  // scale read before arriving: block 0 rewrites it once everyone has arrived, and a
+  // workgroup that reads it late must not unscale with the next step's value
+  const float inv = 1.f / scale[0];
   const bool block_bad = __syncthreads_or(bad);
-  if (tid == 0) {
+  if (gridDim.x == 1) {  // uniform: one workgroup needs no grid barrier
+    if (tid == 0) s_bad = block_bad;
+  } else if (tid == 0) {
     unsigned long long* word = &sync[1 + (gen & 1)];
     const unsigned long long G = gridDim.x;
     __hip_atomic_fetch_add(word, 1ull | ((unsigned long long)block_bad << 32), __ATOMIC_RELAXED,
@@ -295,12 +303,11 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
   }
   __syncthreads();
   const bool any_bad = s_bad;
-  const float inv = 1.f / scale[0];
 #pragma unroll
   for (int k = 0; k < U; ++k) {
     const int t = tt[k];
     if (t < 0) continue;
-    const int o = oo[k], rem = snum[t] - o;
+    const int o = (blockIdx.x * BG + k * THR + tid - soff[t]) * 4, rem = snum[t] - o;
     const f32x4 g = gv[k] * inv;
     store4(sp1[t] + o, rem, g);
     if (any_bad) continue;
