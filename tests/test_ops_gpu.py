@@ -217,7 +217,8 @@ def test_gather(C, dtype):
 
 
 @pytest.mark.parametrize("momentum", [0.0, 0.9])
-@pytest.mark.parametrize("sizes", [(7, 3000, 29034), (5, 200001, 33), (7, 33, 100)])
+# granules per lane chosen by size: U=1, U=2, U=4, and a grid of one
+@pytest.mark.parametrize("sizes", [(7, 3000, 29034), (5, 200001, 33), (5, 300001, 33), (7, 33, 100)])
 def test_fused_amp_sgd_matches_unfused(C, momentum, sizes):
     """Grid-barrier fused unscale+check+SGD+update == the three unfused kernels, over
     several launches sharing one barrier state (generations / parity reuse), with
@@ -262,8 +263,9 @@ def test_fused_amp_sgd_matches_unfused(C, momentum, sizes):
             torch.testing.assert_close(x, y, equal_nan=True)
         assert sa.item() == sb.item() and ta.item() == tb.item() and fa.item() == fb.item() == 0.0, it
     # multi-workgroup grid: one barrier generation per launch (4 eager + 4 graph replays;
-    # capture runs nothing); a grid of one workgroup (<= 256 x 4 granules) skips the barrier
-    solo = sum((n + 3) // 4 for n in sizes) <= 256 * 4
+    # capture runs nothing); a grid of one workgroup (<= 256 lanes x 1 granule at the
+    # default granules-per-lane choice) skips the barrier
+    solo = sum((n + 3) // 4 for n in sizes) <= 256
     assert int(sync[0]) == (0 if solo else 8)
 
 
