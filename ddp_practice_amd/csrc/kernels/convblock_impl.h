@@ -1250,18 +1250,22 @@ slab_reduce_kernel(const float* __restrict__ slab1, int rows1, int n1, float* __
   float* out = first ? out1 : out2;
   const int c0 = (first ? blockIdx.x : blockIdx.x - nb1) * SR_COLS;
   const int col = c0 + (threadIdx.x % SR_COLS), g = threadIdx.x / SR_COLS;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  // 8 then 4 independent row loads in flight per round trip (conv2's 128 slab rows:
+  // one round trip per lane; conv1's 224: three)
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (col < n) {
     int rr = g;
-    for (; rr + 3 * SR_GROUPS < rows; rr += 4 * SR_GROUPS) {
-      a0 += slab[(size_t)rr * n + col];
-      a1 += slab[(size_t)(rr + SR_GROUPS) * n + col];
-      a2 += slab[(size_t)(rr + 2 * SR_GROUPS) * n + col];
-      a3 += slab[(size_t)(rr + 3 * SR_GROUPS) * n + col];
+    for (; rr + 7 * SR_GROUPS < rows; rr += 8 * SR_GROUPS) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += slab[(size_t)(rr + j * SR_GROUPS) * n + col];
     }
-    for (; rr < rows; rr += SR_GROUPS) a0 += slab[(size_t)rr * n + col];
+    for (; rr + 3 * SR_GROUPS < rows; rr += 4 * SR_GROUPS) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] += slab[(size_t)(rr + j * SR_GROUPS) * n + col];
+    }
+    for (; rr < rows; rr += SR_GROUPS) a[0] += slab[(size_t)rr * n + col];
   }
-  part[g][threadIdx.x % SR_COLS] = (a0 + a1) + (a2 + a3);
+  part[g][threadIdx.x % SR_COLS] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
   __syncthreads();
   if (threadIdx.x < SR_COLS && c0 + (int)threadIdx.x < n) {
     float t = 0.f;
