@@ -35,6 +35,9 @@ def prepare():
 
     add_run_args(parser, amp_default="fp16", checkpoint="ddp_checkpoint.pt", distributed=True)
     args = parser.parse_args()
+    from ddp_practice_amd.cli import apply_env
+
+    apply_env(args)
 
     # The following environment variables are set to enable DDP
     os.environ["MASTER_ADDR"] = os.environ.get("DPA_MASTER_ADDR", "localhost")

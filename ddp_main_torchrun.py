@@ -26,6 +26,9 @@ def prepare():
 
     add_run_args(parser, amp_default="fp16", checkpoint="ddp_checkpoint.pt", distributed=True)
     args = parser.parse_args()
+    from ddp_practice_amd.cli import apply_env
+
+    apply_env(args)
     from ddp_practice_amd.runtime.device import select_devices
 
     select_devices(args.gpu)  # specify the GPUs to use

@@ -13,7 +13,11 @@ Additive flags (all optional; defaults reproduce the reference):
   --synthetic / --data-root / --train-samples / --test-samples   data
   --amp-dtype {fp16,bf16,fp32}        precision (reference: fp32 origin, fp16 DDP)
   --no-graph                          run every step eagerly (no hipGraph replay)
-  --no-sync-bn / --bucket-cap-mb      DDP knobs
+  --no-sync-bn / --bucket-cap-mb / --first-bucket-mb   DDP knobs
+  --comm {auto,rccl,xgmi}             collective algorithm selection (parallel/comm.py)
+  --impl {native,torch}               torch = the same program on PyTorch's own modules,
+                                      autocast, GradScaler, SGD, SyncBatchNorm and DDP
+                                      (parity / same-node baseline runs)
   --seed N                            model-init seed
   --resume PATH [--start-epoch N]     load {"model"[, "scaler"]} before training
   --watchdog-timeout S                abort + exit when no progress for S seconds
@@ -45,9 +49,20 @@ def add_run_args(parser, amp_default: str, checkpoint: str, distributed: bool) -
                         help="seconds without progress before aborting (env DPA_WATCHDOG_TIMEOUT; 0 = off)")
     parser.add_argument("--profile", action="store_true", help="emit roctx ranges for rocprofv3 --marker-trace")
     parser.add_argument("--metrics-file", default=None, help="per-epoch JSONL metrics (rank 0)")
+    parser.add_argument("--impl", default="native", choices=["native", "torch"],
+                        help="torch: run the same program on PyTorch's own stack (parity / baseline)")
     if distributed:
         parser.add_argument("--no-sync-bn", action="store_true")
         parser.add_argument("--bucket-cap-mb", type=float, default=None)
+        parser.add_argument("--first-bucket-mb", type=float, default=None)
+        parser.add_argument("--comm", default=None, choices=["auto", "rccl", "xgmi"],
+                            help="collective algorithm: auto (size-selected xGMI engine / RCCL), rccl, xgmi")
+
+
+def apply_env(args) -> None:
+    """Flags that must reach every rank before ``init_process_group`` (spawned children inherit the env)."""
+    if getattr(args, "comm", None):
+        os.environ["DPA_COMM"] = args.comm
 
 
 def load_checkpoint(path: str, model, scaler=None) -> None:
@@ -153,19 +168,29 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
     comm = dist.default_comm() if distributed else None
     amp = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": None}[args.amp_dtype]
 
-    model = ConvNet(amp_dtype=amp).to(dev)  # autocast inside forward, as the reference
-    scaler = GradScaler(enabled=True) if amp is not None else None
+    native = getattr(args, "impl", "native") == "native"
+    # autocast inside forward, as the reference; fused=False: torch's own modules
+    model = ConvNet(amp_dtype=amp, fused=native).to(dev)
+    if native:
+        scaler = GradScaler(enabled=True) if amp is not None else None
+    else:
+        scaler = torch.amp.GradScaler(dev.type) if amp is not None else None
     if args.resume:
         load_checkpoint(args.resume, model, scaler)
-    if distributed:
+    if distributed and native:
         from ddp_practice_amd.parallel import DistributedDataParallel, convert_sync_batchnorm
 
         if not args.no_sync_bn:
             model = convert_sync_batchnorm(model)
         model = DistributedDataParallel(model, device_ids=[local_rank] if gpu else None,
-                                        bucket_cap_mb=args.bucket_cap_mb)
-    criterion = CrossEntropyLoss().to(dev)
-    optimizer = SGD(model.parameters(), 1e-4)
+                                        bucket_cap_mb=args.bucket_cap_mb, first_bucket_mb=args.first_bucket_mb)
+    elif distributed:
+        if not args.no_sync_bn and gpu:  # torch's SyncBatchNorm has no CPU path
+            model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
+        kw = {} if args.bucket_cap_mb is None else {"bucket_cap_mb": args.bucket_cap_mb}
+        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local_rank] if gpu else None, **kw)
+    criterion = (CrossEntropyLoss() if native else torch.nn.CrossEntropyLoss()).to(dev)
+    optimizer = SGD(model.parameters(), 1e-4) if native else torch.optim.SGD(model.parameters(), 1e-4)
     phase("model")
 
     act_dtype = amp if (amp is not None and gpu) else torch.float32
@@ -194,7 +219,7 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
         timeout = float(os.environ["DPA_WATCHDOG_TIMEOUT"])
     watchdog = Watchdog(comm, timeout=timeout, tag=f"rank{rank}") if timeout else None
     faults = FaultInjector(rank)
-    loop = TrainLoop(model, criterion, optimizer, train_dloader, scaler, use_graph=not args.no_graph,
+    loop = TrainLoop(model, criterion, optimizer, train_dloader, scaler, use_graph=native and not args.no_graph,
                      watchdog=watchdog, faults=faults)
     metrics = _Metrics(args.metrics_file, rank, world, dev)
     metrics.start()
@@ -212,7 +237,7 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
         if rank == 0:
             print("begin testing", flush=True)
         with trace_range("evaluate"):
-            correct, size = evaluate(model, test_dloader, comm=comm, dst=0)
+            correct, size = evaluate(model, test_dloader, comm=comm, dst=0, native=native)
         if watchdog is not None:
             watchdog.tick()
         phase("evaluate")

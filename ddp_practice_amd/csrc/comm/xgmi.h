@@ -33,6 +33,8 @@ class XgmiComm {
   // out may alias in; stream == nullptr: the caller's current stream
   void all_reduce(const at::Tensor& in, const at::Tensor& out, RedOp op, hipStream_t stream);
 
+  // test entry: `grid` workgroups exchange `in` through SyncBN site s (comm/xsite.h)
+  void site_probe(int s, const at::Tensor& in, const at::Tensor& out, int grid);
   int error() const;  // 0 ok, 1 a peer never arrived (timeout), 2 aborted
   std::string error_string() const;
   void abort();       // every waiting block gives up (watchdog path)

@@ -339,6 +339,32 @@ XSite XgmiComm::grad_site() const {
   return x;
 }
 
+// Test entry for the in-kernel exchange (comm/xsite.h): `grid` workgroups each
+// exchange the same n (<= kSiteVals) floats through site s and write the
+// rank-ordered global sums to out[block][n] -- the protocol every fused SyncBN
+// consumer runs in its prologue, isolated (numerics, epochs, parity reuse,
+// bounded waits).
+__global__ void __launch_bounds__(256) site_probe_kernel(XSite xs, const float* __restrict__ in,
+                                                         float* __restrict__ out, int n) {
+  __shared__ float vals[kSiteVals];
+  unsigned long long tk = 0;
+  if (threadIdx.x == 0) tk = xsite_ticket(xs);
+  if ((int)threadIdx.x < n) vals[threadIdx.x] = in[threadIdx.x];
+  __syncthreads();
+  xsite_exchange(xs, vals, n, tk, blockIdx.x == 0);
+  if ((int)threadIdx.x < n) out[(long long)blockIdx.x * n + threadIdx.x] = vals[threadIdx.x];
+}
+
+void XgmiComm::site_probe(int s, const at::Tensor& in, const at::Tensor& out, int grid) {
+  TORCH_CHECK(in.is_cuda() && in.scalar_type() == at::kFloat && in.is_contiguous() && in.numel() <= kSiteVals,
+              "site_probe: <= ", kSiteVals, " contiguous f32 values");
+  TORCH_CHECK(out.numel() == (int64_t)grid * in.numel() && out.scalar_type() == at::kFloat && grid >= 1);
+  TORCH_CHECK(s >= 0 && s < kSiteGrad, "site_probe: SyncBN site id");
+  hipLaunchKernelGGL(site_probe_kernel, dim3(grid), dim3(256), 0, cur_stream(), site(s), in.data_ptr<float>(),
+                     out.data_ptr<float>(), (int)in.numel());
+  DPA_CHECK_LAUNCH();
+}
+
 int XgmiComm::error() const { return host_words_ ? __atomic_load_n(&host_words_[0], __ATOMIC_ACQUIRE) : 0; }
 
 std::string XgmiComm::error_string() const {
@@ -458,6 +484,8 @@ void register_xgmi(pybind11::module& m) {
              return dst;
            },
            py::arg("t"), py::arg("op") = "sum", py::arg("out") = py::none())
+      .def("site_probe", &xgmi::XgmiComm::site_probe, py::arg("site"), py::arg("inp"), py::arg("out"),
+           py::arg("grid") = 1)
       .def("error", &xgmi::XgmiComm::error)
       .def("error_string", &xgmi::XgmiComm::error_string)
       .def("abort", &xgmi::XgmiComm::abort)

@@ -458,6 +458,26 @@ void conv_wgrad_bn(at::Tensor x, at::Tensor y, at::Tensor dp, at::Tensor idx, at
   DPA_CHECK_LAUNCH();
 }
 
+// Whether every launch that exchanges SyncBN sums in-kernel (comm/xsite.h: all
+// of its workgroups poll the peers' rows) is co-resident at batch B; if not,
+// ops/convnet_fused.py all-reduces between the launches instead.
+bool sites_resident(int64_t B, at::ScalarType st) {
+  bool ok = true;
+  auto chk = [&](const void* k, int64_t grid) { ok = ok && co_resident(k, (int)grid, cb::NTHR, 0); };
+  with_t(dt_of(at::empty({0}, at::TensorOptions().dtype(st))), [&](auto tag) {
+    typedef decltype(tag) T;
+    chk(reinterpret_cast<const void*>(&cb::conv5x5_kernel<T, 16, 32, 14, 14, 0, 1, 0, 1>), B * 2);
+    ok = ok && co_resident(reinterpret_cast<const void*>(&head_fwd_kernel<T, 32, 14, 14, 16>), (int)B, HF, 0) &&
+         co_resident(reinterpret_cast<const void*>(&head_fwd_kernel<T, 32, 14, 14, 64>), (int)B, HF, 0);
+    chk(reinterpret_cast<const void*>(&cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1, 1>), B * kDgradSplit);
+    chk(reinterpret_cast<const void*>(&cb::conv5x5_wgrad_kernel<T, 16, 32, 14, 14, WG2_ROWS, 2>),
+        wgrad_bn_rows(2, B));
+    chk(reinterpret_cast<const void*>(&cb::conv5x5_wgrad_kernel<T, 1, 16, 28, 28, WG1_ROWS, 2>),
+        wgrad_bn_rows(1, B));
+  });
+  return ok;
+}
+
 }  // namespace cnf
 
 void register_convnet_fused(pybind11::module& m) {
@@ -488,6 +508,7 @@ void register_convnet_fused(pybind11::module& m) {
   s.def("conv2_dgrad", &cnf::conv2_dgrad);
   s.def("conv_wgrad_bn", &cnf::conv_wgrad_bn);
   s.def("wgrad_bn_rows", &cnf::wgrad_bn_rows);
+  s.def("sites_resident", &cnf::sites_resident);
 }
 
 }  // namespace dpa

@@ -25,6 +25,7 @@ constexpr int CHUNK = 4096;
 
 struct MTList {
   int n;
+  unsigned long long first_bits;  // momentum: bit t set = tensor t's buffer is new (b = d)
   int64_t numel[MAXT];
   int64_t chunk_off[MAXT + 1];  // prefix sum of chunks
   float* p0[MAXT];
@@ -67,7 +68,7 @@ unscale_check_kernel(MTList L, const float* __restrict__ scale, float* __restric
 // p0 = param, p1 = grad, p2 = momentum buffer (may be null)
 __global__ void __launch_bounds__(NTHR)
 sgd_kernel(MTList L, float lr, float momentum, float dampening, float wd, int nesterov, int maximize,
-           int first, const float* __restrict__ found_inf, const float* __restrict__ grad_scale) {
+           const float* __restrict__ found_inf, const float* __restrict__ grad_scale) {
   if (found_inf != nullptr && found_inf[0] != 0.f) return;
   const float gs = grad_scale ? 1.f / grad_scale[0] : 1.f;
   const int64_t total = L.chunk_off[L.n];
@@ -78,6 +79,7 @@ sgd_kernel(MTList L, float lr, float momentum, float dampening, float wd, int ne
     float* p = L.p0[t];
     const float* g = L.p1[t];
     float* buf = L.p2[t];
+    const bool first = (L.first_bits >> t) & 1ull;
     float gv[CHUNK / NTHR], pv[CHUNK / NTHR], bv0[CHUNK / NTHR];
 #pragma unroll
     for (int k = 0; k < CHUNK / NTHR; ++k) {
@@ -165,8 +167,8 @@ template <int U, bool XG, int THR = FUSED_THR>
 __global__ void __launch_bounds__(THR)
 amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ tracker, float* __restrict__ found_inf,
                      unsigned long long* __restrict__ sync, float lr, float momentum, float dampening, float wd,
-                     int nesterov, int maximize, int first, float growth, float backoff, int interval,
-                     xgmi::XSite xg) {
+                     int nesterov, int maximize, float growth, float backoff, int interval,
+                     xgmi::XSite xg, int* __restrict__ err, long long barrier_ticks) {
   constexpr int BG = THR * U;  // float4 granules per workgroup
   __shared__ int soff[MAXT + 1];
   __shared__ int snum[MAXT];
@@ -202,7 +204,6 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
     if (rem >= 4) { *reinterpret_cast<f32x4*>(p) = v; return; }
     for (int j = 0; j < rem; ++j) p[j] = v[j];
   };
-  const bool use_buf = momentum != 0.f && !first;
   f32x4 gv[U], pv[U], bv[U];
   int tt[U];  // tensor of each granule (its offset is recomputed after the barrier)
   bool bad = false;
@@ -220,6 +221,7 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
       tt[k] = lo;
       gv[k] = load4(sp1[lo] + o, rem);
       pv[k] = load4(sp0[lo] + o, rem);
+      const bool use_buf = momentum != 0.f && !((L.first_bits >> lo) & 1ull);
       bv[k] = use_buf ? load4(sp2[lo] + o, rem) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
@@ -275,6 +277,9 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
       }
       gv[k] = acc * invw;
     }
+    // a peer that never arrived (timeout / abort: error word set) leaves a partial sum:
+    // take the skip path (no parameter / momentum / scale change) rather than apply it
+    bad |= fail;
   }
 #pragma unroll
   for (int k = 0; k < U; ++k)
@@ -293,10 +298,20 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
     __hip_atomic_fetch_add(word, 1ull | ((unsigned long long)block_bad << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long v;
+    // bounded: the host sizes the grid to be co-resident (amp_sgd_fused), so every workgroup
+    // arrives; should one never do, give up after barrier_ticks, flag it and skip the update
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    bool timed_out = false;
     while (((v = __hip_atomic_fetch_add(word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & 0xffffffffull) <
-           G)
+           G) {
       __builtin_amdgcn_s_sleep(1);
-    s_bad = (v >> 32) != 0;
+      if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > barrier_ticks) {
+        timed_out = true;
+        if (err != nullptr) __hip_atomic_store(err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    s_bad = timed_out || (v >> 32) != 0;
     if (blockIdx.x == 0) {
       __hip_atomic_exchange(&sync[1 + ((gen + 1) & 1)], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_fetch_add(&sync[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -315,6 +330,7 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
     f32x4 d = maximize ? -g : g;
     if (wd != 0.f) d += wd * pv[k];
     if (momentum != 0.f) {
+      const bool first = (L.first_bits >> t) & 1ull;
       const f32x4 bb = first ? d : momentum * bv[k] + (1.f - dampening) * d;
       store4(sp2[t] + o, rem, bb);
       d = nesterov ? d + momentum * bb : bb;
@@ -389,16 +405,26 @@ void unscale_check(std::vector<at::Tensor> grads, at::Tensor scale, at::Tensor f
   });
 }
 
+// first: per tensor, 1 = its momentum buffer is new (b = d, torch's first step); empty = none
+static unsigned long long first_bits(const std::vector<int64_t>& first, size_t s, size_t e) {
+  unsigned long long m = 0;
+  for (size_t i = s; i < e && i < first.size(); ++i)
+    if (first[i]) m |= 1ull << (i - s);
+  return m;
+}
+
 void sgd_step(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std::vector<at::Tensor> bufs,
-              double lr, double momentum, double dampening, double wd, bool nesterov, bool maximize, bool first,
-              c10::optional<at::Tensor> found_inf, c10::optional<at::Tensor> grad_scale) {
+              double lr, double momentum, double dampening, double wd, bool nesterov, bool maximize,
+              std::vector<int64_t> first, c10::optional<at::Tensor> found_inf, c10::optional<at::Tensor> grad_scale) {
   TORCH_CHECK(params.size() == grads.size());
   TORCH_CHECK(bufs.empty() || bufs.size() == params.size());
+  TORCH_CHECK(first.empty() || first.size() == params.size(), "sgd_step: one first flag per tensor");
   const float* fi = found_inf.has_value() ? found_inf->data_ptr<float>() : nullptr;
   const float* gsp = grad_scale.has_value() ? grad_scale->data_ptr<float>() : nullptr;
   for_batches(params.size(), [&](size_t s, size_t e) {
     MTList L{};
     L.n = (int)(e - s);
+    L.first_bits = first_bits(first, s, e);
     L.chunk_off[0] = 0;
     for (size_t i = s; i < e; ++i) {
       check_f32(params[i]); check_f32(grads[i]);
@@ -411,8 +437,7 @@ void sgd_step(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std
       L.chunk_off[k + 1] = L.chunk_off[k] + (L.numel[k] + CHUNK - 1) / CHUNK;
     }
     hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(L.chunk_off[L.n])), dim3(NTHR), 0, cur_stream(), L, (float)lr,
-                       (float)momentum, (float)dampening, (float)wd, (int)nesterov, (int)maximize, (int)first, fi,
-                       gsp);
+                       (float)momentum, (float)dampening, (float)wd, (int)nesterov, (int)maximize, fi, gsp);
     DPA_CHECK_LAUNCH();
   });
 }
@@ -420,19 +445,38 @@ void sgd_step(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std
 // elements the fused AMP-SGD kernel can exchange in one launch (U = 1 granule per lane)
 int64_t amp_sgd_xg_max() { return (int64_t)FUSED_MAX_BLOCKS * FUSED_THR * 4; }
 
+// The fused kernel's largest grid (FUSED_MAX_BLOCKS workgroups) is co-resident on this device.
+bool amp_sgd_resident() {
+  static const bool ok =
+      co_resident(reinterpret_cast<const void*>(&amp_sgd_fused_kernel<1, false>), FUSED_MAX_BLOCKS, FUSED_THR) &&
+      co_resident(reinterpret_cast<const void*>(&amp_sgd_fused_kernel<2, false>), FUSED_MAX_BLOCKS, FUSED_THR) &&
+      co_resident(reinterpret_cast<const void*>(&amp_sgd_fused_kernel<FUSED_U, false>), FUSED_MAX_BLOCKS,
+                  FUSED_THR) &&
+      co_resident(reinterpret_cast<const void*>(&amp_sgd_fused_kernel<1, true>), FUSED_MAX_BLOCKS, FUSED_THR);
+  return ok;
+}
+
+// sync: zero-initialised int64[4] device tensor: [0..2] grid-barrier state, [3] low
+// word = error (3: a workgroup never reached the barrier within kBarrierSeconds)
+constexpr double kBarrierSeconds = 10.0;
+
 void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std::vector<at::Tensor> bufs,
-                   double lr, double momentum, double dampening, double wd, bool nesterov, bool maximize, bool first,
-                   at::Tensor scale, at::Tensor tracker, at::Tensor found_inf, double growth, double backoff,
-                   int64_t interval, at::Tensor sync, std::shared_ptr<xgmi::XgmiComm> xc) {
+                   double lr, double momentum, double dampening, double wd, bool nesterov, bool maximize,
+                   std::vector<int64_t> first, at::Tensor scale, at::Tensor tracker, at::Tensor found_inf,
+                   double growth, double backoff, int64_t interval, at::Tensor sync,
+                   std::shared_ptr<xgmi::XgmiComm> xc) {
   TORCH_CHECK(params.size() == grads.size() && params.size() <= (size_t)MAXT, "fused AMP-SGD: <= ", MAXT,
               " tensors");
   TORCH_CHECK(bufs.empty() || bufs.size() == params.size());
+  TORCH_CHECK(first.empty() || first.size() == params.size(), "fused AMP-SGD: one first flag per tensor");
   check_f32(scale); check_f32(found_inf);
   TORCH_CHECK(tracker.scalar_type() == at::kInt);
-  TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == at::kLong && sync.numel() >= 3 && sync.is_contiguous(),
-              "fused AMP-SGD: sync must be a zero-initialised int64[3] device tensor");
+  TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == at::kLong && sync.numel() >= 4 && sync.is_contiguous(),
+              "fused AMP-SGD: sync must be a zero-initialised int64[4] device tensor");
+  TORCH_CHECK(amp_sgd_resident(), "fused AMP-SGD: grid not co-resident on this device (use the unfused step)");
   MTList L{};
   L.n = (int)params.size();
+  L.first_bits = first_bits(first, 0, params.size());
   L.chunk_off[0] = 0;
   for (size_t i = 0; i < params.size(); ++i) {
     check_f32(params[i]); check_f32(grads[i]);
@@ -453,8 +497,9 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
     hipLaunchKernelGGL(kern, dim3(grid), dim3(FUSED_THR), 0, cur_stream(), L, scale.data_ptr<float>(),
                        tracker.data_ptr<int>(), found_inf.data_ptr<float>(),
                        reinterpret_cast<unsigned long long*>(sync.data_ptr<int64_t>()), (float)lr, (float)momentum,
-                       (float)dampening, (float)wd, (int)nesterov, (int)maximize, (int)first, (float)growth,
-                       (float)backoff, (int)interval, xg);
+                       (float)dampening, (float)wd, (int)nesterov, (int)maximize, (float)growth, (float)backoff,
+                       (int)interval, xg, reinterpret_cast<int*>(sync.data_ptr<int64_t>() + 3),
+                       (long long)(kBarrierSeconds * 1e8));
   };
   if (xc) {
     const xgmi::XSite xg = xc->grad_site();
@@ -522,11 +567,12 @@ void register_optim(pybind11::module& m) {
   s.def("unscale_check", &opt::unscale_check);
   s.def("sgd_step", &opt::sgd_step, pybind11::arg("params"), pybind11::arg("grads"), pybind11::arg("bufs"),
         pybind11::arg("lr"), pybind11::arg("momentum"), pybind11::arg("dampening"), pybind11::arg("weight_decay"),
-        pybind11::arg("nesterov"), pybind11::arg("maximize"), pybind11::arg("first"),
+        pybind11::arg("nesterov"), pybind11::arg("maximize"), pybind11::arg("first") = std::vector<int64_t>{},
         pybind11::arg("found_inf") = pybind11::none(), pybind11::arg("grad_scale") = pybind11::none());
   s.def("update_scale", &opt::update_scale);
   s.def("amp_sgd_fused", &opt::amp_sgd_fused);
   s.def("amp_sgd_xg_max", &opt::amp_sgd_xg_max);
+  s.def("amp_sgd_resident", &opt::amp_sgd_resident);
   s.attr("FUSED_MAX") = opt::FUSED_MAX;
   s.attr("MAXT") = opt::MAXT;
   s.def("flat_copy", &opt::flat_copy);

@@ -187,15 +187,16 @@ class TrainLoop:
 
 
 @torch.no_grad()
-def evaluate(model, loader: DeviceLoader, comm=None, dst: int = 0):
+def evaluate(model, loader: DeviceLoader, comm=None, dst: int = 0, native: bool = True):
     """Reference ``test()``: global accuracy reduced to rank ``dst`` (ddp_main.py:96-112).
 
     Returns (correct, size) as floats on rank ``dst`` (other ranks: their local values).
+    ``native=False`` counts with torch ops (the ``--impl torch`` runs).
     """
     model.eval()
     dev = loader.device
     counters = torch.zeros(2, dtype=torch.float32, device=dev)
-    native = dev.type == "cuda"
+    native = native and dev.type == "cuda"
     if native:
         from .ops.head import accuracy_
     for images, labels in loader:

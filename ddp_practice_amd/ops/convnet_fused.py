@@ -51,13 +51,26 @@ def supported(model, x: torch.Tensor) -> bool:
     return fc.in_features == 32 * 49 and fc.bias is not None and 1 <= n <= 64 and b * (n + 49) + n * 49 <= 16384
 
 
-def _fused_site_engine(comm):
+_RESIDENT: dict = {}
+
+
+def _fused_site_engine(comm, batch: int, dtype: torch.dtype):
     """The communicator's xGMI engine when SyncBN may exchange its sums inside the
     kernels (csrc/comm/xsite.h), else None (all-reduces between the launches).
-    DPA_FUSED_SYNC=0 forces the launch-per-collective path (A/B runs)."""
+
+    Every workgroup of such a launch polls the peers' rows, so the launch is only
+    taken when all its workgroups fit on the device at once (occupancy x CUs,
+    ``convnet.sites_resident``); DPA_FUSED_SYNC=0 forces the launch-per-collective
+    path (A/B runs)."""
     if os.environ.get("DPA_FUSED_SYNC", "1") == "0":
         return None
-    return getattr(comm, "xgmi", None)
+    xc = getattr(comm, "xgmi", None)
+    if xc is None:
+        return None
+    key = (batch, dtype)
+    if key not in _RESIDENT:
+        _RESIDENT[key] = bool(_load_ext().convnet.sites_resident(batch, dtype))
+    return xc if _RESIDENT[key] else None
 
 
 class ConvNetFn(torch.autograd.Function):
@@ -73,7 +86,7 @@ class ConvNetFn(torch.autograd.Function):
         N = wfc.shape[0]
         sync = comm is not None and comm.active and training
         # SyncBN sums exchanged inside the consuming kernels when the xGMI engine is up
-        xc = _fused_site_engine(comm) if sync else None
+        xc = _fused_site_engine(comm, B, cdtype) if sync else None
         y1 = torch.empty((B, 16, 28, 28), dtype=cdtype, device=dev)
         y2 = torch.empty((B, 32, 14, 14), dtype=cdtype, device=dev)
         logits = torch.empty((B, N), dtype=cdtype, device=dev)

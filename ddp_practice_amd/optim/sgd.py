@@ -61,20 +61,7 @@ class SGD(Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        for group in self.param_groups:
-            params, grads, bufs = [], [], []
-            first = False
-            for p in group["params"]:
-                if p.grad is None:
-                    continue
-                params.append(p)
-                grads.append(p.grad)
-                if group["momentum"] != 0:
-                    st = self.state[p]
-                    if "momentum_buffer" not in st or st["momentum_buffer"] is None:
-                        st["momentum_buffer"] = torch.zeros_like(p)
-                        first = True
-                    bufs.append(st["momentum_buffer"])
+        for group, params, grads, bufs, first in self._collect():
             if not params:
                 continue
             native = params[0].is_cuda and all(
@@ -94,9 +81,17 @@ class SGD(Optimizer):
     FUSED_AMP_MAX_NUMEL = 1 << 19  # csrc/kernels/optim.hip FUSED_MAX
 
     def _collect(self):
+        """Per group: params with a grad, their grads and momentum buffers, and one "first"
+        flag per tensor (its buffer was just created: torch's ``buf = d`` step).
+
+        Buffers start at zero, so with dampening 0 the first step's ``momentum*0 + d``
+        IS ``d``: no flag is passed then, which also keeps a device-skipped first step
+        (found_inf) exact -- the buffer simply stays zero.  With dampening != 0 the flags
+        are per tensor; a first step skipped on the device consumes them (documented gap).
+        """
         out = []
         for group in self.param_groups:
-            params, grads, bufs, first = [], [], [], False
+            params, grads, bufs, first = [], [], [], []
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -104,10 +99,13 @@ class SGD(Optimizer):
                 grads.append(p.grad)
                 if group["momentum"] != 0:
                     st = self.state[p]
-                    if st.get("momentum_buffer") is None:
+                    new = st.get("momentum_buffer") is None
+                    if new:
                         st["momentum_buffer"] = torch.zeros_like(p)
-                        first = True
                     bufs.append(st["momentum_buffer"])
+                    first.append(int(new))
+            if group["dampening"] == 0 or not any(first):
+                first = []
             out.append((group, params, grads, bufs, first))
         return out
 
@@ -119,7 +117,10 @@ class SGD(Optimizer):
         ps = [p for p in self.param_groups[0]["params"] if p.grad is not None]
         if not ps or len(ps) > _load_ext().optim.MAXT:
             return False
-        if sum(p.numel() for p in ps) > self.FUSED_AMP_MAX_NUMEL:
+        # the kernel rounds every tensor up to whole float4 granules (csrc/kernels/optim.hip)
+        if sum((p.numel() + 3) // 4 * 4 for p in ps) > self.FUSED_AMP_MAX_NUMEL:
+            return False
+        if not _load_ext().optim.amp_sgd_resident():
             return False
         def aligned(t):  # the kernel moves float4 granules
             return t is None or t.data_ptr() % 16 == 0
@@ -135,7 +136,7 @@ class SGD(Optimizer):
         if sync is None or sync.device != params[0].device:
             # grid-barrier state of the fused kernel (allocated before any graph capture:
             # the first step runs eagerly)
-            sync = self._amp_sync = torch.zeros(3, dtype=torch.int64, device=params[0].device)
+            sync = self._amp_sync = torch.zeros(4, dtype=torch.int64, device=params[0].device)
         # gradients a DDP reducer deferred to this step are averaged inside the kernel
         d = getattr(self, "_deferred_ddp", None)
         xc = d[1] if d is not None and d[0].deferred_pending() else None
@@ -154,7 +155,7 @@ class SGD(Optimizer):
                 d = d.add(p, alpha=wd)
             if mom != 0:
                 b = bufs[i]
-                if first:
+                if first and first[i]:
                     b.copy_(d)
                 else:
                     b.mul_(mom).add_(d, alpha=1 - damp)

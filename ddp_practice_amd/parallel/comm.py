@@ -356,20 +356,41 @@ def open_xgmi(rank: int, world: int, device: torch.device, store, key: str, max_
     return x, err
 
 
-def setup_xgmi(rc: "RcclCommunicator", store, key: str) -> str:
-    """Attach the one-shot xGMI all-reduce (csrc/comm/xgmi_allreduce.hip) to ``rc``.
+def comm_mode() -> str:
+    """Collective algorithm selection (``--comm`` / ``DPA_COMM``): auto | rccl | xgmi.
 
-    DPA_XGMI=0 disables it; DPA_XGMI_MAX_BYTES sets the size up to which it is
-    used (default 1 MiB).  Before attaching, every rank runs a self-test
-    against RCCL (values within fp32 tolerance, results bit-identical across
-    ranks, bounded by a short timeout); any failure on any rank keeps every
-    rank on RCCL.  Returns a status string.
+    auto: the xGMI engine for the messages where it is validated and faster (one-shot up to
+    ``DPA_XGMI_MAX_BYTES``, default 1 MiB), RCCL above; rccl: RCCL only (no engine, no
+    in-kernel exchanges); xgmi: the engine wherever it can take the message.
+    ``DPA_XGMI=0`` is the legacy spelling of rccl.
     """
+    m = os.environ.get("DPA_COMM", "auto").lower()
     if os.environ.get("DPA_XGMI", "1") == "0":
-        return "off (DPA_XGMI=0)"
+        m = "rccl"
+    if m not in ("auto", "rccl", "xgmi"):
+        raise ValueError(f"DPA_COMM must be auto, rccl or xgmi, got {m!r}")
+    return m
+
+
+def setup_xgmi(rc: "RcclCommunicator", store, key: str) -> str:
+    """Attach the xGMI engine (csrc/comm/xgmi_allreduce.hip) to ``rc``.
+
+    ``comm_mode()`` rccl disables it; DPA_XGMI_MAX_BYTES sets the size up to which it
+    is used (default 1 MiB; ``--comm xgmi``: the whole workspace).  Before attaching,
+    every rank runs a self-test against RCCL (values within fp32 tolerance, results
+    bit-identical across ranks, bounded by a short timeout); any failure on any rank
+    keeps every rank on RCCL.  Every rank issues exactly the same collectives whatever
+    happens locally (a rank-local failure only flips its vote), so a misbehaving engine
+    can never desynchronise the RCCL call sequence.  Returns a status string.
+    """
+    mode = comm_mode()
+    if mode == "rccl":
+        return "off (--comm rccl)"
     if store is None:
         store = dist.distributed_c10d._get_default_store()
     max_bytes = int(float(os.environ.get("DPA_XGMI_MAX_BYTES", XGMI_DEFAULT_MAX_BYTES)))
+    if mode == "xgmi":
+        max_bytes = max(max_bytes, int(float(os.environ.get("DPA_XGMI_WORKSPACE_BYTES", 32 << 20))))
     timeout = float(os.environ.get("DPA_XGMI_TIMEOUT", "600"))
     if max_bytes <= 0 or rc.world_size > 8:
         return "off"
@@ -378,40 +399,49 @@ def setup_xgmi(rc: "RcclCommunicator", store, key: str) -> str:
     rc.native.all_reduce(ok, "min")
     if ok.item() != 1.0:
         return f"off (setup failed: {err or 'on a peer'})"
-    try:
-        good = _xgmi_selftest(rc, x)
-    except Exception as e:  # noqa: BLE001
-        good, err = False, f"{type(e).__name__}: {e}"
-    ok.fill_(1.0 if good and x.error() == 0 else 0.0)
-    rc.native.all_reduce(ok, "min")
-    if ok.item() != 1.0:
-        return f"off (self-test failed: {err or x.error_string() or 'on a peer'})"
+    good, err = _xgmi_selftest(rc, x)
+    if not good:
+        return f"off (self-test failed: {err or 'on a peer'})"
     x.set_timeout(timeout)
     rc.native.attach_xgmi(x, max_bytes)
     rc.xgmi = x
     return f"on (<= {max_bytes} B)"
 
 
-def _xgmi_selftest(rc: "RcclCommunicator", x) -> bool:
+def _xgmi_selftest(rc: "RcclCommunicator", x) -> tuple[bool, str]:
+    """Engine vs RCCL on a few sizes/dtypes/ops.  Per case, every rank issues the same
+    RCCL collectives (reference all-reduce, cross-rank equality all-gather, vote); the
+    vote is a min all-reduce so all ranks leave the loop together."""
     g = torch.Generator(device="cpu").manual_seed(1234 + rc.rank)
+    why = ""
+    vote = torch.ones(1, device=rc.device)
     for n, dt, op in ((33, torch.float32, "sum"), (4099, torch.float32, "sum"), (29034, torch.float32, "sum"),
                       (8195, torch.bfloat16, "sum"), (1000, torch.float32, "max")):
         t = torch.randn(n, generator=g).to(device=rc.device, dtype=dt)
-        mine = x.all_reduce(t, op, torch.empty_like(t))
+        mine = torch.zeros_like(t)
+        good = True
+        try:
+            x.all_reduce(t, op, mine)
+        except Exception as e:  # noqa: BLE001 - recorded as this rank's vote
+            good, why = False, f"{type(e).__name__}: {e}"
         ref = torch.empty_like(t)
         rc.native.all_reduce(t, op, ref)
-        torch.cuda.synchronize(rc.device)
-        if x.error() != 0:
-            return False
-        tol = 1e-5 if dt == torch.float32 else 2e-2
-        if not torch.allclose(mine.float(), ref.float(), rtol=tol, atol=tol * rc.world_size):
-            return False
         every = torch.empty(rc.world_size * n, dtype=dt, device=rc.device)
         rc.native.all_gather(every, mine)
+        torch.cuda.synchronize(rc.device)
+        if x.error() != 0:
+            good, why = False, why or x.error_string()
+        tol = 1e-5 if dt == torch.float32 else 2e-2
+        if good and not torch.allclose(mine.float(), ref.float(), rtol=tol, atol=tol * rc.world_size):
+            good, why = False, f"mismatch vs RCCL (n={n}, {dt}, {op})"
         every = every.view(rc.world_size, n)
-        if not bool((every == every[0:1]).all()):
-            return False
-    return True
+        if good and not bool((every == every[0:1]).all()):
+            good, why = False, f"ranks disagree (n={n}, {dt}, {op})"
+        vote.fill_(1.0 if good else 0.0)
+        rc.native.all_reduce(vote, "min")
+        if vote.item() != 1.0:
+            return False, why
+    return True, ""
 
 
 # ------------------------------------------------------------------ process group

@@ -203,7 +203,7 @@ class DistributedDataParallel(nn.Module):
         opt_params = [p for g in optimizer.param_groups for p in g["params"]]
         if {id(p) for p in opt_params} != {id(p) for p in self._params}:
             return False
-        n = sum(p.numel() for p in self._params)
+        n = sum((p.numel() + 3) // 4 * 4 for p in self._params)  # float4 granules, as the kernel counts
         if n > min(int(xc.max_bytes) // 4, int(_load_ext().optim.amp_sgd_xg_max())):
             return False
         self.reducer.set_defer(True)

@@ -49,6 +49,73 @@ def worker(rank, world, port, mode, q):
         assert x is not None, err
         store.set(f"ready{rank}", "1")
         store.wait([f"ready{r}" for r in range(world)])
+        if mode == "site":
+            # in-kernel SyncBN exchange: 4 workgroups per launch, 30 launches through two
+            # sites (epochs, parity reuse), eager and graph-replayed; rank-ordered sums
+            out = {}
+            for it in range(30):
+                n = 1 + (it * 37) % 128
+                t = _data(rank, n, torch.float32, it).to(dev)
+                o = torch.empty(4 * n, device=dev)
+                x.site_probe(it % 2, t, o, 4)
+                torch.cuda.synchronize()
+                assert x.error() == 0, x.error_string()
+                exp = _expect(world, n, torch.float32, it, "sum")
+                for b in range(4):
+                    _check(o[b * n:(b + 1) * n], exp, torch.float32, ("site", it, b))
+                out[f"site{it}"] = o.cpu().numpy().tobytes()
+            t = torch.zeros(64, device=dev)
+            o = torch.empty(2 * 64, device=dev)
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                x.site_probe(3, t, o, 2)
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                x.site_probe(3, t, o, 2)
+            for r in range(10):
+                t.copy_(_data(rank, 64, torch.float32, 100 + r).to(dev))
+                g.replay()
+                torch.cuda.synchronize()
+                assert x.error() == 0, x.error_string()
+                exp = _expect(world, 64, torch.float32, 100 + r, "sum")
+                _check(o[:64], exp, torch.float32, ("site graph", r))
+                _check(o[64:], exp, torch.float32, ("site graph", r))
+            store.set(f"done{rank}", "1")
+            store.wait([f"done{r}" for r in range(world)])
+            x.close()
+            q.put((rank, "ok", out))
+            return
+        if mode in ("site_timeout", "sgd_timeout"):
+            # rank 0 runs an in-kernel exchange whose peer never comes: the kernel must end
+            # with the error word set (1), and the fused AMP-SGD must take the skip path
+            if rank == 0:
+                x.set_timeout(0.5)
+                if mode == "site_timeout":
+                    o = torch.empty(3 * 16, device=dev)
+                    x.site_probe(1, torch.ones(16, device=dev), o, 3)
+                    torch.cuda.synchronize()
+                else:
+                    ps = [torch.randn(n, device=dev) for n in (100, 3000)]
+                    before = [p.clone() for p in ps]
+                    gs = [torch.randn_like(p) for p in ps]
+                    sc = torch.tensor([8.0], device=dev)
+                    tr = torch.zeros(1, dtype=torch.int32, device=dev)
+                    fi = torch.zeros(1, device=dev)
+                    sync = torch.zeros(4, dtype=torch.int64, device=dev)
+                    C.optim.amp_sgd_fused(ps, gs, [], 0.1, 0.0, 0.0, 0.0, False, False, [], sc, tr, fi, 2.0, 0.5,
+                                          2000, sync, x)
+                    torch.cuda.synchronize()
+                    for p, b in zip(ps, before):
+                        assert torch.equal(p, b), "partial-sum update applied after a failed exchange"
+                    assert sc.item() == 4.0 and tr.item() == 0  # skipped step: back-off, as for an inf
+                assert x.error() == 1, x.error()
+            store.set(f"done{rank}", "1")
+            store.wait([f"done{r}" for r in range(world)])
+            q.put((rank, "ok", None))
+            return
         if mode == "timeout":
             # rank 0 waits for a peer that never comes: must return with error 1, not hang
             if rank == 0:

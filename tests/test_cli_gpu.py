@@ -1,0 +1,95 @@
+"""The reference's three programs end to end on the MI355X (its only validation:
+/root/reference/README.md:189-202,454-467): stdout contract, checkpoint format and
+key sets, a checkpoint that loads into plain torch modules, hipGraph replay across
+epochs plus the eager tail batch, and accuracy parity with the same program run on
+PyTorch's own stack (``--impl torch``: nn modules, torch autocast / GradScaler / SGD
+/ SyncBatchNorm / DDP) on identical synthetic data and seed.
+
+The reference's published accuracies (91.55 % fp32 W=1, 89.21 % fp16 W=2) come from
+MNIST, which is not available here: parity against them is unpinned; these tests pin
+parity against torch on the same data instead."""
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from ._dist import free_port
+from .test_cli_cpu import REF_KEYS, _check_stdout
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _run(args, cwd, env_extra=None, timeout=110):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "CUDA_VISIBLE_DEVICES"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, *args], cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "capture failed" not in r.stderr, r.stderr
+    return r.stdout
+
+
+def _load_into_torch(sd):
+    from ddp_practice_amd.models import ConvNet
+
+    m = ConvNet(fused=False)
+    m.load_state_dict({k[len("module."):] if k.startswith("module.") else k: v for k, v in sd.items()})
+    for v in sd.values():  # device tensors, as the reference's torch.save of a .cuda() model writes
+        assert v.dtype in (torch.float32, torch.int64)
+    return m
+
+
+def test_origin_main_gpu(C, tmp_path):
+    out = _run([os.path.join(ROOT, "origin_main.py"), "--gpu", "0", "-e", "2", "--synthetic", "--seed", "0"],
+               tmp_path)
+    acc = _check_stdout(out, 2)
+    assert acc > 50.0
+    ck = torch.load(tmp_path / "origin_checkpoint.pt", weights_only=True)
+    assert list(ck) == ["model"] and list(ck["model"]) == REF_KEYS
+    m = _load_into_torch(ck["model"])
+    assert int(m.layer1[1].num_batches_tracked) == 2 * 1875  # every step of both epochs updated BN
+
+
+def test_ddp_main_spawn_gpu(C, tmp_path):
+    out = _run([os.path.join(ROOT, "ddp_main.py"), "--gpu", "0", "-e", "1", "--synthetic"], tmp_path,
+               {"MASTER_PORT": str(free_port()), "DPA_MASTER_ADDR": "127.0.0.1"})
+    _check_stdout(out, 1)
+    ck = torch.load(tmp_path / "ddp_checkpoint.pt", weights_only=True)
+    assert list(ck["model"]) == ["module." + k for k in REF_KEYS]
+    assert set(ck["scaler"]) == {"scale", "growth_factor", "backoff_factor", "growth_interval", "_growth_tracker"}
+    _load_into_torch(ck["model"])
+
+
+def test_ddp_main_torchrun_gpu(C, tmp_path):
+    out = _run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr=127.0.0.1",
+                f"--master-port={free_port()}", os.path.join(ROOT, "ddp_main_torchrun.py"), "--gpu", "0", "-e", "1",
+                "--synthetic", "--amp-dtype", "bf16"], tmp_path)
+    _check_stdout(out, 1)
+    ck = torch.load(tmp_path / "ddp_checkpoint.pt", weights_only=True)
+    assert list(ck["model"]) == ["module." + k for k in REF_KEYS]
+    _load_into_torch(ck["model"])
+
+
+def _acc(out):
+    m = re.search(r"Accuracy is ([0-9.]+)%", out)
+    assert m, out
+    return float(m.group(1))
+
+
+@pytest.mark.parametrize("script,extra", [("origin_main.py", []), ("ddp_main.py", [])])
+def test_accuracy_parity_with_torch(C, tmp_path, script, extra):
+    """3 epochs, same data / seed / order: native vs the same program on torch's stack."""
+    env = {"MASTER_PORT": str(free_port()), "DPA_MASTER_ADDR": "127.0.0.1"}
+    args = [os.path.join(ROOT, script), "--gpu", "0", "--synthetic", "--seed", "0", *extra]
+    (tmp_path / "n").mkdir()
+    (tmp_path / "t").mkdir()
+    a_native = _acc(_run(args, tmp_path / "n", env))
+    env["MASTER_PORT"] = str(free_port())
+    a_torch = _acc(_run(args + ["--impl", "torch"], tmp_path / "t", env))
+    print(f"{script}: native {a_native:.2f}% torch {a_torch:.2f}%")
+    assert abs(a_native - a_torch) <= 1.0, (a_native, a_torch)

@@ -162,7 +162,7 @@ def test_sgd_and_scaler_kernels(C):
     for g, r in zip(gs, ref_g):
         torch.testing.assert_close(g, r)
     bufs = [torch.zeros_like(p) for p in ps]
-    C.optim.sgd_step(ps, gs, bufs, 0.1, 0.9, 0.0, 1e-4, False, False, True, fi, None)
+    C.optim.sgd_step(ps, gs, bufs, 0.1, 0.9, 0.0, 1e-4, False, False, [1, 1, 1], fi, None)
     opt = torch.optim.SGD([torch.nn.Parameter(p) for p in ref_p], lr=0.1, momentum=0.9, weight_decay=1e-4)
     for p, g in zip(opt.param_groups[0]["params"], ref_g):
         p.grad = g
@@ -175,7 +175,7 @@ def test_sgd_and_scaler_kernels(C):
     fi.zero_()
     C.optim.unscale_check(gs, scale, fi)
     assert fi.item() == 1
-    C.optim.sgd_step(ps, gs, bufs, 0.1, 0.9, 0.0, 0.0, False, False, False, fi, None)
+    C.optim.sgd_step(ps, gs, bufs, 0.1, 0.9, 0.0, 0.0, False, False, [], fi, None)
     for p, b in zip(ps, before):
         assert torch.equal(p, b)
     # update_scale semantics
@@ -230,12 +230,12 @@ def test_fused_amp_sgd_matches_unfused(C, momentum, sizes):
     sa, sb = torch.tensor([512.0], device=DEV), torch.tensor([512.0], device=DEV)
     ta, tb = torch.zeros(1, dtype=torch.int32, device=DEV), torch.zeros(1, dtype=torch.int32, device=DEV)
     fa, fb = torch.zeros(1, device=DEV), torch.zeros(1, device=DEV)
-    sync = torch.zeros(3, dtype=torch.int64, device=DEV)
+    sync = torch.zeros(4, dtype=torch.int64, device=DEV)
     ga = [torch.empty_like(p) for p in ps]
 
     def fused(first):
-        C.optim.amp_sgd_fused(pa, ga, ba, 0.1, momentum, 0.0, 1e-4, False, False, first, sa, ta, fa, 2.0, 0.5, 2,
-                              sync, None)
+        C.optim.amp_sgd_fused(pa, ga, ba, 0.1, momentum, 0.0, 1e-4, False, False, [int(first)] * len(ps), sa, ta,
+                              fa, 2.0, 0.5, 2, sync, None)
 
     graph = None
     for it in range(8):
@@ -256,7 +256,7 @@ def test_fused_amp_sgd_matches_unfused(C, momentum, sizes):
                     fused(False)
             graph.replay()
         C.optim.unscale_check(gb, sb, fb)
-        C.optim.sgd_step(pb, gb, bb, 0.1, momentum, 0.0, 1e-4, False, False, first, fb, None)
+        C.optim.sgd_step(pb, gb, bb, 0.1, momentum, 0.0, 1e-4, False, False, [int(first)] * len(ps), fb, None)
         C.optim.update_scale(sb, tb, fb, 2.0, 0.5, 2)
         torch.cuda.synchronize()
         for x, y in zip(pa + ga + ba, pb + gb + bb):

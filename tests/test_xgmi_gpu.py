@@ -24,3 +24,19 @@ def test_xgmi_allreduce_multiprocess(C, world):
 
 def test_xgmi_wait_is_bounded(C):
     _run(2, "timeout")
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_xsite_exchange_multiprocess(C, world):
+    """The in-kernel SyncBN exchange (csrc/comm/xsite.h) every fused consumer runs."""
+    outs = _run(world, "site")
+    for k, v in outs[0].items():
+        for r in range(1, world):
+            assert v == outs[r][k], f"rank {r} differs from rank 0 on {k}"
+
+
+@pytest.mark.parametrize("mode", ["site_timeout", "sgd_timeout"])
+def test_in_kernel_exchange_wait_is_bounded(C, mode):
+    """A fused SyncBN site and the fused AMP-SGD gradient exchange whose peer never
+    arrives end with the error word set; the optimizer applies nothing."""
+    _run(2, mode)
