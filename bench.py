@@ -349,9 +349,12 @@ def run_rank(args) -> None:
         images, labels = loader.static_batch()
         loader.start_epoch()
         nfull = len(sampler) // B
+        from ddp_practice_amd.data import accepts_deferred
+
+        defer = accepts_deferred(model, images)  # the gather runs inside conv1
 
         def step():
-            loader.fill_(images, labels)
+            loader.fill_(images, labels, defer=defer)
             out = model(images)
             loss = crit(out, labels)
             optimizer.zero_grad(set_to_none=True)

@@ -13,6 +13,7 @@ reference: /root/reference/ddp_main.py:10,126 (``GradScaler()``), :91-93.
 """
 from __future__ import annotations
 
+import weakref
 from typing import Any
 
 import torch
@@ -42,7 +43,13 @@ class _ScaledLossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, loss, scale, ce_node):
         ctx.save_for_backward(scale)
-        return ce_node.scaled  # a view of the loss kernel's output buffer: no launch
+        out = ce_node.scaled  # a view of the loss kernel's output buffer: no launch
+        # the loss node must not keep this output alive: it becomes the output of THIS node,
+        # whose edge leads back to the loss node -- a reference cycle that kept every
+        # step's autograd graph (AccumulateGrad nodes included) alive until the cyclic GC
+        # ran; graph capture after eager steps then synchronised with their stream
+        ce_node.scaled = None
+        return out
 
     @staticmethod
     def backward(ctx, g):
@@ -108,8 +115,6 @@ class GradScaler:
     def _lazy_init(self, dev: torch.device):
         global _ACTIVE
         if self._enabled and dev.type == "cuda":
-            import weakref
-
             _ACTIVE = weakref.ref(self)
         if self._scale is None:
             self._scale = torch.full((1,), self._init_scale, dtype=torch.float32, device=dev)
@@ -147,6 +152,10 @@ class GradScaler:
                 node = ce[0]
                 scaled = _ScaledLossFn.apply(outputs, self._scale, node)
                 base = outputs
+                # weak: the closure is stored on `scaled` itself; a strong reference would be a
+                # reference cycle keeping the step's whole autograd graph alive until the cyclic
+                # GC runs (a later hipGraph capture then syncs with the old nodes' stream)
+                scaled_ref = weakref.ref(scaled)
 
                 def _backward_ce(gradient=None, retain_graph=None, create_graph=False, inputs=None):
                     if gradient is None and not create_graph:
@@ -156,7 +165,7 @@ class GradScaler:
                         finally:
                             node.token.seeded = False
                     else:
-                        torch.Tensor.backward(scaled, gradient, retain_graph, create_graph, inputs)
+                        torch.Tensor.backward(scaled_ref(), gradient, retain_graph, create_graph, inputs)
 
                 scaled.backward = _backward_ce
                 return scaled
@@ -169,12 +178,13 @@ class GradScaler:
                 # through normal autograd.
                 base = outputs
                 seed = s0 if base.dtype == torch.float32 else s0.to(base.dtype)
+                scaled_ref = weakref.ref(scaled)  # no reference cycle (see above)
 
                 def _backward(gradient=None, retain_graph=None, create_graph=False, inputs=None):
                     if gradient is None and not create_graph:
                         _seeded_backward(base, seed, retain_graph, inputs)
                     else:
-                        torch.Tensor.backward(scaled, gradient, retain_graph, create_graph, inputs)
+                        torch.Tensor.backward(scaled_ref(), gradient, retain_graph, create_graph, inputs)
 
                 scaled.backward = _backward
             return scaled

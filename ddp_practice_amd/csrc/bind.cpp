@@ -18,6 +18,7 @@ void register_comm(pybind11::module& m);
 void register_xgmi(pybind11::module& m);
 void register_reducer(pybind11::module& m);
 void register_convnet_fused(pybind11::module& m);
+void register_convnet_head(pybind11::module& m);
 void register_runtime(pybind11::module& m);
 void register_bn_nhwc(pybind11::module& m);
 }
@@ -50,6 +51,7 @@ PYBIND11_MODULE(_C, m) {
   dpa::register_xgmi(m);
   dpa::register_reducer(m);
   dpa::register_convnet_fused(m);
+  dpa::register_convnet_head(m);
   dpa::register_runtime(m);
   dpa::register_bn_nhwc(m);
 }

@@ -54,6 +54,8 @@ struct XSite {
   long long timeout_ticks = 0;           // s_memrealtime ticks (100 MHz)
   long long slot_bytes = kSiteSlotBytes; // one rank's row of granules; a parity holds kMaxRanks rows
   long long max_vals = kSiteVals;        // floats per row
+  int nblk = 0;                          // workgroups of a launch taking tickets (0: the whole grid;
+                                         // set when one launch hosts several roles, each with its site)
   __host__ __device__ bool active() const { return tick != nullptr; }
 };
 
@@ -67,7 +69,7 @@ __device__ __forceinline__ unsigned long long xsite_ticket(const XSite& xs) {
 // Lane 0: the launch's epoch from its ticket (the last ticket of the launch
 // re-arms the word for the next launch).
 __device__ __forceinline__ uint32_t xsite_epoch(const XSite& xs, unsigned long long tk) {
-  const uint32_t nblk = gridDim.x * gridDim.y * gridDim.z;
+  const uint32_t nblk = xs.nblk > 0 ? (uint32_t)xs.nblk : gridDim.x * gridDim.y * gridDim.z;
   if ((uint32_t)tk == nblk - 1u)  // last ticket of this launch: next launch, next epoch
     __hip_atomic_fetch_add(xs.tick, (1ull << 32) - (unsigned long long)nblk, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -96,7 +98,7 @@ __device__ __forceinline__ float xsite_wait(const XSite& xs, const unsigned long
 
 // vals: n (<= kSiteVals, <= blockDim.x) floats of LDS holding this rank's local
 // row; replaced by the rank-ordered sum over all ranks.  tk: lane 0's ticket.
-// pusher: exactly one workgroup of the launch (blockIdx 0).  Called by every
+// pusher: exactly one workgroup of the launch (its role's workgroup 0).  Called by every
 // thread of the workgroup; ends with a barrier.
 __device__ __forceinline__ void xsite_exchange(const XSite& xs, float* vals, int n, unsigned long long tk,
                                                bool pusher) {

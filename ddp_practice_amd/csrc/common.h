@@ -52,8 +52,26 @@ static __device__ unsigned long long dpa_stamps[DPA_MAX_STAMP_BLOCKS * DPA_NSTAM
     if (threadIdx.x == 0 && blockIdx.x < DPA_MAX_STAMP_BLOCKS)                                           \
       dpa_stamps[blockIdx.x * DPA_NSTAMPS + (i)] = __builtin_amdgcn_s_memrealtime();                     \
   } while (0)
+// read_stamps() / clear_stamps() of the calling translation unit's stamp array
+#define DPA_DEF_STAMP_FNS(s)                                                                          \
+  do {                                                                                                \
+    (s).def("read_stamps", []() {                                                                     \
+      auto out = at::empty({DPA_MAX_STAMP_BLOCKS, DPA_NSTAMPS}, at::TensorOptions().dtype(at::kLong)); \
+      DPA_CHECK_HIP(hipDeviceSynchronize());                                                          \
+      DPA_CHECK_HIP(hipMemcpyFromSymbol(out.data_ptr(), HIP_SYMBOL(dpa_stamps),                       \
+                                        sizeof(unsigned long long) * DPA_MAX_STAMP_BLOCKS * DPA_NSTAMPS)); \
+      return out;                                                                                     \
+    });                                                                                               \
+    (s).def("clear_stamps", []() {                                                                    \
+      DPA_CHECK_HIP(hipDeviceSynchronize());                                                          \
+      std::vector<unsigned long long> z(DPA_MAX_STAMP_BLOCKS * DPA_NSTAMPS, 0ull);                    \
+      DPA_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dpa_stamps), z.data(),                               \
+                                      z.size() * sizeof(unsigned long long)));                         \
+    });                                                                                               \
+  } while (0)
 #else
 #define DPA_STAMP(i) do {} while (0)
+#define DPA_DEF_STAMP_FNS(s) do {} while (0)
 #endif
 
 #define DPA_CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a HIP device tensor")

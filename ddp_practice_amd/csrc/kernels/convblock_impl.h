@@ -460,6 +460,22 @@ __device__ __forceinline__ void pack_w2(const WPack<T>& pk) {
   }
 }
 
+// Batch gather fused into the first conv (PRO 3): the input image is read from
+// the uint8 dataset resident in HBM through the epoch's sample order at the
+// device step counter, converted (ToTensor: x * scale + shift, data/loader.py)
+// and staged; split 0 of each image also writes it (and its label) to the
+// batch buffers the rest of the step reads.  The launch's last-arriving
+// workgroup advances the step counter (data.hip gather_kernel's protocol).
+struct GatherIn {
+  const uint8_t* imgs = nullptr;   // [N][npix]
+  const int64_t* labels = nullptr; // [N]
+  const int64_t* order = nullptr;  // epoch order
+  long long order_len = 0;
+  int* ctr = nullptr;              // [0] step, [1] arrivals (self-resetting)
+  int64_t* lab_out = nullptr;      // [B]
+  float scale = 1.f, shift = 0.f;
+};
+
 // ---------------------------------------------------------------------------
 // Implicit-GEMM 5x5 convolution, one (image, m-range) per workgroup.
 //   MODE 0: forward + bias + BN partial sums        (train)
@@ -470,6 +486,8 @@ __device__ __forceinline__ void pack_w2(const WPack<T>& pk) {
 // K = 25*CIN ordered (kh, kw, ci) with ci fastest.
 // ---------------------------------------------------------------------------
 //   PRO 0: the input image is read from x;
+//   PRO 3: (CIN 1) the input image is gathered from the dataset (gin, above) and
+//          written to x by split 0;
 //   PRO 1: the input is produced in the staging pass from the previous block's
 //          pre-BN output (pin: BN finalize -> normalise -> ReLU -> 2x2 max-pool),
 //          which also writes the pooled map + argmax|relu index + xhat at the
@@ -481,17 +499,20 @@ __device__ __forceinline__ void pack_w2(const WPack<T>& pk) {
 //   WPK 0: stage the weight tile from the f32 master weights w;
 //   WPK 1: w is ignored, the tile is copied from the pre-packed wpk (pack_w2);
 //   WPK 2: as 0, and this launch also writes the layer-2 packs (pk).
+// bid: this workgroup's index among the launch's workgroups of this role (blockIdx.x
+// for a launch of its own; conv5x5_kernel / dgrad_wgrad_kernel below).
 template <typename T, int CIN, int COUT, int H, int W, int MODE, int PRO = 0, int EPI = 0, int WPK = 0>
-__global__ void __launch_bounds__(NTHR)
-conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
-               T* __restrict__ y, float* __restrict__ fslab, float* __restrict__ fstats,
-               const float* __restrict__ shift, int nsplit, PoolIn<T> pin = PoolIn<T>{},
-               BwdIn<T> bin = BwdIn<T>{}, BwdEpi<T> epi = BwdEpi<T>{}, const T* __restrict__ wpk = nullptr,
-               WPack<T> pk = WPack<T>{}) {
+__device__ __forceinline__ void
+conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+             T* __restrict__ y, float* __restrict__ fslab, float* __restrict__ fstats,
+             const float* __restrict__ shift, int nsplit, const PoolIn<T>& pin, const BwdIn<T>& bin,
+             const BwdEpi<T>& epi, const T* __restrict__ wpk, const WPack<T>& pk, const int bid,
+             const GatherIn& gin = GatherIn{}) {
   static_assert(CIN == 1 || CIN % 8 == 0, "CIN must be 1 or a multiple of 8");
   static_assert(COUT % 16 == 0, "COUT must be a multiple of 16");
   static_assert((H * W) % 4 == 0, "H*W must be a multiple of 4");
   static_assert(PRO != 2 || MODE == 2, "PRO 2 is a data-grad prologue");
+  static_assert(PRO != 3 || (CIN == 1 && MODE != 2), "PRO 3 gathers single-channel input images");
   static_assert(EPI == 0 || MODE == 2, "EPI 1 is a data-grad epilogue");
   constexpr int HP = H + 4, WPD = W + 4;
   constexpr int K = 25 * CIN;
@@ -522,9 +543,9 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
   __shared__ float lstat[(NTHR / 64) * 2 * COUT];
 
   const int tid = threadIdx.x;
-  const int b = blockIdx.x / nsplit;
+  const int b = bid / nsplit;
   DPA_STAMP(0);
-  const int sp = blockIdx.x % nsplit;
+  const int sp = bid % nsplit;
   const T* xb = x + (size_t)b * CIN * HW;
   const int mt0 = (MT * sp) / nsplit, mt1 = (MT * (sp + 1)) / nsplit;
   // epilogue operands of this lane's channels (co = nt*16 + lane%16), loaded up front
@@ -558,7 +579,7 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
     }
   };
   if constexpr (WPK == 1) {
-    if constexpr (PRO == 0) load_wpk();
+    if constexpr (PRO == 0 || PRO == 3) load_wpk();
   } else {
     if constexpr (KP > K) {
       for (int e = tid; e < COUT * (KP - K); e += NTHR) wl[(e / (KP - K)) * KPW + K + e % (KP - K)] = zero;
@@ -639,6 +660,47 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
       img[imo((h + 2) * WPD + (ww + 2), ci)] = a;
       img[imo((h + 2) * WPD + (ww + 3), ci)] = bb;
     });
+  } else if constexpr (PRO == 3) {
+    // step counter -> sample -> 4 uint8 pixels per lane load
+    static_assert(HW % 4 == 0 && W % 4 == 0, "4-pixel groups stay inside a row");
+    constexpr int G4 = HW / 4, GIT = (G4 + NTHR - 1) / NTHR;
+    const int step = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile int*>(gin.ctr));
+    long long pos = (long long)step * (gridDim.x / nsplit) + b;
+    pos = pos < gin.order_len ? pos : gin.order_len - 1;  // never taken with a correct host-side batch count
+    const int64_t src = gin.order[pos];
+    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(gin.imgs + src * HW);
+    uint32_t v4[GIT];
+#pragma unroll
+    for (int i = 0; i < GIT; ++i)
+      if (tid + i * NTHR < G4) v4[i] = s4[tid + i * NTHR];
+    if (sp == 0 && tid == 0) gin.lab_out[b] = gin.labels[src];
+    T* xo = const_cast<T*>(xb);
+#pragma unroll
+    for (int i = 0; i < GIT; ++i) {
+      const int g = tid + i * NTHR;
+      if (g < G4) {
+        const int h = (4 * g) / W, ww = (4 * g) % W;
+        T px[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          px[k] = Cvt<T>::from_f((float)((v4[i] >> (8 * k)) & 0xffu) * gin.scale + gin.shift);
+          img[imo((h + 2) * WPD + (ww + k + 2), 0)] = px[k];
+        }
+        if (sp == 0) {  // the batch buffer (conv1's weight gradient and the user read it)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) xo[4 * g + k] = px[k];
+        }
+      }
+    }
+    // advance the step counter once every workgroup has read it (relaxed: the next
+    // launch reads it after this one completes)
+    if (tid == 0) {
+      const int arrived = __hip_atomic_fetch_add(&gin.ctr[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (arrived == (int)gridDim.x - 1) {
+        __hip_atomic_store(&gin.ctr[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&gin.ctr[0], step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   } else if constexpr (PRO == 1) {
     __shared__ float sc_s[CIN], beta_s[CIN], mean_s[CIN], istd_s[CIN];
     __shared__ float part[NTHR];
@@ -657,7 +719,7 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
         bot[i] = src[W];  // next input row (2W elements = W pairs)
       }
     }
-    bn_finalize<CIN>(pin.bn, sc_s, beta_s, mean_s, istd_s, part, blockIdx.x == 0);
+    bn_finalize<CIN>(pin.bn, sc_s, beta_s, mean_s, istd_s, part, bid == 0);
     load_wpk();
     DPA_STAMP(3);
     // the pooled map / index / xhat outputs (for the backward) are written by all
@@ -687,7 +749,7 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
     BnBwdStage<T, CIN, H, W, NTHR> st;
     st.load(bin, b);
     DPA_STAMP(8);
-    bn_bwd_coef<CIN, T>(bin, coef, part, sums, blockIdx.x == 0);
+    bn_bwd_coef<CIN, T>(bin, coef, part, sums, bid == 0);
     load_epi();
     load_wpk();
     DPA_STAMP(3);
@@ -790,8 +852,8 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
       }
     }
     __syncthreads();
-    float* row = (MODE == 0 ? fslab + (size_t)blockIdx.x * fslab_row(COUT)
-                            : epi.bslab + (size_t)blockIdx.x * 2 * COUT);
+    float* row = (MODE == 0 ? fslab + (size_t)bid * fslab_row(COUT)
+                            : epi.bslab + (size_t)bid * 2 * COUT);
     if (tid < 2 * COUT) {
       float t = 0.f;
 #pragma unroll
@@ -803,10 +865,21 @@ conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float
         const int p0 = mt0 * 16, p1 = min(mt1 * 16, HW);
         row[2 * COUT] = (float)(p1 - p0);
       }
-      if (blockIdx.x == 0 && tid < COUT) fstats[2 * COUT + 1 + tid] = shift[tid];
+      if (bid == 0 && tid < COUT) fstats[2 * COUT + 1 + tid] = shift[tid];
     }
   }
   DPA_STAMP(7);
+}
+
+template <typename T, int CIN, int COUT, int H, int W, int MODE, int PRO = 0, int EPI = 0, int WPK = 0>
+__global__ void __launch_bounds__(NTHR)
+conv5x5_kernel(const T* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+               T* __restrict__ y, float* __restrict__ fslab, float* __restrict__ fstats,
+               const float* __restrict__ shift, int nsplit, PoolIn<T> pin = PoolIn<T>{},
+               BwdIn<T> bin = BwdIn<T>{}, BwdEpi<T> epi = BwdEpi<T>{}, const T* __restrict__ wpk = nullptr,
+               WPack<T> pk = WPack<T>{}, GatherIn gin = GatherIn{}) {
+  conv5x5_body<T, CIN, COUT, H, W, MODE, PRO, EPI, WPK>(x, w, bias, y, fslab, fstats, shift, nsplit, pin, bin, epi,
+                                                        wpk, pk, (int)blockIdx.x, gin);
 }
 
 // ---------------------------------------------------------------------------
@@ -1026,9 +1099,9 @@ bwd_elemt_kernel(const T* __restrict__ dp, const T* __restrict__ p, const uint8_
 // PRO 2: dy is produced on the fly from the pooled grad of the next block
 // (bin: backward through MaxPool -> ReLU -> BN); needs ROWS == H.
 template <typename T, int CIN, int COUT, int H, int W, int ROWS, int PRO = 0>
-__global__ void __launch_bounds__(NTHR)
-conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* __restrict__ wslab,
-                     int nsplit, BwdIn<T> bin = BwdIn<T>{}) {
+__device__ __forceinline__ void
+conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __restrict__ wslab, int nsplit,
+                   const BwdIn<T>& bin, const int bid) {
   static_assert(PRO == 0 || (PRO == 2 && ROWS % 2 == 0), "PRO 2 works on whole 2x2 pooling windows");
   constexpr int WP = ceil_to(W, 8);
   static_assert((ROWS * WP) % 32 == 0, "ROWS*WP must be a multiple of 32");
@@ -1052,7 +1125,7 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
   __shared__ f32x4 kred[KSPLIT > 1 ? NW : 1][64];
 
   const int tid = threadIdx.x;
-  const int b = blockIdx.x / nsplit, sp = blockIdx.x % nsplit;
+  const int b = bid / nsplit, sp = bid % nsplit;
   DPA_STAMP(0);
   const int r0 = sp * ROWS;
   const T* xb = x + (size_t)b * CIN * H * W;
@@ -1128,7 +1201,7 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
     } else {  // input rows r0-2 .. r0+ROWS+1 -> xpad (kw copies after the barrier below)
       stage_xpad();
     }
-    bn_bwd_coef<COUT, T>(bin, coef, part, sums, blockIdx.x == 0);
+    bn_bwd_coef<COUT, T>(bin, coef, part, sums, bid == 0);
     DPA_STAMP(3);
     st.emit(coef, [&](int co, int h, int ww, T v00, T v01, T v10, T v11) {
       dyl[(co * ROWS + h) * WP + ww] = v00;
@@ -1170,7 +1243,7 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
     __syncthreads();
   }
 
-  float* row_out = wslab + (size_t)blockIdx.x * ROWLEN;
+  float* row_out = wslab + (size_t)bid * ROWLEN;
   DPA_STAMP(5);
   const int lane = tid & 63, wv = tid >> 6;
   const int r = lane & 15, q = lane >> 4;
@@ -1229,6 +1302,13 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
     }
   }
   DPA_STAMP(7);
+}
+
+template <typename T, int CIN, int COUT, int H, int W, int ROWS, int PRO = 0>
+__global__ void __launch_bounds__(NTHR)
+conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* __restrict__ wslab,
+                     int nsplit, BwdIn<T> bin = BwdIn<T>{}) {
+  conv5x5_wgrad_body<T, CIN, COUT, H, W, ROWS, PRO>(x, dy, wslab, nsplit, bin, (int)blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------

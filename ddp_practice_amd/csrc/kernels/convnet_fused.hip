@@ -15,6 +15,8 @@
 // (reference model: /root/reference/origin_main.py:9-31.)  With SyncBN the
 // partial sums are all-reduced between the launches (host side).  Everything
 // is deterministic (no float atomics).
+#include <type_traits>
+
 #include "convblock_impl.h"
 #include "comm/xgmi.h"
 
@@ -388,6 +390,52 @@ void conv1_fwd_pack(at::Tensor x, at::Tensor w1, at::Tensor b1, at::Tensor y1, c
   DPA_CHECK_LAUNCH();
 }
 
+// conv1_fwd_pack with the batch gather fused in (training; cb::GatherIn): x and lab_out
+// are the loader's batch buffers, filled by this launch from the HBM-resident dataset
+// at the device step counter, which the launch then advances (data.hip protocol).
+void conv1_fwd_pack_gather(at::Tensor x, at::Tensor w1, at::Tensor b1, at::Tensor y1, at::Tensor fslab1,
+                           at::Tensor fstats1, at::Tensor shift1, at::Tensor w2, at::Tensor wpk_f, at::Tensor wpk_d,
+                           at::Tensor imgs, at::Tensor labels, at::Tensor order, at::Tensor ctr, at::Tensor lab_out,
+                           double scale, double shift) {
+  DPA_CHECK_INPUT(x); DPA_CHECK_INPUT(w1); DPA_CHECK_INPUT(b1); DPA_CHECK_INPUT(y1); DPA_CHECK_INPUT(w2);
+  DPA_CHECK_INPUT(wpk_f); DPA_CHECK_INPUT(wpk_d); DPA_CHECK_INPUT(imgs); DPA_CHECK_INPUT(labels);
+  DPA_CHECK_INPUT(order); DPA_CHECK_INPUT(ctr); DPA_CHECK_INPUT(lab_out);
+  const int B = (int)x.size(0);
+  typedef cb::SH<0> S;
+  TORCH_CHECK(x.size(1) == 1 && x.size(2) == 28 && x.size(3) == 28 && w1.numel() == 16 * 25 && b1.numel() == 16,
+              "fused conv1 expects the ConvNet shapes");
+  TORCH_CHECK(imgs.scalar_type() == at::kByte && imgs.dim() == 3 && imgs.size(1) == 28 && imgs.size(2) == 28,
+              "gather: uint8 [N][28][28] dataset");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == imgs.size(0));
+  TORCH_CHECK(order.scalar_type() == at::kLong && ctr.scalar_type() == at::kInt && ctr.numel() >= 2);
+  TORCH_CHECK(lab_out.scalar_type() == at::kLong && lab_out.numel() == B);
+  TORCH_CHECK(w2.numel() == 32 * 16 * 25 && w2.scalar_type() == at::kFloat && w1.scalar_type() == at::kFloat);
+  TORCH_CHECK(y1.numel() == (int64_t)B * 16 * 784 && y1.scalar_type() == x.scalar_type());
+  TORCH_CHECK(wpk_f.numel() == cb::W2F_LEN && wpk_d.numel() == cb::W2D_LEN &&
+              wpk_f.scalar_type() == x.scalar_type() && wpk_d.scalar_type() == x.scalar_type());
+  TORCH_CHECK(fslab1.numel() == (int64_t)B * S::SPLIT * cb::fslab_row(16) && fstats1.numel() == cb::stats_len(16) &&
+              shift1.numel() == 16);
+  if (B == 0) return;
+  cb::GatherIn gin;
+  gin.imgs = imgs.data_ptr<uint8_t>();
+  gin.labels = labels.data_ptr<int64_t>();
+  gin.order = order.data_ptr<int64_t>();
+  gin.order_len = order.numel();
+  gin.ctr = ctr.data_ptr<int>();
+  gin.lab_out = lab_out.data_ptr<int64_t>();
+  gin.scale = (float)scale;
+  gin.shift = (float)shift;
+  with_t(dt_of(x), [&](auto tag) {
+    typedef decltype(tag) T;
+    cb::WPack<T> pk{w2.data_ptr<float>(), dptr<T>(wpk_f), dptr<T>(wpk_d)};
+    hipLaunchKernelGGL((cb::conv5x5_kernel<T, 1, 16, 28, 28, 0, 3, 0, 2>), dim3(B * S::SPLIT), dim3(cb::NTHR), 0,
+                       cur_stream(), dptr<T>(x), w1.data_ptr<float>(), b1.data_ptr<float>(), dptr<T>(y1),
+                       fslab1.data_ptr<float>(), fstats1.data_ptr<float>(), shift1.data_ptr<float>(), S::SPLIT,
+                       PoolIn<T>{}, BwdIn<T>{}, BwdEpi<T>{}, nullptr, pk, gin);
+  });
+  DPA_CHECK_LAUNCH();
+}
+
 constexpr int kDgradSplit = 2;
 int64_t dgrad2_rows(int64_t B) { return B * kDgradSplit; }
 
@@ -415,12 +463,73 @@ void conv2_dgrad(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx
   DPA_CHECK_LAUNCH();
 }
 
+// The backward through [BN2 -> ReLU2 -> pool2] feeds two independent products of
+// layer 2: the data grad (-> dp1 + BN1 partial sums, kDgradSplit workgroups per
+// image) and the weight-grad partials (WG2_ROWS-row chunks).  One launch hosts
+// both roles -- workgroups [0, ndg) the data grad, [ndg, grid) the weight grad --
+// so they overlap on the chip instead of running back to back (each alone fills
+// only 64 / 128 of the 256 CUs at B = 32) and one kernel boundary disappears.
+constexpr int WG2_ROWS_ = 4;
+int64_t wgrad_bn_rows(int64_t layer, int64_t B);
+template <typename T>
+__global__ void __launch_bounds__(cb::NTHR)
+conv2_bwd_kernel(const T* __restrict__ wpk_d, T* __restrict__ dp1, BwdIn<T> bi_d, BwdEpi<T> ep,
+                 const T* __restrict__ p1, float* __restrict__ wslab2, BwdIn<T> bi_w, int ndg) {
+  constexpr int nsw = (14 + WG2_ROWS_ - 1) / WG2_ROWS_;
+  if ((int)blockIdx.x < ndg)
+    cb::conv5x5_body<T, 32, 16, 14, 14, 2, 2, 1, 1>(nullptr, nullptr, nullptr, dp1, nullptr, nullptr, nullptr,
+                                                    kDgradSplit, PoolIn<T>{}, bi_d, ep, wpk_d, cb::WPack<T>{},
+                                                    (int)blockIdx.x);
+  else
+    cb::conv5x5_wgrad_body<T, 16, 32, 14, 14, WG2_ROWS_, 2>(p1, nullptr, wslab2, nsw, bi_w, (int)blockIdx.x - ndg);
+}
+
+// [pool2/ReLU2/BN2 backward] -> {conv2 data grad -> dp1 (+BN1 partial sums), conv2 weight-grad partials}
+void conv2_bwd(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx2, at::Tensor fstats2,
+               at::Tensor gsum2, at::Tensor g2, double eps2, at::Tensor dp1, at::Tensor idx1, at::Tensor xh1,
+               at::Tensor bslab1, at::Tensor p1, at::Tensor wslab2, XcPtr xc) {
+  DPA_CHECK_INPUT(y2); DPA_CHECK_INPUT(dp1); DPA_CHECK_INPUT(wpk_d); DPA_CHECK_INPUT(p1); DPA_CHECK_INPUT(wslab2);
+  TORCH_CHECK(wpk_d.numel() == cb::W2D_LEN && wpk_d.scalar_type() == y2.scalar_type(),
+              "packed conv2 data-grad weights");
+  const int B = (int)y2.size(0);
+  TORCH_CHECK(y2.size(1) == 32 && y2.size(2) == 14 && dp2.numel() == (int64_t)B * 32 * 49);
+  TORCH_CHECK(dp1.numel() == (int64_t)B * 16 * 196 && idx1.numel() == dp1.numel() && xh1.numel() == dp1.numel());
+  TORCH_CHECK(p1.numel() == dp1.numel() && p1.scalar_type() == y2.scalar_type());
+  TORCH_CHECK(bslab1.numel() == dgrad2_rows(B) * 32, "BN1 partial-sum slab size");
+  const int ndg = B * kDgradSplit, nwg = (int)wgrad_bn_rows(2, B);
+  TORCH_CHECK(wslab2.numel() == (int64_t)nwg * (32 * 400 + 32), "wgrad slab size");
+  if (B == 0) return;
+  with_t(dt_of(y2), [&](auto tag) {
+    typedef decltype(tag) T;
+    BwdIn<T> bd = bwd_in<T>(dp2, idx2, y2, fstats2, gsum2, c10::nullopt, g2, eps2, 32, c10::nullopt, c10::nullopt);
+    BwdIn<T> bw = bd;
+    bd.xs = site_of(xc, xgmi::kSiteBwd2Dgrad);
+    bw.xs = site_of(xc, xgmi::kSiteBwd2Wgrad);
+    bd.xs.nblk = ndg;  // each role's workgroups take tickets on their own site
+    bw.xs.nblk = nwg;
+    BwdEpi<T> ep{idx1.data_ptr<uint8_t>(), dptr<T>(xh1), bslab1.data_ptr<float>()};
+    if constexpr (std::is_same<T, float>::value) {
+      // fp32 tiles: the two roles' LDS (173 KB) exceed one CU's 160 KB -> two launches
+      bd.xs.nblk = bw.xs.nblk = 0;
+      hipLaunchKernelGGL((cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1, 1>), dim3(ndg), dim3(cb::NTHR), 0,
+                         cur_stream(), nullptr, nullptr, nullptr, dptr<T>(dp1), nullptr, nullptr, nullptr,
+                         kDgradSplit, PoolIn<T>{}, bd, ep, dptr<T>(wpk_d), cb::WPack<T>{});
+      hipLaunchKernelGGL((cb::conv5x5_wgrad_kernel<T, 16, 32, 14, 14, WG2_ROWS_, 2>), dim3(nwg), dim3(cb::NTHR), 0,
+                         cur_stream(), dptr<T>(p1), nullptr, wslab2.data_ptr<float>(), nwg / B, bw);
+    } else {
+      hipLaunchKernelGGL(conv2_bwd_kernel<T>, dim3(ndg + nwg), dim3(cb::NTHR), 0, cur_stream(), dptr<T>(wpk_d),
+                         dptr<T>(dp1), bd, ep, dptr<T>(p1), wslab2.data_ptr<float>(), bw, ndg);
+    }
+  });
+  DPA_CHECK_LAUNCH();
+}
+
 // [pool/ReLU/BN backward of the block whose conv is (CIN->COUT, HxW)] -> weight-grad partials.
 // layer 2: x = p1 [B,16,14,14], (y, dp, idx) = layer-2 tensors; layer 1: x = images, layer-1 tensors.
 // Weight-gradient row chunks (BN backward applied on the fly per chunk): more,
 // shorter workgroups than one image each (B = 32 -> 32 workgroups for 256 CUs).
 constexpr int WG1_ROWS = 4;  // layer 1 (28 rows): 7 chunks per image
-constexpr int WG2_ROWS = 4;  // layer 2 (14 rows): 4 chunks per image (last one 2 rows)
+constexpr int WG2_ROWS = WG2_ROWS_;  // layer 2 (14 rows): 4 chunks per image (last one 2 rows)
 int64_t wgrad_bn_rows(int64_t layer, int64_t B) {
   TORCH_CHECK(layer == 1 || layer == 2);
   return B * (layer == 1 ? (28 + WG1_ROWS - 1) / WG1_ROWS : (14 + WG2_ROWS - 1) / WG2_ROWS);
@@ -470,6 +579,8 @@ bool sites_resident(int64_t B, at::ScalarType st) {
     ok = ok && co_resident(reinterpret_cast<const void*>(&head_fwd_kernel<T, 32, 14, 14, 16>), (int)B, HF, 0) &&
          co_resident(reinterpret_cast<const void*>(&head_fwd_kernel<T, 32, 14, 14, 64>), (int)B, HF, 0);
     chk(reinterpret_cast<const void*>(&cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1, 1>), B * kDgradSplit);
+    if constexpr (!std::is_same<T, float>::value)
+      chk(reinterpret_cast<const void*>(&conv2_bwd_kernel<T>), B * kDgradSplit + wgrad_bn_rows(2, B));
     chk(reinterpret_cast<const void*>(&cb::conv5x5_wgrad_kernel<T, 16, 32, 14, 14, WG2_ROWS, 2>),
         wgrad_bn_rows(2, B));
     chk(reinterpret_cast<const void*>(&cb::conv5x5_wgrad_kernel<T, 1, 16, 28, 28, WG1_ROWS, 2>),
@@ -489,6 +600,7 @@ void register_convnet_fused(pybind11::module& m) {
   s.def("head_bwd_lds", &cnf::head_bwd_lds);
   s.def("dgrad2_rows", &cnf::dgrad2_rows);
   s.def("conv1_fwd_pack", &cnf::conv1_fwd_pack);
+  s.def("conv1_fwd_pack_gather", &cnf::conv1_fwd_pack_gather);
 #ifdef DPA_TIMING
   s.def("read_stamps", []() {
     auto out = at::empty({DPA_MAX_STAMP_BLOCKS, DPA_NSTAMPS}, at::TensorOptions().dtype(at::kLong));
@@ -506,6 +618,7 @@ void register_convnet_fused(pybind11::module& m) {
   s.attr("W2F_LEN") = cb::W2F_LEN;
   s.attr("W2D_LEN") = cb::W2D_LEN;
   s.def("conv2_dgrad", &cnf::conv2_dgrad);
+  s.def("conv2_bwd", &cnf::conv2_bwd);
   s.def("conv_wgrad_bn", &cnf::conv_wgrad_bn);
   s.def("wgrad_bn_rows", &cnf::wgrad_bn_rows);
   s.def("sites_resident", &cnf::sites_resident);

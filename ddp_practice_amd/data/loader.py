@@ -103,10 +103,29 @@ class DeviceLoader:
         labels = torch.empty((b,), dtype=torch.int64, device=self.device)
         return imgs, labels
 
-    def fill_(self, images: torch.Tensor, labels: torch.Tensor, step: int = -1) -> None:
-        """Gather batch ``step`` (or the device counter's step if -1, advancing it)."""
+    @staticmethod
+    def pair(images: torch.Tensor, labels: torch.Tensor) -> None:
+        """Record that ``labels`` are the targets of ``images``: a training forward of the
+        fused ConvNet then computes the loss (and the head backward) in its head launch,
+        and the loss call on the same ``labels`` launches nothing (ops/convnet_fused.py)."""
+        images._dpa_labels = labels
+
+    def fill_(self, images: torch.Tensor, labels: torch.Tensor, step: int = -1, defer: bool = False) -> None:
+        """Gather batch ``step`` (or the device counter's step if -1, advancing it).
+
+        ``defer=True`` (device counter only): launch nothing; the gather is recorded on
+        ``images`` and performed by the first kernel of a model that consumes it
+        (the fused ConvNet's conv1, csrc/kernels/convblock_impl.h PRO 3).  Any other
+        reader must call ``flush_pending(images)`` first; ``accepts_deferred`` says
+        whether a model does it itself.
+        """
+        self.pair(images, labels)
         if self._order is None:
             self.start_epoch()
+        if defer and step < 0 and self.device.type == "cuda":
+            images._dpa_gather = (self._imgs, self._labels, self._order, self._ctr, labels, 1.0 / 255.0, 0.0)
+            return
+        images._dpa_gather = None
         if self.device.type == "cuda":
             _load_ext().data.gather(self._imgs, self._labels, self._order, self._ctr, int(step), images, labels,
                                     1.0 / 255.0, 0.0)
@@ -134,8 +153,27 @@ class DeviceLoader:
 
     def _fill_tail(self, imgs, labels, i):
         # partial last batch: explicit step index, batch_size stride
+        self.pair(imgs, labels)
         if self.device.type == "cuda":
             sub = self._order[i * self.batch_size:]
             _load_ext().data.gather(self._imgs, self._labels, sub, self._ctr, 0, imgs, labels, 1.0 / 255.0, 0.0)
         else:
             self.fill_(imgs, labels, step=i)
+
+
+def flush_pending(images: torch.Tensor) -> None:
+    """Perform a deferred gather (``DeviceLoader.fill_(..., defer=True)``) now, if any."""
+    g = getattr(images, "_dpa_gather", None)
+    if g is None:
+        return
+    images._dpa_gather = None
+    imgs, labels, order, ctr, lab_out, scale, shift = g
+    _load_ext().data.gather(imgs, labels, order, ctr, -1, images, lab_out, scale, shift)
+
+
+def accepts_deferred(model, images: torch.Tensor) -> bool:
+    """Whether ``model(images)`` performs a deferred gather itself (so a training step
+    may hand it the batch without the separate gather launch)."""
+    m = getattr(model, "module", model)
+    f = getattr(m, "accepts_deferred_batch", None)
+    return bool(f is not None and images.is_cuda and f(images))

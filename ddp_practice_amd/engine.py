@@ -83,11 +83,15 @@ class TrainLoop:
         if scaler is not None and getattr(scaler, "_enabled", False) and hasattr(model, "defer_grad_sync_to"):
             model.defer_grad_sync_to(optimizer)
         self.global_step = 0
+        # the model's first kernel gathers the batch itself (no gather launch per step)
+        from .data.loader import accepts_deferred
+
+        self._defer = accepts_deferred(model, self.images)
 
     # -- one step on the static buffers (what gets captured)
     def _step(self, images=None, labels=None, fill=True, before_update=None):
         if fill:
-            self.loader.fill_(self.images, self.labels)
+            self.loader.fill_(self.images, self.labels, defer=self._defer)
         images = self.images if images is None else images
         labels = self.labels if labels is None else labels
         with trace_range("forward"):

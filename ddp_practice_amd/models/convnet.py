@@ -91,7 +91,21 @@ class ConvNet(nn.Module):
         out = out.reshape(out.size(0), -1)
         return self.fc(out)
 
+    def accepts_deferred_batch(self, x: torch.Tensor) -> bool:
+        """The fused forward performs a deferred batch gather (data/loader.py) itself:
+        conv1 reads the HBM-resident dataset directly."""
+        if not (self.fused is True and x.is_cuda):
+            return False
+        from ..ops import convnet_fused
+
+        want = self.amp_dtype if self.amp_dtype is not None else torch.float32
+        return x.dtype == want and x.is_contiguous() and self._native_ok(x) and convnet_fused.supported(self, x)
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if getattr(x, "_dpa_gather", None) is not None and not (self.training and self.accepts_deferred_batch(x)):
+            from ..data.loader import flush_pending
+
+            flush_pending(x)
         native = self._native_ok(x)
         fwd = self._forward_native if native else self._forward_torch
         if self.amp_dtype is not None:

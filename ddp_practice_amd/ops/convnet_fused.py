@@ -52,6 +52,7 @@ def supported(model, x: torch.Tensor) -> bool:
 
 
 _RESIDENT: dict = {}
+_SPLIT_BWD2 = os.environ.get("DPA_SPLIT_BWD2", "0") == "1"
 
 
 def _fused_site_engine(comm, batch: int, dtype: torch.dtype):
@@ -73,9 +74,38 @@ def _fused_site_engine(comm, batch: int, dtype: torch.dtype):
     return xc if _RESIDENT[key] else None
 
 
+class PreCE:
+    """The loss a head-step launch already computed for (logits, labels, scale): the
+    ``cross_entropy`` call finds it here and launches nothing (ops/head.py)."""
+
+    __slots__ = ("target", "ignore_index", "smoothing", "scale", "loss", "dlog", "dls")
+
+    def __init__(self, target, ignore_index, smoothing, scale, loss, dlog, dls):
+        self.target, self.ignore_index, self.smoothing = target, ignore_index, smoothing
+        self.scale, self.loss, self.dlog, self.dls = scale, loss, dlog, dls
+
+
+_HEAD_OK: dict = {}
+HEAD_TIMEOUT_S = float(os.environ.get("DPA_HEAD_TIMEOUT", "30"))
+
+
+def _head_step_ok(B: int, N: int, dtype: torch.dtype) -> bool:
+    """The one-launch head (csrc/kernels/convnet_head.hip) handles this shape and its 32
+    workgroups are co-resident.  DPA_HEAD_STEP=0 forces the three-launch head (A/B)."""
+    if os.environ.get("DPA_HEAD_STEP", "1") == "0":
+        return False
+    H = _load_ext().convnet_head
+    if not H.supported(B, N):
+        return False
+    if dtype not in _HEAD_OK:
+        _HEAD_OK[dtype] = bool(H.resident(dtype))
+    return _HEAD_OK[dtype]
+
+
 class ConvNetFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w1, b1, g1, be1, w2, b2, g2, be2, wfc, bfc, bufs, training, moms, epss, comm, cdtype):
+    def forward(ctx, x, w1, b1, g1, be1, w2, b2, g2, be2, wfc, bfc, bufs, training, moms, epss, comm, cdtype,
+                labels=None, ce_cfg=(-100, 0.0), holder=None, state=None, gather=None):
         cb, cn = _mods()
         rm1, rv1, nbt1, rm2, rv2, nbt2 = bufs
         m1, m2 = (-1.0 if m is None else float(m) for m in moms)
@@ -105,15 +135,55 @@ class ConvNetFn(torch.autograd.Function):
             p2 = torch.empty((B, 32 * 49), dtype=cdtype, device=dev)
             idx2 = torch.empty((B, 32 * 49), dtype=torch.uint8, device=dev)
             xh2 = torch.empty((B, 32 * 49), dtype=cdtype, device=dev)
-            cn.conv1_fwd_pack(x, w1, b1, y1, fslab1, fstats1, rm1, w2, wpk_f, wpk_d)
+            if gather is not None:  # the batch gather runs inside conv1 (data/loader.py defer=True)
+                imgs, lbls, order, ctr, lab_out, gsc, gsh = gather
+                cn.conv1_fwd_pack_gather(x, w1, b1, y1, fslab1, fstats1, rm1, w2, wpk_f, wpk_d, imgs, lbls, order,
+                                         ctr, lab_out, gsc, gsh)
+            else:
+                cn.conv1_fwd_pack(x, w1, b1, y1, fslab1, fstats1, rm1, w2, wpk_f, wpk_d)
             if sync and xc is None:
                 comm.all_reduce_(fslab1)
             cn.conv2_fwd(y1, fslab1, fstats1, g1, be1, rm1, rv1, nbt1, m1, e1, True, w2, b2, y2, fslab2, fstats2,
                          rm2, p1, idx1, xh1, wpk_f, xc)
             if sync and xc is None:
                 comm.all_reduce_(fslab2)
-            cn.head_fwd(y2, fslab2, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, True, wfc, bfc, logits, p2, idx2, xh2,
-                        xc)
+            ctx.spec = None
+            if labels is not None and state is not None and _head_step_ok(B, N, cdtype):
+                # labels known now (paired by the device loader): head forward + loss (+ the head
+                # backward when a GradScaler will seed it with its scale) in one launch
+                from ..amp.grad_scaler import active_scale
+
+                scale = active_scale(dev)
+                f32 = dict(dtype=torch.float32, device=dev)
+                part = torch.empty(32 * B * 16, **f32)
+                loss_buf = torch.empty(2, **f32)
+                dlog = torch.empty((B, N), **f32)
+                dls = torch.empty((B, N), dtype=cdtype, device=dev) if scale is not None else None
+                spec = None
+                if scale is not None:
+                    s_w1, s_w2, s_wfc = w1.shape, w2.shape, wfc.shape
+                    sizes = [s_w1.numel(), 16, 16, 16, s_w2.numel(), 32, 32, 32, s_wfc.numel(), N]
+                    out = torch.empty(sum(sizes), **f32)
+                    views = out.split(sizes)
+                    dp2 = torch.empty_like(p2)
+                    bsum2 = torch.empty(64, **f32)
+                    dlsf = torch.empty(B * N, **f32)
+                    spec = (dls, out, views, dp2, bsum2)
+                    _load_ext().convnet_head.head_step(
+                        y2, fslab2, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, wfc, bfc, logits, p2, idx2, xh2, labels,
+                        int(ce_cfg[0]), float(ce_cfg[1]), scale, part, state, loss_buf, dlog, dls, dlsf, dp2,
+                        views[8], views[9], views[6], views[7], bsum2, xc, HEAD_TIMEOUT_S)
+                else:
+                    _load_ext().convnet_head.head_step(
+                        y2, fslab2, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, wfc, bfc, logits, p2, idx2, xh2, labels,
+                        int(ce_cfg[0]), float(ce_cfg[1]), None, part, state, loss_buf, dlog, None, None, None, None,
+                        None, None, None, None, xc, HEAD_TIMEOUT_S)
+                ctx.spec = spec
+                if holder is not None:
+                    holder["ce"] = PreCE(labels, int(ce_cfg[0]), float(ce_cfg[1]), scale, loss_buf, dlog, dls)
+            else:
+                cn.head_fwd(y2, fslab2, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, True, wfc, bfc, logits, p2, idx2,
+                            xh2, xc)
             ctx.save_for_backward(x, wpk_d, wfc, g1, g2, y1, p1, idx1, xh1, fstats1, y2, p2, idx2, xh2, fstats2)
         else:
             cn.conv1_fwd_pack(x, w1, b1, y1, None, None, None, w2, wpk_f, wpk_d)
@@ -143,24 +213,39 @@ class ConvNetFn(torch.autograd.Function):
         s_w1, s_w2, s_wfc = ctx.shapes
         n_w1, n_w2, n_wfc = s_w1.numel(), s_w2.numel(), s_wfc.numel()
         N = s_wfc[0]
-        # one output buffer for every parameter gradient (views handed to autograd);
-        # [dW1 | db1] and [dW2 | db2] are the rows of the two weight-grad slabs
-        sizes = [n_w1, 16, 16, 16, n_w2, 32, 32, 32, n_wfc, N]
-        out = torch.empty(sum(sizes), dtype=torch.float32, device=dev)
-        dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, dwfc, dbfc = out.split(sizes)
         f32 = dict(dtype=torch.float32, device=dev)
-        # 1. fc backward -> dp2, fc grads, BN2 sums (complete per channel on this rank)
-        bsum2 = torch.empty(64, **f32)
-        dp2 = torch.empty_like(p2)
-        cn.head_bwd(dl, wfc, p2, idx2, xh2, dwfc, dbfc, dg2, dbe2, bsum2, dp2)
+        ctx_spec = ctx.spec
+        if ctx_spec is not None and dlogits.data_ptr() == ctx_spec[0].data_ptr() and \
+                dlogits.dtype == ctx_spec[0].dtype:
+            # the gradient is the one the head-step launch predicted (the GradScaler seeded
+            # the loss with its scale): the fc backward and BN2 sums are already computed
+            # (references dropped: autograd then steals the returned gradient tensors
+            #  instead of copying each into .grad)
+            ctx.spec = spec = None
+            _, out, views, dp2, bsum2 = ctx_spec
+            dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, dwfc, dbfc = views
+            del views, ctx_spec
+        else:
+            # one output buffer for every parameter gradient (views handed to autograd);
+            # [dW1 | db1] and [dW2 | db2] are the rows of the two weight-grad slabs
+            sizes = [n_w1, 16, 16, 16, n_w2, 32, 32, 32, n_wfc, N]
+            out = torch.empty(sum(sizes), **f32)
+            dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, dwfc, dbfc = out.split(sizes)
+            # 1. fc backward -> dp2, fc grads, BN2 sums (complete per channel on this rank)
+            bsum2 = torch.empty(64, **f32)
+            dp2 = torch.empty_like(p2)
+            cn.head_bwd(dl, wfc, p2, idx2, xh2, dwfc, dbfc, dg2, dbe2, bsum2, dp2)
         gsum2 = comm.all_reduce(bsum2) if sync and xc is None else bsum2
-        # 2. BN2 bwd -> conv2 dgrad -> dp1 (+ BN1 partial sums)
+        # 2+3. BN2 bwd -> {conv2 dgrad -> dp1 (+ BN1 partial sums), conv2 wgrad partials}: one launch
+        #      (DPA_SPLIT_BWD2=1: the two as separate launches, A/B runs)
         dp1 = torch.empty((B, 16, 14, 14), dtype=y1.dtype, device=dev)
         bslab1 = torch.empty(cn.dgrad2_rows(B) * 32, **f32)
-        cn.conv2_dgrad(wpk_d, y2, dp2, idx2, fstats2, gsum2, g2, e2, dp1, idx1, xh1, bslab1, xc)
-        # 3. BN2 bwd -> conv2 wgrad partials (independent of 2)
         wslab2 = torch.empty(cn.wgrad_bn_rows(2, B) * (n_w2 + 32), **f32)
-        cn.conv_wgrad_bn(p1, y2, dp2, idx2, fstats2, gsum2, None, g2, e2, None, None, wslab2, xc)
+        if _SPLIT_BWD2:
+            cn.conv2_dgrad(wpk_d, y2, dp2, idx2, fstats2, gsum2, g2, e2, dp1, idx1, xh1, bslab1, xc)
+            cn.conv_wgrad_bn(p1, y2, dp2, idx2, fstats2, gsum2, None, g2, e2, None, None, wslab2, xc)
+        else:
+            cn.conv2_bwd(wpk_d, y2, dp2, idx2, fstats2, gsum2, g2, e2, dp1, idx1, xh1, bslab1, p1, wslab2, xc)
         # 4. BN1 bwd -> conv1 wgrad partials (+ dgamma1 / dbeta1 from the local sums)
         wslab1 = torch.empty(cn.wgrad_bn_rows(1, B) * (n_w1 + 16), **f32)
         if sync and xc is None:
@@ -172,11 +257,16 @@ class ConvNetFn(torch.autograd.Function):
         cb.slab_reduce(wslab1, n_w1 + 16, out.narrow(0, 0, n_w1 + 16), wslab2, n_w2 + 32,
                        out.narrow(0, n_w1 + 48, n_w2 + 32))
         return (None, dw1.view(s_w1), db1, dg1, dbe1, dw2.view(s_w2), db2, dg2, dbe2, dwfc.view(s_wfc), dbfc,
-                None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None)
 
 
 def convnet_forward(model, x, comm=None, cdtype=None):
-    """Run the reference ConvNet module tree through the fused op."""
+    """Run the reference ConvNet module tree through the fused op.
+
+    When ``x`` carries the labels of its batch (``DeviceLoader.fill_`` pairs them) and
+    the model trains, the head, the loss and the head backward run as one launch; the
+    returned logits then carry the computed loss for ``cross_entropy`` (ops/head.py).
+    """
     if cdtype is None:
         from ..amp import compute_dtype
 
@@ -188,6 +278,31 @@ def convnet_forward(model, x, comm=None, cdtype=None):
         raise RuntimeError("fused ConvNet: both BatchNorms must be in the same mode")
     bufs = (bn1.running_mean, bn1.running_var, bn1.num_batches_tracked,
             bn2.running_mean, bn2.running_var, bn2.num_batches_tracked)
-    return ConvNetFn.apply(x, c1.weight, c1.bias, bn1.weight, bn1.bias, c2.weight, c2.bias, bn2.weight, bn2.bias,
-                           fc.weight, fc.bias, bufs, training, (bn1.momentum, bn2.momentum), (bn1.eps, bn2.eps),
-                           comm, cdtype)
+    gather = getattr(x, "_dpa_gather", None)
+    if gather is not None:
+        if training and x.dtype == cdtype and x.is_contiguous():
+            x._dpa_gather = None  # consumed by conv1 below
+        else:
+            from ..data.loader import flush_pending
+
+            flush_pending(x)
+            gather = None
+    labels = getattr(x, "_dpa_labels", None) if training else None
+    holder, state = None, None
+    if labels is not None:
+        if labels.shape != (x.shape[0],) or labels.dtype != torch.int64 or labels.device != x.device:
+            labels = None
+        else:
+            holder = {}
+            state = getattr(model, "_dpa_head_state", None)
+            if state is None or state.device != x.device:
+                # ticket / flag / error words of the head-step launch (zeroed once; the
+                # kernel re-arms them itself, so graph replays need no reset)
+                state = torch.zeros(4, dtype=torch.int64, device=x.device)
+                model._dpa_head_state = state
+    out = ConvNetFn.apply(x, c1.weight, c1.bias, bn1.weight, bn1.bias, c2.weight, c2.bias, bn2.weight, bn2.bias,
+                          fc.weight, fc.bias, bufs, training, (bn1.momentum, bn2.momentum), (bn1.eps, bn2.eps),
+                          comm, cdtype, labels, (-100, 0.0), holder, state, gather)
+    if holder:
+        out._dpa_pre_ce = holder.get("ce")
+    return out

@@ -103,12 +103,42 @@ class CrossEntropyFn(torch.autograd.Function):
         return out, None, None, None, None
 
 
+class PrecomputedCEFn(torch.autograd.Function):
+    """The loss a fused head launch already produced (ops/convnet_fused.py PreCE): no
+    launch forward; backward as CrossEntropyFn (the scaled gradient when seeded)."""
+
+    @staticmethod
+    def forward(ctx, logits, pre):
+        ctx.pre = pre
+        ctx.ldtype = logits.dtype
+        ctx.token = _ScaledSeed(pre.scale) if pre.scale is not None else None
+        ctx.scaled = pre.loss[1] if pre.scale is not None else None
+        return pre.loss[0]
+
+    @staticmethod
+    def backward(ctx, grad):
+        tok = ctx.token
+        if tok is not None and tok.seeded:
+            return ctx.pre.dls, None
+        dlog = ctx.pre.dlog
+        out = torch.empty(dlog.shape, dtype=ctx.ldtype, device=dlog.device)
+        _H().ce_bwd(dlog, grad.reshape(1).to(torch.float32).contiguous(), out)
+        return out, None
+
+
 def cross_entropy(logits, target, ignore_index=-100, label_smoothing=0.0):
     if logits.dim() != 2:
         raise ValueError("native cross_entropy expects [B, C] logits")
     from ..amp.grad_scaler import active_scale
 
     scale = active_scale(logits.device) if logits.requires_grad else None
+    pre = getattr(logits, "_dpa_pre_ce", None)
+    if (pre is not None and pre.target is target and pre.ignore_index == ignore_index
+            and pre.smoothing == label_smoothing and pre.scale is scale and logits.requires_grad):
+        loss = PrecomputedCEFn.apply(logits, pre)
+        if scale is not None and loss.grad_fn is not None:
+            loss._dpa_ce = (loss.grad_fn, scale)
+        return loss
     loss = CrossEntropyFn.apply(logits, target, ignore_index, label_smoothing, scale)
     if scale is not None and loss.grad_fn is not None:
         node = loss.grad_fn

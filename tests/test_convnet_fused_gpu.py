@@ -168,3 +168,118 @@ def test_convnet_model_dispatches_fused(C):
     finally:
         convnet_fused.ConvNetFn.apply = orig
     assert calls == [1]
+
+
+def _step(m, x, y, paired, scaler):
+    from ddp_practice_amd.data import DeviceLoader
+    from ddp_practice_amd.ops.head import cross_entropy
+
+    xx = x.clone()
+    if paired:
+        DeviceLoader.pair(xx, y)
+    if scaler is not None:
+        scaler._lazy_init(x.device)  # the active scaler (as after its first step)
+    out = m(xx)
+    loss = cross_entropy(out, y)
+    (scaler.scale(loss) if scaler is not None else loss).backward()
+    return out, loss
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("B", [32, 12, 64])
+@pytest.mark.parametrize("use_scaler", [True, False])
+def test_head_step_matches_three_launch_head(C, dtype, B, use_scaler):
+    """Head forward + loss + head backward in one launch (labels paired with the batch,
+    csrc/kernels/convnet_head.hip) == the three-launch head (head_fwd, ce_fwd, head_bwd),
+    and the loss / head-backward launches really disappear."""
+    from ddp_practice_amd.amp import GradScaler
+
+    m1 = _model()
+    m1.amp_dtype = None if dtype == torch.float32 else dtype
+    m2 = copy.deepcopy(m1)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.rand(B, 1, 28, 28, generator=g).to(DEV, dtype if dtype != torch.float32 else torch.float32)
+    y = torch.randint(0, 10, (B,), generator=g).to(DEV)
+    y[1] = -100  # an ignored row
+    calls = {"head_bwd": 0, "ce_fwd": 0}
+    orig = {"head_bwd": C.convnet.head_bwd, "ce_fwd": C.head.ce_fwd}
+
+    def spy(name):
+        def f(*a):
+            calls[name] += 1
+            return orig[name](*a)
+        return f
+
+    out_a, loss_a = _step(m1, x, y, False, GradScaler() if use_scaler else None)
+    C.convnet.head_bwd, C.head.ce_fwd = spy("head_bwd"), spy("ce_fwd")
+    try:
+        out_b, loss_b = _step(m2, x, y, True, GradScaler() if use_scaler else None)
+    finally:
+        C.convnet.head_bwd, C.head.ce_fwd = orig["head_bwd"], orig["ce_fwd"]
+    torch.cuda.synchronize()
+    assert calls["ce_fwd"] == 0, "the loss was not taken from the head launch"
+    assert calls["head_bwd"] == (0 if use_scaler else 1)
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert _rel(out_b, out_a) < tol
+    assert abs(loss_b.item() - loss_a.item()) <= tol * max(1.0, abs(loss_a.item()))
+    for (n, p), (_, q) in zip(m1.named_parameters(), m2.named_parameters()):
+        if n.endswith("0.bias"):  # conv bias grad: 0 analytically (BN follows), rounding noise only
+            continue
+        assert _rel(q.grad, p.grad) < (1e-4 if dtype == torch.float32 else 3e-2), n
+    for (n, a), (_, b) in zip(m1.named_buffers(), m2.named_buffers()):
+        torch.testing.assert_close(a.float(), b.float(), rtol=1e-5, atol=1e-6, msg=n)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_deferred_gather_in_conv1(C, dtype):
+    """The batch gather folded into conv1 (DeviceLoader.fill_(defer=True), PRO 3) fills
+    the same batch buffers, advances the same device step counter and trains to the
+    same parameters as the separate gather launch, eagerly and graph-replayed."""
+    from ddp_practice_amd.amp import GradScaler
+    from ddp_practice_amd.data import DeviceLoader, accepts_deferred, synthetic
+    from ddp_practice_amd.nn import CrossEntropyLoss
+    from ddp_practice_amd.optim import SGD
+    from ddp_practice_amd.runtime import CapturedStep
+
+    ds = synthetic(32 * 12, seed=3)
+    amp = None if dtype == torch.float32 else dtype
+    runs = []
+    for defer in (False, True):
+        m = _model()
+        m.amp_dtype = amp
+        loader = DeviceLoader(ds, batch_size=32, shuffle=False, device=DEV, dtype=dtype)
+        images, labels = loader.static_batch()
+        assert accepts_deferred(m, images)
+        opt, scaler, crit = SGD(m.parameters(), lr=0.05), GradScaler(enabled=amp is not None), CrossEntropyLoss()
+        seen = []
+
+        def step():
+            loader.fill_(images, labels, defer=defer)
+            loss = crit(m(images), labels)
+            opt.zero_grad(set_to_none=True)
+            if amp is not None:
+                scaler.scale(loss).backward()
+                scaler.step(opt)
+                scaler.update()
+            else:
+                loss.backward()
+                opt.step()
+
+        loader.start_epoch()
+        for _ in range(3):  # eager
+            step()
+            seen.append((images.clone(), labels.clone()))
+        runner = CapturedStep(step, warmup=1, steps_per_graph=2)
+        assert runner.capture()
+        loader.set_step(5)
+        for _ in range(3):
+            runner.run()
+        seen.append((images.clone(), labels.clone()))
+        torch.cuda.synchronize()
+        runs.append((copy.deepcopy(m.state_dict()), seen, loader._ctr.clone()))
+    (sd_a, seen_a, ctr_a), (sd_b, seen_b, ctr_b) = runs
+    assert torch.equal(ctr_a, ctr_b) and int(ctr_b[0]) == 11 and int(ctr_b[1]) == 0
+    for (xa, ya), (xb, yb) in zip(seen_a, seen_b):
+        assert torch.equal(xa, xb) and torch.equal(ya, yb)
+    for k in sd_a:
+        torch.testing.assert_close(sd_a[k].float(), sd_b[k].float(), rtol=1e-5, atol=1e-6, msg=k)
