@@ -32,9 +32,14 @@ def active_scale(device: torch.device):
     ``loss * scale`` multiply nor the loss-backward launch.
     """
     sc = _ACTIVE() if _ACTIVE is not None else None
-    if sc is None or not sc._enabled or sc._scale is None or sc._scale.device != device:
+    if sc is None or not sc._enabled or device.type != "cuda":
         return None
-    return sc._scale
+    if sc._scale is None:
+        # a fresh scaler: create its scale now, so the very first step takes the same
+        # (pre-scaled) loss path as every later one -- eager and graph-captured training
+        # then run identical kernels from step 0 on
+        sc._lazy_init(device)
+    return sc._scale if sc._scale.device == device else None
 
 
 class _ScaledLossFn(torch.autograd.Function):
@@ -110,6 +115,9 @@ class GradScaler:
         self._fuse_step = fuse_step
         self._single_opt_iters = 0
         self._fused_done = False
+        if enabled and str(self._device).startswith("cuda"):
+            global _ACTIVE
+            _ACTIVE = weakref.ref(self)  # the newest scaler is the one native losses pre-scale for
 
     # ------------------------------------------------------------------ state
     def _lazy_init(self, dev: torch.device):

@@ -157,8 +157,10 @@ class RcclComm : public Collective {
     const RedOp rop = parse_op(op);
     // on the comm stream like every collective: one total order per rank = issue order
     fenced([&](hipStream_t s) {
-      if (use_xgmi(t, dst, rop))
+      if (const int r = route(t, dst, rop); r == 1)
         xgmi_->all_reduce(t, dst, rop, s);
+      else if (r == 2)
+        xgmi_->all_reduce_twoshot(t, dst, rop, s);
       else
         DPA_NCCL(ncclAllReduce(t.data_ptr(), dst.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(rop),
                                comm_.load(), s));
@@ -231,25 +233,30 @@ class RcclComm : public Collective {
     const int i = next_++ % kRing;
     DPA_CHECK_HIP(hipEventRecord(fork_[i], cur));
     DPA_CHECK_HIP(hipStreamWaitEvent(stream_.stream(), fork_[i], 0));
-    if (use_xgmi(t, t, op))
+    if (const int r = route(t, t, op); r == 1)
       xgmi_->all_reduce(t, t, op, stream_.stream());
+    else if (r == 2)
+      xgmi_->all_reduce_twoshot(t, t, op, stream_.stream());
     else
       DPA_NCCL(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t), nccl_op(op), comm_.load(),
                              stream_.stream()));
     DPA_CHECK_HIP(hipEventRecord(slot_[slot], stream_.stream()));
   }
 
-  // Route all-reduces of at most `max_bytes` to the one-shot xGMI engine
-  // (max_bytes <= 0: detach).  Every rank must attach the same way.
-  void attach_xgmi(std::shared_ptr<xgmi::XgmiComm> x, long long max_bytes) {
+  // Route all-reduces of at most `max_bytes` to the one-shot xGMI engine and the ones
+  // above it, up to `twoshot_max_bytes`, to its two-shot (reduce-scatter + all-gather);
+  // RCCL above that (max_bytes <= 0: detach).  Every rank must attach the same way.
+  void attach_xgmi(std::shared_ptr<xgmi::XgmiComm> x, long long max_bytes, long long twoshot_max_bytes) {
     if (x) {
       TORCH_CHECK(x->device() == device_ && x->world() == world_ && x->rank() == rank_,
                   "xgmi engine does not match this communicator");
     }
     xgmi_ = max_bytes > 0 ? std::move(x) : nullptr;
     xgmi_max_ = xgmi_ ? std::min(max_bytes, xgmi_->max_bytes()) : 0;
+    ts_max_ = xgmi_ ? std::min(twoshot_max_bytes, xgmi_->twoshot_max_bytes()) : 0;
   }
   long long xgmi_max_bytes() const { return xgmi_ ? xgmi_max_ : 0; }
+  long long twoshot_max_bytes() const { return xgmi_ ? ts_max_ : 0; }
 
   void wait(int slot, hipStream_t stream) override {
     TORCH_CHECK(slot >= 0 && slot < kSlots, "slot out of range");
@@ -257,9 +264,14 @@ class RcclComm : public Collective {
   }
 
  private:
-  bool use_xgmi(const at::Tensor& in, const at::Tensor& out, RedOp op) const {
-    return xgmi_ && op != RedOp::PROD && (long long)in.nbytes() <= xgmi_max_ && xgmi_->supports(in) &&
-           xgmi_->supports(out);
+  // 0: RCCL, 1: xGMI one-shot, 2: xGMI two-shot.  A pure function of (size, dtype,
+  // alignment, op): identical on every rank for the same collective.
+  int route(const at::Tensor& in, const at::Tensor& out, RedOp op) const {
+    if (!xgmi_ || op == RedOp::PROD) return 0;
+    const long long nb = (long long)in.nbytes();
+    if (nb <= xgmi_max_ && xgmi_->supports(in) && xgmi_->supports(out)) return 1;
+    if (nb <= ts_max_ && xgmi_->supports_twoshot(in) && xgmi_->supports_twoshot(out)) return 2;
+    return 0;
   }
 
   static constexpr int kRing = 64;
@@ -291,7 +303,7 @@ class RcclComm : public Collective {
   int next_ = 0;
   at::Tensor barrier_buf_;
   std::shared_ptr<xgmi::XgmiComm> xgmi_;
-  long long xgmi_max_ = 0;
+  long long xgmi_max_ = 0, ts_max_ = 0;
 };
 
 // Python-implemented collective (torch.distributed / gloo on CPU; tests).
@@ -347,8 +359,10 @@ void register_comm(pybind11::module& m) {
         c.all_reduce_async(t, parse_op(op), slot);
       })
       .def("wait", [](comm::RcclComm& c, int slot) { c.wait(slot, nullptr); })
-      .def("attach_xgmi", &comm::RcclComm::attach_xgmi, py::arg("engine"), py::arg("max_bytes"))
+      .def("attach_xgmi", &comm::RcclComm::attach_xgmi, py::arg("engine"), py::arg("max_bytes"),
+           py::arg("twoshot_max_bytes") = 0)
       .def_property_readonly("xgmi_max_bytes", &comm::RcclComm::xgmi_max_bytes)
+      .def_property_readonly("twoshot_max_bytes", &comm::RcclComm::twoshot_max_bytes)
       .def("async_error", &comm::RcclComm::async_error)
       .def("abort", &comm::RcclComm::abort)
       .def("destroy", &comm::RcclComm::destroy);

@@ -20,7 +20,8 @@ struct Peers {
 class XgmiComm {
  public:
   // max_bytes: largest message this engine takes; timeout_s: bound on every wait
-  XgmiComm(int rank, int world, int device, long long max_bytes, double timeout_s);
+  // max_bytes: largest one-shot message; twoshot_max_bytes: largest two-shot message (0: none)
+  XgmiComm(int rank, int world, int device, long long max_bytes, double timeout_s, long long twoshot_max_bytes = 0);
   ~XgmiComm();
   XgmiComm(const XgmiComm&) = delete;
   XgmiComm& operator=(const XgmiComm&) = delete;
@@ -32,6 +33,11 @@ class XgmiComm {
   bool supports(const at::Tensor& t) const;
   // out may alias in; stream == nullptr: the caller's current stream
   void all_reduce(const at::Tensor& in, const at::Tensor& out, RedOp op, hipStream_t stream);
+  // reduce-scatter + all-gather over direct peer writes (large messages)
+  bool supports_twoshot(const at::Tensor& t) const;
+  void all_reduce_twoshot(const at::Tensor& in, const at::Tensor& out, RedOp op, hipStream_t stream);
+  long long twoshot_max_bytes() const { return ts_max_elems_ * 4; }  // as fp32
+  void set_twoshot_blocks(int g);  // grid of every two-shot launch (before the first one)
 
   // test entry: `grid` workgroups exchange `in` through SyncBN site s (comm/xsite.h)
   void site_probe(int s, const at::Tensor& in, const at::Tensor& out, int grid);
@@ -59,6 +65,10 @@ class XgmiComm {
   unsigned long long* ticks_ = nullptr;  // per-site {epoch | tickets} words (ordinary device memory)
   long long site_off_ = 0;               // byte offset of the fused-site regions in every workspace
   long long grad_off_ = 0;               // byte offset of the gradient-exchange region
+  long long ts_off_ = 0, ts_par_bytes_ = 0, ts_shard_max_ = 0, ts_max_elems_ = 0;  // two-shot region
+  int ts_blocks_ = 0, ts_grid_ = 0;
+  bool ts_used_ = false;
+  uint32_t* ts_ctr_ = nullptr;           // two-shot per-block epoch counters
   Peers peers_;
   int* host_words_ = nullptr;  // [0] error, [1] abort (host-mapped, coherent)
   int* dev_words_ = nullptr;

@@ -49,6 +49,7 @@ namespace xgmi {
 constexpr int kThreads = 256;
 constexpr int kPerThread = 8;                        // elements per lane
 constexpr int kChunkElems = kThreads * kPerThread;   // 2048 elements per block
+constexpr int kTwoShotMaxBlocks = 256;               // two-shot grid cap (one per CU)
 
 typedef __attribute__((ext_vector_type(2))) unsigned long long u64x2;
 
@@ -189,7 +190,205 @@ __global__ __launch_bounds__(kThreads) void oneshot_kernel(Args a) {
   DPA_STAMP(3);
 }
 
-XgmiComm::XgmiComm(int rank, int world, int device, long long slot_bytes, double timeout_s)
+// ---------------------------------------------------------------------------
+// Two-shot all-reduce for large messages (DDP buckets of MBs): reduce-scatter then
+// all-gather, both as direct peer writes over the 7 xGMI links.
+//
+// A one-shot pushes the whole message to every peer: (W-1) * S bytes out per rank
+// (W = 8, 25 MiB bucket: 175 MiB per rank).  Here rank r owns shard r of the
+// message (S/W elements): every rank pushes each peer only that peer's shard
+// (reduce-scatter, (W-1)/W * S), the owner sums the W contributions in rank order,
+// then pushes its reduced shard to every peer (all-gather, (W-1)/W * S again) --
+// 2 (W-1)/W * S per rank, spread over all W-1 links at once (a ring moves the same
+// bytes over one link per direction).  SURVEY.md §2.6 item 2.
+//
+// Same transport as the one-shot: {value, epoch} 8-byte granules (value and tag
+// land together: no flag, no fence), bounded waits, per-block epochs kept in device
+// memory (graph-replayable), parity double-buffering.  Block b handles chunk b
+// (kChunkElems elements) of EVERY shard, so a block's reduce-scatter output is its
+// own all-gather input.  The reduced shard is rounded to the storage dtype before
+// it is pushed, so every rank's result is bit-identical.  The region and the epoch
+// counters are its own (a one-shot and a two-shot never share bytes: a peer may
+// still be reading one collective's granules while this rank starts the next).
+//   region layout, per parity: [RS: W src slots x shard] [AG: the whole message]
+struct TSArgs {
+  Peers peers;              // every rank's two-shot region
+  const void* in;
+  void* out;
+  long long n;              // elements
+  long long shard;          // elements per shard (multiple of kChunkElems)
+  long long stride;         // region slot stride in granules (the largest shard): block b
+                            // touches the same bytes whatever the message size, so its
+                            // per-block epoch alone tells its granules apart
+  long long par_bytes;      // bytes of one parity of the region
+  uint32_t* ctr;            // per-block epoch counters
+  int rank, world;
+  int* err;
+  const int* abort_flag;
+  long long timeout_ticks;
+};
+
+__device__ __forceinline__ bool ts_wait(const TSArgs& a, const unsigned long long* src, unsigned long long& g,
+                                        uint32_t ep, long long t0, unsigned& polls) {
+  while ((uint32_t)(g >> 32) != ep) {
+    __builtin_amdgcn_s_sleep(1);
+    g = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if ((++polls & 255u) == 0) {
+      int why = 0;
+      if (__hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) why = 2;
+      else if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) why = 1;
+      if (why) {
+        __hip_atomic_store(a.err, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return false;
+      }
+    }
+  }
+  return true;
+}
+
+template <typename T>
+__device__ __forceinline__ void ts_load8(const T* p, long long e0, long long n, float (&v)[kPerThread]) {
+  const int ne = (int)max(0LL, min((long long)kPerThread, n - e0));
+  if (ne == kPerThread) {
+    if constexpr (sizeof(T) == 4) {
+      const f32x4 x0 = reinterpret_cast<const f32x4*>(p + e0)[0], x1 = reinterpret_cast<const f32x4*>(p + e0)[1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[j] = x0[j]; v[4 + j] = x1[j]; }
+    } else {
+      const f32x4 raw = *reinterpret_cast<const f32x4*>(p + e0);
+      const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+      for (int j = 0; j < kPerThread; ++j) v[j] = Cvt<T>::to_f(e[j]);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kPerThread; ++j) v[j] = j < ne ? Cvt<T>::to_f(p[e0 + j]) : 0.f;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void ts_store8(T* p, long long e0, long long n, const float (&v)[kPerThread]) {
+  const int ne = (int)max(0LL, min((long long)kPerThread, n - e0));
+  if (ne == kPerThread) {
+    if constexpr (sizeof(T) == 2) {
+      f32x4 raw;
+      T* r = reinterpret_cast<T*>(&raw);
+#pragma unroll
+      for (int j = 0; j < kPerThread; ++j) r[j] = Cvt<T>::from_f(v[j]);
+      *reinterpret_cast<f32x4*>(p + e0) = raw;
+    } else {
+      reinterpret_cast<f32x4*>(p + e0)[0] = f32x4{v[0], v[1], v[2], v[3]};
+      reinterpret_cast<f32x4*>(p + e0)[1] = f32x4{v[4], v[5], v[6], v[7]};
+    }
+  } else {
+    for (int j = 0; j < ne; ++j) p[e0 + j] = Cvt<T>::from_f(v[j]);
+  }
+}
+
+__device__ __forceinline__ void push8(unsigned long long* dst, const float (&v)[kPerThread], uint32_t ep) {
+#pragma unroll
+  for (int j = 0; j < kPerThread; j += 2)
+    *reinterpret_cast<u64x2*>(dst + j) = u64x2{granule(v[j], ep), granule(v[j + 1], ep)};
+}
+
+// op: 0 sum, 1 avg, 2 max, 3 min.  A FIXED grid of G blocks (every call): block b
+// owns chunks b, b+G, b+2G, ... of every shard.  Every block bumps its epoch once per
+// call, so all blocks' epochs equal the call count and a chunk's slot is always
+// written by the same block index on every rank; G is small enough that the grids of
+// all ranks can be resident together even when ranks share a GPU (tests), and a block
+// never waits on a block of its own rank.
+template <typename T, int OP>
+__global__ __launch_bounds__(kThreads) void twoshot_kernel(TSArgs a) {
+  const int b = blockIdx.x, tid = threadIdx.x, G = gridDim.x;
+  uint32_t* ctr = a.ctr + b;
+  const uint32_t ep = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const long long par = (long long)(ep & 1u) * a.par_bytes;
+  const long long nch = a.shard / kChunkElems;                                      // chunks per shard
+  const long long rs_bytes = (long long)a.world * a.stride * 8;                     // RS part of a parity
+  const T* in = static_cast<const T*>(a.in);
+  T* out = static_cast<T*>(a.out);
+  char* mybase = a.peers.base[a.rank] + par;
+  // 1. reduce-scatter push: peer p gets my chunk c of its shard p, into its RS slot [me]
+  for (long long c = b; c < nch; c += G) {
+    const long long c0 = c * kChunkElems + (long long)tid * kPerThread;  // offset inside a shard
+    for (int i = 1; i < a.world; ++i) {
+      const int p = (a.rank + i) % a.world;  // staggered: the ranks start on different links
+      float v[kPerThread];
+      ts_load8<T>(in, (long long)p * a.shard + c0, a.n, v);
+      push8(reinterpret_cast<unsigned long long*>(a.peers.base[p] + par + ((long long)a.rank * a.stride + c0) * 8),
+            v, ep);
+    }
+  }
+  bool ok = true;
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  unsigned polls = 0;
+  const float s = OP == 1 ? 1.f / (float)a.world : 1.f;
+  // 2. my shard's chunks: the W contributions in rank order (identical on every rank),
+  //    rounded to the storage dtype once, then pushed to every peer's AG part
+  for (long long c = b; c < nch && ok; c += G) {
+    const long long c0 = c * kChunkElems + (long long)tid * kPerThread;
+    const long long mine_off = (long long)a.rank * a.shard + c0;
+    float acc[kPerThread];
+    for (int p = 0; p < a.world; ++p) {
+      float v[kPerThread];
+      if (p == a.rank) {
+        ts_load8<T>(in, mine_off, a.n, v);
+      } else {
+        const unsigned long long* src =
+            reinterpret_cast<const unsigned long long*>(mybase + ((long long)p * a.stride + c0) * 8);
+        unsigned long long g[kPerThread];
+#pragma unroll
+        for (int j = 0; j < kPerThread; ++j)
+          g[j] = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+        for (int j = 0; j < kPerThread; ++j) {
+          if (ok) ok = ts_wait(a, src + j, g[j], ep, t0, polls);
+          v[j] = __uint_as_float((uint32_t)g[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kPerThread; ++j) {
+        if (p == 0) acc[j] = v[j];
+        else if (OP == 2) acc[j] = fmaxf(acc[j], v[j]);
+        else if (OP == 3) acc[j] = fminf(acc[j], v[j]);
+        else acc[j] += v[j];
+      }
+    }
+    if (!ok) break;
+#pragma unroll
+    for (int j = 0; j < kPerThread; ++j) acc[j] = Cvt<T>::to_f(Cvt<T>::from_f(acc[j] * s));
+    for (int i = 1; i < a.world; ++i) {
+      const int p = (a.rank + i) % a.world;
+      push8(reinterpret_cast<unsigned long long*>(a.peers.base[p] + par + rs_bytes +
+                                                  ((long long)a.rank * a.stride + c0) * 8),
+            acc, ep);
+    }
+    ts_store8<T>(out, mine_off, a.n, acc);
+  }
+  // 3. every other shard's chunks from my AG part
+  for (long long c = b; c < nch && ok; c += G) {
+    const long long c0 = c * kChunkElems + (long long)tid * kPerThread;
+    for (int i = 1; i < a.world && ok; ++i) {
+      const int q = (a.rank + a.world - i) % a.world;
+      const unsigned long long* src =
+          reinterpret_cast<const unsigned long long*>(mybase + rs_bytes + ((long long)q * a.stride + c0) * 8);
+      unsigned long long g[kPerThread];
+#pragma unroll
+      for (int j = 0; j < kPerThread; ++j) g[j] = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      float v[kPerThread];
+#pragma unroll
+      for (int j = 0; j < kPerThread; ++j) {
+        if (ok) ok = ts_wait(a, src + j, g[j], ep, t0, polls);
+        v[j] = __uint_as_float((uint32_t)g[j]);
+      }
+      if (ok) ts_store8<T>(out, (long long)q * a.shard + c0, a.n, v);
+    }
+  }
+  __syncthreads();
+  if (tid == 0 && ok) __hip_atomic_store(ctr, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+XgmiComm::XgmiComm(int rank, int world, int device, long long slot_bytes, double timeout_s, long long ts_bytes)
     : rank_(rank), world_(world), device_(device) {
   TORCH_CHECK(world >= 1 && world <= kMaxRanks, "xgmi: 1..", kMaxRanks, " ranks");
   TORCH_CHECK(rank >= 0 && rank < world);
@@ -203,7 +402,18 @@ XgmiComm::XgmiComm(int rank, int world, int device, long long slot_bytes, double
   ctr_off_ = 0;
   site_off_ = 2LL * kMaxRanks * slot_bytes_;  // then kSites fused-site regions (comm/xsite.h)
   grad_off_ = site_off_ + kSites * kSiteBytes;  // then the gradient-exchange slots [2][kMaxRanks]
-  ws_bytes_ = ((grad_off_ + 2LL * kMaxRanks * slot_bytes_ + 4095) / 4096) * 4096;
+  // then the two-shot region: 2 parities x ([W shards of RS slots] + [the whole message]),
+  // i.e. 2 x 2 x the message as granules; shards are whole chunks
+  ts_off_ = grad_off_ + 2LL * kMaxRanks * slot_bytes_;
+  if (ts_bytes > 0) {
+    const long long ts_elems = std::max(ts_bytes, 4LL) / 4;
+    ts_shard_max_ = ((ts_elems + world_ - 1) / world_ + kChunkElems - 1) / kChunkElems * kChunkElems;
+    ts_max_elems_ = ts_elems;
+    ts_par_bytes_ = 2LL * world_ * ts_shard_max_ * 8;
+    ts_blocks_ = kTwoShotMaxBlocks;
+    ts_grid_ = (int)std::min<long long>(kTwoShotMaxBlocks, ts_shard_max_ / kChunkElems);
+  }
+  ws_bytes_ = ((ts_off_ + 2 * ts_par_bytes_ + 4095) / 4096) * 4096;
   timeout_ticks_ = (long long)(timeout_s * 1e8);
   c10::hip::HIPGuard guard(device_);
   void* p = nullptr;
@@ -216,6 +426,13 @@ XgmiComm::XgmiComm(int rank, int world, int device, long long slot_bytes, double
   DPA_CHECK_HIP(hipMemset(c, 0, (size_t)max_blocks_ * sizeof(uint32_t)));
   DPA_CHECK_HIP(hipDeviceSynchronize());
   ctr_ = static_cast<uint32_t*>(c);
+  if (ts_blocks_ > 0) {
+    void* c2 = nullptr;
+    DPA_CHECK_HIP(hipMalloc(&c2, (size_t)ts_blocks_ * sizeof(uint32_t)));
+    DPA_CHECK_HIP(hipMemset(c2, 0, (size_t)ts_blocks_ * sizeof(uint32_t)));
+    DPA_CHECK_HIP(hipDeviceSynchronize());
+    ts_ctr_ = static_cast<uint32_t*>(c2);
+  }
   void* tk = nullptr;
   DPA_CHECK_HIP(hipMalloc(&tk, kSites * sizeof(unsigned long long)));
   DPA_CHECK_HIP(hipMemset(tk, 0, kSites * sizeof(unsigned long long)));
@@ -243,6 +460,8 @@ void XgmiComm::close() {
   (void)hipFree(local_);
   if (ctr_ != nullptr) (void)hipFree(ctr_);
   ctr_ = nullptr;
+  if (ts_ctr_ != nullptr) (void)hipFree(ts_ctr_);
+  ts_ctr_ = nullptr;
   if (ticks_ != nullptr) (void)hipFree(ticks_);
   ticks_ = nullptr;
   if (host_words_ != nullptr) (void)hipHostFree(host_words_);
@@ -314,6 +533,62 @@ void XgmiComm::all_reduce(const at::Tensor& in, const at::Tensor& out, RedOp op,
     default: DPA_XG(__half); break;
   }
 #undef DPA_XG
+  DPA_CHECK_LAUNCH();
+}
+
+void XgmiComm::set_twoshot_blocks(int g) {
+  TORCH_CHECK(g >= 1 && g <= kTwoShotMaxBlocks, "two-shot grid: 1..", kTwoShotMaxBlocks);
+  TORCH_CHECK(ts_blocks_ > 0, "no two-shot region");
+  // every block's epoch must stay equal: only while no two-shot has run yet
+  TORCH_CHECK(!ts_used_, "set_twoshot_blocks: the two-shot engine has already run");
+  ts_grid_ = (int)std::min<long long>(g, ts_shard_max_ / kChunkElems);
+}
+
+bool XgmiComm::supports_twoshot(const at::Tensor& t) const {
+  const auto st = t.scalar_type();
+  return opened_ && ts_blocks_ > 0 && t.is_cuda() && t.get_device() == device_ && t.is_contiguous() &&
+         (st == at::kFloat || st == at::kBFloat16 || st == at::kHalf) && t.numel() > 0 &&
+         (long long)t.numel() <= ts_max_elems_ && (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0;
+}
+
+void XgmiComm::all_reduce_twoshot(const at::Tensor& in, const at::Tensor& out, RedOp op, hipStream_t stream) {
+  TORCH_CHECK(supports_twoshot(in) && supports_twoshot(out) && in.numel() == out.numel() &&
+                  in.scalar_type() == out.scalar_type(),
+              "xgmi two-shot all_reduce: unsupported tensor (device/dtype/size/alignment)");
+  TORCH_CHECK(op != RedOp::PROD, "xgmi all_reduce: prod is not supported");
+  TSArgs a;
+  for (int p = 0; p < kMaxRanks; ++p) a.peers.base[p] = peers_.base[p] ? peers_.base[p] + ts_off_ : nullptr;
+  a.in = in.data_ptr();
+  a.out = out.data_ptr();
+  a.n = in.numel();
+  // shard: whole chunks, every element inside [0, W * shard)
+  a.shard = ((a.n + world_ - 1) / world_ + kChunkElems - 1) / kChunkElems * kChunkElems;
+  a.stride = ts_shard_max_;
+  ts_used_ = true;
+  a.par_bytes = ts_par_bytes_;
+  a.ctr = ts_ctr_;
+  a.rank = rank_;
+  a.world = world_;
+  a.err = dev_words_;
+  a.abort_flag = dev_words_ + 1;
+  a.timeout_ticks = timeout_ticks_;
+  const int grid = ts_grid_;  // fixed for the engine's lifetime (see twoshot_kernel)
+  hipStream_t s = stream ? stream : cur_stream();
+  const int o = op == RedOp::SUM ? 0 : op == RedOp::AVG ? 1 : op == RedOp::MAX ? 2 : 3;
+  auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), 0, s, a); };
+#define DPA_TS(T)                                \
+  switch (o) {                                   \
+    case 0: launch(twoshot_kernel<T, 0>); break; \
+    case 1: launch(twoshot_kernel<T, 1>); break; \
+    case 2: launch(twoshot_kernel<T, 2>); break; \
+    default: launch(twoshot_kernel<T, 3>); break; \
+  }
+  switch (in.scalar_type()) {
+    case at::kFloat: DPA_TS(float); break;
+    case at::kBFloat16: DPA_TS(__hip_bfloat16); break;
+    default: DPA_TS(__half); break;
+  }
+#undef DPA_TS
   DPA_CHECK_LAUNCH();
 }
 
@@ -436,6 +711,10 @@ class XgmiCollective : public Collective {
       x_->all_reduce(in, out, op, stream_.stream());
       return;
     }
+    if (x_->supports_twoshot(in) && x_->supports_twoshot(out)) {
+      x_->all_reduce_twoshot(in, out, op, stream_.stream());
+      return;
+    }
     TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && out.numel() == n,
                 "xgmi all_reduce: chunked path needs contiguous same-size tensors");
     const auto fi = in.view(-1), fo = out.view(-1);
@@ -472,8 +751,9 @@ void register_xgmi(pybind11::module& m) {
   });
 #endif
   py::class_<xgmi::XgmiComm, std::shared_ptr<xgmi::XgmiComm>>(s, "XgmiComm")
-      .def(py::init<int, int, int, long long, double>(), py::arg("rank"), py::arg("world"), py::arg("device"),
-           py::arg("max_bytes") = 1 << 20, py::arg("timeout_s") = 600.0)
+      .def(py::init<int, int, int, long long, double, long long>(), py::arg("rank"), py::arg("world"),
+           py::arg("device"), py::arg("max_bytes") = 1 << 20, py::arg("timeout_s") = 600.0,
+           py::arg("twoshot_max_bytes") = 0)
       .def("handle", &xgmi::XgmiComm::handle)
       .def("open", &xgmi::XgmiComm::open)
       .def("supports", &xgmi::XgmiComm::supports)
@@ -486,6 +766,16 @@ void register_xgmi(pybind11::module& m) {
            py::arg("t"), py::arg("op") = "sum", py::arg("out") = py::none())
       .def("site_probe", &xgmi::XgmiComm::site_probe, py::arg("site"), py::arg("inp"), py::arg("out"),
            py::arg("grid") = 1)
+      .def("all_reduce_twoshot",
+           [](xgmi::XgmiComm& c, at::Tensor t, const std::string& op, c10::optional<at::Tensor> out) {
+             at::Tensor dst = out.has_value() ? *out : t;
+             c.all_reduce_twoshot(t, dst, parse_op(op), nullptr);
+             return dst;
+           },
+           py::arg("t"), py::arg("op") = "sum", py::arg("out") = py::none())
+      .def("supports_twoshot", &xgmi::XgmiComm::supports_twoshot)
+      .def("set_twoshot_blocks", &xgmi::XgmiComm::set_twoshot_blocks)
+      .def_property_readonly("twoshot_max_bytes", &xgmi::XgmiComm::twoshot_max_bytes)
       .def("error", &xgmi::XgmiComm::error)
       .def("error_string", &xgmi::XgmiComm::error_string)
       .def("abort", &xgmi::XgmiComm::abort)

@@ -1098,10 +1098,16 @@ bwd_elemt_kernel(const T* __restrict__ dp, const T* __restrict__ p, const uint8_
 // ---------------------------------------------------------------------------
 // PRO 2: dy is produced on the fly from the pooled grad of the next block
 // (bin: backward through MaxPool -> ReLU -> BN); needs ROWS == H.
-template <typename T, int CIN, int COUT, int H, int W, int ROWS, int PRO = 0>
+// WT: the partial row is stored write-through (sc1) for an in-launch reduction
+// (MI355X_MICROARCH.md "Valid forms" row 1; convnet_fused.hip wgrad1_reduce_kernel).
+template <typename T, int CIN, int COUT, int H, int W, int ROWS, int PRO = 0, bool WT = false>
 __device__ __forceinline__ void
 conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __restrict__ wslab, int nsplit,
                    const BwdIn<T>& bin, const int bid) {
+  auto put = [](float* p, float v) {
+    if constexpr (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+  };
   static_assert(PRO == 0 || (PRO == 2 && ROWS % 2 == 0), "PRO 2 works on whole 2x2 pooling windows");
   constexpr int WP = ceil_to(W, 8);
   static_assert((ROWS * WP) % 32 == 0, "ROWS*WP must be a multiple of 32");
@@ -1266,7 +1272,7 @@ conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __r
     }
 #pragma unroll
     for (int o = TPC / 2; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
-    if (sub == 0) row_out[COUT * N + co] = a;
+    if (sub == 0) put(&row_out[COUT * N + co], a);
   }
   DPA_STAMP(6);
   const int ks = KSPLIT > 1 ? wv % KSPLIT : 0;
@@ -1298,7 +1304,7 @@ conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __r
     const int col = nt * 16 + r;
     if (col < N) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) row_out[(mt * 16 + 4 * q + i) * N + col] = acc[i];
+      for (int i = 0; i < 4; ++i) put(&row_out[(mt * 16 + 4 * q + i) * N + col], acc[i]);
     }
   }
   DPA_STAMP(7);

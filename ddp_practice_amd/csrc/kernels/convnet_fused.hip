@@ -470,6 +470,7 @@ void conv2_dgrad(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx
 // so they overlap on the chip instead of running back to back (each alone fills
 // only 64 / 128 of the 256 CUs at B = 32) and one kernel boundary disappears.
 constexpr int WG2_ROWS_ = 4;
+constexpr int WG1_ROWS_ = 4;
 int64_t wgrad_bn_rows(int64_t layer, int64_t B);
 template <typename T>
 __global__ void __launch_bounds__(cb::NTHR)
@@ -528,7 +529,7 @@ void conv2_bwd(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx2,
 // layer 2: x = p1 [B,16,14,14], (y, dp, idx) = layer-2 tensors; layer 1: x = images, layer-1 tensors.
 // Weight-gradient row chunks (BN backward applied on the fly per chunk): more,
 // shorter workgroups than one image each (B = 32 -> 32 workgroups for 256 CUs).
-constexpr int WG1_ROWS = 4;  // layer 1 (28 rows): 7 chunks per image
+constexpr int WG1_ROWS = WG1_ROWS_;  // layer 1 (28 rows): 7 chunks per image
 constexpr int WG2_ROWS = WG2_ROWS_;  // layer 2 (14 rows): 4 chunks per image (last one 2 rows)
 int64_t wgrad_bn_rows(int64_t layer, int64_t B) {
   TORCH_CHECK(layer == 1 || layer == 2);
@@ -567,6 +568,139 @@ void conv_wgrad_bn(at::Tensor x, at::Tensor y, at::Tensor dp, at::Tensor idx, at
   DPA_CHECK_LAUNCH();
 }
 
+
+// ---------------------------------------------------------------------------
+// The last backward launch: conv1 weight-grad partials AND every weight-grad
+// column sum, so no separate reduction launch follows.
+//   role A, workgroups [0, nwg1): BN1 bwd -> conv1 wgrad partial row (write-
+//     through), then a two-level in-launch reduction: the last arriver of each
+//     group of RG rows sums them into a group row; the last group sums the group
+//     rows into [dW1 | db1] (tickets on self-resetting counters: graph-replayable).
+//   role B, workgroups [nwg1, grid): column sums of the conv2 weight-grad slab
+//     (written by the previous launch) into [dW2 | db2], RB_COLS columns each.
+// Reference op: /root/reference/origin_main.py:13 (conv1 weight/bias grads),
+// :19 (conv2's); replaces conv_wgrad_bn + slab_reduce (one launch and one
+// kernel boundary less per step).
+// ---------------------------------------------------------------------------
+constexpr int RG = 16;        // role A: rows per group
+constexpr int RB_COLS = 32;   // role B: columns per workgroup (8 row groups of 32 lanes)
+
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// rows x n (row-major) -> out[n]: column sums in row order 0.. (deterministic)
+__device__ __forceinline__ void colsum_sc1(const float* __restrict__ src, int rows, int n, float* __restrict__ out,
+                                           bool wt) {
+  for (int j = threadIdx.x; j < n; j += cb::NTHR) {
+    float a = 0.f;
+    int r = 0;
+    for (; r + 7 < rows; r += 8) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = ld_sc1(src + (size_t)(r + k) * n + j);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a += v[k];
+    }
+    for (; r < rows; ++r) a += ld_sc1(src + (size_t)r * n + j);
+    if (wt) __hip_atomic_store(out + j, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else out[j] = a;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(cb::NTHR)
+wgrad1_reduce_kernel(const T* __restrict__ x, float* __restrict__ wslab1, float* __restrict__ gslab1,
+                     float* __restrict__ out1, BwdIn<T> bi, int nwg1, const float* __restrict__ wslab2, int rows2,
+                     int n2, float* __restrict__ out2, int* __restrict__ cnt) {
+  constexpr int N1 = 16 * 25 + 16;
+  __shared__ int last_s;
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x >= nwg1) {
+    // role B: RB_COLS columns of the conv2 slab, 8 row groups of 32 lanes, fixed-order sums
+    __shared__ float part[8][RB_COLS + 1];
+    const int c0 = ((int)blockIdx.x - nwg1) * RB_COLS;
+    const int col = c0 + (tid % RB_COLS), g = tid / RB_COLS;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    if (col < n2) {
+      int r = g;
+      for (; r + 3 * 8 < rows2; r += 4 * 8) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a[k] += wslab2[(size_t)(r + 8 * k) * n2 + col];
+      }
+      for (; r < rows2; r += 8) a[0] += wslab2[(size_t)r * n2 + col];
+    }
+    part[g][tid % RB_COLS] = (a[0] + a[1]) + (a[2] + a[3]);
+    __syncthreads();
+    if (tid < RB_COLS && c0 + tid < n2) {
+      float t = 0.f;
+#pragma unroll
+      for (int gg = 0; gg < 8; ++gg) t += part[gg][tid];
+      out2[c0 + tid] = t;
+    }
+    return;
+  }
+  // role A
+  const int bid = blockIdx.x;
+  constexpr int ns = (28 + WG1_ROWS_ - 1) / WG1_ROWS_;
+  cb::conv5x5_wgrad_body<T, 1, 16, 28, 28, WG1_ROWS_, 2, true>(x, nullptr, wslab1, ns, bi, bid);
+  const int ng = (nwg1 + RG - 1) / RG, g = bid / RG;
+  const int grows = min(RG, nwg1 - g * RG);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's row has left the CU
+  __syncthreads();
+  if (tid == 0)
+    last_s = __hip_atomic_fetch_add(&cnt[g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == grows - 1;
+  __syncthreads();
+  if (!last_s) return;
+  colsum_sc1(wslab1 + (size_t)g * RG * N1, grows, N1, gslab1 + (size_t)g * N1, true);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __hip_atomic_store(&cnt[g], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm for the next launch
+    last_s = __hip_atomic_fetch_add(&cnt[ng], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+  }
+  __syncthreads();
+  if (!last_s) return;
+  colsum_sc1(gslab1, ng, N1, out1, false);
+  if (tid == 0) __hip_atomic_store(&cnt[ng], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+int64_t wgrad1_counters(int64_t B) { return (wgrad_bn_rows(1, B) + RG - 1) / RG + 1; }
+
+// BN1 bwd -> conv1 wgrad, + the column sums of both weight-grad slabs:
+// out1 = [dW1 | db1] (416 floats), out2 = [dW2 | db2] (12832 floats).
+// cnt: int32[wgrad1_counters(B)], zeroed once (the kernel re-arms it).
+void wgrad1_reduce(at::Tensor x, at::Tensor y1, at::Tensor dp1, at::Tensor idx1, at::Tensor fstats1, at::Tensor gsum,
+                   c10::optional<at::Tensor> lsum, at::Tensor g1, double eps1, at::Tensor dg1, at::Tensor dbe1,
+                   at::Tensor wslab1, at::Tensor gslab1, at::Tensor out1, at::Tensor wslab2, at::Tensor out2,
+                   at::Tensor cnt, XcPtr xc) {
+  DPA_CHECK_INPUT(x); DPA_CHECK_INPUT(y1); DPA_CHECK_INPUT(wslab1); DPA_CHECK_INPUT(wslab2); DPA_CHECK_INPUT(cnt);
+  const int B = (int)y1.size(0);
+  TORCH_CHECK(x.size(1) == 1 && y1.size(1) == 16 && y1.size(2) == 28 && x.scalar_type() == y1.scalar_type());
+  const int nwg1 = (int)wgrad_bn_rows(1, B), ng = (nwg1 + RG - 1) / RG;
+  constexpr int N1 = 16 * 25 + 16, N2 = 32 * 400 + 32;
+  const int rows2 = (int)wgrad_bn_rows(2, B);
+  TORCH_CHECK(wslab1.numel() == (int64_t)nwg1 * N1 && gslab1.numel() >= (int64_t)ng * N1 && out1.numel() == N1,
+              "wgrad1_reduce: conv1 slab sizes");
+  TORCH_CHECK(wslab2.numel() == (int64_t)rows2 * N2 && out2.numel() == N2, "wgrad1_reduce: conv2 slab sizes");
+  TORCH_CHECK(cnt.scalar_type() == at::kInt && cnt.numel() >= ng + 1, "wgrad1_reduce: counters");
+  if (B == 0) return;
+  const int nred = (N2 + RB_COLS - 1) / RB_COLS;
+  with_t(dt_of(y1), [&](auto tag) {
+    typedef decltype(tag) T;
+    BwdIn<T> bi = bwd_in<T>(dp1, idx1, y1, fstats1, gsum, lsum, g1, eps1, 16, dg1, dbe1);
+    if (xc) {
+      TORCH_CHECK(!lsum.has_value(), "fused SyncBN exchange: gsum must be this rank's rows (no lsum)");
+      bi.xs = site_of(xc, xgmi::kSiteBwd1);
+      bi.xs.nblk = nwg1;  // the reduction workgroups take no tickets
+    }
+    hipLaunchKernelGGL(wgrad1_reduce_kernel<T>, dim3(nwg1 + nred), dim3(cb::NTHR), 0, cur_stream(), dptr<T>(x),
+                       wslab1.data_ptr<float>(), gslab1.data_ptr<float>(), out1.data_ptr<float>(), bi, nwg1,
+                       wslab2.data_ptr<float>(), rows2, N2, out2.data_ptr<float>(), cnt.data_ptr<int>());
+  });
+  DPA_CHECK_LAUNCH();
+}
+
 // Whether every launch that exchanges SyncBN sums in-kernel (comm/xsite.h: all
 // of its workgroups poll the peers' rows) is co-resident at batch B; if not,
 // ops/convnet_fused.py all-reduces between the launches instead.
@@ -585,6 +719,7 @@ bool sites_resident(int64_t B, at::ScalarType st) {
         wgrad_bn_rows(2, B));
     chk(reinterpret_cast<const void*>(&cb::conv5x5_wgrad_kernel<T, 1, 16, 28, 28, WG1_ROWS, 2>),
         wgrad_bn_rows(1, B));
+    chk(reinterpret_cast<const void*>(&wgrad1_reduce_kernel<T>), wgrad_bn_rows(1, B));
   });
   return ok;
 }
@@ -622,6 +757,8 @@ void register_convnet_fused(pybind11::module& m) {
   s.def("conv_wgrad_bn", &cnf::conv_wgrad_bn);
   s.def("wgrad_bn_rows", &cnf::wgrad_bn_rows);
   s.def("sites_resident", &cnf::sites_resident);
+  s.def("wgrad1_reduce", &cnf::wgrad1_reduce);
+  s.def("wgrad1_counters", &cnf::wgrad1_counters);
 }
 
 }  // namespace dpa

@@ -19,6 +19,8 @@ from __future__ import annotations
 
 import math
 
+import os
+
 import torch
 
 from .._ext import load as _load_ext
@@ -174,6 +176,8 @@ def flush_pending(images: torch.Tensor) -> None:
 def accepts_deferred(model, images: torch.Tensor) -> bool:
     """Whether ``model(images)`` performs a deferred gather itself (so a training step
     may hand it the batch without the separate gather launch)."""
+    if os.environ.get("DPA_DEFER_GATHER", "1") == "0":
+        return False
     m = getattr(model, "module", model)
     f = getattr(m, "accepts_deferred_batch", None)
     return bool(f is not None and images.is_cuda and f(images))

@@ -53,6 +53,7 @@ def supported(model, x: torch.Tensor) -> bool:
 
 _RESIDENT: dict = {}
 _SPLIT_BWD2 = os.environ.get("DPA_SPLIT_BWD2", "0") == "1"
+_SPLIT_WGRAD1 = os.environ.get("DPA_SPLIT_WGRAD1", "0") == "1"
 
 
 def _fused_site_engine(comm, batch: int, dtype: torch.dtype):
@@ -87,6 +88,7 @@ class PreCE:
 
 _HEAD_OK: dict = {}
 HEAD_TIMEOUT_S = float(os.environ.get("DPA_HEAD_TIMEOUT", "30"))
+_HEAD_SPEC = os.environ.get("DPA_HEAD_SPEC", "1") != "0"  # 0: no speculative head backward (A/B)
 
 
 def _head_step_ok(B: int, N: int, dtype: torch.dtype) -> bool:
@@ -105,7 +107,7 @@ def _head_step_ok(B: int, N: int, dtype: torch.dtype) -> bool:
 class ConvNetFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, b1, g1, be1, w2, b2, g2, be2, wfc, bfc, bufs, training, moms, epss, comm, cdtype,
-                labels=None, ce_cfg=(-100, 0.0), holder=None, state=None, gather=None):
+                labels=None, ce_cfg=(-100, 0.0), holder=None, state=None, gather=None, wcnt=None):
         cb, cn = _mods()
         rm1, rv1, nbt1, rm2, rv2, nbt2 = bufs
         m1, m2 = (-1.0 if m is None else float(m) for m in moms)
@@ -153,7 +155,7 @@ class ConvNetFn(torch.autograd.Function):
                 # backward when a GradScaler will seed it with its scale) in one launch
                 from ..amp.grad_scaler import active_scale
 
-                scale = active_scale(dev)
+                scale = active_scale(dev) if _HEAD_SPEC else None
                 f32 = dict(dtype=torch.float32, device=dev)
                 part = torch.empty(32 * B * 16, **f32)
                 loss_buf = torch.empty(2, **f32)
@@ -192,6 +194,7 @@ class ConvNetFn(torch.autograd.Function):
             cn.head_fwd(y2, None, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, False, wfc, bfc, logits, None, None,
                         None, None)
         ctx.training = training
+        ctx.wcnt = wcnt
         ctx.sync = sync
         ctx.comm = comm
         ctx.xc = xc
@@ -246,18 +249,25 @@ class ConvNetFn(torch.autograd.Function):
             cn.conv_wgrad_bn(p1, y2, dp2, idx2, fstats2, gsum2, None, g2, e2, None, None, wslab2, xc)
         else:
             cn.conv2_bwd(wpk_d, y2, dp2, idx2, fstats2, gsum2, g2, e2, dp1, idx1, xh1, bslab1, p1, wslab2, xc)
-        # 4. BN1 bwd -> conv1 wgrad partials (+ dgamma1 / dbeta1 from the local sums)
+        # 4+5. BN1 bwd -> conv1 wgrad partials (+ dgamma1 / dbeta1 from the local sums), and the
+        #      column sums of both weight-grad slabs -> [dW1 | db1], [dW2 | db2]: one launch
+        #      (DPA_SPLIT_WGRAD1=1: wgrad launch + a separate reduction launch, A/B runs)
         wslab1 = torch.empty(cn.wgrad_bn_rows(1, B) * (n_w1 + 16), **f32)
         if sync and xc is None:
-            gslab1 = comm.all_reduce(bslab1)
-            cn.conv_wgrad_bn(x, y1, dp1, idx1, fstats1, gslab1, bslab1, g1, e1, dg1, dbe1, wslab1, None)
+            gsum1, lsum1, xc1 = comm.all_reduce(bslab1), bslab1, None
         else:
-            cn.conv_wgrad_bn(x, y1, dp1, idx1, fstats1, bslab1, None, g1, e1, dg1, dbe1, wslab1, xc)
-        # 5. weight-grad partial sums -> [dW1 | db1], [dW2 | db2]
-        cb.slab_reduce(wslab1, n_w1 + 16, out.narrow(0, 0, n_w1 + 16), wslab2, n_w2 + 32,
-                       out.narrow(0, n_w1 + 48, n_w2 + 32))
+            gsum1, lsum1, xc1 = bslab1, None, xc
+        out1, out2 = out.narrow(0, 0, n_w1 + 16), out.narrow(0, n_w1 + 48, n_w2 + 32)
+        if _SPLIT_WGRAD1 or ctx.wcnt is None:
+            cn.conv_wgrad_bn(x, y1, dp1, idx1, fstats1, gsum1, lsum1, g1, e1, dg1, dbe1, wslab1, xc1)
+            cb.slab_reduce(wslab1, n_w1 + 16, out1, wslab2, n_w2 + 32, out2)
+        else:
+            cnt = ctx.wcnt
+            gslab1 = torch.empty((cn.wgrad1_counters(B) - 1) * (n_w1 + 16), **f32)
+            cn.wgrad1_reduce(x, y1, dp1, idx1, fstats1, gsum1, lsum1, g1, e1, dg1, dbe1, wslab1, gslab1, out1,
+                             wslab2, out2, cnt, xc1)
         return (None, dw1.view(s_w1), db1, dg1, dbe1, dw2.view(s_w2), db2, dg2, dbe2, dwfc.view(s_wfc), dbfc,
-                None, None, None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None, None)
 
 
 def convnet_forward(model, x, comm=None, cdtype=None):
@@ -300,9 +310,17 @@ def convnet_forward(model, x, comm=None, cdtype=None):
                 # kernel re-arms them itself, so graph replays need no reset)
                 state = torch.zeros(4, dtype=torch.int64, device=x.device)
                 model._dpa_head_state = state
+    wcnt = None
+    if training:
+        # tickets of the in-launch weight-grad reduction (zeroed once, re-armed by the kernel)
+        n = _load_ext().convnet.wgrad1_counters(x.shape[0])
+        wcnt = getattr(model, "_dpa_wgrad_cnt", None)
+        if wcnt is None or wcnt.numel() < n or wcnt.device != x.device:
+            wcnt = torch.zeros(max(n, 64), dtype=torch.int32, device=x.device)
+            model._dpa_wgrad_cnt = wcnt
     out = ConvNetFn.apply(x, c1.weight, c1.bias, bn1.weight, bn1.bias, c2.weight, c2.bias, bn2.weight, bn2.bias,
                           fc.weight, fc.bias, bufs, training, (bn1.momentum, bn2.momentum), (bn1.eps, bn2.eps),
-                          comm, cdtype, labels, (-100, 0.0), holder, state, gather)
+                          comm, cdtype, labels, (-100, 0.0), holder, state, gather, wcnt)
     if holder:
         out._dpa_pre_ce = holder.get("ce")
     return out

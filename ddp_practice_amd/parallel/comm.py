@@ -335,12 +335,14 @@ class XgmiCommunicator(Communicator):
 XGMI_DEFAULT_MAX_BYTES = 1 << 20  # every ConvNet collective (<= 116 KB); RCCL above
 
 
-def open_xgmi(rank: int, world: int, device: torch.device, store, key: str, max_bytes: int, timeout_s: float):
-    """Create this rank's xGMI workspace and map every peer's (handles via the store)."""
+def open_xgmi(rank: int, world: int, device: torch.device, store, key: str, max_bytes: int, timeout_s: float,
+              twoshot_max_bytes: int = 0):
+    """Create this rank's xGMI workspace and map every peer's (handles via the store).
+    ``max_bytes``: largest one-shot message; ``twoshot_max_bytes``: largest two-shot one."""
     C = _load_ext()
     x, err = None, ""
     try:
-        x = C.xgmi.XgmiComm(rank, world, device.index, int(max_bytes), float(timeout_s))
+        x = C.xgmi.XgmiComm(rank, world, device.index, int(max_bytes), float(timeout_s), int(twoshot_max_bytes))
         h = x.handle()
     except Exception as e:  # noqa: BLE001 - any failure here means "use RCCL"
         x, h, err = None, b"", f"{type(e).__name__}: {e}"

@@ -53,7 +53,7 @@ wrap(C.convnet_head, "head_step", lambda a: [("head_step", slice(0, 32))])
 wrap(C.convnet, "conv2_bwd", lambda a: [("conv2_bwd/dgrad", slice(0, 2 * B)),
                                          ("conv2_bwd/wgrad", slice(2 * B, 2 * B + 4 * B))])
 wrap(C.convnet, "conv2_fwd", lambda a: [("conv2_fwd", slice(0, 2 * B))])
-wrap(C.convnet, "conv_wgrad_bn", lambda a: [("wgrad1", slice(0, 7 * B))])
+wrap(C.convnet, "wgrad1_reduce", lambda a: [("wgrad1_reduce/wgrad", slice(0, 7 * B))])
 
 from ddp_practice_amd.amp import GradScaler  # noqa: E402
 from ddp_practice_amd.data import DeviceLoader  # noqa: E402

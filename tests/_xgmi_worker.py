@@ -45,7 +45,7 @@ def worker(rank, world, port, mode, q):
         store = torch.distributed.TCPStore("127.0.0.1", port, world, False, timedelta(seconds=60))  # parent serves
         from ddp_practice_amd.parallel.comm import open_xgmi
 
-        x, err = open_xgmi(rank, world, dev, store, "t", 1 << 20, 20.0)
+        x, err = open_xgmi(rank, world, dev, store, "t", 1 << 20, 20.0, (32 << 20) if mode == "twoshot" else 0)
         assert x is not None, err
         store.set(f"ready{rank}", "1")
         store.wait([f"ready{r}" for r in range(world)])
@@ -83,6 +83,62 @@ def worker(rank, world, port, mode, q):
                 exp = _expect(world, 64, torch.float32, 100 + r, "sum")
                 _check(o[:64], exp, torch.float32, ("site graph", r))
                 _check(o[64:], exp, torch.float32, ("site graph", r))
+            store.set(f"done{rank}", "1")
+            store.wait([f"done{r}" for r in range(world)])
+            x.close()
+            q.put((rank, "ok", out))
+            return
+        if mode == "twoshot":
+            x.set_twoshot_blocks(48)  # all ranks' grids resident together on the one shared GPU
+            # reduce-scatter + all-gather engine: 1 / 8 / 32 MiB, ragged sizes, every dtype
+            # and op, sizes interleaved (each block's slots are size-independent), results
+            # bit-identical across ranks, graph replay, and the RcclComm-style routing via
+            # XgmiCollective (one-shot <= 1 MiB, two-shot above)
+            out = {}
+            it = 0
+            cases = [(262144, "f32", "sum"), (2 << 20, "f32", "sum"), (8 << 20, "f32", "sum"),
+                     (262145, "f32", "avg"), (3000001, "bf16", "sum"), (1 << 20, "f16", "max"),
+                     (777777, "f32", "min"), (5, "f32", "sum"), (2 << 20, "f32", "sum"), (300000, "bf16", "avg")]
+            for n, dn, op in cases:
+                dt = DTYPES[dn]
+                t = _data(rank, n, dt, it).to(dev)
+                o = torch.empty_like(t)
+                x.all_reduce_twoshot(t, op, o)
+                torch.cuda.synchronize()
+                assert x.error() == 0, x.error_string()
+                _check(o, _expect(world, n, dt, it, op), dt, ("twoshot", n, dn, op))
+                out[f"ts{it}"] = o.float().cpu().numpy().tobytes()
+                it += 1
+            xc = C.xgmi.XgmiCollective(x)
+            for n in (100, 1 << 20, 3 << 20):
+                t = _data(rank, n, torch.float32, it).to(dev)
+                xc.all_reduce(t, "sum")
+                torch.cuda.synchronize()
+                assert x.error() == 0, x.error_string()
+                _check(t, _expect(world, n, torch.float32, it, "sum"), torch.float32, ("collective", n))
+                it += 1
+            a = torch.zeros(1 << 21, device=dev)
+            b = torch.zeros(5 << 20, dtype=torch.bfloat16, device=dev)
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                x.all_reduce_twoshot(a)
+                x.all_reduce_twoshot(b)
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                x.all_reduce_twoshot(a)
+                x.all_reduce_twoshot(b, "avg")
+            for r in range(6):
+                a.copy_(_data(rank, 1 << 21, torch.float32, it).to(dev))
+                b.copy_(_data(rank, 5 << 20, torch.bfloat16, it + 1).to(dev))
+                g.replay()
+                torch.cuda.synchronize()
+                assert x.error() == 0, x.error_string()
+                _check(a, _expect(world, 1 << 21, torch.float32, it, "sum"), torch.float32, ("ts graph a", r))
+                _check(b, _expect(world, 5 << 20, torch.bfloat16, it + 1, "avg"), torch.bfloat16, ("ts graph b", r))
+                it += 2
             store.set(f"done{rank}", "1")
             store.wait([f"done{r}" for r in range(world)])
             x.close()

@@ -40,3 +40,13 @@ def test_in_kernel_exchange_wait_is_bounded(C, mode):
     """A fused SyncBN site and the fused AMP-SGD gradient exchange whose peer never
     arrives end with the error word set; the optimizer applies nothing."""
     _run(2, mode)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_xgmi_twoshot_multiprocess(C, world):
+    """Two-shot (reduce-scatter + all-gather) engine for large messages: 1-32 MiB,
+    ragged sizes, every dtype/op, interleaved sizes, graph replay; bit-identical ranks."""
+    outs = _run(world, "twoshot", timeout=240)
+    for k, v in outs[0].items():
+        for r in range(1, world):
+            assert v == outs[r][k], f"rank {r} differs from rank 0 on {k}"
