@@ -26,7 +26,10 @@ PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 # experiment builds: DPA_BUILD_TAG=x [DPA_EXTRA_CFLAGS="-DFOO"] -> ddp_practice_amd/_C_x.so
 # (load it with DPA_EXT_SO=ddp_practice_amd/_C_x.so); the default build is untouched
-_TAG = os.environ.get("DPA_BUILD_TAG", "")
+# DPA_SANITIZE=1: host code under AddressSanitizer + UBSan (device code untouched), built
+# as ddp_practice_amd/_C_asan.so and run on the CPU by scripts/asan_check.sh
+_SANITIZE = os.environ.get("DPA_SANITIZE", "0") == "1"
+_TAG = os.environ.get("DPA_BUILD_TAG", "asan" if _SANITIZE else "")
 BUILD = PKG.parent / "build" / ("native" + (f"_{_TAG}" if _TAG else ""))
 TARGET = PKG / (f"_C_{_TAG}.so" if _TAG else "_C.so")
 ARCH = "gfx950"
@@ -64,6 +67,10 @@ def _flags():
         "-fno-gpu-rdc", "-munsafe-fp-atomics",
         f"-I{CSRC}", f"-I{sysconfig.get_paths()['include']}",
     ]
+    if _SANITIZE:
+        # host side only: every -fsanitize= right after -Xarch_host
+        for x in ("-fsanitize=address", "-fsanitize=undefined", "-fno-omit-frame-pointer", "-O1", "-g"):
+            f += ["-Xarch_host", x]
     f += os.environ.get("DPA_EXTRA_CFLAGS", "").split()
     f += [f"-I{d}" for d in inc]
     return f

@@ -356,6 +356,206 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
   }
 }
 
+// ---------------------------------------------------------------------------
+// Large-model fused AMP step (ResNet-50: 161 tensors, 25.6M floats): the same
+// semantics as amp_sgd_fused_kernel -- unscale, global inf agreement, SGD, scale
+// update -- in ONE launch of a co-resident grid, for any tensor count / size.
+//   * the tensor table lives in device memory (built once per distinct set of
+//     pointers by amp_sgd_table, captured into graphs by value) and is staged in LDS;
+//   * phase A streams the grads once for the non-finite check (no write), the grid
+//     agrees through one arrival word (the bounded barrier of the small kernel), and
+//     phase B streams grads / params / buffers for the update -- the second grad
+//     read mostly hits the 256 MB MALL for ResNet-50's 102 MB of grads;
+//   * each workgroup owns one contiguous range of float4 granules, each lane walks it
+//     with a monotone tensor cursor (no per-granule search).
+// Table (int64): [0] n, [1] total granules, then off[n+1] | numel[n] | p0[n] | p1[n] |
+// p2[n] | first[n]  (p0 param, p1 grad, p2 momentum buffer or 0).
+constexpr int LARGE_THR = 256;
+constexpr int LARGE_MAXT = 512;
+constexpr int LARGE_UNROLL = 4;
+
+__global__ void __launch_bounds__(64) amp_table_kernel(int64_t* __restrict__ table, int n, int s, int e,
+                                                       MTList c, int64_t off_s, int64_t total) {
+  // entries [s, e) of the table from a by-value chunk (graph-capturable, no host copy)
+  const int k = threadIdx.x;
+  int64_t* off = table + 2;
+  int64_t* num = off + n + 1;
+  int64_t* q0 = num + n;
+  int64_t* q1 = q0 + n;
+  int64_t* q2 = q1 + n;
+  int64_t* fst = q2 + n;
+  if (k == 0 && s == 0) { table[0] = n; table[1] = total; }
+  if (k == 0 && e == n) off[n] = total;
+  if (k < e - s) {
+    const int t = s + k;
+    off[t] = off_s + c.chunk_off[k];
+    num[t] = c.numel[k];
+    q0[t] = reinterpret_cast<int64_t>(c.p0[k]);
+    q1[t] = reinterpret_cast<int64_t>(c.p1[k]);
+    q2[t] = reinterpret_cast<int64_t>(c.p2[k]);
+    fst[t] = (c.first_bits >> k) & 1ull;
+  }
+}
+
+__global__ void __launch_bounds__(LARGE_THR)
+amp_sgd_large_kernel(const int64_t* __restrict__ table, float* __restrict__ scale, int* __restrict__ tracker,
+                     float* __restrict__ found_inf, unsigned long long* __restrict__ sync, float lr, float momentum,
+                     float dampening, float wd, int nesterov, int maximize, float growth, float backoff, int interval,
+                     int* __restrict__ err, long long barrier_ticks) {
+  __shared__ long long soff[LARGE_MAXT + 1];
+  __shared__ long long snum[LARGE_MAXT];
+  __shared__ float* sp0[LARGE_MAXT];
+  __shared__ float* sp1[LARGE_MAXT];
+  __shared__ float* sp2[LARGE_MAXT];
+  __shared__ unsigned char sfirst[LARGE_MAXT];
+  __shared__ int s_bad;
+  const int tid = threadIdx.x;
+  const int n = (int)table[0];
+  const long long total = table[1];
+  const int64_t* off = table + 2;
+  for (int t = tid; t <= n; t += LARGE_THR) soff[t] = off[t];
+  for (int t = tid; t < n; t += LARGE_THR) {
+    snum[t] = off[n + 1 + t];
+    sp0[t] = reinterpret_cast<float*>(off[2 * n + 1 + t]);
+    sp1[t] = reinterpret_cast<float*>(off[3 * n + 1 + t]);
+    sp2[t] = reinterpret_cast<float*>(off[4 * n + 1 + t]);
+    sfirst[t] = (unsigned char)off[5 * n + 1 + t];
+  }
+  unsigned long long gen = 0;
+  if (tid == 0 && gridDim.x > 1)
+    gen = __hip_atomic_fetch_add(&sync[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  // this workgroup's granule range, whole lanes-rows so every lane steps by LARGE_THR
+  const long long per = ((total + gridDim.x - 1) / gridDim.x + LARGE_THR - 1) / LARGE_THR * LARGE_THR;
+  const long long g0 = (long long)blockIdx.x * per, g1 = min(total, g0 + per);
+  int t0 = 0;  // tensor holding g0 (binary search once per workgroup)
+  if (g0 < total) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (soff[mid] <= g0) lo = mid; else hi = mid - 1;
+    }
+    t0 = lo;
+  }
+  auto load4 = [](const float* p, long long rem) {
+    if (rem >= 4) return *reinterpret_cast<const f32x4*>(p);
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < rem; ++j) v[j] = p[j];
+    return v;
+  };
+  auto store4 = [](float* p, long long rem, f32x4 v) {
+    if (rem >= 4) { *reinterpret_cast<f32x4*>(p) = v; return; }
+    for (int j = 0; j < rem; ++j) p[j] = v[j];
+  };
+  // phase A: non-finite check over this range (LARGE_UNROLL granule loads in flight per lane)
+  bool bad = false;
+  {
+    int t = t0;
+    for (long long base = g0 + tid; base < g1; base += (long long)LARGE_THR * LARGE_UNROLL) {
+      f32x4 v[LARGE_UNROLL];
+#pragma unroll
+      for (int u = 0; u < LARGE_UNROLL; ++u) {
+        const long long gi = base + (long long)u * LARGE_THR;
+        v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (gi < g1) {
+          while (soff[t + 1] <= gi) ++t;
+          const long long o = (gi - soff[t]) * 4;
+          v[u] = load4(sp1[t] + o, snum[t] - o);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < LARGE_UNROLL; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bad |= !isfinite(v[u][j]);
+    }
+  }
+  const float inv = 1.f / scale[0];  // read before arriving (block 0 rewrites it after the barrier)
+  const bool block_bad = __syncthreads_or(bad);
+  if (gridDim.x == 1) {
+    if (tid == 0) s_bad = block_bad;
+  } else if (tid == 0) {
+    unsigned long long* word = &sync[1 + (gen & 1)];
+    const unsigned long long G = gridDim.x;
+    __hip_atomic_fetch_add(word, 1ull | ((unsigned long long)block_bad << 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long v;
+    const long long ts = (long long)__builtin_amdgcn_s_memrealtime();
+    bool timed_out = false;
+    while (((v = __hip_atomic_fetch_add(word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & 0xffffffffull) <
+           G) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((long long)__builtin_amdgcn_s_memrealtime() - ts > barrier_ticks) {
+        timed_out = true;
+        if (err != nullptr) __hip_atomic_store(err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    s_bad = timed_out || (v >> 32) != 0;
+    if (blockIdx.x == 0) {
+      __hip_atomic_exchange(&sync[1 + ((gen + 1) & 1)], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&sync[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  const bool any_bad = s_bad;
+  // phase B: unscaled grads written back (torch semantics); the update only if all finite
+  {
+    int t = t0;
+    for (long long base = g0 + tid; base < g1; base += (long long)LARGE_THR * LARGE_UNROLL) {
+      f32x4 gv[LARGE_UNROLL], pv[LARGE_UNROLL], bv[LARGE_UNROLL];
+      int tt[LARGE_UNROLL];
+#pragma unroll
+      for (int u = 0; u < LARGE_UNROLL; ++u) {
+        const long long gi = base + (long long)u * LARGE_THR;
+        tt[u] = -1;
+        if (gi < g1) {
+          while (soff[t + 1] <= gi) ++t;
+          tt[u] = t;
+          const long long o = (gi - soff[t]) * 4, rem = snum[t] - o;
+          gv[u] = load4(sp1[t] + o, rem);
+          if (!any_bad) {
+            pv[u] = load4(sp0[t] + o, rem);
+            bv[u] = (momentum != 0.f && !sfirst[t]) ? load4(sp2[t] + o, rem) : f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < LARGE_UNROLL; ++u) {
+        const int tu = tt[u];
+        if (tu < 0) continue;
+        const long long o = (base + (long long)u * LARGE_THR - soff[tu]) * 4, rem = snum[tu] - o;
+        const f32x4 g = gv[u] * inv;
+        store4(sp1[tu] + o, rem, g);
+        if (any_bad) continue;
+        f32x4 d = maximize ? -g : g;
+        if (wd != 0.f) d += wd * pv[u];
+        if (momentum != 0.f) {
+          const f32x4 bb = sfirst[tu] ? d : momentum * bv[u] + (1.f - dampening) * d;
+          store4(sp2[tu] + o, rem, bb);
+          d = nesterov ? d + momentum * bb : bb;
+        }
+        store4(sp0[tu] + o, rem, pv[u] - lr * d);
+      }
+    }
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    found_inf[0] = 0.f;
+    if (any_bad) {
+      scale[0] = scale[0] * backoff;
+      tracker[0] = 0;
+    } else {
+      const int succ = tracker[0] + 1;
+      if (succ == interval) {
+        const float ns = scale[0] * growth;
+        if (isfinite(ns)) scale[0] = ns;
+        tracker[0] = 0;
+      } else {
+        tracker[0] = succ;
+      }
+    }
+  }
+}
+
 // direction 0: flat[off_t + i] = src_t[i] * s ; direction 1: dst_t[i] = flat[off_t + i] * s
 __global__ void __launch_bounds__(NTHR)
 flat_copy_kernel(MTList L, float* __restrict__ flat, float s, int direction) {
@@ -525,6 +725,79 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
   DPA_CHECK_LAUNCH();
 }
 
+// Grid of the large fused step: 2 workgroups per CU when both fit at once, else 1.
+static int large_grid() {
+  static const int g = [] {
+    int dev = 0, cus = 0;
+    DPA_CHECK_HIP(hipGetDevice(&dev));
+    DPA_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const void* k = reinterpret_cast<const void*>(&amp_sgd_large_kernel);
+    for (int per = 2; per >= 1; --per)
+      if (co_resident(k, cus * per, LARGE_THR)) return cus * per;
+    return 0;
+  }();
+  return g;
+}
+
+bool amp_sgd_large_resident() { return large_grid() > 0; }
+
+// Device table for amp_sgd_large: written by by-value upload launches (one per MAXT
+// tensors), so building it is stream-ordered and graph-capturable.
+at::Tensor amp_sgd_table(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std::vector<at::Tensor> bufs,
+                         std::vector<int64_t> first) {
+  const size_t n = params.size();
+  TORCH_CHECK(n >= 1 && n <= (size_t)LARGE_MAXT, "large fused AMP-SGD: 1..", LARGE_MAXT, " tensors");
+  TORCH_CHECK(grads.size() == n && (bufs.empty() || bufs.size() == n) && (first.empty() || first.size() == n));
+  auto al = [](const float* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  std::vector<int64_t> offs(n + 1, 0);
+  for (size_t i = 0; i < n; ++i) {
+    check_f32(params[i]); check_f32(grads[i]);
+    TORCH_CHECK(params[i].numel() == grads[i].numel());
+    if (!bufs.empty()) { check_f32(bufs[i]); TORCH_CHECK(bufs[i].numel() == params[i].numel()); }
+    TORCH_CHECK(al(params[i].data_ptr<float>()) && al(grads[i].data_ptr<float>()) &&
+                    (bufs.empty() || al(bufs[i].data_ptr<float>())),
+                "large fused AMP-SGD needs 16-byte aligned tensors");
+    offs[i + 1] = offs[i] + (params[i].numel() + 3) / 4;
+  }
+  auto table = at::empty({(int64_t)(2 + (n + 1) + 5 * n)}, params[0].options().dtype(at::kLong));
+  for_batches(n, [&](size_t s, size_t e) {
+    MTList c{};
+    c.n = (int)(e - s);
+    c.first_bits = first_bits(first, s, e);
+    for (size_t i = s; i < e; ++i) {
+      const int k = (int)(i - s);
+      c.numel[k] = params[i].numel();
+      c.chunk_off[k] = offs[i] - offs[s];
+      c.p0[k] = params[i].data_ptr<float>();
+      c.p1[k] = grads[i].data_ptr<float>();
+      c.p2[k] = bufs.empty() ? nullptr : bufs[i].data_ptr<float>();
+    }
+    hipLaunchKernelGGL(amp_table_kernel, dim3(1), dim3(64), 0, cur_stream(), table.data_ptr<int64_t>(), (int)n,
+                       (int)s, (int)e, c, offs[s], offs[n]);
+    DPA_CHECK_LAUNCH();
+  });
+  return table;
+}
+
+void amp_sgd_large(at::Tensor table, double lr, double momentum, double dampening, double wd, bool nesterov,
+                   bool maximize, at::Tensor scale, at::Tensor tracker, at::Tensor found_inf, double growth,
+                   double backoff, int64_t interval, at::Tensor sync) {
+  check_f32(scale); check_f32(found_inf);
+  TORCH_CHECK(tracker.scalar_type() == at::kInt);
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kLong, "large fused AMP-SGD: table from amp_sgd_table");
+  TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == at::kLong && sync.numel() >= 4 && sync.is_contiguous(),
+              "large fused AMP-SGD: sync must be a zero-initialised int64[4] device tensor");
+  const int grid = large_grid();
+  TORCH_CHECK(grid > 0, "large fused AMP-SGD: grid not co-resident on this device (use the unfused step)");
+  hipLaunchKernelGGL(amp_sgd_large_kernel, dim3(grid), dim3(LARGE_THR), 0, cur_stream(), table.data_ptr<int64_t>(),
+                     scale.data_ptr<float>(), tracker.data_ptr<int>(), found_inf.data_ptr<float>(),
+                     reinterpret_cast<unsigned long long*>(sync.data_ptr<int64_t>()), (float)lr, (float)momentum,
+                     (float)dampening, (float)wd, (int)nesterov, (int)maximize, (float)growth, (float)backoff,
+                     (int)interval, reinterpret_cast<int*>(sync.data_ptr<int64_t>() + 3),
+                     (long long)(kBarrierSeconds * 1e8));
+  DPA_CHECK_LAUNCH();
+}
+
 void update_scale(at::Tensor scale, at::Tensor tracker, at::Tensor found_inf, double growth, double backoff,
                   int64_t interval) {
   check_f32(scale); check_f32(found_inf);
@@ -573,6 +846,11 @@ void register_optim(pybind11::module& m) {
   s.def("amp_sgd_fused", &opt::amp_sgd_fused);
   s.def("amp_sgd_xg_max", &opt::amp_sgd_xg_max);
   s.def("amp_sgd_resident", &opt::amp_sgd_resident);
+  s.def("amp_sgd_table", &opt::amp_sgd_table, pybind11::arg("params"), pybind11::arg("grads"), pybind11::arg("bufs"),
+        pybind11::arg("first") = std::vector<int64_t>{});
+  s.def("amp_sgd_large", &opt::amp_sgd_large);
+  s.def("amp_sgd_large_resident", &opt::amp_sgd_large_resident);
+  s.attr("LARGE_MAXT") = opt::LARGE_MAXT;
   s.attr("FUSED_MAX") = opt::FUSED_MAX;
   s.attr("MAXT") = opt::MAXT;
   s.def("flat_copy", &opt::flat_copy);

@@ -53,7 +53,7 @@ def supported(model, x: torch.Tensor) -> bool:
 
 _RESIDENT: dict = {}
 _SPLIT_BWD2 = os.environ.get("DPA_SPLIT_BWD2", "0") == "1"
-_SPLIT_WGRAD1 = os.environ.get("DPA_SPLIT_WGRAD1", "0") == "1"
+_SPLIT_WGRAD1 = os.environ.get("DPA_SPLIT_WGRAD1", "1") == "1"  # merged launch measured slower (15.0 vs 10.9 us)
 
 
 def _fused_site_engine(comm, batch: int, dtype: torch.dtype):

@@ -109,40 +109,79 @@ class SGD(Optimizer):
             out.append((group, params, grads, bufs, first))
         return out
 
-    def can_fuse_amp(self) -> bool:
-        """One parameter group of small f32 device tensors: unscale + inf-check +
-        SGD + scale update fit one launch of <= 128 co-resident workgroups."""
+    def _fuse_kind(self) -> str | None:
+        """"small": one launch of <= 128 co-resident workgroups holding every value in
+        registers (<= 2^19 floats, <= 36 tensors: the ConvNet); "large": the grid-stride
+        two-phase launch with a device tensor table (any size, <= 512 tensors: ResNet-50);
+        None: the multi-tensor unscale / SGD / update launches."""
         if len(self.param_groups) != 1:
-            return False
+            return None
         ps = [p for p in self.param_groups[0]["params"] if p.grad is not None]
-        if not ps or len(ps) > _load_ext().optim.MAXT:
-            return False
-        # the kernel rounds every tensor up to whole float4 granules (csrc/kernels/optim.hip)
-        if sum((p.numel() + 3) // 4 * 4 for p in ps) > self.FUSED_AMP_MAX_NUMEL:
-            return False
-        if not _load_ext().optim.amp_sgd_resident():
-            return False
-        def aligned(t):  # the kernel moves float4 granules
+        if not ps:
+            return None
+
+        def aligned(t):  # the kernels move float4 granules
             return t is None or t.data_ptr() % 16 == 0
 
-        return all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and p.grad.dtype == torch.float32
+        if not all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and p.grad.dtype == torch.float32
                    and p.grad.is_contiguous() and aligned(p) and aligned(p.grad)
-                   and aligned(self.state.get(p, {}).get("momentum_buffer")) for p in ps)
+                   and aligned(self.state.get(p, {}).get("momentum_buffer")) for p in ps):
+            return None
+        O = _load_ext().optim
+        # the kernel rounds every tensor up to whole float4 granules (csrc/kernels/optim.hip)
+        if (len(ps) <= O.MAXT and sum((p.numel() + 3) // 4 * 4 for p in ps) <= self.FUSED_AMP_MAX_NUMEL
+                and O.amp_sgd_resident()):
+            return "small"
+        if len(ps) <= O.LARGE_MAXT and O.amp_sgd_large_resident():
+            return "large"
+        return None
+
+    def can_fuse_amp(self) -> bool:
+        """Unscale + inf-check + SGD + scale update as one launch (see _fuse_kind)."""
+        return self._fuse_kind() is not None
+
+    def _large_table(self, params, grads, bufs, first):
+        """Device tensor table of the large fused step, cached per set of pointers (DDP
+        bucket-view grads and the optimizer state keep them fixed; freshly allocated
+        grads may not).  A table first built during graph capture stays referenced for
+        the life of the optimizer (the graph reads it on every replay)."""
+        key = (tuple(p.data_ptr() for p in params), tuple(g.data_ptr() for g in grads),
+               tuple(b.data_ptr() for b in bufs), tuple(first))
+        cache = self.__dict__.setdefault("_amp_tables", {})
+        t = cache.get(key)
+        if t is None:
+            t = _load_ext().optim.amp_sgd_table(params, grads, bufs, first)
+            if torch.cuda.is_current_stream_capturing():
+                self.__dict__.setdefault("_amp_tables_pinned", []).append(t)
+            if len(cache) >= 8:  # eager tables: the allocator's stream order makes freeing safe
+                cache.pop(next(iter(cache)))
+            cache[key] = t
+        return t
 
     @torch.no_grad()
     def fused_amp_step(self, scale, tracker, found_inf, growth, backoff, interval):
         (group, params, grads, bufs, first), = self._collect()
-        sync = getattr(self, "_amp_sync", None)
+        kind = self._fuse_kind()
+        name = "_amp_sync" if kind == "small" else "_amp_sync_large"
+        sync = getattr(self, name, None)
         if sync is None or sync.device != params[0].device:
             # grid-barrier state of the fused kernel (allocated before any graph capture:
             # the first step runs eagerly)
-            sync = self._amp_sync = torch.zeros(4, dtype=torch.int64, device=params[0].device)
+            sync = torch.zeros(4, dtype=torch.int64, device=params[0].device)
+            setattr(self, name, sync)
+        O = _load_ext().optim
+        if kind == "large":
+            self._flush_deferred()
+            O.amp_sgd_large(self._large_table(params, grads, bufs, first), group["lr"], group["momentum"],
+                            group["dampening"], group["weight_decay"], group["nesterov"], group["maximize"],
+                            scale, tracker, found_inf, growth, backoff, interval, sync)
+            return
         # gradients a DDP reducer deferred to this step are averaged inside the kernel
         d = getattr(self, "_deferred_ddp", None)
         xc = d[1] if d is not None and d[0].deferred_pending() else None
-        _load_ext().optim.amp_sgd_fused(params, grads, bufs, group["lr"], group["momentum"], group["dampening"],
-                                        group["weight_decay"], group["nesterov"], group["maximize"], first,
-                                        scale, tracker, found_inf, growth, backoff, interval, sync, xc)
+        O.amp_sgd_fused(params, grads, bufs, group["lr"], group["momentum"], group["dampening"],
+                        group["weight_decay"], group["nesterov"], group["maximize"], first,
+                        scale, tracker, found_inf, growth, backoff, interval, sync, xc)
         if xc is not None:
             d[0].consume_deferred()
 

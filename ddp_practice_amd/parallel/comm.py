@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import datetime
 import os
+import time
 
 import torch
 import torch.distributed as dist
@@ -259,6 +260,10 @@ class RcclCommunicator(Communicator):
         self._c.destroy()
 
 
+XGMI_DEFAULT_MAX_BYTES = 1 << 20  # one-shot: every ConvNet collective (<= 116 KB)
+XGMI_DEFAULT_TWOSHOT_MAX_BYTES = 32 << 20  # two-shot above it: a 25 MiB DDP bucket; RCCL above
+
+
 class XgmiCommunicator(Communicator):
     """All-reduce-only communicator on the one-shot xGMI engine.
 
@@ -271,7 +276,7 @@ class XgmiCommunicator(Communicator):
     """
 
     def __init__(self, rank: int, world_size: int, device: torch.device, store=None, key: str = "dpa_xgmi",
-                 max_bytes: int = 4 << 20, group=None):
+                 max_bytes: int = 4 << 20, group=None, twoshot_max_bytes: int = XGMI_DEFAULT_TWOSHOT_MAX_BYTES):
         C = _load_ext()
         self.rank, self.world_size = rank, world_size
         self.device = torch.device(device)
@@ -279,9 +284,12 @@ class XgmiCommunicator(Communicator):
         if store is None:
             store = dist.distributed_c10d._get_default_store()
         x, err = open_xgmi(rank, world_size, self.device, store, key, max_bytes,
-                           float(os.environ.get("DPA_XGMI_TIMEOUT", "600")))
+                           float(os.environ.get("DPA_XGMI_TIMEOUT", "600")), twoshot_max_bytes)
         if x is None:
             raise RuntimeError(f"xgmi communicator: {err}")
+        if twoshot_max_bytes > 0:
+            # ranks may share one GPU here: every rank's two-shot grid must be resident at once
+            x.set_twoshot_blocks(max(8, 192 // max(world_size, 1)))
         self.xgmi = x
         self._c = C.xgmi.XgmiCollective(x)
 
@@ -332,7 +340,6 @@ class XgmiCommunicator(Communicator):
 
 
 # ------------------------------------------------------------------ xGMI one-shot engine
-XGMI_DEFAULT_MAX_BYTES = 1 << 20  # every ConvNet collective (<= 116 KB); RCCL above
 
 
 def open_xgmi(rank: int, world: int, device: torch.device, store, key: str, max_bytes: int, timeout_s: float,
@@ -377,13 +384,17 @@ def comm_mode() -> str:
 def setup_xgmi(rc: "RcclCommunicator", store, key: str) -> str:
     """Attach the xGMI engine (csrc/comm/xgmi_allreduce.hip) to ``rc``.
 
-    ``comm_mode()`` rccl disables it; DPA_XGMI_MAX_BYTES sets the size up to which it
-    is used (default 1 MiB; ``--comm xgmi``: the whole workspace).  Before attaching,
-    every rank runs a self-test against RCCL (values within fp32 tolerance, results
-    bit-identical across ranks, bounded by a short timeout); any failure on any rank
-    keeps every rank on RCCL.  Every rank issues exactly the same collectives whatever
-    happens locally (a rank-local failure only flips its vote), so a misbehaving engine
-    can never desynchronise the RCCL call sequence.  Returns a status string.
+    ``comm_mode()`` rccl disables it.  One-shot up to DPA_XGMI_MAX_BYTES (default
+    1 MiB: every ConvNet collective); above that the two-shot (reduce-scatter +
+    all-gather over direct peer writes) up to DPA_XGMI_TWOSHOT_MAX_BYTES (default
+    32 MiB: a 25 MiB DDP bucket).  In auto mode the two-shot range is then trimmed by
+    a timing probe against RCCL (DPA_XGMI_PROBE=0 skips it); ``--comm xgmi`` keeps
+    the whole range.  Before attaching, every rank runs a self-test against RCCL
+    (values within fp32 tolerance, results bit-identical across ranks, bounded by a
+    short timeout); any failure on any rank keeps every rank on RCCL.  Every rank
+    issues exactly the same collectives whatever happens locally (a rank-local failure
+    only flips its vote), so a misbehaving engine can never desynchronise the RCCL
+    call sequence.  Returns a status string.
     """
     mode = comm_mode()
     if mode == "rccl":
@@ -391,39 +402,76 @@ def setup_xgmi(rc: "RcclCommunicator", store, key: str) -> str:
     if store is None:
         store = dist.distributed_c10d._get_default_store()
     max_bytes = int(float(os.environ.get("DPA_XGMI_MAX_BYTES", XGMI_DEFAULT_MAX_BYTES)))
-    if mode == "xgmi":
-        max_bytes = max(max_bytes, int(float(os.environ.get("DPA_XGMI_WORKSPACE_BYTES", 32 << 20))))
+    ts_max = int(float(os.environ.get("DPA_XGMI_TWOSHOT_MAX_BYTES", XGMI_DEFAULT_TWOSHOT_MAX_BYTES)))
     timeout = float(os.environ.get("DPA_XGMI_TIMEOUT", "600"))
     if max_bytes <= 0 or rc.world_size > 8:
         return "off"
-    x, err = open_xgmi(rc.rank, rc.world_size, rc.device, store, key, max_bytes, 20.0)
+    x, err = open_xgmi(rc.rank, rc.world_size, rc.device, store, key, max_bytes, 20.0, max(ts_max, 0))
     ok = torch.tensor([1.0 if x is not None else 0.0], device=rc.device)
     rc.native.all_reduce(ok, "min")
     if ok.item() != 1.0:
         return f"off (setup failed: {err or 'on a peer'})"
-    good, err = _xgmi_selftest(rc, x)
+    good, err = _xgmi_selftest(rc, x, ts_max > 0)
     if not good:
         return f"off (self-test failed: {err or 'on a peer'})"
+    if ts_max > 0 and mode == "auto" and os.environ.get("DPA_XGMI_PROBE", "1") != "0":
+        ts_max = _probe_twoshot(rc, x, max_bytes, ts_max)
     x.set_timeout(timeout)
-    rc.native.attach_xgmi(x, max_bytes)
+    rc.native.attach_xgmi(x, max_bytes, max(ts_max, 0))
     rc.xgmi = x
-    return f"on (<= {max_bytes} B)"
+    return f"on (one-shot <= {max_bytes} B, two-shot <= {max(ts_max, 0)} B)"
 
 
-def _xgmi_selftest(rc: "RcclCommunicator", x) -> tuple[bool, str]:
+def _probe_twoshot(rc: "RcclCommunicator", x, lo: int, hi: int) -> int:
+    """Largest probed size in (lo, hi] up to which the two-shot beats RCCL on this node
+    (fp32, 5 timed repetitions after 2 warm-ups; each rank's times max-reduced so
+    every rank picks the same bound).  Returns 0 if RCCL wins at the smallest size."""
+    sizes = [b for b in (2 << 20, 8 << 20, 32 << 20, 128 << 20) if lo < b <= hi] or [hi]
+    best = 0
+    for nb in sizes:
+        t = torch.ones(nb // 4, device=rc.device)
+        times = torch.zeros(2, device=rc.device)
+        for i, fn in enumerate((lambda: x.all_reduce_twoshot(t), lambda: rc.native.all_reduce(t, "sum"))):
+            for _ in range(2):
+                fn()
+            torch.cuda.synchronize(rc.device)
+            rc.native.barrier()
+            t0 = time.perf_counter()
+            for _ in range(5):
+                fn()
+            torch.cuda.synchronize(rc.device)
+            times[i] = time.perf_counter() - t0
+        rc.native.all_reduce(times, "max")
+        if x.error() != 0:
+            return 0
+        ts, rccl = times.tolist()
+        if ts <= rccl:
+            best = nb
+        else:
+            break
+    return best
+
+
+def _xgmi_selftest(rc: "RcclCommunicator", x, twoshot: bool = False) -> tuple[bool, str]:
     """Engine vs RCCL on a few sizes/dtypes/ops.  Per case, every rank issues the same
     RCCL collectives (reference all-reduce, cross-rank equality all-gather, vote); the
     vote is a min all-reduce so all ranks leave the loop together."""
     g = torch.Generator(device="cpu").manual_seed(1234 + rc.rank)
     why = ""
     vote = torch.ones(1, device=rc.device)
-    for n, dt, op in ((33, torch.float32, "sum"), (4099, torch.float32, "sum"), (29034, torch.float32, "sum"),
-                      (8195, torch.bfloat16, "sum"), (1000, torch.float32, "max")):
+    cases = [(33, torch.float32, "sum", 1), (4099, torch.float32, "sum", 1), (29034, torch.float32, "sum", 1),
+             (8195, torch.bfloat16, "sum", 1), (1000, torch.float32, "max", 1)]
+    if twoshot:
+        cases += [(1 << 20, torch.float32, "sum", 2), (700001, torch.bfloat16, "sum", 2)]
+    for n, dt, op, how in cases:
         t = torch.randn(n, generator=g).to(device=rc.device, dtype=dt)
         mine = torch.zeros_like(t)
         good = True
         try:
-            x.all_reduce(t, op, mine)
+            if how == 1:
+                x.all_reduce(t, op, mine)
+            else:
+                x.all_reduce_twoshot(t, op, mine)
         except Exception as e:  # noqa: BLE001 - recorded as this rank's vote
             good, why = False, f"{type(e).__name__}: {e}"
         ref = torch.empty_like(t)

@@ -329,3 +329,90 @@ def test_cross_entropy_prescaled_by_active_scaler(C, dtype):
             scaled.backward()
         tol = 1e-5 if dtype == torch.float32 else 1e-2
         torch.testing.assert_close(a.grad.float(), r.grad, rtol=tol, atol=tol * 256)
+
+
+@pytest.mark.parametrize("momentum,damp,nesterov", [(0.0, 0.0, False), (0.9, 0.0, True), (0.9, 0.1, False)])
+def test_large_fused_amp_sgd_matches_unfused(C, momentum, damp, nesterov):
+    """Large-model fused step (device tensor table, grid-stride two-phase launch) ==
+    the unfused unscale / SGD / update kernels: 161 tensors (ResNet-50's count) with
+    ragged sizes and 6.1M floats (> the small kernel's 2^19), non-finite grads on some
+    steps, eager and graph-replayed, the table built once and reused."""
+    torch.manual_seed(1)
+    g = torch.Generator().manual_seed(3)
+    sizes = [int(x) for x in torch.randint(1, 90000, (161,), generator=g)]
+    sizes[0], sizes[7], sizes[100] = 1, 3, 2_000_001
+    ps = [torch.randn(n, device=DEV) for n in sizes]
+    pa, pb = [p.clone() for p in ps], [p.clone() for p in ps]
+    ba = [torch.zeros_like(p) for p in ps] if momentum else []
+    bb = [torch.zeros_like(p) for p in ps] if momentum else []
+    sa, sb = torch.tensor([1024.0], device=DEV), torch.tensor([1024.0], device=DEV)
+    ta, tb = torch.zeros(1, dtype=torch.int32, device=DEV), torch.zeros(1, dtype=torch.int32, device=DEV)
+    fa, fb = torch.zeros(1, device=DEV), torch.zeros(1, device=DEV)
+    sync = torch.zeros(4, dtype=torch.int64, device=DEV)
+    ga = [torch.empty_like(p) for p in ps]
+    tables = {f: C.optim.amp_sgd_table(pa, ga, ba, [int(f)] * len(ps) if damp else []) for f in (True, False)}
+
+    def fused(first):
+        C.optim.amp_sgd_large(tables[first], 0.05, momentum, damp, 1e-4, nesterov, False, sa, ta, fa, 2.0, 0.5, 3,
+                              sync)
+
+    graph = None
+    for it in range(8):
+        gs = [torch.randn_like(p) * 1024 for p in ps]
+        if it in (2, 5):
+            x = gs[(it * 37) % len(gs)]
+            x[it % x.numel()] = float("nan") if it == 2 else float("-inf")
+        for x, y in zip(ga, gs):
+            x.copy_(y)
+        gb = [y.clone() for y in gs]
+        first = it == 0
+        if it < 4:
+            fused(first)
+        else:
+            if graph is None:
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    fused(False)
+            graph.replay()
+        C.optim.unscale_check(gb, sb, fb)
+        C.optim.sgd_step(pb, gb, bb, 0.05, momentum, damp, 1e-4, nesterov, False,
+                         [int(first)] * len(ps) if damp else [], fb, None)
+        C.optim.update_scale(sb, tb, fb, 2.0, 0.5, 3)
+        torch.cuda.synchronize()
+        for x, y in zip(pa + ga + ba, pb + gb + bb):
+            torch.testing.assert_close(x, y, equal_nan=True)
+        assert sa.item() == sb.item() and ta.item() == tb.item() and fa.item() == fb.item() == 0.0, it
+    assert int(sync[0]) == 8 and int(sync[3]) == 0
+
+
+def test_sgd_picks_large_fused_step(C):
+    """GradScaler + SGD on a ResNet-sized parameter set take the one-launch large path."""
+    from ddp_practice_amd.amp import GradScaler
+    from ddp_practice_amd.optim import SGD
+
+    ps = [torch.nn.Parameter(torch.randn(n, device=DEV)) for n in (600000, 5, 9408, 2048) * 10]
+    opt = SGD(ps, lr=0.1, momentum=0.9)
+    sc = GradScaler()
+    calls = {"large": 0, "sgd": 0}
+    orig_l, orig_s = C.optim.amp_sgd_large, C.optim.sgd_step
+
+    def spy_l(*a):
+        calls["large"] += 1
+        return orig_l(*a)
+
+    def spy_s(*a, **k):
+        calls["sgd"] += 1
+        return orig_s(*a, **k)
+
+    C.optim.amp_sgd_large, C.optim.sgd_step = spy_l, spy_s
+    try:
+        for _ in range(3):
+            loss = sum((p * p).sum() for p in ps)
+            opt.zero_grad(set_to_none=False)
+            sc.scale(loss).backward()
+            sc.step(opt)
+            sc.update()
+    finally:
+        C.optim.amp_sgd_large, C.optim.sgd_step = orig_l, orig_s
+    assert opt._fuse_kind() == "large"
+    assert calls["large"] >= 2  # the first iteration runs unfused (GradScaler learns the optimizer count)
