@@ -21,6 +21,7 @@ void register_convnet_fused(pybind11::module& m);
 void register_convnet_head(pybind11::module& m);
 void register_runtime(pybind11::module& m);
 void register_bn_nhwc(pybind11::module& m);
+void register_conv_igemm(pybind11::module& m);
 }
 
 // Opt-in (DPA_NATIVE_BACKTRACE=1) host-side SIGSEGV handler printing the native
@@ -54,4 +55,5 @@ PYBIND11_MODULE(_C, m) {
   dpa::register_convnet_head(m);
   dpa::register_runtime(m);
   dpa::register_bn_nhwc(m);
+  dpa::register_conv_igemm(m);
 }

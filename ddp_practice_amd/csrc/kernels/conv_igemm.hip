@@ -1,0 +1,411 @@
+// NHWC implicit-GEMM convolution on MFMA for the ResNet-50 stress config
+// (BASELINE.json config 5; the reference has no ResNet, its conv semantics are
+// torch's: /root/reference/ddp_main.py:83-93 trains the ConvNet with nn.Conv2d).
+//
+//   y[p][k] = sum_{r,s,c} x[n][oh*st+r-pad][ow*st+s-pad][c] * w[k][r][s][c]
+//   (p = (n, oh, ow): GEMM M = N*OH*OW pixels, N = Cout, K = R*S*C)
+//
+// with the BatchNorm statistics of the (storage-rounded) output produced in the
+// epilogue -- per channel sum(y - shift), sum((y - shift)^2) around the running
+// mean, the layout ops/bn_nhwc.py's kernels consume -- so a BN after a conv
+// needs no separate statistics pass over the activation.
+//
+// Geometry (MI355X, 64-wide waves, 160 KB LDS):
+//   * workgroup = 4 waves, tile 128 pixels x BN (64|128) channels, K-step 64
+//     (one filter tap (r,s) x 64 input channels: C % 64 == 0);
+//   * operands staged global -> registers -> LDS (double-buffered, one barrier
+//     per K-step), 16-B chunks, rows of 64 bf16 with the chunk index XOR-swizzled
+//     by (row & 7): the MFMA fragment reads (ds_read_b128) are at most 2-way;
+//   * MFMA orientation: A = weights (rows = output channels), B = pixels, so a
+//     lane's accumulator holds 4 CONSECUTIVE channels of one pixel
+//     (C/D map: row = 4*(lane>>4) + j, col = lane & 15): the BN sums reduce over
+//     lanes only, and the rounded tile is staged through LDS so it leaves as
+//     whole-row 16-B stores;
+//   * XCD-aware workgroup order (the channel tiles of one pixel tile share an L2);
+//   * the pixel tile's im2col addresses (n, ih0, iw0) are computed once per
+//     workgroup; padding / ragged M are zero-filled in the loader.
+#include "common.h"
+
+namespace dpa {
+namespace igemm {
+
+constexpr int THR = 256;
+constexpr int BM = 128;  // pixels per workgroup
+constexpr int BK = 64;   // reduction elements per K-step
+constexpr int SHIFT_OFF = 4;  // stats layout of bn_nhwc.hip: [2C] = rows, shift at [2C+4 ...)
+
+struct Geom {
+  int N, H, W, C, OH, OW, K, R, S, stride, pad;
+  long long M;  // N*OH*OW
+};
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
+
+// Statistics tree (all in the conv launch, deterministic: fixed-order sums):
+// every workgroup writes its [2][BN] partial row for its channel tile; the last
+// arriver of each group of G1 pixel tiles (ticket) sums the group's rows into a
+// level-2 row; the last level-2 arriver sums those and writes the final stats.
+// Tickets are re-armed by their last arriver (graph replays need no reset).
+constexpr int G1 = 32;
+
+struct StatArgs {
+  float* part;        // [nct][rows][2*BN] level 1, then [nct][NG][2*BN] level 2
+  unsigned* tickets;  // [nct][NG] + [nct], zero-initialised
+  float* stats;       // [3K+4]
+  const float* shift; // running mean (the sums are taken around it)
+  int64_t* nbt;       // num_batches_tracked (bumped once) or null
+};
+
+// Hand-off without fences (MI355X_MICROARCH.md "valid forms"): partial rows are
+// written with agent-scope relaxed atomic stores (write-through past the XCD's L2),
+// every wave drains its stores, one relaxed ticket per workgroup; the last arriver
+// reads the rows with agent-scope atomic loads.  No release fence: that would write
+// back the whole L2 (the conv output is dirty in it) once per workgroup.
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool last_arriver(unsigned* ticket, unsigned n, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores are done
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == n - 1;
+    *s_flag = last;
+    if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
+// dst[0, W) = sum over rows g < n of src[g*W + .] in row order (W = 2*BN <= 256 floats;
+// src read with write-through loads; dst written write-through when `wt`): lane owns a
+// column, THR/W row groups, combined in group order via scr
+template <int W>
+__device__ __forceinline__ void sum_rows(const float* __restrict__ src, int n, float* __restrict__ dst, float* scr,
+                                         bool wt) {
+  constexpr int RG = THR / W;
+  const int col = threadIdx.x % W, rg = threadIdx.x / W;
+  float acc = 0.f;
+  for (int g0 = rg; g0 < n; g0 += 8 * RG) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int gg = g0 + u * RG;
+      v[u] = ld_wt(src + (long long)(gg < n ? gg : 0) * W + col);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (g0 + u * RG < n) acc += v[u];
+  }
+  scr[rg * W + col] = acc;
+  __syncthreads();
+  if ((int)threadIdx.x < W) {
+    float t = 0.f;
+    for (int r = 0; r < RG; ++r) t += scr[r * W + threadIdx.x];
+    if (wt) st_wt(dst + threadIdx.x, t); else dst[threadIdx.x] = t;
+  }
+  __syncthreads();
+}
+
+// slab: [gridDim(pixel tiles)][2][K] partial statistics (null: none)
+template <typename T, int BN>
+__global__ void __launch_bounds__(THR)
+conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__ y, StatArgs sa, Geom g) {
+  using MMT = MM<T>;
+  typedef typename MMT::frag frag;
+  constexpr int CT = BN / 32;         // 16-channel tiles per wave (2 channel-waves)
+  constexpr int PT = 4;               // 16-pixel tiles per wave (64 pixels)
+  constexpr int BLD = BN / 32;        // B (weight) 16-B chunks per thread per K-step
+  __shared__ __attribute__((aligned(16))) T lds[2][(BM + BN) * BK];
+  __shared__ __attribute__((aligned(16))) float red[4][2][BN];
+  __shared__ int s_flag;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wp = wave & 1, wc = wave >> 1;  // pixel half, channel half
+  const int nct = g.K / BN;
+  // XCD-aware tile order: the hardware deals workgroup i to XCD i % 8; remap so that
+  // consecutive logical tiles -- the nct channel tiles of one pixel tile, which read the
+  // same activation rows -- run on one XCD and share its L2 (bijective for any grid)
+  const unsigned nwg = gridDim.x, hw = blockIdx.x;
+  const unsigned q8 = nwg / 8, r8 = nwg % 8, xcd = hw % 8, slot = hw / 8;
+  const unsigned lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const long long bm = lid / nct;
+  const int bn = (int)(lid % nct);
+  const long long p0 = bm * BM;
+  const int k0 = bn * BN;
+  const int KT = g.R * g.S * (g.C / BK);
+  const int cpt = g.C / BK;
+  // loader geometry: chunk cc of rows rr + 32 i
+  const int cc = tid & 7, rr = tid >> 3;
+  long long xb[4];
+  int ih0[4], iw0[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long long p = p0 + rr + 32 * i;
+    if (p < g.M) {
+      const int ow = (int)(p % g.OW);
+      const long long t = p / g.OW;
+      const int oh = (int)(t % g.OH);
+      const int n = (int)(t / g.OH);
+      xb[i] = (long long)n * g.H * g.W * g.C;
+      ih0[i] = oh * g.stride - g.pad;
+      iw0[i] = ow * g.stride - g.pad;
+    } else {
+      xb[i] = -1;
+      ih0[i] = iw0[i] = 0;
+    }
+  }
+  const long long wrow = (long long)g.R * g.S * g.C;
+  f32x4 rx[4], rw[BLD];
+  auto gload = [&](int kt) {
+    const int rs = kt / cpt, c0 = (kt - rs * cpt) * BK + cc * 8;
+    const int r = rs / g.S, s = rs - r * g.S;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ih = ih0[i] + r, iw = iw0[i] + s;
+      const bool ok = xb[i] >= 0 && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+      rx[i] = ok ? *reinterpret_cast<const f32x4*>(x + xb[i] + ((long long)ih * g.W + iw) * g.C + c0)
+                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < BLD; ++i)
+      rw[i] = *reinterpret_cast<const f32x4*>(w + (long long)(k0 + rr + 32 * i) * wrow + (long long)kt * BK + cc * 8);
+  };
+  auto lstore = [&](int buf) {
+    T* A = lds[buf];           // weights: rows [0, BN)
+    T* B = lds[buf] + BN * BK;  // pixels:  rows [0, BM)
+#pragma unroll
+    for (int i = 0; i < BLD; ++i) *reinterpret_cast<f32x4*>(A + swz(rr + 32 * i, cc)) = rw[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<f32x4*>(B + swz(rr + 32 * i, cc)) = rx[i];
+  };
+  f32x4 acc[CT][PT];
+#pragma unroll
+  for (int a = 0; a < CT; ++a)
+#pragma unroll
+    for (int b = 0; b < PT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < KT; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < KT) gload(kt + 1);
+    const T* A = lds[buf];
+    const T* B = lds[buf] + BN * BK;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      frag fa[CT], fb[PT];
+#pragma unroll
+      for (int a = 0; a < CT; ++a)
+        fa[a] = *reinterpret_cast<const frag*>(A + swz(wc * (BN / 2) + a * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int b = 0; b < PT; ++b)
+        fb[b] = *reinterpret_cast<const frag*>(B + swz(wp * 64 + b * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int a = 0; a < CT; ++a)
+#pragma unroll
+        for (int b = 0; b < PT; ++b) acc[a][b] = MMT::mma(fa[a], fb[b], acc[a][b]);
+    }
+    if (kt + 1 < KT) lstore(buf ^ 1);
+    __syncthreads();
+  }
+  // epilogue: lane holds channels k0 + wc*BN/2 + 16a + 4fq + j of pixel p0 + wp*64 + 16b + fr.
+  // The rounded tile goes through LDS ([pixel][channel], rows padded by 16 B: the
+  // 8-byte writes of a 16-pixel column are conflict-free) and leaves as whole 16-B
+  // chunks, consecutive lanes along a pixel's channels (full rows per store).
+  constexpr int RS = BN + 8;  // LDS row stride (elements)
+  T* tile = lds[0];
+#pragma unroll
+  for (int a = 0; a < CT; ++a) {
+    const int cl = wc * (BN / 2) + a * 16 + 4 * fq;
+#pragma unroll
+    for (int b = 0; b < PT; ++b) {
+      const int pl = wp * 64 + b * 16 + fr;
+      T v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = Cvt<T>::from_f(acc[a][b][j]);
+      *reinterpret_cast<u16x4*>(tile + pl * RS + cl) = *reinterpret_cast<const u16x4*>(v);
+    }
+  }
+  __syncthreads();
+  // With statistics, each lane first sums its fixed 8-channel chunk over its rows of
+  // the tile (the rounded values, around the running mean) and the workgroup's partial
+  // row goes out (write-through) and is ticketed BEFORE the output stores are issued:
+  // the ticket's store drain then never waits for the output tile.
+  constexpr int CPR = BN / 8;        // 16-B chunks per pixel row
+  constexpr int RPI = THR / CPR;     // pixel rows per pass
+  const bool stats = sa.part != nullptr;
+  const int ch = tid % CPR;
+  bool last1 = false;
+  long long rows = 0;
+  int NG = 0, grp = 0, gsz = 0;
+  if (stats) {
+    float s1[8], s2[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s1[j] = s2[j] = 0.f;
+      sh[j] = sa.shift[k0 + ch * 8 + j];
+    }
+#pragma unroll
+    for (int it = 0; it < BM / RPI; ++it) {
+      const int pl = it * RPI + tid / CPR;
+      if (p0 + pl < g.M) {
+        const f32x4 raw = *reinterpret_cast<const f32x4*>(tile + pl * RS + ch * 8);
+        const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = Cvt<T>::to_f(e[j]) - sh[j];
+          s1[j] += d;
+          s2[j] = fmaf(d, d, s2[j]);
+        }
+      }
+    }
+    // lanes of one wave sharing the chunk: xor over the row bits of the lane index
+#pragma unroll
+    for (int o = CPR; o < 64; o <<= 1)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s1[j] += __shfl_xor(s1[j], o);
+        s2[j] += __shfl_xor(s2[j], o);
+      }
+    if (lane < CPR)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[wave][0][ch * 8 + j] = s1[j];
+        red[wave][1][ch * 8 + j] = s2[j];
+      }
+    __syncthreads();
+    rows = (g.M + BM - 1) / BM;
+    NG = (int)((rows + G1 - 1) / G1);
+    float* lvl1 = sa.part + (long long)bn * rows * (2 * BN);
+    for (int t = tid; t < 2 * BN; t += THR) {
+      const int q = t / BN, c = t % BN;
+      st_wt(lvl1 + bm * (2 * BN) + t, red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c]);
+    }
+    grp = (int)(bm / G1);
+    gsz = (int)min((long long)G1, rows - (long long)grp * G1);
+    last1 = last_arriver(sa.tickets + bn * NG + grp, (unsigned)gsz, &s_flag);
+  }
+  // output stores: whole 16-B chunks, consecutive lanes along a pixel's channels
+#pragma unroll
+  for (int it = 0; it < BM / RPI; ++it) {
+    const int pl = it * RPI + tid / CPR;
+    const long long p = p0 + pl;
+    if (p < g.M)
+      *reinterpret_cast<f32x4*>(y + p * g.K + k0 + ch * 8) = *reinterpret_cast<const f32x4*>(tile + pl * RS + ch * 8);
+  }
+  if (!last1) return;
+  __syncthreads();  // every lane is done with the tile: its LDS becomes the tree's scratch
+  float* scr = reinterpret_cast<float*>(lds[1]);
+  float* lvl1 = sa.part + (long long)bn * rows * (2 * BN);
+  float* lvl2 = sa.part + (long long)nct * rows * (2 * BN) + (long long)bn * NG * (2 * BN);
+  sum_rows<2 * BN>(lvl1 + (long long)grp * G1 * (2 * BN), gsz, lvl2 + (long long)grp * (2 * BN), scr, true);
+  if (!last_arriver(sa.tickets + nct * NG + bn, (unsigned)NG, &s_flag)) return;
+  float* tot = &red[0][0][0];
+  sum_rows<2 * BN>(lvl2, NG, tot, scr, false);
+  for (int t = tid; t < BN; t += THR) {
+    sa.stats[k0 + t] = tot[t];
+    sa.stats[g.K + k0 + t] = tot[BN + t];
+    sa.stats[2 * g.K + SHIFT_OFF + k0 + t] = sa.shift[k0 + t];
+  }
+  if (bn == 0 && tid == 0) {
+    sa.stats[2 * g.K] = (float)g.M;
+    if (sa.nbt != nullptr) sa.nbt[0] = sa.nbt[0] + 1;
+  }
+}
+
+static Geom geom(const at::Tensor& x, const at::Tensor& w, int stride, int pad) {
+  // x: [N, C, H, W] channels_last; w: [K, C, R, S] channels_last (= [K][R][S][C] in memory)
+  Geom g;
+  g.N = (int)x.size(0); g.C = (int)x.size(1); g.H = (int)x.size(2); g.W = (int)x.size(3);
+  g.K = (int)w.size(0); g.R = (int)w.size(2); g.S = (int)w.size(3);
+  g.stride = stride; g.pad = pad;
+  g.OH = (g.H + 2 * pad - g.R) / stride + 1;
+  g.OW = (g.W + 2 * pad - g.S) / stride + 1;
+  g.M = (long long)g.N * g.OH * g.OW;
+  return g;
+}
+
+bool supported(int64_t C, int64_t K) { return C % BK == 0 && K % 64 == 0; }
+
+static int tile_n(int64_t K) { return K % 128 == 0 ? 128 : 64; }
+
+// statistics workspace: level-1 + level-2 partial rows (floats) and tickets (int32)
+int64_t stat_part_len(int64_t M, int64_t K) {
+  const int64_t rows = (M + BM - 1) / BM, ng = (rows + G1 - 1) / G1;
+  return 2 * K * (rows + ng);
+}
+int64_t stat_tickets_len(int64_t M, int64_t K) {
+  const int64_t rows = (M + BM - 1) / BM, ng = (rows + G1 - 1) / G1;
+  return (K / tile_n(K)) * (ng + 1);
+}
+
+// y: [N, K, OH, OW] channels_last (preallocated).  With `stats` (fp32 [3K+4], the
+// bn_nhwc layout), also part / tickets (stat_part_len / stat_tickets_len; tickets
+// zero-initialised once), shift (running mean) and nbt: the fused BN statistics.
+void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t pad, c10::optional<at::Tensor> part,
+              c10::optional<at::Tensor> tickets, c10::optional<at::Tensor> stats, c10::optional<at::Tensor> shift,
+              c10::optional<at::Tensor> nbt) {
+  TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "conv_fwd: device tensors");
+  TORCH_CHECK(x.scalar_type() == w.scalar_type() && x.scalar_type() == y.scalar_type(), "conv_fwd: one dtype");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "conv_fwd: bf16 / f16");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  y.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_fwd: channels_last x / w / y");
+  const Geom g = geom(x, w, (int)stride, (int)pad);
+  TORCH_CHECK(w.size(1) == g.C && supported(g.C, g.K), "conv_fwd: needs C % 64 == 0 and Cout % 64 == 0");
+  TORCH_CHECK(y.size(0) == g.N && y.size(1) == g.K && y.size(2) == g.OH && y.size(3) == g.OW, "conv_fwd: y shape");
+  const bool st = stats.has_value();
+  TORCH_CHECK(st == part.has_value() && st == tickets.has_value() && st == shift.has_value(),
+              "conv_fwd: part, tickets, stats and shift go together");
+  StatArgs sa{nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (st) {
+    TORCH_CHECK(part->scalar_type() == at::kFloat && part->numel() >= stat_part_len(g.M, g.K), "conv_fwd: part size");
+    TORCH_CHECK(tickets->scalar_type() == at::kInt && tickets->numel() >= stat_tickets_len(g.M, g.K),
+                "conv_fwd: tickets size");
+    TORCH_CHECK(stats->scalar_type() == at::kFloat && stats->numel() >= 3 * g.K + 4, "conv_fwd: stats size");
+    TORCH_CHECK(shift->scalar_type() == at::kFloat && shift->numel() == g.K, "conv_fwd: shift size");
+    sa.part = part->data_ptr<float>();
+    sa.tickets = reinterpret_cast<unsigned*>(tickets->data_ptr<int>());
+    sa.stats = stats->data_ptr<float>();
+    sa.shift = shift->data_ptr<float>();
+    sa.nbt = nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr;
+  }
+  const int BN = tile_n(g.K);
+  const long long rows = (g.M + BM - 1) / BM;
+  const long long blocks = rows * (g.K / BN);
+  TORCH_CHECK(blocks < (1LL << 31), "conv_fwd: grid too large");
+  auto launch = [&](auto tag) {
+    using T = decltype(tag);
+    const T* xp = reinterpret_cast<const T*>(x.data_ptr());
+    const T* wp = reinterpret_cast<const T*>(w.data_ptr());
+    T* yp = reinterpret_cast<T*>(y.data_ptr());
+    if (BN == 128)
+      hipLaunchKernelGGL((conv_fwd_kernel<T, 128>), dim3((unsigned)blocks), dim3(THR), 0, cur_stream(), xp, wp, yp,
+                         sa, g);
+    else
+      hipLaunchKernelGGL((conv_fwd_kernel<T, 64>), dim3((unsigned)blocks), dim3(THR), 0, cur_stream(), xp, wp, yp, sa,
+                         g);
+  };
+  if (x.scalar_type() == at::kBFloat16) launch(__hip_bfloat16{}); else launch(__half{});
+  DPA_CHECK_LAUNCH();
+}
+
+}  // namespace igemm
+
+void register_conv_igemm(pybind11::module& m) {
+  auto s = m.def_submodule("conv_igemm", "NHWC implicit-GEMM convolution on MFMA (+ fused BN statistics)");
+  s.def("conv_fwd", &igemm::conv_fwd, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
+        pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("part") = pybind11::none(),
+        pybind11::arg("tickets") = pybind11::none(), pybind11::arg("stats") = pybind11::none(),
+        pybind11::arg("shift") = pybind11::none(), pybind11::arg("nbt") = pybind11::none());
+  s.def("supported", &igemm::supported);
+  s.def("stat_part_len", &igemm::stat_part_len);
+  s.def("stat_tickets_len", &igemm::stat_tickets_len);
+}
+
+}  // namespace dpa

@@ -7,11 +7,14 @@ architecture is He et al. 2015 with the v1.5 stride placement (stride on the
 
 Execution on a HIP device (``fused=True``): activations are bf16/f16/f32
 ``channels_last`` (NHWC in memory) end to end;
-  * 1x1 convolutions are GEMMs on the NHWC rows ([N*H*W, Cin] x [Cin, Cout],
-    hipBLASLt; the weight gradient as a split-K batched GEMM with fp32
-    partials: ops/conv1x1.py; stride-2 projections subsample first);
-  * 3x3 / 7x7 convolutions go to MIOpen's NHWC kernels (ops/conv_nhwc.py: one
-    cast+layout copy of the weight each way);
+  * forward convolutions (1x1 and 3x3, any stride; C and Cout multiples of 64)
+    run on the hand-written NHWC implicit-GEMM MFMA kernel, which also produces
+    the following BatchNorm's batch statistics in its epilogue
+    (csrc/kernels/conv_igemm.hip, ops/conv_igemm.py; DPA_IGEMM=0: library path);
+  * backward: 1x1 convolutions are GEMMs on the NHWC rows (hipBLASLt; the weight
+    gradient as a split-K batched GEMM with fp32 partials: ops/conv1x1.py), 3x3
+    and the 7x7 stem (also its forward: C = 3) on MIOpen's NHWC kernels
+    (ops/conv_nhwc.py: one cast+layout copy of the weight each way);
   * every BatchNorm runs on the native NHWC kernels with its ReLU and, for the
     last BN of a bottleneck, the residual add fused in (ops/bn_nhwc.py), as
     SyncBatchNorm when the module was converted (one small all-reduce each way);
@@ -30,16 +33,23 @@ from ..ops.conv1x1 import GradTap, conv1x1
 from ..ops.conv_nhwc import conv_nhwc
 
 
-def _conv(x: torch.Tensor, conv: nn.Conv2d, cdtype: torch.dtype) -> torch.Tensor:
+def _conv(x: torch.Tensor, conv: nn.Conv2d, cdtype: torch.dtype, bn: nn.Module | None = None, tap=None):
+    """conv(x) -> (output, statistics of the following training BN ``bn`` when the conv
+    kernel produced them, else None)."""
+    want = bn if (bn is not None and bn.training) else None
     if conv.kernel_size == (1, 1) and conv.padding == (0, 0) and conv.groups == 1 and conv.bias is None:
-        return conv1x1(x, conv.weight, conv.stride[0], cdtype)
+        if want is None:
+            return conv1x1(x, conv.weight, conv.stride[0], cdtype, tap), None
+        return conv1x1(x, conv.weight, conv.stride[0], cdtype, tap, want)
     if conv.bias is None and conv.groups == 1 and conv.dilation == (1, 1):
-        return conv_nhwc(x, conv.weight, conv.stride, conv.padding, cdtype)
+        if want is None:
+            return conv_nhwc(x, conv.weight, conv.stride, conv.padding, cdtype), None
+        return conv_nhwc(x, conv.weight, conv.stride, conv.padding, cdtype, want)
     w = conv.weight.to(cdtype)
     out = F.conv2d(x, w, None if conv.bias is None else conv.bias.to(cdtype), conv.stride, conv.padding,
                    conv.dilation, conv.groups)
-    return out if out.is_contiguous(memory_format=torch.channels_last) else \
-        out.contiguous(memory_format=torch.channels_last)
+    return (out if out.is_contiguous(memory_format=torch.channels_last) else
+            out.contiguous(memory_format=torch.channels_last)), None
 
 
 def _comm_of(bn: nn.Module):
@@ -83,15 +93,18 @@ class Bottleneck(nn.Module):
         # identity blocks: conv1's dgrad GEMM accumulates the residual gradient (GradTap)
         tap = GradTap() if (self.downsample is None and self.bn3.training and torch.is_grad_enabled()
                             and x.requires_grad and x.is_contiguous(memory_format=torch.channels_last)) else None
-        c1 = conv1x1(x, self.conv1.weight, 1, cdtype, tap) if tap is not None else _conv(x, self.conv1, cdtype)
-        out = bn_act(c1, self.bn1, relu=True, comm=_comm_of(self.bn1))
-        out = bn_act(_conv(out, self.conv2, cdtype), self.bn2, relu=True, comm=_comm_of(self.bn2))
+        # each conv hands the following BN its batch statistics (ops/conv_igemm.py)
+        c1, st = _conv(x, self.conv1, cdtype, self.bn1, tap)
+        out = bn_act(c1, self.bn1, relu=True, comm=_comm_of(self.bn1), stats=st)
+        c2, st = _conv(out, self.conv2, cdtype, self.bn2)
+        out = bn_act(c2, self.bn2, relu=True, comm=_comm_of(self.bn2), stats=st)
         identity = x
         if self.downsample is not None:
             conv, bn = self.downsample[0], self.downsample[1]
-            identity = bn_act(_conv(x, conv, cdtype), bn, relu=False, comm=_comm_of(bn))
-        return bn_act(_conv(out, self.conv3, cdtype), self.bn3, res=identity, relu=True, comm=_comm_of(self.bn3),
-                      tap=tap)
+            cd, st = _conv(x, conv, cdtype, bn)
+            identity = bn_act(cd, bn, relu=False, comm=_comm_of(bn), stats=st)
+        c3, st = _conv(out, self.conv3, cdtype, self.bn3)
+        return bn_act(c3, self.bn3, res=identity, relu=True, comm=_comm_of(self.bn3), tap=tap, stats=st)
 
 
 class ResNet(nn.Module):
@@ -147,7 +160,8 @@ class ResNet(nn.Module):
 
         cdtype = compute_dtype(x) if self.amp_dtype is not None else torch.float32
         x = x.to(dtype=cdtype, memory_format=torch.channels_last)
-        x = bn_act(_conv(x, self.conv1, cdtype), self.bn1, relu=True, comm=_comm_of(self.bn1))
+        c, st = _conv(x, self.conv1, cdtype, self.bn1)
+        x = bn_act(c, self.bn1, relu=True, comm=_comm_of(self.bn1), stats=st)
         x = max_pool_3x3s2(x)
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
             for blk in layer:

@@ -47,7 +47,7 @@ def _cl(t: torch.Tensor) -> torch.Tensor:
 class BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, res, running_mean, running_var, nbt, momentum, eps, training, relu, comm,
-                tap=None):
+                tap=None, pre=None):
         K = _K()
         x = _cl(x)
         C = x.shape[1]
@@ -57,9 +57,12 @@ class BNActFn(torch.autograd.Function):
         mom = -1.0 if momentum is None else float(momentum)
         f32 = dict(dtype=torch.float32, device=dev)
         if training:
-            part, ticket = _Workspace.get(dev, C)
-            stats = torch.empty(3 * C + 4, **f32)
-            K.fwd_stats(x, C, running_mean, part, ticket, stats, nbt)
+            if pre is not None:  # computed in the producing conv's epilogue (ops/conv_igemm.py)
+                stats = pre
+            else:
+                part, ticket = _Workspace.get(dev, C)
+                stats = torch.empty(3 * C + 4, **f32)
+                K.fwd_stats(x, C, running_mean, part, ticket, stats, nbt)
             sync = comm is not None and comm.active
             if sync:
                 comm.all_reduce_(stats.narrow(0, 0, 2 * C + 1))
@@ -98,14 +101,17 @@ class BNActFn(torch.autograd.Function):
         K.bwd_elemt(dy, y, x, C, ctx.act, save, sums, stats, weight, bias, dx, dres)
         if ctx.tap is not None:  # d(res) goes to the consumer's GEMM (ops/conv1x1.py GradTap)
             ctx.tap.grad, dres = dres, None
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None
 
 
-def bn_act(x, bn, res=None, relu=True, comm=None, tap=None):
+def bn_act(x, bn, res=None, relu=True, comm=None, tap=None, stats=None):
     """BatchNorm module ``bn`` applied to channels_last ``x`` (+ res) (+ ReLU).
-    ``tap``: hand d(res) to a GradTap instead of returning it (ops/conv1x1.py)."""
+    ``tap``: hand d(res) to a GradTap instead of returning it (ops/conv1x1.py).
+    ``stats``: the batch statistics already computed by the producing conv
+    (ops/conv_igemm.py; training only) -- no statistics pass here."""
     return BNActFn.apply(x, bn.weight, bn.bias, res, bn.running_mean, bn.running_var, bn.num_batches_tracked,
-                         bn.momentum, bn.eps, bn.training, relu, comm if bn.training else None, tap)
+                         bn.momentum, bn.eps, bn.training, relu, comm if bn.training else None, tap,
+                         stats if bn.training else None)
 
 
 class MaxPoolFn(torch.autograd.Function):

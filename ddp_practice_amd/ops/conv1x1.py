@@ -20,6 +20,8 @@ from __future__ import annotations
 
 import torch
 
+from . import conv_igemm as _igemm
+
 WGRAD_CHUNK_ROWS = 2048
 WGRAD_MAX_SPLIT = 64
 
@@ -73,26 +75,46 @@ class GradTap:
 
 class Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride: int, cdtype: torch.dtype, tap: GradTap | None = None):
+    def forward(ctx, x, weight, stride: int, cdtype: torch.dtype, tap: GradTap | None = None, bn=None):
         in_shape = x.shape
-        if stride != 1:
-            x = x[:, :, ::stride, ::stride]
-        N, C, H, W = x.shape
-        rows = _rows(x.to(cdtype))
-        w = weight.reshape(weight.shape[0], C).to(cdtype)
-        out = torch.mm(rows, w.t())
-        ctx.save_for_backward(rows, w)
-        ctx.geom = (N, C, H, W, stride, in_shape)
-        ctx.wshape = weight.shape
-        ctx.tap = tap
         if tap is not None and stride != 1:
             raise ValueError("conv1x1: a gradient tap needs stride 1")
-        return out.view(N, H, W, -1).permute(0, 3, 1, 2)
+        ctx.tap = tap
+        ctx.wshape = weight.shape
+        C = x.shape[1]
+        w = weight.reshape(weight.shape[0], C).to(cdtype)
+        if _igemm.usable(x, weight, cdtype):
+            # implicit-GEMM kernel: strided rows read in place, the BN statistics fused
+            xc = x.to(cdtype)
+            xc = xc if xc.is_contiguous(memory_format=torch.channels_last) else \
+                xc.contiguous(memory_format=torch.channels_last)
+            out, stats = _igemm.conv_fwd(xc, w.view(weight.shape[0], C, 1, 1), stride, 0, bn)
+            N, _, H, W = out.shape
+            ctx.save_for_backward(xc, w)
+            ctx.lazy_rows = True
+        else:
+            if stride != 1:
+                x = x[:, :, ::stride, ::stride]
+            N, C, H, W = x.shape
+            rows = _rows(x.to(cdtype))
+            out = torch.mm(rows, w.t()).view(N, H, W, -1).permute(0, 3, 1, 2)
+            stats = None
+            ctx.save_for_backward(rows, w)
+            ctx.lazy_rows = False
+        ctx.geom = (N, C, H, W, stride, in_shape)
+        ctx.n_out = 1 if bn is None else 2
+        if bn is None:
+            return out
+        if stats is not None:
+            ctx.mark_non_differentiable(stats)
+        return out, stats
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, *_):
         rows, w = ctx.saved_tensors
         N, C, H, W, stride, in_shape = ctx.geom
+        if ctx.lazy_rows:  # saved the (unstrided) input: its [P, C] rows at the output pixels
+            rows = _rows(rows[:, :, ::stride, ::stride] if stride != 1 else rows)
         dyr = _rows(dy.to(rows.dtype))
         dx = dw = None
         acc = None
@@ -112,12 +134,13 @@ class Conv1x1Fn(torch.autograd.Function):
                 dx = full
         if ctx.needs_input_grad[1]:
             dw = _wgrad(dyr, rows).view(ctx.wshape)
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
 def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int, cdtype: torch.dtype,
-            tap: GradTap | None = None) -> torch.Tensor:
+            tap: GradTap | None = None, bn=None):
     """Bias-free 1x1 conv (stride 1 or 2) of ``x`` with the fp32 ``weight``; the
     output is a channels_last [N, Cout, H', W'] tensor in ``cdtype``.  ``tap``:
-    see :class:`GradTap`."""
-    return Conv1x1Fn.apply(x, weight, int(stride), cdtype, tap)
+    see :class:`GradTap`.  With ``bn`` (the training BatchNorm that follows): returns
+    (output, its statistics or None) -- ops/conv_igemm.py."""
+    return Conv1x1Fn.apply(x, weight, int(stride), cdtype, tap, bn)

@@ -1,0 +1,64 @@
+"""Forward convolution on the hand-written NHWC implicit-GEMM MFMA kernel
+(csrc/kernels/conv_igemm.hip) with the following BatchNorm's statistics fused
+into its epilogue (ResNet-50 stress model, models/resnet.py).
+
+``conv_forward(x, weight, stride, pad, cdtype, bn)`` returns the channels_last
+output and, when ``bn`` is a training BatchNorm, the statistics vector that
+``ops/bn_nhwc.bn_act(..., stats=...)`` consumes instead of running its own
+statistics pass over the activation (sums around the running mean, row count,
+shift copy; num_batches_tracked bumped in the same launch).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from .._ext import load as _load_ext
+
+_CL = torch.channels_last
+ENABLED = os.environ.get("DPA_IGEMM", "1") != "0"  # 0: MIOpen / hipBLASLt forward + separate stats (A/B)
+
+
+def _K():
+    return _load_ext().conv_igemm
+
+
+class _StatWS:
+    """Per-device partial rows + tickets of the in-launch statistics tree (stream-ordered
+    reuse: every launch re-arms the tickets it used)."""
+
+    _by_dev: dict = {}
+
+    @classmethod
+    def get(cls, dev: torch.device, M: int, K: int):
+        k = _K()
+        need_p, need_t = int(k.stat_part_len(M, K)), int(k.stat_tickets_len(M, K))
+        ws = cls._by_dev.get(dev)
+        if ws is None or ws[0].numel() < need_p or ws[1].numel() < need_t:
+            part = torch.empty(max(need_p, 1 << 20), dtype=torch.float32, device=dev)
+            tickets = torch.zeros(max(need_t, 1 << 12), dtype=torch.int32, device=dev)
+            ws = cls._by_dev[dev] = (part, tickets)
+        return ws
+
+
+def usable(x: torch.Tensor, weight: torch.Tensor, cdtype: torch.dtype) -> bool:
+    return (ENABLED and x.is_cuda and cdtype in (torch.bfloat16, torch.float16) and weight.dim() == 4
+            and bool(_K().supported(weight.shape[1], weight.shape[0])))
+
+
+def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn=None):
+    """y = conv(x, w) on the implicit-GEMM kernel; x, w channels_last in the compute dtype.
+    With ``bn`` (a training BatchNorm module): also its statistics, returned as the second
+    value (None otherwise)."""
+    N, C, H, W = x.shape
+    K, _, R, S = w.shape
+    OH, OW = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
+    y = torch.empty((N, K, OH, OW), dtype=x.dtype, device=x.device, memory_format=_CL)
+    if bn is None:
+        _K().conv_fwd(x, w, y, stride, pad)
+        return y, None
+    part, tickets = _StatWS.get(x.device, N * OH * OW, K)
+    stats = torch.empty(3 * K + 4, dtype=torch.float32, device=x.device)
+    _K().conv_fwd(x, w, y, stride, pad, part, tickets, stats, bn.running_mean, bn.num_batches_tracked)
+    return y, stats

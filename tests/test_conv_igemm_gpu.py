@@ -1,0 +1,56 @@
+"""NHWC implicit-GEMM convolution on MFMA (csrc/kernels/conv_igemm.hip) vs a
+plain PyTorch fp32 reference of the same op, and its fused BN statistics vs
+the statistics of the storage-rounded output."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CL = torch.channels_last
+
+
+def _run(C, N, Cin, H, W, K, R, stride, pad, dtype, stats):
+    g = torch.Generator().manual_seed(R * 131 + K + H)
+    x = torch.randn(N, Cin, H, W, generator=g).to(DEV, dtype).contiguous(memory_format=CL)
+    w = (torch.randn(K, Cin, R, R, generator=g) / (Cin * R * R) ** 0.5).to(DEV, dtype).contiguous(memory_format=CL)
+    OH = (H + 2 * pad - R) // stride + 1
+    OW = (W + 2 * pad - R) // stride + 1
+    y = torch.empty(N, K, OH, OW, dtype=dtype, device=DEV, memory_format=CL)
+    ref = F.conv2d(x.float(), w.float(), None, stride, pad)
+    if stats:
+        M = N * OH * OW
+        part = torch.empty(C.conv_igemm.stat_part_len(M, K), device=DEV)
+        tk = torch.zeros(C.conv_igemm.stat_tickets_len(M, K), dtype=torch.int32, device=DEV)
+        st = torch.empty(3 * K + 4, device=DEV)
+        shift = torch.randn(K, generator=g).to(DEV) * 0.1
+        nbt = torch.zeros(1, dtype=torch.int64, device=DEV)
+        for _ in range(2):  # the tickets re-arm themselves
+            C.conv_igemm.conv_fwd(x, w, y, stride, pad, part, tk, st, shift, nbt)
+        assert int(tk.abs().sum()) == 0
+    else:
+        C.conv_igemm.conv_fwd(x, w, y, stride, pad)
+    torch.cuda.synchronize()
+    tol = 2e-2 if dtype == torch.bfloat16 else 4e-3
+    err = ((y.float() - ref).abs().max() / ref.abs().max()).item()
+    assert err < tol, err
+    if stats:
+        yr = y.float().permute(0, 2, 3, 1).reshape(-1, K) - shift
+        torch.testing.assert_close(st[:K], yr.sum(0), rtol=1e-4, atol=1e-2)
+        torch.testing.assert_close(st[K:2 * K], (yr * yr).sum(0), rtol=1e-4, atol=1e-2)
+        assert st[2 * K].item() == M and int(nbt) == 2
+        torch.testing.assert_close(st[2 * K + 4:3 * K + 4], shift)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [
+    (2, 64, 14, 14, 64, 3, 1, 1),     # 3x3 s1, BN=64 tile
+    (2, 128, 15, 15, 128, 3, 2, 1),   # 3x3 s2, odd input
+    (3, 64, 7, 7, 256, 1, 1, 0),      # 1x1 expand, ragged M = 147
+    (2, 256, 14, 14, 128, 1, 2, 0),   # 1x1 s2 projection
+    (1, 192, 9, 9, 192, 3, 1, 1),     # Cout = 192: BN=64 tiles
+    (8, 64, 56, 56, 64, 1, 1, 0),     # 196 pixel tiles: two-level statistics tree (G1 = 32)
+])
+@pytest.mark.parametrize("stats", [False, True])
+def test_conv_fwd_matches_torch(C, dtype, shape, stats):
+    _run(C, *shape, dtype, stats)
