@@ -24,6 +24,9 @@
 //   * XCD-aware workgroup order (the channel tiles of one pixel tile share an L2);
 //   * the pixel tile's im2col addresses (n, ih0, iw0) are computed once per
 //     workgroup; padding / ragged M are zero-filled in the loader.
+#include <algorithm>
+#include <type_traits>
+
 #include "common.h"
 
 namespace dpa {
@@ -318,6 +321,184 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------
+// Weight gradient:  dW[k][r][s][c] = sum_p dy[p][k] * x[n][oh*st+r-pad][ow*st+s-pad][c]
+// GEMM M = Cout, N = R*S*C, reduction over the pixels p -- both operands are stored
+// pixel-major, so they are staged in LDS as [64 pixels][cols] rows and read TRANSPOSED
+// into the MFMA operands with ds_read_b64_tr_b16 (each 16-lane group: 4 pixel rows x
+// 16 columns; two reads make a lane's 8 consecutive pixels).  Row chunks are XOR-
+// swizzled by 2*f(row), f(row) = (row&3) | ((row>>1)&4): the 8 rows one 32-lane half
+// reads map to 8 distinct chunk pairs (conflict-free with 16 chunks per row).
+// Split over the pixels: S partial fp32 tiles -> wgrad_reduce_kernel, which also
+// writes the fp32 OIHW gradient directly (no separate layout/cast pass).
+typedef __attribute__((ext_vector_type(4))) short v4s;
+
+template <int CH>  // 16-B chunks per LDS row
+__device__ __forceinline__ int wswz(int row, int chunk) {
+  const int f = (row & 3) | ((row >> 1) & 4);
+  const int m = CH >= 16 ? 2 * f : 2 * (f & 3);
+  return row * CH * 8 + ((chunk ^ m) << 3);
+}
+
+template <typename T, int BM, int BN>
+__global__ void __launch_bounds__(THR)
+conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ slab, Geom g, int splits,
+                  long long pps) {
+  typedef typename MM<T>::frag frag;
+  constexpr int BP = 64;                 // pixels per K-step
+  constexpr int CHA = BM / 8, CHB = BN / 8;
+  constexpr int LA = BP * CHA / THR, LB = BP * CHB / THR;  // 16-B loads per thread
+  constexpr int MT = BM / 32, NT = BN / 32;
+  __shared__ __attribute__((aligned(16))) T lds[2][BP * (BM + BN)];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int RSC = g.R * g.S * g.C;
+  const int tm = g.K / BM, tn = RSC / BN, tiles = tm * tn;
+  const unsigned nwg = gridDim.x, hw = blockIdx.x;
+  const unsigned q8 = nwg / 8, r8 = nwg % 8, xcd = hw % 8, slot = hw / 8;
+  const unsigned lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int sp = (int)(lid / tiles), tile = (int)(lid % tiles);
+  const int k0 = (tile / tn) * BM, n0 = (tile % tn) * BN;
+  const int rs = n0 / g.C, c0 = n0 - rs * g.C, fr_ = rs / g.S, fs_ = rs - fr_ * g.S;
+  const long long pa = sp * pps, pb = min(g.M, pa + pps);
+  const int steps = (int)((pb - pa + BP - 1) / BP);
+  f32x4 ra[LA], rb[LB];
+  auto gload = [&](int t) {
+    const long long pbase = pa + (long long)t * BP;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int e = i * THR + tid, row = e / CHA, cc = e % CHA;
+      const long long p = pbase + row;
+      ra[i] = p < pb ? *reinterpret_cast<const f32x4*>(dy + p * g.K + k0 + cc * 8) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int e = i * THR + tid, row = e / CHB, cc = e % CHB;
+      const long long p = pbase + row;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (p < pb) {
+        const unsigned pu = (unsigned)p, q = pu / (unsigned)g.OW;  // M < 2^31 (host check)
+        const int ow = (int)(pu - q * (unsigned)g.OW);
+        const unsigned n = q / (unsigned)g.OH;
+        const int oh = (int)(q - n * (unsigned)g.OH);
+        const int ih = oh * g.stride + fr_ - g.pad, iw = ow * g.stride + fs_ - g.pad;
+        if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
+          v = *reinterpret_cast<const f32x4*>(x + (((long long)n * g.H + ih) * g.W + iw) * g.C + c0 + cc * 8);
+      }
+      rb[i] = v;
+    }
+  };
+  auto lstore = [&](int buf) {
+    T* A = lds[buf];
+    T* B = lds[buf] + BP * BM;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int e = i * THR + tid;
+      *reinterpret_cast<f32x4*>(A + wswz<CHA>(e / CHA, e % CHA)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int e = i * THR + tid;
+      *reinterpret_cast<f32x4*>(B + wswz<CHB>(e / CHB, e % CHB)) = rb[i];
+    }
+  };
+  // transposed fragment: 8 consecutive pixel rows (32kk + 8g .. +7) of column cb + (lane & 15)
+  const int grp = lane >> 4, gi = lane & 15, q = gi >> 2, pq = gi & 3;
+  auto trfrag = [&](const T* base, int kk, int cb, auto chtag) -> frag {
+    constexpr int CH = decltype(chtag)::value;
+    const int row = 32 * kk + 8 * grp + q, col = cb + 4 * pq;
+    const T* a0 = base + wswz<CH>(row, col >> 3) + (col & 7);
+    const T* a1 = base + wswz<CH>(row + 4, col >> 3) + (col & 7);
+    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)a0);
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)a1);
+    typedef __attribute__((ext_vector_type(8))) short v8s;
+    const v8s v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(frag, v);
+  };
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (steps > 0) {
+    gload(0);
+    lstore(0);
+  }
+  __syncthreads();
+  for (int t = 0; t < steps; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < steps) gload(t + 1);
+    const T* A = lds[buf];
+    const T* B = lds[buf] + BP * BM;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      frag fa[MT], fb[NT];
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+        fa[a] = trfrag(A, kk, wm * (BM / 2) + a * 16, std::integral_constant<int, CHA>{});
+#pragma unroll
+      for (int b = 0; b < NT; ++b)
+        fb[b] = trfrag(B, kk, wn * (BN / 2) + b * 16, std::integral_constant<int, CHB>{});
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b) acc[a][b] = MM<T>::mma(fa[a], fb[b], acc[a][b]);
+    }
+    if (t + 1 < steps) lstore(buf ^ 1);
+    __syncthreads();
+  }
+  // partial tile: C[m = k][n = (r,s,c)]; lane: col n = lane & 15, rows 4*(lane>>4) + j
+  float* out = slab + (long long)sp * g.K * RSC;
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = k0 + wm * (BM / 2) + a * 16 + 4 * grp + j, n = n0 + wn * (BN / 2) + b * 16 + gi;
+        out[(long long)m * RSC + n] = acc[a][b][j];
+      }
+}
+
+// grad[k][c][r][s] (fp32 OIHW) = sum over splits of slab[sp][k][(r*S + s)*C + c]:
+// a workgroup owns 256 consecutive slab columns as 64 float4 quads x 4 split groups
+// (every 4th split, fixed order, 4 loads in flight), combined through LDS in group
+// order, written in the OIHW order.
+__global__ void __launch_bounds__(256)
+wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ grad, int splits, int K, int C, int R, int S) {
+  __shared__ f32x4 part[4][64];
+  const long long RSC = (long long)R * S * C, total = (long long)K * RSC;
+  const int qd = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const long long col = (blockIdx.x * 64LL + qd) * 4;  // total % 4 == 0 (C % 64 == 0)
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (col < total) {
+    int sp = rg;
+    for (; sp + 12 < splits; sp += 16) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(slab + (long long)sp * total + col);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(slab + (long long)(sp + 4) * total + col);
+      const f32x4 c = *reinterpret_cast<const f32x4*>(slab + (long long)(sp + 8) * total + col);
+      const f32x4 d = *reinterpret_cast<const f32x4*>(slab + (long long)(sp + 12) * total + col);
+      acc += a;
+      acc += b;
+      acc += c;
+      acc += d;
+    }
+    for (; sp < splits; sp += 4) acc += *reinterpret_cast<const f32x4*>(slab + (long long)sp * total + col);
+  }
+  part[rg][qd] = acc;
+  __syncthreads();
+  if (rg == 0 && col < total) {
+    const f32x4 t = part[0][qd] + part[1][qd] + part[2][qd] + part[3][qd];
+    const int k = (int)(col / RSC);
+    const long long n = col - (long long)k * RSC;  // (r*S + s)*C + c, c % 4 == 0
+    const int c = (int)(n % C), rs = (int)(n / C);
+    float* o = grad + ((long long)k * C + c) * R * S + rs;
+    const int st = R * S;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j * st] = t[j];
+  }
+}
+
 static Geom geom(const at::Tensor& x, const at::Tensor& w, int stride, int pad) {
   // x: [N, C, H, W] channels_last; w: [K, C, R, S] channels_last (= [K][R][S][C] in memory)
   Geom g;
@@ -395,6 +576,57 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
   DPA_CHECK_LAUNCH();
 }
 
+// wgrad tile shapes: BM | Cout, BN | C (a column tile stays inside one filter tap)
+static int wtile(int64_t v) { return v % 128 == 0 ? 128 : 64; }
+
+int64_t wgrad_splits(int64_t M, int64_t K, int64_t C, int64_t R, int64_t S) {
+  // ~2-4 workgroups per CU, each at least 16 K-steps of 64 pixels, and the fp32
+  // partials at most ~48 MB (written and re-read once: ~12 us at HBM rate)
+  const int64_t tiles = (K / wtile(K)) * (R * S * C / wtile(C));
+  int64_t sp = std::max<int64_t>(1, 768 / tiles);
+  sp = std::min<int64_t>(sp, std::max<int64_t>(1, M / 1024));
+  sp = std::min<int64_t>(sp, std::max<int64_t>(1, (12LL << 20) / (K * R * S * C)));
+  return sp;
+}
+
+// dy: [N, K, OH, OW] channels_last; x: [N, C, H, W] channels_last; grad: fp32 [K, C, R, S]
+// contiguous (written, not accumulated); slab: fp32 >= splits * K * R*S*C
+void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor grad, int64_t stride, int64_t pad, at::Tensor slab) {
+  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && grad.is_cuda() && slab.is_cuda(), "conv_wgrad: device tensors");
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf),
+              "conv_wgrad: bf16 / f16 activations");
+  TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_wgrad: channels_last dy / x");
+  TORCH_CHECK(grad.scalar_type() == at::kFloat && grad.is_contiguous() && grad.dim() == 4, "conv_wgrad: fp32 grad");
+  const Geom g = geom(x, grad, (int)stride, (int)pad);
+  TORCH_CHECK(grad.size(1) == g.C && supported(g.C, g.K), "conv_wgrad: needs C % 64 == 0 and Cout % 64 == 0");
+  TORCH_CHECK(dy.size(0) == g.N && dy.size(1) == g.K && dy.size(2) == g.OH && dy.size(3) == g.OW, "conv_wgrad: dy");
+  TORCH_CHECK(g.M < (1LL << 31), "conv_wgrad: too many pixels");
+  const int64_t sp = wgrad_splits(g.M, g.K, g.C, g.R, g.S);
+  const int64_t RSC = (int64_t)g.R * g.S * g.C;
+  TORCH_CHECK(slab.scalar_type() == at::kFloat && slab.numel() >= sp * g.K * RSC, "conv_wgrad: slab too small");
+  const long long pps = ((g.M + sp - 1) / sp + 63) / 64 * 64;
+  const int BM = wtile(g.K), BN = wtile(g.C);
+  const long long blocks = sp * (g.K / BM) * (RSC / BN);
+  auto launch = [&](auto tag) {
+    using T = decltype(tag);
+    const T* dp = reinterpret_cast<const T*>(dy.data_ptr());
+    const T* xp = reinterpret_cast<const T*>(x.data_ptr());
+    float* sl = slab.data_ptr<float>();
+    const dim3 gr((unsigned)blocks), th(THR);
+    if (BM == 128 && BN == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 128>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+    else if (BM == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 64>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+    else if (BN == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 128>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 64>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+  };
+  if (x.scalar_type() == at::kBFloat16) launch(__hip_bfloat16{}); else launch(__half{});
+  DPA_CHECK_LAUNCH();
+  const long long total = (long long)g.K * RSC;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, cur_stream(),
+                     slab.data_ptr<float>(), grad.data_ptr<float>(), (int)sp, g.K, g.C, g.R, g.S);
+  DPA_CHECK_LAUNCH();
+}
+
 }  // namespace igemm
 
 void register_conv_igemm(pybind11::module& m) {
@@ -406,6 +638,8 @@ void register_conv_igemm(pybind11::module& m) {
   s.def("supported", &igemm::supported);
   s.def("stat_part_len", &igemm::stat_part_len);
   s.def("stat_tickets_len", &igemm::stat_tickets_len);
+  s.def("conv_wgrad", &igemm::conv_wgrad);
+  s.def("wgrad_splits", &igemm::wgrad_splits);
 }
 
 }  // namespace dpa

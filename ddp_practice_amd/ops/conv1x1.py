@@ -111,11 +111,12 @@ class Conv1x1Fn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, *_):
-        rows, w = ctx.saved_tensors
+        saved, w = ctx.saved_tensors
         N, C, H, W, stride, in_shape = ctx.geom
-        if ctx.lazy_rows:  # saved the (unstrided) input: its [P, C] rows at the output pixels
-            rows = _rows(rows[:, :, ::stride, ::stride] if stride != 1 else rows)
-        dyr = _rows(dy.to(rows.dtype))
+        dyc = dy.to(w.dtype)
+        if not dyc.is_contiguous(memory_format=torch.channels_last):
+            dyc = dyc.contiguous(memory_format=torch.channels_last)
+        dyr = _rows(dyc)
         dx = dw = None
         acc = None
         if ctx.tap is not None:
@@ -133,7 +134,13 @@ class Conv1x1Fn(torch.autograd.Function):
                 full[:, :, ::stride, ::stride] = dx
                 dx = full
         if ctx.needs_input_grad[1]:
-            dw = _wgrad(dyr, rows).view(ctx.wshape)
+            if ctx.lazy_rows and _igemm.usable(dyc, w.view(ctx.wshape), w.dtype):
+                # implicit-GEMM weight gradient over the (strided) input pixels, fp32 out
+                dw = _igemm.conv_wgrad(dyc, saved, tuple(ctx.wshape), stride, 0)
+            else:
+                # saved: the [P, C] rows, or (lazy) the unstrided input
+                rows = _rows(saved[:, :, ::stride, ::stride] if stride != 1 else saved) if ctx.lazy_rows else saved
+                dw = _wgrad(dyr, rows).view(ctx.wshape)
         return dx, dw, None, None, None, None
 
 

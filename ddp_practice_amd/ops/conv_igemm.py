@@ -62,3 +62,26 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn=None):
     stats = torch.empty(3 * K + 4, dtype=torch.float32, device=x.device)
     _K().conv_fwd(x, w, y, stride, pad, part, tickets, stats, bn.running_mean, bn.num_batches_tracked)
     return y, stats
+
+
+class _WgradWS:
+    _by_dev: dict = {}
+
+    @classmethod
+    def get(cls, dev: torch.device, n: int):
+        ws = cls._by_dev.get(dev)
+        if ws is None or ws.numel() < n:
+            ws = cls._by_dev[dev] = torch.empty(max(n, 1 << 22), dtype=torch.float32, device=dev)
+        return ws
+
+
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, wshape, stride: int, pad: int) -> torch.Tensor:
+    """fp32 OIHW weight gradient of a conv on the implicit-GEMM kernel (pixel-split
+    partials reduced straight into the OIHW layout); dy, x channels_last."""
+    K, C, R, S = wshape
+    N, _, OH, OW = dy.shape
+    sp = int(_K().wgrad_splits(N * OH * OW, K, C, R, S))
+    slab = _WgradWS.get(dy.device, sp * K * C * R * S)
+    grad = torch.empty(wshape, dtype=torch.float32, device=dy.device)
+    _K().conv_wgrad(dy, x, grad, stride, pad, slab)
+    return grad

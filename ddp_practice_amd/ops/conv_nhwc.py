@@ -48,13 +48,30 @@ class ConvNHWCFn(torch.autograd.Function):
         stride, padding = ctx.conf
         dy = dy.to(w.dtype)
         dy = dy if dy.is_contiguous(memory_format=_CL) else dy.contiguous(memory_format=_CL)
-        mask = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False]
-        dx, dw, _ = torch.ops.aten.convolution_backward(dy, x.to(w.dtype), w, None, stride, padding, [1, 1], False,
-                                                        [0, 0], 1, mask)
-        if dw is not None:
-            g = torch.empty(dw.shape, dtype=ctx.wdtype, device=dw.device)
-            g.copy_(dw)  # cdtype NHWC -> fp32 NCHW in one kernel
-            dw = g
+        dx = None
+        if (ctx.needs_input_grad[0] and stride == [1, 1] and padding[0] == padding[1]
+                and w.shape[2] == w.shape[3] and _igemm.usable(dy, w.transpose(0, 1), w.dtype)):
+            # stride-1 data gradient = a forward conv of dy with the flipped, transposed
+            # filter on the implicit-GEMM kernel (pad R-1-p)
+            R = w.shape[2]
+            wt = torch.empty((w.shape[1], w.shape[0], R, R), dtype=w.dtype, device=w.device, memory_format=_CL)
+            wt.copy_(w.flip(2, 3).transpose(0, 1))
+            dx, _ = _igemm.conv_fwd(dy, wt, 1, R - 1 - padding[0])
+        dw = None
+        xc = x.to(w.dtype)
+        if (ctx.needs_input_grad[1] and ctx.wdtype == torch.float32 and stride[0] == stride[1]
+                and padding[0] == padding[1] and _igemm.usable(dy, w, w.dtype)):
+            # weight gradient on the implicit-GEMM kernel, written as the fp32 OIHW .grad
+            dw = _igemm.conv_wgrad(dy, xc, tuple(w.shape), stride[0], padding[0])
+        mask = [ctx.needs_input_grad[0] and dx is None, ctx.needs_input_grad[1] and dw is None, False]
+        if mask[0] or mask[1]:
+            dx2, dw2, _ = torch.ops.aten.convolution_backward(dy, xc, w, None, stride, padding, [1, 1], False,
+                                                              [0, 0], 1, mask)
+            if dx is None:
+                dx = dx2
+            if dw2 is not None:
+                dw = torch.empty(dw2.shape, dtype=ctx.wdtype, device=dw2.device)
+                dw.copy_(dw2)  # cdtype NHWC -> fp32 NCHW in one kernel
         return dx, dw, None, None, None, None
 
 

@@ -54,3 +54,54 @@ def _run(C, N, Cin, H, W, K, R, stride, pad, dtype, stats):
 @pytest.mark.parametrize("stats", [False, True])
 def test_conv_fwd_matches_torch(C, dtype, shape, stats):
     _run(C, *shape, dtype, stats)
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 14, 14, 128, 3, 1, 1), (2, 128, 9, 9, 64, 3, 2, 1), (2, 64, 8, 8, 64, 1, 1, 0)])
+def test_conv_ops_fwd_bwd_with_stats(C, shape):
+    """ops conv_nhwc / conv1x1 with the implicit-GEMM forward (+BN statistics) and the
+    stride-1 data gradient on the same kernel == fp32 torch autograd."""
+    from ddp_practice_amd.ops.conv1x1 import conv1x1
+    from ddp_practice_amd.ops.conv_nhwc import conv_nhwc
+
+    N, Cin, H, W, K, R, stride, pad = shape
+    g = torch.Generator().manual_seed(7)
+    x0 = torch.randn(N, Cin, H, W, generator=g)
+    w0 = torch.randn(K, Cin, R, R, generator=g) / (Cin * R * R) ** 0.5
+    dy0 = torch.randn(N, K, (H + 2 * pad - R) // stride + 1, (W + 2 * pad - R) // stride + 1, generator=g)
+    xr, wr = x0.clone().requires_grad_(), w0.clone().requires_grad_()
+    F.conv2d(xr, wr, None, stride, pad).backward(dy0)
+    bn = torch.nn.BatchNorm2d(K).to(DEV)
+    x = x0.to(DEV, torch.bfloat16).contiguous(memory_format=CL).requires_grad_()
+    w = w0.to(DEV).requires_grad_()
+    if R == 1:
+        y, st = conv1x1(x, w, stride, torch.bfloat16, None, bn)
+    else:
+        y, st = conv_nhwc(x, w, (stride, stride), (pad, pad), torch.bfloat16, bn)
+    assert st is not None and int(bn.num_batches_tracked) == 1
+    y.backward(dy0.to(DEV, torch.bfloat16).contiguous(memory_format=CL))
+    for got, ref in ((x.grad, xr.grad), (w.grad, wr.grad)):
+        err = ((got.float().cpu() - ref).abs().max() / ref.abs().max()).item()
+        assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [
+    (2, 64, 14, 14, 64, 3, 1, 1),     # 64 x 576: BM=64, BN=64
+    (2, 128, 15, 15, 128, 3, 2, 1),   # stride 2, odd input
+    (3, 256, 7, 7, 128, 1, 1, 0),     # 1x1, ragged pixel count
+    (2, 128, 14, 14, 256, 1, 2, 0),   # 1x1 s2 projection
+    (4, 64, 28, 28, 128, 3, 1, 1),    # several pixel splits
+])
+def test_conv_wgrad_matches_torch(C, dtype, shape):
+    from ddp_practice_amd.ops.conv_igemm import conv_wgrad
+
+    N, Cin, H, W, K, R, stride, pad = shape
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(N, Cin, H, W, generator=g).to(DEV, dtype).contiguous(memory_format=CL)
+    OH = (H + 2 * pad - R) // stride + 1
+    dy = torch.randn(N, K, OH, OH, generator=g).to(DEV, dtype).contiguous(memory_format=CL)
+    w = torch.zeros(K, Cin, R, R, device=DEV, requires_grad=True)
+    F.conv2d(x.float(), w, None, stride, pad).backward(dy.float())
+    got = conv_wgrad(dy, x, (K, Cin, R, R), stride, pad)
+    err = ((got - w.grad).abs().max() / w.grad.abs().max()).item()
+    assert err < 1e-2, err
