@@ -283,6 +283,9 @@ class XgmiCommunicator(Communicator):
         self.group = group
         if store is None:
             store = dist.distributed_c10d._get_default_store()
+        # ranks may share one GPU (the test tier): every rank's one-shot grid (one 256-lane
+        # workgroup per 8 KB of message) must be resident at once -> <= ~1024 workgroups total
+        max_bytes = min(int(max_bytes), max(1, 1024 // max(world_size, 1)) * 8192)
         x, err = open_xgmi(rank, world_size, self.device, store, key, max_bytes,
                            float(os.environ.get("DPA_XGMI_TIMEOUT", "600")), twoshot_max_bytes)
         if x is None:
@@ -290,6 +293,7 @@ class XgmiCommunicator(Communicator):
         if twoshot_max_bytes > 0:
             # ranks may share one GPU here: every rank's two-shot grid must be resident at once
             x.set_twoshot_blocks(max(8, 192 // max(world_size, 1)))
+        self.xgmi_status = f"one-shot <= {max_bytes} B, two-shot <= {max(twoshot_max_bytes, 0)} B"
         self.xgmi = x
         self._c = C.xgmi.XgmiCollective(x)
 
