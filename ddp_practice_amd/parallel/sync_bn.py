@@ -44,7 +44,8 @@ class _SyncBNFn(torch.autograd.Function):
         invstd = torch.rsqrt(var + eps)
         with torch.no_grad():
             nbt.add_(1)
-            mom = momentum if momentum is not None else 1.0 / float(nbt.item())
+            # cumulative average (momentum=None) stays on the device: no host sync
+            mom = momentum if momentum is not None else nbt.reciprocal().float()
             running_mean.mul_(1 - mom).add_(mean * mom)
             running_var.mul_(1 - mom).add_(var * (n / (n - 1).clamp_min(1)) * mom)
         shp = (1, C) + (1,) * (x.dim() - 2)
@@ -78,6 +79,18 @@ class _SyncBNFn(torch.autograd.Function):
                 None, None)
 
 
+class _NativeBN:
+    """bn_act(relu=False) with the module's buffers; gamma / beta passed explicitly so
+    a non-affine module can use constant ones / zeros."""
+
+    @staticmethod
+    def apply(x, w, b, mod, comm):
+        from ..ops.bn_nhwc import BNActFn
+
+        return BNActFn.apply(x, w, b, None, mod.running_mean, mod.running_var, mod.num_batches_tracked,
+                             mod.momentum, mod.eps, True, False, comm, None, None)
+
+
 class SyncBatchNorm(_BatchNorm):
     """Drop-in for torch.nn.SyncBatchNorm (same parameters / buffers / state_dict)."""
 
@@ -97,9 +110,28 @@ class SyncBatchNorm(_BatchNorm):
             return pg
         return _comm.default_comm()
 
+    def _native(self, x) -> bool:
+        """4-D device input in training: the channels_last kernels of ops/bn_nhwc.py
+        (statistics, one all-reduce of 2C+1 floats, apply; backward sums, one all-reduce,
+        elementwise) instead of the torch-op path below."""
+        return (x.is_cuda and x.dim() == 4 and self.training and self.track_running_stats
+                and x.dtype in (torch.float32, torch.float16, torch.bfloat16))
+
     def forward(self, x):
         self._check_input_dim(x)
         comm = self.comm
+        if self._native(x):
+            from ..ops.bn_nhwc import bn_act
+
+            C = x.shape[1]
+            if not self.affine:  # the kernels take gamma / beta: identity affine
+                if getattr(self, "_ones", None) is None or self._ones.device != x.device:
+                    self._ones = torch.ones(C, device=x.device)
+                    self._zeros = torch.zeros(C, device=x.device)
+            w = self.weight if self.affine else self._ones
+            b = self.bias if self.affine else self._zeros
+            y = _NativeBN.apply(x, w, b, self, comm if comm.active else None)
+            return y if x.is_contiguous(memory_format=torch.channels_last) else y.contiguous()
         if not self.training or not self.track_running_stats or not comm.active:
             if self.training and self.track_running_stats:
                 # the same shifted-sum path, world of one
