@@ -1121,9 +1121,17 @@ conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __r
   constexpr int XR = ROWS + 4;
   constexpr int ROWLEN = COUT * N + COUT;
   typedef MM<T> mm;
-  __shared__ __attribute__((aligned(16))) T dyl[COUT * ROWS * WP];
+  // LDS pitches padded by 16 B so the MFMA operand reads spread over the banks:
+  //  * dy rows (A operand: 16 lanes = 16 output channels) DYS apart;
+  //  * input copies (B operand) XCS apart per (kw, ci); with CIN >= 16 the GEMM columns
+  //    run ci-fastest (column n = tap*CIN + ci), so the 16 lanes of a fragment read 16
+  //    channels of one tap: 16 distinct 4-bank windows.  (CIN = 1: 16 taps, <= 2-way.)
+  constexpr int DYS = ROWS * WP + 8;
+  constexpr int XCS = XR * WP + 8;
+  constexpr bool CIF = CIN >= 16;  // ci-fastest column order
+  __shared__ __attribute__((aligned(16))) T dyl[COUT * DYS];
   constexpr int WX = WP + 4;  // padded input row (2 halo columns each side, room for the kw shift)
-  __shared__ __attribute__((aligned(16))) T xs[5 * CIN * XR * WP];
+  __shared__ __attribute__((aligned(16))) T xs[5 * CIN * XCS];
   // whole image per workgroup: the 5 shifted copies are written straight from
   // registers (no padded staging image, no LDS->LDS copy pass)
   constexpr bool DIRECT = (ROWS == H);
@@ -1166,23 +1174,23 @@ conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __r
   // dy chunk -> dyl[co][rr][0..WP) (pad columns zero)
   for (int e = tid; e < COUT * ROWS * (WP - W); e += NTHR) {
     const int cr = e / (WP - W), cc = W + e % (WP - W);
-    dyl[cr * WP + cc] = zero;
+    dyl[(cr / ROWS) * DYS + (cr % ROWS) * WP + cc] = zero;
   }
   if (r0 + ROWS > H) {  // rows past the image (last chunk): zero
     for (int e = tid; e < COUT * ROWS * WP; e += NTHR)
-      if (r0 + (e / WP) % ROWS >= H) dyl[e] = zero;
+      if (r0 + (e / WP) % ROWS >= H) dyl[(e / (ROWS * WP)) * DYS + e % (ROWS * WP)] = zero;
   }
   // xs[kw][ci][rr][c] = x[ci][r0 + rr - 2][c + kw - 2] (zero outside the image)
   auto scatter5 = [&](int ci, int rr, int w, T v) {
 #pragma unroll
     for (int kw = 0; kw < 5; ++kw) {
       const int c = w + 2 - kw;
-      if (c >= 0 && c < WP) xs[((kw * CIN + ci) * XR + rr) * WP + c] = v;
+      if (c >= 0 && c < WP) xs[(kw * CIN + ci) * XCS + rr * WP + c] = v;
     }
   };
   if constexpr (DIRECT) {
-    constexpr int NZ = 5 * CIN * XR * WP * (int)sizeof(T) / 16;
-    static_assert((5 * CIN * XR * WP * sizeof(T)) % 16 == 0, "xs must be a whole number of 16-B chunks");
+    constexpr int NZ = 5 * CIN * XCS * (int)sizeof(T) / 16;
+    static_assert((5 * CIN * XCS * sizeof(T)) % 16 == 0, "xs must be a whole number of 16-B chunks");
     uint4* z = reinterpret_cast<uint4*>(xs);
     for (int e = tid; e < NZ; e += NTHR) z[e] = make_uint4(0u, 0u, 0u, 0u);
   } else {
@@ -1210,15 +1218,15 @@ conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __r
     bn_bwd_coef<COUT, T>(bin, coef, part, sums, bid == 0);
     DPA_STAMP(3);
     st.emit(coef, [&](int co, int h, int ww, T v00, T v01, T v10, T v11) {
-      dyl[(co * ROWS + h) * WP + ww] = v00;
-      dyl[(co * ROWS + h) * WP + ww + 1] = v01;
-      dyl[(co * ROWS + h + 1) * WP + ww] = v10;
-      dyl[(co * ROWS + h + 1) * WP + ww + 1] = v11;
+      dyl[co * DYS + h * WP + ww] = v00;
+      dyl[co * DYS + h * WP + ww + 1] = v01;
+      dyl[co * DYS + (h + 1) * WP + ww] = v10;
+      dyl[co * DYS + (h + 1) * WP + ww + 1] = v11;
     });
   } else if constexpr (DIRECT) {  // both operands are full [C][H][W] images
     stage_chw<T, COUT, H, W>(dyb, [&](int co, int h, int ww, T a, T bb) {
-      dyl[(co * ROWS + h) * WP + ww] = a;
-      dyl[(co * ROWS + h) * WP + ww + 1] = bb;
+      dyl[co * DYS + h * WP + ww] = a;
+      dyl[co * DYS + h * WP + ww + 1] = bb;
     });
     __syncthreads();  // xs zero-fill before the scatter
     stage_chw<T, CIN, H, W>(xb, [&](int ci, int h, int ww, T a, T bb) {
@@ -1229,7 +1237,7 @@ conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __r
     for (int e = tid; e < COUT * ROWS * W; e += NTHR) {
       const int co = e / (ROWS * W), rem = e % (ROWS * W);
       const int rr = rem / W, cc = rem % W;
-      if (r0 + rr < H) dyl[(co * ROWS + rr) * WP + cc] = dyb[(co * H + r0 + rr) * W + cc];
+      if (r0 + rr < H) dyl[co * DYS + rr * WP + cc] = dyb[(co * H + r0 + rr) * W + cc];
     }
     stage_xpad();
   }
@@ -1242,7 +1250,7 @@ conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __r
       const int rowid = e / (WP / 8);  // (kw, ci, rr)
       const int kw = rowid / (CIN * XR), cr = rowid % (CIN * XR);
       const T* srcp = &xpad[cr * WX + 8 * c8 + kw];
-      T* dstp = &xs[rowid * WP + 8 * c8];
+      T* dstp = &xs[(kw * CIN + cr / XR) * XCS + (cr % XR) * WP + 8 * c8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) dstp[j] = srcp[j];
     }
@@ -1265,7 +1273,7 @@ conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __r
     const int co = tid / TPC, sub = tid % TPC;
     float a = 0.f;
     for (int i = sub * 8; i < E; i += TPC * 8) {
-      const typename mm::frag v = mm::ld(&dyl[co * ROWS * WP + i]);
+      const typename mm::frag v = mm::ld(&dyl[co * DYS + i]);
       const T* e = reinterpret_cast<const T*>(&v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) a += Cvt<T>::to_f(e[j]);
@@ -1282,9 +1290,10 @@ conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __r
     const int mt = pr / NTL, nt = pr % NTL;
     int n = nt * 16 + r;
     n = n < N ? n : 0;
-    const int ci = n / 25, kh = (n % 25) / 5, kw = n % 5;
-    const T* brow = &xs[((kw * CIN + ci) * XR + kh) * WP];
-    const T* arow = &dyl[(mt * 16 + r) * ROWS * WP];
+    const int ci = CIF ? n % CIN : n / 25, tap = CIF ? n / CIN : n % 25;
+    const int kh = tap / 5, kw = tap % 5;
+    const T* brow = &xs[(kw * CIN + ci) * XCS + kh * WP];
+    const T* arow = &dyl[(mt * 16 + r) * DYS];
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = ks; s < KSTEPS; s += KSPLIT) {
@@ -1300,11 +1309,12 @@ conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __r
       if (ks != 0) continue;
       for (int k2 = 1; k2 < KSPLIT; ++k2) acc += kred[wv + k2][lane];
     }
-    // D[row = 4q+i][col = r]: dW[co = mt*16+4q+i][n]
+    // D[row = 4q+i][col = r]: dW[co = mt*16+4q+i][ci][kh][kw] (natural order in the row)
     const int col = nt * 16 + r;
     if (col < N) {
+      const int nat = CIF ? (col % CIN) * 25 + col / CIN : col;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) put(&row_out[(mt * 16 + 4 * q + i) * N + col], acc[i]);
+      for (int i = 0; i < 4; ++i) put(&row_out[(mt * 16 + 4 * q + i) * N + nat], acc[i]);
     }
   }
   DPA_STAMP(7);
