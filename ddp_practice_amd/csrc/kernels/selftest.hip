@@ -83,7 +83,31 @@ double launch_floor(at::Tensor buf, int64_t n, int64_t reps, bool graph, int64_t
   return std::chrono::duration<double, std::micro>(t1 - t0).count() / (double)(n * reps);
 }
 
+// Workgroup start probe: per workgroup [start s_memrealtime, XCC id, end], so the
+// dispatch order / per-XCD start offsets of a launch can be measured.  `spin`
+// (100 MHz ticks) keeps every workgroup alive for a while (one wave per workgroup).
+__global__ void __launch_bounds__(64) xcd_probe_kernel(long long* out, long long spin) {
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  // HW_REG_XCC_ID (hwreg 20), bits [3:0]
+  const int xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xf;
+  long long t = t0;
+  while (t - t0 < spin) t = (long long)__builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    out[3 * blockIdx.x] = t0;
+    out[3 * blockIdx.x + 1] = xcc;
+    out[3 * blockIdx.x + 2] = t;
+  }
+}
+
+void xcd_probe(at::Tensor out, int64_t blocks, int64_t spin) {
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kLong && out.numel() >= 3 * blocks, "xcd_probe: out");
+  hipLaunchKernelGGL(xcd_probe_kernel, dim3((unsigned)blocks), dim3(64), 0, cur_stream(),
+                     reinterpret_cast<long long*>(out.data_ptr<int64_t>()), (long long)spin);
+  DPA_CHECK_LAUNCH();
+}
+
 void register_selftest(pybind11::module& m) {
+  m.def("xcd_probe", &xcd_probe, "per-workgroup start time / XCC id of one launch");
   m.def("launch_floor", &launch_floor, "us per dependent no-op kernel (eager or hipGraph)");
   m.def("mfma_selftest", &mfma_selftest, "16x16x32 bf16 and 16x16x4 f32 MFMA lane-map test");
 }
