@@ -40,6 +40,7 @@ constexpr int SHIFT_OFF = 4;  // stats layout of bn_nhwc.hip: [2C] = rows, shift
 struct Geom {
   int N, H, W, C, OH, OW, K, R, S, stride, pad;
   long long M;  // N*OH*OW
+  int accumulate = 0;  // conv_fwd: y += conv(x, w) (a residual gradient already in y)
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
@@ -298,8 +299,18 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
   for (int it = 0; it < BM / RPI; ++it) {
     const int pl = it * RPI + tid / CPR;
     const long long p = p0 + pl;
-    if (p < g.M)
-      *reinterpret_cast<f32x4*>(y + p * g.K + k0 + ch * 8) = *reinterpret_cast<const f32x4*>(tile + pl * RS + ch * 8);
+    if (p < g.M) {
+      f32x4* dst = reinterpret_cast<f32x4*>(y + p * g.K + k0 + ch * 8);
+      f32x4 raw = *reinterpret_cast<const f32x4*>(tile + pl * RS + ch * 8);
+      if (g.accumulate) {  // y += tile, summed in fp32, rounded once
+        const f32x4 old = *dst;
+        const T* a = reinterpret_cast<const T*>(&old);
+        T* b = reinterpret_cast<T*>(&raw);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = Cvt<T>::from_f(Cvt<T>::to_f(a[j]) + Cvt<T>::to_f(b[j]));
+      }
+      *dst = raw;
+    }
   }
   if (!last1) return;
   __syncthreads();  // every lane is done with the tile: its LDS becomes the tree's scratch
@@ -530,17 +541,19 @@ int64_t stat_tickets_len(int64_t M, int64_t K) {
 // zero-initialised once), shift (running mean) and nbt: the fused BN statistics.
 void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t pad, c10::optional<at::Tensor> part,
               c10::optional<at::Tensor> tickets, c10::optional<at::Tensor> stats, c10::optional<at::Tensor> shift,
-              c10::optional<at::Tensor> nbt) {
+              c10::optional<at::Tensor> nbt, bool accumulate) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "conv_fwd: device tensors");
   TORCH_CHECK(x.scalar_type() == w.scalar_type() && x.scalar_type() == y.scalar_type(), "conv_fwd: one dtype");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "conv_fwd: bf16 / f16");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast) &&
                   y.is_contiguous(at::MemoryFormat::ChannelsLast),
               "conv_fwd: channels_last x / w / y");
-  const Geom g = geom(x, w, (int)stride, (int)pad);
+  Geom g = geom(x, w, (int)stride, (int)pad);
+  g.accumulate = accumulate ? 1 : 0;
   TORCH_CHECK(w.size(1) == g.C && supported(g.C, g.K), "conv_fwd: needs C % 64 == 0 and Cout % 64 == 0");
   TORCH_CHECK(y.size(0) == g.N && y.size(1) == g.K && y.size(2) == g.OH && y.size(3) == g.OW, "conv_fwd: y shape");
   const bool st = stats.has_value();
+  TORCH_CHECK(!(st && accumulate), "conv_fwd: statistics of an accumulated output are not supported");
   TORCH_CHECK(st == part.has_value() && st == tickets.has_value() && st == shift.has_value(),
               "conv_fwd: part, tickets, stats and shift go together");
   StatArgs sa{nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -634,7 +647,8 @@ void register_conv_igemm(pybind11::module& m) {
   s.def("conv_fwd", &igemm::conv_fwd, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("y"),
         pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("part") = pybind11::none(),
         pybind11::arg("tickets") = pybind11::none(), pybind11::arg("stats") = pybind11::none(),
-        pybind11::arg("shift") = pybind11::none(), pybind11::arg("nbt") = pybind11::none());
+        pybind11::arg("shift") = pybind11::none(), pybind11::arg("nbt") = pybind11::none(),
+        pybind11::arg("accumulate") = false);
   s.def("supported", &igemm::supported);
   s.def("stat_part_len", &igemm::stat_part_len);
   s.def("stat_tickets_len", &igemm::stat_tickets_len);

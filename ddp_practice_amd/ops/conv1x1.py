@@ -107,6 +107,8 @@ class Conv1x1Fn(torch.autograd.Function):
             return out
         if stats is not None:
             ctx.mark_non_differentiable(stats)
+        # no zero tensor materialised for the statistics output's (absent) gradient
+        ctx.set_materialize_grads(False)
         return out, stats
 
     @staticmethod
@@ -121,11 +123,23 @@ class Conv1x1Fn(torch.autograd.Function):
         acc = None
         if ctx.tap is not None:
             acc, ctx.tap.grad = ctx.tap.grad, None
+        K = w.shape[0]
+        mine = (ctx.needs_input_grad[0] and stride == 1 and _igemm.dgrad_1x1_here(K, H)
+                and _igemm.usable(dyc, w.t().reshape(C, K, 1, 1), w.dtype))
+        if mine:
+            # dX = dY @ W as a 1x1 conv of dy with the transposed filter on the
+            # implicit-GEMM kernel (accumulating onto a tapped residual gradient)
+            wt = w.t().contiguous().view(C, K, 1, 1)
         if ctx.needs_input_grad[0] and acc is not None:
             if acc.shape != (N, C, H, W) or not acc.is_contiguous(memory_format=torch.channels_last):
                 raise RuntimeError("conv1x1: tapped gradient does not match the input")
-            _rows(acc).addmm_(dyr, w)  # acc <- acc + dY @ W (GEMM epilogue accumulate)
+            if mine:
+                _igemm.conv_acc(dyc, wt, acc)
+            else:
+                _rows(acc).addmm_(dyr, w)  # acc <- acc + dY @ W (GEMM epilogue accumulate)
             dx = acc
+        elif mine:
+            dx, _ = _igemm.conv_fwd(dyc, wt, 1, 0)
         elif ctx.needs_input_grad[0]:
             dx = torch.mm(dyr, w).view(N, H, W, C).permute(0, 3, 1, 2)
             if stride != 1:

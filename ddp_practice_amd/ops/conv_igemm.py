@@ -47,6 +47,20 @@ def usable(x: torch.Tensor, weight: torch.Tensor, cdtype: torch.dtype) -> bool:
             and bool(_K().supported(weight.shape[1], weight.shape[0])))
 
 
+def dgrad_1x1_here(K: int, OH: int) -> bool:
+    """Shapes where the implicit-GEMM kernel beats hipBLASLt on a 1x1 data gradient
+    (profiles/r2_conv_igemm_fwd_vs_library_bs128.txt, read as dgrad = conv K -> C):
+    up to 512 gradient channels at 14x14 and above."""
+    return ENABLED and K <= 512 and OH >= 14
+
+
+def conv_acc(x: torch.Tensor, w: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """y += conv1x1(x, w) in place (stride 1): the data gradient accumulated onto a
+    residual gradient already in y (ops/conv1x1.py GradTap)."""
+    _K().conv_fwd(x, w, y, 1, 0, accumulate=True)
+    return y
+
+
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn=None):
     """y = conv(x, w) on the implicit-GEMM kernel; x, w channels_last in the compute dtype.
     With ``bn`` (a training BatchNorm module): also its statistics, returned as the second

@@ -40,6 +40,8 @@ class ConvNHWCFn(torch.autograd.Function):
             return out
         if stats is not None:
             ctx.mark_non_differentiable(stats)
+        # no zero tensor materialised for the statistics output's (absent) gradient
+        ctx.set_materialize_grads(False)
         return out, stats
 
     @staticmethod

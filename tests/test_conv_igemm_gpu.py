@@ -56,7 +56,8 @@ def test_conv_fwd_matches_torch(C, dtype, shape, stats):
     _run(C, *shape, dtype, stats)
 
 
-@pytest.mark.parametrize("shape", [(2, 64, 14, 14, 128, 3, 1, 1), (2, 128, 9, 9, 64, 3, 2, 1), (2, 64, 8, 8, 64, 1, 1, 0)])
+@pytest.mark.parametrize("shape", [(2, 64, 14, 14, 128, 3, 1, 1), (2, 128, 9, 9, 64, 3, 2, 1), (2, 64, 8, 8, 64, 1, 1, 0),
+                                   (2, 128, 14, 14, 64, 1, 1, 0)])
 def test_conv_ops_fwd_bwd_with_stats(C, shape):
     """ops conv_nhwc / conv1x1 with the implicit-GEMM forward (+BN statistics) and the
     stride-1 data gradient on the same kernel == fp32 torch autograd."""
@@ -105,3 +106,27 @@ def test_conv_wgrad_matches_torch(C, dtype, shape):
     got = conv_wgrad(dy, x, (K, Cin, R, R), stride, pad)
     err = ((got - w.grad).abs().max() / w.grad.abs().max()).item()
     assert err < 1e-2, err
+
+
+def test_conv1x1_tapped_dgrad_accumulates(C):
+    """Identity-block conv1: the residual gradient handed over by the block's last BN
+    (GradTap) is accumulated by the 1x1 data-gradient kernel in its epilogue."""
+    from ddp_practice_amd.ops.conv1x1 import GradTap, conv1x1
+
+    g = torch.Generator().manual_seed(3)
+    N, Cin, H, K = 2, 256, 14, 64
+    x0 = torch.randn(N, Cin, H, H, generator=g)
+    w0 = torch.randn(K, Cin, 1, 1, generator=g) / Cin ** 0.5
+    dy0 = torch.randn(N, K, H, H, generator=g)
+    res0 = torch.randn(N, Cin, H, H, generator=g)
+    xr = x0.clone().requires_grad_()
+    F.conv2d(xr, w0).backward(dy0)
+    ref = xr.grad + res0
+    x = x0.to(DEV, torch.bfloat16).contiguous(memory_format=CL).requires_grad_()
+    w = w0.to(DEV).requires_grad_()
+    tap = GradTap()
+    y = conv1x1(x, w, 1, torch.bfloat16, tap)
+    tap.grad = res0.to(DEV, torch.bfloat16).contiguous(memory_format=CL)
+    y.backward(dy0.to(DEV, torch.bfloat16).contiguous(memory_format=CL))
+    err = ((x.grad.float().cpu() - ref).abs().max() / ref.abs().max()).item()
+    assert err < 2e-2, err
