@@ -510,6 +510,64 @@ wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ grad, in
   }
 }
 
+// ---------------------------------------------------------------------------
+// Per-step weight packing for every implicit-GEMM conv of a network in ONE launch:
+// fp32 OIHW master weights -> the compute-dtype forward filter wf[k][r][s][c] (the
+// channels_last layout the kernels read) and, where a data gradient runs on the
+// kernel, the flipped transposed filter wd[c][R-1-r][S-1-s][k] (for a 1x1 conv: the
+// plain transpose).  64 x 64 (k, c) tiles of one tap through LDS: both writes are
+// whole 128-B rows.  Table (int64, 8 per conv): src, wf, wd (0: none), K, C, R*S,
+// first tile (prefix over the convs), unused.
+template <typename T>
+__global__ void __launch_bounds__(256)
+pack_weights_kernel(const int64_t* __restrict__ table, int n) {
+  __shared__ float tile[64][65];
+  const long long t = blockIdx.x;
+  int lo = 0, hi = n - 1;  // the conv holding tile t
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (table[8 * mid + 6] <= t) lo = mid; else hi = mid - 1;
+  }
+  const int64_t* d = table + 8 * lo;
+  const float* src = reinterpret_cast<const float*>(d[0]);
+  T* wf = reinterpret_cast<T*>(d[1]);
+  T* wd = reinterpret_cast<T*>(d[2]);
+  const int K = (int)d[3], C = (int)d[4], RS = (int)d[5];
+  const long long lt = t - d[6];
+  const int rs = (int)(lt % RS);
+  const long long kc = lt / RS;
+  const int ct = C / 64, k0 = (int)(kc / ct) * 64, c0 = (int)(kc % ct) * 64;
+  const int tid = threadIdx.x, cl = tid & 63, rg = tid >> 6;
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = src[((long long)(k0 + rg * 16 + i) * C + c0 + cl) * RS + rs];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int kl = rg * 16 + i;
+    wf[((long long)(k0 + kl) * RS + rs) * C + c0 + cl] = Cvt<T>::from_f(v[i]);
+    tile[kl][cl] = v[i];
+  }
+  if (wd == nullptr) return;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = rg * 16 + i;  // lanes along k
+    wd[((long long)(c0 + c) * RS + (RS - 1 - rs)) * K + k0 + cl] = Cvt<T>::from_f(tile[cl][c]);
+  }
+}
+
+void pack_weights(at::Tensor table, int64_t n, int64_t tiles, int64_t dtype_code) {
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kLong && table.numel() >= 8 * n, "pack_weights: table");
+  if (tiles <= 0) return;
+  if (dtype_code == 0)
+    hipLaunchKernelGGL(pack_weights_kernel<__hip_bfloat16>, dim3((unsigned)tiles), dim3(256), 0, cur_stream(),
+                       table.data_ptr<int64_t>(), (int)n);
+  else
+    hipLaunchKernelGGL(pack_weights_kernel<__half>, dim3((unsigned)tiles), dim3(256), 0, cur_stream(),
+                       table.data_ptr<int64_t>(), (int)n);
+  DPA_CHECK_LAUNCH();
+}
+
 static Geom geom(const at::Tensor& x, const at::Tensor& w, int stride, int pad) {
   // x: [N, C, H, W] channels_last; w: [K, C, R, S] channels_last (= [K][R][S][C] in memory)
   Geom g;
@@ -653,6 +711,7 @@ void register_conv_igemm(pybind11::module& m) {
   s.def("stat_part_len", &igemm::stat_part_len);
   s.def("stat_tickets_len", &igemm::stat_tickets_len);
   s.def("conv_wgrad", &igemm::conv_wgrad);
+  s.def("pack_weights", &igemm::pack_weights);
   s.def("wgrad_splits", &igemm::wgrad_splits);
 }
 

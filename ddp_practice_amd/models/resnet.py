@@ -29,22 +29,27 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..amp import autocast, compute_dtype
+from ..ops import conv_igemm as _igemm
 from ..ops.conv1x1 import GradTap, conv1x1
 from ..ops.conv_nhwc import conv_nhwc
+
+
+_PACKS: dict = {}  # id(module) -> this forward's packed filters (ops/conv_igemm.WeightPack)
 
 
 def _conv(x: torch.Tensor, conv: nn.Conv2d, cdtype: torch.dtype, bn: nn.Module | None = None, tap=None):
     """conv(x) -> (output, statistics of the following training BN ``bn`` when the conv
     kernel produced them, else None)."""
     want = bn if (bn is not None and bn.training) else None
+    pk = _PACKS.get(id(conv))
     if conv.kernel_size == (1, 1) and conv.padding == (0, 0) and conv.groups == 1 and conv.bias is None:
         if want is None:
-            return conv1x1(x, conv.weight, conv.stride[0], cdtype, tap), None
-        return conv1x1(x, conv.weight, conv.stride[0], cdtype, tap, want)
+            return conv1x1(x, conv.weight, conv.stride[0], cdtype, tap, None, pk), None
+        return conv1x1(x, conv.weight, conv.stride[0], cdtype, tap, want, pk)
     if conv.bias is None and conv.groups == 1 and conv.dilation == (1, 1):
         if want is None:
-            return conv_nhwc(x, conv.weight, conv.stride, conv.padding, cdtype), None
-        return conv_nhwc(x, conv.weight, conv.stride, conv.padding, cdtype, want)
+            return conv_nhwc(x, conv.weight, conv.stride, conv.padding, cdtype, None, pk), None
+        return conv_nhwc(x, conv.weight, conv.stride, conv.padding, cdtype, want, pk)
     w = conv.weight.to(cdtype)
     out = F.conv2d(x, w, None if conv.bias is None else conv.bias.to(cdtype), conv.stride, conv.padding,
                    conv.dilation, conv.groups)
@@ -160,6 +165,16 @@ class ResNet(nn.Module):
 
         cdtype = compute_dtype(x) if self.amp_dtype is not None else torch.float32
         x = x.to(dtype=cdtype, memory_format=torch.channels_last)
+        _PACKS.clear()
+        if _igemm.ENABLED and cdtype in (torch.bfloat16, torch.float16):
+            # every implicit-GEMM conv's filters for this step in one launch
+            pack = getattr(self, "_wpack", None)
+            if pack is None or pack.cdtype != cdtype:
+                convs = [(m, m.stride == (1, 1) and (m.kernel_size == (3, 3) or m.weight.shape[0] <= 512))
+                         for m in self.modules() if isinstance(m, nn.Conv2d) and m.bias is None and m.groups == 1
+                         and m.weight.shape[0] % 64 == 0 and m.weight.shape[1] % 64 == 0]
+                pack = self._wpack = _igemm.WeightPack(convs, cdtype)
+            _PACKS.update(pack.run())
         c, st = _conv(x, self.conv1, cdtype, self.bn1)
         x = bn_act(c, self.bn1, relu=True, comm=_comm_of(self.bn1), stats=st)
         x = max_pool_3x3s2(x)

@@ -75,14 +75,16 @@ class GradTap:
 
 class Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride: int, cdtype: torch.dtype, tap: GradTap | None = None, bn=None):
+    def forward(ctx, x, weight, stride: int, cdtype: torch.dtype, tap: GradTap | None = None, bn=None, packed=None):
         in_shape = x.shape
         if tap is not None and stride != 1:
             raise ValueError("conv1x1: a gradient tap needs stride 1")
         ctx.tap = tap
         ctx.wshape = weight.shape
         C = x.shape[1]
-        w = weight.reshape(weight.shape[0], C).to(cdtype)
+        # packed: this step's compute-dtype filter (and its transpose) from ops/conv_igemm.WeightPack
+        w = packed[0].view(weight.shape[0], C) if packed is not None else weight.reshape(weight.shape[0], C).to(cdtype)
+        ctx.wt = packed[1] if packed is not None else None
         if _igemm.usable(x, weight, cdtype):
             # implicit-GEMM kernel: strided rows read in place, the BN statistics fused
             xc = x.to(cdtype)
@@ -129,7 +131,7 @@ class Conv1x1Fn(torch.autograd.Function):
         if mine:
             # dX = dY @ W as a 1x1 conv of dy with the transposed filter on the
             # implicit-GEMM kernel (accumulating onto a tapped residual gradient)
-            wt = w.t().contiguous().view(C, K, 1, 1)
+            wt = ctx.wt if ctx.wt is not None else w.t().contiguous().view(C, K, 1, 1)
         if ctx.needs_input_grad[0] and acc is not None:
             if acc.shape != (N, C, H, W) or not acc.is_contiguous(memory_format=torch.channels_last):
                 raise RuntimeError("conv1x1: tapped gradient does not match the input")
@@ -155,13 +157,13 @@ class Conv1x1Fn(torch.autograd.Function):
                 # saved: the [P, C] rows, or (lazy) the unstrided input
                 rows = _rows(saved[:, :, ::stride, ::stride] if stride != 1 else saved) if ctx.lazy_rows else saved
                 dw = _wgrad(dyr, rows).view(ctx.wshape)
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
 def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int, cdtype: torch.dtype,
-            tap: GradTap | None = None, bn=None):
+            tap: GradTap | None = None, bn=None, packed=None):
     """Bias-free 1x1 conv (stride 1 or 2) of ``x`` with the fp32 ``weight``; the
     output is a channels_last [N, Cout, H', W'] tensor in ``cdtype``.  ``tap``:
     see :class:`GradTap`.  With ``bn`` (the training BatchNorm that follows): returns
     (output, its statistics or None) -- ops/conv_igemm.py."""
-    return Conv1x1Fn.apply(x, weight, int(stride), cdtype, tap, bn)
+    return Conv1x1Fn.apply(x, weight, int(stride), cdtype, tap, bn, packed)

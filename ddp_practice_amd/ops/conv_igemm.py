@@ -99,3 +99,44 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, wshape, stride: int, pad: int)
     grad = torch.empty(wshape, dtype=torch.float32, device=dy.device)
     _K().conv_wgrad(dy, x, grad, stride, pad, slab)
     return grad
+
+
+class WeightPack:
+    """One launch per forward that writes, for every implicit-GEMM conv of a network,
+    the compute-dtype filter in the kernels' layout and, where the data gradient also
+    runs on the kernel, its flipped transpose (csrc/kernels/conv_igemm.hip
+    pack_weights_kernel) -- instead of 2-3 cast / flip / transpose copies per conv.
+
+    ``convs``: (module, wants_dgrad_filter) pairs.  The buffers persist (the same
+    addresses every step: graph-capturable); the tile table is rebuilt only when a
+    weight tensor is replaced."""
+
+    def __init__(self, convs, cdtype: torch.dtype):
+        self.items = [(m, bool(d)) for m, d in convs]
+        self.cdtype = cdtype
+        self._key = None
+        self._bufs: dict = {}
+        self._table = None
+        self._tiles = 0
+
+    def _build(self, dev):
+        rows, tiles = [], 0
+        for m, want_d in self.items:
+            w = m.weight
+            K, C, R, S = w.shape
+            wf = torch.empty((K, C, R, S), dtype=self.cdtype, device=dev, memory_format=_CL)
+            wd = torch.empty((C, K, R, S), dtype=self.cdtype, device=dev, memory_format=_CL) if want_d else None
+            self._bufs[id(m)] = (wf, wd)
+            rows.append([w.data_ptr(), wf.data_ptr(), wd.data_ptr() if wd is not None else 0, K, C, R * S, tiles, 0])
+            tiles += (K // 64) * (C // 64) * R * S
+        self._table = torch.tensor(rows, dtype=torch.int64).reshape(-1).to(dev)
+        self._tiles = tiles
+
+    def run(self) -> dict:
+        key = tuple(m.weight.data_ptr() for m, _ in self.items)
+        if key != self._key:
+            self._build(self.items[0][0].weight.device)
+            self._key = key
+        code = 0 if self.cdtype == torch.bfloat16 else 1
+        _K().pack_weights(self._table, len(self.items), self._tiles, code)
+        return self._bufs

@@ -20,10 +20,14 @@ _CL = torch.channels_last
 
 class ConvNHWCFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride, padding, cdtype: torch.dtype, bn=None):
+    def forward(ctx, x, weight, stride, padding, cdtype: torch.dtype, bn=None, packed=None):
         x = x if x.is_contiguous(memory_format=_CL) else x.contiguous(memory_format=_CL)
-        w = torch.empty(weight.shape, dtype=cdtype, device=weight.device, memory_format=_CL)
-        w.copy_(weight)  # fp32 NCHW -> cdtype NHWC in one kernel
+        if packed is not None:  # this step's filters from ops/conv_igemm.WeightPack
+            w = packed[0]
+        else:
+            w = torch.empty(weight.shape, dtype=cdtype, device=weight.device, memory_format=_CL)
+            w.copy_(weight)  # fp32 NCHW -> cdtype NHWC in one kernel
+        ctx.wt = packed[1] if packed is not None else None
         stats = None
         if (_igemm.usable(x, weight, cdtype) and stride[0] == stride[1] and padding[0] == padding[1]):
             # hand-written implicit GEMM (+ the next BN's statistics in its epilogue)
@@ -56,8 +60,10 @@ class ConvNHWCFn(torch.autograd.Function):
             # stride-1 data gradient = a forward conv of dy with the flipped, transposed
             # filter on the implicit-GEMM kernel (pad R-1-p)
             R = w.shape[2]
-            wt = torch.empty((w.shape[1], w.shape[0], R, R), dtype=w.dtype, device=w.device, memory_format=_CL)
-            wt.copy_(w.flip(2, 3).transpose(0, 1))
+            wt = ctx.wt
+            if wt is None:
+                wt = torch.empty((w.shape[1], w.shape[0], R, R), dtype=w.dtype, device=w.device, memory_format=_CL)
+                wt.copy_(w.flip(2, 3).transpose(0, 1))
             dx, _ = _igemm.conv_fwd(dy, wt, 1, R - 1 - padding[0])
         dw = None
         xc = x.to(w.dtype)
@@ -74,10 +80,10 @@ class ConvNHWCFn(torch.autograd.Function):
             if dw2 is not None:
                 dw = torch.empty(dw2.shape, dtype=ctx.wdtype, device=dw2.device)
                 dw.copy_(dw2)  # cdtype NHWC -> fp32 NCHW in one kernel
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
-def conv_nhwc(x: torch.Tensor, weight: torch.Tensor, stride, padding, cdtype: torch.dtype, bn=None):
+def conv_nhwc(x: torch.Tensor, weight: torch.Tensor, stride, padding, cdtype: torch.dtype, bn=None, packed=None):
     """Bias-free conv of channels_last ``x`` with the fp32 ``weight`` in ``cdtype``.  With
     ``bn`` (the training BatchNorm that follows): returns (output, its statistics or None)."""
-    return ConvNHWCFn.apply(x, weight, tuple(stride), tuple(padding), cdtype, bn)
+    return ConvNHWCFn.apply(x, weight, tuple(stride), tuple(padding), cdtype, bn, packed)
