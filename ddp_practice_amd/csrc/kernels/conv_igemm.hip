@@ -25,6 +25,7 @@
 //   * the pixel tile's im2col addresses (n, ih0, iw0) are computed once per
 //     workgroup; padding / ragged M are zero-filled in the loader.
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -654,8 +655,16 @@ int64_t wgrad_splits(int64_t M, int64_t K, int64_t C, int64_t R, int64_t S) {
   // ~2-4 workgroups per CU, each at least 16 K-steps of 64 pixels, and the fp32
   // partials at most ~48 MB (written and re-read once: ~12 us at HBM rate)
   const int64_t tiles = (K / wtile(K)) * (R * S * C / wtile(C));
-  int64_t sp = std::max<int64_t>(1, 768 / tiles);
-  sp = std::min<int64_t>(sp, std::max<int64_t>(1, M / 1024));
+  static const int64_t target = [] {
+    const char* e = std::getenv("DPA_WGRAD_BLOCKS");
+    return e != nullptr ? std::atoll(e) : 768LL;
+  }();
+  static const int64_t minpix = [] {
+    const char* e = std::getenv("DPA_WGRAD_MINPIX");
+    return e != nullptr ? std::atoll(e) : 1024LL;
+  }();
+  int64_t sp = std::max<int64_t>(1, target / tiles);
+  sp = std::min<int64_t>(sp, std::max<int64_t>(1, M / minpix));
   sp = std::min<int64_t>(sp, std::max<int64_t>(1, (12LL << 20) / (K * R * S * C)));
   return sp;
 }
