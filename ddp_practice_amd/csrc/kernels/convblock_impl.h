@@ -573,9 +573,10 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
       static_assert((COUT * KPW * sizeof(T)) % 16 == 0, "packed weight tile must be whole 16-B chunks");
       static_assert(COUT * KPW == (MODE == 2 ? W2D_LEN : W2F_LEN), "pre-packed weights exist for layer 2 only");
       const uint4* src = reinterpret_cast<const uint4*>(wpk);
+      // unconditional (clamped) loads: a conditional load into the array made hipcc keep
+      // it in scratch and wait vmcnt(0) after every single load
 #pragma unroll
-      for (int i = 0; i < WIT; ++i)
-        if (tid + i * NTHR < WN16) wreg[i] = src[tid + i * NTHR];
+      for (int i = 0; i < WIT; ++i) wreg[i] = src[min(tid + i * NTHR, WN16 - 1)];
     }
   };
   if constexpr (WPK == 1) {
@@ -706,40 +707,91 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
     __shared__ float part[NTHR];
     typedef typename Pair2<T>::type P;
     constexpr int NPO = CIN * HW;  // pooled outputs of one image = this conv's input
-    constexpr int IT = (NPO + NTHR - 1) / NTHR;
     const T* yb = pin.y + (size_t)b * CIN * 4 * HW;
-    P top[IT], bot[IT];
-#pragma unroll
-    for (int i = 0; i < IT; ++i) {  // issued before the statistics reduction: the latencies overlap
-      const int e = tid + i * NTHR;
-      if (e < NPO) {
-        const int ci = e / HW, pix = e % HW, ho = pix / W, wo = pix % W;
-        const P* src = reinterpret_cast<const P*>(yb + ((size_t)ci * 2 * H + 2 * ho) * 2 * W + 2 * wo);
-        top[i] = src[0];
-        bot[i] = src[W];  // next input row (2W elements = W pairs)
-      }
-    }
-    bn_finalize<CIN>(pin.bn, sc_s, beta_s, mean_s, istd_s, part, bid == 0);
-    load_wpk();
-    DPA_STAMP(3);
-    // the pooled map / index / xhat outputs (for the backward) are written by all
-    // nsplit workgroups of the image, each its share (was: split 0 alone)
     const bool wr = pin.p_out != nullptr;
     const int e_lo = NPO * sp / nsplit, e_hi = NPO * (sp + 1) / nsplit;
+    if constexpr (CIN % 8 == 0 && sizeof(T) == 2) {
+      // a lane owns 8 channels of one pooled pixel (lanes along the pixels: every load
+      // instruction reads consecutive pairs of one row): ONE 16-B LDS write of the 8
+      // pooled values instead of eight 2-B writes to the same bank group
+      constexpr int NO = CIN / 8, NPI = NO * HW, IT8 = (NPI + NTHR - 1) / NTHR;
+      P top[IT8][8], bot[IT8][8];
 #pragma unroll
-    for (int i = 0; i < IT; ++i) {
-      const int e = tid + i * NTHR;
-      if (e < NPO) {
-        const int ci = e / HW, pix = e % HW, ho = pix / W, wo = pix % W;
-        float best, xh;
-        int bi;
-        bn_relu_max4x<T>(top[i], bot[i], sc_s[ci], beta_s[ci], mean_s[ci], istd_s[ci], best, bi, xh);
-        const T pv = Cvt<T>::from_f(best);
-        img[imo((ho + 2) * WPD + (wo + 2), ci)] = pv;
-        if (wr && e >= e_lo && e < e_hi) {
-          pin.p_out[(size_t)b * NPO + e] = pv;
-          pin.idx_out[(size_t)b * NPO + e] = (uint8_t)(bi | (best > 0.f ? IDX_RELU : 0));
-          pin.xh_out[(size_t)b * NPO + e] = Cvt<T>::from_f(xh);
+      for (int i = 0; i < IT8; ++i) {  // issued before the statistics reduction: the latencies overlap
+        const int e8 = tid + i * NTHR;
+        if (e8 < NPI) {
+          const int o = e8 / HW, pix = e8 % HW, ho = pix / W, wo = pix % W;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const P* src =
+                reinterpret_cast<const P*>(yb + ((size_t)(8 * o + j) * 2 * H + 2 * ho) * 2 * W + 2 * wo);
+            top[i][j] = src[0];
+            bot[i][j] = src[W];  // next input row (2W elements = W pairs)
+          }
+        }
+      }
+      bn_finalize<CIN>(pin.bn, sc_s, beta_s, mean_s, istd_s, part, bid == 0);
+      load_wpk();
+      DPA_STAMP(3);
+#pragma unroll
+      for (int i = 0; i < IT8; ++i) {
+        const int e8 = tid + i * NTHR;
+        if (e8 < NPI) {
+          const int o = e8 / HW, pix = e8 % HW, ho = pix / W, wo = pix % W;
+          unsigned pk[4];  // the 8 pooled values packed in registers (no local array in memory)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int ci = 8 * o + j;
+            float best, xh;
+            int bi;
+            bn_relu_max4x<T>(top[i][j], bot[i][j], sc_s[ci], beta_s[ci], mean_s[ci], istd_s[ci], best, bi, xh);
+            const T pvj = Cvt<T>::from_f(best);
+            const unsigned bits = __builtin_bit_cast(unsigned short, pvj);
+            if (j & 1) pk[j >> 1] |= bits << 16; else pk[j >> 1] = bits;
+            const int e = ci * HW + pix;  // (ci, pix) index of the pooled outputs
+            if (wr && e >= e_lo && e < e_hi) {
+              pin.p_out[(size_t)b * NPO + e] = pvj;
+              pin.idx_out[(size_t)b * NPO + e] = (uint8_t)(bi | (best > 0.f ? IDX_RELU : 0));
+              pin.xh_out[(size_t)b * NPO + e] = Cvt<T>::from_f(xh);
+            }
+          }
+          // imo keeps each 8-channel group of a pixel contiguous (the swizzle moves groups)
+          *reinterpret_cast<uint4*>(&img[imo((ho + 2) * WPD + (wo + 2), 8 * o)]) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        }
+      }
+    } else {
+      constexpr int IT = (NPO + NTHR - 1) / NTHR;
+      P top[IT], bot[IT];
+#pragma unroll
+      for (int i = 0; i < IT; ++i) {  // issued before the statistics reduction: the latencies overlap
+        const int e = tid + i * NTHR;
+        if (e < NPO) {
+          const int ci = e / HW, pix = e % HW, ho = pix / W, wo = pix % W;
+          const P* src = reinterpret_cast<const P*>(yb + ((size_t)ci * 2 * H + 2 * ho) * 2 * W + 2 * wo);
+          top[i] = src[0];
+          bot[i] = src[W];  // next input row (2W elements = W pairs)
+        }
+      }
+      bn_finalize<CIN>(pin.bn, sc_s, beta_s, mean_s, istd_s, part, bid == 0);
+      load_wpk();
+      DPA_STAMP(3);
+      // the pooled map / index / xhat outputs (for the backward) are written by all
+      // nsplit workgroups of the image, each its share (was: split 0 alone)
+#pragma unroll
+      for (int i = 0; i < IT; ++i) {
+        const int e = tid + i * NTHR;
+        if (e < NPO) {
+          const int ci = e / HW, pix = e % HW, ho = pix / W, wo = pix % W;
+          float best, xh;
+          int bi;
+          bn_relu_max4x<T>(top[i], bot[i], sc_s[ci], beta_s[ci], mean_s[ci], istd_s[ci], best, bi, xh);
+          const T pv = Cvt<T>::from_f(best);
+          img[imo((ho + 2) * WPD + (wo + 2), ci)] = pv;
+          if (wr && e >= e_lo && e < e_hi) {
+            pin.p_out[(size_t)b * NPO + e] = pv;
+            pin.idx_out[(size_t)b * NPO + e] = (uint8_t)(bi | (best > 0.f ? IDX_RELU : 0));
+            pin.xh_out[(size_t)b * NPO + e] = Cvt<T>::from_f(xh);
+          }
         }
       }
     }
