@@ -415,6 +415,77 @@ struct BnBwdStage {
   }
 };
 
+// As BnBwdStage (whole images), but a lane owns 8 CHANNELS of one 2x2 window
+// (lanes along the windows: each load instruction still reads consecutive pairs of
+// one row) and the sink receives the window's 4 pixels as 8-channel vectors: the
+// data-grad kernel writes them as 16-B LDS stores into its [pixel][channel] image.
+template <typename T, int C, int H, int W, int NT_>
+struct BnBwdStage8 {
+  typedef typename Pair2<T>::type P;
+  static_assert(C % 8 == 0 && sizeof(T) == 2, "8-channel staging: 16-bit types, C % 8 == 0");
+  static constexpr int HO = H / 2, WO = W / 2, PP = HO * WO;
+  static constexpr int NO = C / 8, NWIN = NO * PP;
+  static constexpr int IT = (NWIN + NT_ - 1) / NT_;
+  P top[IT][8], bot[IT][8];
+  T g[IT][8];
+  uint8_t ix[IT][8];
+
+  __device__ __forceinline__ void load(const BwdIn<T>& bi, int b) {
+    const T* yb = bi.y + (size_t)b * C * H * W;
+    const T* dpb = bi.dp + (size_t)b * C * PP;
+    const uint8_t* ib = bi.idx + (size_t)b * C * PP;
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = min((int)threadIdx.x + i * NT_, NWIN - 1);  // clamped: unconditional loads
+      const int o = e / PP, pix = e % PP, ho = pix / WO, wo = pix % WO;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = 8 * o + j;
+        const P* src = reinterpret_cast<const P*>(yb + ((size_t)c * H + 2 * ho) * W + 2 * wo);
+        top[i][j] = src[0];
+        bot[i][j] = src[W / 2];
+        g[i][j] = dpb[c * PP + pix];
+        ix[i][j] = ib[c * PP + pix];
+      }
+    }
+  }
+
+  // sink(h, w, c0, q00, q01, q10, q11): the 4 pixels of window (h, w) (top-left),
+  // channels c0 .. c0+7, each packed as uint4
+  template <typename Sink>
+  __device__ __forceinline__ void emit(const float* coef, Sink&& sink) {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = (int)threadIdx.x + i * NT_;
+      if (e < NWIN) {
+        const int o = e / PP, pix = e % PP, ho = pix / WO, wo = pix % WO;
+        unsigned q[4][4];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int c = 8 * o + j;
+          const float k1 = coef[c], k2 = coef[C + c], gi = coef[2 * C + c], mean = coef[3 * C + c],
+                      istd = coef[4 * C + c];
+          T v[4];
+          __builtin_memcpy(&v[0], &top[i][j], 2 * sizeof(T));
+          __builtin_memcpy(&v[2], &bot[i][j], 2 * sizeof(T));
+          const int k = ix[i][j] & IDX_POS;
+          const float gg = (ix[i][j] & IDX_RELU) ? Cvt<T>::to_f(g[i][j]) : 0.f;
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const float xh = (Cvt<T>::to_f(v[qq]) - mean) * istd;
+            const T o_ = Cvt<T>::from_f(gi * ((qq == k ? gg : 0.f) - k1 - xh * k2));
+            const unsigned bits = __builtin_bit_cast(unsigned short, o_);
+            if (j & 1) q[qq][j >> 1] |= bits << 16; else q[qq][j >> 1] = bits;
+          }
+        }
+        sink(2 * ho, 2 * wo, 8 * o, make_uint4(q[0][0], q[0][1], q[0][2], q[0][3]),
+             make_uint4(q[1][0], q[1][1], q[1][2], q[1][3]), make_uint4(q[2][0], q[2][1], q[2][2], q[2][3]),
+             make_uint4(q[3][0], q[3][1], q[3][2], q[3][3]));
+      }
+    }
+  }
+};
+
 // Epilogue of the data-grad kernel that produces a pooled grad: per-workgroup
 // BN partial sums of the block below ([S1 | S2] per channel -> one slab row).
 template <typename T>
@@ -798,19 +869,35 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
   } else {
     __shared__ float coef[5 * CIN], sums[2 * CIN];
     __shared__ float part[NTHR];
-    BnBwdStage<T, CIN, H, W, NTHR> st;
-    st.load(bin, b);
-    DPA_STAMP(8);
-    bn_bwd_coef<CIN, T>(bin, coef, part, sums, bid == 0);
-    load_epi();
-    load_wpk();
-    DPA_STAMP(3);
-    st.emit(coef, [&](int c, int h, int ww, T v00, T v01, T v10, T v11) {
-      img[imo((h + 2) * WPD + (ww + 2), c)] = v00;
-      img[imo((h + 2) * WPD + (ww + 3), c)] = v01;
-      img[imo((h + 3) * WPD + (ww + 2), c)] = v10;
-      img[imo((h + 3) * WPD + (ww + 3), c)] = v11;
-    });
+    if constexpr (CIN % 8 == 0 && sizeof(T) == 2) {
+      BnBwdStage8<T, CIN, H, W, NTHR> st;
+      st.load(bin, b);
+      DPA_STAMP(8);
+      bn_bwd_coef<CIN, T>(bin, coef, part, sums, bid == 0);
+      load_epi();
+      load_wpk();
+      DPA_STAMP(3);
+      st.emit(coef, [&](int h, int ww, int c0, uint4 q00, uint4 q01, uint4 q10, uint4 q11) {
+        *reinterpret_cast<uint4*>(&img[imo((h + 2) * WPD + (ww + 2), c0)]) = q00;
+        *reinterpret_cast<uint4*>(&img[imo((h + 2) * WPD + (ww + 3), c0)]) = q01;
+        *reinterpret_cast<uint4*>(&img[imo((h + 3) * WPD + (ww + 2), c0)]) = q10;
+        *reinterpret_cast<uint4*>(&img[imo((h + 3) * WPD + (ww + 3), c0)]) = q11;
+      });
+    } else {
+      BnBwdStage<T, CIN, H, W, NTHR> st;
+      st.load(bin, b);
+      DPA_STAMP(8);
+      bn_bwd_coef<CIN, T>(bin, coef, part, sums, bid == 0);
+      load_epi();
+      load_wpk();
+      DPA_STAMP(3);
+      st.emit(coef, [&](int c, int h, int ww, T v00, T v01, T v10, T v11) {
+        img[imo((h + 2) * WPD + (ww + 2), c)] = v00;
+        img[imo((h + 2) * WPD + (ww + 3), c)] = v01;
+        img[imo((h + 3) * WPD + (ww + 2), c)] = v10;
+        img[imo((h + 3) * WPD + (ww + 3), c)] = v11;
+      });
+    }
     store_epi();
   }
   if constexpr (WPK == 1) {

@@ -101,11 +101,14 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
   __shared__ float part_s[NT];
   // MFMA operand tiles (row-major, k contiguous: every fragment is one 16-B read)
   __shared__ __attribute__((aligned(16))) E pcl[BMAX * KP];   // A fwd: p2 slice [b][j]
-  __shared__ __attribute__((aligned(16))) E pct[KP * BMAX];   // B dW: p2 slice as [j][b]
+  // transposed tiles' rows padded by 16 B: their column-wise 2-byte writes (lanes along
+  // the rows) then spread over the banks instead of hitting one bank pair
+  constexpr int PCT_S = BMAX + 8, WDL_S = 32 + 8, DLT_S = BMAX + 8;
+  __shared__ __attribute__((aligned(16))) E pct[KP * PCT_S];  // B dW: p2 slice as [j][b]
   __shared__ __attribute__((aligned(16))) E wcl[NMAX * KP];   // B fwd: W slice [n][j]
-  __shared__ __attribute__((aligned(16))) E wdl[KP * 32];     // B dp2: W slice [j][n] (k = n padded to 32)
+  __shared__ __attribute__((aligned(16))) E wdl[KP * WDL_S];  // B dp2: W slice [j][n] (k = n padded to 32)
   __shared__ __attribute__((aligned(16))) E dll[BMAX * 32];   // A dp2: dls [b][n]
-  __shared__ __attribute__((aligned(16))) E dlt[NMAX * BMAX]; // A dW: dls as [n][b]
+  __shared__ __attribute__((aligned(16))) E dlt[NMAX * DLT_S]; // A dW: dls as [n][b]
   __shared__ float lg_s[BMAX * NMAX];                         // logits (rounded) / dls, f32
   __shared__ float dd_s[BMAX * NMAX];                         // (softmax - onehot) / count
   __shared__ int64_t tgt_s[BMAX];
@@ -148,15 +151,11 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
     wv_[i] = (e < NMAX * PP && n < N) ? wfc[(size_t)n * K + c * PP + j] : 0.f;
   }
   // zero the tiles' padding (rows past B, k past 49 / N)
-  for (int e = tid; e < BMAX * KP; e += NT) {
-    pcl[e] = ez;
-    pct[e] = ez;
-  }
-  for (int e = tid; e < BMAX * 32; e += NT) {
-    dll[e] = ez;
-    wdl[e] = ez;
-  }
-  for (int e = tid; e < NMAX * BMAX; e += NT) dlt[e] = ez;
+  for (int e = tid; e < BMAX * KP; e += NT) pcl[e] = ez;
+  for (int e = tid; e < KP * PCT_S; e += NT) pct[e] = ez;
+  for (int e = tid; e < BMAX * 32; e += NT) dll[e] = ez;
+  for (int e = tid; e < KP * WDL_S; e += NT) wdl[e] = ez;
+  for (int e = tid; e < NMAX * DLT_S; e += NT) dlt[e] = ez;
   for (int e = tid; e < NMAX * KP; e += NT) wcl[e] = ez;
   if (tid < BMAX) tgt_s[tid] = tgt_r;
   if (tid < NMAX) bias_s[tid] = bias_r;
@@ -170,7 +169,7 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
       const int n = e / PP, j = e % PP;
       const E wq = Cvt<T>::from_f(wv_[i]);
       wcl[n * KP + j] = wq;
-      wdl[j * 32 + n] = wq;
+      wdl[j * WDL_S + n] = wq;
     }
   }
   // 2. BN -> ReLU -> 2x2 max of this channel; pooled value, argmax|relu index, xhat.
@@ -192,7 +191,7 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
         ixr[i] = (uint8_t)(bi | (best > 0.f ? IDX_RELU : 0));
         xqr[i] = Cvt<T>::from_f(xh);
         pcl[b * KP + j] = pvr[i];
-        pct[j * BMAX + b] = pvr[i];
+        pct[j * PCT_S + b] = pvr[i];
         ix_s[e] = ixr[i];
         xh_s[e] = Cvt<T>::to_f(xqr[i]);
       }
@@ -366,7 +365,7 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
     const int b = o / NMAX, n = o % NMAX;
     const E dq = Cvt<T>::from_f(n < N ? lg_s[o] : 0.f);
     dll[b * 32 + n] = dq;
-    dlt[n * BMAX + b] = dq;
+    dlt[n * DLT_S + b] = dq;
   }
   __syncthreads();
   float s1 = 0.f, s2 = 0.f;
@@ -374,7 +373,7 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
     const typename mm::frag a = mm::ld(&dll[(16 * wv + r) * 32 + 8 * q]);
 #pragma unroll
     for (int nt = 0; nt < KP / 16; ++nt) {
-      const typename mm::frag bf = mm::ld(&wdl[(16 * nt + r) * 32 + 8 * q]);
+      const typename mm::frag bf = mm::ld(&wdl[(16 * nt + r) * WDL_S + 8 * q]);
       const f32x4 acc = mm::mma(a, bf, f32x4{0.f, 0.f, 0.f, 0.f});
       const int j = 16 * nt + r;
 #pragma unroll
@@ -397,8 +396,8 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < BMAX / 32; ++s) {
-      const typename mm::frag a = mm::ld(&dlt[r * BMAX + 32 * s + 8 * q]);
-      const typename mm::frag bf = mm::ld(&pct[(16 * wv + r) * BMAX + 32 * s + 8 * q]);
+      const typename mm::frag a = mm::ld(&dlt[r * DLT_S + 32 * s + 8 * q]);
+      const typename mm::frag bf = mm::ld(&pct[(16 * wv + r) * PCT_S + 32 * s + 8 * q]);
       acc = mm::mma(a, bf, acc);
     }
     const int j = 16 * wv + r;
