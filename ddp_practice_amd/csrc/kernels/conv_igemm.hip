@@ -42,7 +42,22 @@ struct Geom {
   int N, H, W, C, OH, OW, K, R, S, stride, pad;
   long long M;  // N*OH*OW
   int accumulate = 0;  // conv_fwd: y += conv(x, w) (a residual gradient already in y)
+  long long cls_rows = 0;  // MODE_S2T: pixel tiles per output parity class
+  const void* aux = nullptr;  // conv_fwd epilogue: y[n][oh][ow] += aux[n][oh/2][ow/2] at even (oh, ow)
 };
+
+// Loader modes of the implicit-GEMM kernels:
+//   MODE_GEN  one filter tap x 64 input channels per K-step (C % 64 == 0);
+//   MODE_STEM the 7x7 / stride-2 stem on a 4-channel (3 + one zero) NHWC image: K is
+//             the flattened (r, s, c) space padded to 8 x 8 x 4 = 256 (4 K-steps), a
+//             16-B chunk is two horizontally adjacent taps x 4 channels (two 8-B loads);
+//             the packed filter is [K][8][8][4] with zeros in the padding;
+//   MODE_S2T  the data gradient of a 3x3 / stride-2 / pad-1 conv (a transposed conv):
+//             dx is split by output parity (py, px) into four stride-1 sub-convolutions
+//             of dy with 1, 2, 2 and 4 of the taps -- no zero-inserted dy, no wasted MFMA
+//             -- each written with stride 2 into dx; filter = the flipped transpose.
+constexpr int MODE_GEN = 0, MODE_STEM = 1, MODE_S2T = 2;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ (row & 7)) << 3); }
 
@@ -117,7 +132,7 @@ __device__ __forceinline__ void sum_rows(const float* __restrict__ src, int n, f
 }
 
 // slab: [gridDim(pixel tiles)][2][K] partial statistics (null: none)
-template <typename T, int BN>
+template <typename T, int BN, int MODE = MODE_GEN>
 __global__ void __launch_bounds__(THR)
 conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__ y, StatArgs sa, Geom g) {
   using MMT = MM<T>;
@@ -137,12 +152,20 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
   const unsigned nwg = gridDim.x, hw = blockIdx.x;
   const unsigned q8 = nwg / 8, r8 = nwg % 8, xcd = hw % 8, slot = hw / 8;
   const unsigned lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
-  const long long bm = lid / nct;
+  const long long bm_all = lid / nct;
   const int bn = (int)(lid % nct);
+  int cls = 0;  // MODE_S2T: output parity class (py, px)
+  long long bm = bm_all;
+  if constexpr (MODE == MODE_S2T) {
+    cls = (int)(bm_all / g.cls_rows);
+    bm = bm_all - (long long)cls * g.cls_rows;
+  }
+  const int py = cls >> 1, px = cls & 1;
+  const int nsx = px ? 2 : 1;  // MODE_S2T: column taps of this class
   const long long p0 = bm * BM;
   const int k0 = bn * BN;
-  const int KT = g.R * g.S * (g.C / BK);
-  const int cpt = g.C / BK;
+  const int cpt = MODE == MODE_STEM ? 1 : g.C / BK;
+  const int KT = MODE == MODE_STEM ? 4 : (MODE == MODE_S2T ? (py ? 2 : 1) * nsx : g.R * g.S) * cpt;
   // loader geometry: chunk cc of rows rr + 32 i
   const int cc = tid & 7, rr = tid >> 3;
   long long xb[4];
@@ -156,28 +179,58 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
       const int oh = (int)(t % g.OH);
       const int n = (int)(t / g.OH);
       xb[i] = (long long)n * g.H * g.W * g.C;
-      ih0[i] = oh * g.stride - g.pad;
-      iw0[i] = ow * g.stride - g.pad;
+      ih0[i] = MODE == MODE_S2T ? oh : oh * g.stride - g.pad;
+      iw0[i] = MODE == MODE_S2T ? ow : ow * g.stride - g.pad;
     } else {
       xb[i] = -1;
       ih0[i] = iw0[i] = 0;
     }
   }
-  const long long wrow = (long long)g.R * g.S * g.C;
+  const long long wrow = MODE == MODE_STEM ? 256 : (long long)g.R * g.S * g.C;
   f32x4 rx[4], rw[BLD];
   auto gload = [&](int kt) {
-    const int rs = kt / cpt, c0 = (kt - rs * cpt) * BK + cc * 8;
-    const int r = rs / g.S, s = rs - r * g.S;
+    long long woff;  // this K-step's offset inside a filter row
+    if constexpr (MODE == MODE_STEM) {
+      const int r = 2 * kt + (cc >> 2), s = (cc & 3) * 2;  // taps (r, s) and (r, s + 1)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ih = ih0[i] + r, iw = iw0[i] + s;
-      const bool ok = xb[i] >= 0 && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-      rx[i] = ok ? *reinterpret_cast<const f32x4*>(x + xb[i] + ((long long)ih * g.W + iw) * g.C + c0)
-                 : f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < 4; ++i) {
+        const int ih = ih0[i] + r, iw = iw0[i] + s;
+        const bool rok = xb[i] >= 0 && r < 7 && (unsigned)ih < (unsigned)g.H;
+        const T* px_ = x + xb[i] + ((long long)ih * g.W + iw) * 4;
+        f32x2 lo = {0.f, 0.f}, hi = {0.f, 0.f};
+        if (rok && (unsigned)iw < (unsigned)g.W) lo = *reinterpret_cast<const f32x2*>(px_);
+        if (rok && s + 1 < 7 && (unsigned)(iw + 1) < (unsigned)g.W) hi = *reinterpret_cast<const f32x2*>(px_ + 4);
+        rx[i] = f32x4{lo[0], lo[1], hi[0], hi[1]};
+      }
+      woff = (long long)kt * BK + cc * 8;
+    } else if constexpr (MODE == MODE_S2T) {
+      const int t = kt / cpt, c0 = (kt - t * cpt) * BK + cc * 8;
+      const int ri = t / nsx, si = t - ri * nsx;
+      const int r = py ? (ri ? 2 : 0) : 1, s = px ? (si ? 2 : 0) : 1;  // forward-filter tap
+      const int dh = (py && !ri) ? 1 : 0, dw = (px && !si) ? 1 : 0;    // dy row / col offset
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ih = ih0[i] + dh, iw = iw0[i] + dw;
+        const bool ok = xb[i] >= 0 && ih < g.H && iw < g.W;
+        rx[i] = ok ? *reinterpret_cast<const f32x4*>(x + xb[i] + ((long long)ih * g.W + iw) * g.C + c0)
+                   : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      woff = (long long)(8 - (r * 3 + s)) * g.C + c0;  // flipped filter: tap 8 - (3r + s)
+    } else {
+      const int rs = kt / cpt, c0 = (kt - rs * cpt) * BK + cc * 8;
+      const int r = rs / g.S, s = rs - r * g.S;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ih = ih0[i] + r, iw = iw0[i] + s;
+        const bool ok = xb[i] >= 0 && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+        rx[i] = ok ? *reinterpret_cast<const f32x4*>(x + xb[i] + ((long long)ih * g.W + iw) * g.C + c0)
+                   : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      woff = (long long)kt * BK + cc * 8;
     }
 #pragma unroll
     for (int i = 0; i < BLD; ++i)
-      rw[i] = *reinterpret_cast<const f32x4*>(w + (long long)(k0 + rr + 32 * i) * wrow + (long long)kt * BK + cc * 8);
+      rw[i] = *reinterpret_cast<const f32x4*>(w + (long long)(k0 + rr + 32 * i) * wrow + woff);
   };
   auto lstore = [&](int buf) {
     T* A = lds[buf];           // weights: rows [0, BN)
@@ -296,19 +349,36 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
     last1 = last_arriver(sa.tickets + bn * NG + grp, (unsigned)gsz, &s_flag);
   }
   // output stores: whole 16-B chunks, consecutive lanes along a pixel's channels
+  const T* aux = reinterpret_cast<const T*>(g.aux);
 #pragma unroll
   for (int it = 0; it < BM / RPI; ++it) {
     const int pl = it * RPI + tid / CPR;
     const long long p = p0 + pl;
     if (p < g.M) {
-      f32x4* dst = reinterpret_cast<f32x4*>(y + p * g.K + k0 + ch * 8);
+      long long op = p;  // output pixel
+      int oh = 0, ow = 0, n = 0;
+      if (MODE == MODE_S2T || aux != nullptr) {
+        ow = (int)(p % g.OW);
+        const long long t = p / g.OW;
+        oh = (int)(t % g.OH);
+        n = (int)(t / g.OH);
+      }
+      if constexpr (MODE == MODE_S2T) op = ((long long)n * (2 * g.OH) + 2 * oh + py) * (2 * g.OW) + 2 * ow + px;
+      f32x4* dst = reinterpret_cast<f32x4*>(y + op * g.K + k0 + ch * 8);
       f32x4 raw = *reinterpret_cast<const f32x4*>(tile + pl * RS + ch * 8);
-      if (g.accumulate) {  // y += tile, summed in fp32, rounded once
-        const f32x4 old = *dst;
+      const bool add_aux = aux != nullptr && !(oh & 1) && !(ow & 1);
+      if (g.accumulate || add_aux) {  // y (+)= tile (+ aux), summed in fp32, rounded once
+        f32x4 old = {0.f, 0.f, 0.f, 0.f}, ax = {0.f, 0.f, 0.f, 0.f};
+        if (g.accumulate) old = *dst;
+        if (add_aux)
+          ax = *reinterpret_cast<const f32x4*>(
+              aux + (((long long)n * (g.OH >> 1) + (oh >> 1)) * (g.OW >> 1) + (ow >> 1)) * g.K + k0 + ch * 8);
         const T* a = reinterpret_cast<const T*>(&old);
+        const T* e = reinterpret_cast<const T*>(&ax);
         T* b = reinterpret_cast<T*>(&raw);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) b[j] = Cvt<T>::from_f(Cvt<T>::to_f(a[j]) + Cvt<T>::to_f(b[j]));
+        for (int j = 0; j < 8; ++j)
+          b[j] = Cvt<T>::from_f(Cvt<T>::to_f(a[j]) + Cvt<T>::to_f(e[j]) + Cvt<T>::to_f(b[j]));
       }
       *dst = raw;
     }
@@ -352,7 +422,7 @@ __device__ __forceinline__ int wswz(int row, int chunk) {
   return row * CH * 8 + ((chunk ^ m) << 3);
 }
 
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, int MODE = MODE_GEN>
 __global__ void __launch_bounds__(THR)
 conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ slab, Geom g, int splits,
                   long long pps) {
@@ -364,7 +434,7 @@ conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __re
   __shared__ __attribute__((aligned(16))) T lds[2][BP * (BM + BN)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
-  const int RSC = g.R * g.S * g.C;
+  const int RSC = MODE == MODE_STEM ? 256 : g.R * g.S * g.C;  // stem: [8][8][4] padded columns
   const int tm = g.K / BM, tn = RSC / BN, tiles = tm * tn;
   const unsigned nwg = gridDim.x, hw = blockIdx.x;
   const unsigned q8 = nwg / 8, r8 = nwg % 8, xcd = hw % 8, slot = hw / 8;
@@ -393,9 +463,21 @@ conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __re
         const int ow = (int)(pu - q * (unsigned)g.OW);
         const unsigned n = q / (unsigned)g.OH;
         const int oh = (int)(q - n * (unsigned)g.OH);
-        const int ih = oh * g.stride + fr_ - g.pad, iw = ow * g.stride + fs_ - g.pad;
-        if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
-          v = *reinterpret_cast<const f32x4*>(x + (((long long)n * g.H + ih) * g.W + iw) * g.C + c0 + cc * 8);
+        if constexpr (MODE == MODE_STEM) {
+          // column n0 + 8cc: taps (r, s), (r, s + 1) of the [8][8][4] padded filter space
+          const int col = n0 + cc * 8, r = col >> 5, s = (col >> 2) & 7;
+          const int ih = oh * g.stride + r - g.pad, iw = ow * g.stride + s - g.pad;
+          const bool rok = r < 7 && (unsigned)ih < (unsigned)g.H;
+          const T* px_ = x + (((long long)n * g.H + ih) * g.W + iw) * 4;
+          f32x2 lo = {0.f, 0.f}, hi = {0.f, 0.f};
+          if (rok && (unsigned)iw < (unsigned)g.W) lo = *reinterpret_cast<const f32x2*>(px_);
+          if (rok && s + 1 < 7 && (unsigned)(iw + 1) < (unsigned)g.W) hi = *reinterpret_cast<const f32x2*>(px_ + 4);
+          v = f32x4{lo[0], lo[1], hi[0], hi[1]};
+        } else {
+          const int ih = oh * g.stride + fr_ - g.pad, iw = ow * g.stride + fs_ - g.pad;
+          if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
+            v = *reinterpret_cast<const f32x4*>(x + (((long long)n * g.H + ih) * g.W + iw) * g.C + c0 + cc * 8);
+        }
       }
       rb[i] = v;
     }
@@ -475,9 +557,11 @@ conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __re
 // grad[k][c][r][s] (fp32 OIHW) = sum over splits of slab[sp][k][(r*S + s)*C + c]:
 // a workgroup owns 256 consecutive slab columns as 64 float4 quads x 4 split groups
 // (every 4th split, fixed order, 4 loads in flight), combined through LDS in group
-// order, written in the OIHW order.
+// order, written in the OIHW order of a [K][Cd][Rd][Sd] gradient (Cd <= C, Rd <= R,
+// Sd <= S: the stem's padded columns are dropped here).
 __global__ void __launch_bounds__(256)
-wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ grad, int splits, int K, int C, int R, int S) {
+wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ grad, int splits, int K, int C, int R, int S,
+                    int Cd, int Rd, int Sd) {
   __shared__ f32x4 part[4][64];
   const long long RSC = (long long)R * S * C, total = (long long)K * RSC;
   const int qd = threadIdx.x & 63, rg = threadIdx.x >> 6;
@@ -503,11 +587,14 @@ wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ grad, in
     const f32x4 t = part[0][qd] + part[1][qd] + part[2][qd] + part[3][qd];
     const int k = (int)(col / RSC);
     const long long n = col - (long long)k * RSC;  // (r*S + s)*C + c, c % 4 == 0
-    const int c = (int)(n % C), rs = (int)(n / C);
-    float* o = grad + ((long long)k * C + c) * R * S + rs;
-    const int st = R * S;
+    const int c = (int)(n % C), rs = (int)(n / C), r = rs / S, s = rs - r * S;
+    if (r < Rd && s < Sd) {
+      float* o = grad + (((long long)k * Cd + c) * Rd + r) * Sd + s;
+      const int st = Rd * Sd;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j * st] = t[j];
+      for (int j = 0; j < 4; ++j)
+        if (c + j < Cd) o[j * st] = t[j];
+    }
   }
 }
 
@@ -557,6 +644,61 @@ pack_weights_kernel(const int64_t* __restrict__ table, int n) {
   }
 }
 
+// Stem operands in one launch: the [N][3][H][W] image (fp32 or the compute dtype)
+// -> the 4-channel NHWC image [N][H][W][4] (one 8-B store per pixel, 4th channel 0),
+// and, in the trailing workgroups, the fp32 [K][3][7][7] filter -> [K][8][8][4] in the
+// compute dtype with zeros in the padding (the MODE_STEM K space).
+template <typename T, typename S>
+__global__ void __launch_bounds__(256)
+stem_pack_kernel(const S* __restrict__ x, T* __restrict__ x4, long long npix, int HW, const float* __restrict__ w,
+                 T* __restrict__ w4, int K, long long xblocks) {
+  if ((long long)blockIdx.x < xblocks) {
+    const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (p >= npix) return;
+    const long long n = p / HW, hw = p - n * HW;
+    const S* src = x + n * 3 * HW + hw;
+    T v[4] = {Cvt<T>::from_f(Cvt<S>::to_f(src[0])), Cvt<T>::from_f(Cvt<S>::to_f(src[HW])),
+              Cvt<T>::from_f(Cvt<S>::to_f(src[2 * HW])), Cvt<T>::from_f(0.f)};
+    *reinterpret_cast<u16x4*>(x4 + p * 4) = *reinterpret_cast<const u16x4*>(v);
+    return;
+  }
+  const int e = (int)((long long)blockIdx.x - xblocks) * 256 + threadIdx.x;
+  if (e >= K * 256) return;
+  const int k = e >> 8, rem = e & 255, r = rem >> 5, s = (rem >> 2) & 7, c = rem & 3;
+  w4[e] = Cvt<T>::from_f(r < 7 && s < 7 && c < 3 ? w[((k * 3 + c) * 7 + r) * 7 + s] : 0.f);
+}
+
+// x: [N, 3, H, W] contiguous (fp32 / bf16 / f16); w: fp32 [K, 3, 7, 7]; x4: [N, 4, H, W]
+// channels_last, w4: [K, 4, 8, 8] channels_last, both in the compute dtype.
+void stem_pack(at::Tensor x, at::Tensor w, at::Tensor x4, at::Tensor w4) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 4 && x.size(1) == 3, "stem_pack: x [N, 3, H, W]");
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.is_contiguous() && w.size(1) == 3 && w.size(2) == 7 &&
+                  w.size(3) == 7, "stem_pack: fp32 [K, 3, 7, 7] filter");
+  TORCH_CHECK(x4.is_contiguous(at::MemoryFormat::ChannelsLast) && x4.size(0) == x.size(0) && x4.size(1) == 4 &&
+                  x4.size(2) == x.size(2) && x4.size(3) == x.size(3), "stem_pack: x4 [N, 4, H, W] channels_last");
+  TORCH_CHECK(w4.is_contiguous(at::MemoryFormat::ChannelsLast) && w4.size(0) == w.size(0) && w4.size(1) == 4 &&
+                  w4.size(2) == 8 && w4.size(3) == 8 && w4.scalar_type() == x4.scalar_type(), "stem_pack: w4");
+  TORCH_CHECK(x4.scalar_type() == at::kBFloat16 || x4.scalar_type() == at::kHalf, "stem_pack: bf16 / f16");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == x4.scalar_type(), "stem_pack: x dtype");
+  const long long HW = x.size(2) * x.size(3), npix = x.size(0) * HW;
+  const int K = (int)w.size(0);
+  const long long xblocks = (npix + 255) / 256, wblocks = ((long long)K * 256 + 255) / 256;
+  auto launch = [&](auto tag) {
+    using T = decltype(tag);
+    T* x4p = reinterpret_cast<T*>(x4.data_ptr());
+    T* w4p = reinterpret_cast<T*>(w4.data_ptr());
+    if (x.scalar_type() == at::kFloat)
+      hipLaunchKernelGGL((stem_pack_kernel<T, float>), dim3((unsigned)(xblocks + wblocks)), dim3(256), 0,
+                         cur_stream(), x.data_ptr<float>(), x4p, npix, (int)HW, w.data_ptr<float>(), w4p, K, xblocks);
+    else
+      hipLaunchKernelGGL((stem_pack_kernel<T, T>), dim3((unsigned)(xblocks + wblocks)), dim3(256), 0, cur_stream(),
+                         reinterpret_cast<const T*>(x.data_ptr()), x4p, npix, (int)HW, w.data_ptr<float>(), w4p, K,
+                         xblocks);
+  };
+  if (x4.scalar_type() == at::kBFloat16) launch(__hip_bfloat16{}); else launch(__half{});
+  DPA_CHECK_LAUNCH();
+}
+
 void pack_weights(at::Tensor table, int64_t n, int64_t tiles, int64_t dtype_code) {
   TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kLong && table.numel() >= 8 * n, "pack_weights: table");
   if (tiles <= 0) return;
@@ -598,9 +740,15 @@ int64_t stat_tickets_len(int64_t M, int64_t K) {
 // y: [N, K, OH, OW] channels_last (preallocated).  With `stats` (fp32 [3K+4], the
 // bn_nhwc layout), also part / tickets (stat_part_len / stat_tickets_len; tickets
 // zero-initialised once), shift (running mean) and nbt: the fused BN statistics.
+//
+// mode MODE_STEM: x = the stem_pack image [N, 4, H, W], w = [K, 4, 8, 8] (stride 2, pad 3,
+// a 7x7 filter); mode MODE_S2T: x = dy [N, Cf, OHf, OWf] of a 3x3 / stride-2 / pad-1 conv,
+// w = its flipped transposed filter [Cin, Cf, 3, 3], y = dx [N, Cin, 2 OHf, 2 OWf].
+// aux (MODE_GEN, channels_last [N, K, OH/2, OW/2]): added at the even output pixels --
+// a stride-2 1x1 conv's data gradient folded into this one's output.
 void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t pad, c10::optional<at::Tensor> part,
               c10::optional<at::Tensor> tickets, c10::optional<at::Tensor> stats, c10::optional<at::Tensor> shift,
-              c10::optional<at::Tensor> nbt, bool accumulate) {
+              c10::optional<at::Tensor> nbt, bool accumulate, int64_t mode, c10::optional<at::Tensor> aux) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "conv_fwd: device tensors");
   TORCH_CHECK(x.scalar_type() == w.scalar_type() && x.scalar_type() == y.scalar_type(), "conv_fwd: one dtype");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "conv_fwd: bf16 / f16");
@@ -609,8 +757,36 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
               "conv_fwd: channels_last x / w / y");
   Geom g = geom(x, w, (int)stride, (int)pad);
   g.accumulate = accumulate ? 1 : 0;
-  TORCH_CHECK(w.size(1) == g.C && supported(g.C, g.K), "conv_fwd: needs C % 64 == 0 and Cout % 64 == 0");
-  TORCH_CHECK(y.size(0) == g.N && y.size(1) == g.K && y.size(2) == g.OH && y.size(3) == g.OW, "conv_fwd: y shape");
+  TORCH_CHECK(mode == MODE_GEN || mode == MODE_STEM || mode == MODE_S2T, "conv_fwd: mode");
+  if (mode == MODE_STEM) {
+    TORCH_CHECK(g.C == 4 && w.size(1) == 4 && g.R == 8 && g.S == 8 && stride == 2 && pad == 3 && g.K % 64 == 0,
+                "conv_fwd: stem needs the stem_pack operands (x [N,4,H,W], w [K,4,8,8]), stride 2, pad 3");
+    g.R = g.S = 7;
+    g.OH = (g.H + 2 * g.pad - 7) / 2 + 1;
+    g.OW = (g.W + 2 * g.pad - 7) / 2 + 1;
+    g.M = (long long)g.N * g.OH * g.OW;
+  } else {
+    TORCH_CHECK(w.size(1) == g.C && supported(g.C, g.K), "conv_fwd: needs C % 64 == 0 and Cout % 64 == 0");
+  }
+  if (mode == MODE_S2T) {
+    TORCH_CHECK(g.R == 3 && g.S == 3 && stride == 2 && pad == 1, "conv_fwd: the S2T mode is a 3x3/s2/p1 dgrad");
+    g.OH = g.H;
+    g.OW = g.W;
+    g.M = (long long)g.N * g.OH * g.OW;
+    g.cls_rows = (g.M + BM - 1) / BM;
+    TORCH_CHECK(y.size(0) == g.N && y.size(1) == g.K && y.size(2) == 2 * g.OH && y.size(3) == 2 * g.OW,
+                "conv_fwd: S2T dx must be [N, Cin, 2 OHf, 2 OWf]");
+    TORCH_CHECK(!stats.has_value() && !aux.has_value(), "conv_fwd: S2T has no statistics / aux");
+  } else {
+    TORCH_CHECK(y.size(0) == g.N && y.size(1) == g.K && y.size(2) == g.OH && y.size(3) == g.OW, "conv_fwd: y shape");
+  }
+  if (aux.has_value()) {
+    TORCH_CHECK(mode == MODE_GEN && g.OH % 2 == 0 && g.OW % 2 == 0 && aux->scalar_type() == y.scalar_type() &&
+                    aux->is_contiguous(at::MemoryFormat::ChannelsLast) && aux->size(0) == g.N &&
+                    aux->size(1) == g.K && aux->size(2) == g.OH / 2 && aux->size(3) == g.OW / 2,
+                "conv_fwd: aux must be [N, K, OH/2, OW/2] channels_last in y's dtype");
+    g.aux = aux->data_ptr();
+  }
   const bool st = stats.has_value();
   TORCH_CHECK(!(st && accumulate), "conv_fwd: statistics of an accumulated output are not supported");
   TORCH_CHECK(st == part.has_value() && st == tickets.has_value() && st == shift.has_value(),
@@ -630,19 +806,24 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
   }
   const int BN = tile_n(g.K);
   const long long rows = (g.M + BM - 1) / BM;
-  const long long blocks = rows * (g.K / BN);
+  const long long blocks = rows * (g.K / BN) * (mode == MODE_S2T ? 4 : 1);
   TORCH_CHECK(blocks < (1LL << 31), "conv_fwd: grid too large");
   auto launch = [&](auto tag) {
     using T = decltype(tag);
     const T* xp = reinterpret_cast<const T*>(x.data_ptr());
     const T* wp = reinterpret_cast<const T*>(w.data_ptr());
     T* yp = reinterpret_cast<T*>(y.data_ptr());
-    if (BN == 128)
-      hipLaunchKernelGGL((conv_fwd_kernel<T, 128>), dim3((unsigned)blocks), dim3(THR), 0, cur_stream(), xp, wp, yp,
-                         sa, g);
-    else
-      hipLaunchKernelGGL((conv_fwd_kernel<T, 64>), dim3((unsigned)blocks), dim3(THR), 0, cur_stream(), xp, wp, yp, sa,
-                         g);
+    const dim3 gr((unsigned)blocks), th(THR);
+    if (mode == MODE_STEM) {
+      if (BN == 128) hipLaunchKernelGGL((conv_fwd_kernel<T, 128, MODE_STEM>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+      else hipLaunchKernelGGL((conv_fwd_kernel<T, 64, MODE_STEM>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+    } else if (mode == MODE_S2T) {
+      if (BN == 128) hipLaunchKernelGGL((conv_fwd_kernel<T, 128, MODE_S2T>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+      else hipLaunchKernelGGL((conv_fwd_kernel<T, 64, MODE_S2T>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+    } else {
+      if (BN == 128) hipLaunchKernelGGL((conv_fwd_kernel<T, 128>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+      else hipLaunchKernelGGL((conv_fwd_kernel<T, 64>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+    }
   };
   if (x.scalar_type() == at::kBFloat16) launch(__hip_bfloat16{}); else launch(__half{});
   DPA_CHECK_LAUNCH();
@@ -670,20 +851,33 @@ int64_t wgrad_splits(int64_t M, int64_t K, int64_t C, int64_t R, int64_t S) {
 }
 
 // dy: [N, K, OH, OW] channels_last; x: [N, C, H, W] channels_last; grad: fp32 [K, C, R, S]
-// contiguous (written, not accumulated); slab: fp32 >= splits * K * R*S*C
-void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor grad, int64_t stride, int64_t pad, at::Tensor slab) {
+// contiguous (written, not accumulated); slab: fp32 >= splits * K * R*S*C.
+// mode MODE_STEM: x = the stem_pack image [N, 4, H, W], grad [K, 3, 7, 7] (stride 2, pad 3).
+void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor grad, int64_t stride, int64_t pad, at::Tensor slab,
+                int64_t mode) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && grad.is_cuda() && slab.is_cuda(), "conv_wgrad: device tensors");
   TORCH_CHECK(dy.scalar_type() == x.scalar_type() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf),
               "conv_wgrad: bf16 / f16 activations");
   TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) && x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "conv_wgrad: channels_last dy / x");
   TORCH_CHECK(grad.scalar_type() == at::kFloat && grad.is_contiguous() && grad.dim() == 4, "conv_wgrad: fp32 grad");
-  const Geom g = geom(x, grad, (int)stride, (int)pad);
-  TORCH_CHECK(grad.size(1) == g.C && supported(g.C, g.K), "conv_wgrad: needs C % 64 == 0 and Cout % 64 == 0");
+  const bool stem = mode == MODE_STEM;
+  TORCH_CHECK(mode == MODE_GEN || stem, "conv_wgrad: mode");
+  Geom g = geom(x, grad, (int)stride, (int)pad);
+  int Cd = g.C, Rd = g.R, Sd = g.S;  // gradient dims (the stem's padded K space drops to these)
+  if (stem) {
+    TORCH_CHECK(x.size(1) == 4 && grad.size(1) == 3 && g.R == 7 && g.S == 7 && stride == 2 && pad == 3 &&
+                    g.K % 64 == 0, "conv_wgrad: stem needs the stem_pack image and a [K, 3, 7, 7] gradient");
+    g.C = 4;
+    Cd = 3;
+  } else {
+    TORCH_CHECK(grad.size(1) == g.C && supported(g.C, g.K), "conv_wgrad: needs C % 64 == 0 and Cout % 64 == 0");
+  }
   TORCH_CHECK(dy.size(0) == g.N && dy.size(1) == g.K && dy.size(2) == g.OH && dy.size(3) == g.OW, "conv_wgrad: dy");
   TORCH_CHECK(g.M < (1LL << 31), "conv_wgrad: too many pixels");
-  const int64_t sp = wgrad_splits(g.M, g.K, g.C, g.R, g.S);
-  const int64_t RSC = (int64_t)g.R * g.S * g.C;
+  const int SR = stem ? 8 : g.R, SS = stem ? 8 : g.S;  // slab column space [SR][SS][C]
+  const int64_t sp = wgrad_splits(g.M, g.K, g.C, SR, SS);
+  const int64_t RSC = (int64_t)SR * SS * g.C;
   TORCH_CHECK(slab.scalar_type() == at::kFloat && slab.numel() >= sp * g.K * RSC, "conv_wgrad: slab too small");
   const long long pps = ((g.M + sp - 1) / sp + 63) / 64 * 64;
   const int BM = wtile(g.K), BN = wtile(g.C);
@@ -694,7 +888,9 @@ void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor grad, int64_t stride, in
     const T* xp = reinterpret_cast<const T*>(x.data_ptr());
     float* sl = slab.data_ptr<float>();
     const dim3 gr((unsigned)blocks), th(THR);
-    if (BM == 128 && BN == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 128>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+    if (stem && BM == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 64, MODE_STEM>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+    else if (stem) hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 64, MODE_STEM>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+    else if (BM == 128 && BN == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 128>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
     else if (BM == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 64>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
     else if (BN == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 128>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
     else hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 64>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
@@ -703,7 +899,7 @@ void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor grad, int64_t stride, in
   DPA_CHECK_LAUNCH();
   const long long total = (long long)g.K * RSC;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, cur_stream(),
-                     slab.data_ptr<float>(), grad.data_ptr<float>(), (int)sp, g.K, g.C, g.R, g.S);
+                     slab.data_ptr<float>(), grad.data_ptr<float>(), (int)sp, g.K, g.C, SR, SS, Cd, Rd, Sd);
   DPA_CHECK_LAUNCH();
 }
 
@@ -715,11 +911,15 @@ void register_conv_igemm(pybind11::module& m) {
         pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("part") = pybind11::none(),
         pybind11::arg("tickets") = pybind11::none(), pybind11::arg("stats") = pybind11::none(),
         pybind11::arg("shift") = pybind11::none(), pybind11::arg("nbt") = pybind11::none(),
-        pybind11::arg("accumulate") = false);
+        pybind11::arg("accumulate") = false, pybind11::arg("mode") = 0, pybind11::arg("aux") = pybind11::none());
   s.def("supported", &igemm::supported);
   s.def("stat_part_len", &igemm::stat_part_len);
   s.def("stat_tickets_len", &igemm::stat_tickets_len);
-  s.def("conv_wgrad", &igemm::conv_wgrad);
+  s.def("conv_wgrad", &igemm::conv_wgrad, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("grad"),
+        pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("slab"), pybind11::arg("mode") = 0);
+  s.def("stem_pack", &igemm::stem_pack);
+  s.attr("MODE_STEM") = igemm::MODE_STEM;
+  s.attr("MODE_S2T") = igemm::MODE_S2T;
   s.def("pack_weights", &igemm::pack_weights);
   s.def("wgrad_splits", &igemm::wgrad_splits);
 }

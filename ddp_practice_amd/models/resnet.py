@@ -11,10 +11,15 @@ Execution on a HIP device (``fused=True``): activations are bf16/f16/f32
     run on the hand-written NHWC implicit-GEMM MFMA kernel, which also produces
     the following BatchNorm's batch statistics in its epilogue
     (csrc/kernels/conv_igemm.hip, ops/conv_igemm.py; DPA_IGEMM=0: library path);
-  * backward: 1x1 convolutions are GEMMs on the NHWC rows (hipBLASLt; the weight
-    gradient as a split-K batched GEMM with fp32 partials: ops/conv1x1.py), 3x3
-    and the 7x7 stem (also its forward: C = 3) on MIOpen's NHWC kernels
-    (ops/conv_nhwc.py: one cast+layout copy of the weight each way);
+  * the 7x7 / stride-2 stem (C = 3) runs on the same kernel's stem mode: the image
+    is packed to 4-channel NHWC in one launch and the K space is (r, s, c) padded to
+    8 x 8 x 4 (forward + statistics, and the weight gradient);
+  * backward: every weight gradient and every 3x3 data gradient (stride 1, and
+    stride 2 as four output-parity sub-convolutions) run on the implicit-GEMM
+    kernel, as do the 1x1 data gradients of <= 512 channels; wider 1x1 data
+    gradients are plain GEMMs on the NHWC rows (hipBLASLt, ops/conv1x1.py).  A
+    projection block's two input gradients (conv1 and downsample) are combined in
+    the conv epilogue instead of by a separate add;
   * every BatchNorm runs on the native NHWC kernels with its ReLU and, for the
     last BN of a bottleneck, the residual add fused in (ops/bn_nhwc.py), as
     SyncBatchNorm when the module was converted (one small all-reduce each way);
@@ -37,15 +42,16 @@ from ..ops.conv_nhwc import conv_nhwc
 _PACKS: dict = {}  # id(module) -> this forward's packed filters (ops/conv_igemm.WeightPack)
 
 
-def _conv(x: torch.Tensor, conv: nn.Conv2d, cdtype: torch.dtype, bn: nn.Module | None = None, tap=None):
+def _conv(x: torch.Tensor, conv: nn.Conv2d, cdtype: torch.dtype, bn: nn.Module | None = None, tap=None,
+          xtap=None):
     """conv(x) -> (output, statistics of the following training BN ``bn`` when the conv
     kernel produced them, else None)."""
     want = bn if (bn is not None and bn.training) else None
     pk = _PACKS.get(id(conv))
     if conv.kernel_size == (1, 1) and conv.padding == (0, 0) and conv.groups == 1 and conv.bias is None:
         if want is None:
-            return conv1x1(x, conv.weight, conv.stride[0], cdtype, tap, None, pk), None
-        return conv1x1(x, conv.weight, conv.stride[0], cdtype, tap, want, pk)
+            return conv1x1(x, conv.weight, conv.stride[0], cdtype, tap, None, pk, xtap), None
+        return conv1x1(x, conv.weight, conv.stride[0], cdtype, tap, want, pk, xtap)
     if conv.bias is None and conv.groups == 1 and conv.dilation == (1, 1):
         if want is None:
             return conv_nhwc(x, conv.weight, conv.stride, conv.padding, cdtype, None, pk), None
@@ -95,18 +101,22 @@ class Bottleneck(nn.Module):
     def forward_native(self, x: torch.Tensor, cdtype: torch.dtype) -> torch.Tensor:
         from ..ops.bn_nhwc import bn_act
 
-        # identity blocks: conv1's dgrad GEMM accumulates the residual gradient (GradTap)
-        tap = GradTap() if (self.downsample is None and self.bn3.training and torch.is_grad_enabled()
-                            and x.requires_grad and x.is_contiguous(memory_format=torch.channels_last)) else None
+        grad_x = (self.bn3.training and torch.is_grad_enabled() and x.requires_grad
+                  and x.is_contiguous(memory_format=torch.channels_last))
+        # identity blocks: conv1's dgrad GEMM accumulates the residual gradient (GradTap);
+        # projection blocks: conv1 and the downsample conv share x's gradient (one of them
+        # folds the other's product into its own, ops/conv1x1.Conv1x1Fn)
+        tap = GradTap() if (grad_x and self.downsample is None) else None
+        xtap = GradTap() if (grad_x and self.downsample is not None) else None
         # each conv hands the following BN its batch statistics (ops/conv_igemm.py)
-        c1, st = _conv(x, self.conv1, cdtype, self.bn1, tap)
+        c1, st = _conv(x, self.conv1, cdtype, self.bn1, tap, xtap)
         out = bn_act(c1, self.bn1, relu=True, comm=_comm_of(self.bn1), stats=st)
         c2, st = _conv(out, self.conv2, cdtype, self.bn2)
         out = bn_act(c2, self.bn2, relu=True, comm=_comm_of(self.bn2), stats=st)
         identity = x
         if self.downsample is not None:
             conv, bn = self.downsample[0], self.downsample[1]
-            cd, st = _conv(x, conv, cdtype, bn)
+            cd, st = _conv(x, conv, cdtype, bn, None, xtap)
             identity = bn_act(cd, bn, relu=False, comm=_comm_of(bn), stats=st)
         c3, st = _conv(out, self.conv3, cdtype, self.bn3)
         return bn_act(c3, self.bn3, res=identity, relu=True, comm=_comm_of(self.bn3), tap=tap, stats=st)
@@ -164,18 +174,24 @@ class ResNet(nn.Module):
         from ..ops.bn_nhwc import bn_act, global_avg_pool, max_pool_3x3s2
 
         cdtype = compute_dtype(x) if self.amp_dtype is not None else torch.float32
-        x = x.to(dtype=cdtype, memory_format=torch.channels_last)
         _PACKS.clear()
         if _igemm.ENABLED and cdtype in (torch.bfloat16, torch.float16):
-            # every implicit-GEMM conv's filters for this step in one launch
+            # every implicit-GEMM conv's filters for this step in one launch (with the flipped
+            # transpose where the data gradient runs on the kernel: every 3x3, and 1x1 convs
+            # of <= 512 output channels, ops/conv_igemm.dgrad_1x1_here)
             pack = getattr(self, "_wpack", None)
             if pack is None or pack.cdtype != cdtype:
-                convs = [(m, m.stride == (1, 1) and (m.kernel_size == (3, 3) or m.weight.shape[0] <= 512))
+                convs = [(m, m.kernel_size == (3, 3) or m.weight.shape[0] <= 512)
                          for m in self.modules() if isinstance(m, nn.Conv2d) and m.bias is None and m.groups == 1
                          and m.weight.shape[0] % 64 == 0 and m.weight.shape[1] % 64 == 0]
                 pack = self._wpack = _igemm.WeightPack(convs, cdtype)
             _PACKS.update(pack.run())
-        c, st = _conv(x, self.conv1, cdtype, self.bn1)
+        if _igemm.stem_usable(x, self.conv1, cdtype):
+            # 7x7 stem straight from the NCHW image (packed to 4-channel NHWC in-launch)
+            c, st = _igemm.stem_conv(x, self.conv1, cdtype, self.bn1)
+        else:
+            x = x.to(dtype=cdtype, memory_format=torch.channels_last)
+            c, st = _conv(x, self.conv1, cdtype, self.bn1)
         x = bn_act(c, self.bn1, relu=True, comm=_comm_of(self.bn1), stats=st)
         x = max_pool_3x3s2(x)
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):

@@ -74,12 +74,22 @@ class GradTap:
 
 
 class Conv1x1Fn(torch.autograd.Function):
+    """``xtap``: a :class:`GradTap` shared by the two 1x1 convs that read the same input
+    (a projection block's conv1 and its downsample conv).  Whichever backward runs
+    first deposits its data gradient there (stride 2: the compact [N, C, H/2, W/2]
+    product, not scattered) and returns none; the second folds it into its own -- the
+    stride-1 conv's implicit-GEMM epilogue adds a compact one at the even pixels
+    (``aux``) or accumulates onto a full one -- so autograd's separate gradient add,
+    the zero-filled stride-2 gradient and its scatter disappear."""
+
     @staticmethod
-    def forward(ctx, x, weight, stride: int, cdtype: torch.dtype, tap: GradTap | None = None, bn=None, packed=None):
+    def forward(ctx, x, weight, stride: int, cdtype: torch.dtype, tap: GradTap | None = None, bn=None, packed=None,
+                xtap: GradTap | None = None):
         in_shape = x.shape
         if tap is not None and stride != 1:
             raise ValueError("conv1x1: a gradient tap needs stride 1")
         ctx.tap = tap
+        ctx.xtap = xtap
         ctx.wshape = weight.shape
         C = x.shape[1]
         # packed: this step's compute-dtype filter (and its transpose) from ops/conv_igemm.WeightPack
@@ -126,13 +136,23 @@ class Conv1x1Fn(torch.autograd.Function):
         if ctx.tap is not None:
             acc, ctx.tap.grad = ctx.tap.grad, None
         K = w.shape[0]
-        mine = (ctx.needs_input_grad[0] and stride == 1 and _igemm.dgrad_1x1_here(K, H)
+        mine = (ctx.needs_input_grad[0] and _igemm.dgrad_1x1_here(K, H)
                 and _igemm.usable(dyc, w.t().reshape(C, K, 1, 1), w.dtype))
+        wt = None
         if mine:
             # dX = dY @ W as a 1x1 conv of dy with the transposed filter on the
             # implicit-GEMM kernel (accumulating onto a tapped residual gradient)
             wt = ctx.wt if ctx.wt is not None else w.t().contiguous().view(C, K, 1, 1)
-        if ctx.needs_input_grad[0] and acc is not None:
+        xt = ctx.xtap
+        if ctx.needs_input_grad[0] and xt is not None:
+            dx = Conv1x1Fn._shared_dgrad(xt, dyc, dyr, w, wt, (N, C, H, W), stride, in_shape)
+        elif ctx.needs_input_grad[0] and stride != 1:
+            # compact dY @ W, scattered into the zero-filled input gradient
+            cpt = Conv1x1Fn._compact(dyc, dyr, w, wt, (N, C, H, W))
+            n0, c0, h0, w0 = in_shape
+            dx = torch.zeros((n0, h0, w0, c0), dtype=cpt.dtype, device=cpt.device).permute(0, 3, 1, 2)
+            dx[:, :, ::stride, ::stride] = cpt
+        elif ctx.needs_input_grad[0] and acc is not None:
             if acc.shape != (N, C, H, W) or not acc.is_contiguous(memory_format=torch.channels_last):
                 raise RuntimeError("conv1x1: tapped gradient does not match the input")
             if mine:
@@ -140,15 +160,8 @@ class Conv1x1Fn(torch.autograd.Function):
             else:
                 _rows(acc).addmm_(dyr, w)  # acc <- acc + dY @ W (GEMM epilogue accumulate)
             dx = acc
-        elif mine:
-            dx, _ = _igemm.conv_fwd(dyc, wt, 1, 0)
         elif ctx.needs_input_grad[0]:
-            dx = torch.mm(dyr, w).view(N, H, W, C).permute(0, 3, 1, 2)
-            if stride != 1:
-                n0, c0, h0, w0 = in_shape
-                full = torch.zeros((n0, h0, w0, c0), dtype=dx.dtype, device=dx.device).permute(0, 3, 1, 2)
-                full[:, :, ::stride, ::stride] = dx
-                dx = full
+            dx = Conv1x1Fn._compact(dyc, dyr, w, wt, (N, C, H, W))
         if ctx.needs_input_grad[1]:
             if ctx.lazy_rows and _igemm.usable(dyc, w.view(ctx.wshape), w.dtype):
                 # implicit-GEMM weight gradient over the (strided) input pixels, fp32 out
@@ -157,13 +170,51 @@ class Conv1x1Fn(torch.autograd.Function):
                 # saved: the [P, C] rows, or (lazy) the unstrided input
                 rows = _rows(saved[:, :, ::stride, ::stride] if stride != 1 else saved) if ctx.lazy_rows else saved
                 dw = _wgrad(dyr, rows).view(ctx.wshape)
-        return dx, dw, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None
+
+    @staticmethod
+    def _compact(dyc, dyr, w, wt, geom):
+        """dY @ W over the output pixels: [N, C, H, W] channels_last (H, W of dy)."""
+        N, C, H, W = geom
+        if wt is not None:
+            return _igemm.conv_fwd(dyc, wt, 1, 0)[0]
+        return torch.mm(dyr, w).view(N, H, W, C).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def _shared_dgrad(xt, dyc, dyr, w, wt, geom, stride, in_shape):
+        other = xt.grad
+        xt.grad = None
+        if other is None:  # first of the pair: leave the (compact) product for the second
+            xt.grad = (Conv1x1Fn._compact(dyc, dyr, w, wt, geom), stride)
+            return None
+        t, ostride = other
+        if stride == 1 and ostride == 1:
+            if wt is not None:
+                _igemm.conv_acc(dyc, wt, t)
+            else:
+                _rows(t).addmm_(dyr, w)
+            return t
+        if stride == 1 and ostride == 2:
+            if wt is not None and t.is_contiguous(memory_format=torch.channels_last):
+                return _igemm.conv_fwd(dyc, wt, 1, 0, aux=t)[0]  # + t at the even pixels, in the epilogue
+            dx = Conv1x1Fn._compact(dyc, dyr, w, None, geom)
+            dx[:, :, ::2, ::2] += t
+            return dx
+        cpt = Conv1x1Fn._compact(dyc, dyr, w, wt, geom)
+        if ostride == 1:  # the stride-1 conv ran first: its full gradient takes ours at the strided pixels
+            t[:, :, ::stride, ::stride] += cpt
+            return t
+        n0, c0, h0, w0 = in_shape
+        dx = torch.zeros((n0, h0, w0, c0), dtype=cpt.dtype, device=cpt.device).permute(0, 3, 1, 2)
+        dx[:, :, ::stride, ::stride] = cpt
+        dx[:, :, ::ostride, ::ostride] += t
+        return dx
 
 
 def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int, cdtype: torch.dtype,
-            tap: GradTap | None = None, bn=None, packed=None):
+            tap: GradTap | None = None, bn=None, packed=None, xtap: GradTap | None = None):
     """Bias-free 1x1 conv (stride 1 or 2) of ``x`` with the fp32 ``weight``; the
     output is a channels_last [N, Cout, H', W'] tensor in ``cdtype``.  ``tap``:
     see :class:`GradTap`.  With ``bn`` (the training BatchNorm that follows): returns
     (output, its statistics or None) -- ops/conv_igemm.py."""
-    return Conv1x1Fn.apply(x, weight, int(stride), cdtype, tap, bn, packed)
+    return Conv1x1Fn.apply(x, weight, int(stride), cdtype, tap, bn, packed, xtap)

@@ -61,21 +61,91 @@ def conv_acc(x: torch.Tensor, w: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     return y
 
 
-def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn=None):
+def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn=None, aux=None, mode: int = 0):
     """y = conv(x, w) on the implicit-GEMM kernel; x, w channels_last in the compute dtype.
     With ``bn`` (a training BatchNorm module): also its statistics, returned as the second
-    value (None otherwise)."""
+    value (None otherwise).  ``aux`` ([N, K, OH/2, OW/2] channels_last): added into the
+    even output pixels (a stride-2 1x1 conv's data gradient folded in).  ``mode``:
+    MODE_STEM (x, w from :func:`stem_conv`'s pack, R = 7 semantics)."""
     N, C, H, W = x.shape
     K, _, R, S = w.shape
+    if mode == _K().MODE_STEM:
+        R = S = 7
     OH, OW = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
     y = torch.empty((N, K, OH, OW), dtype=x.dtype, device=x.device, memory_format=_CL)
     if bn is None:
-        _K().conv_fwd(x, w, y, stride, pad)
+        _K().conv_fwd(x, w, y, stride, pad, mode=mode, aux=aux)
         return y, None
     part, tickets = _StatWS.get(x.device, N * OH * OW, K)
     stats = torch.empty(3 * K + 4, dtype=torch.float32, device=x.device)
-    _K().conv_fwd(x, w, y, stride, pad, part, tickets, stats, bn.running_mean, bn.num_batches_tracked)
+    _K().conv_fwd(x, w, y, stride, pad, part, tickets, stats, bn.running_mean, bn.num_batches_tracked, mode=mode,
+                  aux=aux)
     return y, stats
+
+
+def dgrad_s2(dy: torch.Tensor, wt: torch.Tensor, in_hw) -> torch.Tensor | None:
+    """Data gradient of a 3x3 / stride-2 / pad-1 conv on the implicit-GEMM kernel
+    (MODE_S2T: four output-parity sub-convolutions, csrc/kernels/conv_igemm.hip).
+    ``wt``: the flipped transposed filter [Cin, Cout, 3, 3] channels_last; ``in_hw``: the
+    forward input's (H, W).  None when the shape is not covered (odd input sizes)."""
+    N, Kf, OH, OW = dy.shape
+    H, W = in_hw
+    if H != 2 * OH or W != 2 * OW:
+        return None
+    dx = torch.empty((N, wt.shape[0], H, W), dtype=dy.dtype, device=dy.device, memory_format=_CL)
+    _K().conv_fwd(dy, wt, dx, 2, 1, mode=_K().MODE_S2T)
+    return dx
+
+
+def stem_usable(x: torch.Tensor, conv, cdtype: torch.dtype) -> bool:
+    """The 7x7 / stride-2 / pad-3 stem over a 3-channel image runs on the kernel's
+    MODE_STEM (the image needs no gradient: it is the network input)."""
+    return (ENABLED and x.is_cuda and x.dim() == 4 and x.shape[1] == 3 and not x.requires_grad
+            and cdtype in (torch.bfloat16, torch.float16) and x.dtype in (torch.float32, cdtype)
+            and conv.kernel_size == (7, 7) and conv.stride == (2, 2) and conv.padding == (3, 3)
+            and conv.bias is None and conv.groups == 1 and conv.dilation == (1, 1)
+            and conv.weight.dtype == torch.float32 and conv.weight.shape[0] % 64 == 0)
+
+
+class StemConvFn(torch.autograd.Function):
+    """ResNet stem on the implicit-GEMM kernel: one launch packs the image to 4-channel
+    NHWC and the filter to the padded [K][8][8][4] space, one conv launch (+ the
+    following BN's statistics); backward = the weight gradient only."""
+
+    @staticmethod
+    def forward(ctx, x, weight, cdtype, bn):
+        N, _, H, W = x.shape
+        K = weight.shape[0]
+        x4 = torch.empty((N, 4, H, W), dtype=cdtype, device=x.device, memory_format=_CL)
+        w4 = torch.empty((K, 4, 8, 8), dtype=cdtype, device=x.device, memory_format=_CL)
+        _K().stem_pack(x.contiguous(), weight.contiguous(), x4, w4)
+        y, stats = conv_fwd(x4, w4, 2, 3, bn, mode=_K().MODE_STEM)
+        ctx.save_for_backward(x4)
+        ctx.wshape = tuple(weight.shape)
+        ctx.set_materialize_grads(False)
+        if stats is not None:
+            ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, dy, *_):
+        (x4,) = ctx.saved_tensors
+        if dy is None:
+            return None, None, None, None
+        dy = dy.to(x4.dtype)
+        dy = dy if dy.is_contiguous(memory_format=_CL) else dy.contiguous(memory_format=_CL)
+        K = ctx.wshape[0]
+        N, _, OH, OW = dy.shape
+        sp = int(_K().wgrad_splits(N * OH * OW, K, 4, 8, 8))
+        slab = _WgradWS.get(dy.device, sp * K * 256)
+        grad = torch.empty(ctx.wshape, dtype=torch.float32, device=dy.device)
+        _K().conv_wgrad(dy, x4, grad, 2, 3, slab, mode=_K().MODE_STEM)
+        return None, grad, None, None
+
+
+def stem_conv(x: torch.Tensor, conv, cdtype: torch.dtype, bn=None):
+    """(output channels_last in ``cdtype``, statistics of ``bn`` or None)."""
+    return StemConvFn.apply(x, conv.weight, cdtype, bn if (bn is not None and bn.training) else None)
 
 
 class _WgradWS:

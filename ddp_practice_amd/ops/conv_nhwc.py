@@ -6,8 +6,11 @@ copies per step: fp32->bf16 cast, NCHW->NHWC weight copy (MIOpen wants the
 weight in the activation's layout), and the bf16 NHWC weight gradient cast back
 to an fp32 NCHW ``.grad``.  Here the forward does the cast and the layout change
 in one copy and the backward one combined copy, straight into the fp32 gradient.
-Used by the ResNet-50 stress model (models/resnet.py) for its 16 3x3 convs and
-the 7x7 stem.
+Used by the ResNet-50 stress model (models/resnet.py) for its 16 3x3 convs: the
+hand-written implicit-GEMM kernel (ops/conv_igemm.py) takes every forward, weight
+gradient and data gradient (stride 1, and stride 2 as four parity sub-convolutions);
+MIOpen remains the fallback for shapes outside it.  The 7x7 stem has its own mode
+(ops/conv_igemm.stem_conv).
 """
 from __future__ import annotations
 
@@ -65,6 +68,14 @@ class ConvNHWCFn(torch.autograd.Function):
                 wt = torch.empty((w.shape[1], w.shape[0], R, R), dtype=w.dtype, device=w.device, memory_format=_CL)
                 wt.copy_(w.flip(2, 3).transpose(0, 1))
             dx, _ = _igemm.conv_fwd(dy, wt, 1, R - 1 - padding[0])
+        elif (ctx.needs_input_grad[0] and stride == [2, 2] and padding == [1, 1] and tuple(w.shape[2:]) == (3, 3)
+              and _igemm.usable(dy, w.transpose(0, 1), w.dtype)):
+            # stride-2 data gradient: four output-parity sub-convolutions in one launch
+            wt = ctx.wt
+            if wt is None:
+                wt = torch.empty((w.shape[1], w.shape[0], 3, 3), dtype=w.dtype, device=w.device, memory_format=_CL)
+                wt.copy_(w.flip(2, 3).transpose(0, 1))
+            dx = _igemm.dgrad_s2(dy, wt, tuple(x.shape[2:]))
         dw = None
         xc = x.to(w.dtype)
         if (ctx.needs_input_grad[1] and ctx.wdtype == torch.float32 and stride[0] == stride[1]

@@ -130,3 +130,89 @@ def test_conv1x1_tapped_dgrad_accumulates(C):
     y.backward(dy0.to(DEV, torch.bfloat16).contiguous(memory_format=CL))
     err = ((x.grad.float().cpu() - ref).abs().max() / ref.abs().max()).item()
     assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N,H", [(2, 32), (3, 23)])
+def test_stem_conv_fwd_wgrad(C, dtype, N, H):
+    """7x7 / stride-2 / pad-3 stem on the kernel's stem mode (4-channel NHWC image,
+    (r, s, c) K space padded to 8x8x4) == fp32 torch: output, BN statistics and the
+    weight gradient (the padded columns dropped)."""
+    from ddp_practice_amd.ops import conv_igemm as I
+
+    g = torch.Generator().manual_seed(5 + H)
+    x0 = torch.rand(N, 3, H, H, generator=g)
+    conv = torch.nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+    w0 = conv.weight.detach().clone()
+    wr = w0.clone().requires_grad_()
+    ref = F.conv2d(x0, wr, None, 2, 3)
+    dy0 = torch.randn(ref.shape, generator=g)
+    ref.backward(dy0)
+    conv = conv.to(DEV)
+    bn = torch.nn.BatchNorm2d(64).to(DEV)
+    assert I.stem_usable(x0.to(DEV), conv, dtype)
+    y, st = I.stem_conv(x0.to(DEV), conv, dtype, bn)
+    assert y.is_contiguous(memory_format=CL) and y.dtype == dtype
+    tol = 2e-2 if dtype == torch.bfloat16 else 4e-3
+    err = ((y.float().cpu() - ref.detach()).abs().max() / ref.detach().abs().max()).item()
+    assert err < tol, err
+    yr = y.float().permute(0, 2, 3, 1).reshape(-1, 64)
+    torch.testing.assert_close(st[:64], yr.sum(0), rtol=1e-4, atol=1e-2)
+    y.backward(dy0.to(DEV, dtype).contiguous(memory_format=CL))
+    err = ((conv.weight.grad.cpu() - wr.grad).abs().max() / wr.grad.abs().max()).item()
+    assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [(2, 64, 16, 16, 64), (2, 128, 14, 14, 192), (3, 64, 10, 10, 128)])
+def test_conv3x3_s2_dgrad(C, dtype, shape):
+    """Data gradient of a 3x3 / stride-2 conv as four output-parity sub-convolutions
+    (MODE_S2T) == fp32 torch autograd, through ops/conv_nhwc."""
+    from ddp_practice_amd.ops.conv_nhwc import conv_nhwc
+
+    N, Cin, H, W, K = shape
+    g = torch.Generator().manual_seed(17)
+    x0 = torch.randn(N, Cin, H, W, generator=g)
+    w0 = torch.randn(K, Cin, 3, 3, generator=g) / (Cin * 9) ** 0.5
+    xr = x0.clone().requires_grad_()
+    out = F.conv2d(xr, w0, None, 2, 1)
+    dy0 = torch.randn(out.shape, generator=g)
+    out.backward(dy0)
+    x = x0.to(DEV, dtype).contiguous(memory_format=CL).requires_grad_()
+    w = w0.to(DEV).requires_grad_()
+    y = conv_nhwc(x, w, (2, 2), (1, 1), dtype)
+    y.backward(dy0.to(DEV, dtype).contiguous(memory_format=CL))
+    err = ((x.grad.float().cpu() - xr.grad).abs().max() / xr.grad.abs().max()).item()
+    assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("stride,order", [(1, "ds_first"), (2, "ds_first"), (2, "conv1_first")])
+def test_projection_block_shared_input_grad(C, stride, order):
+    """A projection block's conv1 (stride 1) and downsample conv (stride s) share the
+    input gradient through one tap: the second backward folds the first's product into
+    its own (stride 2: added at the even pixels in the conv epilogue)."""
+    from ddp_practice_amd.ops.conv1x1 import GradTap, conv1x1
+
+    g = torch.Generator().manual_seed(23 + stride)
+    N, Cin, H, K1, Kd = 2, 128, 28, 64, 256
+    x0 = torch.randn(N, Cin, H, H, generator=g)
+    w1 = torch.randn(K1, Cin, 1, 1, generator=g) / Cin ** 0.5
+    wd = torch.randn(Kd, Cin, 1, 1, generator=g) / Cin ** 0.5
+    d1 = torch.randn(N, K1, H, H, generator=g)
+    dd = torch.randn(N, Kd, H // stride, H // stride, generator=g)
+    xr = x0.clone().requires_grad_()
+    (F.conv2d(xr, w1) * d1).sum().add((F.conv2d(xr, wd, stride=stride) * dd).sum()).backward()
+    x = x0.to(DEV, torch.bfloat16).contiguous(memory_format=CL).requires_grad_()
+    tap = GradTap()
+    y1 = conv1x1(x, w1.to(DEV), 1, torch.bfloat16, None, None, None, tap)
+    yd = conv1x1(x, wd.to(DEV), stride, torch.bfloat16, None, None, None, tap)
+    g1 = d1.to(DEV, torch.bfloat16).contiguous(memory_format=CL)
+    gd = dd.to(DEV, torch.bfloat16).contiguous(memory_format=CL)
+    # order the two backward nodes explicitly (autograd.backward of both outputs picks its own)
+    first, second = ((yd, gd), (y1, g1)) if order == "ds_first" else ((y1, g1), (yd, gd))
+    torch.autograd.backward([first[0]], [first[1]], retain_graph=True)
+    assert x.grad is None and tap.grad is not None
+    torch.autograd.backward([second[0]], [second[1]])
+    assert tap.grad is None
+    err = ((x.grad.float().cpu() - xr.grad).abs().max() / xr.grad.abs().max()).item()
+    assert err < 2e-2, err
