@@ -344,6 +344,8 @@ def run_rank(args) -> None:
     if args.impl == "native":
         model, optimizer, scaler = build(1)
         fused_grad = dist_path and amp is not None and model.defer_grad_sync_to(optimizer)
+        # no DDP: conv1's weight-gradient column sums run inside the fused AMP step (engine.TrainLoop does the same)
+        slab_sink = not dist_path and amp is not None and model.set_slab_sink(optimizer)
         sampler = DistributedSampler(train_ds, num_replicas=world, rank=rank)
         loader = DeviceLoader(train_ds, batch_size=B, sampler=sampler, device=dev, dtype=act)
         images, labels = loader.static_batch()

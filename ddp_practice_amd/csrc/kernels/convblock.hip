@@ -1,6 +1,4 @@
 // Host side of the fused conv-block kernels (device code: convblock_impl.h).
-#include <cstdlib>
-
 #include "convblock_impl.h"
 
 namespace dpa {
@@ -227,20 +225,6 @@ void slab_reduce(at::Tensor slab1, int64_t n1, at::Tensor out1, c10::optional<at
     rows2 = (int)(slab2->numel() / n2);
   } else {
     n2 = 0;
-  }
-  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  const bool vec = n1 % 4 == 0 && n2 % 4 == 0 && al16(slab1.data_ptr()) && al16(out1.data_ptr()) &&
-                   (!slab2.has_value() || (al16(slab2->data_ptr()) && al16(out2->data_ptr())));
-  static const bool scalar_only = std::getenv("DPA_SLAB_SCALAR") != nullptr;  // A/B runs
-  if (vec && !scalar_only) {
-    const int64_t nb = (n1 / 4 + SRV_Q - 1) / SRV_Q + (n2 / 4 + SRV_Q - 1) / SRV_Q;
-    if (nb == 0) return;
-    hipLaunchKernelGGL(slab_reduce4_kernel, dim3(nb), dim3(NTHR), 0, cur_stream(),
-                       slab1.data_ptr<float>(), rows1, (int)n1, out1.data_ptr<float>(),
-                       slab2.has_value() ? slab2->data_ptr<float>() : nullptr, rows2, (int)n2,
-                       out2.has_value() ? out2->data_ptr<float>() : nullptr);
-    DPA_CHECK_LAUNCH();
-    return;
   }
   const int64_t nblk = (n1 + SR_COLS - 1) / SR_COLS + (n2 + SR_COLS - 1) / SR_COLS;
   if (nblk == 0) return;

@@ -1473,17 +1473,17 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
 // (independent loads in flight), then combine through LDS.
 // ---------------------------------------------------------------------------
 constexpr int SR_COLS = 16, SR_GROUPS = NTHR / SR_COLS;
-static __global__ void __launch_bounds__(NTHR)
-slab_reduce_kernel(const float* __restrict__ slab1, int rows1, int n1, float* __restrict__ out1,
-                   const float* __restrict__ slab2, int rows2, int n2, float* __restrict__ out2) {
+__device__ __forceinline__ void slab_reduce_body(const float* __restrict__ slab1, int rows1, int n1,
+                                                 float* __restrict__ out1, const float* __restrict__ slab2, int rows2,
+                                                 int n2, float* __restrict__ out2, int bid) {
   __shared__ float part[SR_GROUPS][SR_COLS + 1];
   const int nb1 = (n1 + SR_COLS - 1) / SR_COLS;
-  const bool first = (int)blockIdx.x < nb1;
+  const bool first = bid < nb1;
   const float* slab = first ? slab1 : slab2;
   const int rows = first ? rows1 : rows2;
   const int n = first ? n1 : n2;
   float* out = first ? out1 : out2;
-  const int c0 = (first ? blockIdx.x : blockIdx.x - nb1) * SR_COLS;
+  const int c0 = (first ? bid : bid - nb1) * SR_COLS;
   const int col = c0 + (threadIdx.x % SR_COLS), g = threadIdx.x / SR_COLS;
   // 8 then 4 independent row loads in flight per round trip (conv2's 128 slab rows:
   // one round trip per lane; conv1's 224: three)
@@ -1509,43 +1509,10 @@ slab_reduce_kernel(const float* __restrict__ slab1, int rows1, int n1, float* __
     out[c0 + threadIdx.x] = t;
   }
 }
-
-// The same sums with float4 column quads (every n % 4 == 0, 16-B aligned slabs and
-// outputs; checked on the host): a workgroup owns 64 columns as 16 quads x 16 row
-// groups, so the ConvNet's two slabs (416 + 12,832 columns) take 208 workgroups --
-// one residency round on 256 CUs -- instead of 828 scalar-column workgroups.
-constexpr int SRV_Q = 16, SRV_GROUPS = NTHR / SRV_Q;
 static __global__ void __launch_bounds__(NTHR)
-slab_reduce4_kernel(const float* __restrict__ slab1, int rows1, int n1, float* __restrict__ out1,
-                    const float* __restrict__ slab2, int rows2, int n2, float* __restrict__ out2) {
-  __shared__ f32x4 part[SRV_GROUPS][SRV_Q];
-  const int nb1 = (n1 / 4 + SRV_Q - 1) / SRV_Q;
-  const bool first = (int)blockIdx.x < nb1;
-  const f32x4* slab = reinterpret_cast<const f32x4*>(first ? slab1 : slab2);
-  const int rows = first ? rows1 : rows2;
-  const int nq = (first ? n1 : n2) / 4;
-  f32x4* out = reinterpret_cast<f32x4*>(first ? out1 : out2);
-  const int q0 = (first ? blockIdx.x : blockIdx.x - nb1) * SRV_Q;
-  const int q = q0 + (threadIdx.x % SRV_Q), g = threadIdx.x / SRV_Q;
-  f32x4 a[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) a[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (q < nq) {
-    int rr = g;
-    for (; rr + 7 * SRV_GROUPS < rows; rr += 8 * SRV_GROUPS) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] += slab[(size_t)(rr + j * SRV_GROUPS) * nq + q];
-    }
-    for (; rr < rows; rr += SRV_GROUPS) a[0] += slab[(size_t)rr * nq + q];
-  }
-  part[g][threadIdx.x % SRV_Q] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-  __syncthreads();
-  if (threadIdx.x < SRV_Q && q0 + (int)threadIdx.x < nq) {
-    f32x4 t = part[0][threadIdx.x];
-#pragma unroll
-    for (int gg = 1; gg < SRV_GROUPS; ++gg) t += part[gg][threadIdx.x];
-    out[q0 + threadIdx.x] = t;
-  }
+slab_reduce_kernel(const float* __restrict__ slab1, int rows1, int n1, float* __restrict__ out1,
+                   const float* __restrict__ slab2, int rows2, int n2, float* __restrict__ out2) {
+  slab_reduce_body(slab1, rows1, n1, out1, slab2, rows2, n2, out2, (int)blockIdx.x);
 }
 
 }  // namespace cb

@@ -701,6 +701,50 @@ void wgrad1_reduce(at::Tensor x, at::Tensor y1, at::Tensor dp1, at::Tensor idx1,
   DPA_CHECK_LAUNCH();
 }
 
+// BN1 bwd -> conv1 weight-grad partial rows (wslab1) AND, in extra workgroups, the
+// column sums of the conv2 weight-grad slab into [dW2 | db2] (independent work that
+// fills the CUs the 224 conv1 workgroups leave idle).  The conv1 slab's own column
+// sums are left to the consumer: the fused AMP-SGD launch (optim.hip SlabSrc) or a
+// slab_reduce launch.
+template <typename T>
+__global__ void __launch_bounds__(cb::NTHR)
+wgrad1_slab2_kernel(const T* __restrict__ x, float* __restrict__ wslab1, BwdIn<T> bi, int nwg1,
+                    const float* __restrict__ wslab2, int rows2, int n2, float* __restrict__ out2) {
+  constexpr int ns = (28 + WG1_ROWS_ - 1) / WG1_ROWS_;
+  if ((int)blockIdx.x < nwg1)
+    cb::conv5x5_wgrad_body<T, 1, 16, 28, 28, WG1_ROWS_, 2>(x, nullptr, wslab1, ns, bi, (int)blockIdx.x);
+  else
+    cb::slab_reduce_body(nullptr, 0, 0, nullptr, wslab2, rows2, n2, out2, (int)blockIdx.x - nwg1);
+}
+
+void conv1_wgrad_slab2(at::Tensor x, at::Tensor y1, at::Tensor dp1, at::Tensor idx1, at::Tensor fstats1,
+                       at::Tensor gsum, c10::optional<at::Tensor> lsum, at::Tensor g1, double eps1, at::Tensor dg1,
+                       at::Tensor dbe1, at::Tensor wslab1, at::Tensor wslab2, at::Tensor out2, XcPtr xc) {
+  DPA_CHECK_INPUT(x); DPA_CHECK_INPUT(y1); DPA_CHECK_INPUT(wslab1); DPA_CHECK_INPUT(wslab2); DPA_CHECK_INPUT(out2);
+  const int B = (int)y1.size(0);
+  TORCH_CHECK(x.size(1) == 1 && y1.size(1) == 16 && y1.size(2) == 28 && x.scalar_type() == y1.scalar_type());
+  const int nwg1 = (int)wgrad_bn_rows(1, B);
+  constexpr int N1 = 16 * 25 + 16, N2 = 32 * 400 + 32;
+  const int rows2 = (int)wgrad_bn_rows(2, B);
+  TORCH_CHECK(wslab1.numel() == (int64_t)nwg1 * N1, "conv1_wgrad_slab2: conv1 slab size");
+  TORCH_CHECK(wslab2.numel() == (int64_t)rows2 * N2 && out2.numel() == N2, "conv1_wgrad_slab2: conv2 slab sizes");
+  if (B == 0) return;
+  const int nred = (N2 + cb::SR_COLS - 1) / cb::SR_COLS;
+  with_t(dt_of(y1), [&](auto tag) {
+    typedef decltype(tag) T;
+    BwdIn<T> bi = bwd_in<T>(dp1, idx1, y1, fstats1, gsum, lsum, g1, eps1, 16, dg1, dbe1);
+    if (xc) {
+      TORCH_CHECK(!lsum.has_value(), "fused SyncBN exchange: gsum must be this rank's rows (no lsum)");
+      bi.xs = site_of(xc, xgmi::kSiteBwd1);
+      bi.xs.nblk = nwg1;  // the reduction workgroups take no tickets
+    }
+    hipLaunchKernelGGL(wgrad1_slab2_kernel<T>, dim3(nwg1 + nred), dim3(cb::NTHR), 0, cur_stream(), dptr<T>(x),
+                       wslab1.data_ptr<float>(), bi, nwg1, wslab2.data_ptr<float>(), rows2, N2,
+                       out2.data_ptr<float>());
+  });
+  DPA_CHECK_LAUNCH();
+}
+
 // Whether every launch that exchanges SyncBN sums in-kernel (comm/xsite.h: all
 // of its workgroups poll the peers' rows) is co-resident at batch B; if not,
 // ops/convnet_fused.py all-reduces between the launches instead.
@@ -720,6 +764,7 @@ bool sites_resident(int64_t B, at::ScalarType st) {
     chk(reinterpret_cast<const void*>(&cb::conv5x5_wgrad_kernel<T, 1, 16, 28, 28, WG1_ROWS, 2>),
         wgrad_bn_rows(1, B));
     chk(reinterpret_cast<const void*>(&wgrad1_reduce_kernel<T>), wgrad_bn_rows(1, B));
+    chk(reinterpret_cast<const void*>(&wgrad1_slab2_kernel<T>), wgrad_bn_rows(1, B));
   });
   return ok;
 }
@@ -758,6 +803,7 @@ void register_convnet_fused(pybind11::module& m) {
   s.def("wgrad_bn_rows", &cnf::wgrad_bn_rows);
   s.def("sites_resident", &cnf::sites_resident);
   s.def("wgrad1_reduce", &cnf::wgrad1_reduce);
+  s.def("conv1_wgrad_slab2", &cnf::conv1_wgrad_slab2);
   s.def("wgrad1_counters", &cnf::wgrad1_counters);
 }
 

@@ -163,12 +163,27 @@ constexpr int64_t FUSED_MAX = (int64_t)FUSED_MAX_BLOCKS * FUSED_BLOCK_GRAN * 4;
 // sums the W ranks' values in rank order and divides by W before the inf check
 // -- the reducer launched no collective for these buckets.  U = 1 granule per
 // lane then (one poll round trip of W x 4 granules per lane, 4x the workgroups).
+//
+// SlabSrc (optional, not with XG): one gradient region [out, out + n) is still the
+// per-workgroup partial rows of a producer (slab [rows][n], e.g. the ConvNet's conv1
+// weight-gradient slab): nblk extra workgroups, appended after the granule grid, sum
+// its columns (16 columns x 16 row groups each, fixed order), check them, write them to
+// `out` write-through and arrive at the grid barrier like the others; the granules
+// inside the region are read (agent scope) only after the barrier.  The separate
+// column-sum launch disappears.
+struct SlabSrc {
+  const float* slab;
+  float* out;
+  int rows, n, nblk;
+};
+constexpr int SS_COLS = 16, SS_GROUPS = FUSED_THR / SS_COLS;
+
 template <int U, bool XG, int THR = FUSED_THR>
 __global__ void __launch_bounds__(THR)
 amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ tracker, float* __restrict__ found_inf,
                      unsigned long long* __restrict__ sync, float lr, float momentum, float dampening, float wd,
                      int nesterov, int maximize, float growth, float backoff, int interval,
-                     xgmi::XSite xg, int* __restrict__ err, long long barrier_ticks) {
+                     xgmi::XSite xg, int* __restrict__ err, long long barrier_ticks, SlabSrc ss) {
   constexpr int BG = THR * U;  // float4 granules per workgroup
   __shared__ int soff[MAXT + 1];
   __shared__ int snum[MAXT];
@@ -207,22 +222,62 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
   f32x4 gv[U], pv[U], bv[U];
   int tt[U];  // tensor of each granule (its offset is recomputed after the barrier)
   bool bad = false;
+  const int nreg = (int)gridDim.x - ss.nblk;  // granule workgroups; the rest reduce the slab
+  unsigned defer = 0;                          // granules whose gradient the slab workgroups produce
+  if ((int)blockIdx.x >= nreg) {
+    __shared__ float spart[SS_GROUPS][SS_COLS + 1];
+    const int c0 = ((int)blockIdx.x - nreg) * SS_COLS;
+    const int col = c0 + tid % SS_COLS, g = tid / SS_COLS;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (col < ss.n) {
+      int r = g;
+      // the association of cb::slab_reduce_body (bitwise the same sums as that launch)
+      for (; r + 7 * SS_GROUPS < ss.rows; r += 8 * SS_GROUPS) {
 #pragma unroll
-  for (int k = 0; k < U; ++k) {
-    const int gi = blockIdx.x * BG + k * THR + tid;
-    tt[k] = -1;
-    if (gi < total) {
-      int lo = 0, hi = n - 1;  // tensor holding granule gi
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (soff[mid] <= gi) lo = mid; else hi = mid - 1;
+        for (int j = 0; j < 8; ++j) a[j] += ss.slab[(size_t)(r + j * SS_GROUPS) * ss.n + col];
       }
-      const int o = (gi - soff[lo]) * 4, rem = snum[lo] - o;
-      tt[k] = lo;
-      gv[k] = load4(sp1[lo] + o, rem);
-      pv[k] = load4(sp0[lo] + o, rem);
-      const bool use_buf = momentum != 0.f && !((L.first_bits >> lo) & 1ull);
-      bv[k] = use_buf ? load4(sp2[lo] + o, rem) : f32x4{0.f, 0.f, 0.f, 0.f};
+      for (; r + 3 * SS_GROUPS < ss.rows; r += 4 * SS_GROUPS) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] += ss.slab[(size_t)(r + j * SS_GROUPS) * ss.n + col];
+      }
+      for (; r < ss.rows; r += SS_GROUPS) a[0] += ss.slab[(size_t)r * ss.n + col];
+    }
+    spart[g][tid % SS_COLS] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    __syncthreads();
+    if (tid < SS_COLS && c0 + tid < ss.n) {
+      float t = 0.f;
+#pragma unroll
+      for (int gg = 0; gg < SS_GROUPS; ++gg) t += spart[gg][tid];
+      bad = !isfinite(t);
+      __hip_atomic_store(ss.out + c0 + tid, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sums have left the CU before the arrival
+#pragma unroll
+    for (int k = 0; k < U; ++k) tt[k] = -1;
+  } else {
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int gi = blockIdx.x * BG + k * THR + tid;
+      tt[k] = -1;
+      if (gi < total) {
+        int lo = 0, hi = n - 1;  // tensor holding granule gi
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (soff[mid] <= gi) lo = mid; else hi = mid - 1;
+        }
+        const int o = (gi - soff[lo]) * 4, rem = snum[lo] - o;
+        tt[k] = lo;
+        const float* gp = sp1[lo] + o;
+        if (!XG && gp >= ss.out && gp < ss.out + ss.n) {
+          defer |= 1u << k;
+          gv[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        } else {
+          gv[k] = load4(gp, rem);
+        }
+        pv[k] = load4(sp0[lo] + o, rem);
+        const bool use_buf = momentum != 0.f && !((L.first_bits >> lo) & 1ull);
+        bv[k] = use_buf ? load4(sp2[lo] + o, rem) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
   }
   if constexpr (XG) {
@@ -324,6 +379,11 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
     const int t = tt[k];
     if (t < 0) continue;
     const int o = (blockIdx.x * BG + k * THR + tid - soff[t]) * 4, rem = snum[t] - o;
+    if ((defer >> k) & 1u) {  // produced by the slab workgroups before they arrived
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        gv[k][j] = j < rem ? __hip_atomic_load(sp1[t] + o + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+    }
     const f32x4 g = gv[k] * inv;
     store4(sp1[t] + o, rem, g);
     if (any_bad) continue;
@@ -664,7 +724,7 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
                    double lr, double momentum, double dampening, double wd, bool nesterov, bool maximize,
                    std::vector<int64_t> first, at::Tensor scale, at::Tensor tracker, at::Tensor found_inf,
                    double growth, double backoff, int64_t interval, at::Tensor sync,
-                   std::shared_ptr<xgmi::XgmiComm> xc) {
+                   std::shared_ptr<xgmi::XgmiComm> xc, c10::optional<at::Tensor> slab, c10::optional<at::Tensor> slab_out) {
   TORCH_CHECK(params.size() == grads.size() && params.size() <= (size_t)MAXT, "fused AMP-SGD: <= ", MAXT,
               " tensors");
   TORCH_CHECK(bufs.empty() || bufs.size() == params.size());
@@ -691,15 +751,36 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
     TORCH_CHECK(al(L.p0[i]) && al(L.p1[i]) && al(L.p2[i]), "fused AMP-SGD needs 16-byte aligned tensors");
   }
   TORCH_CHECK(L.chunk_off[L.n] * 4 <= FUSED_MAX, "fused AMP-SGD handles at most ", FUSED_MAX, " elements");
+  SlabSrc ss{nullptr, nullptr, 0, 0, 0};
+  TORCH_CHECK(slab.has_value() == slab_out.has_value(), "fused AMP-SGD: slab and slab_out go together");
+  if (slab.has_value()) {
+    TORCH_CHECK(!xc, "fused AMP-SGD: a slab-sourced gradient cannot be exchanged in-kernel");
+    check_f32(*slab); check_f32(*slab_out);
+    const int64_t ncol = slab_out->numel();
+    TORCH_CHECK(ncol > 0 && slab->numel() % ncol == 0, "fused AMP-SGD: slab must be [rows][slab_out.numel()]");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(slab_out->data_ptr()) & 15) == 0, "fused AMP-SGD: slab_out alignment");
+    // the region must start and end on granule boundaries of the tensors that cover it
+    const float* lo = slab_out->data_ptr<float>();
+    const float* hi = lo + ncol;
+    for (int i = 0; i < L.n; ++i) {
+      const float* a = L.p1[i];
+      const float* b = a + L.numel[i];
+      if (b <= lo || a >= hi) continue;
+      TORCH_CHECK(a >= lo && b <= hi && (L.numel[i] % 4 == 0 || b == hi),
+                  "fused AMP-SGD: every gradient overlapping slab_out must lie inside it, in whole granules");
+    }
+    ss = SlabSrc{slab->data_ptr<float>(), slab_out->data_ptr<float>(), (int)(slab->numel() / ncol), (int)ncol,
+                 (int)((ncol + SS_COLS - 1) / SS_COLS)};
+  }
   auto launch = [&](auto kern, int bg, xgmi::XSite xg) {
-    const int grid = (int)std::max<int64_t>(1, (L.chunk_off[L.n] + bg - 1) / bg);
+    const int grid = (int)std::max<int64_t>(1, (L.chunk_off[L.n] + bg - 1) / bg) + ss.nblk;
     TORCH_CHECK(grid <= FUSED_MAX_BLOCKS, "fused AMP-SGD: grid exceeds the co-resident bound");
     hipLaunchKernelGGL(kern, dim3(grid), dim3(FUSED_THR), 0, cur_stream(), L, scale.data_ptr<float>(),
                        tracker.data_ptr<int>(), found_inf.data_ptr<float>(),
                        reinterpret_cast<unsigned long long*>(sync.data_ptr<int64_t>()), (float)lr, (float)momentum,
                        (float)dampening, (float)wd, (int)nesterov, (int)maximize, (float)growth, (float)backoff,
                        (int)interval, xg, reinterpret_cast<int*>(sync.data_ptr<int64_t>() + 3),
-                       (long long)(kBarrierSeconds * 1e8));
+                       (long long)(kBarrierSeconds * 1e8), ss);
   };
   if (xc) {
     const xgmi::XSite xg = xc->grad_site();
@@ -843,7 +924,12 @@ void register_optim(pybind11::module& m) {
         pybind11::arg("nesterov"), pybind11::arg("maximize"), pybind11::arg("first") = std::vector<int64_t>{},
         pybind11::arg("found_inf") = pybind11::none(), pybind11::arg("grad_scale") = pybind11::none());
   s.def("update_scale", &opt::update_scale);
-  s.def("amp_sgd_fused", &opt::amp_sgd_fused);
+  s.def("amp_sgd_fused", &opt::amp_sgd_fused, pybind11::arg("params"), pybind11::arg("grads"), pybind11::arg("bufs"),
+        pybind11::arg("lr"), pybind11::arg("momentum"), pybind11::arg("dampening"), pybind11::arg("wd"),
+        pybind11::arg("nesterov"), pybind11::arg("maximize"), pybind11::arg("first"), pybind11::arg("scale"),
+        pybind11::arg("tracker"), pybind11::arg("found_inf"), pybind11::arg("growth"), pybind11::arg("backoff"),
+        pybind11::arg("interval"), pybind11::arg("sync"), pybind11::arg("xc"),
+        pybind11::arg("slab") = pybind11::none(), pybind11::arg("slab_out") = pybind11::none());
   s.def("amp_sgd_xg_max", &opt::amp_sgd_xg_max);
   s.def("amp_sgd_resident", &opt::amp_sgd_resident);
   s.def("amp_sgd_table", &opt::amp_sgd_table, pybind11::arg("params"), pybind11::arg("grads"), pybind11::arg("bufs"),

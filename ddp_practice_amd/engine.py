@@ -82,6 +82,9 @@ class TrainLoop:
         # (parallel/ddp.py defer_grad_sync_to; a no-op without the engine)
         if scaler is not None and getattr(scaler, "_enabled", False) and hasattr(model, "defer_grad_sync_to"):
             model.defer_grad_sync_to(optimizer)
+        elif scaler is not None and getattr(scaler, "_enabled", False) and hasattr(model, "set_slab_sink"):
+            # no DDP: the fused AMP step also sums the conv1 weight-gradient slab (models/convnet.py)
+            model.set_slab_sink(optimizer)
         self.global_step = 0
         # the model's first kernel gathers the batch itself (no gather launch per step)
         from .data.loader import accepts_deferred
@@ -102,6 +105,9 @@ class TrainLoop:
             with trace_range("backward"):
                 self.scaler.scale(loss).backward()
             if before_update is not None:
+                flush = getattr(self.optimizer, "_flush_deferred", None)
+                if flush is not None:
+                    flush()  # the hook reads .grad
                 before_update()
             with trace_range("optimizer"):
                 self.scaler.step(self.optimizer)

@@ -22,6 +22,8 @@ reference's AMP default, ``torch.bfloat16`` = this framework's AMP default.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -100,6 +102,16 @@ class ConvNet(nn.Module):
 
         want = self.amp_dtype if self.amp_dtype is not None else torch.float32
         return x.dtype == want and x.is_contiguous() and self._native_ok(x) and convnet_fused.supported(self, x)
+
+    def set_slab_sink(self, optimizer) -> bool:
+        """Let ``optimizer`` (optim.SGD) sum the conv1 weight-gradient partial rows inside
+        its fused AMP step instead of a separate column-sum launch (ops/convnet_fused.py).
+        Only for a model that is not wrapped by DDP (whose reducer reads ``.grad`` in its
+        autograd hooks); engine.TrainLoop enables it.  Returns whether it was enabled."""
+        if not hasattr(optimizer, "defer_slab") or os.environ.get("DPA_SLAB_SINK", "1") == "0":
+            return False
+        self._dpa_slab_sink = optimizer
+        return True
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if getattr(x, "_dpa_gather", None) is not None and not (self.training and self.accepts_deferred_batch(x)):

@@ -54,6 +54,8 @@ def supported(model, x: torch.Tensor) -> bool:
 _RESIDENT: dict = {}
 _SPLIT_BWD2 = os.environ.get("DPA_SPLIT_BWD2", "0") == "1"
 _SPLIT_WGRAD1 = os.environ.get("DPA_SPLIT_WGRAD1", "1") == "1"  # merged launch measured slower (15.0 vs 10.9 us)
+# conv1 wgrad + conv2 slab sums in one launch even without a slab sink (A/B; then a conv1-only sum launch)
+_WGRAD1_SLAB2 = os.environ.get("DPA_WGRAD1_SLAB2", "0") == "1"
 
 
 def _fused_site_engine(comm, batch: int, dtype: torch.dtype):
@@ -107,7 +109,7 @@ def _head_step_ok(B: int, N: int, dtype: torch.dtype) -> bool:
 class ConvNetFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, b1, g1, be1, w2, b2, g2, be2, wfc, bfc, bufs, training, moms, epss, comm, cdtype,
-                labels=None, ce_cfg=(-100, 0.0), holder=None, state=None, gather=None, wcnt=None):
+                labels=None, ce_cfg=(-100, 0.0), holder=None, state=None, gather=None, wcnt=None, sink=None):
         cb, cn = _mods()
         rm1, rv1, nbt1, rm2, rv2, nbt2 = bufs
         m1, m2 = (-1.0 if m is None else float(m) for m in moms)
@@ -195,6 +197,8 @@ class ConvNetFn(torch.autograd.Function):
                         None, None)
         ctx.training = training
         ctx.wcnt = wcnt
+        ctx.sink = sink
+        ctx.w1b1 = (w1, b1) if sink is not None else None
         ctx.sync = sync
         ctx.comm = comm
         ctx.xc = xc
@@ -258,7 +262,24 @@ class ConvNetFn(torch.autograd.Function):
         else:
             gsum1, lsum1, xc1 = bslab1, None, xc
         out1, out2 = out.narrow(0, 0, n_w1 + 16), out.narrow(0, n_w1 + 48, n_w2 + 32)
-        if _SPLIT_WGRAD1 or ctx.wcnt is None:
+        sink = ctx.sink
+        if sink is not None:
+            sink.flush_slab()  # an earlier backward's sums first (they may be accumulated into)
+            # [dW1 | db1] is left to the optimizer's fused step only when autograd will hand
+            # these views to .grad as they are (no accumulation into an existing .grad)
+            if any(p.grad is not None for p in ctx.w1b1):
+                sink = None
+        ctx.w1b1 = None
+        if sink is not None or _WGRAD1_SLAB2:
+            # conv1 wgrad partials + the conv2 slab's column sums in one launch; the conv1
+            # slab's sums run inside the fused AMP-SGD launch (optim.SGD.defer_slab) or next
+            cn.conv1_wgrad_slab2(x, y1, dp1, idx1, fstats1, gsum1, lsum1, g1, e1, dg1, dbe1, wslab1, wslab2, out2,
+                                 xc1)
+            if sink is not None:
+                sink.defer_slab(wslab1, out1)
+            else:
+                cb.slab_reduce(wslab1, n_w1 + 16, out1)
+        elif _SPLIT_WGRAD1 or ctx.wcnt is None:
             cn.conv_wgrad_bn(x, y1, dp1, idx1, fstats1, gsum1, lsum1, g1, e1, dg1, dbe1, wslab1, xc1)
             cb.slab_reduce(wslab1, n_w1 + 16, out1, wslab2, n_w2 + 32, out2)
         else:
@@ -267,7 +288,7 @@ class ConvNetFn(torch.autograd.Function):
             cn.wgrad1_reduce(x, y1, dp1, idx1, fstats1, gsum1, lsum1, g1, e1, dg1, dbe1, wslab1, gslab1, out1,
                              wslab2, out2, cnt, xc1)
         return (None, dw1.view(s_w1), db1, dg1, dbe1, dw2.view(s_w2), db2, dg2, dbe2, dwfc.view(s_wfc), dbfc,
-                None, None, None, None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None, None, None)
 
 
 def convnet_forward(model, x, comm=None, cdtype=None):
@@ -320,7 +341,8 @@ def convnet_forward(model, x, comm=None, cdtype=None):
             model._dpa_wgrad_cnt = wcnt
     out = ConvNetFn.apply(x, c1.weight, c1.bias, bn1.weight, bn1.bias, c2.weight, c2.bias, bn2.weight, bn2.bias,
                           fc.weight, fc.bias, bufs, training, (bn1.momentum, bn2.momentum), (bn1.eps, bn2.eps),
-                          comm, cdtype, labels, (-100, 0.0), holder, state, gather, wcnt)
+                          comm, cdtype, labels, (-100, 0.0), holder, state, gather, wcnt,
+                          getattr(model, "_dpa_slab_sink", None) if training else None)
     if holder:
         out._dpa_pre_ce = holder.get("ce")
     return out

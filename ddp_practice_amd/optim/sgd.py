@@ -48,8 +48,23 @@ class SGD(Optimizer):
                         nesterov=nesterov, maximize=maximize)
         super().__init__(params, defaults)
 
+    def defer_slab(self, slab: torch.Tensor, out: torch.Tensor) -> None:
+        """A gradient region ``out`` that is still the partial rows ``slab`` [rows][out.numel()]
+        of its producer (the ConvNet's conv1 weight gradient, ops/convnet_fused.py): the next
+        fused AMP step sums the columns inside its own launch (csrc/kernels/optim.hip
+        SlabSrc); any other gradient reader flushes first (``_flush_deferred``)."""
+        self.flush_slab()
+        self._pending_slab = (slab, out)
+
+    def flush_slab(self) -> None:
+        ps = self.__dict__.pop("_pending_slab", None)
+        if ps is not None:
+            _load_ext().convblock.slab_reduce(ps[0], ps[1].numel(), ps[1])
+
     def _flush_deferred(self):
-        """Average gradients a DDP reducer left to this optimizer (DDP.defer_grad_sync_to)."""
+        """Average gradients a DDP reducer left to this optimizer (DDP.defer_grad_sync_to)
+        and sum a deferred gradient slab (defer_slab)."""
+        self.flush_slab()
         d = getattr(self, "_deferred_ddp", None)
         if d is not None:
             d[0].flush_deferred()
@@ -179,9 +194,13 @@ class SGD(Optimizer):
         # gradients a DDP reducer deferred to this step are averaged inside the kernel
         d = getattr(self, "_deferred_ddp", None)
         xc = d[1] if d is not None and d[0].deferred_pending() else None
+        if xc is not None:
+            self.flush_slab()
+        ps = self.__dict__.pop("_pending_slab", None)  # summed inside the launch (SlabSrc)
         O.amp_sgd_fused(params, grads, bufs, group["lr"], group["momentum"], group["dampening"],
                         group["weight_decay"], group["nesterov"], group["maximize"], first,
-                        scale, tracker, found_inf, growth, backoff, interval, sync, xc)
+                        scale, tracker, found_inf, growth, backoff, interval, sync, xc,
+                        ps[0] if ps is not None else None, ps[1] if ps is not None else None)
         if xc is not None:
             d[0].consume_deferred()
 

@@ -283,3 +283,90 @@ def test_deferred_gather_in_conv1(C, dtype):
         assert torch.equal(xa, xb) and torch.equal(ya, yb)
     for k in sd_a:
         torch.testing.assert_close(sd_a[k].float(), sd_b[k].float(), rtol=1e-5, atol=1e-6, msg=k)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_slab_sink_matches_separate_sums(C, dtype):
+    """conv1's weight-gradient column sums inside the fused AMP-SGD launch (SGD.defer_slab,
+    csrc/kernels/optim.hip SlabSrc) + conv2's inside the conv1 wgrad launch == the separate
+    column-sum launch, bitwise, eagerly and graph-replayed; no slab_reduce launch is left
+    once the fused step runs, and a .grad reader (unscale_) still sees the summed values."""
+    from ddp_practice_amd.amp import GradScaler
+    from ddp_practice_amd.data import DeviceLoader, synthetic
+    from ddp_practice_amd.nn import CrossEntropyLoss
+    from ddp_practice_amd.optim import SGD
+    from ddp_practice_amd.runtime import CapturedStep
+
+    ds = synthetic(32 * 12, seed=4)
+    runs = []
+    orig = C.convblock.slab_reduce
+    for sink in (False, True):
+        m = _model()
+        m.amp_dtype = dtype
+        loader = DeviceLoader(ds, batch_size=32, shuffle=False, device=DEV, dtype=dtype)
+        images, labels = loader.static_batch()
+        opt, scaler, crit = SGD(m.parameters(), lr=0.05), GradScaler(), CrossEntropyLoss()
+        if sink:
+            assert m.set_slab_sink(opt)
+        calls = [0]
+
+        def spy(*a, **k):
+            calls[0] += 1
+            return orig(*a, **k)
+
+        def step():
+            loader.fill_(images, labels, defer=True)
+            loss = crit(m(images), labels)
+            opt.zero_grad(set_to_none=True)
+            scaler.scale(loss).backward()
+            scaler.step(opt)
+            scaler.update()
+
+        C.convblock.slab_reduce = spy
+        try:
+            loader.start_epoch()
+            step()  # the first step is unfused: unscale_ flushes the deferred sums
+            calls[0] = 0
+            for _ in range(2):
+                step()
+            eager_calls = calls[0]
+            runner = CapturedStep(step, warmup=1, steps_per_graph=2)
+            assert runner.capture()
+            for _ in range(3):
+                runner.run()
+        finally:
+            C.convblock.slab_reduce = orig
+        torch.cuda.synchronize()
+        assert "_pending_slab" not in opt.__dict__
+        runs.append((copy.deepcopy(m.state_dict()), eager_calls))
+    (sd_a, calls_a), (sd_b, calls_b) = runs
+    assert calls_a == 2 and calls_b == 0, (calls_a, calls_b)
+    for k in sd_a:
+        assert torch.equal(sd_a[k], sd_b[k]), k
+
+
+def test_slab_sink_flushes_for_grad_readers(C):
+    """With a slab sink, .grad read through GradScaler.unscale_ (or accumulated over two
+    backward passes) equals the no-sink gradients."""
+    from ddp_practice_amd.amp import GradScaler
+    from ddp_practice_amd.nn import CrossEntropyLoss
+    from ddp_practice_amd.optim import SGD
+
+    g = torch.Generator(device="cpu").manual_seed(9)
+    x = torch.rand(32, 1, 28, 28, generator=g).to(DEV, torch.bfloat16)
+    y = torch.randint(0, 10, (32,), generator=g).to(DEV)
+    grads = []
+    for sink in (False, True):
+        m = _model()
+        m.amp_dtype = torch.bfloat16
+        opt, scaler, crit = SGD(m.parameters(), lr=0.05), GradScaler(), CrossEntropyLoss()
+        if sink:
+            m.set_slab_sink(opt)
+        opt.zero_grad(set_to_none=True)
+        for _ in range(2):  # two backward passes accumulate into .grad
+            scaler.scale(crit(m(x), y)).backward()
+        scaler.unscale_(opt)
+        torch.cuda.synchronize()
+        grads.append([p.grad.clone() for p in m.parameters()])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
