@@ -245,4 +245,24 @@ inline bool co_resident(const void* kernel, int grid, int threads, size_t lds = 
   return (long long)grid <= (long long)eff * cus;
 }
 
+// Column `col` of a [rows][n] slab summed over rows g, g + G, g + 2G, ... in that order.
+// Up to 16 rows per lane are loaded in ONE batch (clamped addresses, every load in flight
+// before the first add; the surplus is dropped by a select on registers), so a lane
+// costs one memory round trip for the ConvNet's 224- and 128-row slabs.  Shared by the
+// column-sum launch and the fused AMP-SGD SlabSrc workgroups (csrc/kernels/optim.hip):
+// both produce bitwise the same sums.
+template <int G>
+__device__ __forceinline__ float slab_colsum(const float* __restrict__ slab, int rows, int n, int col, int g) {
+  if (rows <= 0 || n <= 0) return 0.f;
+  const int cc = col < n ? col : n - 1;
+  float v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) v[j] = slab[(size_t)min(g + j * G, rows - 1) * n + cc];
+  float a = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a += (g + j * G < rows) ? v[j] : 0.f;
+  for (int r = g + 16 * G; r < rows; r += G) a += slab[(size_t)r * n + cc];
+  return col < n ? a : 0.f;
+}
+
 }  // namespace dpa

@@ -1485,22 +1485,7 @@ __device__ __forceinline__ void slab_reduce_body(const float* __restrict__ slab1
   float* out = first ? out1 : out2;
   const int c0 = (first ? bid : bid - nb1) * SR_COLS;
   const int col = c0 + (threadIdx.x % SR_COLS), g = threadIdx.x / SR_COLS;
-  // 8 then 4 independent row loads in flight per round trip (conv2's 128 slab rows:
-  // one round trip per lane; conv1's 224: three)
-  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (col < n) {
-    int rr = g;
-    for (; rr + 7 * SR_GROUPS < rows; rr += 8 * SR_GROUPS) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] += slab[(size_t)(rr + j * SR_GROUPS) * n + col];
-    }
-    for (; rr + 3 * SR_GROUPS < rows; rr += 4 * SR_GROUPS) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) a[j] += slab[(size_t)(rr + j * SR_GROUPS) * n + col];
-    }
-    for (; rr < rows; rr += SR_GROUPS) a[0] += slab[(size_t)rr * n + col];
-  }
-  part[g][threadIdx.x % SR_COLS] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  part[g][threadIdx.x % SR_COLS] = slab_colsum<SR_GROUPS>(slab, rows, n, col, g);
   __syncthreads();
   if (threadIdx.x < SR_COLS && c0 + (int)threadIdx.x < n) {
     float t = 0.f;

@@ -166,10 +166,11 @@ constexpr int64_t FUSED_MAX = (int64_t)FUSED_MAX_BLOCKS * FUSED_BLOCK_GRAN * 4;
 //
 // SlabSrc (optional, not with XG): one gradient region [out, out + n) is still the
 // per-workgroup partial rows of a producer (slab [rows][n], e.g. the ConvNet's conv1
-// weight-gradient slab): nblk extra workgroups, appended after the granule grid, sum
-// its columns (16 columns x 16 row groups each, fixed order), check them, write them to
-// `out` write-through and arrive at the grid barrier like the others; the granules
-// inside the region are read (agent scope) only after the barrier.  The separate
+// weight-gradient slab): nblk extra workgroups, appended after the granule grid, own
+// it -- they sum its columns (16 columns x 16 row groups each, the association of the
+// column-sum launch), check them, load the matching params / buffers, arrive at the
+// grid barrier like the others and then apply the same update per element (unscaled
+// gradient written to `out`).  The granule workgroups skip the region, and the separate
 // column-sum launch disappears.
 struct SlabSrc {
   const float* slab;
@@ -222,36 +223,33 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
   f32x4 gv[U], pv[U], bv[U];
   int tt[U];  // tensor of each granule (its offset is recomputed after the barrier)
   bool bad = false;
-  const int nreg = (int)gridDim.x - ss.nblk;  // granule workgroups; the rest reduce the slab
-  unsigned defer = 0;                          // granules whose gradient the slab workgroups produce
+  const int nreg = (int)gridDim.x - ss.nblk;  // granule workgroups; the rest own the slab region
+  // slab workgroup lane (< SS_COLS): its column's sum, tensor and element, param / buffer
+  float st_sum = 0.f, st_p = 0.f, st_b = 0.f;
+  int st_t = -1, st_e = 0;
   if ((int)blockIdx.x >= nreg) {
     __shared__ float spart[SS_GROUPS][SS_COLS + 1];
     const int c0 = ((int)blockIdx.x - nreg) * SS_COLS;
     const int col = c0 + tid % SS_COLS, g = tid / SS_COLS;
-    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (col < ss.n) {
-      int r = g;
-      // the association of cb::slab_reduce_body (bitwise the same sums as that launch)
-      for (; r + 7 * SS_GROUPS < ss.rows; r += 8 * SS_GROUPS) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] += ss.slab[(size_t)(r + j * SS_GROUPS) * ss.n + col];
+    if (tid < SS_COLS && col < ss.n) {  // param / buffer loads in flight with the slab's
+      const float* gp = ss.out + col;
+      for (int i = 0; i < n; ++i)  // the tensor whose gradient holds this column (host-checked: one)
+        if (gp >= sp1[i] && gp < sp1[i] + snum[i]) {
+          st_t = i;
+          st_e = (int)(gp - sp1[i]);
+        }
+      if (st_t >= 0) {
+        st_p = sp0[st_t][st_e];
+        if (momentum != 0.f && !((L.first_bits >> st_t) & 1ull)) st_b = sp2[st_t][st_e];
       }
-      for (; r + 3 * SS_GROUPS < ss.rows; r += 4 * SS_GROUPS) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) a[j] += ss.slab[(size_t)(r + j * SS_GROUPS) * ss.n + col];
-      }
-      for (; r < ss.rows; r += SS_GROUPS) a[0] += ss.slab[(size_t)r * ss.n + col];
     }
-    spart[g][tid % SS_COLS] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    spart[g][tid % SS_COLS] = slab_colsum<SS_GROUPS>(ss.slab, ss.rows, ss.n, col, g);  // = slab_reduce
     __syncthreads();
-    if (tid < SS_COLS && c0 + tid < ss.n) {
-      float t = 0.f;
+    if (tid < SS_COLS && col < ss.n) {
 #pragma unroll
-      for (int gg = 0; gg < SS_GROUPS; ++gg) t += spart[gg][tid];
-      bad = !isfinite(t);
-      __hip_atomic_store(ss.out + c0 + tid, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through
+      for (int gg = 0; gg < SS_GROUPS; ++gg) st_sum += spart[gg][tid];
+      bad = !isfinite(st_sum);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sums have left the CU before the arrival
 #pragma unroll
     for (int k = 0; k < U; ++k) tt[k] = -1;
   } else {
@@ -266,14 +264,10 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
           if (soff[mid] <= gi) lo = mid; else hi = mid - 1;
         }
         const int o = (gi - soff[lo]) * 4, rem = snum[lo] - o;
-        tt[k] = lo;
         const float* gp = sp1[lo] + o;
-        if (!XG && gp >= ss.out && gp < ss.out + ss.n) {
-          defer |= 1u << k;
-          gv[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-        } else {
-          gv[k] = load4(gp, rem);
-        }
+        if (!XG && gp >= ss.out && gp < ss.out + ss.n) continue;  // the slab workgroups own it
+        tt[k] = lo;
+        gv[k] = load4(gp, rem);
         pv[k] = load4(sp0[lo] + o, rem);
         const bool use_buf = momentum != 0.f && !((L.first_bits >> lo) & 1ull);
         bv[k] = use_buf ? load4(sp2[lo] + o, rem) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -379,11 +373,6 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
     const int t = tt[k];
     if (t < 0) continue;
     const int o = (blockIdx.x * BG + k * THR + tid - soff[t]) * 4, rem = snum[t] - o;
-    if ((defer >> k) & 1u) {  // produced by the slab workgroups before they arrived
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        gv[k][j] = j < rem ? __hip_atomic_load(sp1[t] + o + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
-    }
     const f32x4 g = gv[k] * inv;
     store4(sp1[t] + o, rem, g);
     if (any_bad) continue;
@@ -396,6 +385,21 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
       d = nesterov ? d + momentum * bb : bb;
     }
     store4(sp0[t] + o, rem, pv[k] - lr * d);
+  }
+  if (st_t >= 0) {  // a slab column: the same update, one element
+    const float g = st_sum * inv;
+    sp1[st_t][st_e] = g;
+    if (!any_bad) {
+      float d = maximize ? -g : g;
+      if (wd != 0.f) d += wd * st_p;
+      if (momentum != 0.f) {
+        const bool first = (L.first_bits >> st_t) & 1ull;
+        const float bb = first ? d : momentum * st_b + (1.f - dampening) * d;
+        sp2[st_t][st_e] = bb;
+        d = nesterov ? d + momentum * bb : bb;
+      }
+      sp0[st_t][st_e] = st_p - lr * d;
+    }
   }
   if (blockIdx.x == 0 && tid == 0) {
     // every workgroup read scale[0] before arriving, and block 0 passed the barrier
