@@ -495,6 +495,34 @@ def _xgmi_selftest(rc: "RcclCommunicator", x, twoshot: bool = False) -> tuple[bo
         rc.native.all_reduce(vote, "min")
         if vote.item() != 1.0:
             return False, why
+    # the in-kernel exchange sites (fused SyncBN consumers, the fused AMP-SGD gradient
+    # average: csrc/comm/xsite.h) -- the same peer-write protocol run from inside a
+    # multi-workgroup launch; every workgroup must see the rank-ordered sum
+    for it, n in enumerate((65, 96, 1568)):
+        t = torch.randn(n, generator=g).to(device=rc.device)
+        o = torch.empty(4 * n, device=rc.device)
+        good = True
+        try:
+            x.site_probe(it % 2, t, o, 4)
+        except Exception as e:  # noqa: BLE001 - recorded as this rank's vote
+            good, why = False, f"{type(e).__name__}: {e}"
+        ref = torch.empty_like(t)
+        rc.native.all_reduce(t, "sum", ref)
+        every = torch.empty(rc.world_size * 4 * n, device=rc.device)
+        rc.native.all_gather(every, o)
+        torch.cuda.synchronize(rc.device)
+        if x.error() != 0:
+            good, why = False, why or x.error_string()
+        if good and not all(torch.allclose(o[b * n:(b + 1) * n], ref, rtol=1e-5, atol=1e-5 * rc.world_size)
+                            for b in range(4)):
+            good, why = False, f"site mismatch vs RCCL (n={n})"
+        every = every.view(rc.world_size, 4 * n)
+        if good and not bool((every == every[0:1]).all()):
+            good, why = False, f"site: ranks disagree (n={n})"
+        vote.fill_(1.0 if good else 0.0)
+        rc.native.all_reduce(vote, "min")
+        if vote.item() != 1.0:
+            return False, why
     return True, ""
 
 

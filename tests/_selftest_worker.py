@@ -1,0 +1,90 @@
+"""Worker for tests/test_comm_cpu_selftest.py: the xGMI start-up self-test
+(parallel/comm._xgmi_selftest) driven over gloo with a torch stand-in for the
+engine, so its vote / collective symmetry runs on CPU."""
+import os
+import traceback
+
+import torch
+import torch.distributed as dist
+
+from tests._dist import client_env
+
+
+class _Native:
+    """The RcclCommunicator.native calls the self-test makes, on gloo."""
+
+    def __init__(self):
+        self.calls = 0
+
+    def all_reduce(self, t, op, out=None):
+        self.calls += 1
+        r = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+        if out is None:
+            dist.all_reduce(t, op=r)
+            return t
+        out.copy_(t)
+        dist.all_reduce(out, op=r)
+        return out
+
+    def all_gather(self, out, t):
+        self.calls += 1
+        parts = list(out.view(dist.get_world_size(), -1).unbind(0))
+        dist.all_gather(parts, t.contiguous())
+        return out
+
+
+class _RC:
+    def __init__(self, rank, world):
+        self.rank, self.world_size, self.device = rank, world, torch.device("cpu")
+        self.native = _Native()
+
+
+class _Engine:
+    """Correct collectives, except on rank `bad` for the case kind `bad_kind`."""
+
+    def __init__(self, rank, bad, bad_kind):
+        self.rank, self.bad, self.bad_kind = rank, bad, bad_kind
+
+    def _sum(self, t, op):
+        o = t.clone()
+        dist.all_reduce(o, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX}[op])
+        return o
+
+    def all_reduce(self, t, op, out):
+        out.copy_(self._sum(t, op))
+        if self.rank == self.bad and self.bad_kind == "oneshot":
+            out.add_(1.0)
+
+    def all_reduce_twoshot(self, t, op, out):
+        out.copy_(self._sum(t, op))
+
+    def site_probe(self, site, t, o, nblk):
+        s = self._sum(t, "sum")
+        if self.rank == self.bad and self.bad_kind == "site":
+            raise RuntimeError("site probe failed on this rank")
+        o.copy_(s.repeat(nblk))
+
+    def error(self):
+        return 0
+
+    def error_string(self):
+        return ""
+
+
+def run(rank, world, port, bad, bad_kind, q):
+    try:
+        os.environ.update(client_env(rank, world, port))
+        dist.init_process_group("gloo")
+        torch.cuda.synchronize = lambda *a, **k: None  # CPU stand-in: nothing to wait for
+        from ddp_practice_amd.parallel.comm import _xgmi_selftest
+
+        rc = _RC(rank, world)
+        good, why = _xgmi_selftest(rc, _Engine(rank, bad, bad_kind), twoshot=True)
+        # every rank issued the same number of collectives: the call sequences stayed matched
+        calls = torch.tensor([rc.native.calls])
+        every = [torch.zeros(1, dtype=calls.dtype) for _ in range(world)]
+        dist.all_gather(every, calls)
+        dist.destroy_process_group()
+        q.put((rank, "ok", (good, why, [int(c) for c in every])))
+    except Exception:  # noqa: BLE001
+        q.put((rank, "err", traceback.format_exc()))
