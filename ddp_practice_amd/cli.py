@@ -19,6 +19,9 @@ Additive flags (all optional; defaults reproduce the reference):
                                       autocast, GradScaler, SGD, SyncBatchNorm and DDP
                                       (parity / same-node baseline runs)
   --seed N                            model-init seed
+  --model {convnet,resnet50}          resnet50 = BASELINE.json config 5 (ResNet-50, torchvision
+                                      layout) on a synthetic ImageNet-shaped set
+                                      (--image-size, --num-classes; data/imagenet.py)
   --resume PATH [--start-epoch N]     load {"model"[, "scaler"]} before training
   --watchdog-timeout S                abort + exit when no progress for S seconds
   --profile                           roctx ranges (rocprofv3 --marker-trace)
@@ -51,6 +54,10 @@ def add_run_args(parser, amp_default: str, checkpoint: str, distributed: bool) -
     parser.add_argument("--metrics-file", default=None, help="per-epoch JSONL metrics (rank 0)")
     parser.add_argument("--impl", default="native", choices=["native", "torch"],
                         help="torch: run the same program on PyTorch's own stack (parity / baseline)")
+    parser.add_argument("--model", default="convnet", choices=["convnet", "resnet50"],
+                        help="resnet50: ResNet-50 on synthetic 3 x S x S images (BASELINE.json config 5)")
+    parser.add_argument("--image-size", type=int, default=224, help="resnet50: synthetic image side")
+    parser.add_argument("--num-classes", type=int, default=1000, help="resnet50: synthetic label count")
     if distributed:
         parser.add_argument("--no-sync-bn", action="store_true")
         parser.add_argument("--bucket-cap-mb", type=float, default=None)
@@ -146,8 +153,19 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
     # extension and the model; joined before the loaders need them.
     ds_box: dict = {}
 
+    resnet = getattr(args, "model", "convnet") == "resnet50"
+
     def _build_datasets():
         try:
+            if resnet:  # no ImageNet reader (no network): the synthetic set, small by default
+                from ddp_practice_amd.data import synthetic_imagenet
+
+                kw = dict(classes=args.num_classes, hw=args.image_size)
+                ds_box["train"] = synthetic_imagenet(args.train_samples or 1280, seed=1,
+                                                     name="synthetic-imagenet-train", **kw)
+                ds_box["test"] = synthetic_imagenet(args.test_samples or 256, seed=2,
+                                                    name="synthetic-imagenet-test", **kw)
+                return
             ds_box["train"] = MNIST(root=args.data_root, train=True, force_synthetic=args.synthetic,
                                     n=args.train_samples)
             ds_box["test"] = MNIST(root=args.data_root, train=False, force_synthetic=args.synthetic,
@@ -170,7 +188,12 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
 
     native = getattr(args, "impl", "native") == "native"
     # autocast inside forward, as the reference; fused=False: torch's own modules
-    model = ConvNet(amp_dtype=amp, fused=native).to(dev)
+    if resnet:
+        from ddp_practice_amd.models import resnet50
+
+        model = resnet50(num_classes=args.num_classes, amp_dtype=amp, fused=native).to(dev)
+    else:
+        model = ConvNet(amp_dtype=amp, fused=native).to(dev)
     if native:
         scaler = GradScaler(enabled=True) if amp is not None else None
     else:
@@ -219,8 +242,9 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
         timeout = float(os.environ["DPA_WATCHDOG_TIMEOUT"])
     watchdog = Watchdog(comm, timeout=timeout, tag=f"rank{rank}") if timeout else None
     faults = FaultInjector(rank)
+    # ResNet-50: hundreds of launches per step, one step per captured graph is enough
     loop = TrainLoop(model, criterion, optimizer, train_dloader, scaler, use_graph=native and not args.no_graph,
-                     watchdog=watchdog, faults=faults)
+                     steps_per_graph=1 if resnet else 16, watchdog=watchdog, faults=faults)
     metrics = _Metrics(args.metrics_file, rank, world, dev)
     metrics.start()
     try:

@@ -48,7 +48,7 @@ class DeviceLoader:
         self._order: torch.Tensor | None = None
         self._ctr = None
         self._imgs, self._labels = dataset.to_device(self.device)
-        self._hw = tuple(dataset.images.shape[1:])
+        self._chw = dataset.sample_shape
 
     # ----------------------------------------------------------- ordering
     def epoch_order(self) -> torch.Tensor:
@@ -101,7 +101,7 @@ class DeviceLoader:
 
     def static_batch(self, batch_size: int | None = None):
         b = batch_size or self.batch_size
-        imgs = torch.empty((b, 1) + self._hw, dtype=self.dtype, device=self.device)
+        imgs = torch.empty((b,) + self._chw, dtype=self.dtype, device=self.device)
         labels = torch.empty((b,), dtype=torch.int64, device=self.device)
         return imgs, labels
 
@@ -137,7 +137,7 @@ class DeviceLoader:
                 self._ctr[0] += 1
             b = images.shape[0]
             sel = self._order[step * self.batch_size: step * self.batch_size + b]
-            images.copy_((self._imgs[sel].to(torch.float32) / 255.0).unsqueeze(1).to(images.dtype))
+            images.copy_((self._imgs[sel].to(torch.float32) / 255.0).reshape(images.shape).to(images.dtype))
             labels.copy_(self._labels[sel])
 
     def set_step(self, step: int) -> None:

@@ -25,21 +25,28 @@ import torch
 
 
 class ImageDataset:
-    """uint8 images [N, H, W] + int64 labels [N]; items are (float [1,H,W] in [0,1], int)."""
+    """uint8 images [N, H, W] (one channel, MNIST) or [N, C, H, W] + int64 labels [N];
+    items are (float [C,H,W] in [0,1], int)."""
 
     def __init__(self, images: torch.Tensor, labels: torch.Tensor, name: str = ""):
-        assert images.dtype == torch.uint8 and images.dim() == 3
+        assert images.dtype == torch.uint8 and images.dim() in (3, 4)
         assert labels.dtype == torch.int64 and labels.numel() == images.shape[0]
         self.images = images
         self.labels = labels
         self.name = name
         self._dev_cache: dict = {}
 
+    @property
+    def sample_shape(self) -> tuple:
+        """(C, H, W) of one item (what ToTensor yields)."""
+        s = tuple(self.images.shape[1:])
+        return (1,) + s if len(s) == 2 else s
+
     def __len__(self):
         return self.images.shape[0]
 
     def __getitem__(self, i):
-        return self.images[i].float().div_(255.0).unsqueeze(0), int(self.labels[i])
+        return self.images[i].float().div_(255.0).reshape(self.sample_shape), int(self.labels[i])
 
     @property
     def num_classes(self) -> int:

@@ -68,3 +68,29 @@ def test_ddp_main_torchrun_cpu(tmp_path):
     ck = torch.load(tmp_path / "ddp_checkpoint.pt", weights_only=True)
     assert list(ck["model"]) == ["module." + k for k in REF_KEYS]
     assert set(ck["scaler"]) == {"scale", "growth_factor", "backoff_factor", "growth_interval", "_growth_tracker"}
+
+
+def test_origin_main_resnet50_cpu(tmp_path):
+    """``--model resnet50`` (BASELINE.json config 5) through the reference CLI: the
+    synthetic ImageNet-shaped set at a small image size, torchvision state_dict keys."""
+    out = _run([os.path.join(ROOT, "origin_main.py"), "-e", "1", "-b", "8", "--model", "resnet50",
+                "--image-size", "32", "--num-classes", "10", "--train-samples", "32", "--test-samples", "16",
+                "--seed", "0"], tmp_path)
+    _check_stdout(out, 1)
+    ck = torch.load(tmp_path / "origin_checkpoint.pt", weights_only=True)
+    from ddp_practice_amd.models import resnet50
+
+    m = resnet50(num_classes=10)
+    assert list(ck["model"]) == list(m.state_dict())
+    m.load_state_dict(ck["model"])
+
+
+def test_ddp_main_resnet50_cpu(tmp_path):
+    out = _run([os.path.join(ROOT, "ddp_main.py"), "-e", "1", "-b", "4", "--model", "resnet50", "--image-size", "32",
+                "--num-classes", "10", "--train-samples", "16", "--test-samples", "8", "--cpu-procs", "2",
+                "--amp-dtype", "fp32"], tmp_path, {"MASTER_PORT": str(free_port()), "DPA_MASTER_ADDR": "127.0.0.1"})
+    _check_stdout(out, 1)
+    ck = torch.load(tmp_path / "ddp_checkpoint.pt", weights_only=True)
+    from ddp_practice_amd.models import resnet50
+
+    assert list(ck["model"]) == ["module." + k for k in resnet50(num_classes=10).state_dict()]

@@ -93,3 +93,19 @@ def test_accuracy_parity_with_torch(C, tmp_path, script, extra):
     a_torch = _acc(_run(args + ["--impl", "torch"], tmp_path / "t", env))
     print(f"{script}: native {a_native:.2f}% torch {a_torch:.2f}%")
     assert abs(a_native - a_torch) <= 1.0, (a_native, a_torch)
+
+
+def test_origin_main_resnet50_gpu(C, tmp_path):
+    """``--model resnet50`` through the reference CLI on the native NHWC path: bf16 AMP,
+    graph replay of the full batches plus the eager tail batch (36 = 2 x 16 + 4 samples),
+    BN counters advanced by every step, checkpoint loadable into the torch modules."""
+    out = _run([os.path.join(ROOT, "origin_main.py"), "--gpu", "0", "-e", "1", "-b", "16", "--model", "resnet50",
+                "--amp-dtype", "bf16", "--train-samples", "36", "--test-samples", "32", "--seed", "0"], tmp_path)
+    _check_stdout(out, 1)
+    ck = torch.load(tmp_path / "origin_checkpoint.pt", weights_only=True)
+    from ddp_practice_amd.models import resnet50
+
+    m = resnet50(fused=False)
+    m.load_state_dict(ck["model"])
+    assert int(m.bn1.num_batches_tracked) == 3
+    assert all(torch.isfinite(v).all() for v in ck["model"].values() if v.is_floating_point())
