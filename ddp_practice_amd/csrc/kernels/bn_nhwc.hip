@@ -113,20 +113,37 @@ __device__ __forceinline__ void row_range(long long M, long long& r0, long long&
   r1 = r0 + per < M ? r0 + per : M;
 }
 
-// Last-arriver election over `n` workgroups (agent-scope release / acquire).
-__device__ __forceinline__ bool ticket_last(unsigned* ticket, int n, int* s_flag) {
+// Write-through hand-off (MI355X_MICROARCH.md "Valid forms", row 1): partial rows
+// stored with agent-scope relaxed atomic stores (sc1, past the XCD's L2) and read
+// back with agent-scope atomic loads, so the ticket needs no release / acquire
+// fence -- an agent release writes back the whole L2 of the XCD, once per
+// workgroup.  g_handoff_wt (bn_nhwc.set_handoff) = 0 restores the fenced form.
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Last-arriver election over `n` workgroups: fenced (wt = 0: agent-scope release /
+// acquire around the ticket) or write-through (wt = 1: the rows were stored sc1).
+__device__ __forceinline__ bool ticket_last(unsigned* ticket, int n, int* s_flag, int wt) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its partial-row stores are done
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!wt) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = t == (unsigned)n - 1;
     *s_flag = last;
     if (last) {
       __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm for the next launch
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!wt) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     }
   }
   __syncthreads();
@@ -137,8 +154,12 @@ __device__ __forceinline__ bool ticket_last(unsigned* ticket, int n, int* s_flag
 // 16-B column vectors; the RG = THR/(W/4) row groups of the block each sum
 // every RG-th row with up to 16 loads in flight per lane, then the RG partials
 // are added in group order through LDS (scr: >= THR*4 floats).
+__device__ __forceinline__ f32x4 ld4(const float* p, int wt) {
+  if (!wt) return *reinterpret_cast<const f32x4*>(p);
+  return f32x4{ld_wt(p), ld_wt(p + 1), ld_wt(p + 2), ld_wt(p + 3)};
+}
 __device__ __noinline__ void sum_rows(const float* __restrict__ src, int n, int W, float* __restrict__ dst,
-                                      float* scr) {
+                                      float* scr, int wt, int wt_dst) {
   const int W4 = W / 4;
   const int RG = W4 >= THR ? 1 : THR / W4;
   for (int base = 0; base < W4; base += THR) {
@@ -151,7 +172,7 @@ __device__ __noinline__ void sum_rows(const float* __restrict__ src, int n, int 
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
           const int g = g0 + u * RG;
-          v[u] = *reinterpret_cast<const f32x4*>(src + (size_t)(g < n ? g : n - 1) * W + 4 * col);
+          v[u] = ld4(src + (size_t)(g < n ? g : n - 1) * W + 4 * col, wt);
         }
 #pragma unroll
         for (int u = 0; u < 16; ++u)
@@ -165,7 +186,12 @@ __device__ __noinline__ void sum_rows(const float* __restrict__ src, int n, int 
     if ((int)threadIdx.x < nc) {
       f32x4 t = {0.f, 0.f, 0.f, 0.f};
       for (int r = 0; r < RG; ++r) t += *reinterpret_cast<const f32x4*>(scr + 4 * ((size_t)r * nc + threadIdx.x));
-      *reinterpret_cast<f32x4*>(dst + 4 * (base + threadIdx.x)) = t;
+      float* d = dst + 4 * (base + threadIdx.x);
+      if (wt_dst) {
+        st_wt(d, t[0]); st_wt(d + 1, t[1]); st_wt(d + 2, t[2]); st_wt(d + 3, t[3]);
+      } else {
+        *reinterpret_cast<f32x4*>(d) = t;
+      }
     }
   }
 }
@@ -174,23 +200,26 @@ __device__ __noinline__ void sum_rows(const float* __restrict__ src, int n, int 
 // true in the single workgroup per chunk that ends with the chunk's W totals in
 // red[0, W).  part: [Gc*Gr + Gc*NG][W] floats; tickets: [Gc*NG + Gc].
 __device__ bool chunk_reduce(float* __restrict__ part, unsigned* __restrict__ tickets, int W, float* red,
-                             float* scr, int* s_flag) {
+                             float* scr, int* s_flag, int wt) {
   const int Gr = gridDim.x, Gc = gridDim.y, y = blockIdx.y;
   const int NG = (Gr + G1 - 1) / G1;
   float* p1 = part + (size_t)y * Gr * W;
   float* p2 = part + (size_t)Gc * Gr * W + (size_t)y * NG * W;
-  for (int t = threadIdx.x; t < W; t += THR) p1[(size_t)blockIdx.x * W + t] = red[t];
+  for (int t = threadIdx.x; t < W; t += THR) {
+    if (wt) st_wt(p1 + (size_t)blockIdx.x * W + t, red[t]);
+    else p1[(size_t)blockIdx.x * W + t] = red[t];
+  }
   const int grp = blockIdx.x / G1;
   const int gsz = min(G1, Gr - grp * G1);
-  if (!ticket_last(tickets + y * NG + grp, gsz, s_flag)) return false;
+  if (!ticket_last(tickets + y * NG + grp, gsz, s_flag, wt)) return false;
   if (NG == 1) {
-    sum_rows(p1, gsz, W, red, scr);
+    sum_rows(p1, gsz, W, red, scr, wt, 0);
     __syncthreads();
     return true;
   }
-  sum_rows(p1 + (size_t)grp * G1 * W, gsz, W, p2 + (size_t)grp * W, scr);
-  if (!ticket_last(tickets + Gc * NG + y, NG, s_flag)) return false;
-  sum_rows(p2, NG, W, red, scr);
+  sum_rows(p1 + (size_t)grp * G1 * W, gsz, W, p2 + (size_t)grp * W, scr, wt, wt);
+  if (!ticket_last(tickets + Gc * NG + y, NG, s_flag, wt)) return false;
+  sum_rows(p2, NG, W, red, scr, wt, 0);
   __syncthreads();
   return true;
 }
@@ -223,7 +252,7 @@ template <typename T>
 __global__ void __launch_bounds__(THR)
 fwd_stats_kernel(const T* __restrict__ x, long long M, int C, const float* __restrict__ shift,
                  float* __restrict__ part, unsigned* __restrict__ tickets, float* __restrict__ stats,
-                 int64_t* __restrict__ nbt) {
+                 int64_t* __restrict__ nbt, int wt) {
   constexpr int VEC = V16<T>::N;
   __shared__ float scratch[2 * THR * VEC];
   __shared__ float red[2 * CC_MAX];
@@ -263,7 +292,7 @@ fwd_stats_kernel(const T* __restrict__ x, long long M, int C, const float* __res
     }
   }
   block_combine<VEC>(g, s1, s2, red, scratch);
-  if (!chunk_reduce(part, tickets, 2 * g.CC, red, scratch, &s_flag)) return;
+  if (!chunk_reduce(part, tickets, 2 * g.CC, red, scratch, &s_flag, wt)) return;
   const int cb = (int)blockIdx.y * g.CC;
   for (int t = threadIdx.x; t < g.CC; t += THR) {
     stats[cb + t] = red[t];
@@ -396,7 +425,7 @@ __global__ void __launch_bounds__(THR)
 bwd_stats_kernel(const T* __restrict__ dy, const T* __restrict__ y, const T* __restrict__ x, long long M, int C,
                  const float* __restrict__ save, const float* __restrict__ gamma, const float* __restrict__ beta,
                  float* __restrict__ part, unsigned* __restrict__ tickets, float* __restrict__ out,
-                 float* __restrict__ dgamma, float* __restrict__ dbeta) {
+                 float* __restrict__ dgamma, float* __restrict__ dbeta, int wt) {
   constexpr int VEC = V16<T>::N;
   __shared__ float scratch[2 * THR * VEC];
   __shared__ float red[2 * CC_MAX];
@@ -441,7 +470,7 @@ bwd_stats_kernel(const T* __restrict__ dy, const T* __restrict__ y, const T* __r
     }
   }
   block_combine<VEC>(g, s1, s2, red, scratch);
-  if (!chunk_reduce(part, tickets, 2 * g.CC, red, scratch, &s_flag)) return;
+  if (!chunk_reduce(part, tickets, 2 * g.CC, red, scratch, &s_flag, wt)) return;
   const int cb = (int)blockIdx.y * g.CC;
   for (int t = threadIdx.x; t < g.CC; t += THR) {
     out[cb + t] = dbeta[cb + t] = red[t];
@@ -663,6 +692,8 @@ struct Grid2 {
 static int g_stats_target = 0;
 static int g_apply_target = 512;
 static int g_elemt_target = 1024;
+static int g_handoff_wt = 1;  // statistics ticket trees: write-through hand-off (1) or fenced (0)
+void set_handoff(int64_t wt) { g_handoff_wt = wt ? 1 : 0; }
 void set_grid_targets(int64_t stats, int64_t apply, int64_t elemt) {
   TORCH_CHECK(stats >= 0 && apply >= 1 && elemt >= 1);
   g_stats_target = (int)stats;
@@ -710,7 +741,7 @@ void fwd_stats(at::Tensor x, int64_t C, at::Tensor shift, at::Tensor part, at::T
     hipLaunchKernelGGL(fwd_stats_kernel<T>, dim3(g.Gr, g.Gc), dim3(THR), 0, cur_stream(), dp<T>(x), M, (int)C,
                        shift.data_ptr<float>(), part.data_ptr<float>(),
                        reinterpret_cast<unsigned*>(ticket.data_ptr<int>()), stats.data_ptr<float>(),
-                       nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr);
+                       nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr, g_handoff_wt);
   });
   DPA_CHECK_LAUNCH();
 }
@@ -760,7 +791,7 @@ void bwd_stats(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, int64_t
                          act == ACT_Y ? dp<T>(*y) : nullptr, dp<T>(x), M, (int)C, save.data_ptr<float>(),
                          gamma.data_ptr<float>(), beta.data_ptr<float>(), part.data_ptr<float>(),
                          reinterpret_cast<unsigned*>(ticket.data_ptr<int>()), out.data_ptr<float>(),
-                         dgamma.data_ptr<float>(), dbeta.data_ptr<float>());
+                         dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), g_handoff_wt);
     };
     if (act == ACT_Y) go(bwd_stats_kernel<T, ACT_Y>);
     else if (act == ACT_RECOMPUTE) go(bwd_stats_kernel<T, ACT_RECOMPUTE>);
@@ -856,6 +887,7 @@ void register_bn_nhwc(pybind11::module& m) {
   auto s = m.def_submodule("bn_nhwc", "channels-last BatchNorm(+add)(+ReLU), max-pool 3x3/2, global avg-pool");
   s.def("fwd_stats", &bnh::fwd_stats);
   s.def("set_grid_targets", &bnh::set_grid_targets);
+  s.def("set_handoff", &bnh::set_handoff);
   s.def("apply", &bnh::apply);
   s.def("bwd_stats", &bnh::bwd_stats);
   s.def("bwd_elemt", &bnh::bwd_elemt);

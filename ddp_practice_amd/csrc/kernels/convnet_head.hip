@@ -15,13 +15,15 @@
 // Decomposition: one workgroup per BN2 channel c (C = 32).  A channel owns 49
 // of the 1568 fc inputs, so it computes its BN / ReLU / pool slice and a K = 49
 // split of the logits (MFMA 16x16x32: rows = images, cols = classes).  The
-// partial logits travel to the last-arriving workgroup (write-through `sc1`
-// stores + one agent-scope ticket, MI355X_MICROARCH.md "Valid forms" row 1: no
-// release / acquire fence), which adds the bias, rounds the logits to the
-// storage dtype and runs the loss (16 lanes per row, as head.hip ce_fwd_kernel:
-// same formula, same rounding).  When an active GradScaler supplies the scale,
-// it publishes d(scale*loss)/dlogits the same way and every workgroup does its
-// channel's share of the fc backward on MFMA:
+// partial logits are stored write-through (`sc1`) and every workgroup takes one
+// agent-scope ticket (MI355X_MICROARCH.md "Valid forms" row 1: no release /
+// acquire fence).  Without a backward the last arriver adds the bias, rounds the
+// logits to the storage dtype and runs the loss (16 lanes per row, as head.hip
+// ce_fwd_kernel: same formula, same rounding).  When an active GradScaler
+// supplies the scale, the last ticket releases every workgroup, each of which
+// sums the partials and runs the same loss itself (fixed order: identical
+// d(scale*loss)/dlogits everywhere, no second hand-off) and does its channel's
+// share of the fc backward on MFMA:
 //   dp2[b, c*49 + j]   = sum_n dls[b, n] * W[n, c*49 + j]       (B x 49, K = N)
 //   dW[n, c*49 + j]    = sum_b dls[b, n] * p2[b, c*49 + j]      (N x 49, K = B)
 // plus the BN2 backward sums of channel c (complete: the channel is whole here).
@@ -45,8 +47,8 @@ constexpr int NMAX = 16;   // classes (one MFMA column tile)
 constexpr int KP = 64;     // 49 fc inputs per channel, padded to 2 MFMA k-steps
 constexpr int IT = (BMAX * PP + NT - 1) / NT;  // pooled outputs per lane
 
-// state: int64[4] zero-initialised once: [0] {generation:32 | tickets:32},
-// [1] flag (= generation + 1 once the loss gradient is published), [2] error word
+// state: int64[4] zero-initialised once: [0] {generation:32 | tickets:32} (the last
+// ticket stores (generation + 1) << 32: re-arm and release), [1] unused, [2] error word
 struct HeadStep {
   const int64_t* target;
   int64_t ignore_index;
@@ -57,7 +59,8 @@ struct HeadStep {
   float* loss;          // [2]: loss, loss * scale
   float* dlog;          // [B][N] (softmax - onehot) / count, f32
   void* dls;            // [B][N] dlog * scale, storage dtype (null without scaler)
-  float* dlsf;          // [B][N] the same values as f32, write-through (hand-off to the workgroups)
+  float* dlsf;          // [B][N] f32 scratch of the earlier two-hand-off protocol (unused; its
+                        // presence still selects the speculative backward on the host)
   int do_bwd;
   void* dp2;            // [B][K] storage dtype
   float* dwfc;          // [N][K]
@@ -122,7 +125,6 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
   const int tid = threadIdx.x, c = blockIdx.x;
   const int lane = tid & 63, wv = tid >> 6, r = lane & 15, q = lane >> 4;
   const int NPO = B * PP;  // pooled outputs of this channel
-  const E ez = Cvt<T>::from_f(0.f);
 
   DPA_STAMP(0);
   // 1. loads: this channel's pre-BN maps (two row pairs per pooled output) and W slice
@@ -151,12 +153,19 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
     wv_[i] = (e < NMAX * PP && n < N) ? wfc[(size_t)n * K + c * PP + j] : 0.f;
   }
   // zero the tiles' padding (rows past B, k past 49 / N)
-  for (int e = tid; e < BMAX * KP; e += NT) pcl[e] = ez;
-  for (int e = tid; e < KP * PCT_S; e += NT) pct[e] = ez;
-  for (int e = tid; e < BMAX * 32; e += NT) dll[e] = ez;
-  for (int e = tid; e < KP * WDL_S; e += NT) wdl[e] = ez;
-  for (int e = tid; e < NMAX * DLT_S; e += NT) dlt[e] = ez;
-  for (int e = tid; e < NMAX * KP; e += NT) wcl[e] = ez;
+  {  // 16-B LDS writes (every tile is 16-B aligned and a whole number of 16-B chunks)
+    auto zero = [&](E* t, int n) {
+      for (int e = tid; e < n * (int)sizeof(E) / 16; e += NT) reinterpret_cast<f32x4*>(t)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    static_assert((BMAX * KP) % 8 == 0 && (KP * PCT_S) % 8 == 0 && (BMAX * 32) % 8 == 0 && (KP * WDL_S) % 8 == 0 &&
+                  (NMAX * DLT_S) % 8 == 0 && (NMAX * KP) % 8 == 0, "head tiles: whole 16-B chunks");
+    zero(pcl, BMAX * KP);
+    zero(pct, KP * PCT_S);
+    zero(dll, BMAX * 32);
+    zero(wdl, KP * WDL_S);
+    zero(dlt, NMAX * DLT_S);
+    zero(wcl, NMAX * KP);
+  }
   if (tid < BMAX) tgt_s[tid] = tgt_r;
   if (tid < NMAX) bias_s[tid] = bias_r;
   cb::bn_finalize<C>(bn, sc_s, beta_s, mean_s, istd_s, part_s, c == 0);  // ends with a barrier
@@ -237,36 +246,63 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
   const unsigned long long tk = tk_s;
   const uint32_t gen = (uint32_t)(tk >> 32);
   const bool last = (uint32_t)tk == (uint32_t)(gridDim.x - 1);
-
+  // The last ticket re-arms the word for the next launch ((gen + 1) << 32: stream order, no
+  // workgroup of this launch takes a ticket after it) and that same store releases the
+  // waiting workgroups: with the speculative backward EVERY workgroup then sums the C
+  // partial logits and runs the loss itself (identical fixed-order arithmetic, so identical
+  // results), instead of the last arriver computing it and publishing the loss gradient
+  // behind a second flag -- one cross-workgroup hand-off on the serial path instead of two.
   if (last) {
-    // 4. logits = sum of the C partials + bias, rounded to the storage dtype (every load sc1)
-    constexpr int OIT = BMAX * NMAX / NT;
-    T lgr[OIT];
-#pragma unroll
-    for (int k = 0; k < OIT; ++k) {
-      const int o = tid + k * NT;
-      const int b = o / NMAX, n = o % NMAX;
-      if (b < B) {
-        float v[C];
-#pragma unroll
-        for (int cc = 0; cc < C; ++cc) v[cc] = ld_wt(&hs.part[((size_t)cc * B + b) * NMAX + n]);
-        float t = bias_s[n];
-#pragma unroll
-        for (int cc = 0; cc < C; ++cc) t += v[cc];
-        lgr[k] = Cvt<T>::from_f(t);
-        lg_s[o] = Cvt<T>::to_f(lgr[k]);
+    if (tid == 0)
+      __hip_atomic_exchange(&hs.state[0], ((unsigned long long)(gen + 1u)) << 32, __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT);
+  } else if (hs.do_bwd) {
+    // bounded wait for the last ticket: a timeout sets the error word and goes on
+    if (tid == 0) {
+      const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+      while ((uint32_t)(__hip_atomic_load(&hs.state[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == gen) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > hs.timeout_ticks) {
+          __hip_atomic_store(&hs.state[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
       }
     }
-    if (tid == 0) cnt_s = 0;
     __syncthreads();
-    DPA_STAMP(4);
-    // 5. cross entropy (mean over non-ignored rows), 16 lanes per row (ce_fwd_kernel's math);
-    //    per-element gradients to LDS first, so the hand-off below drains only dlsf
-    if (tid < B && tgt_s[tid] != hs.ignore_index) atomicAdd(&cnt_s, 1);
-    __syncthreads();
-    const float cnt = (float)cnt_s;
-    const float inv = cnt > 0.f ? 1.f / cnt : 0.f;
-    const float scv = scale_r;
+  } else {
+    store_pooled();  // no backward: the last arriver alone computes the loss
+    return;
+  }
+  // one writer of the launch-wide outputs (logits, loss, dlog, dls)
+  const bool writer = hs.do_bwd ? c == 0 : true;
+  DPA_STAMP(4);
+  // 4. logits = sum of the C partials + bias, rounded to the storage dtype (every load sc1)
+  constexpr int OIT = BMAX * NMAX / NT;
+  T lgr[OIT];
+#pragma unroll
+  for (int k = 0; k < OIT; ++k) {
+    const int o = tid + k * NT;
+    const int b = o / NMAX, n = o % NMAX;
+    if (b < B && n < N) {
+      float v[C];
+#pragma unroll
+      for (int cc = 0; cc < C; ++cc) v[cc] = ld_wt(&hs.part[((size_t)cc * B + b) * NMAX + n]);
+      float t = bias_s[n];
+#pragma unroll
+      for (int cc = 0; cc < C; ++cc) t += v[cc];
+      lgr[k] = Cvt<T>::from_f(t);
+      lg_s[o] = Cvt<T>::to_f(lgr[k]);
+    }
+  }
+  if (tid == 0) cnt_s = 0;
+  __syncthreads();
+  // 5. cross entropy (mean over non-ignored rows), 16 lanes per row (ce_fwd_kernel's math)
+  if (tid < B && tgt_s[tid] != hs.ignore_index) atomicAdd(&cnt_s, 1);
+  __syncthreads();
+  const float cnt = (float)cnt_s;
+  const float inv = cnt > 0.f ? 1.f / cnt : 0.f;
+  const float scv = scale_r;
+  {
     const int gl = tid % 16, gr = tid / 16;
     float lsum = 0.f;
     for (int r0 = 0; r0 < B; r0 += NT / 16) {
@@ -294,26 +330,15 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
         dd_s[b * NMAX + gl] = d;
       }
     }
-    lsum = wave_sum(lsum);
-    if (lane == 0) red[0][wv] = lsum;
-    __syncthreads();
-    // the loss gradient the scaler will seed: publish first (write-through + ONE flag)
-    if (hs.do_bwd) {
-      for (int o = tid; o < B * NMAX; o += NT) {
-        const int b = o / NMAX, n = o % NMAX;
-        const float dq = Cvt<T>::to_f(Cvt<T>::from_f(dd_s[o] * scv));
-        lg_s[o] = n < N ? dq : 0.f;  // this workgroup's own copy for its backward share
-        if (n < N) st_wt<T>(&hs.dlsf[(size_t)b * N + n], dq);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+    if (writer) {
+      lsum = wave_sum(lsum);
+      if (lane == 0) red[0][wv] = lsum;
     }
+  }
+  __syncthreads();
+  DPA_STAMP(5);
+  if (writer) {  // outputs nobody in this launch waits for
     if (tid == 0) {
-      // re-arm the ticket word for the next launch (stream order: no workgroup of this
-      // launch takes a ticket after this one), then release the waiting workgroups
-      __hip_atomic_exchange(&hs.state[0], ((unsigned long long)(gen + 1u)) << 32, __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&hs.state[1], (unsigned long long)(gen + 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       float tl = 0.f;
 #pragma unroll
       for (int i = 0; i < NT / 64; ++i) tl += red[0][i];
@@ -321,8 +346,6 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
       hs.loss[0] = l;
       if (hs.scale != nullptr) hs.loss[1] = l * scv;
     }
-    DPA_STAMP(5);
-    // outputs nobody in this launch waits for
 #pragma unroll
     for (int k = 0; k < OIT; ++k) {
       const int o = tid + k * NT;
@@ -334,29 +357,13 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
         if (hs.dls != nullptr) reinterpret_cast<T*>(hs.dls)[(size_t)b * N + n] = Cvt<T>::from_f(d * scv);
       }
     }
-    store_pooled();
-    if (!hs.do_bwd) return;
-  } else {
-    store_pooled();
-    if (!hs.do_bwd) return;
-    // wait for the loss gradient (bounded: a timeout sets the error word and goes on)
-    if (tid == 0) {
-      const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-      while (__hip_atomic_load(&hs.state[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
-             (unsigned long long)(gen + 1u)) {
-        __builtin_amdgcn_s_sleep(1);
-        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > hs.timeout_ticks) {
-          __hip_atomic_store(&hs.state[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    DPA_STAMP(5);
-    for (int o = tid; o < B * NMAX; o += NT) {
-      const int b = o / NMAX, n = o % NMAX;
-      lg_s[o] = n < N ? ld_wt(&hs.dlsf[(size_t)b * N + n]) : 0.f;
-    }
+  }
+  store_pooled();
+  if (!hs.do_bwd) return;
+  // the loss gradient the scaler seeds: d(scale * loss)/dlogits rounded to the storage dtype
+  for (int o = tid; o < B * NMAX; o += NT) {
+    const int n = o % NMAX;
+    lg_s[o] = n < N ? Cvt<T>::to_f(Cvt<T>::from_f(dd_s[o] * scv)) : 0.f;
   }
   __syncthreads();
   DPA_STAMP(6);
