@@ -1276,6 +1276,10 @@ conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __r
   constexpr bool DIRECT = (ROWS == H);
   __shared__ __attribute__((aligned(16))) T xpad[DIRECT ? 8 : CIN * XR * WX];
   __shared__ f32x4 kred[KSPLIT > 1 ? NW : 1][64];
+  // the partial row in natural order, staged for whole-chunk stores where LDS allows
+  constexpr size_t LDS_BASE = sizeof(T) * ((size_t)COUT * DYS + 5 * CIN * XCS + (DIRECT ? 8 : CIN * XR * WX));
+  constexpr bool STAGE = CIF && LDS_BASE + sizeof(float) * COUT * N <= 144 * 1024;
+  __shared__ __attribute__((aligned(16))) float wtile[STAGE ? COUT * N : 4];
 
   const int tid = threadIdx.x;
   const int b = bid / nsplit, sp = bid % nsplit;
@@ -1453,7 +1457,23 @@ conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __r
     if (col < N) {
       const int nat = CIF ? (col % CIN) * 25 + col / CIN : col;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) put(&row_out[(mt * 16 + 4 * q + i) * N + nat], acc[i]);
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (STAGE) wtile[(mt * 16 + 4 * q + i) * N + nat] = acc[i];
+        else put(&row_out[(mt * 16 + 4 * q + i) * N + nat], acc[i]);
+      }
+    }
+  }
+  if constexpr (STAGE) {
+    // ci-fastest columns land 25 floats apart in the natural row: 64-lane stores to ~40
+    // lines each.  Staged through LDS instead, the row leaves as whole 16-B chunks
+    // (consecutive lanes, consecutive addresses).
+    static_assert((COUT * N) % 4 == 0 && ROWLEN % 4 == 0, "wgrad rows: whole 16-B chunks");
+    __syncthreads();
+    if constexpr (WT) {  // 4-B write-through stores, consecutive lanes on consecutive words
+      for (int e = tid; e < COUT * N; e += NTHR) put(&row_out[e], wtile[e]);
+    } else {
+      for (int e = tid; e < COUT * N / 4; e += NTHR)
+        *reinterpret_cast<f32x4*>(&row_out[4 * e]) = *reinterpret_cast<const f32x4*>(&wtile[4 * e]);
     }
   }
   DPA_STAMP(7);
