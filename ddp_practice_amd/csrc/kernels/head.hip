@@ -2,6 +2,8 @@
 // log-softmax + NLL + analytic gradient), plus the eval accuracy counter.
 // reference: /root/reference/origin_main.py:24,30,63 (fc, criterion),
 //            ddp_main.py:104-107 (argmax == label accumulation).
+#include <map>
+
 #include "common.h"
 
 namespace dpa {
@@ -254,6 +256,104 @@ ce_fwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ target, 
   }
 }
 
+// Many-row variant (B > 64): RT rows per workgroup, a GL = 64-lane group per row with
+// the row held in registers (VPL values per lane: one read of the logits), grid-stride
+// over row groups.  The per-workgroup loss partials are handed to the last-arriving
+// workgroup write-through (MI355X_MICROARCH.md "Valid forms" row 1, as conv_igemm.hip's
+// statistics tree), which sums them in workgroup order (deterministic) and writes the
+// loss.  ws: [CE_MAXG] floats + one self-re-arming ticket word after them.
+constexpr int CE_RT = 4, CE_RTHR = CE_RT * 64, CE_MAXG = 1024;
+
+template <typename T, int VPL>
+__global__ void __launch_bounds__(CE_RTHR)
+ce_fwd_rows_kernel(const T* __restrict__ logits, const int64_t* __restrict__ target, float* __restrict__ loss,
+                   float* __restrict__ dlog, int B, int N, int64_t ignore_index, float smoothing,
+                   const float* __restrict__ scale, T* __restrict__ dls, float* __restrict__ ws) {
+  __shared__ float red[CE_RT];
+  __shared__ int cnt_s, last_s;
+  const int tid = threadIdx.x, gl = tid & 63, gr = tid >> 6;
+  if (tid == 0) cnt_s = 0;
+  __syncthreads();
+  int c = 0;
+  for (int b = tid; b < B; b += CE_RTHR) c += target[b] != ignore_index;
+  if (c) atomicAdd(&cnt_s, c);  // integer: order-independent
+  __syncthreads();
+  const float cnt = (float)cnt_s;
+  const float inv = cnt > 0.f ? 1.f / cnt : 0.f;
+  const float sc = scale != nullptr ? scale[0] : 0.f;
+  float lsum = 0.f;
+  for (int r0 = blockIdx.x * CE_RT; r0 < B; r0 += gridDim.x * CE_RT) {
+    const int b = r0 + gr;
+    const bool rv = b < B;
+    const T* row = logits + (size_t)(rv ? b : 0) * N;
+    const int64_t t = rv ? target[b] : ignore_index;
+    float v[VPL];
+#pragma unroll
+    for (int k = 0; k < VPL; ++k) {
+      const int n = gl + 64 * k;
+      v[k] = (rv && n < N) ? Cvt<T>::to_f(row[n]) : -INFINITY;
+    }
+    float mx = -INFINITY, sx = 0.f;
+#pragma unroll
+    for (int k = 0; k < VPL; ++k) {
+      mx = fmaxf(mx, v[k]);
+      if (gl + 64 * k < N) sx += rv ? v[k] : 0.f;
+    }
+    mx = group_max<64>(mx);
+    sx = group_sum<64>(sx);
+    float se = 0.f;
+#pragma unroll
+    for (int k = 0; k < VPL; ++k) {
+      v[k] = (gl + 64 * k < N && rv) ? __expf(v[k] - mx) : 0.f;
+      se += v[k];
+    }
+    se = group_sum<64>(se);
+    const float lse = mx + __logf(se);
+    const bool use = rv && t != ignore_index;
+    if (use && gl == 0) {
+      const float xt = (t >= 0 && t < N) ? Cvt<T>::to_f(row[t]) : NAN;  // bad target -> NaN loss
+      lsum += (1.f - smoothing) * (lse - xt) + smoothing * (lse - sx / (float)N);
+    }
+    if (rv) {
+      const float rs = 1.f / se;
+#pragma unroll
+      for (int k = 0; k < VPL; ++k) {
+        const int n = gl + 64 * k;
+        if (n < N) {
+          float d = 0.f;
+          if (use) {
+            const float oh = (n == t ? 1.f - smoothing : 0.f) + smoothing / (float)N;
+            d = (v[k] * rs - oh) * inv;
+          }
+          dlog[(size_t)b * N + n] = d;
+          if (dls != nullptr) dls[(size_t)b * N + n] = Cvt<T>::from_f(d * sc);
+        }
+      }
+    }
+  }
+  lsum = wave_sum(lsum);
+  if (gl == 0) red[gr] = lsum;
+  __syncthreads();
+  unsigned* ticket = reinterpret_cast<unsigned*>(ws + CE_MAXG);
+  if (tid == 0) {
+    float tl = 0.f;
+#pragma unroll
+    for (int i = 0; i < CE_RT; ++i) tl += red[i];
+    __hip_atomic_store(ws + blockIdx.x, tl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned k = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_s = k == gridDim.x - 1;
+    if (last_s) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+  }
+  __syncthreads();
+  if (!last_s || tid != 0) return;
+  float tl = 0.f;
+  for (int g = 0; g < (int)gridDim.x; ++g) tl += __hip_atomic_load(ws + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const float l = cnt > 0.f ? tl / cnt : NAN;
+  loss[0] = l;
+  if (scale != nullptr) loss[1] = l * sc;
+}
+
 // dlogits (storage T) = dlog * grad[0]
 template <typename T>
 __global__ void ce_bwd_kernel(const float* __restrict__ dlog, const float* __restrict__ grad,
@@ -328,6 +428,28 @@ void ce_fwd(at::Tensor logits, at::Tensor target, at::Tensor loss, at::Tensor dl
   if (scale.has_value()) {
     TORCH_CHECK(loss.numel() >= 2 && scale->scalar_type() == at::kFloat && dls->numel() == logits.numel() &&
                 dls->scalar_type() == logits.scalar_type());
+  }
+  if (B > 64 && N <= 64 * 16) {  // many rows: the multi-workgroup kernel (one read of each row)
+    static auto* wss = new std::map<int, at::Tensor>();  // per device: partials + ticket, zeroed once (never freed)
+    const int dev = logits.get_device();
+    auto it = wss->find(dev);
+    if (it == wss->end())
+      it = wss->emplace(dev, at::zeros({CE_MAXG + 4}, logits.options().dtype(at::kFloat))).first;
+    float* ws = it->second.data_ptr<float>();
+    const int G = (int)std::min<int64_t>((B + CE_RT - 1) / CE_RT, CE_MAXG);
+    DPA_DISPATCH_T(dt_of(logits), {
+      auto go = [&](auto vpl) {
+        hipLaunchKernelGGL((ce_fwd_rows_kernel<T, decltype(vpl)::value>), dim3(G), dim3(CE_RTHR), 0, cur_stream(),
+                           dptr<T>(logits), target.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                           dlog.data_ptr<float>(), B, N, ignore_index, (float)smoothing,
+                           scale.has_value() ? scale->data_ptr<float>() : nullptr,
+                           dls.has_value() ? dptr<T>(*dls) : nullptr, ws);
+      };
+      if (N <= 256) go(std::integral_constant<int, 4>{});
+      else go(std::integral_constant<int, 16>{});
+    });
+    DPA_CHECK_LAUNCH();
+    return;
   }
   DPA_DISPATCH_T(dt_of(logits), {
     auto go = [&](auto gl) {

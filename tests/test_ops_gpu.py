@@ -138,6 +138,27 @@ def test_cross_entropy(C, dtype):
     torch.testing.assert_close(a.grad.float(), r.grad, rtol=1e-2, atol=1e-3)
 
 
+@pytest.mark.parametrize("B,N", [(128, 1000), (257, 100), (96, 1024)])
+def test_cross_entropy_many_rows(C, B, N):
+    """B > 64: the multi-workgroup CE kernel (rows held in registers, loss partials summed
+    by the last-arriving workgroup) vs torch; called twice (the ticket re-arms itself)."""
+    from ddp_practice_amd.ops.head import cross_entropy
+
+    torch.manual_seed(1)
+    logits = (torch.randn(B, N, device=DEV) * 3).to(torch.bfloat16)
+    tgt = torch.randint(0, N, (B,), device=DEV)
+    tgt[5] = -100
+    r = logits.float().clone().requires_grad_()
+    ref = F.cross_entropy(r, tgt)
+    (ref * 3).backward()
+    for _ in range(2):
+        a = logits.clone().requires_grad_()
+        loss = cross_entropy(a, tgt)
+        torch.testing.assert_close(loss, ref, rtol=1e-5, atol=1e-5)
+        (loss * 3).backward()
+        torch.testing.assert_close(a.grad.float(), r.grad, rtol=1e-2, atol=1e-4)
+
+
 def test_accuracy(C):
     from ddp_practice_amd.ops.head import accuracy_
 
