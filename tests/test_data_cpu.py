@@ -112,3 +112,28 @@ def test_image_dataset_getitem_totensor_semantics():
     ds = ImageDataset(imgs, torch.tensor([3, 4]))
     x, y = ds[1]
     assert y == 4 and torch.allclose(x[0], imgs[1].float() / 255.0)
+
+
+def test_synthetic_imagenet_multichannel_loader():
+    """[N, C, H, W] uint8 datasets (the CLIs' --model resnet50 set): ToTensor items are
+    [C, H, W], and the loader's batches match a manual gather."""
+    import torch
+
+    from ddp_practice_amd.data import DeviceLoader, synthetic_imagenet
+
+    ds = synthetic_imagenet(10, seed=3, classes=7, hw=20)
+    assert ds.images.shape == (10, 3, 20, 20) and ds.sample_shape == (3, 20, 20)
+    assert int(ds.labels.max()) < 7
+    x, y = ds[4]
+    assert x.shape == (3, 20, 20) and torch.equal(x, ds.images[4].float() / 255.0) and y == int(ds.labels[4])
+    again = synthetic_imagenet(10, seed=3, classes=7, hw=20)
+    assert torch.equal(again.images, ds.images)  # deterministic
+    ld = DeviceLoader(ds, batch_size=4, device="cpu")
+    seen = 0
+    for imgs, labels in ld:
+        assert imgs.shape[1:] == (3, 20, 20)
+        for i in range(imgs.shape[0]):
+            src = int(ld._order[seen + i])
+            assert torch.equal(imgs[i], ds.images[src].float() / 255.0) and int(labels[i]) == int(ds.labels[src])
+        seen += imgs.shape[0]
+    assert seen == 10
