@@ -153,11 +153,14 @@ __device__ __forceinline__ float strided_rowsum(const float* __restrict__ src, i
   return acc;
 }
 
-// part: >= blockDim.x floats of LDS; ends with __syncthreads().
+// part: >= NTHR floats of LDS; ends with __syncthreads().  Every caller runs NTHR-thread
+// workgroups: the constant, not blockDim.x -- on gfx950 blockDim is a load from the hidden
+// kernel arguments, and the s_waitcnt vmcnt(0) before its use waited for every load the
+// kernel had issued so far (a whole memory round trip ahead of the slab loads, head .s).
 template <int C>
 __device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, float* beta_s, float* mean_s,
                                             float* istd_s, float* part, bool leader) {
-  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int tid = threadIdx.x, nthr = NTHR;
   if (bp.train) {
     constexpr int RL = 2 * C + 1;
     const int G = nthr / RL;
@@ -178,7 +181,9 @@ __device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, flo
     unsigned long long tk = 0;
     if (xon && tid == 0) tk = xgmi::xsite_ticket(bp.xs);  // latency hides behind the slab loads
     part[tid] = g < G ? strided_rowsum(bp.fslab, bp.nrows, RL, j, g, G) : 0.f;
+    DPA_STAMP(11);
     __syncthreads();
+    DPA_STAMP(12);
     if (tid < RL) {
       float t = 0.f;
       for (int gg = 0; gg < G; ++gg) t += part[gg * RL + tid];
@@ -284,10 +289,11 @@ struct BwdIn {
 };
 
 // Column sums of rows x RL floats (row-major) -> out[0..RL) in LDS, using the
-// whole workgroup; part: >= blockDim.x floats of LDS.  Ends with a barrier.
+// whole (NTHR-thread) workgroup; part: >= NTHR floats of LDS.  Ends with a barrier.
+// (NTHR, not blockDim.x: see bn_finalize)
 __device__ __forceinline__ void colsum_rows(const float* __restrict__ src, int rows, int RL, float* part,
                                             float* out) {
-  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int tid = threadIdx.x, nthr = NTHR;
   const int G = nthr / RL;
   const int j = tid % RL, g = tid / RL;
   part[tid] = g < G ? strided_rowsum(src, rows, RL, j, g, G) : 0.f;

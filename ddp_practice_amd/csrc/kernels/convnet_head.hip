@@ -116,6 +116,7 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
   __shared__ float dd_s[BMAX * NMAX];                         // (softmax - onehot) / count
   __shared__ int64_t tgt_s[BMAX];
   __shared__ float bias_s[NMAX];
+  __shared__ E wdummy_s[2];
   __shared__ uint8_t ix_s[BMAX * PP];
   __shared__ float xh_s[BMAX * PP];
   __shared__ float red[2][NT / 64];
@@ -128,21 +129,24 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
 
   DPA_STAMP(0);
   // 1. loads: this channel's pre-BN maps (two row pairs per pooled output) and W slice
+  // Every load below is unconditional (clamped index, the value discarded where out of
+  // range): a conditional load into a register array made hipcc branch around each load
+  // and wait vmcnt(0) after it -- one memory round trip per load (head_step .s, ROCm 7.2).
   P top[IT], bot[IT];
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
-    const int e = tid + i * NT;
-    if (e < NPO) {
-      const int b = e / PP, j = e % PP, ho = j / WO, wo = j % WO;
-      const P* src = reinterpret_cast<const P*>(y + (((size_t)b * C + c) * H + 2 * ho) * W + 2 * wo);
-      top[i] = src[0];
-      bot[i] = src[W / 2];
-    }
+    const int e = min(tid + i * NT, NPO - 1);
+    const int b = e / PP, j = e % PP, ho = j / WO, wo = j % WO;
+    const P* src = reinterpret_cast<const P*>(y + (((size_t)b * C + c) * H + 2 * ho) * W + 2 * wo);
+    top[i] = src[0];
+    bot[i] = src[W / 2];
   }
   // the loss' inputs, loaded by every workgroup now (only the last arriver uses them, but
   // it cannot know it is last yet): no dependent global load on its serial path later
-  const int64_t tgt_r = tid < B ? hs.target[tid] : hs.ignore_index;
-  const float bias_r = tid < N ? bfc[tid] : 0.f;
+  const int64_t tgt_ld = hs.target[min(tid, B - 1)];
+  const float bias_ld = bfc[min(tid, N - 1)];
+  const int64_t tgt_r = tid < B ? tgt_ld : hs.ignore_index;
+  const float bias_r = tid < N ? bias_ld : 0.f;
   const float scale_r = hs.scale != nullptr ? hs.scale[0] : 0.f;
   constexpr int WIT = (NMAX * PP + NT - 1) / NT;
   float wv_[WIT];
@@ -150,8 +154,12 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
   for (int i = 0; i < WIT; ++i) {
     const int e = tid + i * NT;
     const int n = e / PP, j = e % PP;
-    wv_[i] = (e < NMAX * PP && n < N) ? wfc[(size_t)n * K + c * PP + j] : 0.f;
+    const float v = wfc[(size_t)min(n, N - 1) * K + c * PP + j];  // unconditional (see above)
+    // a multiply, not a select: with a select (or a guarded use below) hipcc re-branches the
+    // load by the condition and waits for it inside the branch
+    wv_[i] = v * ((e < NMAX * PP && n < N) ? 1.f : 0.f);
   }
+  DPA_STAMP(8);
   // zero the tiles' padding (rows past B, k past 49 / N)
   {  // 16-B LDS writes (every tile is 16-B aligned and a whole number of 16-B chunks)
     auto zero = [&](E* t, int n) {
@@ -166,20 +174,21 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
     zero(dlt, NMAX * DLT_S);
     zero(wcl, NMAX * KP);
   }
+  DPA_STAMP(9);
   if (tid < BMAX) tgt_s[tid] = tgt_r;
   if (tid < NMAX) bias_s[tid] = bias_r;
+  DPA_STAMP(10);
   cb::bn_finalize<C>(bn, sc_s, beta_s, mean_s, istd_s, part_s, c == 0);  // ends with a barrier
   DPA_STAMP(1);
   // W slice -> tiles
 #pragma unroll
-  for (int i = 0; i < WIT; ++i) {
+  for (int i = 0; i < WIT; ++i) {  // unconditional stores (lanes past the slice write a dummy word)
     const int e = tid + i * NT;
-    if (e < NMAX * PP) {
-      const int n = e / PP, j = e % PP;
-      const E wq = Cvt<T>::from_f(wv_[i]);
-      wcl[n * KP + j] = wq;
-      wdl[j * WDL_S + n] = wq;
-    }
+    const bool ok = e < NMAX * PP;
+    const int ec = ok ? e : 0, n = ec / PP, j = ec % PP;
+    const E wq = Cvt<T>::from_f(wv_[i]);
+    *(ok ? &wcl[n * KP + j] : &wdummy_s[0]) = wq;
+    *(ok ? &wdl[j * WDL_S + n] : &wdummy_s[1]) = wq;
   }
   // 2. BN -> ReLU -> 2x2 max of this channel; pooled value, argmax|relu index, xhat.
   //    LDS now; the global copies (read by later kernels) are written after the ticket,
@@ -245,7 +254,7 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
   DPA_STAMP(3);
   const unsigned long long tk = tk_s;
   const uint32_t gen = (uint32_t)(tk >> 32);
-  const bool last = (uint32_t)tk == (uint32_t)(gridDim.x - 1);
+  const bool last = (uint32_t)tk == (uint32_t)(C - 1);  // grid = C workgroups (not gridDim: a hidden-arg load)
   // The last ticket re-arms the word for the next launch ((gen + 1) << 32: stream order, no
   // workgroup of this launch takes a ticket after it) and that same store releases the
   // waiting workgroups: with the speculative backward EVERY workgroup then sums the C
