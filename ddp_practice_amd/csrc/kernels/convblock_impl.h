@@ -137,20 +137,32 @@ struct BNParams {
 // a slab of up to RSUM_U * G rows costs one L2 round trip instead of one per
 // 4 rows (the partial-sum slabs are 64-256 rows: this was 3-5 serial trips).
 constexpr int RSUM_U = 24;
-__device__ __forceinline__ float strided_rowsum(const float* __restrict__ src, int rows, int RL, int j, int g,
-                                                int G) {
+template <typename F>
+__device__ __forceinline__ float strided_rowsum(const float* __restrict__ src, int rows, int RL, int j, int g, int G,
+                                                F&& after_issue) {
+  // The first batch is peeled out of the loop (at a loop header hipcc waits vmcnt(0) for the
+  // previous iteration's loads, which on entry also waited for every load the kernel had
+  // issued before), and the loads are unconditional (clamped row, masked by a multiply: a
+  // conditional load was branched around and its add waited right behind it) -- so the whole
+  // batch is issued behind the kernel's earlier loads instead of a round trip after them.
   float acc = 0.f;
-  for (int base = g; base < rows; base += RSUM_U * G) {
+  auto batch = [&](int base, bool first) {
     float v[RSUM_U];
 #pragma unroll
     for (int u = 0; u < RSUM_U; ++u) {
       const int rr = base + u * G;
-      v[u] = rr < rows ? src[(size_t)rr * RL + j] : 0.f;
+      v[u] = src[(size_t)min(rr, rows - 1) * RL + j] * (rr < rows ? 1.f : 0.f);
     }
+    if (first) after_issue();  // e.g. an atomic whose round trip then overlaps these loads
 #pragma unroll
     for (int u = 0; u < RSUM_U; ++u) acc += v[u];
-  }
+  };
+  batch(g, true);
+  for (int base = g + RSUM_U * G; base < rows; base += RSUM_U * G) batch(base, false);
   return acc;
+}
+__device__ __forceinline__ float strided_rowsum(const float* __restrict__ src, int rows, int RL, int j, int g, int G) {
+  return strided_rowsum(src, rows, RL, j, g, G, [] {});
 }
 
 // part: >= NTHR floats of LDS; ends with __syncthreads().  Every caller runs NTHR-thread
@@ -179,8 +191,17 @@ __device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, flo
     const int64_t nb0 = leader ? bp.nbt[0] : 0;
     const bool xon = bp.xs.active();
     unsigned long long tk = 0;
-    if (xon && tid == 0) tk = xgmi::xsite_ticket(bp.xs);  // latency hides behind the slab loads
-    part[tid] = g < G ? strided_rowsum(bp.fslab, bp.nrows, RL, j, g, G) : 0.f;
+    // the SyncBN ticket is taken right after the slab loads are issued: its round trip overlaps
+    // theirs (taken before them, its returned value's wait held the loads back)
+    auto ticket = [&] {
+      if (xon && tid == 0) tk = xgmi::xsite_ticket(bp.xs);
+    };
+    if (g < G) {
+      part[tid] = strided_rowsum(bp.fslab, bp.nrows, RL, j, g, G, ticket);
+    } else {
+      ticket();
+      part[tid] = 0.f;
+    }
     DPA_STAMP(11);
     __syncthreads();
     DPA_STAMP(12);
