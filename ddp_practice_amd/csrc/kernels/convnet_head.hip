@@ -45,7 +45,6 @@ constexpr int C = 32, H = 14, W = 14, HO = 7, WO = 7, PP = 49, K = C * PP;
 constexpr int BMAX = 64;   // images (4 MFMA row tiles)
 constexpr int NMAX = 16;   // classes (one MFMA column tile)
 constexpr int KP = 64;     // 49 fc inputs per channel, padded to 2 MFMA k-steps
-constexpr int IT = (BMAX * PP + NT - 1) / NT;  // pooled outputs per lane
 
 // state: int64[4] zero-initialised once: [0] {generation:32 | tickets:32} (the last
 // ticket stores (generation + 1) << 32: re-arm and release), [1] unused, [2] error word
@@ -92,7 +91,7 @@ __device__ __forceinline__ float gsum(float v) {
   return v;
 }
 
-template <typename T>
+template <typename T, int BM>  // BM: images the tiles are sized for (32 or BM)
 __global__ void __launch_bounds__(NT)
 head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__ wfc, const float* __restrict__ bfc,
                  T* __restrict__ logits, T* __restrict__ p_out, uint8_t* __restrict__ idx_out,
@@ -100,25 +99,26 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
   typedef MM<T> mm;
   typedef T E;  // operand tiles in the storage dtype (MM<T>::ld reads 8 of them)
   typedef typename Pair2<T>::type P;
+  constexpr int ITB = (BM * PP + NT - 1) / NT;  // pooled outputs per lane
   __shared__ float sc_s[C], beta_s[C], mean_s[C], istd_s[C];
   __shared__ float part_s[NT];
   // MFMA operand tiles (row-major, k contiguous: every fragment is one 16-B read)
-  __shared__ __attribute__((aligned(16))) E pcl[BMAX * KP];   // A fwd: p2 slice [b][j]
+  __shared__ __attribute__((aligned(16))) E pcl[BM * KP];   // A fwd: p2 slice [b][j]
   // transposed tiles' rows padded by 16 B: their column-wise 2-byte writes (lanes along
   // the rows) then spread over the banks instead of hitting one bank pair
-  constexpr int PCT_S = BMAX + 8, WDL_S = 32 + 8, DLT_S = BMAX + 8;
+  constexpr int PCT_S = BM + 8, WDL_S = 32 + 8, DLT_S = BM + 8;
   __shared__ __attribute__((aligned(16))) E pct[KP * PCT_S];  // B dW: p2 slice as [j][b]
   __shared__ __attribute__((aligned(16))) E wcl[NMAX * KP];   // B fwd: W slice [n][j]
   __shared__ __attribute__((aligned(16))) E wdl[KP * WDL_S];  // B dp2: W slice [j][n] (k = n padded to 32)
-  __shared__ __attribute__((aligned(16))) E dll[BMAX * 32];   // A dp2: dls [b][n]
+  __shared__ __attribute__((aligned(16))) E dll[BM * 32];   // A dp2: dls [b][n]
   __shared__ __attribute__((aligned(16))) E dlt[NMAX * DLT_S]; // A dW: dls as [n][b]
-  __shared__ float lg_s[BMAX * NMAX];                         // logits (rounded) / dls, f32
-  __shared__ float dd_s[BMAX * NMAX];                         // (softmax - onehot) / count
-  __shared__ int64_t tgt_s[BMAX];
+  __shared__ float lg_s[BM * NMAX];                         // logits (rounded) / dls, f32
+  __shared__ float dd_s[BM * NMAX];                         // (softmax - onehot) / count
+  __shared__ int64_t tgt_s[BM];
   __shared__ float bias_s[NMAX];
   __shared__ E wdummy_s[2];
-  __shared__ uint8_t ix_s[BMAX * PP];
-  __shared__ float xh_s[BMAX * PP];
+  __shared__ uint8_t ix_s[BM * PP];
+  __shared__ float xh_s[BM * PP];
   __shared__ float red[2][NT / 64];
   __shared__ unsigned long long tk_s;
   __shared__ int cnt_s;
@@ -132,9 +132,9 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
   // Every load below is unconditional (clamped index, the value discarded where out of
   // range): a conditional load into a register array made hipcc branch around each load
   // and wait vmcnt(0) after it -- one memory round trip per load (head_step .s, ROCm 7.2).
-  P top[IT], bot[IT];
+  P top[ITB], bot[ITB];
 #pragma unroll
-  for (int i = 0; i < IT; ++i) {
+  for (int i = 0; i < ITB; ++i) {
     const int e = min(tid + i * NT, NPO - 1);
     const int b = e / PP, j = e % PP, ho = j / WO, wo = j % WO;
     const P* src = reinterpret_cast<const P*>(y + (((size_t)b * C + c) * H + 2 * ho) * W + 2 * wo);
@@ -165,17 +165,17 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
     auto zero = [&](E* t, int n) {
       for (int e = tid; e < n * (int)sizeof(E) / 16; e += NT) reinterpret_cast<f32x4*>(t)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
-    static_assert((BMAX * KP) % 8 == 0 && (KP * PCT_S) % 8 == 0 && (BMAX * 32) % 8 == 0 && (KP * WDL_S) % 8 == 0 &&
+    static_assert((BM * KP) % 8 == 0 && (KP * PCT_S) % 8 == 0 && (BM * 32) % 8 == 0 && (KP * WDL_S) % 8 == 0 &&
                   (NMAX * DLT_S) % 8 == 0 && (NMAX * KP) % 8 == 0, "head tiles: whole 16-B chunks");
-    zero(pcl, BMAX * KP);
+    zero(pcl, BM * KP);
     zero(pct, KP * PCT_S);
-    zero(dll, BMAX * 32);
+    zero(dll, BM * 32);
     zero(wdl, KP * WDL_S);
     zero(dlt, NMAX * DLT_S);
     zero(wcl, NMAX * KP);
   }
   DPA_STAMP(9);
-  if (tid < BMAX) tgt_s[tid] = tgt_r;
+  if (tid < BM) tgt_s[tid] = tgt_r;
   if (tid < NMAX) bias_s[tid] = bias_r;
   DPA_STAMP(10);
   cb::bn_finalize<C>(bn, sc_s, beta_s, mean_s, istd_s, part_s, c == 0);  // ends with a barrier
@@ -193,12 +193,12 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
   // 2. BN -> ReLU -> 2x2 max of this channel; pooled value, argmax|relu index, xhat.
   //    LDS now; the global copies (read by later kernels) are written after the ticket,
   //    so the hand-off's vmcnt(0) drains only the partial-logit stores
-  T pvr[IT], xqr[IT];
-  uint8_t ixr[IT];
+  T pvr[ITB], xqr[ITB];
+  uint8_t ixr[ITB];
   {
     const float sc = sc_s[c], bt = beta_s[c], mn = mean_s[c], is = istd_s[c];
 #pragma unroll
-    for (int i = 0; i < IT; ++i) {
+    for (int i = 0; i < ITB; ++i) {
       const int e = tid + i * NT;
       if (e < NPO) {
         const int b = e / PP, j = e % PP;
@@ -217,7 +217,7 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
   }
   auto store_pooled = [&]() {
 #pragma unroll
-    for (int i = 0; i < IT; ++i) {
+    for (int i = 0; i < ITB; ++i) {
       const int e = tid + i * NT;
       if (e < NPO) {
         const size_t o = (size_t)(e / PP) * K + c * PP + e % PP;
@@ -286,7 +286,7 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
   const bool writer = hs.do_bwd ? c == 0 : true;
   DPA_STAMP(4);
   // 4. logits = sum of the C partials + bias, rounded to the storage dtype (every load sc1)
-  constexpr int OIT = BMAX * NMAX / NT;
+  constexpr int OIT = BM * NMAX / NT;
   T lgr[OIT];
 #pragma unroll
   for (int k = 0; k < OIT; ++k) {
@@ -411,7 +411,7 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
   {  // dW rows n (16), columns 16w..16w+15 of this channel, K = images
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < BMAX / 32; ++s) {
+    for (int s = 0; s < BM / 32; ++s) {
       const typename mm::frag a = mm::ld(&dlt[r * DLT_S + 32 * s + 8 * q]);
       const typename mm::frag bf = mm::ld(&pct[(16 * wv + r) * PCT_S + 32 * s + 8 * q]);
       acc = mm::mma(a, bf, acc);
@@ -463,7 +463,8 @@ bool resident(at::ScalarType st) {
   bool ok = true;
   with_t(dt_of(at::empty({0}, at::TensorOptions().dtype(st))), [&](auto tag) {
     typedef decltype(tag) T;
-    ok = co_resident(reinterpret_cast<const void*>(&head_step_kernel<T>), C, NT, 0);
+    ok = co_resident(reinterpret_cast<const void*>(&head_step_kernel<T, 32>), C, NT, 0) &&
+         co_resident(reinterpret_cast<const void*>(&head_step_kernel<T, BMAX>), C, NT, 0);
   });
   return ok;
 }
@@ -531,7 +532,9 @@ void head_step(at::Tensor y2, at::Tensor fslab2, at::Tensor fstats2, at::Tensor 
   with_t(dt_of(y2), [&](auto tag) {
     typedef decltype(tag) T;
     if (bwd) TORCH_CHECK(dls->scalar_type() == y2.scalar_type() && dp2->scalar_type() == y2.scalar_type());
-    hipLaunchKernelGGL(head_step_kernel<T>, dim3(C), dim3(NT), 0, cur_stream(), dptr<T>(y2), bp,
+    // tiles sized for 32 images where the batch fits (fewer load / zeroing / MFMA iterations)
+    auto kern = B <= 32 ? head_step_kernel<T, 32> : head_step_kernel<T, BMAX>;
+    hipLaunchKernelGGL(kern, dim3(C), dim3(NT), 0, cur_stream(), dptr<T>(y2), bp,
                        wfc.data_ptr<float>(), bfc.data_ptr<float>(), dptr<T>(logits), dptr<T>(p2),
                        idx2.data_ptr<uint8_t>(), dptr<T>(xh2), B, N, hs);
   });
