@@ -572,6 +572,8 @@ struct GatherIn {
   int* ctr = nullptr;              // [0] step, [1] arrivals (self-resetting)
   int64_t* lab_out = nullptr;      // [B]
   float scale = 1.f, shift = 0.f;
+  int nimg = 0;                    // B (the launch has nimg * nsplit workgroups; not gridDim,
+                                   // a hidden-argument load with its own wait on gfx950)
 };
 
 // ---------------------------------------------------------------------------
@@ -764,7 +766,7 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
     static_assert(HW % 4 == 0 && W % 4 == 0, "4-pixel groups stay inside a row");
     constexpr int G4 = HW / 4, GIT = (G4 + NTHR - 1) / NTHR;
     const int step = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile int*>(gin.ctr));
-    long long pos = (long long)step * (gridDim.x / nsplit) + b;
+    long long pos = (long long)step * gin.nimg + b;
     pos = pos < gin.order_len ? pos : gin.order_len - 1;  // never taken with a correct host-side batch count
     const int64_t src = gin.order[pos];
     const uint32_t* s4 = reinterpret_cast<const uint32_t*>(gin.imgs + src * HW);
@@ -795,7 +797,7 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
     // launch reads it after this one completes)
     if (tid == 0) {
       const int arrived = __hip_atomic_fetch_add(&gin.ctr[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (arrived == (int)gridDim.x - 1) {
+      if (arrived == gin.nimg * nsplit - 1) {
         __hip_atomic_store(&gin.ctr[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&gin.ctr[0], step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }

@@ -425,6 +425,7 @@ void conv1_fwd_pack_gather(at::Tensor x, at::Tensor w1, at::Tensor b1, at::Tenso
   gin.lab_out = lab_out.data_ptr<int64_t>();
   gin.scale = (float)scale;
   gin.shift = (float)shift;
+  gin.nimg = (int)B;
   with_t(dt_of(x), [&](auto tag) {
     typedef decltype(tag) T;
     cb::WPack<T> pk{w2.data_ptr<float>(), dptr<T>(wpk_f), dptr<T>(wpk_d)};

@@ -184,7 +184,9 @@ __global__ void __launch_bounds__(THR)
 amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ tracker, float* __restrict__ found_inf,
                      unsigned long long* __restrict__ sync, float lr, float momentum, float dampening, float wd,
                      int nesterov, int maximize, float growth, float backoff, int interval,
-                     xgmi::XSite xg, int* __restrict__ err, long long barrier_ticks, SlabSrc ss) {
+                     xgmi::XSite xg, int* __restrict__ err, long long barrier_ticks, SlabSrc ss, int grid) {
+  // grid == the launch's workgroup count, passed in: gridDim is a load from the hidden kernel
+  // arguments on gfx950, and its wait at the top of the kernel came before the table loads
   constexpr int BG = THR * U;  // float4 granules per workgroup
   __shared__ int soff[MAXT + 1];
   __shared__ int snum[MAXT];
@@ -206,7 +208,7 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
   // the barrier generation is only used by lane 0: issued after the table
   // barrier, its load stays in flight (no LDS round trip) with the gradients'
   unsigned long long gen = 0;
-  if (tid == 0 && gridDim.x > 1)
+  if (tid == 0 && grid > 1)
     gen = __hip_atomic_fetch_add(&sync[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   unsigned long long tk = 0;
   if (XG && tid == 0) tk = xgmi::xsite_ticket(xg);
@@ -223,7 +225,7 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
   f32x4 gv[U], pv[U], bv[U];
   int tt[U];  // tensor of each granule (its offset is recomputed after the barrier)
   bool bad = false;
-  const int nreg = (int)gridDim.x - ss.nblk;  // granule workgroups; the rest own the slab region
+  const int nreg = grid - ss.nblk;  // granule workgroups; the rest own the slab region
   // slab workgroup lane (< SS_COLS): its column's sum, tensor and element, param / buffer
   float st_sum = 0.f, st_p = 0.f, st_b = 0.f;
   int st_t = -1, st_e = 0;
@@ -339,11 +341,11 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
   // workgroup that reads it late must not unscale with the next step's value
   const float inv = 1.f / scale[0];
   const bool block_bad = __syncthreads_or(bad);
-  if (gridDim.x == 1) {  // uniform: one workgroup needs no grid barrier
+  if (grid == 1) {  // uniform: one workgroup needs no grid barrier
     if (tid == 0) s_bad = block_bad;
   } else if (tid == 0) {
     unsigned long long* word = &sync[1 + (gen & 1)];
-    const unsigned long long G = gridDim.x;
+    const unsigned long long G = (unsigned long long)grid;
     __hip_atomic_fetch_add(word, 1ull | ((unsigned long long)block_bad << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long v;
@@ -784,7 +786,7 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
                        reinterpret_cast<unsigned long long*>(sync.data_ptr<int64_t>()), (float)lr, (float)momentum,
                        (float)dampening, (float)wd, (int)nesterov, (int)maximize, (float)growth, (float)backoff,
                        (int)interval, xg, reinterpret_cast<int*>(sync.data_ptr<int64_t>() + 3),
-                       (long long)(kBarrierSeconds * 1e8), ss);
+                       (long long)(kBarrierSeconds * 1e8), ss, grid);
   };
   if (xc) {
     const xgmi::XSite xg = xc->grad_site();
