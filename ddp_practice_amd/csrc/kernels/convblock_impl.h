@@ -660,23 +660,28 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
   // --- stage weights (batched float4 reads in natural [co][ci][kh][kw] order,
   //     scattered LDS writes to wl[co][(kh*5+kw)*CIN + ci])
   const T zero = Cvt<T>::from_f(0.f);
-  // WPK 1: the packed tile's loads are issued here and land in LDS just before
-  // the compute barrier, so their latency overlaps the prologue's own loads
+  // WPK 1: the pre-packed tile goes global -> LDS directly (global_load_lds_dwordx4: no
+  // VGPRs, so it can be issued with the prologue's first loads without register pressure);
+  // with a BN prologue it is issued before the statistics reduction, whose loads and barrier
+  // then cover its latency (the barrier's vmcnt(0) retires it; the tile is read only after
+  // the compute barrier).  LDS destination = wave-uniform base + lane x 16 B: wl is a
+  // contiguous run of 16-B chunks, chunk c at byte 16c.
   constexpr int WN16 = WPK == 1 ? COUT * KPW * (int)sizeof(T) / 16 : 1;
   constexpr int WIT = (WN16 + NTHR - 1) / NTHR;
-  uint4 wreg[WPK == 1 ? WIT : 1];
-  // with a BN prologue (PRO 1/2) the tile's loads are issued after the
-  // prologue's statistics barrier: a barrier waits for every outstanding load,
-  // and the tile is needed only at the MFMA loop
   auto load_wpk = [&]() {
     if constexpr (WPK == 1) {
       static_assert((COUT * KPW * sizeof(T)) % 16 == 0, "packed weight tile must be whole 16-B chunks");
       static_assert(COUT * KPW == (MODE == 2 ? W2D_LEN : W2F_LEN), "pre-packed weights exist for layer 2 only");
+      typedef __attribute__((address_space(3))) void* lds_ptr_t;
       const uint4* src = reinterpret_cast<const uint4*>(wpk);
-      // unconditional (clamped) loads: a conditional load into the array made hipcc keep
-      // it in scratch and wait vmcnt(0) after every single load
+      uint4* dstl = reinterpret_cast<uint4*>(wl);
+      const int wv0 = (tid >> 6) * 64, ln = tid & 63;
 #pragma unroll
-      for (int i = 0; i < WIT; ++i) wreg[i] = src[min(tid + i * NTHR, WN16 - 1)];
+      for (int i = 0; i < WIT; ++i) {
+        const int c0 = i * NTHR + wv0;  // this wave's first chunk (wave-uniform)
+        if (c0 + ln < WN16)             // lanes past the tile are masked off: they write nothing
+          __builtin_amdgcn_global_load_lds(src + c0 + ln, (lds_ptr_t)(dstl + c0), 16, 0, 0);
+      }
     }
   };
   if constexpr (WPK == 1) {
@@ -830,8 +835,8 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
           }
         }
       }
-      bn_finalize<CIN>(pin.bn, sc_s, beta_s, mean_s, istd_s, part, bid == 0);
       load_wpk();
+      bn_finalize<CIN>(pin.bn, sc_s, beta_s, mean_s, istd_s, part, bid == 0);
       DPA_STAMP(3);
 #pragma unroll
       for (int i = 0; i < IT8; ++i) {
@@ -872,8 +877,8 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
           bot[i] = src[W];  // next input row (2W elements = W pairs)
         }
       }
-      bn_finalize<CIN>(pin.bn, sc_s, beta_s, mean_s, istd_s, part, bid == 0);
       load_wpk();
+      bn_finalize<CIN>(pin.bn, sc_s, beta_s, mean_s, istd_s, part, bid == 0);
       DPA_STAMP(3);
       // the pooled map / index / xhat outputs (for the backward) are written by all
       // nsplit workgroups of the image, each its share (was: split 0 alone)
@@ -902,9 +907,9 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
       BnBwdStage8<T, CIN, H, W, NTHR> st;
       st.load(bin, b);
       DPA_STAMP(8);
+      load_wpk();
       bn_bwd_coef<CIN, T>(bin, coef, part, sums, bid == 0);
       load_epi();
-      load_wpk();
       DPA_STAMP(3);
       st.emit(coef, [&](int h, int ww, int c0, uint4 q00, uint4 q01, uint4 q10, uint4 q11) {
         *reinterpret_cast<uint4*>(&img[imo((h + 2) * WPD + (ww + 2), c0)]) = q00;
@@ -916,9 +921,9 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
       BnBwdStage<T, CIN, H, W, NTHR> st;
       st.load(bin, b);
       DPA_STAMP(8);
+      load_wpk();
       bn_bwd_coef<CIN, T>(bin, coef, part, sums, bid == 0);
       load_epi();
-      load_wpk();
       DPA_STAMP(3);
       st.emit(coef, [&](int c, int h, int ww, T v00, T v01, T v10, T v11) {
         img[imo((h + 2) * WPD + (ww + 2), c)] = v00;
@@ -928,12 +933,6 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
       });
     }
     store_epi();
-  }
-  if constexpr (WPK == 1) {
-    uint4* dst = reinterpret_cast<uint4*>(wl);
-#pragma unroll
-    for (int i = 0; i < WIT; ++i)
-      if (tid + i * NTHR < WN16) dst[tid + i * NTHR] = wreg[i];
   }
   DPA_STAMP(4);
   __syncthreads();
