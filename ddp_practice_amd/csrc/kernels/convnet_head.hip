@@ -423,10 +423,15 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
       if (n < N && j < PP) hs.dwfc[(size_t)n * K + c * PP + j] = acc[i];
     }
   }
-  if (c == 0 && tid < N) {
+  if (c == 0) {  // fc bias gradient: 16 lanes per class (a serial loop over the batch in one
+                 // lane made workgroup 0, and so the launch, ~1 us longer)
+    static_assert(NT == 16 * NMAX, "dbfc: one 16-lane group per class");
+    const int n = tid / 16, l = tid % 16;
     float a = 0.f;
-    for (int b = 0; b < B; ++b) a += lg_s[b * NMAX + tid];
-    hs.dbfc[tid] = a;
+    if (n < N)
+      for (int b = l; b < B; b += 16) a += lg_s[b * NMAX + n];
+    a = gsum<16>(a);
+    if (n < N && l == 0) hs.dbfc[n] = a;
   }
   s1 = wave_sum(s1);
   s2 = wave_sum(s2);
