@@ -196,12 +196,20 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
   __shared__ int s_bad;
   const int tid = threadIdx.x;
   const int n = L.n;
-  if (tid <= n) soff[tid] = (int)L.chunk_off[tid];
-  if (tid < n) {
-    snum[tid] = (int)L.numel[tid];
-    sp0[tid] = L.p0[tid];
-    sp1[tid] = L.p1[tid];
-    sp2[tid] = L.p2[tid];
+  {  // the table: every load issued before any LDS write (clamped index; a guarded load was
+     // branched and waited for before the next group's loads were issued)
+    const int ti = min(tid, MAXT - 1);
+    const int64_t co = L.chunk_off[min(tid, MAXT)], nu = L.numel[ti];
+    float* const a0 = L.p0[ti];
+    float* const a1 = L.p1[ti];
+    float* const a2 = L.p2[ti];
+    if (tid <= n) soff[tid] = (int)co;
+    if (tid < n) {
+      snum[tid] = (int)nu;
+      sp0[tid] = a0;
+      sp1[tid] = a1;
+      sp2[tid] = a2;
+    }
   }
   __syncthreads();
   const int total = soff[n];

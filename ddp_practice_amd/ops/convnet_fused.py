@@ -65,8 +65,17 @@ def _fused_site_engine(comm, batch: int, dtype: torch.dtype):
     Every workgroup of such a launch polls the peers' rows, so the launch is only
     taken when all its workgroups fit on the device at once (occupancy x CUs,
     ``convnet.sites_resident``); DPA_FUSED_SYNC=0 forces the launch-per-collective
-    path (A/B runs)."""
-    if os.environ.get("DPA_FUSED_SYNC", "1") == "0":
+    path (A/B runs).
+
+    Measured on one MI355X shared by the ranks: the in-kernel SyncBN exchange completes
+    with 2 ranks but stalls with 3 or 4 (the fused gradient exchange of the AMP-SGD launch
+    completes with 3), profiles/r2d_fused_sync_multirank.txt.  Until that is understood,
+    3+ ranks take the launch-per-collective SyncBN path unless DPA_FUSED_SYNC=1 forces the
+    sites."""
+    flag = os.environ.get("DPA_FUSED_SYNC")
+    if flag == "0":
+        return None
+    if flag != "1" and getattr(comm, "world_size", 1) > 2:
         return None
     xc = getattr(comm, "xgmi", None)
     if xc is None:
