@@ -262,6 +262,8 @@ def run_rank(args) -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     gpu = torch.cuda.is_available()
     local_rank = 0 if args.share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
+    if args.share_gpu:
+        os.environ["DPA_SHARED_GPU"] = "1"  # ranks share one device (ops/convnet_fused.py)
     if gpu:
         torch.cuda.set_device(local_rank)
         dev = torch.device("cuda", local_rank)
@@ -484,6 +486,8 @@ def bench_resnet(args):
         os.environ["DPA_COMM"] = args.comm
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = 0 if args.share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
+    if args.share_gpu:
+        os.environ["DPA_SHARED_GPU"] = "1"  # ranks share one device (ops/convnet_fused.py)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist_path = world > 1 or args.force_collectives

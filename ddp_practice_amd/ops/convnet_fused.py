@@ -67,15 +67,16 @@ def _fused_site_engine(comm, batch: int, dtype: torch.dtype):
     ``convnet.sites_resident``); DPA_FUSED_SYNC=0 forces the launch-per-collective
     path (A/B runs).
 
-    Measured on one MI355X shared by the ranks: the in-kernel SyncBN exchange completes
-    with 2 ranks but stalls with 3 or 4 (the fused gradient exchange of the AMP-SGD launch
-    completes with 3), profiles/r2d_fused_sync_multirank.txt.  Until that is understood,
-    3+ ranks take the launch-per-collective SyncBN path unless DPA_FUSED_SYNC=1 forces the
-    sites."""
+    The residency check is per rank, which is what matters with one rank per GPU.  Ranks
+    SHARING one GPU (DPA_SHARED_GPU=1, bench.py --share-gpu) need all their launches'
+    workgroups resident together: at batch 32 that holds for 2 ranks but not for 3 or 4,
+    which then stall in the exchange (with batch 8 they complete;
+    profiles/r2d_fused_sync_multirank.txt).  So 3+ ranks sharing a GPU take the
+    launch-per-collective path unless DPA_FUSED_SYNC=1 forces the sites."""
     flag = os.environ.get("DPA_FUSED_SYNC")
     if flag == "0":
         return None
-    if flag != "1" and getattr(comm, "world_size", 1) > 2:
+    if flag != "1" and os.environ.get("DPA_SHARED_GPU") == "1" and getattr(comm, "world_size", 1) > 2:
         return None
     xc = getattr(comm, "xgmi", None)
     if xc is None:
