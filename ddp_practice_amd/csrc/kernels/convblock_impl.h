@@ -400,18 +400,19 @@ struct BnBwdStage {
     const T* yb = bi.y + (size_t)b * C * H * W;
     const T* dpb = bi.dp + (size_t)b * C * PP;
     const uint8_t* ib = bi.idx + (size_t)b * C * PP;
+    // unconditional loads (clamped window; emit() skips the out-of-range ones): guarded
+    // loads were branched around and waited for group by group (conv2_bwd / wgrad1 .s,
+    // scripts/asm_loads.py)
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-      const int e = threadIdx.x + i * NT_;
-      const int c = e / CPP, pix = e % CPP, ho = ho0 + pix / WO, wo = pix % WO;
-      if (e < NWIN && ho < HO) {
-        const P* src = reinterpret_cast<const P*>(yb + ((size_t)c * H + 2 * ho) * W + 2 * wo);
-        top[i] = src[0];
-        bot[i] = src[W / 2];
-        const int ew = c * PP + ho * WO + wo;
-        g[i] = dpb[ew];
-        ix[i] = ib[ew];
-      }
+      const int e = min((int)threadIdx.x + i * NT_, NWIN - 1);
+      const int c = e / CPP, pix = e % CPP, ho = min(ho0 + pix / WO, HO - 1), wo = pix % WO;
+      const P* src = reinterpret_cast<const P*>(yb + ((size_t)c * H + 2 * ho) * W + 2 * wo);
+      top[i] = src[0];
+      bot[i] = src[W / 2];
+      const int ew = c * PP + ho * WO + wo;
+      g[i] = dpb[ew];
+      ix[i] = ib[ew];
     }
   }
 
