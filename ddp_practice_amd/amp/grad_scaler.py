@@ -155,7 +155,10 @@ class GradScaler:
             # 0-d scale: a 0-d loss stays 0-d, so backward needs no sum-to-shape reduction
             s0 = self._scale.to(outputs.device, non_blocking=True).view(())
             ce = getattr(outputs, "_dpa_ce", None)
-            if ce is not None and ce[1] is self._scale and outputs.requires_grad and outputs.dim() == 0:
+            # the pre-scaled value is handed out once (see _ScaledLossFn); a second scale() of
+            # the same loss (logging, a retry) takes the generic multiply below
+            if (ce is not None and ce[1] is self._scale and getattr(ce[0], "scaled", None) is not None
+                    and outputs.requires_grad and outputs.dim() == 0):
                 # native CE loss: its kernel already wrote loss*scale and d(scale*loss)/dlogits
                 node = ce[0]
                 scaled = _ScaledLossFn.apply(outputs, self._scale, node)

@@ -158,19 +158,24 @@ class SGD(Optimizer):
     def _large_table(self, params, grads, bufs, first):
         """Device tensor table of the large fused step, cached per set of pointers (DDP
         bucket-view grads and the optimizer state keep them fixed; freshly allocated
-        grads may not).  A table first built during graph capture stays referenced for
-        the life of the optimizer (the graph reads it on every replay)."""
-        key = (tuple(p.data_ptr() for p in params), tuple(g.data_ptr() for g in grads),
-               tuple(b.data_ptr() for b in bufs), tuple(first))
+        grads may not).  Any table looked up during graph capture -- built then, or an
+        eager warm-up's table reused from the cache -- stays referenced for the life of
+        the optimizer (the graph reads it on every replay).  The key carries every
+        tensor's size too: memory reused at the same address for a different size must
+        not hit a stale table."""
+        key = (tuple((p.data_ptr(), p.numel()) for p in params), tuple((g.data_ptr(), g.numel()) for g in grads),
+               tuple((b.data_ptr(), b.numel()) for b in bufs), tuple(first))
         cache = self.__dict__.setdefault("_amp_tables", {})
         t = cache.get(key)
         if t is None:
             t = _load_ext().optim.amp_sgd_table(params, grads, bufs, first)
-            if torch.cuda.is_current_stream_capturing():
-                self.__dict__.setdefault("_amp_tables_pinned", []).append(t)
             if len(cache) >= 8:  # eager tables: the allocator's stream order makes freeing safe
                 cache.pop(next(iter(cache)))
             cache[key] = t
+        if torch.cuda.is_current_stream_capturing():
+            pinned = self.__dict__.setdefault("_amp_tables_pinned", [])
+            if not any(x is t for x in pinned):
+                pinned.append(t)
         return t
 
     @torch.no_grad()

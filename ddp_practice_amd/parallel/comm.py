@@ -415,7 +415,7 @@ def setup_xgmi(rc: "RcclCommunicator", store, key: str) -> str:
     rc.native.all_reduce(ok, "min")
     if ok.item() != 1.0:
         return f"off (setup failed: {err or 'on a peer'})"
-    good, err = _xgmi_selftest(rc, x, ts_max > 0)
+    good, err = _xgmi_selftest(rc, x, max(ts_max, 0))
     if not good:
         return f"off (self-test failed: {err or 'on a peer'})"
     if ts_max > 0 and mode == "auto" and os.environ.get("DPA_XGMI_PROBE", "1") != "0":
@@ -429,26 +429,40 @@ def setup_xgmi(rc: "RcclCommunicator", store, key: str) -> str:
 def _probe_twoshot(rc: "RcclCommunicator", x, lo: int, hi: int) -> int:
     """Largest probed size in (lo, hi] up to which the two-shot beats RCCL on this node
     (fp32, 5 timed repetitions after 2 warm-ups; each rank's times max-reduced so
-    every rank picks the same bound).  Returns 0 if RCCL wins at the smallest size."""
+    every rank picks the same bound).  Returns 0 if RCCL wins at the smallest size.
+
+    Every decision is made from max-reduced values only: a rank whose engine failed
+    (an exception, or its error word set) contributes a failure flag to the same
+    reduction, so every rank leaves the probe at the same size with the same bound and
+    the ranks' collective sequences stay identical."""
     sizes = [b for b in (2 << 20, 8 << 20, 32 << 20, 128 << 20) if lo < b <= hi] or [hi]
     best = 0
     for nb in sizes:
         t = torch.ones(nb // 4, device=rc.device)
-        times = torch.zeros(2, device=rc.device)
+        times = torch.zeros(3, device=rc.device)  # [two-shot s, RCCL s, any local failure]
+        failed = False
         for i, fn in enumerate((lambda: x.all_reduce_twoshot(t), lambda: rc.native.all_reduce(t, "sum"))):
-            for _ in range(2):
-                fn()
-            torch.cuda.synchronize(rc.device)
-            rc.native.barrier()
-            t0 = time.perf_counter()
-            for _ in range(5):
-                fn()
-            torch.cuda.synchronize(rc.device)
-            times[i] = time.perf_counter() - t0
+            try:
+                for _ in range(2):
+                    fn()
+                torch.cuda.synchronize(rc.device)
+                rc.native.barrier()
+                t0 = time.perf_counter()
+                for _ in range(5):
+                    fn()
+                torch.cuda.synchronize(rc.device)
+                times[i] = time.perf_counter() - t0
+            except Exception:  # noqa: BLE001 - only the engine may throw: recorded as this rank's failure
+                if i == 1:
+                    raise
+                failed = True
+                rc.native.barrier()  # the barrier the skipped timing loop would have issued
+        if failed or x.error() != 0:
+            times[2] = 1.0
         rc.native.all_reduce(times, "max")
-        if x.error() != 0:
+        ts, rccl, bad = times.tolist()
+        if bad != 0.0:
             return 0
-        ts, rccl = times.tolist()
         if ts <= rccl:
             best = nb
         else:
@@ -456,17 +470,24 @@ def _probe_twoshot(rc: "RcclCommunicator", x, lo: int, hi: int) -> int:
     return best
 
 
-def _xgmi_selftest(rc: "RcclCommunicator", x, twoshot: bool = False) -> tuple[bool, str]:
+def _xgmi_selftest(rc: "RcclCommunicator", x, twoshot_max_bytes: int = 0) -> tuple[bool, str]:
     """Engine vs RCCL on a few sizes/dtypes/ops.  Per case, every rank issues the same
     RCCL collectives (reference all-reduce, cross-rank equality all-gather, vote); the
-    vote is a min all-reduce so all ranks leave the loop together."""
+    vote is a min all-reduce so all ranks leave the loop together.
+
+    ``twoshot_max_bytes`` > 0 adds two-shot cases sized inside that bound (the engine
+    counts it as fp32 elements for every dtype), so a small DPA_XGMI_TWOSHOT_MAX_BYTES
+    can never turn a valid setting into a failed vote (and the engine off)."""
     g = torch.Generator(device="cpu").manual_seed(1234 + rc.rank)
     why = ""
     vote = torch.ones(1, device=rc.device)
     cases = [(33, torch.float32, "sum", 1), (4099, torch.float32, "sum", 1), (29034, torch.float32, "sum", 1),
              (8195, torch.bfloat16, "sum", 1), (1000, torch.float32, "max", 1)]
-    if twoshot:
-        cases += [(1 << 20, torch.float32, "sum", 2), (700001, torch.bfloat16, "sum", 2)]
+    ts_elems = int(twoshot_max_bytes) // 4
+    if ts_elems > 0:
+        # a whole-chunk fp32 size and an odd (ragged-tail) bf16 size, both within the bound
+        cases += [(min(1 << 20, ts_elems), torch.float32, "sum", 2),
+                  (max(1, min(700001, ts_elems - 1)), torch.bfloat16, "sum", 2)]
     for n, dt, op, how in cases:
         t = torch.randn(n, generator=g).to(device=rc.device, dtype=dt)
         mine = torch.zeros_like(t)

@@ -26,6 +26,10 @@ class _Native:
         dist.all_reduce(out, op=r)
         return out
 
+    def barrier(self):
+        self.calls += 1
+        dist.barrier()
+
     def all_gather(self, out, t):
         self.calls += 1
         parts = list(out.view(dist.get_world_size(), -1).unbind(0))
@@ -55,8 +59,15 @@ class _Engine:
         if self.rank == self.bad and self.bad_kind == "oneshot":
             out.add_(1.0)
 
-    def all_reduce_twoshot(self, t, op, out):
-        out.copy_(self._sum(t, op))
+    def all_reduce_twoshot(self, t, op="sum", out=None):
+        if self.rank == self.bad and self.bad_kind == "twoshot_err":
+            self.err = 1  # a timed-out exchange: the engine's error word, no exception
+        if self.rank == self.bad and self.bad_kind == "twoshot_raise":
+            raise RuntimeError("two-shot launch failed on this rank")
+        # the probe only times the engine: no stand-in gloo traffic that a failing rank
+        # would leave unmatched (the real engine's peers time out instead)
+        r = t.clone() if self.local_only else self._sum(t, op)
+        (t if out is None else out).copy_(r)
 
     def site_probe(self, site, t, o, nblk):
         s = self._sum(t, "sum")
@@ -64,14 +75,19 @@ class _Engine:
             raise RuntimeError("site probe failed on this rank")
         o.copy_(s.repeat(nblk))
 
+    err = 0
+    local_only = False
+
     def error(self):
-        return 0
+        return self.err
 
     def error_string(self):
         return ""
 
 
-def run(rank, world, port, bad, bad_kind, q):
+def run(rank, world, port, bad, bad_kind, *rest):
+    q = rest[-1]
+    ts_max = rest[0] if len(rest) > 1 else 32 << 20  # optional two-shot bound (bytes)
     try:
         os.environ.update(client_env(rank, world, port))
         dist.init_process_group("gloo")
@@ -79,12 +95,33 @@ def run(rank, world, port, bad, bad_kind, q):
         from ddp_practice_amd.parallel.comm import _xgmi_selftest
 
         rc = _RC(rank, world)
-        good, why = _xgmi_selftest(rc, _Engine(rank, bad, bad_kind), twoshot=True)
+        good, why = _xgmi_selftest(rc, _Engine(rank, bad, bad_kind), twoshot_max_bytes=ts_max)
         # every rank issued the same number of collectives: the call sequences stayed matched
         calls = torch.tensor([rc.native.calls])
         every = [torch.zeros(1, dtype=calls.dtype) for _ in range(world)]
         dist.all_gather(every, calls)
         dist.destroy_process_group()
         q.put((rank, "ok", (good, why, [int(c) for c in every])))
+    except Exception:  # noqa: BLE001
+        q.put((rank, "err", traceback.format_exc()))
+
+
+def run_probe(rank, world, port, bad, bad_kind, q):
+    """parallel/comm._probe_twoshot with a stand-in engine failing on rank ``bad``."""
+    try:
+        os.environ.update(client_env(rank, world, port))
+        dist.init_process_group("gloo")
+        torch.cuda.synchronize = lambda *a, **k: None
+        from ddp_practice_amd.parallel.comm import _probe_twoshot
+
+        rc = _RC(rank, world)
+        eng = _Engine(rank, bad, bad_kind)
+        eng.local_only = True
+        best = _probe_twoshot(rc, eng, 1 << 20, 8 << 20)
+        calls = torch.tensor([rc.native.calls])
+        every = [torch.zeros(1, dtype=calls.dtype) for _ in range(world)]
+        dist.all_gather(every, calls)
+        dist.destroy_process_group()
+        q.put((rank, "ok", (best, [int(c) for c in every])))
     except Exception:  # noqa: BLE001
         q.put((rank, "err", traceback.format_exc()))

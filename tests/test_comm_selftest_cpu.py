@@ -17,3 +17,25 @@ def test_selftest_votes_symmetrically(bad, kind):
         assert any(o[1] for o in outs)  # the failing rank names why
     counts = outs[0][2]
     assert len(set(counts)) == 1, f"ranks issued different numbers of collectives: {counts}"
+
+
+def test_selftest_small_twoshot_bound_passes():
+    """DPA_XGMI_TWOSHOT_MAX_BYTES below the self-test's default 4 MiB case is a valid
+    setting: the two-shot cases shrink to fit it instead of failing the vote."""
+    outs = launch(_selftest_worker.run, 2, (-1, "none", 64 << 10), timeout=120)
+    assert {o[0] for o in outs} == {True}, outs
+    assert len(set(outs[0][2])) == 1
+
+
+@pytest.mark.parametrize("bad,kind", [(-1, "none"), (1, "twoshot_err"), (0, "twoshot_raise")])
+def test_twoshot_probe_decides_from_reduced_values(bad, kind):
+    """A two-shot failure on ONE rank (error word or exception) makes EVERY rank leave the
+    probe with bound 0 after the same collectives (the local error was checked
+    after the reduction, so ranks could attach with different bounds or hang)."""
+    outs = launch(_selftest_worker.run_probe, 3, (bad, kind), timeout=120)
+    bests = {o[0] for o in outs}
+    assert len(bests) == 1, outs
+    if bad >= 0:
+        assert bests == {0}, outs
+    counts = outs[0][1]
+    assert len(set(counts)) == 1, f"ranks issued different numbers of collectives: {counts}"
