@@ -11,21 +11,40 @@ backward (+ SyncBN / DDP all-reduces) + unscale/inf-check + SGD + scale
 update, replayed from captured hipGraphs.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-        N > 1 without WORLD_SIZE in the environment: this process launches the N
-        ranks itself (one per GPU, like the reference's mp.spawn,
-        /root/reference/ddp_main.py:173-178) before touching the GPU.
+        N > 1 without WORLD_SIZE in the environment: this process supervises N
+        fresh rank processes (one per GPU, like the reference's mp.spawn,
+        /root/reference/ddp_main.py:173-178) and never touches the GPU itself.
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
-        N ranks started by torchrun (RANK / LOCAL_RANK / WORLD_SIZE from the env).
+        every torchrun worker supervises ONE fresh rank process; the supervisors
+        agree through torchrun's store (ddp_practice_amd/runtime/supervisor.py).
 
-What one run measures (rank 0 prints ONE JSON line):
+Fail-safe multi-GPU runs (N > 1):
+  * every rank arms the native watchdog (DPA_BENCH_WATCHDOG s, default 90:
+    no device progress / host heartbeat -> report, abort the communicator,
+    exit 124) and bounds every xGMI exchange wait (DPA_XGMI_TIMEOUT, default
+    15 s here); after every phase every rank reads the communicator's error word;
+  * an attempt that fails (a rank exits non-zero, stalls past the attempt timeout
+    DPA_BENCH_ATTEMPT_TIMEOUT (300 s), or reports a communicator error) is re-run
+    by the supervisors as fresh processes with ``--comm rccl`` (no xGMI engine, no
+    in-kernel exchanges; ``--share-gpu``: ``--comm host``) and the line says
+    ``"fallback"`` plus the original ``comm_error``;
+  * a successful ``--comm auto`` run with the xGMI engine on is followed by an A/B
+    attempt on ``--comm rccl`` (headline only) -> ``ab`` keys.
+  Exit status: 0 = a measured line (possibly after a fallback); 3 = every attempt
+  failed (the line then has ``value`` null and ``comm_error``); 2 = bad arguments.
+
+What one rank measures (rank 0's record becomes the JSON line):
   1. the reference's whole program on this node: 3 epochs over the 60k-sample
      train set (DistributedSampler shards, graph-replayed full batches + the
      eager tail batch) and the sharded test pass -> ``wall_3epoch_s``,
      ``epoch_img_s``, ``accuracy``; ``process_wall_3epoch_s`` adds process
      start-up (interpreter, imports, rendezvous) as the reference's timer does;
   2. the headline: exactly ``--warmup`` untimed then exactly ``--steps`` timed
-     training steps, barrier + synchronize on both sides, max over ranks;
-  3. the same-node baseline: the reference's step on PyTorch's own modules,
+     training steps, barrier + synchronize on both sides, max over ranks; then
+     ``steady_img_s``: at least one full epoch of graph replays (capture excluded);
+  3. the same headline in the other precisions (``value_fp16`` / ``value_fp32``:
+     the reference's AMP dtype and its fp32 baseline script);
+  4. the same-node baseline: the reference's step on PyTorch's own modules,
      autocast, GradScaler, SGD, SyncBatchNorm and DDP
      (ddp_practice_amd/utils/reference_step.py), same dtype -> ``vs_baseline``
      = value / baseline.  The reference's published number (other hardware,
@@ -36,10 +55,10 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import socket
 import sys
 import time
 
+_IMPORT_T = time.time()
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
@@ -48,6 +67,7 @@ METRIC = "images/sec (whole node) + 3-epoch wall-clock, MNIST ConvNet at 1/2/4/8
 # 180,000 train images / 22.72 s (origin_main.py, 1 GPU, fp32) and / 30.82 s (ddp_main.py, W=2)
 PUBLISHED_IMG_S = {1: 7923.0, 2: 5840.0}
 PUBLISHED_WALL_S = {1: 22.72, 2: 30.82}
+_DT = {"bf16": "bfloat16", "fp16": "float16", "fp32": None}
 
 
 def parse(argv=None):
@@ -57,20 +77,26 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--batch-size", type=int, default=32)
     ap.add_argument("--amp-dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--extra-dtypes", default="fp16,fp32",
+                    help="comma list of other precisions measured the same way (value_<dt>); '' = none")
     ap.add_argument("--impl", default="native", choices=["native", "torch"],
                     help="native = this framework (headline); torch = the reference step on torch's stack")
     ap.add_argument("--steps-per-graph", type=int, default=16)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-sync-bn", action="store_true")
     ap.add_argument("--epochs", type=int, default=3, help="epochs of the measured wall-clock run (0: skip)")
+    ap.add_argument("--no-steady", action="store_true", help="skip the >= 1 epoch steady-state replay timing")
     ap.add_argument("--no-baseline", action="store_true", help="skip the same-node torch baseline")
     ap.add_argument("--baseline-steps", type=int, default=200)
     ap.add_argument("--force-collectives", action="store_true",
                     help="profiling: run the DDP/SyncBN collective path even at --gpus 1")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0, all-reduces on the xGMI engine (not the metric)")
-    ap.add_argument("--comm", default=None, choices=["auto", "rccl", "xgmi"],
-                    help="collective algorithm selection (auto: xGMI engine where it is faster, else RCCL)")
+    ap.add_argument("--comm", default=None, choices=["auto", "rccl", "xgmi", "host"],
+                    help="collective algorithm selection (auto: xGMI engine where it is faster, else RCCL; "
+                         "host: device tensors staged through gloo, the --share-gpu fallback)")
+    ap.add_argument("--no-fallback", action="store_true", help="N > 1: report a failed attempt, do not re-run it")
+    ap.add_argument("--no-ab", action="store_true", help="N > 1: skip the --comm rccl A/B attempt")
     ap.add_argument("--model", default="convnet", choices=["convnet", "resnet50"],
                     help="convnet = the headline config; resnet50 = BASELINE.json stress config 5")
     ap.add_argument("--resnet-impl", default="native", choices=["native", "torch"],
@@ -82,77 +108,141 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-# ----------------------------------------------------------------------------- launcher
-def _free_port() -> int:
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
-def _spawned(local_rank: int, argv: list[str], world: int, port: int, t0: float) -> None:
-    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
-                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                      DPA_BENCH_T0=repr(t0))
-    run_rank(parse(argv))
-
-
-def launch(args, argv: list[str]) -> int:
-    """``--gpus N`` with no launcher: start N ranks (before any GPU call in this process)."""
-    import torch
-
-    n = args.gpus
-    visible = torch.cuda.device_count()  # does not initialise the HIP runtime on this image
-    if visible == 0:
-        print(f"bench.py: no GPU visible: {n} CPU ranks over gloo (plumbing only, not the metric)", file=sys.stderr)
-    elif not args.share_gpu and n > visible:
-        print(f"bench.py: --gpus {n} but only {visible} GPU(s) are visible "
-              f"(use --share-gpu for a one-GPU rehearsal)", file=sys.stderr)
-        return 2
-    if args.share_gpu and visible < 1:
-        print("bench.py: --share-gpu needs one visible GPU", file=sys.stderr)
-        return 2
-    import torch.multiprocessing as mp
-
-    t0 = time.time()
-    try:
-        mp.spawn(_spawned, args=(argv, n, _free_port(), t0), nprocs=n, join=True)
-    except Exception as e:  # noqa: BLE001 - a rank failed: report and exit non-zero
-        print(f"bench.py: a rank failed: {e}", file=sys.stderr)
-        return 1
-    return 0
-
-
+# ----------------------------------------------------------------------------- entry
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     args = parse(argv)
     if args.gpus < 1:
         print("bench.py: --gpus must be >= 1", file=sys.stderr)
         return 2
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        return launch(args, argv)
-    if "WORLD_SIZE" in os.environ:
+    child = os.environ.get("DPA_BENCH_CHILD") == "1"
+    world = int(os.environ.get("WORLD_SIZE", args.gpus))
+    if not child and world > 1:
+        return supervise(args, argv)
+    if "WORLD_SIZE" in os.environ and not child:
         import torch
 
-        world = int(os.environ["WORLD_SIZE"])
-        if world != args.gpus:
-            print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; measuring {world} ranks", file=sys.stderr)
-        ngpu = torch.cuda.device_count()
+        ngpu = torch.cuda.device_count()  # does not initialise the HIP runtime on this image
         if ngpu and not args.share_gpu and int(os.environ.get("LOCAL_WORLD_SIZE", world)) > ngpu:
-            print(f"bench.py: {os.environ.get('LOCAL_WORLD_SIZE', world)} local ranks but "
-                  f"{torch.cuda.device_count()} visible GPU(s)", file=sys.stderr)
+            print(f"bench.py: {os.environ.get('LOCAL_WORLD_SIZE', world)} local ranks but {ngpu} visible GPU(s)",
+                  file=sys.stderr)
             return 2
-    run_rank(args)
-    return 0
+    return run_rank(args)
+
+
+# ----------------------------------------------------------------------------- supervisor (N > 1)
+def _child_argv(argv: list[str], extra: list[str]) -> list[str]:
+    """argv without --comm / --out (the supervisor owns them) plus ``extra``."""
+    out, skip = [], False
+    for a in argv:
+        if skip:
+            skip = False
+            continue
+        if a in ("--comm", "--out"):
+            skip = True
+            continue
+        if a.startswith("--comm=") or a.startswith("--out="):
+            continue
+        out.append(a)
+    return [sys.executable, os.path.abspath(__file__), *out, *extra]
+
+
+def _failed_record(args, n: int, err: str) -> dict:
+    return {"metric": METRIC if args.model == "convnet" else
+            "images/sec (whole node), ResNet-50 stress config (BASELINE.json config 5)",
+            "value": None, "unit": "images/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": args.amp_dtype, "data": "synthetic", "config": {"parallelism": f"dp{n}"},
+            "comm_error": err}
+
+
+def supervise(args, argv: list[str]) -> int:
+    """N ranks as fresh child processes; fallback and A/B attempts (module docstring)."""
+    import torch
+
+    from ddp_practice_amd.runtime.supervisor import Supervisor, summarize
+
+    torchrun = "WORLD_SIZE" in os.environ
+    n = int(os.environ["WORLD_SIZE"]) if torchrun else args.gpus
+    visible = torch.cuda.device_count()  # does not initialise the HIP runtime on this image
+    if not torchrun:
+        if visible == 0:
+            print(f"bench.py: no GPU visible: {n} CPU ranks over gloo (plumbing only, not the metric)",
+                  file=sys.stderr)
+        elif not args.share_gpu and n > visible:
+            print(f"bench.py: --gpus {n} but only {visible} GPU(s) are visible "
+                  f"(use --share-gpu for a one-GPU rehearsal)", file=sys.stderr)
+            return 2
+        if args.share_gpu and visible < 1:
+            print("bench.py: --share-gpu needs one visible GPU", file=sys.stderr)
+            return 2
+    gpu = visible > 0
+    t0 = time.time()
+    sup = Supervisor(n, None if torchrun else list(range(n)),
+                     timeout_s=float(os.environ.get("DPA_BENCH_ATTEMPT_TIMEOUT", "300")),
+                     grace_s=float(os.environ.get("DPA_BENCH_GRACE", "10")))
+    env = {"DPA_BENCH_T0": repr(t0)}
+    mode = args.comm or "auto"
+    fb_mode = "host" if args.share_gpu else "rccl"
+    attempts = []
+
+    def attempt(m: str, extra: list[str], env_over: dict, tag: str, timeout=None):
+        ta = time.time()
+        res = sup.run(_child_argv(argv, ["--comm", m, *extra]), {**env, **env_over}, tag=tag, timeout_s=timeout)
+        err = summarize(res)
+        attempts.append({"comm": m, "tag": tag, "ok": not err, "error": err, "seconds": round(time.time() - ta, 2),
+                         "xgmi_status": [(r.status or {}).get("xgmi_status") for r in res]})
+        rec = (res[0].status or {}).get("record") if not err else None
+        return res, err, rec
+
+    res, err, rec = attempt(mode, [], {}, mode)
+    first_err, fallback = err, None
+    if err and not args.no_fallback and mode != fb_mode:
+        # fresh processes; an injected fault (tests) is a one-off unless DPA_FAULT_RETRY=1
+        over = {} if os.environ.get("DPA_FAULT_RETRY") == "1" else {"DPA_FAULT": ""}
+        res, err, rec = attempt(fb_mode, ["--no-graph"] if fb_mode == "host" else [], over, f"fallback-{fb_mode}")
+        fallback = fb_mode
+    ab = None
+    if (rec is not None and gpu and not args.share_gpu and not args.no_ab and mode == "auto" and fallback is None
+            and args.model == "convnet" and str(rec.get("config", {}).get("comm", "")).find("xgmi on") >= 0):
+        _, ab_err, ab_rec = attempt("rccl", ["--epochs", "0", "--no-baseline", "--extra-dtypes", "", "--no-steady"],
+                                    {}, "ab-rccl", timeout=180)
+        ab = {"auto_ms_per_step": rec.get("ms_per_step"), "auto_img_s": rec.get("value")}
+        if ab_rec is not None:
+            ab.update(rccl_ms_per_step=ab_rec.get("ms_per_step"), rccl_img_s=ab_rec.get("value"),
+                      speedup_auto_vs_rccl=round(ab_rec["ms_per_step"] / rec["ms_per_step"], 3)
+                      if rec.get("ms_per_step") else None)
+        else:
+            ab["rccl_error"] = ab_err
+    if not sup.leader:
+        return 0 if rec is not None else 3
+    if rec is None:
+        rec = _failed_record(args, n, err or first_err)
+        rec["comm_error"] = first_err if first_err == err else f"{first_err} | fallback: {err}"
+    else:
+        rec["comm_error"] = first_err
+    rec["fallback"] = fallback
+    rec["attempts"] = attempts
+    if ab is not None:
+        rec["ab"] = ab
+    rec["supervisor_wall_s"] = round(time.time() - t0, 2)
+    _emit(rec, args.out)
+    return 0 if rec.get("value") is not None else 3
 
 
 # ----------------------------------------------------------------------------- helpers
 def _force_collectives():
     """Profiling/rehearsal: run the DDP + SyncBN collective code path in a world of one."""
+    import socket
+
     from ddp_practice_amd.parallel import comm as _comm
 
     _comm.Communicator.force_active = True
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    if "MASTER_PORT" not in os.environ:
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            s.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(s.getsockname()[1])
     os.environ.setdefault("RANK", "0")
     os.environ.setdefault("WORLD_SIZE", "1")
 
@@ -166,9 +256,6 @@ def _process_t0() -> float:
         return psutil.Process(os.getpid()).create_time()
     except Exception:  # noqa: BLE001
         return _IMPORT_T
-
-
-_IMPORT_T = time.time()
 
 
 def _comm_desc(c) -> str:
@@ -195,15 +282,86 @@ def _emit(rec: dict, out: str | None) -> None:
             f.write(line + "\n")
 
 
+class _Health:
+    """Per-rank failure detection of one bench process: the native watchdog (N > 1), the
+    communicator's error word after every phase, and the status file a supervisor reads."""
+
+    def __init__(self, comm, rank: int, world: int, gpu: bool):
+        import torch
+
+        self.comm, self.rank, self.world, self.gpu = comm, rank, world, gpu
+        self.errors: dict[str, str] = {}
+        self.phases: dict[str, float] = {}
+        self._t = time.perf_counter()
+        self.wd = None
+        if world > 1:
+            from ddp_practice_amd.utils import Watchdog
+
+            self.wd = Watchdog(comm, timeout=float(os.environ.get("DPA_BENCH_WATCHDOG", "90")),
+                               tag=f"bench rank{rank}")
+            self.wd.heartbeat()
+        self._torch = torch
+
+    def beat(self) -> None:
+        if self.wd is not None:
+            self.wd.heartbeat()
+
+    def tick(self) -> None:
+        if self.wd is not None:
+            self.wd.tick()
+
+    def quiet(self) -> None:
+        """A host phase of unknown length follows (library autotuning): device ticks only."""
+        if self.wd is not None:
+            self.wd.disarm()
+
+    def check(self, phase: str) -> str:
+        """Synchronize, then this rank's communicator error word ("" = healthy)."""
+        if self.gpu:
+            self._torch.cuda.synchronize()
+        f = getattr(self.comm, "async_error", None)
+        e = f() if f is not None else ""
+        if e and e != "destroyed":
+            self.errors[phase] = e
+        now = time.perf_counter()
+        self.phases[phase] = round(now - self._t, 4)
+        self._t = now
+        self.beat()
+        return e
+
+    def comm_error(self) -> str:
+        return "; ".join(f"{k}: {v}" for k, v in self.errors.items())
+
+    def finish(self, rec: dict | None, args) -> None:
+        """rank 0: print the line (no supervisor) or hand it to the supervisor with the status."""
+        if self.wd is not None:
+            self.wd.stop()
+        status_file = os.environ.get("DPA_STATUS_FILE")
+        if rec is not None:
+            rec["comm_error"] = self.comm_error()
+            rec["phases_s"] = self.phases
+        if status_file:
+            st = {"rank": self.rank, "world": self.world, "comm_error": self.comm_error(),
+                  "xgmi_status": getattr(self.comm, "xgmi_status", None), "comm": _comm_desc(self.comm),
+                  "phases_s": self.phases, "record": rec}
+            tmp = status_file + ".tmp"
+            with open(tmp, "w") as f:
+                json.dump(st, f)
+            os.replace(tmp, status_file)
+        elif rec is not None:
+            _emit(rec, args.out)
+
+
 class _Chunks:
     """Exactly ``n`` training steps as replays of a K-step graph plus one graph of the remainder,
     keeping the loader's device step counter inside the epoch's full batches."""
 
-    def __init__(self, step, spg: int, loader, nfull: int, graphs: bool):
+    def __init__(self, step, spg: int, loader, nfull: int, graphs: bool, health: _Health | None = None):
         from ddp_practice_amd.runtime import CapturedStep
 
         self.step, self.spg, self.loader, self.nfull = step, max(1, spg), loader, nfull
         self.graphs = graphs
+        self.health = health
         self._mk = lambda k: CapturedStep(step, warmup=1, steps_per_graph=k, enabled=graphs,
                                           pre_capture=lambda: loader.set_step(0))
         self.runners: dict = {}
@@ -236,26 +394,46 @@ class _Chunks:
         self.pos += k
 
     def run(self, n: int) -> None:
-        for _ in range(n // self.spg):
+        tick = self.health.tick if self.health is not None else None
+        for i in range(n // self.spg):
             self._chunk(self.spg)
+            if tick is not None and i % 64 == 63:
+                tick()
         if n % self.spg:
             self._chunk(n % self.spg)
+        if tick is not None:
+            tick()
 
 
 # ----------------------------------------------------------------------------- ConvNet
-def run_rank(args) -> None:
+def run_rank(args) -> int:
     if args.model == "resnet50":
         return bench_resnet(args)
+    import threading
+
+    t_proc0 = _process_t0()
+    marks = {"bench_imported": round(_IMPORT_T - t_proc0, 3)}
     import torch
 
+    marks["torch_imported"] = round(time.time() - t_proc0, 3)
     from ddp_practice_amd import distributed as ddist
-    from ddp_practice_amd.amp import GradScaler
-    from ddp_practice_amd.data import DeviceLoader, DistributedSampler, synthetic
-    from ddp_practice_amd.engine import TrainLoop, evaluate
-    from ddp_practice_amd.models import ConvNet
-    from ddp_practice_amd.nn import CrossEntropyLoss
-    from ddp_practice_amd.optim import SGD
-    from ddp_practice_amd.parallel import DistributedDataParallel, convert_sync_batchnorm
+    from ddp_practice_amd.data import synthetic
+
+    marks["package_imported"] = round(time.time() - t_proc0, 3)
+
+    # the synthetic sets (numpy; releases the GIL in its bulk work) are generated on a side
+    # thread while this one brings up the HIP context, the communicator and the extension
+    box: dict = {}
+
+    def _data():
+        try:
+            box["train"] = synthetic(args.train_samples, seed=1, name="synthetic-MNIST-train")
+            box["test"] = synthetic(args.test_samples, seed=2, name="synthetic-MNIST-test")
+        except BaseException as e:  # noqa: BLE001 - re-raised below
+            box["error"] = e
+
+    th = threading.Thread(target=_data, name="dpa-bench-data", daemon=True)
+    th.start()
 
     if args.comm:
         os.environ["DPA_COMM"] = args.comm
@@ -269,145 +447,75 @@ def run_rank(args) -> None:
         dev = torch.device("cuda", local_rank)
     else:  # CPU plumbing (BASELINE config 1): torch modules, gloo, no graphs, fp32
         dev = torch.device("cpu")
-        args.no_graph, args.no_baseline, args.amp_dtype = True, True, "fp32"
-
-    def sync():
-        if gpu:
-            torch.cuda.synchronize()
+        args.no_graph, args.no_baseline, args.amp_dtype, args.extra_dtypes = True, True, "fp32", ""
 
     dist_path = world > 1 or args.force_collectives
     if args.force_collectives:
         _force_collectives()
+    if world > 1:
+        # a stalled exchange must end well inside the driver's timeout (default 600 s in the engine)
+        os.environ.setdefault("DPA_XGMI_TIMEOUT", "15")
     if dist_path:
-        ddist.init_process_group(backend=("xgmi" if args.share_gpu else "nccl") if gpu else "gloo")
+        if not gpu:
+            backend = "gloo"
+        elif args.comm == "host":
+            backend = "host"
+        else:
+            backend = "xgmi" if args.share_gpu else "nccl"
+        ddist.init_process_group(backend=backend)
     comm = ddist.default_comm()
     rank = ddist.get_rank()
-    amp = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": None}[args.amp_dtype]
+    health = _Health(comm, rank, world, gpu)
+    marks["comm_ready"] = round(time.time() - t_proc0, 3)
+    th.join()
+    marks["data_ready"] = round(time.time() - t_proc0, 3)
+    if "error" in box:
+        raise box["error"]
+    train_ds, test_ds = box["train"], box["test"]
+    health.check("setup")
     B = args.batch_size
-
-    train_ds = synthetic(args.train_samples, seed=1, name="synthetic-MNIST-train")
-    test_ds = synthetic(args.test_samples, seed=2, name="synthetic-MNIST-test")
-
-    def build(seed: int):
-        torch.manual_seed(seed)
-        model = ConvNet(amp_dtype=amp).to(dev)
-        if dist_path:
-            if not args.no_sync_bn:
-                model = convert_sync_batchnorm(model)
-            model = DistributedDataParallel(model, device_ids=[local_rank] if gpu else None)
-        return model, SGD(model.parameters(), lr=1e-4), GradScaler(enabled=amp is not None)
-
-    act = amp if amp is not None else torch.float32
-    crit = CrossEntropyLoss().to(dev)
+    ctx = dict(args=args, world=world, rank=rank, dev=dev, gpu=gpu, dist_path=dist_path, local_rank=local_rank,
+               comm=comm, train_ds=train_ds, test_ds=test_ds, health=health, marks=marks, t_proc0=t_proc0)
     rec_extra: dict = {}
 
     # 1. the reference's program: 3 epochs + sharded test, measured end to end
     if args.epochs > 0 and args.impl == "native":
-        model, opt, scaler = build(0)
-        g = torch.Generator()
-        g.manual_seed(3407 + rank)
-        tr = DeviceLoader(train_ds, batch_size=B, sampler=DistributedSampler(train_ds, num_replicas=world, rank=rank),
-                          generator=g, device=dev, dtype=act)
-        te = DeviceLoader(test_ds, batch_size=B, sampler=DistributedSampler(test_ds, num_replicas=world, rank=rank),
-                          device=dev, dtype=act)
-        loop = TrainLoop(model, crit, opt, tr, scaler if amp is not None else None,
-                         use_graph=not args.no_graph, steps_per_graph=args.steps_per_graph)
-        ddist.barrier()
-        sync()
-        t0 = time.perf_counter()
-        for ep in range(args.epochs):
-            tr.sampler.set_epoch(ep)
-            loop.run_epoch()
-        sync()
-        t_train = time.perf_counter() - t0
-        correct, size = evaluate(model, te, comm=comm if comm.active else None, dst=0)
-        sync()
-        ddist.barrier()
-        t_all = time.perf_counter() - t0
-        t_proc = time.time() - _process_t0()
-        t_train, t_all, t_proc = (ddist.max_over_ranks(v) for v in (t_train, t_all, t_proc))
-        imgs = args.epochs * len(train_ds)
-        rec_extra.update({
-            "wall_3epoch_s": round(t_all, 3),
-            "process_wall_3epoch_s": round(t_proc, 3),
-            "epoch_img_s": round(imgs / t_train, 1),
-            "train_3epoch_s": round(t_train, 3),
-            "epochs": args.epochs,
-            "accuracy": round(correct / size, 4) if rank == 0 and size else None,
-            "steps_per_rank_per_epoch": len(tr),
-            "published_ref_wall_s": PUBLISHED_WALL_S.get(world),
-        })
-        if loop.graph_error is not None:
-            rec_extra["graph_error_3epoch"] = repr(loop.graph_error)
-        del loop, model, opt, scaler, tr, te
+        rec_extra.update(_three_epochs(ctx))
+        health.check("3epoch")
 
-    # 2. the headline: exactly K timed steps after exactly W warm-up steps
-    spg = 1 if args.no_graph else args.steps_per_graph
+    # 2. the headline: exactly K timed steps after exactly W warm-up steps (+ steady state)
+    amp = _amp(args.amp_dtype)
     if args.impl == "native":
-        model, optimizer, scaler = build(1)
-        fused_grad = dist_path and amp is not None and model.defer_grad_sync_to(optimizer)
-        # no DDP: conv1's weight-gradient column sums run inside the fused AMP step (engine.TrainLoop does the same)
-        slab_sink = not dist_path and amp is not None and model.set_slab_sink(optimizer)
-        sampler = DistributedSampler(train_ds, num_replicas=world, rank=rank)
-        loader = DeviceLoader(train_ds, batch_size=B, sampler=sampler, device=dev, dtype=act)
-        images, labels = loader.static_batch()
-        loader.start_epoch()
-        nfull = len(sampler) // B
-        from ddp_practice_amd.data import accepts_deferred
-
-        defer = accepts_deferred(model, images)  # the gather runs inside conv1
-
-        def step():
-            loader.fill_(images, labels, defer=defer)
-            out = model(images)
-            loss = crit(out, labels)
-            optimizer.zero_grad(set_to_none=True)
-            if amp is not None:
-                scaler.scale(loss).backward()
-                scaler.step(optimizer)
-                scaler.update()
-            else:
-                loss.backward()
-                optimizer.step()
-
-        chunks = _Chunks(step, spg, loader, nfull, graphs=not args.no_graph)
-        chunks.prepare(args.warmup)
-        chunks.prepare(args.steps)
-        if chunks.capture_error is not None and rank == 0:
-            print(f"[bench] graph capture failed, eager fallback: {chunks.capture_error!r}", file=sys.stderr)
-        chunks.run(args.warmup)
-        ddist.barrier()
-        sync()
-        t0 = time.perf_counter()
-        chunks.run(args.steps)
-        sync()
-        ddist.barrier()
-        dt = time.perf_counter() - t0
-        captured = chunks.graphs and chunks.capture_error is None
-        impl_desc = "native (fused HIP kernels, C++ reducer/communicator)" if gpu else \
-            "CPU plumbing (torch modules, gloo; not the metric)"
-        grad_avg = ("in AMP-SGD kernel (xGMI)" if fused_grad else "reducer all-reduce") if dist_path \
-            else "none (1 rank)"
+        h = _headline(ctx, amp, steady=not args.no_steady)
     else:
-        from ddp_practice_amd.utils.reference_step import TorchReferenceStep
+        h = _torch_headline(ctx, amp)
+    health.check("headline")
+    ms, img_s = h["ms"], h["img_s"]
+    if "steady_img_s" in h:
+        rec_extra.update(steady_img_s=h["steady_img_s"], steady_ms_per_step=h["steady_ms"],
+                         steady_steps=h["steady_steps"])
 
-        ref = TorchReferenceStep(dev, amp, world, *train_ds.to_device(dev),
-                                 DistributedSampler(train_ds, num_replicas=world, rank=rank).indices().to(dev), B,
-                                 local_rank=local_rank, seed=1)
-        dt = ref.time_steps(args.steps, args.warmup, ddist.barrier)
-        captured, spg = False, 1
-        impl_desc = "torch (nn modules, torch.autocast, torch GradScaler/SGD/SyncBatchNorm/DDP)"
-        grad_avg = "torch DDP" if world > 1 else "none (1 rank)"
-        del ref
-    dt_max = ddist.max_over_ranks(dt)
-    ms = dt_max / args.steps * 1e3
-    img_s = B * world * args.steps / dt_max
+    # 3. the other precisions, same steps / warm-up
+    for dt in [d for d in args.extra_dtypes.split(",") if d and d != args.amp_dtype]:
+        if args.impl != "native":
+            break
+        try:
+            x = _headline(ctx, _amp(dt), steady=not args.no_steady)
+            rec_extra[f"value_{dt}"] = round(x["img_s"], 1)
+            rec_extra[f"ms_per_step_{dt}"] = round(x["ms"], 5)
+            if "steady_img_s" in x:
+                rec_extra[f"steady_img_s_{dt}"] = x["steady_img_s"]
+        except Exception as e:  # noqa: BLE001 - context keys, never the metric
+            rec_extra[f"error_{dt}"] = f"{type(e).__name__}: {e}"
+        health.check(f"headline_{dt}")
 
-    # 3. same-node baseline: the reference step on torch's own stack, same dtype
+    # 4. same-node baseline: the reference step on torch's own stack, same dtype
     base = None
     if args.impl == "native" and not args.no_baseline and not args.share_gpu:
+        health.quiet()  # torch's first convolutions may autotune for a while: device ticks only
         try:
             from ddp_practice_amd.utils.reference_step import TorchReferenceStep
+            from ddp_practice_amd.data import DistributedSampler
 
             ref = TorchReferenceStep(dev, amp, world, *train_ds.to_device(dev),
                                      DistributedSampler(train_ds, num_replicas=world, rank=rank).indices().to(dev),
@@ -419,10 +527,13 @@ def run_rank(args) -> None:
             del ref
         except Exception as e:  # noqa: BLE001 - the baseline is context, never the metric
             rec_extra["baseline_error"] = f"{type(e).__name__}: {e}"
+        health.check("baseline")
     elif args.share_gpu:
         rec_extra["baseline_error"] = "skipped: --share-gpu rehearsal"
 
     seen = _ranks_seen(comm if dist_path else None)
+    health.check("end")
+    rec = None
     if rank == 0:
         pub = PUBLISHED_IMG_S.get(world)
         rec = {
@@ -449,26 +560,204 @@ def run_rank(args) -> None:
                 "seq_len": None,
                 "parallelism": f"dp{world}",
                 "per_rank_batch": B,
-                "impl": impl_desc,
+                "impl": h["impl"],
                 "sync_bn": dist_path and not args.no_sync_bn,
                 "amp": f"autocast {args.amp_dtype} + GradScaler" if amp is not None else "fp32",
                 "optimizer": "SGD(lr=1e-4)",
-                "hipgraph": bool(captured),
-                "steps_per_graph": spg,
+                "hipgraph": bool(h["captured"]),
+                "steps_per_graph": h["spg"],
                 "comm": _comm_desc(comm) if dist_path else "none (1 rank)",
-                "grad_avg": grad_avg,
+                "grad_avg": h["grad_avg"],
                 "shared_gpu": bool(args.share_gpu),
             },
             "ranks_seen": seen,
-            "per_rank_max_s": round(dt_max, 6),
+            "per_rank_max_s": round(h["dt"], 6),
         }
         rec.update(rec_extra)
-        _emit(rec, args.out)
+    health.finish(rec, args)
     ddist.destroy_process_group()
+    return 0
+
+
+def _amp(name: str):
+    import torch
+
+    return {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": None}[name]
+
+
+def _build(ctx, amp, seed: int):
+    from ddp_practice_amd.amp import GradScaler
+    from ddp_practice_amd.models import ConvNet
+    from ddp_practice_amd.optim import SGD
+    from ddp_practice_amd.parallel import DistributedDataParallel, convert_sync_batchnorm
+    import torch
+
+    torch.manual_seed(seed)
+    model = ConvNet(amp_dtype=amp).to(ctx["dev"])
+    if ctx["dist_path"]:
+        if not ctx["args"].no_sync_bn:
+            model = convert_sync_batchnorm(model)
+        model = DistributedDataParallel(model, device_ids=[ctx["local_rank"]] if ctx["gpu"] else None)
+    return model, SGD(model.parameters(), lr=1e-4), GradScaler(enabled=amp is not None)
+
+
+def _three_epochs(ctx) -> dict:
+    import torch
+
+    from ddp_practice_amd import distributed as ddist
+    from ddp_practice_amd.data import DeviceLoader, DistributedSampler
+    from ddp_practice_amd.engine import TrainLoop, evaluate
+    from ddp_practice_amd.nn import CrossEntropyLoss
+    from ddp_practice_amd.utils import FaultInjector
+
+    args, world, rank, dev, comm, health = (ctx[k] for k in ("args", "world", "rank", "dev", "comm", "health"))
+    amp = _amp(args.amp_dtype)
+    act = amp if amp is not None else torch.float32
+    train_ds, test_ds = ctx["train_ds"], ctx["test_ds"]
+    B = args.batch_size
+    model, opt, scaler = _build(ctx, amp, 0)
+    g = torch.Generator()
+    g.manual_seed(3407 + rank)
+    tr = DeviceLoader(train_ds, batch_size=B, sampler=DistributedSampler(train_ds, num_replicas=world, rank=rank),
+                      generator=g, device=dev, dtype=act)
+    te = DeviceLoader(test_ds, batch_size=B, sampler=DistributedSampler(test_ds, num_replicas=world, rank=rank),
+                      device=dev, dtype=act)
+    loop = TrainLoop(model, CrossEntropyLoss().to(dev), opt, tr, scaler if amp is not None else None,
+                     use_graph=not args.no_graph, steps_per_graph=args.steps_per_graph,
+                     watchdog=health.wd, faults=FaultInjector(rank))
+
+    def sync():
+        if ctx["gpu"]:
+            torch.cuda.synchronize()
+
+    ddist.barrier()
+    sync()
+    ctx["marks"]["3epoch_start"] = round(time.time() - ctx["t_proc0"], 3)
+    t0 = time.perf_counter()
+    for ep in range(args.epochs):
+        tr.sampler.set_epoch(ep)
+        loop.run_epoch()
+        health.beat()
+    sync()
+    t_train = time.perf_counter() - t0
+    correct, size = evaluate(model, te, comm=comm if comm.active else None, dst=0)
+    sync()
+    ddist.barrier()
+    t_all = time.perf_counter() - t0
+    t_proc = time.time() - _process_t0()
+    t_train, t_all, t_proc = (ddist.max_over_ranks(v) for v in (t_train, t_all, t_proc))
+    imgs = args.epochs * len(train_ds)
+    out = {
+        "wall_3epoch_s": round(t_all, 3),
+        "process_wall_3epoch_s": round(t_proc, 3),
+        "epoch_img_s": round(imgs / t_train, 1),
+        "train_3epoch_s": round(t_train, 3),
+        "epochs": args.epochs,
+        "accuracy": round(correct / size, 4) if rank == 0 and size else None,
+        "steps_per_rank_per_epoch": len(tr),
+        "published_ref_wall_s": PUBLISHED_WALL_S.get(world),
+    }
+    if loop.graph_error is not None:
+        out["graph_error_3epoch"] = repr(loop.graph_error)
+    ctx["marks"]["3epoch_end"] = round(time.time() - ctx["t_proc0"], 3)
+    out["startup_marks_s"] = ctx["marks"]
+    return out
+
+
+def _headline(ctx, amp, steady: bool) -> dict:
+    """Exactly --warmup untimed + --steps timed steps of the native step (graph replays),
+    then (``steady``) at least one full epoch of replays timed the same way."""
+    import torch
+
+    from ddp_practice_amd import distributed as ddist
+    from ddp_practice_amd.data import DeviceLoader, DistributedSampler, accepts_deferred
+    from ddp_practice_amd.nn import CrossEntropyLoss
+
+    args, world, rank, dev, health = (ctx[k] for k in ("args", "world", "rank", "dev", "health"))
+    B = args.batch_size
+    act = amp if amp is not None else torch.float32
+    train_ds = ctx["train_ds"]
+    model, optimizer, scaler = _build(ctx, amp, 1)
+    crit = CrossEntropyLoss().to(dev)
+    fused_grad = ctx["dist_path"] and amp is not None and model.defer_grad_sync_to(optimizer)
+    # no DDP: conv1's weight-gradient column sums run inside the fused AMP step (engine.TrainLoop does the same)
+    if not ctx["dist_path"] and amp is not None:
+        model.set_slab_sink(optimizer)
+    sampler = DistributedSampler(train_ds, num_replicas=world, rank=rank)
+    loader = DeviceLoader(train_ds, batch_size=B, sampler=sampler, device=dev, dtype=act)
+    images, labels = loader.static_batch()
+    loader.start_epoch()
+    nfull = len(sampler) // B
+    defer = accepts_deferred(model, images)  # the gather runs inside conv1
+
+    def step():
+        loader.fill_(images, labels, defer=defer)
+        out = model(images)
+        loss = crit(out, labels)
+        optimizer.zero_grad(set_to_none=True)
+        if amp is not None:
+            scaler.scale(loss).backward()
+            scaler.step(optimizer)
+            scaler.update()
+        else:
+            loss.backward()
+            optimizer.step()
+
+    spg = 1 if args.no_graph else args.steps_per_graph
+    chunks = _Chunks(step, spg, loader, nfull, graphs=not args.no_graph, health=health)
+    n_steady = max(nfull, args.steps) if steady else 0
+    for n in (args.warmup, args.steps, n_steady):
+        if n:
+            chunks.prepare(n)
+    if chunks.capture_error is not None and rank == 0:
+        print(f"[bench] graph capture failed, eager fallback: {chunks.capture_error!r}", file=sys.stderr)
+
+    def timed(n: int) -> float:
+        ddist.barrier()
+        if ctx["gpu"]:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        chunks.run(n)
+        if ctx["gpu"]:
+            torch.cuda.synchronize()
+        ddist.barrier()
+        return ddist.max_over_ranks(time.perf_counter() - t0)
+
+    chunks.run(args.warmup)
+    dt = timed(args.steps)
+    out = {"dt": dt, "ms": dt / args.steps * 1e3, "img_s": B * world * args.steps / dt,
+           "captured": chunks.graphs and chunks.capture_error is None, "spg": spg,
+           "impl": "native (fused HIP kernels, C++ reducer/communicator)" if ctx["gpu"] else
+                   "CPU plumbing (torch modules, gloo; not the metric)",
+           "grad_avg": ("in AMP-SGD kernel (xGMI)" if fused_grad else "reducer all-reduce") if ctx["dist_path"]
+                       else "none (1 rank)"}
+    if n_steady:
+        ds = timed(n_steady)
+        out.update(steady_img_s=round(B * world * n_steady / ds, 1), steady_ms=round(ds / n_steady * 1e3, 5),
+                   steady_steps=n_steady)
+    del chunks, model, optimizer, scaler, loader
+    return out
+
+
+def _torch_headline(ctx, amp) -> dict:
+    from ddp_practice_amd import distributed as ddist
+    from ddp_practice_amd.data import DistributedSampler
+    from ddp_practice_amd.utils.reference_step import TorchReferenceStep
+
+    args, world, rank, dev = (ctx[k] for k in ("args", "world", "rank", "dev"))
+    train_ds = ctx["train_ds"]
+    ref = TorchReferenceStep(dev, amp, world, *train_ds.to_device(dev),
+                             DistributedSampler(train_ds, num_replicas=world, rank=rank).indices().to(dev),
+                             args.batch_size, local_rank=ctx["local_rank"], seed=1)
+    dt = ddist.max_over_ranks(ref.time_steps(args.steps, args.warmup, ddist.barrier))
+    return {"dt": dt, "ms": dt / args.steps * 1e3, "img_s": args.batch_size * world * args.steps / dt,
+            "captured": False, "spg": 1,
+            "impl": "torch (nn modules, torch.autocast, torch GradScaler/SGD/SyncBatchNorm/DDP)",
+            "grad_avg": "torch DDP" if world > 1 else "none (1 rank)"}
 
 
 # ----------------------------------------------------------------------------- ResNet-50
-def bench_resnet(args):
+def bench_resnet(args) -> int:
     """ResNet-50 training step (BASELINE.json config 5): channels-last AMP + GradScaler,
     SyncBN + DDP over RCCL for N > 1, synthetic 3x224x224 batch, replayed from a hipGraph
     (--no-graph: eager).  Exactly --warmup untimed and --steps timed steps."""
@@ -493,10 +782,14 @@ def bench_resnet(args):
     dist_path = world > 1 or args.force_collectives
     if args.force_collectives:
         _force_collectives()
+    if world > 1:
+        os.environ.setdefault("DPA_XGMI_TIMEOUT", "15")
     if dist_path:
-        ddist.init_process_group(backend="xgmi" if args.share_gpu else "nccl")
+        ddist.init_process_group(backend="host" if args.comm == "host" else "xgmi" if args.share_gpu else "nccl")
     rank = ddist.get_rank()
-    amp = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": None}[args.amp_dtype]
+    c = ddist.default_comm()
+    health = _Health(c, rank, world, True)
+    amp = _amp(args.amp_dtype)
     bs = args.batch_size if args.batch_size != 32 else 128
     torch.manual_seed(0)
     model = resnet50(amp_dtype=amp, fused=args.resnet_impl == "native").to(dev)
@@ -528,10 +821,12 @@ def bench_resnet(args):
 
     # the step is hundreds of launches: capture it (after warm-up, so any library
     # algorithm search is done) and replay, or host overhead becomes the bound
+    health.quiet()
     runner = CapturedStep(step, warmup=2, steps_per_graph=1, enabled=not args.no_graph)
     captured = runner.capture() if not args.no_graph else False
     if not captured and not args.no_graph and rank == 0:
         print(f"[bench] graph capture failed, eager: {runner.capture_error!r}", file=sys.stderr)
+    health.check("setup")
     for _ in range(args.warmup):
         runner.run()
     ddist.barrier()
@@ -539,15 +834,17 @@ def bench_resnet(args):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         runner.run()
+        health.tick()
     torch.cuda.synchronize()
     ddist.barrier()
     dt = ddist.max_over_ranks(time.perf_counter() - t0)
+    health.check("headline")
     ms = dt / args.steps * 1e3
     img_s = bs * world * args.steps / dt
-    c = ddist.default_comm()
     seen = _ranks_seen(c if dist_path else None)
+    rec = None
     if rank == 0:
-        _emit({
+        rec = {
             "metric": "images/sec (whole node), ResNet-50 stress config (BASELINE.json config 5)",
             "value": round(img_s, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
@@ -559,8 +856,10 @@ def bench_resnet(args):
                        "comm": _comm_desc(c) if dist_path else "none", "hipgraph": bool(captured),
                        "shared_gpu": bool(args.share_gpu)},
             "ranks_seen": seen, "per_rank_max_s": round(dt, 6),
-        }, args.out)
+        }
+    health.finish(rec, args)
     ddist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":

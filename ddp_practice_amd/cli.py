@@ -23,7 +23,8 @@ Additive flags (all optional; defaults reproduce the reference):
                                       layout) on a synthetic ImageNet-shaped set
                                       (--image-size, --num-classes; data/imagenet.py)
   --resume PATH [--start-epoch N]     load {"model"[, "scaler"]} before training
-  --watchdog-timeout S                abort + exit when no progress for S seconds
+  --watchdog-timeout S                abort + exit when no progress for S seconds (default at
+                                      world size > 1: 600, torch's ProcessGroupNCCL default; 0 = off)
   --profile                           roctx ranges (rocprofv3 --marker-trace)
   --metrics-file PATH                 per-epoch JSONL (img/s, scale, ...) on rank 0
   --checkpoint PATH                   output file name
@@ -49,7 +50,8 @@ def add_run_args(parser, amp_default: str, checkpoint: str, distributed: bool) -
     parser.add_argument("--resume", default=None, help="checkpoint to load before training")
     parser.add_argument("--start-epoch", type=int, default=0, help="first epoch index (sampler seed) when resuming")
     parser.add_argument("--watchdog-timeout", type=float, default=None,
-                        help="seconds without progress before aborting (env DPA_WATCHDOG_TIMEOUT; 0 = off)")
+                        help="seconds without progress before aborting (env DPA_WATCHDOG_TIMEOUT; default 600 "
+                             "at world size > 1, off for one process; 0 = off)")
     parser.add_argument("--profile", action="store_true", help="emit roctx ranges for rocprofv3 --marker-trace")
     parser.add_argument("--metrics-file", default=None, help="per-epoch JSONL metrics (rank 0)")
     parser.add_argument("--impl", default="native", choices=["native", "torch"],
@@ -86,6 +88,34 @@ def load_checkpoint(path: str, model, scaler=None) -> None:
     model.load_state_dict(sd)
     if scaler is not None and "scaler" in ck and ck["scaler"]:
         scaler.load_state_dict(ck["scaler"])
+
+
+DEFAULT_WATCHDOG_S = 600.0  # torch/distributed/constants.py:21 default_pg_timeout (ProcessGroupNCCL)
+
+
+def watchdog_timeout(args, world: int) -> float:
+    """The watchdog timeout of a run: --watchdog-timeout, else DPA_WATCHDOG_TIMEOUT, else
+    on by default at world size > 1 (the reference's ``init_process_group("nccl")`` arms
+    ProcessGroupNCCL's 10-minute watchdog: /root/reference/ddp_main.py:73).  0 = off."""
+    t = getattr(args, "watchdog_timeout", None)
+    if t is None and "DPA_WATCHDOG_TIMEOUT" in os.environ:
+        t = float(os.environ["DPA_WATCHDOG_TIMEOUT"])
+    if t is None:
+        t = DEFAULT_WATCHDOG_S if world > 1 else 0.0
+    return float(t)
+
+
+def check_health(comm, where: str) -> None:
+    """Raise on every rank when any rank's communicator reported an asynchronous error
+    (parallel/comm.agree_on_errors): training must not go on, and no checkpoint may be
+    written, after updates an exchange failure skipped or corrupted."""
+    if comm is None or not getattr(comm, "active", False):
+        return
+    from ddp_practice_amd.parallel.comm import agree_on_errors
+
+    err = agree_on_errors(comm)
+    if err:
+        raise RuntimeError(f"[ddp_practice_amd] communicator error {where}: {err}")
 
 
 class _Metrics:
@@ -237,11 +267,9 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
                                     dtype=act_dtype, num_workers=2, pin_memory=True)
 
     phase("data")
-    timeout = args.watchdog_timeout
-    if timeout is None and "DPA_WATCHDOG_TIMEOUT" in os.environ:
-        timeout = float(os.environ["DPA_WATCHDOG_TIMEOUT"])
-    watchdog = Watchdog(comm, timeout=timeout, tag=f"rank{rank}") if timeout else None
-    faults = FaultInjector(rank)
+    timeout = watchdog_timeout(args, world)
+    watchdog = Watchdog(comm, timeout=timeout, tag=f"rank{rank}") if timeout > 0 else None
+    faults = FaultInjector(rank, comm=comm)
     # ResNet-50: hundreds of launches per step, one step per captured graph is enough
     loop = TrainLoop(model, criterion, optimizer, train_dloader, scaler, use_graph=native and not args.no_graph,
                      steps_per_graph=1 if resnet else 16, watchdog=watchdog, faults=faults)
@@ -254,6 +282,7 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
             if distributed:
                 train_dloader.sampler.set_epoch(epoch)
             loop.run_epoch()
+            check_health(comm, f"after epoch {epoch - args.start_epoch + 1}")
             metrics.epoch(epoch, len(train_dataset), len(train_dloader), scaler)
             phase(f"epoch {epoch}")
         if loop.graph_error is not None and rank == 0:
@@ -265,6 +294,7 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
         if watchdog is not None:
             watchdog.tick()
         phase("evaluate")
+        check_health(comm, "before saving the checkpoint")
         if rank == 0:
             print(f"Accuracy is {correct / size:.2%}", flush=True)
             with trace_range("checkpoint"):

@@ -148,11 +148,9 @@ __global__ __launch_bounds__(kThreads) void oneshot_kernel(Args a) {
           __builtin_amdgcn_s_sleep(1);
           g[q][j] = __hip_atomic_load(src[q] + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if ((++polls & 255u) == 0) {
-            int why = 0;
-            if (__hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) why = 2;
-            else if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) why = 1;
+            const int why = give_up(a.err, a.abort_flag, t0, a.timeout_ticks);
             if (why) {
-              __hip_atomic_store(a.err, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              if (why > 0) __hip_atomic_store(a.err, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
               fail = true;
               break;
             }
@@ -234,11 +232,9 @@ __device__ __forceinline__ bool ts_wait(const TSArgs& a, const unsigned long lon
     __builtin_amdgcn_s_sleep(1);
     g = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if ((++polls & 255u) == 0) {
-      int why = 0;
-      if (__hip_atomic_load(a.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) why = 2;
-      else if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) why = 1;
+      const int why = give_up(a.err, a.abort_flag, t0, a.timeout_ticks);
       if (why) {
-        __hip_atomic_store(a.err, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (why > 0) __hip_atomic_store(a.err, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return false;
       }
     }

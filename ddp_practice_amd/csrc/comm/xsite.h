@@ -76,6 +76,18 @@ __device__ __forceinline__ uint32_t xsite_epoch(const XSite& xs, unsigned long l
   return (uint32_t)(tk >> 32) + 1u;
 }
 
+// Checked every 256 polls of a bounded wait: 2 = aborted (watchdog), 1 = this wait timed
+// out, -1 = an earlier exchange of this rank already failed (its error word is set):
+// give up at once -- this rank's epochs no longer match its peers', so every later
+// wait would only run into its own timeout; the poisoned engine then costs
+// microseconds per exchange until the error is reported (host error word, watchdog).
+__device__ __forceinline__ int give_up(const int* err, const int* abort_flag, long long t0, long long timeout_ticks) {
+  if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return 2;
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return -1;
+  if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) return 1;
+  return 0;
+}
+
 // Spin until granule *src carries epoch ep (bounded: abort flag / timeout ->
 // error word, fail = true).  g: the granule already loaded.
 __device__ __forceinline__ float xsite_wait(const XSite& xs, const unsigned long long* src, unsigned long long g,
@@ -84,11 +96,9 @@ __device__ __forceinline__ float xsite_wait(const XSite& xs, const unsigned long
     __builtin_amdgcn_s_sleep(1);
     g = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if ((++polls & 255u) == 0) {
-      int why = 0;
-      if (__hip_atomic_load(xs.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) why = 2;
-      else if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xs.timeout_ticks) why = 1;
+      const int why = give_up(xs.err, xs.abort_flag, t0, xs.timeout_ticks);
       if (why) {
-        __hip_atomic_store(xs.err, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (why > 0) __hip_atomic_store(xs.err, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         fail = true;
       }
     }

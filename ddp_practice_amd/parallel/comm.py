@@ -88,6 +88,13 @@ class Communicator:
     def barrier(self) -> None:
         raise NotImplementedError
 
+    # failure detection: a non-empty string once a collective failed asynchronously
+    # (RCCL async error, an xGMI exchange that timed out or was aborted)
+    _injected_error: str = ""  # utils/fault.py "commerr" (tests)
+
+    def async_error(self) -> str:
+        return self._injected_error
+
     @property
     def native(self):
         """C++ Collective handle used by the DDP reducer."""
@@ -182,6 +189,62 @@ class TorchCommunicator(Communicator):
         dist.barrier(group=self.group)
 
 
+class HostCommunicator(TorchCommunicator):
+    """Device tensors staged through host memory over the gloo process group.
+
+    The last-resort fallback of the one-GPU rehearsal (``bench.py --share-gpu``, where RCCL
+    refuses several ranks on one device and the xGMI engine is what failed): slow,
+    synchronous and not capturable (run it with graphs off), but it shares no device
+    memory or spin-waits with a peer, so it cannot stall on one."""
+
+    def __init__(self, device, group=None):
+        super().__init__(group)
+        self.device = torch.device(device)
+        self.xgmi_status = "off (host-staged gloo)"
+
+    @staticmethod
+    def _staged(t, fn):
+        if t.device.type == "cpu":
+            fn(t)
+            return t
+        h = t.detach().cpu()
+        fn(h)
+        t.copy_(h)
+        return t
+
+    def all_reduce_(self, t, op="sum"):
+        return self._staged(t, lambda h: TorchCommunicator.all_reduce_(self, h, op))
+
+    def broadcast_(self, t, src=0):
+        return self._staged(t, lambda h: TorchCommunicator.broadcast_(self, h, src))
+
+    def reduce_(self, t, dst=0, op="sum"):
+        return self._staged(t, lambda h: TorchCommunicator.reduce_(self, h, dst, op))
+
+    def all_gather_into_tensor(self, out, inp):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        TorchCommunicator.all_gather_into_tensor(self, h, inp.detach().cpu())
+        out.copy_(h)
+        return out
+
+    def reduce_scatter_tensor(self, out, inp, op="sum"):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        TorchCommunicator.reduce_scatter_tensor(self, h, inp.detach().cpu(), op)
+        out.copy_(h)
+        return out
+
+    def all_to_all_single(self, out, inp):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        TorchCommunicator.all_to_all_single(self, h, inp.detach().cpu())
+        out.copy_(h)
+        return out
+
+    def barrier(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        dist.barrier(group=self.group)
+
+
 class RcclCommunicator(Communicator):
     """The native RCCL communicator (one per process / GPU)."""
 
@@ -243,7 +306,7 @@ class RcclCommunicator(Communicator):
         self._c.barrier()
 
     def async_error(self) -> str:
-        return self._c.async_error()
+        return self._injected_error or self._c.async_error()
 
     @property
     def xgmi_max_bytes(self) -> int:
@@ -333,7 +396,7 @@ class XgmiCommunicator(Communicator):
         dist.barrier(group=self.group)
 
     def async_error(self) -> str:
-        return self.xgmi.error_string()
+        return self._injected_error or self.xgmi.error_string()
 
     def abort(self):
         self.xgmi.abort()
@@ -380,8 +443,8 @@ def comm_mode() -> str:
     m = os.environ.get("DPA_COMM", "auto").lower()
     if os.environ.get("DPA_XGMI", "1") == "0":
         m = "rccl"
-    if m not in ("auto", "rccl", "xgmi"):
-        raise ValueError(f"DPA_COMM must be auto, rccl or xgmi, got {m!r}")
+    if m not in ("auto", "rccl", "xgmi", "host"):
+        raise ValueError(f"DPA_COMM must be auto, rccl, xgmi or host, got {m!r}")
     return m
 
 
@@ -401,8 +464,8 @@ def setup_xgmi(rc: "RcclCommunicator", store, key: str) -> str:
     call sequence.  Returns a status string.
     """
     mode = comm_mode()
-    if mode == "rccl":
-        return "off (--comm rccl)"
+    if mode in ("rccl", "host"):
+        return f"off (--comm {mode})"
     if store is None:
         store = dist.distributed_c10d._get_default_store()
     max_bytes = int(float(os.environ.get("DPA_XGMI_MAX_BYTES", XGMI_DEFAULT_MAX_BYTES)))
@@ -554,12 +617,14 @@ def init_process_group(backend: str | None = None, init_method: str | None = "en
 
     ``backend``: "nccl"/"rccl" (GPU; the framework's collectives use the native
     RCCL communicator) or "gloo" (CPU).  Default: "nccl" if a GPU is present.
+    Rehearsal backends for ranks sharing one GPU: "xgmi" (all-reduces on the xGMI
+    engine, host collectives on gloo) and "host" (everything staged through gloo).
     """
     global _DEFAULT, _GEN
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     backend = backend.lower()
-    torch_backend = "nccl" if backend in ("nccl", "rccl") else "gloo" if backend == "xgmi" else backend
+    torch_backend = "nccl" if backend in ("nccl", "rccl") else "gloo" if backend in ("xgmi", "host") else backend
     kw = {}
     if timeout is not None:
         kw["timeout"] = timeout
@@ -574,6 +639,10 @@ def init_process_group(backend: str | None = None, init_method: str | None = "en
             device = torch.device("cuda", torch.cuda.current_device())
         _GEN += 1
         _DEFAULT = XgmiCommunicator(r, w, device, key=f"dpa_xgmi_{_GEN}")
+    elif backend == "host":
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
+        _DEFAULT = HostCommunicator(device)
     elif torch_backend == "nccl" and w == 1 and not Communicator.force_active:
         # a world of one has no collective to run: skip the RCCL communicator bring-up
         # (1.15 s of a 3-epoch ddp_main run at W=1, plus 0.3 s of teardown)
@@ -631,6 +700,41 @@ def barrier() -> None:
         _DEFAULT.barrier()
     elif dist.is_initialized():
         dist.barrier()
+
+
+_HEALTH_SEQ = 0
+
+
+def agree_on_errors(comm: Communicator | None = None, timeout_s: float = 600.0) -> str:
+    """Every rank's communicator error word, gathered through the rendezvous store.
+
+    Not through the communicator: it may be the broken part (an xGMI exchange that
+    timed out leaves RCCL healthy but the engine poisoned; a dead peer leaves every
+    collective hanging).  Every rank must call it at the same point (a collective in
+    that sense); all of them return the same string: "" when every rank is healthy,
+    else ``"rank r: <error>; ..."``.  Used before checkpointing and after every epoch,
+    so no rank saves or reports a model trained through skipped updates.
+    """
+    global _HEALTH_SEQ
+    comm = comm if comm is not None else _DEFAULT
+    local = ""
+    if comm is not None:
+        if comm.device.type == "cuda":
+            torch.cuda.synchronize(comm.device)  # the error word covers everything issued so far
+        local = comm.async_error() or ""
+        if local == "destroyed":
+            local = ""
+    world = comm.world_size if comm is not None else 1
+    if world == 1 or not dist.is_initialized():
+        return f"rank 0: {local}" if local else ""
+    _HEALTH_SEQ += 1
+    store = dist.distributed_c10d._get_default_store()
+    key = f"dpa_health/{_GEN}/{_HEALTH_SEQ}"
+    store.set(f"{key}/{comm.rank}", local)
+    keys = [f"{key}/{r}" for r in range(world)]
+    store.wait(keys, datetime.timedelta(seconds=timeout_s))
+    errs = [(r, store.get(k).decode()) for r, k in enumerate(keys)]
+    return "; ".join(f"rank {r}: {e}" for r, e in errs if e)
 
 
 def max_over_ranks(x: float) -> float:

@@ -109,18 +109,52 @@ class DistributedDataParallel(nn.Module):
             mod = getattr(mod, p)
         return mod
 
+    _DTYPE_CODES = {torch.float32: 1, torch.float16: 2, torch.bfloat16: 3, torch.float64: 4}
+    _MAX_DIMS = 8
+
+    def _param_table(self) -> torch.Tensor:
+        """One int64 row per parameter: [ndim, dtype, dim0 .. dim7 (-1 padded)]."""
+        rows = []
+        for p in self._params:
+            if p.dim() > self._MAX_DIMS:
+                raise RuntimeError(f"DDP: parameters of more than {self._MAX_DIMS} dims are not supported")
+            dims = list(p.shape) + [-1] * (self._MAX_DIMS - p.dim())
+            rows.append([p.dim(), self._DTYPE_CODES.get(p.dtype, 99)] + dims)
+        return torch.tensor(rows, dtype=torch.int64).reshape(len(rows), 2 + self._MAX_DIMS)
+
     def _verify_param_shapes(self):
+        """Exact parameter count, shapes and dtypes on every rank (torch's
+        _verify_param_shape_across_processes, torch/distributed/utils.py:281): the count
+        first (every rank must gather the same number of rows), then the whole table,
+        compared row by row with rank 0's."""
         if self.comm.world_size == 1:
             return
-        sig = [float(len(self._params))] + [float(hash(tuple(p.shape)) % 1000003) for p in self._params]
-        t = torch.tensor(sig, dtype=torch.float64, device=self.comm.device)
-        if t.device.type == "cuda":
-            t = t.float()
-        lo, hi = t.clone(), t.clone()
-        self.comm.all_reduce_(lo, "min")
-        self.comm.all_reduce_(hi, "max")
-        if not torch.equal(lo, hi):
-            raise RuntimeError("DDP: parameter shapes/count differ across ranks")
+        W, dev = self.comm.world_size, self.comm.device
+        n = torch.tensor([len(self._params)], dtype=torch.int64, device=dev)
+        counts = torch.empty(W, dtype=torch.int64, device=dev)
+        self.comm.all_gather_into_tensor(counts, n)
+        counts = counts.cpu().tolist()
+        if len(set(counts)) != 1:
+            raise RuntimeError(f"DDP expects the same model on every rank, but the ranks have {counts} "
+                               f"parameters (rank {self.comm.rank} has {len(self._params)})")
+        if not self._params:
+            return
+        mine = self._param_table()
+        every = torch.empty((W,) + tuple(mine.shape), dtype=torch.int64, device=dev)
+        self.comm.all_gather_into_tensor(every, mine.to(dev).contiguous())
+        every = every.cpu()
+        codes = {v: k for k, v in self._DTYPE_CODES.items()}
+        for r in range(1, W):
+            bad = (every[r] != every[0]).any(dim=1).nonzero().flatten().tolist()
+            if bad:
+                i = bad[0]
+
+                def desc(row):
+                    nd = int(row[0])
+                    return f"shape {tuple(int(d) for d in row[2:2 + nd])} dtype {codes.get(int(row[1]), 'other')}"
+
+                raise RuntimeError(f"DDP expects the same model on every rank, but parameter {i} has "
+                                   f"{desc(every[r][i])} on rank {r} and {desc(every[0][i])} on rank 0")
 
     def _flat_broadcast(self, tensors):
         by_dtype: dict = {}

@@ -111,10 +111,12 @@ class SyncBatchNorm(_BatchNorm):
         return _comm.default_comm()
 
     def _native(self, x) -> bool:
-        """4-D device input in training: the channels_last kernels of ops/bn_nhwc.py
+        """Device input in training: the channels_last kernels of ops/bn_nhwc.py
         (statistics, one all-reduce of 2C+1 floats, apply; backward sums, one all-reduce,
-        elementwise) instead of the torch-op path below."""
-        return (x.is_cuda and x.dim() == 4 and self.training and self.track_running_stats
+        elementwise) instead of the torch-op path below.  Any rank >= 2 (BatchNorm1d's
+        [N, C] / [N, C, L], BatchNorm3d's [N, C, D, H, W]) runs as the 4-D view
+        [N, C, prod(rest), 1]: the per-channel statistics are the same reduction."""
+        return (x.is_cuda and x.dim() >= 2 and x.numel() > 0 and self.training and self.track_running_stats
                 and x.dtype in (torch.float32, torch.float16, torch.bfloat16))
 
     def forward(self, x):
@@ -130,6 +132,9 @@ class SyncBatchNorm(_BatchNorm):
                     self._zeros = torch.zeros(C, device=x.device)
             w = self.weight if self.affine else self._ones
             b = self.bias if self.affine else self._zeros
+            if x.dim() != 4:
+                x4 = x.reshape(x.shape[0], C, -1, 1)
+                return _NativeBN.apply(x4, w, b, self, comm if comm.active else None).contiguous().view(x.shape)
             y = _NativeBN.apply(x, w, b, self, comm if comm.active else None)
             return y if x.is_contiguous(memory_format=torch.channels_last) else y.contiguous()
         if not self.training or not self.track_running_stats or not comm.active:

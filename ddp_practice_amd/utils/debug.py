@@ -55,6 +55,9 @@ class CheckedCommunicator(Communicator):
     def __getattr__(self, name):
         return getattr(self.__dict__["inner"], name)
 
+    def async_error(self) -> str:
+        return self._injected_error or self.inner.async_error()
+
     def _check(self, op: str, t: torch.Tensor | None, red: str = "-", root: int = -1) -> None:
         if _capturing():
             return

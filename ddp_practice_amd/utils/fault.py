@@ -12,6 +12,8 @@ checked at their first step).  Kinds:
     slow:secs      sleep once               (straggler)
     inf            write +inf into a parameter gradient before the optimizer step
                    (GradScaler must skip the step and back off the scale)
+    commerr        the communicator reports an asynchronous error from then on
+                   (as after an xGMI exchange timeout): checkpoints must not be written
 
 The reference has no fault injection.
 """
@@ -22,7 +24,7 @@ import time
 
 import torch
 
-_KINDS = ("exit", "raise", "hang", "slow", "inf")
+_KINDS = ("exit", "raise", "hang", "slow", "inf", "commerr")
 
 
 class Fault:
@@ -48,9 +50,10 @@ def parse(spec: str) -> list[Fault]:
 
 
 class FaultInjector:
-    def __init__(self, rank: int, spec: str | None = None):
+    def __init__(self, rank: int, spec: str | None = None, comm=None):
         spec = os.environ.get("DPA_FAULT", "") if spec is None else spec
         self.rank = rank
+        self.comm = comm
         self.faults = [f for f in parse(spec) if f.rank is None or f.rank == rank]
 
     def __bool__(self):
@@ -77,6 +80,8 @@ class FaultInjector:
                     time.sleep(min(1.0, max(0.0, end - time.monotonic())))
             if f.kind == "slow":
                 time.sleep(float(f.arg or 1.0))
+            if f.kind == "commerr" and self.comm is not None:
+                self.comm._injected_error = f"injected communicator error (rank {self.rank}, step {step})"
 
     def corrupt_grads(self, step: int, params) -> bool:
         """Called between backward and the optimizer step (eager steps only)."""

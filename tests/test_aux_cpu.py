@@ -169,3 +169,61 @@ def test_resume_and_metrics(tmp_path):
     assert r.returncode == 0, r.stderr
     second = torch.load(tmp_path / "b.pt", weights_only=True)["model"]
     assert int(second["layer1.1.num_batches_tracked"]) == 2 * int(first["layer1.1.num_batches_tracked"])
+
+
+def test_watchdog_default_on_for_distributed_runs(monkeypatch):
+    """the three CLIs arm the watchdog by default at world size > 1 with torch's
+    ProcessGroupNCCL default (10 min); one process keeps it off; the flag / env override it."""
+    import argparse
+
+    from ddp_practice_amd.cli import DEFAULT_WATCHDOG_S, watchdog_timeout
+
+    monkeypatch.delenv("DPA_WATCHDOG_TIMEOUT", raising=False)
+    ns = argparse.Namespace(watchdog_timeout=None)
+    assert DEFAULT_WATCHDOG_S == 600.0
+    assert watchdog_timeout(ns, 2) == 600.0 and watchdog_timeout(ns, 8) == 600.0
+    assert watchdog_timeout(ns, 1) == 0.0
+    assert watchdog_timeout(argparse.Namespace(watchdog_timeout=0.0), 8) == 0.0
+    assert watchdog_timeout(argparse.Namespace(watchdog_timeout=5.0), 1) == 5.0
+    monkeypatch.setenv("DPA_WATCHDOG_TIMEOUT", "7")
+    assert watchdog_timeout(ns, 2) == 7.0
+
+
+@pytest.mark.slow
+def test_hung_rank_detected_without_flag(tmp_path):
+    """No --watchdog-timeout flag: the default-on watchdog (timeout shortened through the
+    environment only) ends a run whose rank 1 hangs; no checkpoint is written."""
+    r, dt = _cli([os.path.join(ROOT, "ddp_main.py"), "-e", "1", "--synthetic", "--train-samples", "512",
+                  "--test-samples", "64", "--cpu-procs", "2", "--amp-dtype", "fp32",
+                  "--checkpoint", str(tmp_path / "ck.pt")],
+                 {"MASTER_PORT": str(_dist.free_port()), "DPA_MASTER_ADDR": "127.0.0.1", "DPA_FAULT": "1:3:hang",
+                  "DPA_WATCHDOG_TIMEOUT": "4"})
+    assert r.returncode != 0
+    assert "[dpa watchdog]" in r.stderr, r.stderr[-2000:]
+    assert dt < 120
+    assert not (tmp_path / "ck.pt").exists()
+
+
+@pytest.mark.slow
+def test_comm_error_blocks_checkpoint(tmp_path):
+    """A communicator error on ONE rank (injected at step 3, as after an xGMI exchange
+    timeout) is agreed on by every rank after the epoch: all ranks stop with the error, and
+    no checkpoint is saved from a model trained through skipped updates."""
+    r, dt = _cli([os.path.join(ROOT, "ddp_main.py"), "-e", "2", "--synthetic", "--train-samples", "512",
+                  "--test-samples", "64", "--cpu-procs", "2", "--amp-dtype", "fp32",
+                  "--checkpoint", str(tmp_path / "ck.pt")],
+                 {"MASTER_PORT": str(_dist.free_port()), "DPA_MASTER_ADDR": "127.0.0.1",
+                  "DPA_FAULT": "1:3:commerr"})
+    assert r.returncode != 0, r.stdout
+    assert "communicator error after epoch 1" in r.stderr and "rank 1: injected" in r.stderr, r.stderr[-2000:]
+    assert "begin training of epoch 2/2" not in r.stdout
+    assert not (tmp_path / "ck.pt").exists()
+
+
+def test_agree_on_errors_single_process():
+    from ddp_practice_amd.parallel.comm import LocalCommunicator, agree_on_errors
+
+    c = LocalCommunicator()
+    assert agree_on_errors(c) == ""
+    c._injected_error = "boom"
+    assert agree_on_errors(c) == "rank 0: boom"

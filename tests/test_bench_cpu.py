@@ -11,8 +11,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.slow
 
 
-def _bench(args, timeout=300):
+def _bench(args, timeout=300, extra_env=None):
     env = dict(os.environ)
+    env.update(extra_env or {})
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     env["CUDA_VISIBLE_DEVICES"] = ""
@@ -45,3 +46,49 @@ def test_bench_self_launches_two_ranks():
 def test_bench_rejects_bad_gpu_count():
     r = _bench(["--gpus", "0"])
     assert r.returncode == 2 and "--gpus must be >= 1" in r.stderr
+
+
+_SMALL = ["--gpus", "2", "--steps", "7", "--warmup", "3", "--epochs", "1", "--train-samples", "640",
+          "--test-samples", "128"]
+
+
+def test_bench_hung_rank_falls_back_with_comm_error():
+    """rank 1 hangs at step 3 -> both ranks' watchdogs report and exit 124 (no
+    30-min gloo stall), the supervisor re-runs fresh ranks (--comm rccl) and prints ONE line
+    carrying the value, ``fallback`` and the first attempt's ``comm_error``; rc 0."""
+    r = _bench(_SMALL, extra_env={"DPA_FAULT": "1:3:hang", "DPA_BENCH_WATCHDOG": "4"})
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1
+    rec = recs[0]
+    assert rec["value"] > 0 and rec["fallback"] == "rccl"
+    assert "rank 1" in rec["comm_error"] and "watchdog" in rec["comm_error"]
+    assert [a["ok"] for a in rec["attempts"]] == [False, True]
+
+
+def test_bench_every_attempt_failing_reports_rc3():
+    """A fault that recurs in the fallback: one line, value null, comm_error set, rc 3."""
+    r = _bench(_SMALL, extra_env={"DPA_FAULT": "1:2:exit:9", "DPA_FAULT_RETRY": "1"})
+    assert r.returncode == 3, r.stdout + r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1 and recs[0]["value"] is None
+    assert "rank 1: exit 9" in recs[0]["comm_error"]
+
+
+def test_bench_under_torchrun_one_line():
+    """The driver's N > 1 launch: every torchrun worker supervises one fresh rank; rank 0
+    prints the only line."""
+    from tests._dist import free_port
+
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+                        os.path.join(ROOT, "bench.py"), *_SMALL], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout
+    assert recs[0]["n_gpus"] == 2 and recs[0]["ranks_seen"] == 2 and recs[0]["comm_error"] == ""

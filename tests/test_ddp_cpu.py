@@ -52,3 +52,17 @@ def test_bucket_assignment_matches_torch(shapes):
 
 def test_ddp_deferred_grad_sync_flush():
     assert run(W.ddp_deferred_flush, world=2) == [True, True]
+
+
+def test_distributed_facade_async_op_returns_work():
+    assert run(W.facade_async_work, world=2) == [True, True]
+
+
+@pytest.mark.parametrize("kind,needle", [("ok", ""), ("shape", "parameter 0 has shape (3, 8)"),
+                                         ("dtype", "dtype torch.float64"), ("count", "parameters")])
+def test_ddp_exact_shape_and_dtype_check(kind, needle):
+    outs = run(W.ddp_shape_mismatch, world=2, args=(kind,))
+    if kind == "ok":
+        assert outs == ["", ""]
+    else:
+        assert all(needle in o for o in outs), outs

@@ -437,3 +437,52 @@ def test_sgd_picks_large_fused_step(C):
         C.optim.amp_sgd_large, C.optim.sgd_step = orig_l, orig_s
     assert opt._fuse_kind() == "large"
     assert calls["large"] >= 2  # the first iteration runs unfused (GradScaler learns the optimizer count)
+
+
+def test_grad_scaler_scale_twice_on_native_ce(C):
+    """A second GradScaler.scale() of the same native CE loss (logging, a retry) takes the
+    generic multiply instead of failing on the already-consumed pre-scaled value (ADVICE r2);
+    both scaled values and the resulting gradient are right."""
+    from ddp_practice_amd.amp import GradScaler
+    from ddp_practice_amd.ops.head import cross_entropy
+
+    torch.manual_seed(0)
+    sc = GradScaler(init_scale=64.0)
+    sc._lazy_init(torch.device(DEV))
+    logits = torch.randn(16, 10, device=DEV)
+    tgt = torch.randint(0, 10, (16,), device=DEV)
+    r = logits.clone().requires_grad_()
+    ref = torch.nn.functional.cross_entropy(r, tgt)
+    (ref * 64.0).backward()
+    a = logits.clone().requires_grad_()
+    loss = cross_entropy(a, tgt)
+    first = sc.scale(loss)
+    second = sc.scale(loss)
+    torch.testing.assert_close(first.float(), ref.detach() * 64.0, rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(second.float(), ref.detach() * 64.0, rtol=1e-5, atol=1e-3)
+    second.backward()
+    torch.testing.assert_close(a.grad, r.grad, rtol=1e-5, atol=1e-4)
+
+
+def test_large_table_pinned_when_reused_under_capture(C):
+    """The large fused step's device table built by an eager warm-up and then looked up from
+    the cache during capture stays referenced for the optimizer's life, and the
+    cache key carries each tensor's size."""
+    from ddp_practice_amd.optim import SGD
+
+    ps = [torch.nn.Parameter(torch.randn(n, device=DEV)) for n in (600000, 5, 9408, 2048) * 10]
+    opt = SGD(ps, lr=0.1)
+    for p in ps:
+        p.grad = torch.randn_like(p)
+    params, grads = list(ps), [p.grad for p in ps]
+    t_eager = opt._large_table(params, grads, [], [])
+    assert not opt.__dict__.get("_amp_tables_pinned")
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g):
+            t_cap = opt._large_table(params, grads, [], [])
+    assert t_cap is t_eager
+    assert any(x is t_eager for x in opt._amp_tables_pinned)
+    key = next(iter(opt._amp_tables))
+    assert key[0][0] == (ps[0].data_ptr(), ps[0].numel())
