@@ -409,8 +409,6 @@ class _Chunks:
 def run_rank(args) -> int:
     if args.model == "resnet50":
         return bench_resnet(args)
-    import threading
-
     t_proc0 = _process_t0()
     marks = {"bench_imported": round(_IMPORT_T - t_proc0, 3)}
     import torch
@@ -420,20 +418,6 @@ def run_rank(args) -> int:
     from ddp_practice_amd.data import synthetic
 
     marks["package_imported"] = round(time.time() - t_proc0, 3)
-
-    # the synthetic sets (numpy; releases the GIL in its bulk work) are generated on a side
-    # thread while this one brings up the HIP context, the communicator and the extension
-    box: dict = {}
-
-    def _data():
-        try:
-            box["train"] = synthetic(args.train_samples, seed=1, name="synthetic-MNIST-train")
-            box["test"] = synthetic(args.test_samples, seed=2, name="synthetic-MNIST-test")
-        except BaseException as e:  # noqa: BLE001 - re-raised below
-            box["error"] = e
-
-    th = threading.Thread(target=_data, name="dpa-bench-data", daemon=True)
-    th.start()
 
     if args.comm:
         os.environ["DPA_COMM"] = args.comm
@@ -467,11 +451,10 @@ def run_rank(args) -> int:
     rank = ddist.get_rank()
     health = _Health(comm, rank, world, gpu)
     marks["comm_ready"] = round(time.time() - t_proc0, 3)
-    th.join()
+    # the synthetic sets are generated in HBM by one kernel (host numpy on CPU): data/mnist.py
+    train_ds = synthetic(args.train_samples, seed=1, name="synthetic-MNIST-train", device=dev)
+    test_ds = synthetic(args.test_samples, seed=2, name="synthetic-MNIST-test", device=dev)
     marks["data_ready"] = round(time.time() - t_proc0, 3)
-    if "error" in box:
-        raise box["error"]
-    train_ds, test_ds = box["train"], box["test"]
     health.check("setup")
     B = args.batch_size
     ctx = dict(args=args, world=world, rank=rank, dev=dev, gpu=gpu, dist_path=dist_path, local_rank=local_rank,

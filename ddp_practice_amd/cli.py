@@ -178,14 +178,22 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
     from ddp_practice_amd.utils import FaultInjector, Watchdog, set_tracing, trace_range
 
     phase("imports")
-    # The datasets (IDX read or synthetic generation, numpy: releases the GIL in its bulk
-    # ops) are built on a side thread while this one brings up the HIP context, the native
-    # extension and the model; joined before the loaders need them.
+    # The datasets (IDX read or host synthetic generation, numpy: releases the GIL in its
+    # bulk ops) are built on a side thread while this one brings up the HIP context, the
+    # native extension and the model; joined before the loaders need them.  A synthetic
+    # MNIST set on a HIP device is instead generated in HBM by one kernel, on this thread
+    # once the device is current (data/mnist.py synthetic(device=)).
     ds_box: dict = {}
 
     resnet = getattr(args, "model", "convnet") == "resnet50"
+    from ddp_practice_amd.data.mnist import idx_available
+
+    on_device = (not resnet and torch.cuda.is_available()
+                 and (args.synthetic or not idx_available(args.data_root)))
 
     def _build_datasets():
+        if on_device:
+            return
         try:
             if resnet:  # no ImageNet reader (no network): the synthetic set, small by default
                 from ddp_practice_amd.data import synthetic_imagenet
@@ -250,6 +258,11 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
     ds_thread.join()
     if "error" in ds_box:
         raise ds_box["error"]
+    if on_device:
+        ds_box["train"] = MNIST(root=args.data_root, train=True, force_synthetic=True, n=args.train_samples,
+                                device=dev)
+        ds_box["test"] = MNIST(root=args.data_root, train=False, force_synthetic=True, n=args.test_samples,
+                               device=dev)
     train_dataset, test_dataset = ds_box["train"], ds_box["test"]
     if distributed:
         g = torch.Generator()

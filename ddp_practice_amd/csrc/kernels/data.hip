@@ -59,6 +59,59 @@ gather_kernel(const uint8_t* __restrict__ imgs, const int64_t* __restrict__ labe
   }
 }
 
+// ----------------------------------------------------------------------------
+// Synthetic MNIST-shaped set generated in HBM (data/mnist.py ``synthetic(device=)``):
+// image i = clip(variant[label_i, shift_i] * amp_i + 0.25 * N(0,1), 0, 1) as uint8,
+// the per-pixel normal from a counter-based generator (splitmix64 of
+// seed * 2^40 + i * npix + p, Box-Muller), so the set never exists on the host
+// (no 0.5 s of host RNG and no 47 MB upload at start-up) and the host reference
+// (mnist._noise_np) computes the same formula.
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(NTHR)
+synth_kernel(const float* __restrict__ variants, const int64_t* __restrict__ labels,
+             const int64_t* __restrict__ which, const float* __restrict__ amp, int nvar, unsigned long long seed,
+             int64_t n, int npix, uint8_t* __restrict__ out) {
+  const int64_t total = n * npix;
+  for (int64_t e = (int64_t)blockIdx.x * NTHR + threadIdx.x; e < total; e += (int64_t)gridDim.x * NTHR) {
+    const int64_t i = e / npix;
+    const int p = (int)(e - i * npix);
+    const float base = variants[(labels[i] * nvar + which[i]) * npix + p] * amp[i];
+    const unsigned long long z = splitmix64((seed << 40) + (unsigned long long)e);
+    const float u1 = (float)((z >> 40) + 1ull) * (1.0f / 16777216.0f);  // (0, 1]
+    const float u2 = (float)((z >> 16) & 0xFFFFFFull) * (1.0f / 16777216.0f);
+    const float g = sqrtf(-2.0f * logf(u1)) * cosf(6.2831853071795864f * u2);
+    const float v = fminf(fmaxf(base + 0.25f * g, 0.0f), 1.0f) * 255.0f + 0.5f;
+    out[e] = (uint8_t)v;
+  }
+}
+
+void synth(at::Tensor variants, at::Tensor labels, at::Tensor which, at::Tensor amp, int64_t nvar, int64_t seed,
+           at::Tensor out) {
+  DPA_CHECK_INPUT(variants); DPA_CHECK_INPUT(labels); DPA_CHECK_INPUT(which); DPA_CHECK_INPUT(amp);
+  DPA_CHECK_INPUT(out);
+  TORCH_CHECK(variants.scalar_type() == at::kFloat && amp.scalar_type() == at::kFloat);
+  TORCH_CHECK(labels.scalar_type() == at::kLong && which.scalar_type() == at::kLong && out.scalar_type() == at::kByte);
+  const int64_t n = out.size(0);
+  const int npix = (int)(out.numel() / std::max<int64_t>(n, 1));
+  TORCH_CHECK(labels.numel() == n && which.numel() == n && amp.numel() == n && nvar > 0);
+  TORCH_CHECK(variants.numel() % (nvar * npix) == 0, "variants must be [classes, nvar, npix]");
+  const int64_t nclass = variants.numel() / (nvar * npix);
+  (void)nclass;  // labels < classes and which < nvar are the host's contract (data/mnist.py)
+  if (n == 0) return;
+  const int64_t total = n * npix;
+  const int grid = (int)std::min<int64_t>((total + NTHR - 1) / NTHR, 8192);
+  hipLaunchKernelGGL(synth_kernel, dim3(grid), dim3(NTHR), 0, cur_stream(), variants.data_ptr<float>(),
+                     labels.data_ptr<int64_t>(), which.data_ptr<int64_t>(), amp.data_ptr<float>(), (int)nvar,
+                     (unsigned long long)seed, n, npix, out.data_ptr<uint8_t>());
+  DPA_CHECK_LAUNCH();
+}
+
 // step < 0 => use and advance the device counter `ctr` (int32[2]).
 void gather(at::Tensor imgs, at::Tensor labels, at::Tensor order, at::Tensor ctr, int64_t step, at::Tensor out,
             at::Tensor lab_out, double scale, double shift) {
@@ -84,6 +137,7 @@ void gather(at::Tensor imgs, at::Tensor labels, at::Tensor order, at::Tensor ctr
 void register_data(pybind11::module& m) {
   auto s = m.def_submodule("data", "device-resident dataset gather");
   s.def("gather", &data::gather);
+  s.def("synth", &data::synth);
 }
 
 }  // namespace dpa

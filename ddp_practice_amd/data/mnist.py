@@ -53,8 +53,10 @@ class ImageDataset:
         return int(self.labels.max().item()) + 1 if len(self) else 0
 
     def to_device(self, device) -> tuple[torch.Tensor, torch.Tensor]:
-        """The dataset resident in device memory (cached)."""
+        """The dataset resident in device memory (cached; no copy if it was built there)."""
         key = str(device)
+        if key not in self._dev_cache and self.images.device == torch.device(device):
+            self._dev_cache[key] = (self.images, self.labels)
         if key not in self._dev_cache:
             self._dev_cache[key] = (self.images.to(device), self.labels.to(device))
         return self._dev_cache[key]
@@ -117,9 +119,32 @@ def _prototypes(rng: np.random.Generator, classes: int, hw: int) -> np.ndarray:
     return protos
 
 
+def _splitmix64(z: np.ndarray) -> np.ndarray:
+    z = z + np.uint64(0x9E3779B97F4A7C15)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def _noise_np(seed: int, start: int, count: int) -> np.ndarray:
+    """N(0,1) float32 for the flat pixel counters [start, start+count) -- the host twin of
+    csrc/kernels/data.hip synth_kernel (splitmix64 + Box-Muller)."""
+    with np.errstate(over="ignore"):
+        z = _splitmix64((np.uint64(seed) << np.uint64(40)) + np.arange(start, start + count, dtype=np.uint64))
+    u1 = ((z >> np.uint64(40)) + np.uint64(1)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    u2 = ((z >> np.uint64(16)) & np.uint64(0xFFFFFF)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    return (np.sqrt(np.float32(-2.0) * np.log(u1)) * np.cos(np.float32(6.2831853071795864) * u2)).astype(np.float32)
+
+
 def synthetic(n: int, seed: int, classes: int = 10, hw: int = 28, proto_seed: int = 1234,
-              name: str = "synthetic") -> ImageDataset:
-    """Deterministic MNIST-shaped dataset (prototypes shared across splits via ``proto_seed``)."""
+              name: str = "synthetic", device=None) -> ImageDataset:
+    """Deterministic MNIST-shaped dataset (prototypes shared across splits via ``proto_seed``).
+
+    Per sample: a class prototype shifted by up to 2 pixels, scaled by U(0.6, 1), plus
+    0.25 * N(0,1) pixel noise from a counter-based generator.  ``device`` = a HIP device:
+    the images are generated in HBM by one kernel (csrc/kernels/data.hip synth) and never
+    exist on the host; on the host the same formula runs in numpy (equal up to float
+    rounding of the noise)."""
     prng = np.random.default_rng(proto_seed)
     protos = _prototypes(prng, classes, hw)
     shifts = [(dy, dx) for dy in range(-2, 3) for dx in range(-2, 3)]
@@ -127,19 +152,31 @@ def synthetic(n: int, seed: int, classes: int = 10, hw: int = 28, proto_seed: in
     rng = np.random.default_rng(seed)
     labels = rng.integers(0, classes, size=n)
     which = rng.integers(0, len(shifts), size=n)
-    amp = rng.uniform(0.6, 1.0, size=(n, 1, 1)).astype(np.float32)
+    amp = rng.uniform(0.6, 1.0, size=n).astype(np.float32)
+    npix = hw * hw
+    if device is not None and torch.device(device).type == "cuda":
+        from .._ext import load as _load_ext
+
+        dev = torch.device(device)
+        out = torch.empty((n, hw, hw), dtype=torch.uint8, device=dev)
+        lab = torch.from_numpy(labels.astype(np.int64)).to(dev)
+        _load_ext().data.synth(torch.from_numpy(variants).to(dev), lab, torch.from_numpy(which.astype(np.int64)).to(dev),
+                               torch.from_numpy(amp).to(dev), len(shifts), int(seed), out)
+        return ImageDataset(out, lab, name=name)
     out = np.empty((n, hw, hw), np.uint8)
-    chunk = 8192
+    chunk = 4096
+    flat_var = variants.reshape(classes * len(shifts), npix)
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
-        base = variants[labels[s:e], which[s:e]] * amp[s:e]
-        noise = rng.normal(0.0, 0.25, size=base.shape).astype(np.float32)
-        out[s:e] = (np.clip(base + noise, 0.0, 1.0) * 255.0 + 0.5).astype(np.uint8)
+        base = flat_var[labels[s:e] * len(shifts) + which[s:e]] * amp[s:e, None]
+        noise = _noise_np(seed, s * npix, (e - s) * npix).reshape(e - s, npix)
+        v = np.clip(base + np.float32(0.25) * noise, 0.0, 1.0) * np.float32(255.0) + np.float32(0.5)
+        out[s:e] = v.astype(np.uint8).reshape(e - s, hw, hw)
     return ImageDataset(torch.from_numpy(out), torch.from_numpy(labels.astype(np.int64)), name=name)
 
 
 def MNIST(root: str = "./data", train: bool = True, synthetic_fallback: bool = True, force_synthetic: bool = False,
-          n: int | None = None) -> ImageDataset:
+          n: int | None = None, device=None) -> ImageDataset:
     """MNIST from IDX files if present under ``root``, else the synthetic stand-in."""
     if not force_synthetic and idx_available(root):
         return load_idx(root, train)
@@ -147,4 +184,5 @@ def MNIST(root: str = "./data", train: bool = True, synthetic_fallback: bool = T
         raise FileNotFoundError(f"MNIST IDX files not found under {root}/MNIST/raw")
     if n is None:
         n = 60000 if train else 10000
-    return synthetic(n, seed=1 if train else 2, name=f"synthetic-MNIST-{'train' if train else 'test'}")
+    return synthetic(n, seed=1 if train else 2, name=f"synthetic-MNIST-{'train' if train else 'test'}",
+                     device=device)

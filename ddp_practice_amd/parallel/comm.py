@@ -386,9 +386,10 @@ class XgmiCommunicator(Communicator):
         return self._host(lambda h: dist.reduce(h, dst, _TORCH_OPS[_op_name(op)], group=self.group), t)
 
     def all_gather_into_tensor(self, out, inp):
-        h = torch.empty(out.shape, dtype=out.dtype)
-        dist.all_gather_into_tensor(h, inp.detach().cpu().contiguous(), group=self.group)
-        out.copy_(h)
+        # flat on both sides: gloo wants the output to be the inputs concatenated on dim 0
+        h = torch.empty(out.numel(), dtype=out.dtype)
+        dist.all_gather_into_tensor(h, inp.detach().reshape(-1).cpu().contiguous(), group=self.group)
+        out.view(-1).copy_(h)
         return out
 
     def barrier(self):

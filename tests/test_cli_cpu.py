@@ -41,7 +41,7 @@ def test_origin_main_cpu(tmp_path):
     out = _run([os.path.join(ROOT, "origin_main.py"), "-e", "2", "--synthetic", "--train-samples", "2048",
                 "--test-samples", "512", "--seed", "0"], tmp_path)
     acc = _check_stdout(out, 2)
-    assert acc > 20.0  # learns something in 128 tiny steps at lr 1e-4
+    assert acc > 15.0  # learns something in 128 tiny steps at lr 1e-4 (chance: 10 %)
     ck = torch.load(tmp_path / "origin_checkpoint.pt", weights_only=True)
     assert list(ck) == ["model"] and list(ck["model"]) == REF_KEYS
     from ddp_practice_amd.models import ConvNet

@@ -486,3 +486,19 @@ def test_large_table_pinned_when_reused_under_capture(C):
     assert any(x is t_eager for x in opt._amp_tables_pinned)
     key = next(iter(opt._amp_tables))
     assert key[0][0] == (ps[0].data_ptr(), ps[0].numel())
+
+
+def test_synthetic_set_generated_on_device_matches_host(C):
+    """The synthetic MNIST set generated in HBM (csrc/kernels/data.hip synth) is the host
+    formula (data/mnist.py _noise_np): labels identical, pixels equal up to a rare +-1 from
+    float rounding of the noise (logf / cosf vs numpy)."""
+    from ddp_practice_amd.data import synthetic
+
+    host = synthetic(3000, seed=5)
+    dev = synthetic(3000, seed=5, device=DEV)
+    assert dev.images.is_cuda and dev.images.shape == host.images.shape
+    assert torch.equal(dev.labels.cpu(), host.labels)
+    d = (dev.images.cpu().int() - host.images.int()).abs()
+    assert int(d.max()) <= 1 and float((d > 0).float().mean()) < 1e-3
+    ims, lab = dev.to_device(torch.device(DEV))
+    assert ims.data_ptr() == dev.images.data_ptr()  # no copy of a set built on the device
