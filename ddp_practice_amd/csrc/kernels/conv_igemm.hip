@@ -725,7 +725,22 @@ static Geom geom(const at::Tensor& x, const at::Tensor& w, int stride, int pad) 
 
 bool supported(int64_t C, int64_t K) { return C % BK == 0 && K % 64 == 0; }
 
-static int tile_n(int64_t K) { return K % 128 == 0 ? 128 : 64; }
+// Channel tile: 128 where Cout allows it, unless the grid of 128-channel tiles would
+// leave CUs idle -- the deep ResNet layers (7x7 / 14x14 at bs 128: 49-196 pixel tiles)
+// then run 64-channel tiles, twice the workgroups (DPA_IGEMM_FILL: the 128-tile grid
+// size below which 64 is used; 0 = always 128).
+static long long fill_blocks() {
+  static const long long v = [] {
+    const char* e = std::getenv("DPA_IGEMM_FILL");
+    return e ? std::atoll(e) : 512LL;
+  }();
+  return v;
+}
+static int tile_n(int64_t M, int64_t K) {
+  if (K % 128 != 0) return 64;
+  const long long rows = (M + BM - 1) / BM;
+  return rows * (K / 128) < fill_blocks() ? 64 : 128;
+}
 
 // statistics workspace: level-1 + level-2 partial rows (floats) and tickets (int32)
 int64_t stat_part_len(int64_t M, int64_t K) {
@@ -734,7 +749,7 @@ int64_t stat_part_len(int64_t M, int64_t K) {
 }
 int64_t stat_tickets_len(int64_t M, int64_t K) {
   const int64_t rows = (M + BM - 1) / BM, ng = (rows + G1 - 1) / G1;
-  return (K / tile_n(K)) * (ng + 1);
+  return (K / 64) * (ng + 1);  // sized for the 64-channel tile (either tile fits)
 }
 
 // y: [N, K, OH, OW] channels_last (preallocated).  With `stats` (fp32 [3K+4], the
@@ -804,7 +819,7 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
     sa.shift = shift->data_ptr<float>();
     sa.nbt = nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr;
   }
-  const int BN = tile_n(g.K);
+  const int BN = tile_n(g.M, g.K);
   const long long rows = (g.M + BM - 1) / BM;
   const long long blocks = rows * (g.K / BN) * (mode == MODE_S2T ? 4 : 1);
   TORCH_CHECK(blocks < (1LL << 31), "conv_fwd: grid too large");
