@@ -132,7 +132,11 @@ __device__ __forceinline__ void sum_rows(const float* __restrict__ src, int n, f
 }
 
 // slab: [gridDim(pixel tiles)][2][K] partial statistics (null: none)
-template <typename T, int BN, int MODE = MODE_GEN>
+// PIPE: two register sets -- the global loads of K-step t+2 are issued while step t is
+// computed and t+1 waits in the other set, so a load has two compute phases (and a
+// barrier) to arrive instead of one (the operand loads' latency, not the MFMA work,
+// bounded the short-K and few-tile shapes: profiles/r2_conv_igemm_fwd_vs_library_bs128.txt)
+template <typename T, int BN, int MODE = MODE_GEN, bool PIPE = true>
 __global__ void __launch_bounds__(THR)
 conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__ y, StatArgs sa, Geom g) {
   using MMT = MM<T>;
@@ -187,8 +191,7 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
     }
   }
   const long long wrow = MODE == MODE_STEM ? 256 : (long long)g.R * g.S * g.C;
-  f32x4 rx[4], rw[BLD];
-  auto gload = [&](int kt) {
+  auto gload = [&](int kt, f32x4 (&rx)[4], f32x4 (&rw)[BLD]) {
     long long woff;  // this K-step's offset inside a filter row
     if constexpr (MODE == MODE_STEM) {
       const int r = 2 * kt + (cc >> 2), s = (cc & 3) * 2;  // taps (r, s) and (r, s + 1)
@@ -232,7 +235,7 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
     for (int i = 0; i < BLD; ++i)
       rw[i] = *reinterpret_cast<const f32x4*>(w + (long long)(k0 + rr + 32 * i) * wrow + woff);
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](int buf, const f32x4 (&rx)[4], const f32x4 (&rw)[BLD]) {
     T* A = lds[buf];           // weights: rows [0, BN)
     T* B = lds[buf] + BN * BK;  // pixels:  rows [0, BM)
 #pragma unroll
@@ -245,13 +248,8 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
   for (int a = 0; a < CT; ++a)
 #pragma unroll
     for (int b = 0; b < PT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  gload(0);
-  lstore(0);
-  __syncthreads();
   const int fr = lane & 15, fq = lane >> 4;
-  for (int kt = 0; kt < KT; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < KT) gload(kt + 1);
+  auto compute = [&](int buf) {
     const T* A = lds[buf];
     const T* B = lds[buf] + BN * BK;
 #pragma unroll
@@ -268,8 +266,38 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
 #pragma unroll
         for (int b = 0; b < PT; ++b) acc[a][b] = MMT::mma(fa[a], fb[b], acc[a][b]);
     }
-    if (kt + 1 < KT) lstore(buf ^ 1);
+  };
+  f32x4 rxa[4], rwa[BLD];
+  gload(0, rxa, rwa);
+  lstore(0, rxa, rwa);
+  if (KT > 1) gload(1, rxa, rwa);
+  if constexpr (PIPE) {
+    // set a holds odd K-steps, set b even ones: the loop body is unrolled by two so both
+    // sets stay in registers (no dynamic indexing)
+    f32x4 rxb[4], rwb[BLD];
+    if (KT > 2) gload(2, rxb, rwb);
     __syncthreads();
+    for (int kt = 0; kt < KT; kt += 2) {
+      compute(0);
+      if (kt + 1 < KT) lstore(1, rxa, rwa);
+      __syncthreads();
+      if (kt + 3 < KT) gload(kt + 3, rxa, rwa);
+      if (kt + 1 < KT) {
+        compute(1);
+        if (kt + 2 < KT) lstore(0, rxb, rwb);
+        __syncthreads();
+        if (kt + 4 < KT) gload(kt + 4, rxb, rwb);
+      }
+    }
+  } else {
+    __syncthreads();
+    for (int kt = 0; kt < KT; ++kt) {
+      const int buf = kt & 1;
+      compute(buf);
+      if (kt + 1 < KT) lstore(buf ^ 1, rxa, rwa);
+      __syncthreads();
+      if (kt + 2 < KT) gload(kt + 2, rxa, rwa);
+    }
   }
   // epilogue: lane holds channels k0 + wc*BN/2 + 16a + 4fq + j of pixel p0 + wp*64 + 16b + fr.
   // The rounded tile goes through LDS ([pixel][channel], rows padded by 16 B: the
@@ -736,6 +764,14 @@ static long long fill_blocks() {
   }();
   return v;
 }
+// DPA_IGEMM_PIPE=0: the one-register-set forward loop (A/B of conv_fwd_kernel's PIPE)
+static bool fwd_pipe() {
+  static const bool v = [] {
+    const char* e = std::getenv("DPA_IGEMM_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
 static int tile_n(int64_t M, int64_t K) {
   if (K % 128 != 0) return 64;
   const long long rows = (M + BM - 1) / BM;
@@ -829,15 +865,23 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
     const T* wp = reinterpret_cast<const T*>(w.data_ptr());
     T* yp = reinterpret_cast<T*>(y.data_ptr());
     const dim3 gr((unsigned)blocks), th(THR);
+    const bool pipe = fwd_pipe();
+    auto go = [&](auto bn_tag, auto mode_tag) {
+      constexpr int TBN = decltype(bn_tag)::value, TMODE = decltype(mode_tag)::value;
+      if (pipe) hipLaunchKernelGGL((conv_fwd_kernel<T, TBN, TMODE, true>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+      else hipLaunchKernelGGL((conv_fwd_kernel<T, TBN, TMODE, false>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+    };
+    using I128 = std::integral_constant<int, 128>;
+    using I64 = std::integral_constant<int, 64>;
     if (mode == MODE_STEM) {
-      if (BN == 128) hipLaunchKernelGGL((conv_fwd_kernel<T, 128, MODE_STEM>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
-      else hipLaunchKernelGGL((conv_fwd_kernel<T, 64, MODE_STEM>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+      if (BN == 128) go(I128{}, std::integral_constant<int, MODE_STEM>{});
+      else go(I64{}, std::integral_constant<int, MODE_STEM>{});
     } else if (mode == MODE_S2T) {
-      if (BN == 128) hipLaunchKernelGGL((conv_fwd_kernel<T, 128, MODE_S2T>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
-      else hipLaunchKernelGGL((conv_fwd_kernel<T, 64, MODE_S2T>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+      if (BN == 128) go(I128{}, std::integral_constant<int, MODE_S2T>{});
+      else go(I64{}, std::integral_constant<int, MODE_S2T>{});
     } else {
-      if (BN == 128) hipLaunchKernelGGL((conv_fwd_kernel<T, 128>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
-      else hipLaunchKernelGGL((conv_fwd_kernel<T, 64>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+      if (BN == 128) go(I128{}, std::integral_constant<int, MODE_GEN>{});
+      else go(I64{}, std::integral_constant<int, MODE_GEN>{});
     }
   };
   if (x.scalar_type() == at::kBFloat16) launch(__hip_bfloat16{}); else launch(__half{});
