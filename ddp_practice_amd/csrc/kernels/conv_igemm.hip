@@ -450,7 +450,7 @@ __device__ __forceinline__ int wswz(int row, int chunk) {
   return row * CH * 8 + ((chunk ^ m) << 3);
 }
 
-template <typename T, int BM, int BN, int MODE = MODE_GEN>
+template <typename T, int BM, int BN, int MODE = MODE_GEN, bool PIPE = true>  // PIPE: as conv_fwd_kernel
 __global__ void __launch_bounds__(THR)
 conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ slab, Geom g, int splits,
                   long long pps) {
@@ -472,8 +472,7 @@ conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __re
   const int rs = n0 / g.C, c0 = n0 - rs * g.C, fr_ = rs / g.S, fs_ = rs - fr_ * g.S;
   const long long pa = sp * pps, pb = min(g.M, pa + pps);
   const int steps = (int)((pb - pa + BP - 1) / BP);
-  f32x4 ra[LA], rb[LB];
-  auto gload = [&](int t) {
+  auto gload = [&](int t, f32x4 (&ra)[LA], f32x4 (&rb)[LB]) {
     const long long pbase = pa + (long long)t * BP;
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
@@ -510,7 +509,7 @@ conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __re
       rb[i] = v;
     }
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](int buf, const f32x4 (&ra)[LA], const f32x4 (&rb)[LB]) {
     T* A = lds[buf];
     T* B = lds[buf] + BP * BM;
 #pragma unroll
@@ -542,14 +541,7 @@ conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __re
   for (int a = 0; a < MT; ++a)
 #pragma unroll
     for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (steps > 0) {
-    gload(0);
-    lstore(0);
-  }
-  __syncthreads();
-  for (int t = 0; t < steps; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < steps) gload(t + 1);
+  auto compute = [&](int buf) {
     const T* A = lds[buf];
     const T* B = lds[buf] + BP * BM;
 #pragma unroll
@@ -566,8 +558,38 @@ conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __re
 #pragma unroll
         for (int b = 0; b < NT; ++b) acc[a][b] = MM<T>::mma(fa[a], fb[b], acc[a][b]);
     }
-    if (t + 1 < steps) lstore(buf ^ 1);
+  };
+  f32x4 raa[LA], rba[LB];
+  if (steps > 0) {
+    gload(0, raa, rba);
+    lstore(0, raa, rba);
+  }
+  if (steps > 1) gload(1, raa, rba);
+  if constexpr (PIPE) {
+    f32x4 rab[LA], rbb[LB];
+    if (steps > 2) gload(2, rab, rbb);
     __syncthreads();
+    for (int t = 0; t < steps; t += 2) {
+      compute(0);
+      if (t + 1 < steps) lstore(1, raa, rba);
+      __syncthreads();
+      if (t + 3 < steps) gload(t + 3, raa, rba);
+      if (t + 1 < steps) {
+        compute(1);
+        if (t + 2 < steps) lstore(0, rab, rbb);
+        __syncthreads();
+        if (t + 4 < steps) gload(t + 4, rab, rbb);
+      }
+    }
+  } else {
+    __syncthreads();
+    for (int t = 0; t < steps; ++t) {
+      const int buf = t & 1;
+      compute(buf);
+      if (t + 1 < steps) lstore(buf ^ 1, raa, rba);
+      __syncthreads();
+      if (t + 2 < steps) gload(t + 2, raa, rba);
+    }
   }
   // partial tile: C[m = k][n = (r,s,c)]; lane: col n = lane & 15, rows 4*(lane>>4) + j
   float* out = slab + (long long)sp * g.K * RSC;
@@ -947,12 +969,26 @@ void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor grad, int64_t stride, in
     const T* xp = reinterpret_cast<const T*>(x.data_ptr());
     float* sl = slab.data_ptr<float>();
     const dim3 gr((unsigned)blocks), th(THR);
-    if (stem && BM == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 64, MODE_STEM>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
-    else if (stem) hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 64, MODE_STEM>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
-    else if (BM == 128 && BN == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 128>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
-    else if (BM == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 64>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
-    else if (BN == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 128>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
-    else hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 64>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+    const bool pipe = fwd_pipe();
+    auto go = [&](auto bm_tag, auto bn_tag, auto mode_tag) {
+      constexpr int TBM = decltype(bm_tag)::value, TBN = decltype(bn_tag)::value, TMODE = decltype(mode_tag)::value;
+      if (pipe)
+        hipLaunchKernelGGL((conv_wgrad_kernel<T, TBM, TBN, TMODE, true>), gr, th, 0, cur_stream(), dp, xp, sl, g,
+                           (int)sp, pps);
+      else
+        hipLaunchKernelGGL((conv_wgrad_kernel<T, TBM, TBN, TMODE, false>), gr, th, 0, cur_stream(), dp, xp, sl, g,
+                           (int)sp, pps);
+    };
+    using I128 = std::integral_constant<int, 128>;
+    using I64 = std::integral_constant<int, 64>;
+    using MS = std::integral_constant<int, MODE_STEM>;
+    using MG = std::integral_constant<int, MODE_GEN>;
+    if (stem && BM == 128) go(I128{}, I64{}, MS{});
+    else if (stem) go(I64{}, I64{}, MS{});
+    else if (BM == 128 && BN == 128) go(I128{}, I128{}, MG{});
+    else if (BM == 128) go(I128{}, I64{}, MG{});
+    else if (BN == 128) go(I64{}, I128{}, MG{});
+    else go(I64{}, I64{}, MG{});
   };
   if (x.scalar_type() == at::kBFloat16) launch(__hip_bfloat16{}); else launch(__half{});
   DPA_CHECK_LAUNCH();
