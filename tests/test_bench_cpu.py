@@ -92,3 +92,25 @@ def test_bench_under_torchrun_one_line():
     recs = _json_lines(r.stdout)
     assert len(recs) == 1, r.stdout
     assert recs[0]["n_gpus"] == 2 and recs[0]["ranks_seen"] == 2 and recs[0]["comm_error"] == ""
+
+
+def test_bench_under_torchrun_rank_failure_falls_back():
+    """torchrun shape with rank 0's child dying at step 2: every worker's supervisor sees the
+    shared failure flag, kills its child, and all of them re-run fresh children; rank 0's
+    supervisor prints one line with the fallback and the error."""
+    from tests._dist import free_port
+
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(CUDA_VISIBLE_DEVICES="", DPA_FAULT="0:2:exit:7", DPA_BENCH_GRACE="2")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+                        os.path.join(ROOT, "bench.py"), *_SMALL], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout
+    rec = recs[0]
+    assert rec["fallback"] == "rccl" and rec["value"] > 0
+    assert "rank 0: exit 7" in rec["comm_error"]
