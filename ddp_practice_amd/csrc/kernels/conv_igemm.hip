@@ -775,14 +775,14 @@ static Geom geom(const at::Tensor& x, const at::Tensor& w, int stride, int pad) 
 
 bool supported(int64_t C, int64_t K) { return C % BK == 0 && K % 64 == 0; }
 
-// Channel tile: 128 where Cout allows it, unless the grid of 128-channel tiles would
-// leave CUs idle -- the deep ResNet layers (7x7 / 14x14 at bs 128: 49-196 pixel tiles)
-// then run 64-channel tiles, twice the workgroups (DPA_IGEMM_FILL: the 128-tile grid
-// size below which 64 is used; 0 = always 128).
+// Channel tile: 128 where Cout allows it.  DPA_IGEMM_FILL=N: 64-channel tiles when the
+// 128-channel grid has fewer than N workgroups (twice the workgroups on the deep layers).
+// Measured (profiles/r3_igemm_fill_pipe_ab.txt): 3x3 convs at 14x14-28x28 / 256 channels
+// lose 15-23 %, a few deep 1x1 convs gain 5-10 %, the ResNet-50 step loses 2 % -> off.
 static long long fill_blocks() {
   static const long long v = [] {
     const char* e = std::getenv("DPA_IGEMM_FILL");
-    return e ? std::atoll(e) : 512LL;
+    return e ? std::atoll(e) : 0LL;
   }();
   return v;
 }

@@ -280,20 +280,25 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
       const unsigned long long* src = hs.part + (size_t)b * NMAX + n;
 #pragma unroll
       for (int cc = 0; cc < C; ++cc) g[cc] = ld_gran(src + (size_t)cc * BMAX * NMAX);
-      float t = bias_s[n];
+      // rounds of ALL C loads re-issued together (unconditional: a conditional reload was
+      // branched and waited one by one -- one round trip per late granule, not per round)
       const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        bool ready = true;
 #pragma unroll
-      for (int cc = 0; cc < C; ++cc) {
-        while ((uint32_t)(g[cc] >> 32) != ep && !timed_out) {  // bounded: timeout -> error word
-          __builtin_amdgcn_s_sleep(1);
-          g[cc] = ld_gran(src + (size_t)cc * BMAX * NMAX);
-          if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > hs.timeout_ticks) {
-            timed_out = true;
-            __hip_atomic_store(&hs.state[ERR_WORD], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          }
+        for (int cc = 0; cc < C; ++cc) ready &= (uint32_t)(g[cc] >> 32) == ep;
+        if (ready || timed_out) break;  // bounded: timeout -> error word
+        __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+        for (int cc = 0; cc < C; ++cc) g[cc] = ld_gran(src + (size_t)cc * BMAX * NMAX);
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > hs.timeout_ticks) {
+          timed_out = true;
+          __hip_atomic_store(&hs.state[ERR_WORD], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        t += __uint_as_float((uint32_t)g[cc]);
       }
+      float t = bias_s[n];
+#pragma unroll
+      for (int cc = 0; cc < C; ++cc) t += __uint_as_float((uint32_t)g[cc]);
       lgr[k] = Cvt<T>::from_f(t);
       lg_s[o] = Cvt<T>::to_f(lgr[k]);
     }
