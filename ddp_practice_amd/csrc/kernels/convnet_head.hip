@@ -265,12 +265,32 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
     store_pooled();
     return;
   }
+  // 4a. light poll: one lane per (producer, row-tile wave) watches that wave's first granule
+  //     -- a few dozen sc1 loads per round instead of every lane re-reading every partial
+  //     (the full read below then finds (nearly) everything tagged: one more round trip)
+  bool timed_out = false;
+  {
+    const int MTW = (B + 15) / 16;
+    if (tid < C * MTW) {
+      const int cc = tid / MTW, w = tid % MTW;
+      const unsigned long long* src = hs.part + ((size_t)cc * BMAX + 16 * w) * NMAX;
+      const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+      while ((uint32_t)(ld_gran(src) >> 32) != ep) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > hs.timeout_ticks) {
+          __hip_atomic_store(&hs.state[ERR_WORD], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+  }
   DPA_STAMP(4);
   // 4. logits = sum of the C partials + bias, rounded to the storage dtype: every lane issues
-  //    all its granule loads, then re-polls only the ones not yet tagged with this epoch
+  //    all its granule loads, then re-polls (all of them, one round trip per round) while any
+  //    is not yet tagged with this epoch
   constexpr int OIT = BM * NMAX / NT;
   T lgr[OIT];
-  bool timed_out = false;
 #pragma unroll
   for (int k = 0; k < OIT; ++k) {
     const int o = tid + k * NT;
