@@ -15,23 +15,21 @@
 // Decomposition: one workgroup per BN2 channel c (C = 32).  A channel owns 49
 // of the 1568 fc inputs, so it computes its BN / ReLU / pool slice and a K = 49
 // split of the logits (MFMA 16x16x32: rows = images, cols = classes).  The
-// partial logits leave as epoch-tagged 8-byte granules {fp32 value, epoch} in one
-// write-through store each (MI355X_MICROARCH.md "handoff-1to1": the data carries its own
-// readiness -- no ticket, no release flag, no fence).  The epoch of a launch is the
-// workgroup's own launch counter + 1 (state[c]: only workgroup c writes it, every
-// workgroup runs once per launch, launches are stream-ordered).  Without a backward
-// workgroup 0 polls the C partial tiles, adds the bias, rounds the logits to the storage
-// dtype and runs the loss (16 lanes per row, as head.hip ce_fwd_kernel: same formula,
-// same rounding).  When an active GradScaler supplies the scale, EVERY workgroup polls
-// and sums the partials and runs the same loss itself (fixed order: identical
-// d(scale*loss)/dlogits everywhere) and does its channel's share of the fc backward on
-// MFMA:
+// partial logits are stored write-through (`sc1`) and every workgroup takes one
+// agent-scope ticket (MI355X_MICROARCH.md "Valid forms" row 1: no release /
+// acquire fence).  Without a backward the last arriver adds the bias, rounds the
+// logits to the storage dtype and runs the loss (16 lanes per row, as head.hip
+// ce_fwd_kernel: same formula, same rounding).  When an active GradScaler
+// supplies the scale, the last ticket releases every workgroup, each of which
+// sums the partials and runs the same loss itself (fixed order: identical
+// d(scale*loss)/dlogits everywhere, no second hand-off) and does its channel's
+// share of the fc backward on MFMA:
 //   dp2[b, c*49 + j]   = sum_n dls[b, n] * W[n, c*49 + j]       (B x 49, K = N)
 //   dW[n, c*49 + j]    = sum_b dls[b, n] * p2[b, c*49 + j]      (N x 49, K = B)
 // plus the BN2 backward sums of channel c (complete: the channel is whole here).
-// All 32 workgroups of the launch must be co-resident (they wait for each other's
-// granules): 32 << 256 CUs, checked on the host (co_resident); every wait is bounded and
-// sets the error word.
+// All 32 workgroups of the launch must be co-resident (they wait for the last
+// arriver): 32 << 256 CUs, checked on the host (co_resident); every wait is
+// bounded and sets the error word.
 #include "comm/xgmi.h"
 #include "convblock_impl.h"
 
@@ -48,17 +46,14 @@ constexpr int BMAX = 64;   // images (4 MFMA row tiles)
 constexpr int NMAX = 16;   // classes (one MFMA column tile)
 constexpr int KP = 64;     // 49 fc inputs per channel, padded to 2 MFMA k-steps
 
-// state: int64[STATE_LEN] zero-initialised once: [0, C) per-workgroup launch counters,
-// [ERR_WORD] error word (1: a partial never arrived within the timeout).
-// part: [C][BMAX][NMAX] granules, zero-initialised once and kept (a fresh allocation could
-// hold a stale tag equal to a later epoch).
-constexpr int STATE_LEN = 64, ERR_WORD = 40;
+// state: int64[4] zero-initialised once: [0] {generation:32 | tickets:32} (the last
+// ticket stores (generation + 1) << 32: re-arm and release), [1] unused, [2] error word
 struct HeadStep {
   const int64_t* target;
   int64_t ignore_index;
   float smoothing;
   const float* scale;   // GradScaler scale (null: no scaler -> no speculative backward)
-  unsigned long long* part;  // [C][BMAX][NMAX] epoch-tagged partial logits
+  float* part;          // [C][B][NMAX] partial logits (write-through)
   unsigned long long* state;
   float* loss;          // [2]: loss, loss * scale
   float* dlog;          // [B][N] (softmax - onehot) / count, f32
@@ -79,11 +74,7 @@ template <typename T>
 __device__ __forceinline__ void st_wt(float* p, float v) {  // write-through 4-B store (global_store_dword sc1)
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void st_gran(unsigned long long* p, float v, uint32_t ep) {  // dwordx2 sc1
-  __hip_atomic_store(p, ((unsigned long long)ep << 32) | (unsigned long long)__float_as_uint(v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long ld_gran(const unsigned long long* p) {  // L1-bypassing sc1 load
+__device__ __forceinline__ float ld_wt(const float* p) {     // L1-bypassing load (global_load_dword sc1)
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -129,14 +120,12 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
   __shared__ uint8_t ix_s[BM * PP];
   __shared__ float xh_s[BM * PP];
   __shared__ float red[2][NT / 64];
+  __shared__ unsigned long long tk_s;
   __shared__ int cnt_s;
 
   const int tid = threadIdx.x, c = blockIdx.x;
   const int lane = tid & 63, wv = tid >> 6, r = lane & 15, q = lane >> 4;
   const int NPO = B * PP;  // pooled outputs of this channel
-  // this launch's epoch (issued first: its latency hides behind the operand loads); the
-  // counter may be advanced at once -- only the next launch reads it
-  const uint32_t ep = (uint32_t)__hip_atomic_load(&hs.state[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
 
   DPA_STAMP(0);
   // 1. loads: this channel's pre-BN maps (two row pairs per pooled output) and W slice
@@ -253,42 +242,50 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int b = 16 * wv + 4 * q + i;
-      if (b < B) st_gran(&hs.part[((size_t)c * BMAX + b) * NMAX + r], acc[i], ep);
+      if (b < B) st_wt<T>(&hs.part[((size_t)c * B + b) * NMAX + r], acc[i]);
     }
   }
-  if (tid == 0) __hip_atomic_store(&hs.state[c], (unsigned long long)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // publish (write-through stores drained by every wave, then ONE ticket)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    tk_s = __hip_atomic_fetch_add(&hs.state[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
   DPA_STAMP(3);
-  // one writer of the launch-wide outputs (logits, loss, dlog, dls); without a backward
-  // only it needs the logits
-  const bool writer = c == 0;
-  if (!hs.do_bwd && !writer) {
-    store_pooled();
-    return;
-  }
-  // 4a. light poll: one lane per (producer, row-tile wave) watches that wave's first granule
-  //     -- a few dozen sc1 loads per round instead of every lane re-reading every partial
-  //     (the full read below then finds (nearly) everything tagged: one more round trip)
-  bool timed_out = false;
-  {
-    const int MTW = (B + 15) / 16;
-    if (tid < C * MTW) {
-      const int cc = tid / MTW, w = tid % MTW;
-      const unsigned long long* src = hs.part + ((size_t)cc * BMAX + 16 * w) * NMAX;
+  const unsigned long long tk = tk_s;
+  const uint32_t gen = (uint32_t)(tk >> 32);
+  const bool last = (uint32_t)tk == (uint32_t)(C - 1);  // grid = C workgroups (not gridDim: a hidden-arg load)
+  // The last ticket re-arms the word for the next launch ((gen + 1) << 32: stream order, no
+  // workgroup of this launch takes a ticket after it) and that same store releases the
+  // waiting workgroups: with the speculative backward EVERY workgroup then sums the C
+  // partial logits and runs the loss itself (identical fixed-order arithmetic, so identical
+  // results), instead of the last arriver computing it and publishing the loss gradient
+  // behind a second flag -- one cross-workgroup hand-off on the serial path instead of two.
+  if (last) {
+    if (tid == 0)
+      __hip_atomic_exchange(&hs.state[0], ((unsigned long long)(gen + 1u)) << 32, __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT);
+  } else if (hs.do_bwd) {
+    // bounded wait for the last ticket: a timeout sets the error word and goes on
+    if (tid == 0) {
       const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-      while ((uint32_t)(ld_gran(src) >> 32) != ep) {
+      while ((uint32_t)(__hip_atomic_load(&hs.state[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == gen) {
         __builtin_amdgcn_s_sleep(1);
         if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > hs.timeout_ticks) {
-          __hip_atomic_store(&hs.state[ERR_WORD], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(&hs.state[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           break;
         }
       }
     }
     __syncthreads();
+  } else {
+    store_pooled();  // no backward: the last arriver alone computes the loss
+    return;
   }
+  // one writer of the launch-wide outputs (logits, loss, dlog, dls)
+  const bool writer = hs.do_bwd ? c == 0 : true;
   DPA_STAMP(4);
-  // 4. logits = sum of the C partials + bias, rounded to the storage dtype: every lane issues
-  //    all its granule loads, then re-polls (all of them, one round trip per round) while any
-  //    is not yet tagged with this epoch
+  // 4. logits = sum of the C partials + bias, rounded to the storage dtype (every load sc1)
   constexpr int OIT = BM * NMAX / NT;
   T lgr[OIT];
 #pragma unroll
@@ -296,29 +293,12 @@ head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__
     const int o = tid + k * NT;
     const int b = o / NMAX, n = o % NMAX;
     if (b < B && n < N) {
-      unsigned long long g[C];
-      const unsigned long long* src = hs.part + (size_t)b * NMAX + n;
+      float v[C];
 #pragma unroll
-      for (int cc = 0; cc < C; ++cc) g[cc] = ld_gran(src + (size_t)cc * BMAX * NMAX);
-      // rounds of ALL C loads re-issued together (unconditional: a conditional reload was
-      // branched and waited one by one -- one round trip per late granule, not per round)
-      const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-      for (;;) {
-        bool ready = true;
-#pragma unroll
-        for (int cc = 0; cc < C; ++cc) ready &= (uint32_t)(g[cc] >> 32) == ep;
-        if (ready || timed_out) break;  // bounded: timeout -> error word
-        __builtin_amdgcn_s_sleep(2);
-#pragma unroll
-        for (int cc = 0; cc < C; ++cc) g[cc] = ld_gran(src + (size_t)cc * BMAX * NMAX);
-        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > hs.timeout_ticks) {
-          timed_out = true;
-          __hip_atomic_store(&hs.state[ERR_WORD], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      }
+      for (int cc = 0; cc < C; ++cc) v[cc] = ld_wt(&hs.part[((size_t)cc * B + b) * NMAX + n]);
       float t = bias_s[n];
 #pragma unroll
-      for (int cc = 0; cc < C; ++cc) t += __uint_as_float((uint32_t)g[cc]);
+      for (int cc = 0; cc < C; ++cc) t += v[cc];
       lgr[k] = Cvt<T>::from_f(t);
       lg_s[o] = Cvt<T>::to_f(lgr[k]);
     }
@@ -509,10 +489,8 @@ void head_step(at::Tensor y2, at::Tensor fslab2, at::Tensor fstats2, at::Tensor 
   TORCH_CHECK(logits.numel() == (int64_t)B * N && logits.scalar_type() == y2.scalar_type());
   TORCH_CHECK(p2.numel() == (int64_t)B * K && idx2.numel() == p2.numel() && xh2.numel() == p2.numel());
   TORCH_CHECK(target.scalar_type() == at::kLong && target.numel() == B);
-  TORCH_CHECK(part.numel() >= (int64_t)C * BMAX * NMAX && part.scalar_type() == at::kLong && part.is_cuda(),
-              "head_step: part = int64 [C * BMAX * NMAX] granules, zero-initialised once");
-  TORCH_CHECK(state.numel() >= STATE_LEN && state.scalar_type() == at::kLong && state.is_cuda(),
-              "head_step: state = int64 [STATE_LEN], zero-initialised once");
+  TORCH_CHECK(part.numel() >= (int64_t)C * B * NMAX && part.scalar_type() == at::kFloat);
+  TORCH_CHECK(state.numel() >= 4 && state.scalar_type() == at::kLong && state.is_cuda());
   TORCH_CHECK(loss.numel() >= 2 && dlog.numel() == (int64_t)B * N && dlog.scalar_type() == at::kFloat);
   TORCH_CHECK(scale.has_value() == dls.has_value(), "head_step: scale and dls go together");
   const bool bwd = dlsf.has_value();
@@ -542,7 +520,7 @@ void head_step(at::Tensor y2, at::Tensor fslab2, at::Tensor fstats2, at::Tensor 
   hs.ignore_index = ignore_index;
   hs.smoothing = (float)smoothing;
   hs.scale = scale.has_value() ? scale->data_ptr<float>() : nullptr;
-  hs.part = reinterpret_cast<unsigned long long*>(part.data_ptr<int64_t>());
+  hs.part = part.data_ptr<float>();
   hs.state = reinterpret_cast<unsigned long long*>(state.data_ptr<int64_t>());
   hs.loss = loss.data_ptr<float>();
   hs.dlog = dlog.data_ptr<float>();
@@ -578,9 +556,6 @@ void register_convnet_head(pybind11::module& m) {
   DPA_DEF_STAMP_FNS(s);
   s.attr("C") = cnh::C;
   s.attr("NMAX") = cnh::NMAX;
-  s.attr("BMAX") = cnh::BMAX;
-  s.attr("STATE_LEN") = cnh::STATE_LEN;
-  s.attr("ERR_WORD") = cnh::ERR_WORD;
 }
 
 }  // namespace dpa

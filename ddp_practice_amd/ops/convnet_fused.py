@@ -169,9 +169,7 @@ class ConvNetFn(torch.autograd.Function):
 
                 scale = active_scale(dev) if _HEAD_SPEC else None
                 f32 = dict(dtype=torch.float32, device=dev)
-                hstate, hpart = state
-                if hpart is None:  # ticket-protocol build (experiment .so): a partial buffer per call
-                    hpart = torch.empty(32 * B * 16, **f32)
+                part = torch.empty(32 * B * 16, **f32)
                 loss_buf = torch.empty(2, **f32)
                 dlog = torch.empty((B, N), **f32)
                 dls = torch.empty((B, N), dtype=cdtype, device=dev) if scale is not None else None
@@ -187,12 +185,12 @@ class ConvNetFn(torch.autograd.Function):
                     spec = (dls, out, views, dp2, bsum2)
                     _load_ext().convnet_head.head_step(
                         y2, fslab2, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, wfc, bfc, logits, p2, idx2, xh2, labels,
-                        int(ce_cfg[0]), float(ce_cfg[1]), scale, hpart, hstate, loss_buf, dlog, dls, dlsf, dp2,
+                        int(ce_cfg[0]), float(ce_cfg[1]), scale, part, state, loss_buf, dlog, dls, dlsf, dp2,
                         views[8], views[9], views[6], views[7], bsum2, xc, HEAD_TIMEOUT_S)
                 else:
                     _load_ext().convnet_head.head_step(
                         y2, fslab2, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, wfc, bfc, logits, p2, idx2, xh2, labels,
-                        int(ce_cfg[0]), float(ce_cfg[1]), None, hpart, hstate, loss_buf, dlog, None, None, None, None,
+                        int(ce_cfg[0]), float(ce_cfg[1]), None, part, state, loss_buf, dlog, None, None, None, None,
                         None, None, None, None, xc, HEAD_TIMEOUT_S)
                 ctx.spec = spec
                 if holder is not None:
@@ -338,16 +336,10 @@ def convnet_forward(model, x, comm=None, cdtype=None):
         else:
             holder = {}
             state = getattr(model, "_dpa_head_state", None)
-            if state is None or state[0].device != x.device:
-                # (launch counters + error word, epoch-tagged partial-logit granules) of the
-                # head-step launch: zeroed once and kept -- the kernel advances the counters
-                # itself, so graph replays need no reset (csrc/kernels/convnet_head.hip)
-                H = _load_ext().convnet_head
-                if hasattr(H, "STATE_LEN"):
-                    state = (torch.zeros(int(H.STATE_LEN), dtype=torch.int64, device=x.device),
-                             torch.zeros(int(H.C) * int(H.BMAX) * int(H.NMAX), dtype=torch.int64, device=x.device))
-                else:  # ticket / flag / error words of the ticket-protocol head (A/B builds)
-                    state = (torch.zeros(4, dtype=torch.int64, device=x.device), None)
+            if state is None or state.device != x.device:
+                # ticket / flag / error words of the head-step launch (zeroed once; the
+                # kernel re-arms them itself, so graph replays need no reset)
+                state = torch.zeros(4, dtype=torch.int64, device=x.device)
                 model._dpa_head_state = state
     wcnt = None
     if training:
