@@ -583,7 +583,10 @@ def _xgmi_selftest(rc: "RcclCommunicator", x, twoshot_max_bytes: int = 0) -> tup
     # the in-kernel exchange sites (fused SyncBN consumers, the fused AMP-SGD gradient
     # average: csrc/comm/xsite.h) -- the same peer-write protocol run from inside a
     # multi-workgroup launch; every workgroup must see the rank-ordered sum
-    for it, n in enumerate((65, 96, 1568)):
+    # sizes within a SyncBN site's row (csrc/comm/xsite.h kSiteVals = 128 floats; the ConvNet's
+    # rows are 2C+1 = 33 / 65 forward and 2C = 32 / 64 backward): a larger n is rejected by
+    # site_probe, which would fail the vote and turn the engine off on every multi-GPU run
+    for it, n in enumerate((33, 65, 128)):
         t = torch.randn(n, generator=g).to(device=rc.device)
         o = torch.empty(4 * n, device=rc.device)
         good = True

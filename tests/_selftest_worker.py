@@ -70,7 +70,12 @@ class _Engine:
         (t if out is None else out).copy_(r)
 
     def site_probe(self, site, t, o, nblk):
+        # the real engine's limits (csrc/comm/xgmi_allreduce.hip site_probe): a SyncBN site id
+        # and at most kSiteVals = 128 floats -- checked AFTER the stand-in's gloo traffic so a
+        # violation fails this rank's vote instead of desynchronising the stand-in
         s = self._sum(t, "sum")
+        if t.numel() > 128 or not 0 <= site < 7:
+            raise RuntimeError("site_probe: <= 128 contiguous f32 values")
         if self.rank == self.bad and self.bad_kind == "site":
             raise RuntimeError("site probe failed on this rank")
         o.copy_(s.repeat(nblk))

@@ -113,3 +113,11 @@ def test_ddp_syncbn_fused_graph_matches_plain(rccl, amp, graph):
     for (n, p), (_, q) in zip(ddp.module.state_dict().items(), plain.state_dict().items()):
         torch.testing.assert_close(p.float(), q.float(), rtol=tol, atol=tol, msg=n)
     assert int(ddp.module.layer1[1].num_batches_tracked) == 2 * 10
+
+
+def test_xgmi_engine_passes_its_selftest_at_forced_world1(rccl):
+    """The RCCL communicator's start-up self-test (parallel/comm.setup_xgmi) must pass on a
+    healthy device, or every multi-GPU run silently loses the xGMI engine (round 2's self-test
+    probed a SyncBN site with 1568 floats > its 128-float row and failed on every box)."""
+    assert rccl.xgmi_status.startswith("on"), rccl.xgmi_status
+    assert rccl.xgmi is not None and rccl.xgmi_max_bytes > 0
