@@ -132,11 +132,7 @@ __device__ __forceinline__ void sum_rows(const float* __restrict__ src, int n, f
 }
 
 // slab: [gridDim(pixel tiles)][2][K] partial statistics (null: none)
-// PIPE: two register sets -- the global loads of K-step t+2 are issued while step t is
-// computed and t+1 waits in the other set, so a load has two compute phases (and a
-// barrier) to arrive instead of one (the operand loads' latency, not the MFMA work,
-// bounded the short-K and few-tile shapes: profiles/r2_conv_igemm_fwd_vs_library_bs128.txt)
-template <typename T, int BN, int MODE = MODE_GEN, bool PIPE = true>
+template <typename T, int BN, int MODE = MODE_GEN>
 __global__ void __launch_bounds__(THR)
 conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__ y, StatArgs sa, Geom g) {
   using MMT = MM<T>;
@@ -191,7 +187,8 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
     }
   }
   const long long wrow = MODE == MODE_STEM ? 256 : (long long)g.R * g.S * g.C;
-  auto gload = [&](int kt, f32x4 (&rx)[4], f32x4 (&rw)[BLD]) {
+  f32x4 rx[4], rw[BLD];
+  auto gload = [&](int kt) {
     long long woff;  // this K-step's offset inside a filter row
     if constexpr (MODE == MODE_STEM) {
       const int r = 2 * kt + (cc >> 2), s = (cc & 3) * 2;  // taps (r, s) and (r, s + 1)
@@ -235,7 +232,7 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
     for (int i = 0; i < BLD; ++i)
       rw[i] = *reinterpret_cast<const f32x4*>(w + (long long)(k0 + rr + 32 * i) * wrow + woff);
   };
-  auto lstore = [&](int buf, const f32x4 (&rx)[4], const f32x4 (&rw)[BLD]) {
+  auto lstore = [&](int buf) {
     T* A = lds[buf];           // weights: rows [0, BN)
     T* B = lds[buf] + BN * BK;  // pixels:  rows [0, BM)
 #pragma unroll
@@ -248,8 +245,13 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
   for (int a = 0; a < CT; ++a)
 #pragma unroll
     for (int b = 0; b < PT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  gload(0);
+  lstore(0);
+  __syncthreads();
   const int fr = lane & 15, fq = lane >> 4;
-  auto compute = [&](int buf) {
+  for (int kt = 0; kt < KT; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < KT) gload(kt + 1);
     const T* A = lds[buf];
     const T* B = lds[buf] + BN * BK;
 #pragma unroll
@@ -266,38 +268,8 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
 #pragma unroll
         for (int b = 0; b < PT; ++b) acc[a][b] = MMT::mma(fa[a], fb[b], acc[a][b]);
     }
-  };
-  f32x4 rxa[4], rwa[BLD];
-  gload(0, rxa, rwa);
-  lstore(0, rxa, rwa);
-  if (KT > 1) gload(1, rxa, rwa);
-  if constexpr (PIPE) {
-    // set a holds odd K-steps, set b even ones: the loop body is unrolled by two so both
-    // sets stay in registers (no dynamic indexing)
-    f32x4 rxb[4], rwb[BLD];
-    if (KT > 2) gload(2, rxb, rwb);
+    if (kt + 1 < KT) lstore(buf ^ 1);
     __syncthreads();
-    for (int kt = 0; kt < KT; kt += 2) {
-      compute(0);
-      if (kt + 1 < KT) lstore(1, rxa, rwa);
-      __syncthreads();
-      if (kt + 3 < KT) gload(kt + 3, rxa, rwa);
-      if (kt + 1 < KT) {
-        compute(1);
-        if (kt + 2 < KT) lstore(0, rxb, rwb);
-        __syncthreads();
-        if (kt + 4 < KT) gload(kt + 4, rxb, rwb);
-      }
-    }
-  } else {
-    __syncthreads();
-    for (int kt = 0; kt < KT; ++kt) {
-      const int buf = kt & 1;
-      compute(buf);
-      if (kt + 1 < KT) lstore(buf ^ 1, rxa, rwa);
-      __syncthreads();
-      if (kt + 2 < KT) gload(kt + 2, rxa, rwa);
-    }
   }
   // epilogue: lane holds channels k0 + wc*BN/2 + 16a + 4fq + j of pixel p0 + wp*64 + 16b + fr.
   // The rounded tile goes through LDS ([pixel][channel], rows padded by 16 B: the
@@ -450,7 +422,7 @@ __device__ __forceinline__ int wswz(int row, int chunk) {
   return row * CH * 8 + ((chunk ^ m) << 3);
 }
 
-template <typename T, int BM, int BN, int MODE = MODE_GEN, bool PIPE = true>  // PIPE: as conv_fwd_kernel
+template <typename T, int BM, int BN, int MODE = MODE_GEN>
 __global__ void __launch_bounds__(THR)
 conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ slab, Geom g, int splits,
                   long long pps) {
@@ -472,7 +444,8 @@ conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __re
   const int rs = n0 / g.C, c0 = n0 - rs * g.C, fr_ = rs / g.S, fs_ = rs - fr_ * g.S;
   const long long pa = sp * pps, pb = min(g.M, pa + pps);
   const int steps = (int)((pb - pa + BP - 1) / BP);
-  auto gload = [&](int t, f32x4 (&ra)[LA], f32x4 (&rb)[LB]) {
+  f32x4 ra[LA], rb[LB];
+  auto gload = [&](int t) {
     const long long pbase = pa + (long long)t * BP;
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
@@ -509,7 +482,7 @@ conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __re
       rb[i] = v;
     }
   };
-  auto lstore = [&](int buf, const f32x4 (&ra)[LA], const f32x4 (&rb)[LB]) {
+  auto lstore = [&](int buf) {
     T* A = lds[buf];
     T* B = lds[buf] + BP * BM;
 #pragma unroll
@@ -541,7 +514,14 @@ conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __re
   for (int a = 0; a < MT; ++a)
 #pragma unroll
     for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto compute = [&](int buf) {
+  if (steps > 0) {
+    gload(0);
+    lstore(0);
+  }
+  __syncthreads();
+  for (int t = 0; t < steps; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < steps) gload(t + 1);
     const T* A = lds[buf];
     const T* B = lds[buf] + BP * BM;
 #pragma unroll
@@ -558,38 +538,8 @@ conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __re
 #pragma unroll
         for (int b = 0; b < NT; ++b) acc[a][b] = MM<T>::mma(fa[a], fb[b], acc[a][b]);
     }
-  };
-  f32x4 raa[LA], rba[LB];
-  if (steps > 0) {
-    gload(0, raa, rba);
-    lstore(0, raa, rba);
-  }
-  if (steps > 1) gload(1, raa, rba);
-  if constexpr (PIPE) {
-    f32x4 rab[LA], rbb[LB];
-    if (steps > 2) gload(2, rab, rbb);
+    if (t + 1 < steps) lstore(buf ^ 1);
     __syncthreads();
-    for (int t = 0; t < steps; t += 2) {
-      compute(0);
-      if (t + 1 < steps) lstore(1, raa, rba);
-      __syncthreads();
-      if (t + 3 < steps) gload(t + 3, raa, rba);
-      if (t + 1 < steps) {
-        compute(1);
-        if (t + 2 < steps) lstore(0, rab, rbb);
-        __syncthreads();
-        if (t + 4 < steps) gload(t + 4, rab, rbb);
-      }
-    }
-  } else {
-    __syncthreads();
-    for (int t = 0; t < steps; ++t) {
-      const int buf = t & 1;
-      compute(buf);
-      if (t + 1 < steps) lstore(buf ^ 1, raa, rba);
-      __syncthreads();
-      if (t + 2 < steps) gload(t + 2, raa, rba);
-    }
   }
   // partial tile: C[m = k][n = (r,s,c)]; lane: col n = lane & 15, rows 4*(lane>>4) + j
   float* out = slab + (long long)sp * g.K * RSC;
@@ -775,30 +725,7 @@ static Geom geom(const at::Tensor& x, const at::Tensor& w, int stride, int pad) 
 
 bool supported(int64_t C, int64_t K) { return C % BK == 0 && K % 64 == 0; }
 
-// Channel tile: 128 where Cout allows it.  DPA_IGEMM_FILL=N: 64-channel tiles when the
-// 128-channel grid has fewer than N workgroups (twice the workgroups on the deep layers).
-// Measured (profiles/r3_igemm_fill_pipe_ab.txt): 3x3 convs at 14x14-28x28 / 256 channels
-// lose 15-23 %, a few deep 1x1 convs gain 5-10 %, the ResNet-50 step loses 2 % -> off.
-static long long fill_blocks() {
-  static const long long v = [] {
-    const char* e = std::getenv("DPA_IGEMM_FILL");
-    return e ? std::atoll(e) : 0LL;
-  }();
-  return v;
-}
-// DPA_IGEMM_PIPE=0: the one-register-set forward loop (A/B of conv_fwd_kernel's PIPE)
-static bool fwd_pipe() {
-  static const bool v = [] {
-    const char* e = std::getenv("DPA_IGEMM_PIPE");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-static int tile_n(int64_t M, int64_t K) {
-  if (K % 128 != 0) return 64;
-  const long long rows = (M + BM - 1) / BM;
-  return rows * (K / 128) < fill_blocks() ? 64 : 128;
-}
+static int tile_n(int64_t K) { return K % 128 == 0 ? 128 : 64; }
 
 // statistics workspace: level-1 + level-2 partial rows (floats) and tickets (int32)
 int64_t stat_part_len(int64_t M, int64_t K) {
@@ -807,7 +734,7 @@ int64_t stat_part_len(int64_t M, int64_t K) {
 }
 int64_t stat_tickets_len(int64_t M, int64_t K) {
   const int64_t rows = (M + BM - 1) / BM, ng = (rows + G1 - 1) / G1;
-  return (K / 64) * (ng + 1);  // sized for the 64-channel tile (either tile fits)
+  return (K / tile_n(K)) * (ng + 1);
 }
 
 // y: [N, K, OH, OW] channels_last (preallocated).  With `stats` (fp32 [3K+4], the
@@ -877,7 +804,7 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
     sa.shift = shift->data_ptr<float>();
     sa.nbt = nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr;
   }
-  const int BN = tile_n(g.M, g.K);
+  const int BN = tile_n(g.K);
   const long long rows = (g.M + BM - 1) / BM;
   const long long blocks = rows * (g.K / BN) * (mode == MODE_S2T ? 4 : 1);
   TORCH_CHECK(blocks < (1LL << 31), "conv_fwd: grid too large");
@@ -887,23 +814,15 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
     const T* wp = reinterpret_cast<const T*>(w.data_ptr());
     T* yp = reinterpret_cast<T*>(y.data_ptr());
     const dim3 gr((unsigned)blocks), th(THR);
-    const bool pipe = fwd_pipe();
-    auto go = [&](auto bn_tag, auto mode_tag) {
-      constexpr int TBN = decltype(bn_tag)::value, TMODE = decltype(mode_tag)::value;
-      if (pipe) hipLaunchKernelGGL((conv_fwd_kernel<T, TBN, TMODE, true>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
-      else hipLaunchKernelGGL((conv_fwd_kernel<T, TBN, TMODE, false>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
-    };
-    using I128 = std::integral_constant<int, 128>;
-    using I64 = std::integral_constant<int, 64>;
     if (mode == MODE_STEM) {
-      if (BN == 128) go(I128{}, std::integral_constant<int, MODE_STEM>{});
-      else go(I64{}, std::integral_constant<int, MODE_STEM>{});
+      if (BN == 128) hipLaunchKernelGGL((conv_fwd_kernel<T, 128, MODE_STEM>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+      else hipLaunchKernelGGL((conv_fwd_kernel<T, 64, MODE_STEM>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
     } else if (mode == MODE_S2T) {
-      if (BN == 128) go(I128{}, std::integral_constant<int, MODE_S2T>{});
-      else go(I64{}, std::integral_constant<int, MODE_S2T>{});
+      if (BN == 128) hipLaunchKernelGGL((conv_fwd_kernel<T, 128, MODE_S2T>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+      else hipLaunchKernelGGL((conv_fwd_kernel<T, 64, MODE_S2T>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
     } else {
-      if (BN == 128) go(I128{}, std::integral_constant<int, MODE_GEN>{});
-      else go(I64{}, std::integral_constant<int, MODE_GEN>{});
+      if (BN == 128) hipLaunchKernelGGL((conv_fwd_kernel<T, 128>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+      else hipLaunchKernelGGL((conv_fwd_kernel<T, 64>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
     }
   };
   if (x.scalar_type() == at::kBFloat16) launch(__hip_bfloat16{}); else launch(__half{});
@@ -969,26 +888,12 @@ void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor grad, int64_t stride, in
     const T* xp = reinterpret_cast<const T*>(x.data_ptr());
     float* sl = slab.data_ptr<float>();
     const dim3 gr((unsigned)blocks), th(THR);
-    const bool pipe = fwd_pipe();
-    auto go = [&](auto bm_tag, auto bn_tag, auto mode_tag) {
-      constexpr int TBM = decltype(bm_tag)::value, TBN = decltype(bn_tag)::value, TMODE = decltype(mode_tag)::value;
-      if (pipe)
-        hipLaunchKernelGGL((conv_wgrad_kernel<T, TBM, TBN, TMODE, true>), gr, th, 0, cur_stream(), dp, xp, sl, g,
-                           (int)sp, pps);
-      else
-        hipLaunchKernelGGL((conv_wgrad_kernel<T, TBM, TBN, TMODE, false>), gr, th, 0, cur_stream(), dp, xp, sl, g,
-                           (int)sp, pps);
-    };
-    using I128 = std::integral_constant<int, 128>;
-    using I64 = std::integral_constant<int, 64>;
-    using MS = std::integral_constant<int, MODE_STEM>;
-    using MG = std::integral_constant<int, MODE_GEN>;
-    if (stem && BM == 128) go(I128{}, I64{}, MS{});
-    else if (stem) go(I64{}, I64{}, MS{});
-    else if (BM == 128 && BN == 128) go(I128{}, I128{}, MG{});
-    else if (BM == 128) go(I128{}, I64{}, MG{});
-    else if (BN == 128) go(I64{}, I128{}, MG{});
-    else go(I64{}, I64{}, MG{});
+    if (stem && BM == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 64, MODE_STEM>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+    else if (stem) hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 64, MODE_STEM>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+    else if (BM == 128 && BN == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 128>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+    else if (BM == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 64>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+    else if (BN == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 128>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 64>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
   };
   if (x.scalar_type() == at::kBFloat16) launch(__hip_bfloat16{}); else launch(__half{});
   DPA_CHECK_LAUNCH();
