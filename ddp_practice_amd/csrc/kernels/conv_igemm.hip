@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
+#include <vector>
 
 #include "common.h"
 
@@ -74,6 +75,7 @@ struct StatArgs {
   float* stats;       // [3K+4]
   const float* shift; // running mean (the sums are taken around it)
   int64_t* nbt;       // num_batches_tracked (bumped once) or null
+  int defer;          // 1: level-1 rows only (plain stores, no ticket), stat_tree_kernel follows
 };
 
 // Hand-off without fences (MI355X_MICROARCH.md "valid forms"): partial rows are
@@ -245,6 +247,13 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
   for (int a = 0; a < CT; ++a)
 #pragma unroll
     for (int b = 0; b < PT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // the statistics' shift (running mean) for this lane's epilogue chunk, loaded with tile 0:
+  // loaded after the K loop it cost every workgroup a dependent global-load latency
+  float shp[8];
+  if (sa.part != nullptr) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) shp[j] = sa.shift[k0 + (tid % (BN / 8)) * 8 + j];
+  }
   gload(0);
   lstore(0);
   __syncthreads();
@@ -306,7 +315,7 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       s1[j] = s2[j] = 0.f;
-      sh[j] = sa.shift[k0 + ch * 8 + j];
+      sh[j] = shp[j];
     }
 #pragma unroll
     for (int it = 0; it < BM / RPI; ++it) {
@@ -340,13 +349,20 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
     rows = (g.M + BM - 1) / BM;
     NG = (int)((rows + G1 - 1) / G1);
     float* lvl1 = sa.part + (long long)bn * rows * (2 * BN);
-    for (int t = tid; t < 2 * BN; t += THR) {
-      const int q = t / BN, c = t % BN;
-      st_wt(lvl1 + bm * (2 * BN) + t, red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c]);
+    if (sa.defer) {  // plain stores; the tree runs in stat_tree_kernel after this launch
+      for (int t = tid; t < 2 * BN; t += THR) {
+        const int q = t / BN, c = t % BN;
+        lvl1[bm * (2 * BN) + t] = red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c];
+      }
+    } else {
+      for (int t = tid; t < 2 * BN; t += THR) {
+        const int q = t / BN, c = t % BN;
+        st_wt(lvl1 + bm * (2 * BN) + t, red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c]);
+      }
+      grp = (int)(bm / G1);
+      gsz = (int)min((long long)G1, rows - (long long)grp * G1);
+      last1 = last_arriver(sa.tickets + bn * NG + grp, (unsigned)gsz, &s_flag);
     }
-    grp = (int)(bm / G1);
-    gsz = (int)min((long long)G1, rows - (long long)grp * G1);
-    last1 = last_arriver(sa.tickets + bn * NG + grp, (unsigned)gsz, &s_flag);
   }
   // output stores: whole 16-B chunks, consecutive lanes along a pixel's channels
   const T* aux = reinterpret_cast<const T*>(g.aux);
@@ -399,6 +415,315 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
   }
   if (bn == 0 && tid == 0) {
     sa.stats[2 * g.K] = (float)g.M;
+    if (sa.nbt != nullptr) sa.nbt[0] = sa.nbt[0] + 1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 1x1 convolution (pad 0, stride 1 or 2) as a plain GEMM over the NHWC rows:
+//   y[p][k] = sum_c x[row(p)][c] * w[k][c]      (M = pixels, N = Cout, K = C)
+// -- the forward of 36 of ResNet-50's 53 convs and, with the transposed filter, their
+// data gradients.  The general kernel above is LDS-bound on these shapes: a 64 x 64
+// wave tile reads 32 FLOP per LDS byte and its register-staged ds_write_b128 stores
+// cost ~13 LDS cycles per KiB, so the MFMAs idle behind the LDS (2x slower than
+// hipBLASLt on the deep layers, profiles/r2_conv_igemm_fwd_vs_library_bs128.txt).
+// This one:
+//   * BP x BN tile (256 or 128 pixels x 128 or 64 channels), 4 waves as 2 x 2, wave tile
+//     BP/2 x BN/2 (128 x 64: 43 FLOP per LDS byte);
+//   * operands go global -> LDS with global_load_lds_dwordx4 (no VGPRs, no ds_write):
+//     one wave-instruction fills 8 rows of 128 B, lane l its row l/8 at slot l%8; the
+//     XOR swizzle of the LDS image (chunk ^ row&7, the same image the general kernel
+//     writes) goes on the per-lane SOURCE address, since the LDS side is lane-linear;
+//   * two LDS buffers, ONE barrier per K-step: wait the landed tile (vmcnt(0)) +
+//     barrier, issue tile t+1 into the other buffer, MFMA on tile t; every LDS byte
+//     lives in one __shared__ array (a second __shared__ object can make hipcc wait
+//     vmcnt(0) before each K-step's first LDS read, cdna_hip_programming.md §5);
+//   * the epilogue of the general kernel: rounded tile staged through LDS, the next
+//     BN's statistics tree, whole-row stores, accumulate / aux for the fused gradients.
+template <typename T, int BP, int BN>
+struct G1x1Lds {
+  static constexpr int STAGE = (BP + BN) * BK;            // elements per buffer
+  static constexpr int RS = BN + 8;                       // epilogue tile row stride
+  static constexpr int TILE = BP * RS * (int)sizeof(T);   // epilogue tile bytes
+  static constexpr int RED = TILE;                        // float red[4][2][BN]
+  static constexpr int FLAG = RED + 4 * 2 * BN * 4;       // int s_flag
+  static constexpr int SCR = FLAG + 16;                   // float scr[THR]
+  static constexpr int EPI = SCR + THR * 4;
+  static constexpr int MAIN = 2 * STAGE * (int)sizeof(T);
+  static constexpr int SHIFT = MAIN > EPI ? MAIN : EPI;  // float shift[BN] (statistics only)
+  static constexpr int BYTES = SHIFT + BN * 4;
+};
+
+// one global_load_lds_dwordx4: 16 B per lane from `src` (per lane) to dst + 16 * lane (dst
+// wave-uniform).  A non-template device function: called directly inside the kernel
+// template, hipcc's host pass fails to instantiate it and emits no launch stub (undefined
+// __device_stub__ at load time).
+typedef __attribute__((address_space(3))) void* lds_vptr;
+__device__ __forceinline__ void glds16(const void* src, void* dst) {
+  __builtin_amdgcn_global_load_lds(src, (lds_vptr)dst, 16, 0, 0);
+}
+
+template <typename T, int BP, int BN>
+__global__ void __launch_bounds__(THR)
+conv1x1_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__ y, StatArgs sa, Geom g) {
+  using MMT = MM<T>;
+  using L = G1x1Lds<T, BP, BN>;
+  typedef typename MMT::frag frag;
+  constexpr int CT = BN / 32;  // 16-channel tiles per wave
+  constexpr int PT = BP / 32;  // 16-pixel tiles per wave
+  constexpr int AR = BP / 32;  // pixel rows per lane per K-step (8 rows per wave-instruction)
+  constexpr int WR = BN / 32;  // filter rows per lane per K-step
+  __shared__ __attribute__((aligned(16))) unsigned char smem[L::BYTES];
+  T* const lds = reinterpret_cast<T*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wp = wave & 1, wc = wave >> 1;
+  const int nct = g.K / BN;
+  // XCD-aware order (as conv_fwd_kernel): the channel tiles of one pixel tile share an L2
+  const unsigned nwg = gridDim.x, hw = blockIdx.x;
+  const unsigned q8 = nwg / 8, r8 = nwg % 8, xcd = hw % 8, slot = hw / 8;
+  const unsigned lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const long long bm = lid / nct;
+  const int bn = (int)(lid % nct);
+  const long long p0 = bm * BP;
+  const int k0 = bn * BN;
+  // this lane's source rows: wave-instruction i covers rows (4i + wave) * 8 .. + 7, the lane
+  // row (lane >> 3) of them, logical chunk (lane & 7) ^ (row & 7) (row & 7 == lane >> 3)
+  const int lr = lane >> 3, chunk = (lane & 7) ^ lr;
+  unsigned xo[AR], wo[WR];  // element offsets (host-checked < 2^31)
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    long long p = p0 + (i * 4 + wave) * 8 + lr;
+    p = p < g.M ? p : g.M - 1;  // ragged tail: a valid row, its output is not stored
+    long long r = p;
+    if (g.stride != 1) {
+      const int ow = (int)(p % g.OW);
+      const long long t = p / g.OW;
+      const int oh = (int)(t % g.OH);
+      const int n = (int)(t / g.OH);
+      r = ((long long)n * g.H + (long long)oh * g.stride) * g.W + (long long)ow * g.stride;
+    }
+    xo[i] = (unsigned)(r * g.C + chunk * 8);
+  }
+#pragma unroll
+  for (int i = 0; i < WR; ++i) wo[i] = (unsigned)((k0 + (i * 4 + wave) * 8 + lr) * g.C + chunk * 8);
+  const int KT = g.C / BK;
+  auto issue = [&](int kt, int buf) {
+    T* base = lds + buf * L::STAGE;
+    const int ko = kt * BK;
+#pragma unroll
+    for (int i = 0; i < WR; ++i)
+      glds16(w + wo[i] + ko, base + (i * 4 + wave) * 8 * BK);
+#pragma unroll
+    for (int i = 0; i < AR; ++i)
+      glds16(x + xo[i] + ko, base + (BN + (i * 4 + wave) * 8) * BK);
+  };
+  f32x4 acc[CT][PT];
+#pragma unroll
+  for (int a = 0; a < CT; ++a)
+#pragma unroll
+    for (int b = 0; b < PT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  // the statistics' shift (running mean) rides with tile 0 into LDS: loaded after the K loop
+  // it cost every workgroup a dependent global-load latency in its epilogue
+  if (sa.part != nullptr && wave == 0 && lane < BN / 4)
+    glds16(sa.shift + k0 + lane * 4, reinterpret_cast<float*>(smem + L::SHIFT));
+  issue(0, 0);
+  for (int kt = 0; kt < KT; ++kt) {
+    const int buf = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's share of tile kt has landed
+    __syncthreads();  // ... every wave's, and tile kt-1 (the other buffer) is no longer read
+    if (kt + 1 < KT) issue(kt + 1, buf ^ 1);
+    const T* A = lds + buf * L::STAGE;  // filter rows [0, BN)
+    const T* B = A + BN * BK;           // pixel rows [0, BP)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      frag fa[CT], fb[PT];
+#pragma unroll
+      for (int a = 0; a < CT; ++a)
+        fa[a] = *reinterpret_cast<const frag*>(A + swz(wc * (BN / 2) + a * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int b = 0; b < PT; ++b)
+        fb[b] = *reinterpret_cast<const frag*>(B + swz(wp * (BP / 2) + b * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int a = 0; a < CT; ++a)
+#pragma unroll
+        for (int b = 0; b < PT; ++b) acc[a][b] = MMT::mma(fa[a], fb[b], acc[a][b]);
+    }
+  }
+  __syncthreads();  // the last tile is read: the buffers become the epilogue's tile
+  // ---- epilogue (conv_fwd_kernel's, for a BP-pixel tile) ----
+  constexpr int RS = L::RS;
+  T* tile = lds;
+  float(*red)[2][BN] = reinterpret_cast<float(*)[2][BN]>(smem + L::RED);
+  int* s_flag = reinterpret_cast<int*>(smem + L::FLAG);
+  float* scr = reinterpret_cast<float*>(smem + L::SCR);
+  const float* shl = reinterpret_cast<const float*>(smem + L::SHIFT);
+#pragma unroll
+  for (int a = 0; a < CT; ++a) {
+    const int cl = wc * (BN / 2) + a * 16 + 4 * fq;
+#pragma unroll
+    for (int b = 0; b < PT; ++b) {
+      const int pl = wp * (BP / 2) + b * 16 + fr;
+      T v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = Cvt<T>::from_f(acc[a][b][j]);
+      *reinterpret_cast<u16x4*>(tile + pl * RS + cl) = *reinterpret_cast<const u16x4*>(v);
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;     // 16-B chunks per pixel row
+  constexpr int RPI = THR / CPR;  // pixel rows per pass
+  const bool stats = sa.part != nullptr;
+  const int ch = tid % CPR;
+  // output stores: whole 16-B chunks, consecutive lanes along a pixel's channels
+  const T* aux = reinterpret_cast<const T*>(g.aux);
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int it = 0; it < BP / RPI; ++it) {
+      const int pl = it * RPI + tid / CPR;
+      const long long p = p0 + pl;
+      if (p < g.M) {
+        f32x4* dst = reinterpret_cast<f32x4*>(y + p * g.K + k0 + ch * 8);
+        f32x4 raw = *reinterpret_cast<const f32x4*>(tile + pl * RS + ch * 8);
+        int oh = 0, ow = 0, n = 0;
+        if (aux != nullptr) {
+          ow = (int)(p % g.OW);
+          const long long t = p / g.OW;
+          oh = (int)(t % g.OH);
+          n = (int)(t / g.OH);
+        }
+        const bool add_aux = aux != nullptr && !(oh & 1) && !(ow & 1);
+        if (g.accumulate || add_aux) {
+          f32x4 old = {0.f, 0.f, 0.f, 0.f}, ax = {0.f, 0.f, 0.f, 0.f};
+          if (g.accumulate) old = *dst;
+          if (add_aux)
+            ax = *reinterpret_cast<const f32x4*>(
+                aux + (((long long)n * (g.OH >> 1) + (oh >> 1)) * (g.OW >> 1) + (ow >> 1)) * g.K + k0 + ch * 8);
+          const T* a = reinterpret_cast<const T*>(&old);
+          const T* e = reinterpret_cast<const T*>(&ax);
+          T* b = reinterpret_cast<T*>(&raw);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            b[j] = Cvt<T>::from_f(Cvt<T>::to_f(a[j]) + Cvt<T>::to_f(e[j]) + Cvt<T>::to_f(b[j]));
+        }
+        *dst = raw;
+      }
+    }
+  };
+  // Without statistics, or with the tree deferred to stat_tree_kernel, the stores leave
+  // first and drain while the sums are taken from the tile still in LDS; with the
+  // in-launch tree they follow the ticket (its vmcnt(0) must not wait for the tile).
+  const bool stores_first = !stats || sa.defer;
+  if (stores_first) store_tile();
+  bool last1 = false;
+  long long rows = 0;
+  int NG = 0, grp = 0, gsz = 0;
+  if (stats) {
+    float s1[8], s2[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s1[j] = s2[j] = 0.f;
+      sh[j] = shl[ch * 8 + j];
+    }
+    // unconditional reads of clamped rows (a per-row guard was a branch + wait per row)
+    const int plast = (int)min((long long)BP, g.M - p0) - 1;
+    f32x4 raw[BP / RPI];
+#pragma unroll
+    for (int it = 0; it < BP / RPI; ++it)
+      raw[it] = *reinterpret_cast<const f32x4*>(tile + min(it * RPI + tid / CPR, plast) * RS + ch * 8);
+#pragma unroll
+    for (int it = 0; it < BP / RPI; ++it) {
+      const float m = it * RPI + tid / CPR <= plast ? 1.f : 0.f;
+      const T* e = reinterpret_cast<const T*>(&raw[it]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = (Cvt<T>::to_f(e[j]) - sh[j]) * m;
+        s1[j] += d;
+        s2[j] = fmaf(d, d, s2[j]);
+      }
+    }
+#pragma unroll
+    for (int o = CPR; o < 64; o <<= 1)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s1[j] += __shfl_xor(s1[j], o);
+        s2[j] += __shfl_xor(s2[j], o);
+      }
+    if (lane < CPR)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[wave][0][ch * 8 + j] = s1[j];
+        red[wave][1][ch * 8 + j] = s2[j];
+      }
+    __syncthreads();
+    rows = (g.M + BP - 1) / BP;
+    NG = (int)((rows + G1 - 1) / G1);
+    float* lvl1 = sa.part + (long long)bn * rows * (2 * BN);
+    if (sa.defer) {  // plain stores; the tree runs in stat_tree_kernel after this launch
+      for (int t = tid; t < 2 * BN; t += THR) {
+        const int q = t / BN, c = t % BN;
+        lvl1[bm * (2 * BN) + t] = red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c];
+      }
+    } else {
+      for (int t = tid; t < 2 * BN; t += THR) {
+        const int q = t / BN, c = t % BN;
+        st_wt(lvl1 + bm * (2 * BN) + t, red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c]);
+      }
+      grp = (int)(bm / G1);
+      gsz = (int)min((long long)G1, rows - (long long)grp * G1);
+      last1 = last_arriver(sa.tickets + bn * NG + grp, (unsigned)gsz, s_flag);
+    }
+  }
+  if (!stores_first) store_tile();
+  if (!last1) return;
+  __syncthreads();
+  float* lvl1 = sa.part + (long long)bn * rows * (2 * BN);
+  float* lvl2 = sa.part + (long long)nct * rows * (2 * BN) + (long long)bn * NG * (2 * BN);
+  sum_rows<2 * BN>(lvl1 + (long long)grp * G1 * (2 * BN), gsz, lvl2 + (long long)grp * (2 * BN), scr, true);
+  if (!last_arriver(sa.tickets + nct * NG + bn, (unsigned)NG, s_flag)) return;
+  float* tot = &red[0][0][0];
+  sum_rows<2 * BN>(lvl2, NG, tot, scr, false);
+  for (int t = tid; t < BN; t += THR) {
+    sa.stats[k0 + t] = tot[t];
+    sa.stats[g.K + k0 + t] = tot[BN + t];
+    sa.stats[2 * g.K + SHIFT_OFF + k0 + t] = sa.shift[k0 + t];
+  }
+  if (bn == 0 && tid == 0) {
+    sa.stats[2 * g.K] = (float)g.M;
+    if (sa.nbt != nullptr) sa.nbt[0] = sa.nbt[0] + 1;
+  }
+}
+
+// The statistics tree of a conv launch with StatArgs.defer: the conv's workgroups stored
+// their level-1 partial rows with plain stores and exited (no write-through drain, no
+// ticket round trip per workgroup: on a many-round grid that serial hand-off cost each
+// workgroup ~3 us, ~30 us per large conv); this launch runs the same two levels --
+// workgroup (bn, grp) sums its group of G1 rows into a level-2 row, the last of a
+// channel tile's NG arrivals sums those into the final statistics.  Same association
+// as the in-launch tree: the result is bitwise the same.
+template <int BN>
+__global__ void __launch_bounds__(THR) stat_tree_kernel(StatArgs sa, long long M, int BM_, int K) {
+  __shared__ float scr[THR];
+  __shared__ float tot[2 * BN];
+  __shared__ int s_flag;
+  const int nct = K / BN;
+  const long long rows = (M + BM_ - 1) / BM_;
+  const int NG = (int)((rows + G1 - 1) / G1);
+  const int bn = (int)(blockIdx.x / NG), grp = (int)(blockIdx.x % NG);
+  const int gsz = (int)min((long long)G1, rows - (long long)grp * G1);
+  const int k0 = bn * BN, tid = threadIdx.x;
+  float* lvl1 = sa.part + (long long)bn * rows * (2 * BN);
+  float* lvl2 = sa.part + (long long)nct * rows * (2 * BN) + (long long)bn * NG * (2 * BN);
+  sum_rows<2 * BN>(lvl1 + (long long)grp * G1 * (2 * BN), gsz, lvl2 + (long long)grp * (2 * BN), scr, true);
+  if (!last_arriver(sa.tickets + nct * NG + bn, (unsigned)NG, &s_flag)) return;
+  sum_rows<2 * BN>(lvl2, NG, tot, scr, false);
+  for (int t = tid; t < BN; t += THR) {
+    sa.stats[k0 + t] = tot[t];
+    sa.stats[K + k0 + t] = tot[BN + t];
+    sa.stats[2 * K + SHIFT_OFF + k0 + t] = sa.shift[k0 + t];
+  }
+  if (bn == 0 && tid == 0) {
+    sa.stats[2 * K] = (float)M;
     if (sa.nbt != nullptr) sa.nbt[0] = sa.nbt[0] + 1;
   }
 }
@@ -727,6 +1052,72 @@ bool supported(int64_t C, int64_t K) { return C % BK == 0 && K % 64 == 0; }
 
 static int tile_n(int64_t K) { return K % 128 == 0 ? 128 : 64; }
 
+// 1x1 convs on conv1x1_kernel (DPA_G1X1=0: the general kernel, A/B runs; g1x1_config
+// switches both at run time for tests and sweeps)
+static int g_g1x1_on = -1, g_g1x1_bp = -1;
+static long long g_g1x1_min256 = -1;
+
+static void g1x1_init() {
+  if (g_g1x1_on >= 0) return;
+  const char* e = std::getenv("DPA_G1X1");
+  g_g1x1_on = (e == nullptr || e[0] != '0') ? 1 : 0;
+  const char* b = std::getenv("DPA_G1X1_BP");
+  g_g1x1_bp = b != nullptr ? std::atoi(b) : 0;
+  const char* m = std::getenv("DPA_G1X1_MIN256");
+  g_g1x1_min256 = m != nullptr ? std::atoll(m) : (1LL << 40);  // 256-pixel tiles measured slower: off
+}
+
+static bool g1x1_enabled() {
+  g1x1_init();
+  return g_g1x1_on != 0;
+}
+
+// pixel tile of conv1x1_kernel: 256 when the grid still has >= min256 workgroups (default
+// 2 per CU: the 96 KB of LDS leave one 256-pixel workgroup per CU), else 128 (64 KB: two
+// per CU); DPA_G1X1_BP=128|256 forces one.
+static int g1x1_bp(long long M, int64_t K) {
+  g1x1_init();
+  if (g_g1x1_bp == 128 || g_g1x1_bp == 256) return g_g1x1_bp;
+  const long long t256 = (M + 255) / 256 * (K / tile_n(K));
+  return t256 >= g_g1x1_min256 ? 256 : 128;
+}
+
+// deferred statistics tree (StatArgs.defer + stat_tree_kernel) for grids of more than
+// g_defer_min workgroups (several rounds per CU: the in-launch hand-off is then paid
+// serially by every round); DPA_STAT_DEFER_MIN overrides, 0 = always, -1 = never
+static long long g_defer_min = -2;
+static bool defer_stats(long long blocks) {
+  if (g_defer_min == -2) {
+    const char* e = std::getenv("DPA_STAT_DEFER_MIN");
+    g_defer_min = e != nullptr ? std::atoll(e) : 1024LL;
+  }
+  return g_defer_min >= 0 && blocks > g_defer_min;
+}
+int64_t stat_defer_config(int64_t min_blocks) {
+  defer_stats(0);
+  const int64_t prev = g_defer_min;
+  if (min_blocks >= -1) g_defer_min = min_blocks;
+  return prev;
+}
+
+static void launch_stat_tree(const StatArgs& sa, long long M, int bm, int K, int BN) {
+  const long long rows = (M + bm - 1) / bm, NG = (rows + G1 - 1) / G1;
+  const dim3 gr((unsigned)(NG * (K / BN))), th(THR);
+  if (BN == 128) hipLaunchKernelGGL(stat_tree_kernel<128>, gr, th, 0, cur_stream(), sa, M, bm, K);
+  else hipLaunchKernelGGL(stat_tree_kernel<64>, gr, th, 0, cur_stream(), sa, M, bm, K);
+  DPA_CHECK_LAUNCH();
+}
+
+// (on, bp, min256) -> previous; a negative argument leaves that setting alone
+std::vector<int64_t> g1x1_config(int64_t on, int64_t bp, int64_t min256) {
+  g1x1_init();
+  std::vector<int64_t> prev{g_g1x1_on, g_g1x1_bp, g_g1x1_min256};
+  if (on >= 0) g_g1x1_on = on ? 1 : 0;
+  if (bp >= 0) g_g1x1_bp = (int)bp;
+  if (min256 >= 0) g_g1x1_min256 = min256;
+  return prev;
+}
+
 // statistics workspace: level-1 + level-2 partial rows (floats) and tickets (int32)
 int64_t stat_part_len(int64_t M, int64_t K) {
   const int64_t rows = (M + BM - 1) / BM, ng = (rows + G1 - 1) / G1;
@@ -791,7 +1182,7 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
   TORCH_CHECK(!(st && accumulate), "conv_fwd: statistics of an accumulated output are not supported");
   TORCH_CHECK(st == part.has_value() && st == tickets.has_value() && st == shift.has_value(),
               "conv_fwd: part, tickets, stats and shift go together");
-  StatArgs sa{nullptr, nullptr, nullptr, nullptr, nullptr};
+  StatArgs sa{nullptr, nullptr, nullptr, nullptr, nullptr, 0};
   if (st) {
     TORCH_CHECK(part->scalar_type() == at::kFloat && part->numel() >= stat_part_len(g.M, g.K), "conv_fwd: part size");
     TORCH_CHECK(tickets->scalar_type() == at::kInt && tickets->numel() >= stat_tickets_len(g.M, g.K),
@@ -805,9 +1196,33 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
     sa.nbt = nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr;
   }
   const int BN = tile_n(g.K);
+  if (mode == MODE_GEN && g.R == 1 && g.S == 1 && g.pad == 0 && g1x1_enabled() && x.numel() < (1LL << 31) &&
+      w.numel() < (1LL << 31)) {
+    // 1x1: the glds-staged GEMM kernel (pixel tile 256 or 128, see g1x1_bp)
+    const int BP = g1x1_bp(g.M, g.K);
+    const long long blocks = (g.M + BP - 1) / BP * (g.K / BN);
+    TORCH_CHECK(blocks < (1LL << 31), "conv_fwd: grid too large");
+    sa.defer = st && defer_stats(blocks) ? 1 : 0;
+    auto launch = [&](auto tag) {
+      using T = decltype(tag);
+      const T* xp = reinterpret_cast<const T*>(x.data_ptr());
+      const T* wp = reinterpret_cast<const T*>(w.data_ptr());
+      T* yp = reinterpret_cast<T*>(y.data_ptr());
+      const dim3 gr((unsigned)blocks), th(THR);
+      if (BP == 256 && BN == 128) hipLaunchKernelGGL((conv1x1_kernel<T, 256, 128>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+      else if (BP == 256) hipLaunchKernelGGL((conv1x1_kernel<T, 256, 64>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+      else if (BN == 128) hipLaunchKernelGGL((conv1x1_kernel<T, 128, 128>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+      else hipLaunchKernelGGL((conv1x1_kernel<T, 128, 64>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+    };
+    if (x.scalar_type() == at::kBFloat16) launch(__hip_bfloat16{}); else launch(__half{});
+    DPA_CHECK_LAUNCH();
+    if (sa.defer) launch_stat_tree(sa, g.M, BP, (int)g.K, BN);
+    return;
+  }
   const long long rows = (g.M + BM - 1) / BM;
   const long long blocks = rows * (g.K / BN) * (mode == MODE_S2T ? 4 : 1);
   TORCH_CHECK(blocks < (1LL << 31), "conv_fwd: grid too large");
+  sa.defer = st && defer_stats(blocks) ? 1 : 0;
   auto launch = [&](auto tag) {
     using T = decltype(tag);
     const T* xp = reinterpret_cast<const T*>(x.data_ptr());
@@ -827,6 +1242,7 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
   };
   if (x.scalar_type() == at::kBFloat16) launch(__hip_bfloat16{}); else launch(__half{});
   DPA_CHECK_LAUNCH();
+  if (sa.defer) launch_stat_tree(sa, g.M, BM, (int)g.K, BN);
 }
 
 // wgrad tile shapes: BM | Cout, BN | C (a column tile stays inside one filter tap)
@@ -922,6 +1338,9 @@ void register_conv_igemm(pybind11::module& m) {
   s.attr("MODE_S2T") = igemm::MODE_S2T;
   s.def("pack_weights", &igemm::pack_weights);
   s.def("wgrad_splits", &igemm::wgrad_splits);
+  s.def("stat_defer_config", &igemm::stat_defer_config, pybind11::arg("min_blocks") = -2);
+  s.def("g1x1_config", &igemm::g1x1_config, pybind11::arg("on") = -1, pybind11::arg("bp") = -1,
+        pybind11::arg("min256") = -1);
 }
 
 }  // namespace dpa

@@ -106,61 +106,87 @@ linear_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w, const fl
   }
 }
 
-// dx[M][K] = dout[M][N] . w[N][K];  dw[N][K] = dout^T . x;  db[N] = sum_m dout
-// Block j owns columns [64j, 64j+64) of K, wave wv 16 of them.
+// 8 elements base[(k0+j)*ld + col] / base[row*K + k0+j] as MFMA operands: clamped
+// UNCONDITIONAL loads, the out-of-range values masked afterwards (a guarded load is
+// branched around and waited for one by one, cdna_hip_programming.md §5 trap (c))
+template <typename T, typename S>
+__device__ __forceinline__ typename MM<T>::frag col8c(const S* base, int col, int cols, int k0, int K, int ld) {
+  typename MM<T>::frag f;
+  const int cc = col < cols ? col : cols - 1;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = Cvt<S>::to_f(base[(size_t)min(k0 + j, K - 1) * ld + cc]);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = MM<T>::cv(col < cols && k0 + j < K ? v[j] : 0.f);
+  return f;
+}
+template <typename T, typename S>
+__device__ __forceinline__ typename MM<T>::frag row8c(const S* base, int row, int rows, int k0, int K) {
+  typename MM<T>::frag f;
+  const S* p = base + (size_t)(row < rows ? row : rows - 1) * K;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = Cvt<S>::to_f(p[min(k0 + j, K - 1)]);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = MM<T>::cv(row < rows && k0 + j < K ? v[j] : 0.f);
+  return f;
+}
+
+// dx[M][K] = dout[M][N] . w[N][K];  dw[N][K] = dout^T . x;  db[N] = sum_m dout.
+// Grid (ceil(K/64), ydx + ceil(N/16)): wave wv of workgroup (j, y) owns the 16 columns
+// [64j + 16wv, +16) of a 16-row tile -- of dx for y < ydx (row tile y, reduction over N),
+// else of dw (row tile y - ydx, reduction over M; the column-0 workgroups also sum db).
+// (One workgroup per 64 columns looping over every tile took 626 us on ResNet-50's fc,
+// 128 x 1000 x 2048; this grid has ~2k workgroups there.)
 template <typename T>
 __global__ void __launch_bounds__(NTHR)
 linear_bwd_kernel(const T* __restrict__ dout, const T* __restrict__ x, const float* __restrict__ w,
-                  T* __restrict__ dx, float* __restrict__ dw, float* __restrict__ db, int M, int N, int K) {
+                  T* __restrict__ dx, float* __restrict__ dw, float* __restrict__ db, int M, int N, int K, int ydx) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = lane & 15, q = lane >> 4;
   const int c0 = blockIdx.x * 64 + wv * 16;
-  if (dx != nullptr) {
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int col = c0 + r;
+  if ((int)blockIdx.y < ydx) {
+    const int mt = blockIdx.y;
     const int NS = (N + 31) / 32;
-    for (int mt = 0; mt * 16 < M; ++mt) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int s = 0; s < NS; ++s) {
-        const int n0 = 32 * s + 8 * q;
-        const auto a = load_row8<T, T>(dout, mt * 16 + r, M, n0, N);
-        const auto bf = load_col8<T, float>(w, c0 + r, K, n0, N, K);
-        acc = MM<T>::mma(a, bf, acc);
-      }
-      const int col = c0 + r;
-      if (col < K) {
+    for (int s = 0; s < NS; ++s) {
+      const int n0 = 32 * s + 8 * q;
+      const auto a = row8c<T, T>(dout, mt * 16 + r, M, n0, N);
+      const auto bf = col8c<T, float>(w, col, K, n0, N, K);
+      acc = MM<T>::mma(a, bf, acc);
+    }
+    if (col < K) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = mt * 16 + 4 * q + i;
-          if (row < M) dx[(size_t)row * K + col] = Cvt<T>::from_f(acc[i]);
-        }
+      for (int i = 0; i < 4; ++i) {
+        const int row = mt * 16 + 4 * q + i;
+        if (row < M) dx[(size_t)row * K + col] = Cvt<T>::from_f(acc[i]);
       }
+    }
+    return;
+  }
+  const int nt = blockIdx.y - ydx;
+  const int MS = (M + 31) / 32;
+  for (int s = 0; s < MS; ++s) {
+    const int m0 = 32 * s + 8 * q;
+    const auto a = col8c<T, T>(dout, nt * 16 + r, N, m0, M, N);  // dout^T row n
+    const auto bf = col8c<T, T>(x, col, K, m0, M, K);
+    acc = MM<T>::mma(a, bf, acc);
+  }
+  if (col < K) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = nt * 16 + 4 * q + i;
+      if (row < N) dw[(size_t)row * K + col] = acc[i];
     }
   }
-  {
-    const int MS = (M + 31) / 32;
-    for (int nt = 0; nt * 16 < N; ++nt) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int s = 0; s < MS; ++s) {
-        const int m0 = 32 * s + 8 * q;
-        const auto a = load_col8<T, T>(dout, nt * 16 + r, N, m0, M, N);  // dout^T row n
-        const auto bf = load_col8<T, T>(x, c0 + r, K, m0, M, K);
-        acc = MM<T>::mma(a, bf, acc);
-      }
-      const int col = c0 + r;
-      if (col < K) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = nt * 16 + 4 * q + i;
-          if (row < N) dw[(size_t)row * K + col] = acc[i];
-        }
-      }
-    }
-  }
-  if (db != nullptr && blockIdx.x == 0) {
-    for (int n = threadIdx.x; n < N; n += NTHR) {
-      float a = 0.f;
-      for (int m = 0; m < M; ++m) a += Cvt<T>::to_f(dout[(size_t)m * N + n]);
-      db[n] = a;
-    }
+  if (db != nullptr && blockIdx.x == 0 && wv == 0) {  // db for this tile's 16 rows of w
+    const int n = nt * 16 + r, nc = n < N ? n : N - 1;
+    float t = 0.f;
+    for (int m = q; m < M; m += 4) t += Cvt<T>::to_f(dout[(size_t)m * N + nc]);
+    t += __shfl_xor(t, 16);
+    t += __shfl_xor(t, 32);
+    if (q == 0 && n < N) db[n] = t;
   }
 }
 
@@ -410,11 +436,12 @@ void linear_bwd(at::Tensor dout, at::Tensor x, at::Tensor w, c10::optional<at::T
   TORCH_CHECK(dout.scalar_type() == x.scalar_type());
   const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
   if (M == 0) { dw.zero_(); if (db) db->zero_(); return; }
-  const dim3 grid((K + 63) / 64);
+  const int ydx = dx.has_value() ? (M + 15) / 16 : 0;
+  const dim3 grid((K + 63) / 64, ydx + (N + 15) / 16);
   DPA_DISPATCH_T(dt_of(x), {
     hipLaunchKernelGGL(linear_bwd_kernel<T>, grid, dim3(NTHR), 0, cur_stream(), dptr<T>(dout), dptr<T>(x),
                        w.data_ptr<float>(), dx.has_value() ? dptr<T>(*dx) : nullptr, dw.data_ptr<float>(),
-                       db.has_value() ? db->data_ptr<float>() : nullptr, M, N, K);
+                       db.has_value() ? db->data_ptr<float>() : nullptr, M, N, K, ydx);
   });
   DPA_CHECK_LAUNCH();
 }

@@ -16,18 +16,20 @@ Execution on a HIP device (``fused=True``): activations are bf16/f16/f32
     8 x 8 x 4 (forward + statistics, and the weight gradient);
   * backward: every weight gradient and every 3x3 data gradient (stride 1, and
     stride 2 as four output-parity sub-convolutions) run on the implicit-GEMM
-    kernel, as do the 1x1 data gradients of <= 512 channels; wider 1x1 data
-    gradients are plain GEMMs on the NHWC rows (hipBLASLt, ops/conv1x1.py).  A
+    kernel; 1x1 forwards and data gradients run on the glds-staged 1x1 GEMM kernel
+    (conv1x1_kernel: 128-pixel tiles, operands global -> LDS by LDS-DMA).  A
     projection block's two input gradients (conv1 and downsample) are combined in
     the conv epilogue instead of by a separate add;
   * every BatchNorm runs on the native NHWC kernels with its ReLU and, for the
     last BN of a bottleneck, the residual add fused in (ops/bn_nhwc.py), as
     SyncBatchNorm when the module was converted (one small all-reduce each way);
-  * max-pool 3x3/2 and the global average pool are native kernels; fc is a
-    hipBLASLt GEMM.
+  * max-pool 3x3/2 and the global average pool are native kernels; fc runs on the
+    native MFMA linear kernels (ops/head.py).
 On CPU the plain torch modules run (the same math; the CPU test tier).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.nn as nn
@@ -177,11 +179,11 @@ class ResNet(nn.Module):
         _PACKS.clear()
         if _igemm.ENABLED and cdtype in (torch.bfloat16, torch.float16):
             # every implicit-GEMM conv's filters for this step in one launch (with the flipped
-            # transpose where the data gradient runs on the kernel: every 3x3, and 1x1 convs
-            # of <= 512 output channels, ops/conv_igemm.dgrad_1x1_here)
+            # transpose where the data gradient runs on the kernels: every 3x3, and the 1x1
+            # convs ops/conv_igemm.dgrad_1x1_here selects -- all of them by default)
             pack = getattr(self, "_wpack", None)
             if pack is None or pack.cdtype != cdtype:
-                convs = [(m, m.kernel_size == (3, 3) or m.weight.shape[0] <= 512)
+                convs = [(m, m.kernel_size == (3, 3) or _igemm.dgrad_1x1_here(m.weight.shape[0], 14))
                          for m in self.modules() if isinstance(m, nn.Conv2d) and m.bias is None and m.groups == 1
                          and m.weight.shape[0] % 64 == 0 and m.weight.shape[1] % 64 == 0]
                 pack = self._wpack = _igemm.WeightPack(convs, cdtype)
@@ -198,6 +200,12 @@ class ResNet(nn.Module):
             for blk in layer:
                 x = blk.forward_native(x, cdtype)
         feat = global_avg_pool(x)
+        if cdtype in (torch.bfloat16, torch.float16) and os.environ.get("DPA_NATIVE_FC", "1") != "0":
+            # fc on the native MFMA linear kernels (ops/head.py: fp32 master weight read
+            # in-kernel, fp32 weight / bias gradients) -- no hipBLASLt GEMM left in the step
+            from ..ops.head import linear
+
+            return linear(feat, self.fc.weight, self.fc.bias, cdtype)
         return F.linear(feat, self.fc.weight.to(cdtype), self.fc.bias.to(cdtype))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:

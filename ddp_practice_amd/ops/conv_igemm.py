@@ -47,11 +47,15 @@ def usable(x: torch.Tensor, weight: torch.Tensor, cdtype: torch.dtype) -> bool:
             and bool(_K().supported(weight.shape[1], weight.shape[0])))
 
 
+G1X1 = os.environ.get("DPA_G1X1", "1") != "0"  # 1x1 convs on conv1x1_kernel (0: general kernel, A/B)
+
+
 def dgrad_1x1_here(K: int, OH: int) -> bool:
-    """Shapes where the implicit-GEMM kernel beats hipBLASLt on a 1x1 data gradient
-    (profiles/r2_conv_igemm_fwd_vs_library_bs128.txt, read as dgrad = conv K -> C):
-    up to 512 gradient channels at 14x14 and above."""
-    return ENABLED and K <= 512 and OH >= 14
+    """1x1 data gradients that run on the hand-written kernels: every one on the glds 1x1
+    GEMM kernel (network total 1150 us vs hipBLASLt 1485 us at bs 128,
+    profiles/r3_g1x1_bench.txt); with DPA_G1X1=0 only the shapes where the general
+    implicit-GEMM kernel beats hipBLASLt (<= 512 gradient channels at 14x14 and above)."""
+    return ENABLED and (G1X1 or (K <= 512 and OH >= 14))
 
 
 def conv_acc(x: torch.Tensor, w: torch.Tensor, y: torch.Tensor) -> torch.Tensor:

@@ -216,3 +216,58 @@ def test_projection_block_shared_input_grad(C, stride, order):
     assert tap.grad is None
     err = ((x.grad.float().cpu() - xr.grad).abs().max() / xr.grad.abs().max()).item()
     assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("bp", [128, 256])
+@pytest.mark.parametrize("shape", [
+    (3, 64, 7, 7, 256, 1),      # ragged M = 147 (one partial tile), BN = 128
+    (2, 256, 14, 14, 128, 2),   # stride 2
+    (2, 128, 9, 9, 64, 1),      # BN = 64 tiles, ragged M
+    (8, 64, 56, 56, 64, 1),     # many pixel tiles: two-level statistics tree
+])
+def test_conv1x1_glds_kernel_tiles(C, bp, shape):
+    """conv1x1_kernel (glds-staged 1x1 GEMM) with each pixel tile forced == fp32 torch:
+    output, fused BN statistics (tickets re-armed), accumulate and the even-pixel aux add."""
+    K_ = C.conv_igemm
+    prev = K_.g1x1_config(1, bp)
+    try:
+        N, Cin, H, W, K, stride = shape
+        _run(C, N, Cin, H, W, K, 1, stride, 0, torch.bfloat16, True)
+        _run(C, N, Cin, H, W, K, 1, stride, 0, torch.float16, False)
+        g = torch.Generator().manual_seed(bp + K)
+        x = torch.randn(N, Cin, H, W, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=CL)
+        w = (torch.randn(K, Cin, 1, 1, generator=g) / Cin ** 0.5).to(DEV, torch.bfloat16).contiguous(memory_format=CL)
+        ref = F.conv2d(x.float(), w.float(), None, stride)
+        y0 = torch.randn(ref.shape, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=CL)
+        y = y0.clone()
+        K_.conv_fwd(x, w, y, stride, 0, accumulate=True)
+        err = ((y.float() - (ref + y0.float())).abs().max() / ref.abs().max()).item()
+        assert err < 2e-2, err
+        OH, OW = ref.shape[2], ref.shape[3]
+        if OH % 2 == 0 and OW % 2 == 0:
+            aux = torch.randn(N, K, OH // 2, OW // 2, generator=g).to(DEV, torch.bfloat16).contiguous(
+                memory_format=CL)
+            K_.conv_fwd(x, w, y, stride, 0, aux=aux)
+            exp = ref.clone()
+            exp[:, :, ::2, ::2] += aux.float()
+            err = ((y.float() - exp).abs().max() / exp.abs().max()).item()
+            assert err < 2e-2, err
+    finally:
+        K_.g1x1_config(*prev)
+
+
+@pytest.mark.parametrize("shape", [
+    (2, 64, 14, 14, 64, 3, 1, 1),     # general kernel, 3x3
+    (3, 64, 7, 7, 256, 1, 1, 0),      # 1x1 kernel, ragged M
+    (8, 64, 56, 56, 64, 1, 1, 0),     # 1x1, two-level tree
+    (2, 128, 15, 15, 128, 3, 2, 1),   # general kernel, stride 2
+])
+def test_conv_fwd_deferred_statistics(C, shape):
+    """StatArgs.defer: the conv stores its level-1 partial rows and stat_tree_kernel runs
+    the tree after the launch -- same statistics, tickets re-armed."""
+    K_ = C.conv_igemm
+    prev = K_.stat_defer_config(0)  # defer every statistics launch
+    try:
+        _run(C, *shape, torch.bfloat16, True)
+    finally:
+        K_.stat_defer_config(prev)

@@ -97,7 +97,7 @@ def test_conv_block_eval(C, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("M,N,K", [(32, 10, 1568), (7, 10, 1568), (40, 33, 100)])
+@pytest.mark.parametrize("M,N,K", [(32, 10, 1568), (7, 10, 1568), (40, 33, 100), (128, 1000, 2048)])
 def test_linear(C, dtype, M, N, K):
     from ddp_practice_amd.ops.head import linear
 
