@@ -76,6 +76,27 @@ struct StatArgs {
   const float* shift; // running mean (the sums are taken around it)
   int64_t* nbt;       // num_batches_tracked (bumped once) or null
   int defer;          // 1: level-1 rows only (plain stores, no ticket), stat_tree_kernel follows
+  // backward statistics of the BatchNorm whose output gradient this conv produces
+  // (conv1x1_kernel BS > 0): stats = out [S1 | S2], plus dbeta = S1, dgamma = S2
+  float* dgamma = nullptr;
+  float* dbeta = nullptr;
+  int bwd = 0;
+};
+
+// BS (conv1x1_kernel): the output is the gradient dy of a BatchNorm's output; the epilogue
+// also takes that BN's backward sums S1 = sum dz, S2 = sum dz * xhat (dz = dy * relu'),
+// as the separate bn_nhwc bwd_stats pass would (csrc/kernels/bn_nhwc.hip):
+//   BS_Y:   ReLU mask from the BN's output y (a residual was added); the gradient is
+//           accumulated onto the tapped residual gradient (Geom.accumulate)
+//   BS_REC: ReLU mask recomputed from x (fma(x, gamma*invstd, beta - mean*gamma*invstd) > 0)
+constexpr int BS_NONE = 0, BS_Y = 1, BS_REC = 2;
+template <typename T>
+struct BwdStatArgs {
+  const T* x = nullptr;         // the BN's input (this conv's gradient layout [M][K])
+  const T* y = nullptr;         // BS_Y: the BN's output
+  const float* save = nullptr;  // mean[K], invstd[K] of the forward
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
 };
 
 // Hand-off without fences (MI355X_MICROARCH.md "valid forms"): partial rows are
@@ -307,6 +328,49 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
   constexpr int RPI = THR / CPR;     // pixel rows per pass
   const bool stats = sa.part != nullptr;
   const int ch = tid % CPR;
+  // output stores: whole 16-B chunks, consecutive lanes along a pixel's channels
+  const T* aux = reinterpret_cast<const T*>(g.aux);
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int it = 0; it < BM / RPI; ++it) {
+      const int pl = it * RPI + tid / CPR;
+      const long long p = p0 + pl;
+      if (p < g.M) {
+        long long op = p;  // output pixel
+        int oh = 0, ow = 0, n = 0;
+        if (MODE == MODE_S2T || aux != nullptr) {
+          ow = (int)(p % g.OW);
+          const long long t = p / g.OW;
+          oh = (int)(t % g.OH);
+          n = (int)(t / g.OH);
+        }
+        if constexpr (MODE == MODE_S2T) op = ((long long)n * (2 * g.OH) + 2 * oh + py) * (2 * g.OW) + 2 * ow + px;
+        f32x4* dst = reinterpret_cast<f32x4*>(y + op * g.K + k0 + ch * 8);
+        f32x4 raw = *reinterpret_cast<const f32x4*>(tile + pl * RS + ch * 8);
+        const bool add_aux = aux != nullptr && !(oh & 1) && !(ow & 1);
+        if (g.accumulate || add_aux) {  // y (+)= tile (+ aux), summed in fp32, rounded once
+          f32x4 old = {0.f, 0.f, 0.f, 0.f}, ax = {0.f, 0.f, 0.f, 0.f};
+          if (g.accumulate) old = *dst;
+          if (add_aux)
+            ax = *reinterpret_cast<const f32x4*>(
+                aux + (((long long)n * (g.OH >> 1) + (oh >> 1)) * (g.OW >> 1) + (ow >> 1)) * g.K + k0 + ch * 8);
+          const T* a = reinterpret_cast<const T*>(&old);
+          const T* e = reinterpret_cast<const T*>(&ax);
+          T* b = reinterpret_cast<T*>(&raw);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            b[j] = Cvt<T>::from_f(Cvt<T>::to_f(a[j]) + Cvt<T>::to_f(e[j]) + Cvt<T>::to_f(b[j]));
+        }
+        *dst = raw;
+      }
+    }
+  };
+  // Without statistics, or with the tree deferred to stat_tree_kernel, the stores leave
+  // first and drain while the sums are taken from the tile still in LDS (the barrier
+  // after the sums is LDS-only: __syncthreads() would wait for the stores); with the
+  // in-launch tree they follow the ticket, whose vmcnt(0) must not wait for the tile.
+  const bool stores_first = !stats || sa.defer;
+  if (stores_first) store_tile();
   bool last1 = false;
   long long rows = 0;
   int NG = 0, grp = 0, gsz = 0;
@@ -317,18 +381,21 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
       s1[j] = s2[j] = 0.f;
       sh[j] = shp[j];
     }
+    // unconditional reads of clamped rows (a per-row guard was a branch + wait per row)
+    const int plast = (int)min((long long)BM, g.M - p0) - 1;
+    f32x4 raw[BM / RPI];
+#pragma unroll
+    for (int it = 0; it < BM / RPI; ++it)
+      raw[it] = *reinterpret_cast<const f32x4*>(tile + min(it * RPI + tid / CPR, plast) * RS + ch * 8);
 #pragma unroll
     for (int it = 0; it < BM / RPI; ++it) {
-      const int pl = it * RPI + tid / CPR;
-      if (p0 + pl < g.M) {
-        const f32x4 raw = *reinterpret_cast<const f32x4*>(tile + pl * RS + ch * 8);
-        const T* e = reinterpret_cast<const T*>(&raw);
+      const float m = it * RPI + tid / CPR <= plast ? 1.f : 0.f;
+      const T* e = reinterpret_cast<const T*>(&raw[it]);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float d = Cvt<T>::to_f(e[j]) - sh[j];
-          s1[j] += d;
-          s2[j] = fmaf(d, d, s2[j]);
-        }
+      for (int j = 0; j < 8; ++j) {
+        const float d = (Cvt<T>::to_f(e[j]) - sh[j]) * m;
+        s1[j] += d;
+        s2[j] = fmaf(d, d, s2[j]);
       }
     }
     // lanes of one wave sharing the chunk: xor over the row bits of the lane index
@@ -345,7 +412,8 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
         red[wave][0][ch * 8 + j] = s1[j];
         red[wave][1][ch * 8 + j] = s2[j];
       }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
     rows = (g.M + BM - 1) / BM;
     NG = (int)((rows + G1 - 1) / G1);
     float* lvl1 = sa.part + (long long)bn * rows * (2 * BN);
@@ -364,41 +432,7 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
       last1 = last_arriver(sa.tickets + bn * NG + grp, (unsigned)gsz, &s_flag);
     }
   }
-  // output stores: whole 16-B chunks, consecutive lanes along a pixel's channels
-  const T* aux = reinterpret_cast<const T*>(g.aux);
-#pragma unroll
-  for (int it = 0; it < BM / RPI; ++it) {
-    const int pl = it * RPI + tid / CPR;
-    const long long p = p0 + pl;
-    if (p < g.M) {
-      long long op = p;  // output pixel
-      int oh = 0, ow = 0, n = 0;
-      if (MODE == MODE_S2T || aux != nullptr) {
-        ow = (int)(p % g.OW);
-        const long long t = p / g.OW;
-        oh = (int)(t % g.OH);
-        n = (int)(t / g.OH);
-      }
-      if constexpr (MODE == MODE_S2T) op = ((long long)n * (2 * g.OH) + 2 * oh + py) * (2 * g.OW) + 2 * ow + px;
-      f32x4* dst = reinterpret_cast<f32x4*>(y + op * g.K + k0 + ch * 8);
-      f32x4 raw = *reinterpret_cast<const f32x4*>(tile + pl * RS + ch * 8);
-      const bool add_aux = aux != nullptr && !(oh & 1) && !(ow & 1);
-      if (g.accumulate || add_aux) {  // y (+)= tile (+ aux), summed in fp32, rounded once
-        f32x4 old = {0.f, 0.f, 0.f, 0.f}, ax = {0.f, 0.f, 0.f, 0.f};
-        if (g.accumulate) old = *dst;
-        if (add_aux)
-          ax = *reinterpret_cast<const f32x4*>(
-              aux + (((long long)n * (g.OH >> 1) + (oh >> 1)) * (g.OW >> 1) + (ow >> 1)) * g.K + k0 + ch * 8);
-        const T* a = reinterpret_cast<const T*>(&old);
-        const T* e = reinterpret_cast<const T*>(&ax);
-        T* b = reinterpret_cast<T*>(&raw);
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          b[j] = Cvt<T>::from_f(Cvt<T>::to_f(a[j]) + Cvt<T>::to_f(e[j]) + Cvt<T>::to_f(b[j]));
-      }
-      *dst = raw;
-    }
-  }
+  if (!stores_first) store_tile();
   if (!last1) return;
   __syncthreads();  // every lane is done with the tile: its LDS becomes the tree's scratch
   float* scr = reinterpret_cast<float*>(lds[1]);
@@ -451,7 +485,8 @@ struct G1x1Lds {
   static constexpr int EPI = SCR + THR * 4;
   static constexpr int MAIN = 2 * STAGE * (int)sizeof(T);
   static constexpr int SHIFT = MAIN > EPI ? MAIN : EPI;  // float shift[BN] (statistics only)
-  static constexpr int BYTES = SHIFT + BN * 4;
+  static constexpr int BWC = SHIFT + BN * 4;              // float mean|invstd|gamma|beta [4][BN] (BS)
+  static constexpr int BYTES = BWC + 4 * BN * 4;
 };
 
 // one global_load_lds_dwordx4: 16 B per lane from `src` (per lane) to dst + 16 * lane (dst
@@ -463,9 +498,10 @@ __device__ __forceinline__ void glds16(const void* src, void* dst) {
   __builtin_amdgcn_global_load_lds(src, (lds_vptr)dst, 16, 0, 0);
 }
 
-template <typename T, int BP, int BN>
+template <typename T, int BP, int BN, int BS = BS_NONE>
 __global__ void __launch_bounds__(THR)
-conv1x1_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__ y, StatArgs sa, Geom g) {
+conv1x1_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__ y, StatArgs sa, Geom g,
+               BwdStatArgs<T> bs) {
   using MMT = MM<T>;
   using L = G1x1Lds<T, BP, BN>;
   typedef typename MMT::frag frag;
@@ -525,8 +561,33 @@ conv1x1_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__
   const int fr = lane & 15, fq = lane >> 4;
   // the statistics' shift (running mean) rides with tile 0 into LDS: loaded after the K loop
   // it cost every workgroup a dependent global-load latency in its epilogue
-  if (sa.part != nullptr && wave == 0 && lane < BN / 4)
+  if (BS == BS_NONE && sa.part != nullptr && wave == 0 && lane < BN / 4)
     glds16(sa.shift + k0 + lane * 4, reinterpret_cast<float*>(smem + L::SHIFT));
+  // BS: the BN's per-channel constants ride with tile 0 too (wave w: array w), and this
+  // lane's epilogue chunks of x (and y, and the accumulated-onto gradient) are loaded into
+  // registers now -- they land with tile 0 instead of stalling the epilogue
+  constexpr int CPR = BN / 8;     // 16-B chunks per pixel row (epilogue)
+  constexpr int RPI = THR / CPR;  // pixel rows per pass
+  constexpr int NIT = BS != BS_NONE ? BP / RPI : 1;
+  const int ch = tid % CPR;
+  f32x4 bxr[NIT], byr[NIT], bor[NIT];
+  if constexpr (BS != BS_NONE) {
+    if (lane < BN / 4 && (BS == BS_REC || wave < 2)) {
+      const float* src = wave == 0 ? bs.save + k0 : wave == 1 ? bs.save + g.K + k0 : wave == 2 ? bs.gamma + k0
+                                                                                                : bs.beta + k0;
+      glds16(src + lane * 4, reinterpret_cast<float*>(smem + L::BWC) + wave * BN);
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const long long pp = min(p0 + it * RPI + tid / CPR, g.M - 1);
+      const long long o = pp * g.K + k0 + ch * 8;
+      bxr[it] = *reinterpret_cast<const f32x4*>(bs.x + o);
+      if constexpr (BS == BS_Y) {
+        byr[it] = *reinterpret_cast<const f32x4*>(bs.y + o);
+        bor[it] = *reinterpret_cast<const f32x4*>(y + o);  // the tapped residual gradient
+      }
+    }
+  }
   issue(0, 0);
   for (int kt = 0; kt < KT; ++kt) {
     const int buf = kt & 1;
@@ -571,10 +632,22 @@ conv1x1_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__
     }
   }
   __syncthreads();
-  constexpr int CPR = BN / 8;     // 16-B chunks per pixel row
-  constexpr int RPI = THR / CPR;  // pixel rows per pass
-  const bool stats = sa.part != nullptr;
-  const int ch = tid % CPR;
+  const bool stats = BS == BS_NONE && sa.part != nullptr;
+  // BS: this lane's 8 channels' BN constants, and its running sums of dz, dz * xhat
+  float bmu[8], bis[8], bsc[8], bsh[8], bs1[8], bs2[8];
+  if constexpr (BS != BS_NONE) {
+    const float* bwc = reinterpret_cast<const float*>(smem + L::BWC);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bmu[j] = bwc[ch * 8 + j];
+      bis[j] = bwc[BN + ch * 8 + j];
+      if (BS == BS_REC) {
+        bsc[j] = bwc[2 * BN + ch * 8 + j] * bis[j];
+        bsh[j] = fmaf(-bmu[j], bsc[j], bwc[3 * BN + ch * 8 + j]);
+      }
+      bs1[j] = bs2[j] = 0.f;
+    }
+  }
   // output stores: whole 16-B chunks, consecutive lanes along a pixel's channels
   const T* aux = reinterpret_cast<const T*>(g.aux);
   auto store_tile = [&]() {
@@ -595,7 +668,8 @@ conv1x1_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__
         const bool add_aux = aux != nullptr && !(oh & 1) && !(ow & 1);
         if (g.accumulate || add_aux) {
           f32x4 old = {0.f, 0.f, 0.f, 0.f}, ax = {0.f, 0.f, 0.f, 0.f};
-          if (g.accumulate) old = *dst;
+          if constexpr (BS == BS_Y) old = bor[it];  // prefetched with tile 0
+          else if (g.accumulate) old = *dst;
           if (add_aux)
             ax = *reinterpret_cast<const f32x4*>(
                 aux + (((long long)n * (g.OH >> 1) + (oh >> 1)) * (g.OW >> 1) + (ow >> 1)) * g.K + k0 + ch * 8);
@@ -607,6 +681,19 @@ conv1x1_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__
             b[j] = Cvt<T>::from_f(Cvt<T>::to_f(a[j]) + Cvt<T>::to_f(e[j]) + Cvt<T>::to_f(b[j]));
         }
         *dst = raw;
+        if constexpr (BS != BS_NONE) {  // the BN backward sums of the stored (rounded) gradient
+          const T* d = reinterpret_cast<const T*>(&raw);
+          const T* xv = reinterpret_cast<const T*>(&bxr[it]);
+          const T* yv = reinterpret_cast<const T*>(&byr[it]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float xf = Cvt<T>::to_f(xv[j]);
+            const bool on = BS == BS_Y ? Cvt<T>::to_f(yv[j]) > 0.f : fmaf(xf, bsc[j], bsh[j]) > 0.f;
+            const float z = on ? Cvt<T>::to_f(d[j]) : 0.f;
+            bs1[j] += z;
+            bs2[j] = fmaf(z, (xf - bmu[j]) * bis[j], bs2[j]);
+          }
+        }
       }
     }
   };
@@ -615,6 +702,30 @@ conv1x1_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__
   // in-launch tree they follow the ticket (its vmcnt(0) must not wait for the tile).
   const bool stores_first = !stats || sa.defer;
   if (stores_first) store_tile();
+  if constexpr (BS != BS_NONE) {  // -> level-1 row of this pixel tile (stat_tree_kernel follows)
+#pragma unroll
+    for (int o = CPR; o < 64; o <<= 1)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bs1[j] += __shfl_xor(bs1[j], o);
+        bs2[j] += __shfl_xor(bs2[j], o);
+      }
+    if (lane < CPR)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[wave][0][ch * 8 + j] = bs1[j];
+        red[wave][1][ch * 8 + j] = bs2[j];
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const long long nrows = (g.M + BP - 1) / BP;
+    float* lvl1 = sa.part + (long long)bn * nrows * (2 * BN);
+    for (int t = tid; t < 2 * BN; t += THR) {
+      const int q = t / BN, c = t % BN;
+      lvl1[bm * (2 * BN) + t] = red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c];
+    }
+    return;
+  }
   bool last1 = false;
   long long rows = 0;
   int NG = 0, grp = 0, gsz = 0;
@@ -655,7 +766,10 @@ conv1x1_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__
         red[wave][0][ch * 8 + j] = s1[j];
         red[wave][1][ch * 8 + j] = s2[j];
       }
-    __syncthreads();
+    // LDS-only barrier: __syncthreads() is a workgroup fence whose vmcnt(0) would wait
+    // here for the whole output tile's stores to drain (~30 us on a 56x56 x 256 conv)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
     rows = (g.M + BP - 1) / BP;
     NG = (int)((rows + G1 - 1) / G1);
     float* lvl1 = sa.part + (long long)bn * rows * (2 * BN);
@@ -717,6 +831,13 @@ __global__ void __launch_bounds__(THR) stat_tree_kernel(StatArgs sa, long long M
   sum_rows<2 * BN>(lvl1 + (long long)grp * G1 * (2 * BN), gsz, lvl2 + (long long)grp * (2 * BN), scr, true);
   if (!last_arriver(sa.tickets + nct * NG + bn, (unsigned)NG, &s_flag)) return;
   sum_rows<2 * BN>(lvl2, NG, tot, scr, false);
+  if (sa.bwd) {  // BN backward sums: out = [S1 | S2], dbeta = S1, dgamma = S2 (bn_nhwc layout)
+    for (int t = tid; t < BN; t += THR) {
+      sa.stats[k0 + t] = sa.dbeta[k0 + t] = tot[t];
+      sa.stats[K + k0 + t] = sa.dgamma[k0 + t] = tot[BN + t];
+    }
+    return;
+  }
   for (int t = tid; t < BN; t += THR) {
     sa.stats[k0 + t] = tot[t];
     sa.stats[K + k0 + t] = tot[BN + t];
@@ -867,6 +988,134 @@ conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __re
     __syncthreads();
   }
   // partial tile: C[m = k][n = (r,s,c)]; lane: col n = lane & 15, rows 4*(lane>>4) + j
+  float* out = slab + (long long)sp * g.K * RSC;
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = k0 + wm * (BM / 2) + a * 16 + 4 * grp + j, n = n0 + wn * (BN / 2) + b * 16 + gi;
+        out[(long long)m * RSC + n] = acc[a][b][j];
+      }
+}
+
+// The same weight gradient with both operand tiles staged global -> LDS by LDS-DMA
+// (MODE_GEN): no VGPR staging and no ds_write_b128 pass (the register-staged loop pays
+// ~13 LDS cycles per KiB written).  A wave-instruction fills 64/CH whole rows of the
+// [64 pixels][CH chunks] image, lane l row l / CH at slot l % CH; the wswz swizzle goes on
+// the per-lane source address (logical chunk = slot ^ xor(row)); padding taps and pixels
+// past the split's end read a 16-B zero page instead of being zero-filled by the loader.
+// One barrier per 64-pixel step: wait the landed step (vmcnt(0)) + barrier, issue step
+// t+1 into the other buffer, MFMA on step t (as conv1x1_kernel).
+__device__ __attribute__((aligned(16))) unsigned char g_zero16[16] = {0};
+
+template <int CH>
+__device__ __forceinline__ int wswz_xor(int row) {
+  const int f = (row & 3) | ((row >> 1) & 4);
+  return CH >= 16 ? 2 * f : 2 * (f & 3);
+}
+
+template <typename T, int BM, int BN>
+__global__ void __launch_bounds__(THR)
+conv_wgrad_glds_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ slab, Geom g,
+                       int splits, long long pps) {
+  typedef typename MM<T>::frag frag;
+  constexpr int BP = 64;
+  constexpr int CHA = BM / 8, CHB = BN / 8;
+  constexpr int IA = CHA / 4, IB = CHB / 4;  // wave-instructions per wave per step
+  constexpr int MT = BM / 32, NT = BN / 32;
+  constexpr int STAGE = BP * (BM + BN);
+  __shared__ __attribute__((aligned(16))) T lds[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int RSC = g.R * g.S * g.C;
+  const int tm = g.K / BM, tn = RSC / BN, tiles = tm * tn;
+  const unsigned nwg = gridDim.x, hw = blockIdx.x;
+  const unsigned q8 = nwg / 8, r8 = nwg % 8, xcd = hw % 8, slot = hw / 8;
+  const unsigned lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int sp = (int)(lid / tiles), tile = (int)(lid % tiles);
+  const int k0 = (tile / tn) * BM, n0 = (tile % tn) * BN;
+  const int rs = n0 / g.C, c0 = n0 - rs * g.C, fr_ = rs / g.S, fs_ = rs - fr_ * g.S;
+  const long long pa = sp * pps, pb = min(g.M, pa + pps);
+  const int steps = (int)((pb - pa + BP - 1) / BP);
+  const bool plain = g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0;  // x rows = pixels
+  // this lane's rows and source chunks (row = (i*4 + wave) * (64/CH) + lane / CH)
+  const int ra = lane / CHA, rb = lane / CHB;
+  auto issue = [&](int t, int buf) {
+    T* A = lds + buf * STAGE;
+    T* B = A + BP * BM;
+    const long long pbase = pa + (long long)t * BP;
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const int row = (i * 4 + wave) * (64 / CHA) + ra;
+      const int ck = (lane % CHA) ^ wswz_xor<CHA>(row);
+      const long long p = pbase + row;
+      const void* src = p < pb ? (const void*)(dy + p * g.K + k0 + ck * 8) : (const void*)g_zero16;
+      glds16(src, A + (i * 4 + wave) * (64 / CHA) * BM);
+    }
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int row = (i * 4 + wave) * (64 / CHB) + rb;
+      const int ck = (lane % CHB) ^ wswz_xor<CHB>(row);
+      const long long p = pbase + row;
+      const void* src = g_zero16;
+      if (p < pb) {
+        if (plain) {
+          src = x + p * g.C + c0 + ck * 8;
+        } else {
+          const unsigned pu = (unsigned)p, q = pu / (unsigned)g.OW;  // M < 2^31 (host check)
+          const int ow = (int)(pu - q * (unsigned)g.OW);
+          const unsigned n = q / (unsigned)g.OH;
+          const int oh = (int)(q - n * (unsigned)g.OH);
+          const int ih = oh * g.stride + fr_ - g.pad, iw = ow * g.stride + fs_ - g.pad;
+          if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
+            src = x + (((long long)n * g.H + ih) * g.W + iw) * g.C + c0 + ck * 8;
+        }
+      }
+      glds16(src, B + (i * 4 + wave) * (64 / CHB) * BN);
+    }
+  };
+  const int grp = lane >> 4, gi = lane & 15, q = gi >> 2, pq = gi & 3;
+  auto trfrag = [&](const T* base, int kk, int cb, auto chtag) -> frag {
+    constexpr int CH = decltype(chtag)::value;
+    const int row = 32 * kk + 8 * grp + q, col = cb + 4 * pq;
+    const T* a0 = base + wswz<CH>(row, col >> 3) + (col & 7);
+    const T* a1 = base + wswz<CH>(row + 4, col >> 3) + (col & 7);
+    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)a0);
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)a1);
+    typedef __attribute__((ext_vector_type(8))) short v8s;
+    const v8s v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(frag, v);
+  };
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (steps > 0) issue(0, 0);
+  for (int t = 0; t < steps; ++t) {
+    const int buf = t & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 < steps) issue(t + 1, buf ^ 1);
+    const T* A = lds + buf * STAGE;
+    const T* B = A + BP * BM;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      frag fa[MT], fb[NT];
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+        fa[a] = trfrag(A, kk, wm * (BM / 2) + a * 16, std::integral_constant<int, CHA>{});
+#pragma unroll
+      for (int b = 0; b < NT; ++b)
+        fb[b] = trfrag(B, kk, wn * (BN / 2) + b * 16, std::integral_constant<int, CHB>{});
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b) acc[a][b] = MM<T>::mma(fa[a], fb[b], acc[a][b]);
+    }
+  }
   float* out = slab + (long long)sp * g.K * RSC;
 #pragma unroll
   for (int a = 0; a < MT; ++a)
@@ -1137,9 +1386,20 @@ int64_t stat_tickets_len(int64_t M, int64_t K) {
 // w = its flipped transposed filter [Cin, Cf, 3, 3], y = dx [N, Cin, 2 OHf, 2 OWf].
 // aux (MODE_GEN, channels_last [N, K, OH/2, OW/2]): added at the even output pixels --
 // a stride-2 1x1 conv's data gradient folded into this one's output.
+//
+// bn_x (1x1, stride 1, on conv1x1_kernel): y is the output gradient of a training BatchNorm
+// whose input was bn_x; the epilogue also produces that BN's backward sums (bn_nhwc
+// bwd_stats: bn_out = [S1 | S2], bn_dbeta = S1, bn_dgamma = S2) -- bn_y given: the ReLU
+// mask comes from the BN's output (and y accumulates onto the tapped residual gradient,
+// accumulate = true); else it is recomputed from bn_x with bn_gamma / bn_beta.  bn_save =
+// the forward's [mean | invstd]; part / tickets = the statistics workspace.
 void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t pad, c10::optional<at::Tensor> part,
               c10::optional<at::Tensor> tickets, c10::optional<at::Tensor> stats, c10::optional<at::Tensor> shift,
-              c10::optional<at::Tensor> nbt, bool accumulate, int64_t mode, c10::optional<at::Tensor> aux) {
+              c10::optional<at::Tensor> nbt, bool accumulate, int64_t mode, c10::optional<at::Tensor> aux,
+              c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_y, c10::optional<at::Tensor> bn_save,
+              c10::optional<at::Tensor> bn_gamma, c10::optional<at::Tensor> bn_beta,
+              c10::optional<at::Tensor> bn_out, c10::optional<at::Tensor> bn_dgamma,
+              c10::optional<at::Tensor> bn_dbeta) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "conv_fwd: device tensors");
   TORCH_CHECK(x.scalar_type() == w.scalar_type() && x.scalar_type() == y.scalar_type(), "conv_fwd: one dtype");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "conv_fwd: bf16 / f16");
@@ -1179,8 +1439,35 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
     g.aux = aux->data_ptr();
   }
   const bool st = stats.has_value();
+  const bool bwdst = bn_x.has_value();
   TORCH_CHECK(!(st && accumulate), "conv_fwd: statistics of an accumulated output are not supported");
-  TORCH_CHECK(st == part.has_value() && st == tickets.has_value() && st == shift.has_value(),
+  if (bwdst) {
+    TORCH_CHECK(mode == MODE_GEN && g.R == 1 && g.S == 1 && g.pad == 0 && g.stride == 1 && g1x1_enabled() &&
+                    x.numel() < (1LL << 31) && w.numel() < (1LL << 31),
+                "conv_fwd: BN backward sums need the 1x1 / stride-1 kernel");
+    TORCH_CHECK(!st && !aux.has_value() && part.has_value() && tickets.has_value(),
+                "conv_fwd: BN backward sums take part / tickets and no forward statistics / aux");
+    TORCH_CHECK(accumulate == bn_y.has_value(), "conv_fwd: bn_y (ReLU after a residual) goes with accumulate");
+    TORCH_CHECK(bn_save.has_value() && bn_out.has_value() && bn_dgamma.has_value() && bn_dbeta.has_value() &&
+                    (bn_y.has_value() || (bn_gamma.has_value() && bn_beta.has_value())),
+                "conv_fwd: BN backward sums need save / out / dgamma / dbeta (+ gamma / beta to recompute)");
+    auto rows_like_y = [&](const at::Tensor& t) {
+      return t.scalar_type() == y.scalar_type() && t.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+             t.sizes() == y.sizes();
+    };
+    TORCH_CHECK(rows_like_y(*bn_x) && (!bn_y.has_value() || rows_like_y(*bn_y)), "conv_fwd: bn_x / bn_y like y");
+    for (const at::Tensor* t : {&*bn_save, &*bn_out})
+      TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() >= 2 * g.K, "conv_fwd: bn f32");
+    for (const at::Tensor* t : {&*bn_dgamma, &*bn_dbeta})
+      TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == g.K, "conv_fwd: bn dgamma / dbeta");
+    if (!bn_y.has_value())
+      TORCH_CHECK(bn_gamma->scalar_type() == at::kFloat && bn_gamma->numel() == g.K && bn_beta->numel() == g.K,
+                  "conv_fwd: bn gamma / beta");
+    TORCH_CHECK(part->scalar_type() == at::kFloat && part->numel() >= stat_part_len(g.M, g.K) &&
+                    tickets->scalar_type() == at::kInt && tickets->numel() >= stat_tickets_len(g.M, g.K),
+                "conv_fwd: statistics workspace");
+  }
+  TORCH_CHECK(st == shift.has_value() && (bwdst || (st == part.has_value() && st == tickets.has_value())),
               "conv_fwd: part, tickets, stats and shift go together");
   StatArgs sa{nullptr, nullptr, nullptr, nullptr, nullptr, 0};
   if (st) {
@@ -1199,26 +1486,52 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
   if (mode == MODE_GEN && g.R == 1 && g.S == 1 && g.pad == 0 && g1x1_enabled() && x.numel() < (1LL << 31) &&
       w.numel() < (1LL << 31)) {
     // 1x1: the glds-staged GEMM kernel (pixel tile 256 or 128, see g1x1_bp)
-    const int BP = g1x1_bp(g.M, g.K);
+    const int BP = bwdst ? 128 : g1x1_bp(g.M, g.K);
     const long long blocks = (g.M + BP - 1) / BP * (g.K / BN);
     TORCH_CHECK(blocks < (1LL << 31), "conv_fwd: grid too large");
     sa.defer = st && defer_stats(blocks) ? 1 : 0;
+    if (bwdst) {  // the BN backward sums: level-1 rows in the conv, the tree after it
+      sa.part = part->data_ptr<float>();
+      sa.tickets = reinterpret_cast<unsigned*>(tickets->data_ptr<int>());
+      sa.stats = bn_out->data_ptr<float>();
+      sa.dgamma = bn_dgamma->data_ptr<float>();
+      sa.dbeta = bn_dbeta->data_ptr<float>();
+      sa.bwd = 1;
+      sa.defer = 1;
+    }
     auto launch = [&](auto tag) {
       using T = decltype(tag);
       const T* xp = reinterpret_cast<const T*>(x.data_ptr());
       const T* wp = reinterpret_cast<const T*>(w.data_ptr());
       T* yp = reinterpret_cast<T*>(y.data_ptr());
       const dim3 gr((unsigned)blocks), th(THR);
-      if (BP == 256 && BN == 128) hipLaunchKernelGGL((conv1x1_kernel<T, 256, 128>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
-      else if (BP == 256) hipLaunchKernelGGL((conv1x1_kernel<T, 256, 64>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
-      else if (BN == 128) hipLaunchKernelGGL((conv1x1_kernel<T, 128, 128>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
-      else hipLaunchKernelGGL((conv1x1_kernel<T, 128, 64>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g);
+      BwdStatArgs<T> bs;
+      if (bwdst) {
+        bs.x = reinterpret_cast<const T*>(bn_x->data_ptr());
+        bs.y = bn_y.has_value() ? reinterpret_cast<const T*>(bn_y->data_ptr()) : nullptr;
+        bs.save = bn_save->data_ptr<float>();
+        bs.gamma = bn_gamma.has_value() ? bn_gamma->data_ptr<float>() : nullptr;
+        bs.beta = bn_beta.has_value() ? bn_beta->data_ptr<float>() : nullptr;
+        if (bn_y.has_value()) {
+          if (BN == 128) hipLaunchKernelGGL((conv1x1_kernel<T, 128, 128, BS_Y>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+          else hipLaunchKernelGGL((conv1x1_kernel<T, 128, 64, BS_Y>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        } else {
+          if (BN == 128) hipLaunchKernelGGL((conv1x1_kernel<T, 128, 128, BS_REC>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+          else hipLaunchKernelGGL((conv1x1_kernel<T, 128, 64, BS_REC>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        }
+        return;
+      }
+      if (BP == 256 && BN == 128) hipLaunchKernelGGL((conv1x1_kernel<T, 256, 128>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+      else if (BP == 256) hipLaunchKernelGGL((conv1x1_kernel<T, 256, 64>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+      else if (BN == 128) hipLaunchKernelGGL((conv1x1_kernel<T, 128, 128>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+      else hipLaunchKernelGGL((conv1x1_kernel<T, 128, 64>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
     };
     if (x.scalar_type() == at::kBFloat16) launch(__hip_bfloat16{}); else launch(__half{});
     DPA_CHECK_LAUNCH();
     if (sa.defer) launch_stat_tree(sa, g.M, BP, (int)g.K, BN);
     return;
   }
+  TORCH_CHECK(!bwdst, "conv_fwd: BN backward sums need the 1x1 kernel");
   const long long rows = (g.M + BM - 1) / BM;
   const long long blocks = rows * (g.K / BN) * (mode == MODE_S2T ? 4 : 1);
   TORCH_CHECK(blocks < (1LL << 31), "conv_fwd: grid too large");
@@ -1243,6 +1556,23 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
   if (x.scalar_type() == at::kBFloat16) launch(__hip_bfloat16{}); else launch(__half{});
   DPA_CHECK_LAUNCH();
   if (sa.defer) launch_stat_tree(sa, g.M, BM, (int)g.K, BN);
+}
+
+// weight gradients on conv_wgrad_glds_kernel: DPA_WGRAD_GLDS = 1 (default) the 1x1 convs,
+// 2 every MODE_GEN conv, 0 none (the register-staged kernel); wgrad_config sets it at run time
+static int g_wgrad_glds = -1;
+static int wgrad_glds() {
+  if (g_wgrad_glds < 0) {
+    const char* e = std::getenv("DPA_WGRAD_GLDS");
+    g_wgrad_glds = e == nullptr ? 1 : std::atoi(e);
+  }
+  return g_wgrad_glds;
+}
+int64_t wgrad_config(int64_t glds) {
+  wgrad_glds();
+  const int64_t prev = g_wgrad_glds;
+  if (glds >= 0) g_wgrad_glds = (int)glds;
+  return prev;
 }
 
 // wgrad tile shapes: BM | Cout, BN | C (a column tile stays inside one filter tap)
@@ -1304,6 +1634,14 @@ void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor grad, int64_t stride, in
     const T* xp = reinterpret_cast<const T*>(x.data_ptr());
     float* sl = slab.data_ptr<float>();
     const dim3 gr((unsigned)blocks), th(THR);
+    // 1x1 (mode 1, default) or every MODE_GEN conv (mode 2): on 3x3 it measured ~5 % slower
+    if (!stem && ((g.R == 1 && g.S == 1 && wgrad_glds() >= 1) || wgrad_glds() == 2)) {
+      if (BM == 128 && BN == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 128, 128>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+      else if (BM == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 128, 64>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+      else if (BN == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 64, 128>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+      else hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 64, 64>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+      return;
+    }
     if (stem && BM == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 64, MODE_STEM>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
     else if (stem) hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 64, MODE_STEM>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
     else if (BM == 128 && BN == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 128>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
@@ -1327,7 +1665,11 @@ void register_conv_igemm(pybind11::module& m) {
         pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("part") = pybind11::none(),
         pybind11::arg("tickets") = pybind11::none(), pybind11::arg("stats") = pybind11::none(),
         pybind11::arg("shift") = pybind11::none(), pybind11::arg("nbt") = pybind11::none(),
-        pybind11::arg("accumulate") = false, pybind11::arg("mode") = 0, pybind11::arg("aux") = pybind11::none());
+        pybind11::arg("accumulate") = false, pybind11::arg("mode") = 0, pybind11::arg("aux") = pybind11::none(),
+        pybind11::arg("bn_x") = pybind11::none(), pybind11::arg("bn_y") = pybind11::none(),
+        pybind11::arg("bn_save") = pybind11::none(), pybind11::arg("bn_gamma") = pybind11::none(),
+        pybind11::arg("bn_beta") = pybind11::none(), pybind11::arg("bn_out") = pybind11::none(),
+        pybind11::arg("bn_dgamma") = pybind11::none(), pybind11::arg("bn_dbeta") = pybind11::none());
   s.def("supported", &igemm::supported);
   s.def("stat_part_len", &igemm::stat_part_len);
   s.def("stat_tickets_len", &igemm::stat_tickets_len);
@@ -1338,6 +1680,7 @@ void register_conv_igemm(pybind11::module& m) {
   s.attr("MODE_S2T") = igemm::MODE_S2T;
   s.def("pack_weights", &igemm::pack_weights);
   s.def("wgrad_splits", &igemm::wgrad_splits);
+  s.def("wgrad_config", &igemm::wgrad_config, pybind11::arg("glds") = -1);
   s.def("stat_defer_config", &igemm::stat_defer_config, pybind11::arg("min_blocks") = -2);
   s.def("g1x1_config", &igemm::g1x1_config, pybind11::arg("on") = -1, pybind11::arg("bp") = -1,
         pybind11::arg("min256") = -1);

@@ -42,18 +42,20 @@ from ..ops.conv_nhwc import conv_nhwc
 
 
 _PACKS: dict = {}  # id(module) -> this forward's packed filters (ops/conv_igemm.WeightPack)
+_FUSE_BN_BWD = os.environ.get("DPA_FUSE_BN_BWD", "1") != "0"  # BNTap hand-off (0: own bwd_stats pass, A/B)
 
 
 def _conv(x: torch.Tensor, conv: nn.Conv2d, cdtype: torch.dtype, bn: nn.Module | None = None, tap=None,
-          xtap=None):
+          xtap=None, btap=None):
     """conv(x) -> (output, statistics of the following training BN ``bn`` when the conv
-    kernel produced them, else None)."""
+    kernel produced them, else None).  ``btap``: the BNTap of the BN that produced ``x``
+    (a 1x1 conv's data gradient then also takes that BN's backward sums)."""
     want = bn if (bn is not None and bn.training) else None
     pk = _PACKS.get(id(conv))
     if conv.kernel_size == (1, 1) and conv.padding == (0, 0) and conv.groups == 1 and conv.bias is None:
         if want is None:
-            return conv1x1(x, conv.weight, conv.stride[0], cdtype, tap, None, pk, xtap), None
-        return conv1x1(x, conv.weight, conv.stride[0], cdtype, tap, want, pk, xtap)
+            return conv1x1(x, conv.weight, conv.stride[0], cdtype, tap, None, pk, xtap, btap), None
+        return conv1x1(x, conv.weight, conv.stride[0], cdtype, tap, want, pk, xtap, btap)
     if conv.bias is None and conv.groups == 1 and conv.dilation == (1, 1):
         if want is None:
             return conv_nhwc(x, conv.weight, conv.stride, conv.padding, cdtype, None, pk), None
@@ -101,27 +103,36 @@ class Bottleneck(nn.Module):
         return self.relu(out + identity)
 
     def forward_native(self, x: torch.Tensor, cdtype: torch.dtype) -> torch.Tensor:
-        from ..ops.bn_nhwc import bn_act
+        from ..ops.bn_nhwc import BNTap, bn_act
 
-        grad_x = (self.bn3.training and torch.is_grad_enabled() and x.requires_grad
-                  and x.is_contiguous(memory_format=torch.channels_last))
+        train = self.bn3.training and torch.is_grad_enabled()
+        grad_x = train and x.requires_grad and x.is_contiguous(memory_format=torch.channels_last)
         # identity blocks: conv1's dgrad GEMM accumulates the residual gradient (GradTap);
         # projection blocks: conv1 and the downsample conv share x's gradient (one of them
         # folds the other's product into its own, ops/conv1x1.Conv1x1Fn)
         tap = GradTap() if (grad_x and self.downsample is None) else None
         xtap = GradTap() if (grad_x and self.downsample is not None) else None
+        # BN backward sums taken by the consuming 1x1 conv's data-gradient epilogue
+        # (ops/bn_nhwc.BNTap): bn2 -> conv3, and the previous block's bn3 -> this conv1
+        # when this is an identity block (its dgrad then holds the whole gradient of x)
+        bt_in = getattr(x, "_dpa_btap", None) if tap is not None else None
+        bt2 = BNTap() if train and _FUSE_BN_BWD else None
+        bt3 = BNTap() if train and _FUSE_BN_BWD else None
         # each conv hands the following BN its batch statistics (ops/conv_igemm.py)
-        c1, st = _conv(x, self.conv1, cdtype, self.bn1, tap, xtap)
+        c1, st = _conv(x, self.conv1, cdtype, self.bn1, tap, xtap, bt_in)
         out = bn_act(c1, self.bn1, relu=True, comm=_comm_of(self.bn1), stats=st)
         c2, st = _conv(out, self.conv2, cdtype, self.bn2)
-        out = bn_act(c2, self.bn2, relu=True, comm=_comm_of(self.bn2), stats=st)
+        out = bn_act(c2, self.bn2, relu=True, comm=_comm_of(self.bn2), stats=st, btap=bt2)
         identity = x
         if self.downsample is not None:
             conv, bn = self.downsample[0], self.downsample[1]
             cd, st = _conv(x, conv, cdtype, bn, None, xtap)
             identity = bn_act(cd, bn, relu=False, comm=_comm_of(bn), stats=st)
-        c3, st = _conv(out, self.conv3, cdtype, self.bn3)
-        return bn_act(c3, self.bn3, res=identity, relu=True, comm=_comm_of(self.bn3), tap=tap, stats=st)
+        c3, st = _conv(out, self.conv3, cdtype, self.bn3, btap=bt2)
+        y = bn_act(c3, self.bn3, res=identity, relu=True, comm=_comm_of(self.bn3), tap=tap, stats=st, btap=bt3)
+        if bt3 is not None:
+            y._dpa_btap = bt3
+        return y
 
 
 class ResNet(nn.Module):

@@ -44,10 +44,32 @@ def _cl(t: torch.Tensor) -> torch.Tensor:
     return t if t.is_contiguous(memory_format=_CL) else t.contiguous(memory_format=_CL)
 
 
+class BNTap:
+    """Hand-off of a training BatchNorm's backward sums from the 1x1 conv that consumes its
+    output (ops/conv1x1.py): that conv's data-gradient kernel produces dy for this BN, and
+    its epilogue also takes S1 = sum dz, S2 = sum dz * xhat (csrc/kernels/conv_igemm.hip,
+    BS epilogue), so the backward here skips its bwd_stats pass over dy / x (/ y).
+
+    The forward fills x, y (act 1: the ReLU follows a residual add), act, save (mean |
+    invstd), weight, bias; the conv's backward sets ``sums`` = (out, dgamma, dbeta) and
+    ``grad_ptr`` = the gradient it wrote; the BN backward uses them when dy is that tensor.
+    """
+
+    __slots__ = ("x", "y", "act", "save", "weight", "bias", "sums", "grad_ptr")
+
+    def __init__(self):
+        self.x = self.y = self.save = self.weight = self.bias = self.sums = None
+        self.act = 0
+        self.grad_ptr = 0
+
+    def clear(self):
+        self.x = self.y = self.save = self.weight = self.bias = self.sums = None
+
+
 class BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, res, running_mean, running_var, nbt, momentum, eps, training, relu, comm,
-                tap=None, pre=None):
+                tap=None, pre=None, btap=None):
         K = _K()
         x = _cl(x)
         C = x.shape[1]
@@ -74,6 +96,12 @@ class BNActFn(torch.autograd.Function):
             ctx.save_for_backward(x, y if ctx.act == 1 else None, weight, bias, save, stats)
             ctx.sync, ctx.comm, ctx.has_res = sync, comm, res is not None
             ctx.tap = tap if res is not None else None
+            ctx.btap = btap if ctx.act in (1, 2) else None
+            if ctx.btap is not None:
+                bt = ctx.btap
+                bt.x, bt.y, bt.act, bt.save, bt.weight, bt.bias = x, (y if ctx.act == 1 else None), ctx.act, save, \
+                    weight, bias
+                bt.sums = None
         else:
             dummy = torch.empty(2 * C + 1, **f32)
             K.apply(x, resc, y, C, dummy, weight, bias, running_mean, running_var, nbt, mom, float(eps), False,
@@ -89,29 +117,37 @@ class BNActFn(torch.autograd.Function):
         x, y, weight, bias, save, stats = ctx.saved_tensors
         C = x.shape[1]
         dy = _cl(dy)
-        part, ticket = _Workspace.get(x.device, C)
         f32 = dict(dtype=torch.float32, device=x.device)
-        out = torch.empty(2 * C, **f32)
-        dgamma = torch.empty(C, **f32)
-        dbeta = torch.empty(C, **f32)
-        K.bwd_stats(dy, y, x, C, ctx.act, save, weight, bias, part, ticket, out, dgamma, dbeta)
+        bt = getattr(ctx, "btap", None)
+        if bt is not None and bt.sums is not None and bt.grad_ptr == dy.data_ptr():
+            out, dgamma, dbeta = bt.sums  # taken by the consumer conv's data-gradient epilogue
+        else:
+            part, ticket = _Workspace.get(x.device, C)
+            out = torch.empty(2 * C, **f32)
+            dgamma = torch.empty(C, **f32)
+            dbeta = torch.empty(C, **f32)
+            K.bwd_stats(dy, y, x, C, ctx.act, save, weight, bias, part, ticket, out, dgamma, dbeta)
+        if bt is not None:
+            bt.clear()
+            ctx.btap = None
         sums = ctx.comm.all_reduce(out) if ctx.sync else out
         dx = torch.empty_like(x, memory_format=_CL)
         dres = torch.empty_like(x, memory_format=_CL) if ctx.has_res else None
         K.bwd_elemt(dy, y, x, C, ctx.act, save, sums, stats, weight, bias, dx, dres)
         if ctx.tap is not None:  # d(res) goes to the consumer's GEMM (ops/conv1x1.py GradTap)
             ctx.tap.grad, dres = dres, None
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None, None
 
 
-def bn_act(x, bn, res=None, relu=True, comm=None, tap=None, stats=None):
+def bn_act(x, bn, res=None, relu=True, comm=None, tap=None, stats=None, btap=None):
     """BatchNorm module ``bn`` applied to channels_last ``x`` (+ res) (+ ReLU).
     ``tap``: hand d(res) to a GradTap instead of returning it (ops/conv1x1.py).
     ``stats``: the batch statistics already computed by the producing conv
-    (ops/conv_igemm.py; training only) -- no statistics pass here."""
+    (ops/conv_igemm.py; training only) -- no statistics pass here.
+    ``btap``: a :class:`BNTap` the consuming 1x1 conv fills with this BN's backward sums."""
     return BNActFn.apply(x, bn.weight, bn.bias, res, bn.running_mean, bn.running_var, bn.num_batches_tracked,
                          bn.momentum, bn.eps, bn.training, relu, comm if bn.training else None, tap,
-                         stats if bn.training else None)
+                         stats if bn.training else None, btap if bn.training else None)
 
 
 class MaxPoolFn(torch.autograd.Function):

@@ -84,8 +84,9 @@ class Conv1x1Fn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, stride: int, cdtype: torch.dtype, tap: GradTap | None = None, bn=None, packed=None,
-                xtap: GradTap | None = None):
+                xtap: GradTap | None = None, btap=None):
         in_shape = x.shape
+        ctx.btap = btap if stride == 1 else None  # ops/bn_nhwc.BNTap of the BN that produced x
         if tap is not None and stride != 1:
             raise ValueError("conv1x1: a gradient tap needs stride 1")
         ctx.tap = tap
@@ -155,13 +156,18 @@ class Conv1x1Fn(torch.autograd.Function):
         elif ctx.needs_input_grad[0] and acc is not None:
             if acc.shape != (N, C, H, W) or not acc.is_contiguous(memory_format=torch.channels_last):
                 raise RuntimeError("conv1x1: tapped gradient does not match the input")
-            if mine:
+            if mine and _igemm.dgrad_bn(dyc, wt, ctx.btap, acc) is not None:
+                pass  # accumulated, with the producing BN's backward sums (ops/bn_nhwc.BNTap)
+            elif mine:
                 _igemm.conv_acc(dyc, wt, acc)
             else:
                 _rows(acc).addmm_(dyr, w)  # acc <- acc + dY @ W (GEMM epilogue accumulate)
             dx = acc
         elif ctx.needs_input_grad[0]:
-            dx = Conv1x1Fn._compact(dyc, dyr, w, wt, (N, C, H, W))
+            dx = _igemm.dgrad_bn(dyc, wt, ctx.btap) if mine else None
+            if dx is None:
+                dx = Conv1x1Fn._compact(dyc, dyr, w, wt, (N, C, H, W))
+        ctx.btap = None
         if ctx.needs_input_grad[1]:
             if ctx.lazy_rows and _igemm.usable(dyc, w.view(ctx.wshape), w.dtype):
                 # implicit-GEMM weight gradient over the (strided) input pixels, fp32 out
@@ -170,7 +176,7 @@ class Conv1x1Fn(torch.autograd.Function):
                 # saved: the [P, C] rows, or (lazy) the unstrided input
                 rows = _rows(saved[:, :, ::stride, ::stride] if stride != 1 else saved) if ctx.lazy_rows else saved
                 dw = _wgrad(dyr, rows).view(ctx.wshape)
-        return dx, dw, None, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None
 
     @staticmethod
     def _compact(dyc, dyr, w, wt, geom):
@@ -212,9 +218,11 @@ class Conv1x1Fn(torch.autograd.Function):
 
 
 def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int, cdtype: torch.dtype,
-            tap: GradTap | None = None, bn=None, packed=None, xtap: GradTap | None = None):
+            tap: GradTap | None = None, bn=None, packed=None, xtap: GradTap | None = None, btap=None):
     """Bias-free 1x1 conv (stride 1 or 2) of ``x`` with the fp32 ``weight``; the
     output is a channels_last [N, Cout, H', W'] tensor in ``cdtype``.  ``tap``:
     see :class:`GradTap`.  With ``bn`` (the training BatchNorm that follows): returns
-    (output, its statistics or None) -- ops/conv_igemm.py."""
-    return Conv1x1Fn.apply(x, weight, int(stride), cdtype, tap, bn, packed, xtap)
+    (output, its statistics or None) -- ops/conv_igemm.py.  ``btap``: the
+    ops/bn_nhwc.BNTap of the BatchNorm that produced ``x`` -- the data gradient then also
+    takes that BN's backward sums."""
+    return Conv1x1Fn.apply(x, weight, int(stride), cdtype, tap, bn, packed, xtap, btap)

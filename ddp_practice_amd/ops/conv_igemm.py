@@ -87,6 +87,35 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn=None, a
     return y, stats
 
 
+def dgrad_bn(dy: torch.Tensor, wt: torch.Tensor, bt, acc: torch.Tensor | None = None) -> torch.Tensor | None:
+    """1x1 / stride-1 data gradient dx = conv(dy, wt) (+= acc, the tapped residual gradient)
+    whose epilogue also takes the backward sums of the BatchNorm that produced the conv's
+    input (``bt``: ops/bn_nhwc.BNTap, filled by that BN's forward).  Stores the sums in
+    ``bt`` and returns dx; None when the shapes do not allow it (the BN then runs its own
+    statistics pass)."""
+    if bt is None or bt.x is None or not G1X1:
+        return None
+    if (acc is None) != (bt.act == 2):  # act 1 (ReLU after a residual add) <-> accumulated dx
+        return None
+    N, _, H, W = dy.shape
+    C = wt.shape[0]
+    shape = (N, C, H, W)
+    if tuple(bt.x.shape) != shape or bt.x.dtype != dy.dtype or not bt.x.is_contiguous(memory_format=_CL):
+        return None
+    if acc is not None and (tuple(acc.shape) != shape or not acc.is_contiguous(memory_format=_CL)):
+        return None
+    f32 = dict(dtype=torch.float32, device=dy.device)
+    part, tickets = _StatWS.get(dy.device, N * H * W, C)
+    out, dgamma, dbeta = torch.empty(2 * C, **f32), torch.empty(C, **f32), torch.empty(C, **f32)
+    dx = acc if acc is not None else torch.empty(shape, dtype=dy.dtype, device=dy.device, memory_format=_CL)
+    _K().conv_fwd(dy, wt, dx, 1, 0, part, tickets, accumulate=acc is not None, bn_x=bt.x,
+                  bn_y=bt.y if bt.act == 1 else None, bn_save=bt.save, bn_gamma=bt.weight, bn_beta=bt.bias,
+                  bn_out=out, bn_dgamma=dgamma, bn_dbeta=dbeta)
+    bt.sums = (out, dgamma, dbeta)
+    bt.grad_ptr = dx.data_ptr()
+    return dx
+
+
 def dgrad_s2(dy: torch.Tensor, wt: torch.Tensor, in_hw) -> torch.Tensor | None:
     """Data gradient of a 3x3 / stride-2 / pad-1 conv on the implicit-GEMM kernel
     (MODE_S2T: four output-parity sub-convolutions, csrc/kernels/conv_igemm.hip).

@@ -32,7 +32,7 @@ def timeit(fn, n=20):
     return e0.elapsed_time(e1) / n * 1e3
 
 
-tot_me = tot_ref = tot_wme = tot_wref = 0.0
+tot_me = tot_ref = tot_wme = tot_wref = tot_wold = 0.0
 from ddp_practice_amd.ops.conv_igemm import conv_wgrad  # noqa: E402
 print(f"{'shape':34s} {'GFLOP':>7s} {'mine us':>8s} {'TF/s':>6s} {'nostat':>7s} {'ref us':>8s} {'TF/s':>6s}")
 for Cin, H, K, R, st, cnt in SHAPES:
@@ -61,19 +61,25 @@ for Cin, H, K, R, st, cnt in SHAPES:
     err = ((y.float() - ref).abs().max() / ref.abs().max()).item()
     dy = torch.randn_like(y)
     wshape = tuple(w.shape)
+    C.conv_igemm.wgrad_config(0)
+    t_wold = timeit(lambda: conv_wgrad(dy, x, wshape, st, pad))
+    C.conv_igemm.wgrad_config(2)
     t_wme = timeit(lambda: conv_wgrad(dy, x, wshape, st, pad))
     t_wref = timeit(lambda: torch.ops.aten.convolution_backward(dy, x, w, None, [st, st], [pad, pad], [1, 1], False,
                                                                 [0, 0], 1, [False, True, False]))
+    C.conv_igemm.wgrad_config(1)
     gw = conv_wgrad(dy, x, wshape, st, pad)
     rw = torch.ops.aten.convolution_backward(dy.float(), x.float(), w.float(), None, [st, st], [pad, pad], [1, 1],
                                              False, [0, 0], 1, [False, True, False])[1]
     werr = ((gw - rw).abs().max() / rw.abs().max()).item()
     tot_wme += t_wme * cnt
+    tot_wold += t_wold * cnt
     tot_wref += t_wref * cnt
     tot_me += t_me * cnt
     tot_ref += t_ref * cnt
     print(f"{str((Cin, H, K, R, st)):34s} {fl:7.2f} {t_me:8.1f} {fl / t_me * 1e3:6.0f} {t_ns:7.1f} {t_ref:8.1f} "
-          f"{fl / t_ref * 1e3:6.0f}  err={err:.1e} | wgrad {t_wme:7.1f} vs {t_wref:7.1f} err={werr:.1e} x{cnt}")
+          f"{fl / t_ref * 1e3:6.0f}  err={err:.1e} | wgrad glds {t_wme:7.1f} reg {t_wold:7.1f} MIOpen {t_wref:7.1f} "
+          f"err={werr:.1e} x{cnt}")
 print(f"network forward convs (x count): mine {tot_me:.0f} us, reference {tot_ref:.0f} us "
       "(mine includes the BN statistics; reference does not)")
-print(f"network wgrad (x count): mine {tot_wme:.0f} us, MIOpen {tot_wref:.0f} us")
+print(f"network wgrad (x count): glds {tot_wme:.0f} us, register-staged {tot_wold:.0f} us, MIOpen {tot_wref:.0f} us")

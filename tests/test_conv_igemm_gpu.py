@@ -271,3 +271,87 @@ def test_conv_fwd_deferred_statistics(C, shape):
         _run(C, *shape, torch.bfloat16, True)
     finally:
         K_.stat_defer_config(prev)
+
+
+@pytest.mark.parametrize("shape", [
+    (2, 64, 14, 14, 64, 3, 1, 1),     # 3x3: padding taps read the zero page
+    (2, 128, 15, 15, 128, 3, 2, 1),   # stride 2, odd input
+    (3, 256, 7, 7, 128, 1, 1, 0),     # 1x1, ragged pixel count (split past the end)
+    (2, 128, 14, 14, 256, 1, 2, 0),   # 1x1 stride 2
+    (4, 64, 28, 28, 128, 3, 1, 1),    # several pixel splits
+])
+def test_conv_wgrad_glds_matches_register_staged(C, shape):
+    """conv_wgrad_glds_kernel (LDS-DMA staging, zero page for padding) == the register-staged
+    weight-gradient kernel bit for bit (same tiles, same MFMA order) and == fp32 torch."""
+    from ddp_practice_amd.ops.conv_igemm import conv_wgrad
+
+    K_ = C.conv_igemm
+    N, Cin, H, W, K, R, stride, pad = shape
+    g = torch.Generator().manual_seed(29)
+    x = torch.randn(N, Cin, H, W, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=CL)
+    OH = (H + 2 * pad - R) // stride + 1
+    dy = torch.randn(N, K, OH, OH, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=CL)
+    prev = K_.wgrad_config(2)  # the glds kernel for every shape (default: 1x1 only)
+    try:
+        got = conv_wgrad(dy, x, (K, Cin, R, R), stride, pad)
+        K_.wgrad_config(0)
+        old = conv_wgrad(dy, x, (K, Cin, R, R), stride, pad)
+    finally:
+        K_.wgrad_config(prev)
+    assert torch.equal(got, old)
+    w = torch.zeros(K, Cin, R, R, device=DEV, requires_grad=True)
+    F.conv2d(x.float(), w, None, stride, pad).backward(dy.float())
+    err = ((got - w.grad).abs().max() / w.grad.abs().max()).item()
+    assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("act", [1, 2])
+@pytest.mark.parametrize("shape", [(2, 128, 14, 14, 64), (3, 64, 7, 7, 256), (2, 256, 28, 28, 128)])
+def test_dgrad_epilogue_bn_backward_sums(C, act, shape):
+    """1x1 data gradient with the producing BatchNorm's backward sums in its epilogue
+    (ops/conv_igemm.dgrad_bn, kernel BS modes): dx == fp32 torch (accumulated onto the
+    tapped residual gradient for act 1) and S1 = sum dz, S2 = sum dz * xhat of the STORED
+    dx == the same sums in fp64 (dz = dx * relu', mask from y (act 1) or recomputed from x)."""
+    from ddp_practice_amd.ops.bn_nhwc import BNTap
+    from ddp_practice_amd.ops.conv_igemm import dgrad_bn
+
+    N, K, H, W, Cc = shape
+    g = torch.Generator().manual_seed(41 + act + Cc)
+    bf = dict(device=DEV, dtype=torch.bfloat16)
+    dy = torch.randn(N, K, H, W, generator=g).to(**bf).contiguous(memory_format=CL)
+    wt = (torch.randn(Cc, K, 1, 1, generator=g) / K ** 0.5).to(**bf).contiguous(memory_format=CL)
+    x = torch.randn(N, Cc, H, W, generator=g).to(**bf).contiguous(memory_format=CL)
+    mean = torch.randn(Cc, generator=g) * 0.1
+    invstd = torch.rand(Cc, generator=g) + 0.5
+    gamma, beta = torch.randn(Cc, generator=g), torch.randn(Cc, generator=g) * 0.3
+    bt = BNTap()
+    bt.x, bt.act = x, act
+    bt.save = torch.cat([mean, invstd]).to(DEV)
+    bt.weight, bt.bias = gamma.to(DEV), beta.to(DEV)
+    acc = None
+    if act == 1:
+        bt.y = torch.randn(N, Cc, H, W, generator=g).to(**bf).contiguous(memory_format=CL)
+        acc = torch.randn(N, Cc, H, W, generator=g).to(**bf).contiguous(memory_format=CL)
+    acc0 = acc.clone() if acc is not None else None
+    dx = dgrad_bn(dy, wt, bt, acc)
+    assert dx is not None and bt.sums is not None and bt.grad_ptr == dx.data_ptr()
+    ref = F.conv2d(dy.float(), wt.float())
+    if acc0 is not None:
+        ref = ref + acc0.float()
+    err = ((dx.float() - ref).abs().max() / ref.abs().max()).item()
+    assert err < 2e-2, err
+    xd, dd = x.double().cpu(), dx.double().cpu()
+    if act == 1:
+        mask = bt.y.double().cpu() > 0
+    else:
+        s = (gamma * invstd).double().view(1, -1, 1, 1)
+        b = (beta.double() - mean.double() * gamma.double() * invstd.double()).view(1, -1, 1, 1)
+        mask = (xd * s + b) > 0
+    dz = torch.where(mask, dd, torch.zeros_like(dd))
+    xhat = (xd - mean.double().view(1, -1, 1, 1)) * invstd.double().view(1, -1, 1, 1)
+    s1, s2 = dz.sum((0, 2, 3)), (dz * xhat).sum((0, 2, 3))
+    out, dgamma, dbeta = (t.double().cpu() for t in bt.sums)
+    scale = dz.abs().sum((0, 2, 3)) + 1.0
+    assert ((out[:Cc] - s1).abs() / scale).max() < 1e-4
+    assert ((out[Cc:] - s2).abs() / scale).max() < 1e-4
+    assert torch.equal(dbeta, out[:Cc]) and torch.equal(dgamma, out[Cc:])
