@@ -77,13 +77,13 @@ struct StatArgs {
   int64_t* nbt;       // num_batches_tracked (bumped once) or null
   int defer;          // 1: level-1 rows only (plain stores, no ticket), stat_tree_kernel follows
   // backward statistics of the BatchNorm whose output gradient this conv produces
-  // (conv1x1_kernel BS > 0): stats = out [S1 | S2], plus dbeta = S1, dgamma = S2
+  // (conv_glds_kernel BS > 0): stats = out [S1 | S2], plus dbeta = S1, dgamma = S2
   float* dgamma = nullptr;
   float* dbeta = nullptr;
   int bwd = 0;
 };
 
-// BS (conv1x1_kernel): the output is the gradient dy of a BatchNorm's output; the epilogue
+// BS (conv_glds_kernel): the output is the gradient dy of a BatchNorm's output; the epilogue
 // also takes that BN's backward sums S1 = sum dz, S2 = sum dz * xhat (dz = dy * relu'),
 // as the separate bn_nhwc bwd_stats pass would (csrc/kernels/bn_nhwc.hip):
 //   BS_Y:   ReLU mask from the BN's output y (a residual was added); the gradient is
@@ -454,10 +454,12 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// 1x1 convolution (pad 0, stride 1 or 2) as a plain GEMM over the NHWC rows:
-//   y[p][k] = sum_c x[row(p)][c] * w[k][c]      (M = pixels, N = Cout, K = C)
-// -- the forward of 36 of ResNet-50's 53 convs and, with the transposed filter, their
-// data gradients.  The general kernel above is LDS-bound on these shapes: a 64 x 64
+// Implicit-GEMM convolution with both operands staged by LDS-DMA (MODE_GEN: any R x S,
+// stride, padding; C % 64 == 0).  Written first for the 1x1 convs, a plain GEMM over the
+// NHWC rows (y[p][k] = sum_c x[row(p)][c] * w[k][c]; M = pixels, N = Cout, K = C) -- the
+// forward of 36 of ResNet-50's 53 convs and, with the transposed filter, their data
+// gradients; a K-step is one filter tap x 64 channels, a padding tap reads a zero page.
+// The general kernel above is LDS-bound on these shapes: a 64 x 64
 // wave tile reads 32 FLOP per LDS byte and its register-staged ds_write_b128 stores
 // cost ~13 LDS cycles per KiB, so the MFMAs idle behind the LDS (2x slower than
 // hipBLASLt on the deep layers, profiles/r2_conv_igemm_fwd_vs_library_bs128.txt).
@@ -498,9 +500,13 @@ __device__ __forceinline__ void glds16(const void* src, void* dst) {
   __builtin_amdgcn_global_load_lds(src, (lds_vptr)dst, 16, 0, 0);
 }
 
-template <typename T, int BP, int BN, int BS = BS_NONE>
+// 16 zero bytes: the LDS-DMA source of padding taps and out-of-range rows (a DMA cannot
+// zero-fill; its per-lane source address can point here instead)
+__device__ __attribute__((aligned(16))) unsigned char g_zero16[16] = {0};
+
+template <typename T, int BP, int BN, int BS = BS_NONE, bool KXK = false>
 __global__ void __launch_bounds__(THR)
-conv1x1_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__ y, StatArgs sa, Geom g,
+conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__ y, StatArgs sa, Geom g,
                BwdStatArgs<T> bs) {
   using MMT = MM<T>;
   using L = G1x1Lds<T, BP, BN>;
@@ -523,35 +529,63 @@ conv1x1_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__
   const long long p0 = bm * BP;
   const int k0 = bn * BN;
   // this lane's source rows: wave-instruction i covers rows (4i + wave) * 8 .. + 7, the lane
-  // row (lane >> 3) of them, logical chunk (lane & 7) ^ (row & 7) (row & 7 == lane >> 3)
+  // row (lane >> 3) of them, logical chunk (lane & 7) ^ (row & 7) (row & 7 == lane >> 3).
+  // KXK: a K-step is one filter tap (r, s) x 64 input channels (C % 64 == 0): the pixel's
+  // input row is (n, oh*st - pad + r, ow*st - pad + s) and a padding tap reads the zero
+  // page; else (1x1, pad 0) the K-steps walk the pixel's own input row (no bounds checks,
+  // no per-step tap arithmetic: the general form costs the 1x1 shapes 5-12 %).
   const int lr = lane >> 3, chunk = (lane & 7) ^ lr;
-  unsigned xo[AR], wo[WR];  // element offsets (host-checked < 2^31)
+  unsigned xo[AR], wo[WR];  // element offsets of the pixel rows / (n, ih0, iw0), filter rows (< 2^31)
+  int ih0[AR], iw0[AR];
 #pragma unroll
   for (int i = 0; i < AR; ++i) {
     long long p = p0 + (i * 4 + wave) * 8 + lr;
     p = p < g.M ? p : g.M - 1;  // ragged tail: a valid row, its output is not stored
-    long long r = p;
-    if (g.stride != 1) {
+    if constexpr (KXK) {
       const int ow = (int)(p % g.OW);
       const long long t = p / g.OW;
       const int oh = (int)(t % g.OH);
       const int n = (int)(t / g.OH);
-      r = ((long long)n * g.H + (long long)oh * g.stride) * g.W + (long long)ow * g.stride;
+      ih0[i] = oh * g.stride - g.pad;
+      iw0[i] = ow * g.stride - g.pad;
+      xo[i] = (unsigned)((((long long)n * g.H + ih0[i]) * g.W + iw0[i]) * g.C + chunk * 8);
+    } else {
+      long long r = p;
+      if (g.stride != 1) {
+        const int ow = (int)(p % g.OW);
+        const long long t = p / g.OW;
+        const int oh = (int)(t % g.OH);
+        const int n = (int)(t / g.OH);
+        r = ((long long)n * g.H + (long long)oh * g.stride) * g.W + (long long)ow * g.stride;
+      }
+      xo[i] = (unsigned)(r * g.C + chunk * 8);
+      ih0[i] = iw0[i] = 0;
     }
-    xo[i] = (unsigned)(r * g.C + chunk * 8);
   }
+  const int wrow = KXK ? g.R * g.S * g.C : g.C;
 #pragma unroll
-  for (int i = 0; i < WR; ++i) wo[i] = (unsigned)((k0 + (i * 4 + wave) * 8 + lr) * g.C + chunk * 8);
-  const int KT = g.C / BK;
+  for (int i = 0; i < WR; ++i) wo[i] = (unsigned)((k0 + (i * 4 + wave) * 8 + lr) * wrow + chunk * 8);
+  const int cpt = g.C / BK;
+  const int KT = KXK ? g.R * g.S * cpt : cpt;
   auto issue = [&](int kt, int buf) {
     T* base = lds + buf * L::STAGE;
-    const int ko = kt * BK;
 #pragma unroll
     for (int i = 0; i < WR; ++i)
-      glds16(w + wo[i] + ko, base + (i * 4 + wave) * 8 * BK);
+      glds16(w + wo[i] + kt * BK, base + (i * 4 + wave) * 8 * BK);
+    if constexpr (KXK) {
+      const int rs = kt / cpt, c0 = (kt - rs * cpt) * BK;  // wave-uniform
+      const int r = rs / g.S, s = rs - r * g.S;
+      const int xk = (r * g.W + s) * g.C + c0;
 #pragma unroll
-    for (int i = 0; i < AR; ++i)
-      glds16(x + xo[i] + ko, base + (BN + (i * 4 + wave) * 8) * BK);
+      for (int i = 0; i < AR; ++i) {
+        const bool ok = (unsigned)(ih0[i] + r) < (unsigned)g.H && (unsigned)(iw0[i] + s) < (unsigned)g.W;
+        glds16(ok ? (const void*)(x + (int)xo[i] + xk) : (const void*)g_zero16,
+               base + (BN + (i * 4 + wave) * 8) * BK);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < AR; ++i) glds16(x + xo[i] + kt * BK, base + (BN + (i * 4 + wave) * 8) * BK);
+    }
   };
   f32x4 acc[CT][PT];
 #pragma unroll
@@ -815,6 +849,51 @@ conv1x1_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__
 // workgroup (bn, grp) sums its group of G1 rows into a level-2 row, the last of a
 // channel tile's NG arrivals sums those into the final statistics.  Same association
 // as the in-launch tree: the result is bitwise the same.
+// One-level variant for grids of <= S1_MAXROWS pixel tiles (most convs past 28x28): a
+// workgroup of 1024 lanes owns S1_COLS of the 2*BN level-1 columns of one channel tile as
+// 16 row groups x 64 columns, each group with every row it sums in flight (16 loads),
+// combined in group order through LDS -- one dependent round trip instead of the two
+// levels' three (rows, ticket, level-2 rows).  Fixed order: deterministic.
+constexpr int S1_THR = 1024, S1_COLS = 64, S1_RG = S1_THR / S1_COLS, S1_MAXROWS = 256;
+template <int BN>
+__global__ void __launch_bounds__(S1_THR) stat_sum1_kernel(StatArgs sa, long long M, int BM_, int K) {
+  __shared__ float part[S1_RG][S1_COLS];
+  const int nct = K / BN, bn = blockIdx.x, c0 = blockIdx.y * S1_COLS;
+  const int rows = (int)((M + BM_ - 1) / BM_);
+  const int col = threadIdx.x % S1_COLS, rg = threadIdx.x / S1_COLS;
+  const float* lvl1 = sa.part + (long long)bn * rows * (2 * BN) + c0 + col;
+  float v[S1_MAXROWS / S1_RG];
+#pragma unroll
+  for (int u = 0; u < S1_MAXROWS / S1_RG; ++u) {
+    const int r = rg + u * S1_RG;
+    v[u] = lvl1[(long long)(r < rows ? r : 0) * (2 * BN)];
+  }
+  float a = 0.f;
+#pragma unroll
+  for (int u = 0; u < S1_MAXROWS / S1_RG; ++u)
+    if (rg + u * S1_RG < rows) a += v[u];
+  part[rg][col] = a;
+  __syncthreads();
+  if (threadIdx.x >= S1_COLS) return;
+  float t = 0.f;
+#pragma unroll
+  for (int g = 0; g < S1_RG; ++g) t += part[g][threadIdx.x];
+  const int cc = c0 + threadIdx.x;  // column of [S1 | S2] (or [sum | sumsq])
+  const int h = cc / BN, k = bn * BN + cc % BN;
+  if (sa.bwd) {
+    if (h == 0) sa.stats[k] = sa.dbeta[k] = t;
+    else sa.stats[K + k] = sa.dgamma[k] = t;
+    return;
+  }
+  sa.stats[h * K + k] = t;
+  if (h == 0) sa.stats[2 * K + SHIFT_OFF + k] = sa.shift[k];
+  if (bn == 0 && cc == 0) {
+    sa.stats[2 * K] = (float)M;
+    if (sa.nbt != nullptr) sa.nbt[0] = sa.nbt[0] + 1;
+  }
+  (void)nct;
+}
+
 template <int BN>
 __global__ void __launch_bounds__(THR) stat_tree_kernel(StatArgs sa, long long M, int BM_, int K) {
   __shared__ float scr[THR];
@@ -1007,9 +1086,7 @@ conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __re
 // the per-lane source address (logical chunk = slot ^ xor(row)); padding taps and pixels
 // past the split's end read a 16-B zero page instead of being zero-filled by the loader.
 // One barrier per 64-pixel step: wait the landed step (vmcnt(0)) + barrier, issue step
-// t+1 into the other buffer, MFMA on step t (as conv1x1_kernel).
-__device__ __attribute__((aligned(16))) unsigned char g_zero16[16] = {0};
-
+// t+1 into the other buffer, MFMA on step t (as conv_glds_kernel).
 template <int CH>
 __device__ __forceinline__ int wswz_xor(int row) {
   const int f = (row & 3) | ((row >> 1) & 4);
@@ -1301,7 +1378,7 @@ bool supported(int64_t C, int64_t K) { return C % BK == 0 && K % 64 == 0; }
 
 static int tile_n(int64_t K) { return K % 128 == 0 ? 128 : 64; }
 
-// 1x1 convs on conv1x1_kernel (DPA_G1X1=0: the general kernel, A/B runs; g1x1_config
+// 1x1 convs on conv_glds_kernel (DPA_G1X1=0: the general kernel, A/B runs; g1x1_config
 // switches both at run time for tests and sweeps)
 static int g_g1x1_on = -1, g_g1x1_bp = -1;
 static long long g_g1x1_min256 = -1;
@@ -1321,7 +1398,23 @@ static bool g1x1_enabled() {
   return g_g1x1_on != 0;
 }
 
-// pixel tile of conv1x1_kernel: 256 when the grid still has >= min256 workgroups (default
+// KxK convs (any stride / padding) on the glds kernel too (DPA_G3X3=0: 1x1 only, A/B runs)
+static int g_g3x3_on = -1;
+static bool g3x3_enabled() {
+  if (g_g3x3_on < 0) {
+    const char* e = std::getenv("DPA_G3X3");
+    g_g3x3_on = (e == nullptr || e[0] != '0') ? 1 : 0;
+  }
+  return g_g3x3_on != 0;
+}
+int64_t g3x3_config(int64_t on) {
+  g3x3_enabled();
+  const int64_t prev = g_g3x3_on;
+  if (on >= 0) g_g3x3_on = on ? 1 : 0;
+  return prev;
+}
+
+// pixel tile of conv_glds_kernel: 256 when the grid still has >= min256 workgroups (default
 // 2 per CU: the 96 KB of LDS leave one 256-pixel workgroup per CU), else 128 (64 KB: two
 // per CU); DPA_G1X1_BP=128|256 forces one.
 static int g1x1_bp(long long M, int64_t K) {
@@ -1338,7 +1431,7 @@ static long long g_defer_min = -2;
 static bool defer_stats(long long blocks) {
   if (g_defer_min == -2) {
     const char* e = std::getenv("DPA_STAT_DEFER_MIN");
-    g_defer_min = e != nullptr ? std::atoll(e) : 1024LL;
+    g_defer_min = e != nullptr ? std::atoll(e) : 0LL;  // always: measured 14.73 vs 14.77-14.84 ms (1024)
   }
   return g_defer_min >= 0 && blocks > g_defer_min;
 }
@@ -1351,6 +1444,13 @@ int64_t stat_defer_config(int64_t min_blocks) {
 
 static void launch_stat_tree(const StatArgs& sa, long long M, int bm, int K, int BN) {
   const long long rows = (M + bm - 1) / bm, NG = (rows + G1 - 1) / G1;
+  if (rows <= S1_MAXROWS) {  // one level: every row in flight at once, no ticket
+    const dim3 gr((unsigned)(K / BN), (unsigned)(2 * BN / S1_COLS)), th(S1_THR);
+    if (BN == 128) hipLaunchKernelGGL(stat_sum1_kernel<128>, gr, th, 0, cur_stream(), sa, M, bm, K);
+    else hipLaunchKernelGGL(stat_sum1_kernel<64>, gr, th, 0, cur_stream(), sa, M, bm, K);
+    DPA_CHECK_LAUNCH();
+    return;
+  }
   const dim3 gr((unsigned)(NG * (K / BN))), th(THR);
   if (BN == 128) hipLaunchKernelGGL(stat_tree_kernel<128>, gr, th, 0, cur_stream(), sa, M, bm, K);
   else hipLaunchKernelGGL(stat_tree_kernel<64>, gr, th, 0, cur_stream(), sa, M, bm, K);
@@ -1387,7 +1487,7 @@ int64_t stat_tickets_len(int64_t M, int64_t K) {
 // aux (MODE_GEN, channels_last [N, K, OH/2, OW/2]): added at the even output pixels --
 // a stride-2 1x1 conv's data gradient folded into this one's output.
 //
-// bn_x (1x1, stride 1, on conv1x1_kernel): y is the output gradient of a training BatchNorm
+// bn_x (1x1, stride 1, on conv_glds_kernel): y is the output gradient of a training BatchNorm
 // whose input was bn_x; the epilogue also produces that BN's backward sums (bn_nhwc
 // bwd_stats: bn_out = [S1 | S2], bn_dbeta = S1, bn_dgamma = S2) -- bn_y given: the ReLU
 // mask comes from the BN's output (and y accumulates onto the tapped residual gradient,
@@ -1483,10 +1583,10 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
     sa.nbt = nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr;
   }
   const int BN = tile_n(g.K);
-  if (mode == MODE_GEN && g.R == 1 && g.S == 1 && g.pad == 0 && g1x1_enabled() && x.numel() < (1LL << 31) &&
-      w.numel() < (1LL << 31)) {
-    // 1x1: the glds-staged GEMM kernel (pixel tile 256 or 128, see g1x1_bp)
-    const int BP = bwdst ? 128 : g1x1_bp(g.M, g.K);
+  if (mode == MODE_GEN && g1x1_enabled() && x.numel() < (1LL << 31) && w.numel() < (1LL << 31) &&
+      (g3x3_enabled() || (g.R == 1 && g.S == 1 && g.pad == 0))) {
+    // the glds-staged implicit-GEMM kernel (pixel tile 256 or 128, see g1x1_bp)
+    const int BP = (bwdst || !(g.R == 1 && g.S == 1 && g.pad == 0)) ? 128 : g1x1_bp(g.M, g.K);
     const long long blocks = (g.M + BP - 1) / BP * (g.K / BN);
     TORCH_CHECK(blocks < (1LL << 31), "conv_fwd: grid too large");
     sa.defer = st && defer_stats(blocks) ? 1 : 0;
@@ -1513,18 +1613,23 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
         bs.gamma = bn_gamma.has_value() ? bn_gamma->data_ptr<float>() : nullptr;
         bs.beta = bn_beta.has_value() ? bn_beta->data_ptr<float>() : nullptr;
         if (bn_y.has_value()) {
-          if (BN == 128) hipLaunchKernelGGL((conv1x1_kernel<T, 128, 128, BS_Y>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
-          else hipLaunchKernelGGL((conv1x1_kernel<T, 128, 64, BS_Y>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+          if (BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_Y>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+          else hipLaunchKernelGGL((conv_glds_kernel<T, 128, 64, BS_Y>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
         } else {
-          if (BN == 128) hipLaunchKernelGGL((conv1x1_kernel<T, 128, 128, BS_REC>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
-          else hipLaunchKernelGGL((conv1x1_kernel<T, 128, 64, BS_REC>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+          if (BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_REC>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+          else hipLaunchKernelGGL((conv_glds_kernel<T, 128, 64, BS_REC>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
         }
         return;
       }
-      if (BP == 256 && BN == 128) hipLaunchKernelGGL((conv1x1_kernel<T, 256, 128>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
-      else if (BP == 256) hipLaunchKernelGGL((conv1x1_kernel<T, 256, 64>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
-      else if (BN == 128) hipLaunchKernelGGL((conv1x1_kernel<T, 128, 128>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
-      else hipLaunchKernelGGL((conv1x1_kernel<T, 128, 64>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+      if (!(g.R == 1 && g.S == 1 && g.pad == 0)) {  // KxK: tap-walking loader (128-pixel tiles)
+        if (BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_NONE, true>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        else hipLaunchKernelGGL((conv_glds_kernel<T, 128, 64, BS_NONE, true>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        return;
+      }
+      if (BP == 256 && BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 256, 128>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+      else if (BP == 256) hipLaunchKernelGGL((conv_glds_kernel<T, 256, 64>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+      else if (BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+      else hipLaunchKernelGGL((conv_glds_kernel<T, 128, 64>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
     };
     if (x.scalar_type() == at::kBFloat16) launch(__hip_bfloat16{}); else launch(__half{});
     DPA_CHECK_LAUNCH();
@@ -1681,6 +1786,7 @@ void register_conv_igemm(pybind11::module& m) {
   s.def("pack_weights", &igemm::pack_weights);
   s.def("wgrad_splits", &igemm::wgrad_splits);
   s.def("wgrad_config", &igemm::wgrad_config, pybind11::arg("glds") = -1);
+  s.def("g3x3_config", &igemm::g3x3_config, pybind11::arg("on") = -1);
   s.def("stat_defer_config", &igemm::stat_defer_config, pybind11::arg("min_blocks") = -2);
   s.def("g1x1_config", &igemm::g1x1_config, pybind11::arg("on") = -1, pybind11::arg("bp") = -1,
         pybind11::arg("min256") = -1);

@@ -17,7 +17,7 @@ Execution on a HIP device (``fused=True``): activations are bf16/f16/f32
   * backward: every weight gradient and every 3x3 data gradient (stride 1, and
     stride 2 as four output-parity sub-convolutions) run on the implicit-GEMM
     kernel; 1x1 forwards and data gradients run on the glds-staged 1x1 GEMM kernel
-    (conv1x1_kernel: 128-pixel tiles, operands global -> LDS by LDS-DMA).  A
+    (conv_glds_kernel: 128-pixel tiles, operands global -> LDS by LDS-DMA).  A
     projection block's two input gradients (conv1 and downsample) are combined in
     the conv epilogue instead of by a separate add;
   * every BatchNorm runs on the native NHWC kernels with its ReLU and, for the

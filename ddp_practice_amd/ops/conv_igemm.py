@@ -47,7 +47,7 @@ def usable(x: torch.Tensor, weight: torch.Tensor, cdtype: torch.dtype) -> bool:
             and bool(_K().supported(weight.shape[1], weight.shape[0])))
 
 
-G1X1 = os.environ.get("DPA_G1X1", "1") != "0"  # 1x1 convs on conv1x1_kernel (0: general kernel, A/B)
+G1X1 = os.environ.get("DPA_G1X1", "1") != "0"  # 1x1 convs on conv_glds_kernel (0: general kernel, A/B)
 
 
 def dgrad_1x1_here(K: int, OH: int) -> bool:

@@ -34,7 +34,8 @@ def timeit(fn, n=20):
 
 tot_me = tot_ref = tot_wme = tot_wref = tot_wold = 0.0
 from ddp_practice_amd.ops.conv_igemm import conv_wgrad  # noqa: E402
-print(f"{'shape':34s} {'GFLOP':>7s} {'mine us':>8s} {'TF/s':>6s} {'nostat':>7s} {'ref us':>8s} {'TF/s':>6s}")
+print(f"{'shape':34s} {'GFLOP':>7s} {'mine us':>8s} {'TF/s':>6s} {'nostat':>7s} {'ref us':>8s} {'TF/s':>6s} "
+      "(gen: the register-staged kernel for KxK)")
 for Cin, H, K, R, st, cnt in SHAPES:
     pad = R // 2
     x = torch.randn(B, Cin, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
@@ -47,6 +48,9 @@ for Cin, H, K, R, st, cnt in SHAPES:
     sts = torch.empty(3 * K + 4, device="cuda")
     shift = torch.zeros(K, device="cuda")
     fl = 2.0 * M * K * Cin * R * R / 1e9
+    prev3 = C.conv_igemm.g3x3_config(0)
+    t_gen = timeit(lambda: C.conv_igemm.conv_fwd(x, w, y, st, pad, part, tk, sts, shift, None))
+    C.conv_igemm.g3x3_config(prev3)
     t_me = timeit(lambda: C.conv_igemm.conv_fwd(x, w, y, st, pad, part, tk, sts, shift, None))
     t_ns = timeit(lambda: C.conv_igemm.conv_fwd(x, w, y, st, pad))
     if R == 1:
@@ -78,7 +82,7 @@ for Cin, H, K, R, st, cnt in SHAPES:
     tot_me += t_me * cnt
     tot_ref += t_ref * cnt
     print(f"{str((Cin, H, K, R, st)):34s} {fl:7.2f} {t_me:8.1f} {fl / t_me * 1e3:6.0f} {t_ns:7.1f} {t_ref:8.1f} "
-          f"{fl / t_ref * 1e3:6.0f}  err={err:.1e} | wgrad glds {t_wme:7.1f} reg {t_wold:7.1f} MIOpen {t_wref:7.1f} "
+          f"{fl / t_ref * 1e3:6.0f}  gen {t_gen:6.1f} err={err:.1e} | wgrad glds {t_wme:7.1f} reg {t_wold:7.1f} MIOpen {t_wref:7.1f} "
           f"err={werr:.1e} x{cnt}")
 print(f"network forward convs (x count): mine {tot_me:.0f} us, reference {tot_ref:.0f} us "
       "(mine includes the BN statistics; reference does not)")

@@ -1,4 +1,4 @@
-"""ResNet-50 (bs 128) 1x1 conv shapes: conv1x1_kernel (256- and 128-pixel tiles, +BN
+"""ResNet-50 (bs 128) 1x1 conv shapes: conv_glds_kernel (256- and 128-pixel tiles, +BN
 statistics) vs the general implicit-GEMM kernel vs hipBLASLt (torch.mm), with the error
 of each against an fp32 reference.  Forward shapes and the data-gradient GEMMs
 (dX[P, Cin] = dY[P, Cout] @ W: the 1x1 conv Cout -> Cin on dy, stride 1).

@@ -226,7 +226,7 @@ def test_projection_block_shared_input_grad(C, stride, order):
     (8, 64, 56, 56, 64, 1),     # many pixel tiles: two-level statistics tree
 ])
 def test_conv1x1_glds_kernel_tiles(C, bp, shape):
-    """conv1x1_kernel (glds-staged 1x1 GEMM) with each pixel tile forced == fp32 torch:
+    """conv_glds_kernel (glds-staged 1x1 GEMM) with each pixel tile forced == fp32 torch:
     output, fused BN statistics (tickets re-armed), accumulate and the even-pixel aux add."""
     K_ = C.conv_igemm
     prev = K_.g1x1_config(1, bp)
@@ -259,14 +259,17 @@ def test_conv1x1_glds_kernel_tiles(C, bp, shape):
 @pytest.mark.parametrize("shape", [
     (2, 64, 14, 14, 64, 3, 1, 1),     # general kernel, 3x3
     (3, 64, 7, 7, 256, 1, 1, 0),      # 1x1 kernel, ragged M
-    (8, 64, 56, 56, 64, 1, 1, 0),     # 1x1, two-level tree
+    (8, 64, 56, 56, 64, 1, 1, 0),     # 1x1, 196 pixel tiles: one-level reduction
+    (12, 64, 56, 56, 64, 1, 1, 0),    # 294 pixel tiles: two-level tree
     (2, 128, 15, 15, 128, 3, 2, 1),   # general kernel, stride 2
 ])
-def test_conv_fwd_deferred_statistics(C, shape):
-    """StatArgs.defer: the conv stores its level-1 partial rows and stat_tree_kernel runs
-    the tree after the launch -- same statistics, tickets re-armed."""
+@pytest.mark.parametrize("defer_min", [0, -1])
+def test_conv_fwd_deferred_statistics(C, shape, defer_min):
+    """StatArgs.defer (defer_min 0, the default): the conv stores its level-1 partial rows
+    and a reduction launch (one or two levels) follows; defer_min -1: the in-launch ticket
+    tree -- same statistics, tickets re-armed."""
     K_ = C.conv_igemm
-    prev = K_.stat_defer_config(0)  # defer every statistics launch
+    prev = K_.stat_defer_config(defer_min)
     try:
         _run(C, *shape, torch.bfloat16, True)
     finally:
@@ -306,7 +309,8 @@ def test_conv_wgrad_glds_matches_register_staged(C, shape):
 
 
 @pytest.mark.parametrize("act", [1, 2])
-@pytest.mark.parametrize("shape", [(2, 128, 14, 14, 64), (3, 64, 7, 7, 256), (2, 256, 28, 28, 128)])
+@pytest.mark.parametrize("shape", [(2, 128, 14, 14, 64), (3, 64, 7, 7, 256), (2, 256, 28, 28, 128),
+                                   (12, 64, 56, 56, 64)])
 def test_dgrad_epilogue_bn_backward_sums(C, act, shape):
     """1x1 data gradient with the producing BatchNorm's backward sums in its epilogue
     (ops/conv_igemm.dgrad_bn, kernel BS modes): dx == fp32 torch (accumulated onto the
@@ -355,3 +359,22 @@ def test_dgrad_epilogue_bn_backward_sums(C, act, shape):
     assert ((out[:Cc] - s1).abs() / scale).max() < 1e-4
     assert ((out[Cc:] - s2).abs() / scale).max() < 1e-4
     assert torch.equal(dbeta, out[:Cc]) and torch.equal(dgamma, out[Cc:])
+
+
+@pytest.mark.parametrize("on", [0, 1])
+@pytest.mark.parametrize("shape", [
+    (2, 64, 14, 14, 64, 3, 1, 1),     # 3x3 s1 p1: padding taps read the zero page
+    (2, 128, 15, 15, 128, 3, 2, 1),   # 3x3 s2, odd input
+    (1, 192, 9, 9, 192, 3, 1, 1),     # Cout = 192: 64-channel tiles
+    (2, 64, 12, 12, 128, 5, 1, 2),    # 5x5
+])
+def test_conv_kxk_glds_and_register_kernels(C, on, shape):
+    """KxK convs on the glds kernel (on = 1, the default) and on the register-staged
+    general kernel (on = 0) == fp32 torch, with statistics."""
+    K_ = C.conv_igemm
+    prev = K_.g3x3_config(on)
+    try:
+        _run(C, *shape, torch.bfloat16, True)
+        _run(C, *shape, torch.float16, False)
+    finally:
+        K_.g3x3_config(prev)
