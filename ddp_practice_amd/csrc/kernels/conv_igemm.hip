@@ -1542,9 +1542,10 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
   const bool bwdst = bn_x.has_value();
   TORCH_CHECK(!(st && accumulate), "conv_fwd: statistics of an accumulated output are not supported");
   if (bwdst) {
-    TORCH_CHECK(mode == MODE_GEN && g.R == 1 && g.S == 1 && g.pad == 0 && g.stride == 1 && g1x1_enabled() &&
-                    x.numel() < (1LL << 31) && w.numel() < (1LL << 31),
-                "conv_fwd: BN backward sums need the 1x1 / stride-1 kernel");
+    TORCH_CHECK(mode == MODE_GEN && g.stride == 1 && g1x1_enabled() && x.numel() < (1LL << 31) &&
+                    w.numel() < (1LL << 31) && ((g.R == 1 && g.S == 1 && g.pad == 0) || g3x3_enabled()),
+                "conv_fwd: BN backward sums need the LDS-DMA kernel (stride 1)");
+    TORCH_CHECK(bn_y.has_value() || !accumulate, "conv_fwd: recomputed-mask BN sums on an accumulated output");
     TORCH_CHECK(!st && !aux.has_value() && part.has_value() && tickets.has_value(),
                 "conv_fwd: BN backward sums take part / tickets and no forward statistics / aux");
     TORCH_CHECK(accumulate == bn_y.has_value(), "conv_fwd: bn_y (ReLU after a residual) goes with accumulate");
@@ -1612,7 +1613,11 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
         bs.save = bn_save->data_ptr<float>();
         bs.gamma = bn_gamma.has_value() ? bn_gamma->data_ptr<float>() : nullptr;
         bs.beta = bn_beta.has_value() ? bn_beta->data_ptr<float>() : nullptr;
-        if (bn_y.has_value()) {
+        if (!(g.R == 1 && g.S == 1 && g.pad == 0)) {  // KxK data gradient (recomputed ReLU mask)
+          TORCH_CHECK(!bn_y.has_value(), "conv_fwd: KxK BN sums take the recomputed mask");
+          if (BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_REC, true>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+          else hipLaunchKernelGGL((conv_glds_kernel<T, 128, 64, BS_REC, true>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        } else if (bn_y.has_value()) {
           if (BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_Y>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
           else hipLaunchKernelGGL((conv_glds_kernel<T, 128, 64, BS_Y>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
         } else {

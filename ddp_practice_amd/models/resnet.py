@@ -43,6 +43,10 @@ from ..ops.conv_nhwc import conv_nhwc
 
 _PACKS: dict = {}  # id(module) -> this forward's packed filters (ops/conv_igemm.WeightPack)
 _FUSE_BN_BWD = os.environ.get("DPA_FUSE_BN_BWD", "1") != "0"  # BNTap hand-off (0: own bwd_stats pass, A/B)
+# bn1 -> the 3x3 conv2's data gradient: off by default -- the 3x3 epilogue's extra cost
+# (+281 us over 13 launches) cancels the bwd_stats pass it removes (-297 us),
+# profiles/r3s2h_resnet50_steady_bn1_fused.txt
+_FUSE_BN1 = os.environ.get("DPA_FUSE_BN1", "0") == "1"
 
 
 def _conv(x: torch.Tensor, conv: nn.Conv2d, cdtype: torch.dtype, bn: nn.Module | None = None, tap=None,
@@ -58,8 +62,8 @@ def _conv(x: torch.Tensor, conv: nn.Conv2d, cdtype: torch.dtype, bn: nn.Module |
         return conv1x1(x, conv.weight, conv.stride[0], cdtype, tap, want, pk, xtap, btap)
     if conv.bias is None and conv.groups == 1 and conv.dilation == (1, 1):
         if want is None:
-            return conv_nhwc(x, conv.weight, conv.stride, conv.padding, cdtype, None, pk), None
-        return conv_nhwc(x, conv.weight, conv.stride, conv.padding, cdtype, want, pk)
+            return conv_nhwc(x, conv.weight, conv.stride, conv.padding, cdtype, None, pk, btap), None
+        return conv_nhwc(x, conv.weight, conv.stride, conv.padding, cdtype, want, pk, btap)
     w = conv.weight.to(cdtype)
     out = F.conv2d(x, w, None if conv.bias is None else conv.bias.to(cdtype), conv.stride, conv.padding,
                    conv.dilation, conv.groups)
@@ -112,16 +116,18 @@ class Bottleneck(nn.Module):
         # folds the other's product into its own, ops/conv1x1.Conv1x1Fn)
         tap = GradTap() if (grad_x and self.downsample is None) else None
         xtap = GradTap() if (grad_x and self.downsample is not None) else None
-        # BN backward sums taken by the consuming 1x1 conv's data-gradient epilogue
+        # BN backward sums taken by the consuming conv's data-gradient epilogue
         # (ops/bn_nhwc.BNTap): bn2 -> conv3, and the previous block's bn3 -> this conv1
-        # when this is an identity block (its dgrad then holds the whole gradient of x)
+        # when this is an identity block (its dgrad then holds the whole gradient of x);
+        # bn1 -> conv2 (stride 1) with DPA_FUSE_BN1=1
         bt_in = getattr(x, "_dpa_btap", None) if tap is not None else None
+        bt1 = BNTap() if train and _FUSE_BN1 and self.conv2.stride == (1, 1) else None
         bt2 = BNTap() if train and _FUSE_BN_BWD else None
         bt3 = BNTap() if train and _FUSE_BN_BWD else None
         # each conv hands the following BN its batch statistics (ops/conv_igemm.py)
         c1, st = _conv(x, self.conv1, cdtype, self.bn1, tap, xtap, bt_in)
-        out = bn_act(c1, self.bn1, relu=True, comm=_comm_of(self.bn1), stats=st)
-        c2, st = _conv(out, self.conv2, cdtype, self.bn2)
+        out = bn_act(c1, self.bn1, relu=True, comm=_comm_of(self.bn1), stats=st, btap=bt1)
+        c2, st = _conv(out, self.conv2, cdtype, self.bn2, btap=bt1)
         out = bn_act(c2, self.bn2, relu=True, comm=_comm_of(self.bn2), stats=st, btap=bt2)
         identity = x
         if self.downsample is not None:

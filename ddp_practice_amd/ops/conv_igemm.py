@@ -87,15 +87,20 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn=None, a
     return y, stats
 
 
-def dgrad_bn(dy: torch.Tensor, wt: torch.Tensor, bt, acc: torch.Tensor | None = None) -> torch.Tensor | None:
-    """1x1 / stride-1 data gradient dx = conv(dy, wt) (+= acc, the tapped residual gradient)
-    whose epilogue also takes the backward sums of the BatchNorm that produced the conv's
-    input (``bt``: ops/bn_nhwc.BNTap, filled by that BN's forward).  Stores the sums in
+def dgrad_bn(dy: torch.Tensor, wt: torch.Tensor, bt, acc: torch.Tensor | None = None,
+             pad: int = 0) -> torch.Tensor | None:
+    """Stride-1 data gradient dx = conv(dy, wt, pad) (+= acc, the tapped residual gradient;
+    1x1 only) whose epilogue also takes the backward sums of the BatchNorm that produced the
+    conv's input (``bt``: ops/bn_nhwc.BNTap, filled by that BN's forward).  ``wt``: the
+    flipped transposed filter, ``pad`` = R - 1 - the forward padding.  Stores the sums in
     ``bt`` and returns dx; None when the shapes do not allow it (the BN then runs its own
     statistics pass)."""
     if bt is None or bt.x is None or not G1X1:
         return None
     if (acc is None) != (bt.act == 2):  # act 1 (ReLU after a residual add) <-> accumulated dx
+        return None
+    R, S = wt.shape[2], wt.shape[3]
+    if (R, S) != (1, 1) and (acc is not None or 2 * pad != R - 1 or R != S):
         return None
     N, _, H, W = dy.shape
     C = wt.shape[0]
@@ -108,7 +113,7 @@ def dgrad_bn(dy: torch.Tensor, wt: torch.Tensor, bt, acc: torch.Tensor | None = 
     part, tickets = _StatWS.get(dy.device, N * H * W, C)
     out, dgamma, dbeta = torch.empty(2 * C, **f32), torch.empty(C, **f32), torch.empty(C, **f32)
     dx = acc if acc is not None else torch.empty(shape, dtype=dy.dtype, device=dy.device, memory_format=_CL)
-    _K().conv_fwd(dy, wt, dx, 1, 0, part, tickets, accumulate=acc is not None, bn_x=bt.x,
+    _K().conv_fwd(dy, wt, dx, 1, pad, part, tickets, accumulate=acc is not None, bn_x=bt.x,
                   bn_y=bt.y if bt.act == 1 else None, bn_save=bt.save, bn_gamma=bt.weight, bn_beta=bt.bias,
                   bn_out=out, bn_dgamma=dgamma, bn_dbeta=dbeta)
     bt.sums = (out, dgamma, dbeta)

@@ -23,7 +23,7 @@ _CL = torch.channels_last
 
 class ConvNHWCFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride, padding, cdtype: torch.dtype, bn=None, packed=None):
+    def forward(ctx, x, weight, stride, padding, cdtype: torch.dtype, bn=None, packed=None, btap=None):
         x = x if x.is_contiguous(memory_format=_CL) else x.contiguous(memory_format=_CL)
         if packed is not None:  # this step's filters from ops/conv_igemm.WeightPack
             w = packed[0]
@@ -31,6 +31,7 @@ class ConvNHWCFn(torch.autograd.Function):
             w = torch.empty(weight.shape, dtype=cdtype, device=weight.device, memory_format=_CL)
             w.copy_(weight)  # fp32 NCHW -> cdtype NHWC in one kernel
         ctx.wt = packed[1] if packed is not None else None
+        ctx.btap = btap  # ops/bn_nhwc.BNTap of the BN that produced x (stride-1 dgrad takes its sums)
         stats = None
         if (_igemm.usable(x, weight, cdtype) and stride[0] == stride[1] and padding[0] == padding[1]):
             # hand-written implicit GEMM (+ the next BN's statistics in its epilogue)
@@ -67,7 +68,9 @@ class ConvNHWCFn(torch.autograd.Function):
             if wt is None:
                 wt = torch.empty((w.shape[1], w.shape[0], R, R), dtype=w.dtype, device=w.device, memory_format=_CL)
                 wt.copy_(w.flip(2, 3).transpose(0, 1))
-            dx, _ = _igemm.conv_fwd(dy, wt, 1, R - 1 - padding[0])
+            dx = _igemm.dgrad_bn(dy, wt, ctx.btap, None, R - 1 - padding[0])
+            if dx is None:
+                dx, _ = _igemm.conv_fwd(dy, wt, 1, R - 1 - padding[0])
         elif (ctx.needs_input_grad[0] and stride == [2, 2] and padding == [1, 1] and tuple(w.shape[2:]) == (3, 3)
               and _igemm.usable(dy, w.transpose(0, 1), w.dtype)):
             # stride-2 data gradient: four output-parity sub-convolutions in one launch
@@ -91,10 +94,14 @@ class ConvNHWCFn(torch.autograd.Function):
             if dw2 is not None:
                 dw = torch.empty(dw2.shape, dtype=ctx.wdtype, device=dw2.device)
                 dw.copy_(dw2)  # cdtype NHWC -> fp32 NCHW in one kernel
-        return dx, dw, None, None, None, None, None
+        ctx.btap = None
+        return dx, dw, None, None, None, None, None, None
 
 
-def conv_nhwc(x: torch.Tensor, weight: torch.Tensor, stride, padding, cdtype: torch.dtype, bn=None, packed=None):
+def conv_nhwc(x: torch.Tensor, weight: torch.Tensor, stride, padding, cdtype: torch.dtype, bn=None, packed=None,
+              btap=None):
     """Bias-free conv of channels_last ``x`` with the fp32 ``weight`` in ``cdtype``.  With
-    ``bn`` (the training BatchNorm that follows): returns (output, its statistics or None)."""
-    return ConvNHWCFn.apply(x, weight, tuple(stride), tuple(padding), cdtype, bn, packed)
+    ``bn`` (the training BatchNorm that follows): returns (output, its statistics or None).
+    ``btap``: the ops/bn_nhwc.BNTap of the BN that produced ``x`` (a stride-1 data gradient
+    then also takes that BN's backward sums)."""
+    return ConvNHWCFn.apply(x, weight, tuple(stride), tuple(padding), cdtype, bn, packed, btap)

@@ -308,10 +308,10 @@ def test_conv_wgrad_glds_matches_register_staged(C, shape):
     assert err < 1e-2, err
 
 
-@pytest.mark.parametrize("act", [1, 2])
+@pytest.mark.parametrize("act,R", [(1, 1), (2, 1), (2, 3)])
 @pytest.mark.parametrize("shape", [(2, 128, 14, 14, 64), (3, 64, 7, 7, 256), (2, 256, 28, 28, 128),
                                    (12, 64, 56, 56, 64)])
-def test_dgrad_epilogue_bn_backward_sums(C, act, shape):
+def test_dgrad_epilogue_bn_backward_sums(C, act, R, shape):
     """1x1 data gradient with the producing BatchNorm's backward sums in its epilogue
     (ops/conv_igemm.dgrad_bn, kernel BS modes): dx == fp32 torch (accumulated onto the
     tapped residual gradient for act 1) and S1 = sum dz, S2 = sum dz * xhat of the STORED
@@ -323,7 +323,7 @@ def test_dgrad_epilogue_bn_backward_sums(C, act, shape):
     g = torch.Generator().manual_seed(41 + act + Cc)
     bf = dict(device=DEV, dtype=torch.bfloat16)
     dy = torch.randn(N, K, H, W, generator=g).to(**bf).contiguous(memory_format=CL)
-    wt = (torch.randn(Cc, K, 1, 1, generator=g) / K ** 0.5).to(**bf).contiguous(memory_format=CL)
+    wt = (torch.randn(Cc, K, R, R, generator=g) / (K * R * R) ** 0.5).to(**bf).contiguous(memory_format=CL)
     x = torch.randn(N, Cc, H, W, generator=g).to(**bf).contiguous(memory_format=CL)
     mean = torch.randn(Cc, generator=g) * 0.1
     invstd = torch.rand(Cc, generator=g) + 0.5
@@ -337,9 +337,9 @@ def test_dgrad_epilogue_bn_backward_sums(C, act, shape):
         bt.y = torch.randn(N, Cc, H, W, generator=g).to(**bf).contiguous(memory_format=CL)
         acc = torch.randn(N, Cc, H, W, generator=g).to(**bf).contiguous(memory_format=CL)
     acc0 = acc.clone() if acc is not None else None
-    dx = dgrad_bn(dy, wt, bt, acc)
+    dx = dgrad_bn(dy, wt, bt, acc, R // 2)
     assert dx is not None and bt.sums is not None and bt.grad_ptr == dx.data_ptr()
-    ref = F.conv2d(dy.float(), wt.float())
+    ref = F.conv2d(dy.float(), wt.float(), None, 1, R // 2)
     if acc0 is not None:
         ref = ref + acc0.float()
     err = ((dx.float() - ref).abs().max() / ref.abs().max()).item()
