@@ -476,7 +476,7 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
 //     vmcnt(0) before each K-step's first LDS read, cdna_hip_programming.md §5);
 //   * the epilogue of the general kernel: rounded tile staged through LDS, the next
 //     BN's statistics tree, whole-row stores, accumulate / aux for the fused gradients.
-template <typename T, int BP, int BN>
+template <typename T, int BP, int BN, int NS = 2>
 struct G1x1Lds {
   static constexpr int STAGE = (BP + BN) * BK;            // elements per buffer
   static constexpr int RS = BN + 8;                       // epilogue tile row stride
@@ -485,7 +485,7 @@ struct G1x1Lds {
   static constexpr int FLAG = RED + 4 * 2 * BN * 4;       // int s_flag
   static constexpr int SCR = FLAG + 16;                   // float scr[THR]
   static constexpr int EPI = SCR + THR * 4;
-  static constexpr int MAIN = 2 * STAGE * (int)sizeof(T);
+  static constexpr int MAIN = NS * STAGE * (int)sizeof(T);
   static constexpr int SHIFT = MAIN > EPI ? MAIN : EPI;  // float shift[BN] (statistics only)
   static constexpr int BWC = SHIFT + BN * 4;              // float mean|invstd|gamma|beta [4][BN] (BS)
   static constexpr int BYTES = BWC + 4 * BN * 4;
@@ -504,12 +504,16 @@ __device__ __forceinline__ void glds16(const void* src, void* dst) {
 // zero-fill; its per-lane source address can point here instead)
 __device__ __attribute__((aligned(16))) unsigned char g_zero16[16] = {0};
 
-template <typename T, int BP, int BN, int BS = BS_NONE, bool KXK = false>
+// NS = 3 (DPA_GLDS_STAGES=3): three LDS buffers, two tiles in flight across every barrier --
+// the wait is a counted vmcnt (this wave's DMAs of the newest tile stay outstanding) and the
+// barrier a raw s_barrier (__syncthreads() would add vmcnt(0)); one workgroup per CU (96 KB).
+template <typename T, int BP, int BN, int BS = BS_NONE, bool KXK = false, int NS = 2>
 __global__ void __launch_bounds__(THR)
 conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__ y, StatArgs sa, Geom g,
                BwdStatArgs<T> bs) {
   using MMT = MM<T>;
-  using L = G1x1Lds<T, BP, BN>;
+  using L = G1x1Lds<T, BP, BN, NS>;
+  static_assert(NS == 2 || (NS == 3 && BS == BS_NONE), "three stages: forward / plain data gradients only");
   typedef typename MMT::frag frag;
   constexpr int CT = BN / 32;  // 16-channel tiles per wave
   constexpr int PT = BP / 32;  // 16-pixel tiles per wave
@@ -623,11 +627,23 @@ conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict
     }
   }
   issue(0, 0);
+  if (NS == 3 && KT > 1) issue(1, 1);
+  int buf = 0;
   for (int kt = 0; kt < KT; ++kt) {
-    const int buf = kt & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's share of tile kt has landed
-    __syncthreads();  // ... every wave's, and tile kt-1 (the other buffer) is no longer read
-    if (kt + 1 < KT) issue(kt + 1, buf ^ 1);
+    if constexpr (NS == 2) {
+      buf = kt & 1;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's share of tile kt has landed
+      __syncthreads();  // ... every wave's, and tile kt-1 (the other buffer) is no longer read
+      if (kt + 1 < KT) issue(kt + 1, buf ^ 1);
+    } else {
+      // tile kt landed (tile kt+1's WR + AR DMAs of this wave may still be in flight);
+      // the barrier orders every wave's DMAs of tile kt before any read, and every wave's
+      // reads of buffer (kt+2)%3 (= tile kt-1, done: its MFMAs have issued) before refill
+      if (kt + 1 < KT) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WR + AR) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + 2 < KT) issue(kt + 2, buf == 0 ? 2 : buf - 1);
+    }
     const T* A = lds + buf * L::STAGE;  // filter rows [0, BN)
     const T* B = A + BN * BK;           // pixel rows [0, BP)
 #pragma unroll
@@ -644,6 +660,7 @@ conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict
 #pragma unroll
         for (int b = 0; b < PT; ++b) acc[a][b] = MMT::mma(fa[a], fb[b], acc[a][b]);
     }
+    if constexpr (NS == 3) buf = buf == 2 ? 0 : buf + 1;
   }
   __syncthreads();  // the last tile is read: the buffers become the epilogue's tile
   // ---- epilogue (conv_fwd_kernel's, for a BP-pixel tile) ----
@@ -1398,6 +1415,23 @@ static bool g1x1_enabled() {
   return g_g1x1_on != 0;
 }
 
+// LDS buffers of conv_glds_kernel (forward / plain data gradients): 2 (default) or 3
+// (DPA_GLDS_STAGES=3; glds_config(stages) at run time)
+static int g_glds_stages = -1;
+static int glds_stages() {
+  if (g_glds_stages < 0) {
+    const char* e = std::getenv("DPA_GLDS_STAGES");
+    g_glds_stages = e != nullptr && std::atoi(e) == 3 ? 3 : 2;
+  }
+  return g_glds_stages;
+}
+int64_t glds_config(int64_t stages) {
+  glds_stages();
+  const int64_t prev = g_glds_stages;
+  if (stages == 2 || stages == 3) g_glds_stages = (int)stages;
+  return prev;
+}
+
 // KxK convs (any stride / padding) on the glds kernel too (DPA_G3X3=0: 1x1 only, A/B runs)
 static int g_g3x3_on = -1;
 static bool g3x3_enabled() {
@@ -1626,7 +1660,15 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
         }
         return;
       }
-      if (!(g.R == 1 && g.S == 1 && g.pad == 0)) {  // KxK: tap-walking loader (128-pixel tiles)
+      const bool kxk = !(g.R == 1 && g.S == 1 && g.pad == 0);
+      if (glds_stages() == 3 && BP == 128) {  // three LDS buffers (one workgroup per CU)
+        if (kxk && BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_NONE, true, 3>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        else if (kxk) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 64, BS_NONE, true, 3>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        else if (BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_NONE, false, 3>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        else hipLaunchKernelGGL((conv_glds_kernel<T, 128, 64, BS_NONE, false, 3>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        return;
+      }
+      if (kxk) {  // KxK: tap-walking loader (128-pixel tiles)
         if (BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_NONE, true>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
         else hipLaunchKernelGGL((conv_glds_kernel<T, 128, 64, BS_NONE, true>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
         return;
@@ -1792,6 +1834,7 @@ void register_conv_igemm(pybind11::module& m) {
   s.def("wgrad_splits", &igemm::wgrad_splits);
   s.def("wgrad_config", &igemm::wgrad_config, pybind11::arg("glds") = -1);
   s.def("g3x3_config", &igemm::g3x3_config, pybind11::arg("on") = -1);
+  s.def("glds_config", &igemm::glds_config, pybind11::arg("stages") = -1);
   s.def("stat_defer_config", &igemm::stat_defer_config, pybind11::arg("min_blocks") = -2);
   s.def("g1x1_config", &igemm::g1x1_config, pybind11::arg("on") = -1, pybind11::arg("bp") = -1,
         pybind11::arg("min256") = -1);

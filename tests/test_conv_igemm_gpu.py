@@ -378,3 +378,44 @@ def test_conv_kxk_glds_and_register_kernels(C, on, shape):
         _run(C, *shape, torch.float16, False)
     finally:
         K_.g3x3_config(prev)
+
+
+@pytest.mark.parametrize("shape", [
+    (3, 64, 7, 7, 256, 1, 1, 0),      # 1x1, ragged M, one K-step (no second tile in flight)
+    (2, 256, 14, 14, 128, 1, 2, 0),   # 1x1 stride 2, 4 K-steps
+    (4, 1024, 7, 7, 64, 1, 1, 0),     # 1x1, 16 K-steps, 64-channel tiles
+    (2, 128, 15, 15, 128, 3, 2, 1),   # 3x3 stride 2: 18 K-steps through the zero page
+    (2, 64, 14, 14, 64, 3, 1, 1),     # 3x3, 9 K-steps
+])
+def test_conv_glds_three_stage_pipeline_bitwise(C, shape):
+    """conv_glds_kernel with three LDS buffers (two tiles in flight across a raw barrier)
+    == the two-buffer loop bit for bit (same tiles, same MFMA order), statistics included."""
+    K_ = C.conv_igemm
+    N, Cin, H, W, K, R, stride, pad = shape
+    g = torch.Generator().manual_seed(53 + K)
+    x = torch.randn(N, Cin, H, W, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=CL)
+    w = (torch.randn(K, Cin, R, R, generator=g) / (Cin * R * R) ** 0.5).to(DEV, torch.bfloat16).contiguous(
+        memory_format=CL)
+    OH = (H + 2 * pad - R) // stride + 1
+    M = N * OH * OH
+    outs = []
+    prev = K_.glds_config(2)
+    try:
+        for stages in (2, 3, 2, 3):
+            K_.glds_config(stages)
+            y = torch.empty(N, K, OH, OH, dtype=torch.bfloat16, device=DEV, memory_format=CL)
+            part = torch.empty(K_.stat_part_len(M, K), device=DEV)
+            tk = torch.zeros(K_.stat_tickets_len(M, K), dtype=torch.int32, device=DEV)
+            st = torch.empty(3 * K + 4, device=DEV)
+            K_.conv_fwd(x, w, y, stride, pad, part, tk, st, torch.zeros(K, device=DEV), None)
+            torch.cuda.synchronize()
+            outs.append((y, st))
+    finally:
+        K_.glds_config(prev)
+    def defined(st):  # [sums | sumsq | rows], shift copy (the 3 floats between are padding)
+        return torch.cat([st[:2 * K + 1], st[2 * K + 4:3 * K + 4]])
+
+    for y, st in outs[1:]:
+        assert torch.equal(y, outs[0][0]) and torch.equal(defined(st), defined(outs[0][1]))
+    ref = F.conv2d(x.float(), w.float(), None, stride, pad)
+    assert ((outs[1][0].float() - ref).abs().max() / ref.abs().max()).item() < 2e-2
