@@ -1222,37 +1222,44 @@ conv_wgrad_glds_kernel(const T* __restrict__ dy, const T* __restrict__ x, float*
       }
 }
 
+constexpr int WR_QC = 16;  // float4 columns per wgrad_reduce_kernel workgroup
+
 // grad[k][c][r][s] (fp32 OIHW) = sum over splits of slab[sp][k][(r*S + s)*C + c]:
-// a workgroup owns 256 consecutive slab columns as 64 float4 quads x 4 split groups
+// a workgroup owns 64 consecutive slab columns as 16 float4 quads x 16 split groups
 // (every 4th split, fixed order, 4 loads in flight), combined through LDS in group
 // order, written in the OIHW order of a [K][Cd][Rd][Sd] gradient (Cd <= C, Rd <= R,
 // Sd <= S: the stem's padded columns are dropped here).
 __global__ void __launch_bounds__(256)
 wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ grad, int splits, int K, int C, int R, int S,
                     int Cd, int Rd, int Sd) {
-  __shared__ f32x4 part[4][64];
+  // 16 float4 columns x 16 split groups per workgroup (was 64 x 4: a grid of ~150
+  // workgroups whose lanes each waited ~6 dependent rounds of 4 loads)
+  constexpr int QC = WR_QC, SG = 256 / WR_QC;
+  __shared__ f32x4 part[SG][QC];
   const long long RSC = (long long)R * S * C, total = (long long)K * RSC;
-  const int qd = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const long long col = (blockIdx.x * 64LL + qd) * 4;  // total % 4 == 0 (C % 64 == 0)
+  const int qd = threadIdx.x % QC, rg = threadIdx.x / QC;
+  const long long col = (blockIdx.x * (long long)QC + qd) * 4;  // total % 4 == 0 (C % 64 == 0)
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (col < total) {
     int sp = rg;
-    for (; sp + 12 < splits; sp += 16) {
+    for (; sp + 3 * SG < splits; sp += 4 * SG) {
       const f32x4 a = *reinterpret_cast<const f32x4*>(slab + (long long)sp * total + col);
-      const f32x4 b = *reinterpret_cast<const f32x4*>(slab + (long long)(sp + 4) * total + col);
-      const f32x4 c = *reinterpret_cast<const f32x4*>(slab + (long long)(sp + 8) * total + col);
-      const f32x4 d = *reinterpret_cast<const f32x4*>(slab + (long long)(sp + 12) * total + col);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(slab + (long long)(sp + SG) * total + col);
+      const f32x4 c = *reinterpret_cast<const f32x4*>(slab + (long long)(sp + 2 * SG) * total + col);
+      const f32x4 d = *reinterpret_cast<const f32x4*>(slab + (long long)(sp + 3 * SG) * total + col);
       acc += a;
       acc += b;
       acc += c;
       acc += d;
     }
-    for (; sp < splits; sp += 4) acc += *reinterpret_cast<const f32x4*>(slab + (long long)sp * total + col);
+    for (; sp < splits; sp += SG) acc += *reinterpret_cast<const f32x4*>(slab + (long long)sp * total + col);
   }
   part[rg][qd] = acc;
   __syncthreads();
   if (rg == 0 && col < total) {
-    const f32x4 t = part[0][qd] + part[1][qd] + part[2][qd] + part[3][qd];
+    f32x4 t = part[0][qd];
+#pragma unroll
+    for (int gg = 1; gg < SG; ++gg) t += part[gg][qd];
     const int k = (int)(col / RSC);
     const long long n = col - (long long)k * RSC;  // (r*S + s)*C + c, c % 4 == 0
     const int c = (int)(n % C), rs = (int)(n / C), r = rs / S, s = rs - r * S;
@@ -1804,7 +1811,8 @@ void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor grad, int64_t stride, in
   if (x.scalar_type() == at::kBFloat16) launch(__hip_bfloat16{}); else launch(__half{});
   DPA_CHECK_LAUNCH();
   const long long total = (long long)g.K * RSC;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, cur_stream(),
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + 4 * WR_QC - 1) / (4 * WR_QC))), dim3(256), 0,
+                     cur_stream(),
                      slab.data_ptr<float>(), grad.data_ptr<float>(), (int)sp, g.K, g.C, SR, SS, Cd, Rd, Sd);
   DPA_CHECK_LAUNCH();
 }
