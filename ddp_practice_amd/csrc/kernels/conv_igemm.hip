@@ -1738,12 +1738,12 @@ int64_t wgrad_config(int64_t glds) {
 static int wtile(int64_t v) { return v % 128 == 0 ? 128 : 64; }
 
 int64_t wgrad_splits(int64_t M, int64_t K, int64_t C, int64_t R, int64_t S) {
-  // ~2-4 workgroups per CU, each at least 16 K-steps of 64 pixels, and the fp32
+  // ~2 workgroups per CU, each at least 16 K-steps of 64 pixels, and the fp32
   // partials at most ~48 MB (written and re-read once: ~12 us at HBM rate)
   const int64_t tiles = (K / wtile(K)) * (R * S * C / wtile(C));
   static const int64_t target = [] {
     const char* e = std::getenv("DPA_WGRAD_BLOCKS");
-    return e != nullptr ? std::atoll(e) : 768LL;
+    return e != nullptr ? std::atoll(e) : 512LL;  // ResNet-50 sweep: 384 15.01, 512 14.50, 768 14.59, 1024 14.67 ms
   }();
   static const int64_t minpix = [] {
     const char* e = std::getenv("DPA_WGRAD_MINPIX");
