@@ -1439,6 +1439,23 @@ int64_t glds_config(int64_t stages) {
   return prev;
 }
 
+// 128-channel tiles of conv_glds_kernel narrowed to 64 when the grid would have fewer than
+// this many workgroups (DPA_G1X1_BN64_BELOW; 0 = never; bn64_config at run time)
+static long long g_bn64_below = -1;
+static long long bn64_below() {
+  if (g_bn64_below < 0) {
+    const char* e = std::getenv("DPA_G1X1_BN64_BELOW");
+    g_bn64_below = e != nullptr ? std::atoll(e) : 0LL;
+  }
+  return g_bn64_below;
+}
+int64_t bn64_config(int64_t below) {
+  bn64_below();
+  const int64_t prev = g_bn64_below;
+  if (below >= 0) g_bn64_below = below;
+  return prev;
+}
+
 // KxK convs (any stride / padding) on the glds kernel too (DPA_G3X3=0: 1x1 only, A/B runs)
 static int g_g3x3_on = -1;
 static bool g3x3_enabled() {
@@ -1515,7 +1532,7 @@ int64_t stat_part_len(int64_t M, int64_t K) {
 }
 int64_t stat_tickets_len(int64_t M, int64_t K) {
   const int64_t rows = (M + BM - 1) / BM, ng = (rows + G1 - 1) / G1;
-  return (K / tile_n(K)) * (ng + 1);
+  return (K / 64) * (ng + 1);  // 64-channel tiles at most (conv_glds_kernel may narrow 128 -> 64)
 }
 
 // y: [N, K, OH, OW] channels_last (preallocated).  With `stats` (fp32 [3K+4], the
@@ -1624,11 +1641,13 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
     sa.shift = shift->data_ptr<float>();
     sa.nbt = nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr;
   }
-  const int BN = tile_n(g.K);
+  const int BN0 = tile_n(g.K);
   if (mode == MODE_GEN && g1x1_enabled() && x.numel() < (1LL << 31) && w.numel() < (1LL << 31) &&
       (g3x3_enabled() || (g.R == 1 && g.S == 1 && g.pad == 0))) {
-    // the glds-staged implicit-GEMM kernel (pixel tile 256 or 128, see g1x1_bp)
+    // the glds-staged implicit-GEMM kernel (pixel tile 256 or 128, see g1x1_bp; 64-channel
+    // tiles when 128-channel ones leave the grid below g_bn64_below workgroups)
     const int BP = (bwdst || !(g.R == 1 && g.S == 1 && g.pad == 0)) ? 128 : g1x1_bp(g.M, g.K);
+    const int BN = BN0 == 128 && BP == 128 && (g.M + 127) / 128 * (g.K / 128) < bn64_below() ? 64 : BN0;
     const long long blocks = (g.M + BP - 1) / BP * (g.K / BN);
     TORCH_CHECK(blocks < (1LL << 31), "conv_fwd: grid too large");
     sa.defer = st && defer_stats(blocks) ? 1 : 0;
@@ -1691,6 +1710,7 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
     return;
   }
   TORCH_CHECK(!bwdst, "conv_fwd: BN backward sums need the 1x1 kernel");
+  const int BN = BN0;
   const long long rows = (g.M + BM - 1) / BM;
   const long long blocks = rows * (g.K / BN) * (mode == MODE_S2T ? 4 : 1);
   TORCH_CHECK(blocks < (1LL << 31), "conv_fwd: grid too large");
@@ -1843,6 +1863,7 @@ void register_conv_igemm(pybind11::module& m) {
   s.def("wgrad_config", &igemm::wgrad_config, pybind11::arg("glds") = -1);
   s.def("g3x3_config", &igemm::g3x3_config, pybind11::arg("on") = -1);
   s.def("glds_config", &igemm::glds_config, pybind11::arg("stages") = -1);
+  s.def("bn64_config", &igemm::bn64_config, pybind11::arg("below") = -1);
   s.def("stat_defer_config", &igemm::stat_defer_config, pybind11::arg("min_blocks") = -2);
   s.def("g1x1_config", &igemm::g1x1_config, pybind11::arg("on") = -1, pybind11::arg("bp") = -1,
         pybind11::arg("min256") = -1);
