@@ -957,11 +957,20 @@ __global__ void __launch_bounds__(THR) stat_tree_kernel(StatArgs sa, long long M
 // writes the fp32 OIHW gradient directly (no separate layout/cast pass).
 typedef __attribute__((ext_vector_type(4))) short v4s;
 
+// With 8 chunks per row (128-B rows: 64-channel tiles) one 32-lane half reads rows
+// {0..3, 8..11} (+4, +32kk), the even ones in one bank half: their 4 chunk pairs must
+// differ, so the XOR there is 2*f8(row), f8 = bit 1 | bit 3 of the row (was 2*(row&3):
+// rows r and r+8 shared a pair, 2-way -- 1.6 conflict cycles per LDS instruction in the
+// 64-wide wgrad kernels, profiles/r3s2l_resnet50_pmc_pass1.txt).
+template <int CH>
+__device__ __forceinline__ int wswz_xor(int row) {
+  if constexpr (CH >= 16) return 2 * ((row & 3) | ((row >> 1) & 4));
+  return 2 * (((row >> 1) & 1) | ((row >> 2) & 2));
+}
+
 template <int CH>  // 16-B chunks per LDS row
 __device__ __forceinline__ int wswz(int row, int chunk) {
-  const int f = (row & 3) | ((row >> 1) & 4);
-  const int m = CH >= 16 ? 2 * f : 2 * (f & 3);
-  return row * CH * 8 + ((chunk ^ m) << 3);
+  return row * CH * 8 + ((chunk ^ wswz_xor<CH>(row)) << 3);
 }
 
 template <typename T, int BM, int BN, int MODE = MODE_GEN>
@@ -1104,11 +1113,6 @@ conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __re
 // past the split's end read a 16-B zero page instead of being zero-filled by the loader.
 // One barrier per 64-pixel step: wait the landed step (vmcnt(0)) + barrier, issue step
 // t+1 into the other buffer, MFMA on step t (as conv_glds_kernel).
-template <int CH>
-__device__ __forceinline__ int wswz_xor(int row) {
-  const int f = (row & 3) | ((row >> 1) & 4);
-  return CH >= 16 ? 2 * f : 2 * (f & 3);
-}
 
 template <typename T, int BM, int BN>
 __global__ void __launch_bounds__(THR)
