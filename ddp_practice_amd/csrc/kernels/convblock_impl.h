@@ -615,7 +615,16 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
   static_assert(PRO != 2 || MODE == 2, "PRO 2 is a data-grad prologue");
   static_assert(PRO != 3 || (CIN == 1 && MODE != 2), "PRO 3 gathers single-channel input images");
   static_assert(EPI == 0 || MODE == 2, "EPI 1 is a data-grad epilogue");
-  constexpr int HP = H + 4, WPD = W + 4;
+  constexpr int NCH = CIN >= 8 ? CIN / 8 : 1;              // 16-B groups per pixel
+#ifdef DPA_IMG_PAD8
+  // 32-B pixels (CIN 16): pad rows to W + 8 so a row wrap shifts the pixel index by a
+  // multiple of 8 (one 256-B bank row) and read unswizzled: the 16 lanes of a
+  // ds_read_b128 group then hit 16 distinct 16-B slots (experiment build)
+  constexpr bool PAD8 = NCH == 2;
+#else
+  constexpr bool PAD8 = false;
+#endif
+  constexpr int HP = H + 4, WPD = W + (PAD8 ? 8 : 4);
   constexpr int K = 25 * CIN;
   constexpr int KP = ceil_to(K, 32);
   constexpr int KS = KP / 32;
@@ -631,10 +640,9 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
   // pixels x one 16-B group; with a 32/64-B pixel pitch those 16 addresses would
   // share 8/4 bank groups (2/4-way conflicts), swizzled they hit 16 distinct ones
   // (conv2 dgrad: SQ_LDS_BANK_CONFLICT -54 %)
-  constexpr int NCH = CIN >= 8 ? CIN / 8 : 1;              // 16-B groups per pixel
   constexpr int PPB = NCH <= 16 ? 16 / NCH : 1;            // pixels per 256-B bank row
   auto imo = [](int px, int c) -> int {
-    if constexpr (NCH <= 1) {
+    if constexpr (NCH <= 1 || PAD8) {
       return px * CIN + c;
     } else {
       return px * CIN + ((((c >> 3) ^ ((px / PPB) & (NCH - 1)))) << 3) + (c & 7);
