@@ -866,12 +866,13 @@ conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict
 // workgroup (bn, grp) sums its group of G1 rows into a level-2 row, the last of a
 // channel tile's NG arrivals sums those into the final statistics.  Same association
 // as the in-launch tree: the result is bitwise the same.
-// One-level variant for grids of <= S1_MAXROWS pixel tiles (most convs past 28x28): a
+// One-level variant for grids of <= S1_MAXROWS pixel tiles (every ResNet-50 conv but the
+// 56x56 ones): a
 // workgroup of 1024 lanes owns S1_COLS of the 2*BN level-1 columns of one channel tile as
 // 16 row groups x 64 columns, each group with every row it sums in flight (16 loads),
 // combined in group order through LDS -- one dependent round trip instead of the two
 // levels' three (rows, ticket, level-2 rows).  Fixed order: deterministic.
-constexpr int S1_THR = 1024, S1_COLS = 64, S1_RG = S1_THR / S1_COLS, S1_MAXROWS = 256;
+constexpr int S1_THR = 1024, S1_COLS = 64, S1_RG = S1_THR / S1_COLS, S1_MAXROWS = 1024;
 template <int BN>
 __global__ void __launch_bounds__(S1_THR) stat_sum1_kernel(StatArgs sa, long long M, int BM_, int K) {
   __shared__ float part[S1_RG][S1_COLS];
