@@ -873,22 +873,23 @@ conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict
 // combined in group order through LDS -- one dependent round trip instead of the two
 // levels' three (rows, ticket, level-2 rows).  Fixed order: deterministic.
 constexpr int S1_THR = 1024, S1_COLS = 64, S1_RG = S1_THR / S1_COLS, S1_MAXROWS = 1024;
-template <int BN>
+// NL: loads per lane, all in flight (16: up to 256 rows; 64: up to S1_MAXROWS)
+template <int BN, int NL>
 __global__ void __launch_bounds__(S1_THR) stat_sum1_kernel(StatArgs sa, long long M, int BM_, int K) {
   __shared__ float part[S1_RG][S1_COLS];
   const int nct = K / BN, bn = blockIdx.x, c0 = blockIdx.y * S1_COLS;
   const int rows = (int)((M + BM_ - 1) / BM_);
   const int col = threadIdx.x % S1_COLS, rg = threadIdx.x / S1_COLS;
   const float* lvl1 = sa.part + (long long)bn * rows * (2 * BN) + c0 + col;
-  float v[S1_MAXROWS / S1_RG];
+  float v[NL];
 #pragma unroll
-  for (int u = 0; u < S1_MAXROWS / S1_RG; ++u) {
+  for (int u = 0; u < NL; ++u) {
     const int r = rg + u * S1_RG;
     v[u] = lvl1[(long long)(r < rows ? r : 0) * (2 * BN)];
   }
   float a = 0.f;
 #pragma unroll
-  for (int u = 0; u < S1_MAXROWS / S1_RG; ++u)
+  for (int u = 0; u < NL; ++u)
     if (rg + u * S1_RG < rows) a += v[u];
   part[rg][col] = a;
   __syncthreads();
@@ -1509,8 +1510,13 @@ static void launch_stat_tree(const StatArgs& sa, long long M, int bm, int K, int
   const long long rows = (M + bm - 1) / bm, NG = (rows + G1 - 1) / G1;
   if (rows <= S1_MAXROWS) {  // one level: every row in flight at once, no ticket
     const dim3 gr((unsigned)(K / BN), (unsigned)(2 * BN / S1_COLS)), th(S1_THR);
-    if (BN == 128) hipLaunchKernelGGL(stat_sum1_kernel<128>, gr, th, 0, cur_stream(), sa, M, bm, K);
-    else hipLaunchKernelGGL(stat_sum1_kernel<64>, gr, th, 0, cur_stream(), sa, M, bm, K);
+    if (rows <= 16 * S1_RG) {
+      if (BN == 128) hipLaunchKernelGGL((stat_sum1_kernel<128, 16>), gr, th, 0, cur_stream(), sa, M, bm, K);
+      else hipLaunchKernelGGL((stat_sum1_kernel<64, 16>), gr, th, 0, cur_stream(), sa, M, bm, K);
+    } else {
+      if (BN == 128) hipLaunchKernelGGL((stat_sum1_kernel<128, S1_MAXROWS / S1_RG>), gr, th, 0, cur_stream(), sa, M, bm, K);
+      else hipLaunchKernelGGL((stat_sum1_kernel<64, S1_MAXROWS / S1_RG>), gr, th, 0, cur_stream(), sa, M, bm, K);
+    }
     DPA_CHECK_LAUNCH();
     return;
   }

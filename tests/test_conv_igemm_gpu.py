@@ -260,7 +260,8 @@ def test_conv1x1_glds_kernel_tiles(C, bp, shape):
     (2, 64, 14, 14, 64, 3, 1, 1),     # general kernel, 3x3
     (3, 64, 7, 7, 256, 1, 1, 0),      # 1x1 kernel, ragged M
     (8, 64, 56, 56, 64, 1, 1, 0),     # 1x1, 196 pixel tiles: one-level reduction
-    (12, 64, 56, 56, 64, 1, 1, 0),    # 294 pixel tiles: two-level tree
+    (12, 64, 56, 56, 64, 1, 1, 0),    # 294 pixel tiles: one level, 64 rows in flight per lane
+    (48, 64, 56, 56, 64, 1, 1, 0),    # 1176 pixel tiles: two-level tree
     (2, 128, 15, 15, 128, 3, 2, 1),   # general kernel, stride 2
 ])
 @pytest.mark.parametrize("defer_min", [0, -1])
