@@ -390,6 +390,105 @@ apply_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__
   }
 }
 
+// A projection bottleneck's tail in one pass: y = relu(bn(x) + bn_r(res)) -- the
+// downsample conv's BatchNorm applied while reading its raw output (apply_kernel would
+// first write the normalised identity and read it back: one pass of 2 tensors less).
+// Both BNs' coefficients, running stats and saves are handled as in apply_kernel.
+struct BnCo {
+  const float* stats;
+  const float* gamma;
+  const float* beta;
+  float* rmean;
+  float* rvar;
+  const int64_t* nbt;
+  float momentum, eps;
+  float* save;
+};
+
+template <int VEC>
+__device__ __forceinline__ void bn_coef(const BnCo& p, int c0, int C, int train, bool leader, float* s, float* b) {
+  float mean[VEC], istd[VEC], ga[VEC], be[VEC];
+  ldf<VEC>(p.gamma + c0, ga);
+  ldf<VEC>(p.beta + c0, be);
+  if (train) {
+    float s1[VEC], s2[VEC], sh[VEC], var[VEC];
+    ldf<VEC>(p.stats + c0, s1);
+    ldf<VEC>(p.stats + C + c0, s2);
+    ldf<VEC>(p.stats + 2 * C + SHIFT_OFF + c0, sh);
+    const float n = p.stats[2 * C];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const float m1 = s1[j] / n;
+      var[j] = fmaxf(s2[j] / n - m1 * m1, 0.f);
+      mean[j] = sh[j] + m1;
+      istd[j] = rsqrtf(var[j] + p.eps);
+    }
+    if (leader) {
+      stf<VEC>(p.save + c0, mean);
+      stf<VEC>(p.save + C + c0, istd);
+      const float mom = p.momentum >= 0.f ? p.momentum : 1.f / (float)p.nbt[0];
+      float rm[VEC], rv[VEC];
+      ldf<VEC>(p.rmean + c0, rm);
+      ldf<VEC>(p.rvar + c0, rv);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        rm[j] = (1.f - mom) * rm[j] + mom * mean[j];
+        rv[j] = (1.f - mom) * rv[j] + mom * var[j] * (n / fmaxf(n - 1.f, 1.f));
+      }
+      stf<VEC>(p.rmean + c0, rm);
+      stf<VEC>(p.rvar + c0, rv);
+    }
+  } else {
+    float rv[VEC];
+    ldf<VEC>(p.rmean + c0, mean);
+    ldf<VEC>(p.rvar + c0, rv);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) istd[j] = rsqrtf(rv[j] + p.eps);
+  }
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    s[j] = ga[j] * istd[j];
+    b[j] = fmaf(-mean[j], s[j], be[j]);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(THR)
+apply_resbn_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y, long long M, int C,
+                   BnCo m, BnCo r, int train) {
+  constexpr int VEC = V16<T>::N;
+  const Chunk<VEC> g(C);
+  if (!g.active) return;
+  float s[VEC], b[VEC], rs[VEC], rb[VEC];
+  const bool leader = blockIdx.x == 0 && g.ro == 0;
+  bn_coef<VEC>(m, g.c0, C, train, leader, s, b);
+  bn_coef<VEC>(r, g.c0, C, train, leader, rs, rb);
+  long long r0, r1;
+  row_range(M, r0, r1);
+  auto row = [&](long long rr, float* a, const float* q) {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) a[j] = fmaxf(fmaf(a[j], s[j], b[j]) + fmaf(q[j], rs[j], rb[j]), 0.f);
+    store_vec<T>(y + rr * C + g.c0, a);
+  };
+  long long rr = r0 + g.ro;
+  for (; rr + (U - 1) * g.RP < r1; rr += U * g.RP) {
+    float a[U][VEC], q[U][VEC];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      load_vec<T>(x + (rr + u * g.RP) * C + g.c0, a[u]);
+      load_vec<T>(res + (rr + u * g.RP) * C + g.c0, q[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) row(rr + u * g.RP, a[u], q[u]);
+  }
+  for (; rr < r1; rr += g.RP) {
+    float a[VEC], q[VEC];
+    load_vec<T>(x + rr * C + g.c0, a);
+    load_vec<T>(res + rr * C + g.c0, q);
+    row(rr, a, q);
+  }
+}
+
 // ReLU-derivative source of the backward kernels
 enum { ACT_NONE = 0, ACT_Y = 1, ACT_RECOMPUTE = 2 };
 
@@ -772,6 +871,36 @@ void apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor y, int64_t C,
   DPA_CHECK_LAUNCH();
 }
 
+// y = relu(bn(x) + bn_r(res)); both BNs' running stats / saves updated (train)
+void apply_resbn(at::Tensor x, at::Tensor res, at::Tensor y, int64_t C, at::Tensor stats, at::Tensor gamma,
+                 at::Tensor beta, at::Tensor rmean, at::Tensor rvar, at::Tensor nbt, double momentum, double eps,
+                 at::Tensor save, at::Tensor rstats, at::Tensor rgamma, at::Tensor rbeta, at::Tensor rrmean,
+                 at::Tensor rrvar, at::Tensor rnbt, double rmomentum, double reps, at::Tensor rsave, bool train) {
+  const long long M = x.numel() / C;
+  check_rows(x, M, (int)C);
+  check_rows(res, M, (int)C);
+  check_rows(y, M, (int)C);
+  TORCH_CHECK(x.scalar_type() == res.scalar_type() && x.scalar_type() == y.scalar_type(), "apply_resbn: one dtype");
+  for (const at::Tensor* t : {&stats, &gamma, &beta, &rmean, &rvar, &save, &rstats, &rgamma, &rbeta, &rrmean, &rrvar,
+                              &rsave})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "apply_resbn: fp32 contiguous BN tensors");
+  TORCH_CHECK(save.numel() >= 2 * C && rsave.numel() >= 2 * C && gamma.numel() == C && rgamma.numel() == C,
+              "apply_resbn: sizes");
+  if (train)
+    TORCH_CHECK(stats.numel() >= 3 * C + SHIFT_OFF && rstats.numel() >= 3 * C + SHIFT_OFF, "apply_resbn: stats");
+  BnCo m{stats.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(), rmean.data_ptr<float>(),
+         rvar.data_ptr<float>(), nbt.data_ptr<int64_t>(), (float)momentum, (float)eps, save.data_ptr<float>()};
+  BnCo r{rstats.data_ptr<float>(), rgamma.data_ptr<float>(), rbeta.data_ptr<float>(), rrmean.data_ptr<float>(),
+         rrvar.data_ptr<float>(), rnbt.data_ptr<int64_t>(), (float)rmomentum, (float)reps, rsave.data_ptr<float>()};
+  dispatch(x, [&](auto tag) {
+    typedef decltype(tag) T;
+    const Grid2 g = chunk_grid<T>(M, (int)C, g_apply_target, CC_ELT);
+    hipLaunchKernelGGL(apply_resbn_kernel<T>, dim3(g.Gr, g.Gc), dim3(THR), 0, cur_stream(), dp<T>(x), dp<T>(res),
+                       dp<T>(y), M, (int)C, m, r, (int)train);
+  });
+  DPA_CHECK_LAUNCH();
+}
+
 // act: 0 = no ReLU, 1 = ReLU derivative from y, 2 = recomputed from x (no residual)
 void bwd_stats(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, int64_t C, int64_t act, at::Tensor save,
                at::Tensor gamma, at::Tensor beta, at::Tensor part, at::Tensor ticket, at::Tensor out,
@@ -889,6 +1018,7 @@ void register_bn_nhwc(pybind11::module& m) {
   s.def("set_grid_targets", &bnh::set_grid_targets);
   s.def("set_handoff", &bnh::set_handoff);
   s.def("apply", &bnh::apply);
+  s.def("apply_resbn", &bnh::apply_resbn);
   s.def("bwd_stats", &bnh::bwd_stats);
   s.def("bwd_elemt", &bnh::bwd_elemt);
   s.def("maxpool_fwd", &bnh::maxpool_fwd);

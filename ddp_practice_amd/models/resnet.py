@@ -47,6 +47,8 @@ _FUSE_BN_BWD = os.environ.get("DPA_FUSE_BN_BWD", "1") != "0"  # BNTap hand-off (
 # (+281 us over 13 launches) cancels the bwd_stats pass it removes (-297 us),
 # profiles/r3s2h_resnet50_steady_bn1_fused.txt
 _FUSE_BN1 = os.environ.get("DPA_FUSE_BN1", "0") == "1"
+# a projection block's downsample BN applied inside bn3's residual add (ops/bn_nhwc.bn_res_bn)
+_FUSE_DS_BN = os.environ.get("DPA_FUSE_DS_BN", "1") != "0"
 
 
 def _conv(x: torch.Tensor, conv: nn.Conv2d, cdtype: torch.dtype, bn: nn.Module | None = None, tap=None,
@@ -130,12 +132,21 @@ class Bottleneck(nn.Module):
         c2, st = _conv(out, self.conv2, cdtype, self.bn2, btap=bt1)
         out = bn_act(c2, self.bn2, relu=True, comm=_comm_of(self.bn2), stats=st, btap=bt2)
         identity = x
+        cd = std = None
         if self.downsample is not None:
             conv, bn = self.downsample[0], self.downsample[1]
-            cd, st = _conv(x, conv, cdtype, bn, None, xtap)
-            identity = bn_act(cd, bn, relu=False, comm=_comm_of(bn), stats=st)
+            cd, std = _conv(x, conv, cdtype, bn, None, xtap)
+            if not _FUSE_DS_BN:
+                identity = bn_act(cd, bn, relu=False, comm=_comm_of(bn), stats=std)
         c3, st = _conv(out, self.conv3, cdtype, self.bn3, btap=bt2)
-        y = bn_act(c3, self.bn3, res=identity, relu=True, comm=_comm_of(self.bn3), tap=tap, stats=st, btap=bt3)
+        if cd is not None and _FUSE_DS_BN:
+            # downsample BN applied inside the residual add (no normalised identity written)
+            from ..ops.bn_nhwc import bn_res_bn
+
+            y = bn_res_bn(c3, self.bn3, cd, self.downsample[1], comm=_comm_of(self.bn3), stats=st, rstats=std,
+                          btap=bt3)
+        else:
+            y = bn_act(c3, self.bn3, res=identity, relu=True, comm=_comm_of(self.bn3), tap=tap, stats=st, btap=bt3)
         if bt3 is not None:
             y._dpa_btap = bt3
         return y

@@ -150,6 +150,98 @@ def bn_act(x, bn, res=None, relu=True, comm=None, tap=None, stats=None, btap=Non
                          stats if bn.training else None, btap if bn.training else None)
 
 
+class BNResBNFn(torch.autograd.Function):
+    """relu(bn(x) + bn_r(r)): a projection bottleneck's last BatchNorm with the downsample
+    conv's BatchNorm applied to the residual in the same pass (csrc/kernels/bn_nhwc.hip
+    apply_resbn_kernel) -- the normalised identity is never written.  Backward: bn's
+    backward (ReLU mask from y) gives dx and dz = d(bn_r output), then bn_r's backward
+    (no ReLU) on dz, on the same kernels as two BNActFn backwards."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, r, rweight, rbias, bn, rbn, comm, pre, rpre, btap):
+        K = _K()
+        x, r = _cl(x), _cl(r)
+        C = x.shape[1]
+        dev = x.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        y = torch.empty_like(x, memory_format=_CL)
+        training = bn.training
+        stats = rstats = None
+        if training:
+            stats, rstats = pre, rpre
+            part, ticket = _Workspace.get(dev, C)
+            if stats is None:
+                stats = torch.empty(3 * C + 4, **f32)
+                K.fwd_stats(x, C, bn.running_mean, part, ticket, stats, bn.num_batches_tracked)
+            if rstats is None:
+                rstats = torch.empty(3 * C + 4, **f32)
+                K.fwd_stats(r, C, rbn.running_mean, part, ticket, rstats, rbn.num_batches_tracked)
+            sync = comm is not None and comm.active
+            if sync:
+                comm.all_reduce_(stats.narrow(0, 0, 2 * C + 1))
+                comm.all_reduce_(rstats.narrow(0, 0, 2 * C + 1))
+        else:
+            sync = False
+            stats = rstats = torch.empty(3 * C + 4, **f32)  # unused in eval
+        save, rsave = torch.empty(2 * C, **f32), torch.empty(2 * C, **f32)
+        mom = -1.0 if bn.momentum is None else float(bn.momentum)
+        rmom = -1.0 if rbn.momentum is None else float(rbn.momentum)
+        K.apply_resbn(x, r, y, C, stats, weight, bias, bn.running_mean, bn.running_var, bn.num_batches_tracked, mom,
+                      float(bn.eps), save, rstats, rweight, rbias, rbn.running_mean, rbn.running_var,
+                      rbn.num_batches_tracked, rmom, float(rbn.eps), rsave, training)
+        ctx.training = training
+        if training:
+            ctx.save_for_backward(x, y, weight, bias, save, stats, r, rweight, rbias, rsave, rstats)
+            ctx.sync, ctx.comm = sync, comm
+            ctx.btap = btap
+            if btap is not None:
+                btap.x, btap.y, btap.act, btap.save, btap.weight, btap.bias = x, y, 1, save, weight, bias
+                btap.sums = None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        if not ctx.training:
+            raise RuntimeError("BNResBNFn: backward through an eval-mode BatchNorm is not supported")
+        K = _K()
+        x, y, weight, bias, save, stats, r, rweight, rbias, rsave, rstats = ctx.saved_tensors
+        C = x.shape[1]
+        dy = _cl(dy)
+        f32 = dict(dtype=torch.float32, device=x.device)
+        part, ticket = _Workspace.get(x.device, C)
+        bt = ctx.btap
+        if bt is not None and bt.sums is not None and bt.grad_ptr == dy.data_ptr():
+            out, dgamma, dbeta = bt.sums
+        else:
+            out, dgamma, dbeta = torch.empty(2 * C, **f32), torch.empty(C, **f32), torch.empty(C, **f32)
+            K.bwd_stats(dy, y, x, C, 1, save, weight, bias, part, ticket, out, dgamma, dbeta)
+        if bt is not None:
+            bt.clear()
+            ctx.btap = None
+        sums = ctx.comm.all_reduce(out) if ctx.sync else out
+        dx = torch.empty_like(x, memory_format=_CL)
+        dz = torch.empty_like(x, memory_format=_CL)
+        K.bwd_elemt(dy, y, x, C, 1, save, sums, stats, weight, bias, dx, dz)
+        # the downsample BN (no ReLU) on dz
+        rout, rdgamma, rdbeta = torch.empty(2 * C, **f32), torch.empty(C, **f32), torch.empty(C, **f32)
+        K.bwd_stats(dz, None, r, C, 0, rsave, rweight, rbias, part, ticket, rout, rdgamma, rdbeta)
+        rsums = ctx.comm.all_reduce(rout) if ctx.sync else rout
+        dr = torch.empty_like(r, memory_format=_CL)
+        K.bwd_elemt(dz, None, r, C, 0, rsave, rsums, rstats, rweight, rbias, dr, None)
+        return dx, dgamma, dbeta, dr, rdgamma, rdbeta, None, None, None, None, None, None
+
+
+def bn_res_bn(x, bn, r, rbn, comm=None, stats=None, rstats=None, btap=None):
+    """relu(bn(x) + rbn(r)) in one pass (a projection bottleneck's tail; ``bn`` and ``rbn``
+    in the same mode).  ``stats`` / ``rstats``: the producing convs' statistics (training);
+    ``btap``: as bn_act."""
+    if bn.training != rbn.training:
+        raise RuntimeError("bn_res_bn: both BatchNorms must be in the same mode")
+    return BNResBNFn.apply(x, bn.weight, bn.bias, r, rbn.weight, rbn.bias, bn, rbn, comm if bn.training else None,
+                           stats if bn.training else None, rstats if bn.training else None,
+                           btap if bn.training else None)
+
+
 class MaxPoolFn(torch.autograd.Function):
     """MaxPool2d(kernel 3, stride 2, padding 1) on channels_last."""
 

@@ -178,3 +178,44 @@ def test_resnet50_native_matches_torch_path(C, amp):
     with torch.no_grad():
         e = _rel(m(x), r64(x.double()))
     assert e < max(fac * e_ref, floor), (e, e_ref)
+
+
+@pytest.mark.parametrize("C", [256, 64, 24])
+def test_bn_res_bn_fwd_bwd(C):
+    """relu(bn(x) + bn_r(r)) in one pass (ops/bn_nhwc.bn_res_bn) == float64 torch: output,
+    both BNs' running stats, and every gradient (x, r, both BNs' affine parameters)."""
+    from ddp_practice_amd.ops.bn_nhwc import bn_res_bn
+
+    torch.manual_seed(1)
+    N, H, W = 3, 7, 9
+    cl = torch.channels_last
+    x = (torch.randn(N, C, H, W, device=DEV) * 2 + 0.5).to(torch.bfloat16).contiguous(memory_format=cl)
+    r = (torch.randn(N, C, H, W, device=DEV) - 0.3).to(torch.bfloat16).contiguous(memory_format=cl)
+    bn, rbn = torch.nn.BatchNorm2d(C).to(DEV), torch.nn.BatchNorm2d(C).to(DEV)
+    with torch.no_grad():
+        for m in (bn, rbn):
+            m.weight.uniform_(0.5, 1.5)
+            m.bias.uniform_(-0.3, 0.3)
+            m.running_mean.uniform_(-0.2, 0.2)
+    ref, rref = copy.deepcopy(bn).double(), copy.deepcopy(rbn).double()
+    xs, rs = x.detach().clone().requires_grad_(), r.detach().clone().requires_grad_()
+    y = bn_res_bn(xs, bn, rs, rbn)
+    x64, r64 = x.double().detach().requires_grad_(), r.double().detach().requires_grad_()
+    y64 = (ref(x64) + rref(r64)).relu()
+    assert _rel(y, y64) < 1e-2
+    for m, mr in ((bn, ref), (rbn, rref)):
+        assert _rel(m.running_mean, mr.running_mean) < 1e-5 and _rel(m.running_var, mr.running_var) < 1e-5
+        assert int(m.num_batches_tracked) == 1
+    g = torch.randn_like(y64)
+    (y.double() * g).sum().backward()
+    (y64 * g).sum().backward()
+    assert _rel(xs.grad, x64.grad) < 3e-2 and _rel(rs.grad, r64.grad) < 3e-2
+    for m, mr in ((bn, ref), (rbn, rref)):
+        assert _rel(m.weight.grad, mr.weight.grad) < 3e-2 and _rel(m.bias.grad, mr.bias.grad) < 3e-2
+    bn.eval()
+    rbn.eval()
+    ref.eval()
+    rref.eval()
+    with torch.no_grad():
+        ye = bn_res_bn(x, bn, r, rbn)
+        assert _rel(ye, (ref(x.double()) + rref(r.double())).relu()) < 1e-2
