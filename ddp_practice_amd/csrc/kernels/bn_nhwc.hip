@@ -636,6 +636,95 @@ bwd_elemt_kernel(const T* __restrict__ dy, const T* __restrict__ y, const T* __r
   }
 }
 
+// bwd_elemt_kernel<T, ACT_Y, true> of a projection block's last BN that also takes the
+// downsample BN's backward sums from the dz it writes: rout = [S1 | S2] with S1 = sum dz,
+// S2 = sum dz * (r - mean_r) * invstd_r (r: the downsample conv's output), rdbeta = S1,
+// rdgamma = S2 -- the downsample BN's own statistics pass over dz and r disappears.
+template <typename T>
+__global__ void __launch_bounds__(THR)
+bwd_elemt_rbn_kernel(const T* __restrict__ dy, const T* __restrict__ y, const T* __restrict__ x, long long M, int C,
+                     const float* __restrict__ save, const float* __restrict__ sums, const float* __restrict__ fstats,
+                     const float* __restrict__ gamma, const float* __restrict__ beta, T* __restrict__ dx,
+                     T* __restrict__ dres, const T* __restrict__ r, const float* __restrict__ rsave,
+                     float* __restrict__ part, unsigned* __restrict__ tickets, float* __restrict__ rout,
+                     float* __restrict__ rdgamma, float* __restrict__ rdbeta, int wt) {
+  constexpr int VEC = V16<T>::N;
+  __shared__ float scratch[2 * THR * VEC];
+  __shared__ float red[2 * CC_ELT];
+  __shared__ int s_flag;
+  const Chunk<VEC> g(C);
+  float s1[VEC], s2[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) s1[j] = s2[j] = 0.f;
+  if (g.active) {
+    BwdLane<VEC, ACT_Y> L;
+    L.init(g.c0, C, save, gamma, beta);
+    float gi[VEC], k1[VEC], k2[VEC], rmu[VEC], ris[VEC];
+    const float n = fstats[2 * C];
+    ldf<VEC>(gamma + g.c0, gi);
+    ldf<VEC>(sums + g.c0, k1);
+    ldf<VEC>(sums + C + g.c0, k2);
+    ldf<VEC>(rsave + g.c0, rmu);
+    ldf<VEC>(rsave + C + g.c0, ris);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      gi[j] *= L.is[j];
+      k1[j] /= n;
+      k2[j] /= n;
+    }
+    auto row = [&](long long o, const float* d, const float* xv, const float* yv, const float* rv) {
+      float z[VEC], e[VEC];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        z[j] = L.dz(j, d[j], xv[j], yv[j]);
+        const float xh = (xv[j] - L.mu[j]) * L.is[j];
+        e[j] = gi[j] * (z[j] - k1[j] - xh * k2[j]);
+      }
+      store_vec<T>(dx + o, e);
+      store_vec<T>(dres + o, z);
+      // the downsample BN's sums of dz (dy masked: already a storage-exact value, so these
+      // are the sums its own statistics pass over the stored dres would take)
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        s1[j] += z[j];
+        s2[j] = fmaf(z[j], (rv[j] - rmu[j]) * ris[j], s2[j]);
+      }
+    };
+    long long r0, r1;
+    row_range(M, r0, r1);
+    long long rr = r0 + g.ro;
+    for (; rr + (U - 1) * g.RP < r1; rr += U * g.RP) {
+      float d[U][VEC], xv[U][VEC], yv[U][VEC], rv[U][VEC];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long o = (rr + u * g.RP) * C + g.c0;
+        load_vec<T>(dy + o, d[u]);
+        load_vec<T>(x + o, xv[u]);
+        load_vec<T>(y + o, yv[u]);
+        load_vec<T>(r + o, rv[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) row((rr + u * g.RP) * C + g.c0, d[u], xv[u], yv[u], rv[u]);
+    }
+    for (; rr < r1; rr += g.RP) {
+      float d[VEC], xv[VEC], yv[VEC], rv[VEC];
+      const long long o = rr * C + g.c0;
+      load_vec<T>(dy + o, d);
+      load_vec<T>(x + o, xv);
+      load_vec<T>(y + o, yv);
+      load_vec<T>(r + o, rv);
+      row(o, d, xv, yv, rv);
+    }
+  }
+  block_combine<VEC>(g, s1, s2, red, scratch);
+  if (!chunk_reduce(part, tickets, 2 * g.CC, red, scratch, &s_flag, wt)) return;
+  const int cb = (int)blockIdx.y * g.CC;
+  for (int t = threadIdx.x; t < g.CC; t += THR) {
+    rout[cb + t] = rdbeta[cb + t] = red[t];
+    rout[C + cb + t] = rdgamma[cb + t] = red[g.CC + t];
+  }
+}
+
 // ----------------------------------------------------------------------------
 // MaxPool2d(3, 2, padding 1) NHWC: out + argmax tap (0..8, first max in kh, kw order)
 template <typename T>
@@ -956,6 +1045,30 @@ void bwd_elemt(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, int64_t
   DPA_CHECK_LAUNCH();
 }
 
+// bwd_elemt (act 1, with dres) + the downsample BN's backward sums of dres (see the kernel)
+void bwd_elemt_rbn(at::Tensor dy, at::Tensor y, at::Tensor x, int64_t C, at::Tensor save, at::Tensor sums,
+                   at::Tensor fstats, at::Tensor gamma, at::Tensor beta, at::Tensor dx, at::Tensor dres, at::Tensor r,
+                   at::Tensor rsave, at::Tensor part, at::Tensor ticket, at::Tensor rout, at::Tensor rdgamma,
+                   at::Tensor rdbeta) {
+  const long long M = x.numel() / C;
+  for (const at::Tensor* t : {&dy, &y, &x, &dx, &dres, &r}) check_rows(*t, M, (int)C);
+  TORCH_CHECK(rsave.numel() >= 2 * C && rout.numel() >= 2 * C && rdgamma.numel() == C && rdbeta.numel() == C,
+              "bwd_elemt_rbn: sizes");
+  dispatch(x, [&](auto tag) {
+    typedef decltype(tag) T;
+    Grid2 g = chunk_grid<T>(M, (int)C, g_elemt_target, CC_ELT);
+    g.Gr = std::min(g.Gr, MAXGR);
+    check_workspace(g, (int)C, part, ticket);
+    hipLaunchKernelGGL(bwd_elemt_rbn_kernel<T>, dim3(g.Gr, g.Gc), dim3(THR), 0, cur_stream(), dp<T>(dy), dp<T>(y),
+                       dp<T>(x), M, (int)C, save.data_ptr<float>(), sums.data_ptr<float>(), fstats.data_ptr<float>(),
+                       gamma.data_ptr<float>(), beta.data_ptr<float>(), dp<T>(dx), dp<T>(dres), dp<T>(r),
+                       rsave.data_ptr<float>(), part.data_ptr<float>(),
+                       reinterpret_cast<unsigned*>(ticket.data_ptr<int>()), rout.data_ptr<float>(),
+                       rdgamma.data_ptr<float>(), rdbeta.data_ptr<float>(), g_handoff_wt);
+  });
+  DPA_CHECK_LAUNCH();
+}
+
 void maxpool_fwd(at::Tensor x, at::Tensor y, at::Tensor idx) {
   TORCH_CHECK(x.dim() == 4 && y.dim() == 4, "maxpool: NHWC tensors [N][H][W][C]");
   const int N = (int)x.size(0), H = (int)x.size(1), W = (int)x.size(2), C = (int)x.size(3);
@@ -1019,6 +1132,7 @@ void register_bn_nhwc(pybind11::module& m) {
   s.def("set_handoff", &bnh::set_handoff);
   s.def("apply", &bnh::apply);
   s.def("apply_resbn", &bnh::apply_resbn);
+  s.def("bwd_elemt_rbn", &bnh::bwd_elemt_rbn);
   s.def("bwd_stats", &bnh::bwd_stats);
   s.def("bwd_elemt", &bnh::bwd_elemt);
   s.def("maxpool_fwd", &bnh::maxpool_fwd);

@@ -12,6 +12,8 @@ local sums (torch/nn/modules/_functions.py:10-205).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .._ext import load as _load_ext
@@ -150,6 +152,11 @@ def bn_act(x, bn, res=None, relu=True, comm=None, tap=None, stats=None, btap=Non
                          stats if bn.training else None, btap if bn.training else None)
 
 
+# the downsample BN's backward sums inside bn3's elementwise pass: measured slower (14.79-14.80 vs
+# 14.69-14.75 ms, profiles/r3s2s_resnet50_rbn_sums_rejected.jsonl), opt-in
+_FUSE_RBN_SUMS = os.environ.get("DPA_FUSE_RBN_SUMS", "0") == "1"
+
+
 class BNResBNFn(torch.autograd.Function):
     """relu(bn(x) + bn_r(r)): a projection bottleneck's last BatchNorm with the downsample
     conv's BatchNorm applied to the residual in the same pass (csrc/kernels/bn_nhwc.hip
@@ -221,10 +228,15 @@ class BNResBNFn(torch.autograd.Function):
         sums = ctx.comm.all_reduce(out) if ctx.sync else out
         dx = torch.empty_like(x, memory_format=_CL)
         dz = torch.empty_like(x, memory_format=_CL)
-        K.bwd_elemt(dy, y, x, C, 1, save, sums, stats, weight, bias, dx, dz)
-        # the downsample BN (no ReLU) on dz
+        # bn's elementwise backward, which also takes the downsample BN's sums of dz
         rout, rdgamma, rdbeta = torch.empty(2 * C, **f32), torch.empty(C, **f32), torch.empty(C, **f32)
-        K.bwd_stats(dz, None, r, C, 0, rsave, rweight, rbias, part, ticket, rout, rdgamma, rdbeta)
+        if _FUSE_RBN_SUMS:
+            K.bwd_elemt_rbn(dy, y, x, C, save, sums, stats, weight, bias, dx, dz, r, rsave, part, ticket, rout,
+                            rdgamma, rdbeta)
+        else:  # A/B: the elementwise pass, then the downsample BN's own statistics pass
+            K.bwd_elemt(dy, y, x, C, 1, save, sums, stats, weight, bias, dx, dz)
+            K.bwd_stats(dz, None, r, C, 0, rsave, rweight, rbias, part, ticket, rout, rdgamma, rdbeta)
+        # the downsample BN (no ReLU) on dz
         rsums = ctx.comm.all_reduce(rout) if ctx.sync else rout
         dr = torch.empty_like(r, memory_format=_CL)
         K.bwd_elemt(dz, None, r, C, 0, rsave, rsums, rstats, rweight, rbias, dr, None)
