@@ -794,10 +794,15 @@ maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx, T*
         const long long o = (((long long)n * OH + oh) * OW + ow) * C + c0;
         float g[VEC];
         load_vec<T>(dy + o, g);
-        const uint8_t want = (uint8_t)(kh * 3 + kw);
+        const unsigned want = (unsigned)(kh * 3 + kw);
+        // the VEC argmax bytes of this vector as ONE load (o % VEC == 0: C % VEC == 0), not VEC
+        // byte loads
+        unsigned long long iv;
+        if constexpr (VEC == 8) iv = *reinterpret_cast<const unsigned long long*>(idx + o);
+        else iv = *reinterpret_cast<const unsigned*>(idx + o);  // fp32: 4 bytes (o % 4 == 0)
 #pragma unroll
         for (int j = 0; j < VEC; ++j)
-          if (idx[o + j] == want) acc[j] += g[j];
+          if (((iv >> (8 * j)) & 0xffull) == want) acc[j] += g[j];
       }
     }
     store_vec<T>(dx + (((long long)n * H + h) * W + w) * C + c0, acc);
@@ -1093,6 +1098,7 @@ void maxpool_bwd(at::Tensor dy, at::Tensor idx, at::Tensor dx) {
   TORCH_CHECK(idx.numel() == dy.numel());
   dispatch(dx, [&](auto tag) {
     typedef decltype(tag) T;
+    TORCH_CHECK(C % V16<T>::N == 0, "maxpool_bwd: channels must be a multiple of ", V16<T>::N);
     hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(elt_grid((long long)N * H * W * C / V16<T>::N)), dim3(THR), 0,
                        cur_stream(), dp<T>(dy), idx.data_ptr<uint8_t>(), dp<T>(dx), N, H, W, C, OH, OW);
   });
