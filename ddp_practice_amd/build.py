@@ -120,6 +120,20 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = True) ->
             changed |= c
             if verbose and c:
                 print(f"[build] compiled {s.relative_to(PKG.parent)}", flush=True)
+    # the tree's source digest, compiled in as _C.source_digest (checked by _ext.load())
+    from ddp_practice_amd._ext import source_digest
+
+    dsrc = BUILD / "source_digest.cpp"
+    dtext = f'extern "C" const char dpa_source_digest[] = "{source_digest(CSRC)}";\n'
+    dobj = BUILD / "source_digest.o"
+    if not dsrc.exists() or dsrc.read_text() != dtext or not dobj.exists():
+        dsrc.write_text(dtext)
+        r = subprocess.run(["hipcc", "-x", "c++", "-fPIC", "-c", str(dsrc), "-o", str(dobj)],
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {dsrc}\n{r.stderr}")
+        changed = True
+    objs.append(dobj)
     if changed or force or not TARGET.exists():
         _, libdirs = _torch_dirs()
         torch_lib = libdirs[0]

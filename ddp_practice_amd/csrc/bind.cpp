@@ -24,6 +24,10 @@ void register_bn_nhwc(pybind11::module& m);
 void register_conv_igemm(pybind11::module& m);
 }
 
+// sha1 of the sources this library was built from (build.py generates it; _ext.py compares
+// it with the tree on import so a stale binary cannot pass for the current kernels)
+extern "C" const char dpa_source_digest[];
+
 // Opt-in (DPA_NATIVE_BACKTRACE=1) host-side SIGSEGV handler printing the native
 // stack: diagnostics for crashes inside the HIP runtime / RCCL / torch.
 static void dpa_segv_handler(int sig) {
@@ -43,6 +47,7 @@ PYBIND11_MODULE(_C, m) {
     signal(SIGABRT, dpa_segv_handler);
   }
   m.doc() = "ddp_practice_amd native extension (gfx950 HIP kernels, RCCL communicator, DDP reducer)";
+  m.attr("source_digest") = pybind11::str(dpa_source_digest);
   dpa::register_selftest(m);
   dpa::register_convblock(m);
   dpa::register_head(m);

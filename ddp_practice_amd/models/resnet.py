@@ -108,7 +108,9 @@ class Bottleneck(nn.Module):
             identity = self.downsample(x)
         return self.relu(out + identity)
 
-    def forward_native(self, x: torch.Tensor, cdtype: torch.dtype) -> torch.Tensor:
+    def forward_native(self, x: torch.Tensor, cdtype: torch.dtype, bt_in=None):
+        """Native block forward; returns (y, the BNTap of bn3 or None).  ``bt_in``: the
+        previous block's bn3 tap (the BN that produced ``x``)."""
         from ..ops.bn_nhwc import BNTap, bn_act
 
         train = self.bn3.training and torch.is_grad_enabled()
@@ -122,7 +124,7 @@ class Bottleneck(nn.Module):
         # (ops/bn_nhwc.BNTap): bn2 -> conv3, and the previous block's bn3 -> this conv1
         # when this is an identity block (its dgrad then holds the whole gradient of x);
         # bn1 -> conv2 (stride 1) with DPA_FUSE_BN1=1
-        bt_in = getattr(x, "_dpa_btap", None) if tap is not None else None
+        bt_in = bt_in if tap is not None else None
         bt1 = BNTap() if train and _FUSE_BN1 and self.conv2.stride == (1, 1) else None
         bt2 = BNTap() if train and _FUSE_BN_BWD else None
         bt3 = BNTap() if train and _FUSE_BN_BWD else None
@@ -147,9 +149,7 @@ class Bottleneck(nn.Module):
                           btap=bt3)
         else:
             y = bn_act(c3, self.bn3, res=identity, relu=True, comm=_comm_of(self.bn3), tap=tap, stats=st, btap=bt3)
-        if bt3 is not None:
-            y._dpa_btap = bt3
-        return y
+        return y, bt3
 
 
 class ResNet(nn.Module):
@@ -225,8 +225,9 @@ class ResNet(nn.Module):
         x = bn_act(c, self.bn1, relu=True, comm=_comm_of(self.bn1), stats=st)
         x = max_pool_3x3s2(x)
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            bt = None
             for blk in layer:
-                x = blk.forward_native(x, cdtype)
+                x, bt = blk.forward_native(x, cdtype, bt)
         feat = global_avg_pool(x)
         if cdtype in (torch.bfloat16, torch.float16) and os.environ.get("DPA_NATIVE_FC", "1") != "0":
             # fc on the native MFMA linear kernels (ops/head.py: fp32 master weight read

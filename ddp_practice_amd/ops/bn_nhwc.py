@@ -13,6 +13,7 @@ local sums (torch/nn/modules/_functions.py:10-205).
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 
@@ -52,20 +53,63 @@ class BNTap:
     its epilogue also takes S1 = sum dz, S2 = sum dz * xhat (csrc/kernels/conv_igemm.hip,
     BS epilogue), so the backward here skips its bwd_stats pass over dy / x (/ y).
 
-    The forward fills x, y (act 1: the ReLU follows a residual add), act, save (mean |
-    invstd), weight, bias; the conv's backward sets ``sums`` = (out, dgamma, dbeta) and
-    ``grad_ptr`` = the gradient it wrote; the BN backward uses them when dy is that tensor.
+    The forward binds the BN's autograd node (``bind``): x and y (act 1: the ReLU follows a
+    residual add) are read back from that node's saved tensors through a weak reference, so
+    the tap holds no activation and forms no reference cycle with the BN's own output (the
+    output -> grad_fn -> tap -> output cycle kept activations alive until the cycle collector
+    ran when no backward followed).  The conv's backward sets ``sums`` = (out,
+    dgamma, dbeta) and ``grad_ptr`` / ``grad_ver`` = the gradient it wrote and its version;
+    the BN backward uses the sums only when dy is that tensor, unmodified (autograd adds a
+    second consumer's gradient in place, which keeps the pointer but bumps the version).
     """
 
-    __slots__ = ("x", "y", "act", "save", "weight", "bias", "sums", "grad_ptr")
+    __slots__ = ("_node", "_ix", "_iy", "act", "save", "weight", "bias", "sums", "grad_ptr", "grad_ver")
 
     def __init__(self):
-        self.x = self.y = self.save = self.weight = self.bias = self.sums = None
+        self._node = None
+        self._ix = self._iy = -1
+        self.save = self.weight = self.bias = self.sums = None
         self.act = 0
         self.grad_ptr = 0
+        self.grad_ver = -1
+
+    def bind(self, ctx, ix: int, iy: int, act: int, save, weight, bias) -> None:
+        """``ctx``: the BN's autograd node; ``ix`` / ``iy``: positions of x / y in its saved
+        tensors (``iy`` -1: y not needed)."""
+        self._node = weakref.ref(ctx)
+        self._ix, self._iy = ix, iy
+        self.act, self.save, self.weight, self.bias = act, save, weight, bias
+        self.sums = None
+
+    def bind_tensors(self, x, y, act: int, save, weight, bias) -> None:
+        """Direct binding (kernel tests, no autograd node): holds x / y strongly."""
+        held = type("_Held", (), {"saved_tensors": (x, y)})()
+        self._node = lambda: held
+        self._ix, self._iy = 0, (1 if y is not None else -1)
+        self.act, self.save, self.weight, self.bias = act, save, weight, bias
+        self.sums = None
+
+    def _saved(self, i: int):
+        node = self._node() if self._node is not None else None
+        if node is None or i < 0:
+            return None
+        return node.saved_tensors[i]
+
+    @property
+    def x(self):
+        return self._saved(self._ix)
+
+    @property
+    def y(self):
+        return self._saved(self._iy)
+
+    def matches(self, dy: torch.Tensor) -> bool:
+        """The consumer's sums are valid for ``dy``: same tensor, not modified since."""
+        return self.sums is not None and self.grad_ptr == dy.data_ptr() and self.grad_ver == dy._version
 
     def clear(self):
-        self.x = self.y = self.save = self.weight = self.bias = self.sums = None
+        self._node = None
+        self.save = self.weight = self.bias = self.sums = None
 
 
 class BNActFn(torch.autograd.Function):
@@ -100,10 +144,7 @@ class BNActFn(torch.autograd.Function):
             ctx.tap = tap if res is not None else None
             ctx.btap = btap if ctx.act in (1, 2) else None
             if ctx.btap is not None:
-                bt = ctx.btap
-                bt.x, bt.y, bt.act, bt.save, bt.weight, bt.bias = x, (y if ctx.act == 1 else None), ctx.act, save, \
-                    weight, bias
-                bt.sums = None
+                ctx.btap.bind(ctx, 0, 1 if ctx.act == 1 else -1, ctx.act, save, weight, bias)
         else:
             dummy = torch.empty(2 * C + 1, **f32)
             K.apply(x, resc, y, C, dummy, weight, bias, running_mean, running_var, nbt, mom, float(eps), False,
@@ -121,7 +162,7 @@ class BNActFn(torch.autograd.Function):
         dy = _cl(dy)
         f32 = dict(dtype=torch.float32, device=x.device)
         bt = getattr(ctx, "btap", None)
-        if bt is not None and bt.sums is not None and bt.grad_ptr == dy.data_ptr():
+        if bt is not None and bt.matches(dy):
             out, dgamma, dbeta = bt.sums  # taken by the consumer conv's data-gradient epilogue
         else:
             part, ticket = _Workspace.get(x.device, C)
@@ -202,8 +243,7 @@ class BNResBNFn(torch.autograd.Function):
             ctx.sync, ctx.comm = sync, comm
             ctx.btap = btap
             if btap is not None:
-                btap.x, btap.y, btap.act, btap.save, btap.weight, btap.bias = x, y, 1, save, weight, bias
-                btap.sums = None
+                btap.bind(ctx, 0, 1, 1, save, weight, bias)
         return y
 
     @staticmethod
@@ -217,7 +257,7 @@ class BNResBNFn(torch.autograd.Function):
         f32 = dict(dtype=torch.float32, device=x.device)
         part, ticket = _Workspace.get(x.device, C)
         bt = ctx.btap
-        if bt is not None and bt.sums is not None and bt.grad_ptr == dy.data_ptr():
+        if bt is not None and bt.matches(dy):
             out, dgamma, dbeta = bt.sums
         else:
             out, dgamma, dbeta = torch.empty(2 * C, **f32), torch.empty(C, **f32), torch.empty(C, **f32)

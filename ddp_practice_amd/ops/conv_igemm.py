@@ -95,7 +95,10 @@ def dgrad_bn(dy: torch.Tensor, wt: torch.Tensor, bt, acc: torch.Tensor | None = 
     flipped transposed filter, ``pad`` = R - 1 - the forward padding.  Stores the sums in
     ``bt`` and returns dx; None when the shapes do not allow it (the BN then runs its own
     statistics pass)."""
-    if bt is None or bt.x is None or not G1X1:
+    if bt is None or not G1X1:
+        return None
+    bx = bt.x  # the producing BN's saved input (None once its node is gone)
+    if bx is None:
         return None
     if (acc is None) != (bt.act == 2):  # act 1 (ReLU after a residual add) <-> accumulated dx
         return None
@@ -105,7 +108,7 @@ def dgrad_bn(dy: torch.Tensor, wt: torch.Tensor, bt, acc: torch.Tensor | None = 
     N, _, H, W = dy.shape
     C = wt.shape[0]
     shape = (N, C, H, W)
-    if tuple(bt.x.shape) != shape or bt.x.dtype != dy.dtype or not bt.x.is_contiguous(memory_format=_CL):
+    if tuple(bx.shape) != shape or bx.dtype != dy.dtype or not bx.is_contiguous(memory_format=_CL):
         return None
     if acc is not None and (tuple(acc.shape) != shape or not acc.is_contiguous(memory_format=_CL)):
         return None
@@ -113,11 +116,12 @@ def dgrad_bn(dy: torch.Tensor, wt: torch.Tensor, bt, acc: torch.Tensor | None = 
     part, tickets = _StatWS.get(dy.device, N * H * W, C)
     out, dgamma, dbeta = torch.empty(2 * C, **f32), torch.empty(C, **f32), torch.empty(C, **f32)
     dx = acc if acc is not None else torch.empty(shape, dtype=dy.dtype, device=dy.device, memory_format=_CL)
-    _K().conv_fwd(dy, wt, dx, 1, pad, part, tickets, accumulate=acc is not None, bn_x=bt.x,
+    _K().conv_fwd(dy, wt, dx, 1, pad, part, tickets, accumulate=acc is not None, bn_x=bx,
                   bn_y=bt.y if bt.act == 1 else None, bn_save=bt.save, bn_gamma=bt.weight, bn_beta=bt.bias,
                   bn_out=out, bn_dgamma=dgamma, bn_dbeta=dbeta)
     bt.sums = (out, dgamma, dbeta)
     bt.grad_ptr = dx.data_ptr()
+    bt.grad_ver = dx._version
     return dx
 
 

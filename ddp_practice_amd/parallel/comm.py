@@ -484,6 +484,10 @@ def setup_xgmi(rc: "RcclCommunicator", store, key: str) -> str:
         return f"off (self-test failed: {err or 'on a peer'})"
     if ts_max > 0 and mode == "auto" and os.environ.get("DPA_XGMI_PROBE", "1") != "0":
         ts_max = _probe_twoshot(rc, x, max_bytes, ts_max)
+        if ts_max < 0:
+            # an engine failure during the probe (exception or error word on any rank): the
+            # engine may be poisoned, so it is not attached at all -- every rank stays on RCCL
+            return "off (two-shot probe failed)"
     x.set_timeout(timeout)
     rc.native.attach_xgmi(x, max_bytes, max(ts_max, 0))
     rc.xgmi = x
@@ -493,7 +497,8 @@ def setup_xgmi(rc: "RcclCommunicator", store, key: str) -> str:
 def _probe_twoshot(rc: "RcclCommunicator", x, lo: int, hi: int) -> int:
     """Largest probed size in (lo, hi] up to which the two-shot beats RCCL on this node
     (fp32, 5 timed repetitions after 2 warm-ups; each rank's times max-reduced so
-    every rank picks the same bound).  Returns 0 if RCCL wins at the smallest size.
+    every rank picks the same bound).  Returns 0 if RCCL wins at the smallest size and
+    -1 if the engine failed on any rank (the caller must then not attach it).
 
     Every decision is made from max-reduced values only: a rank whose engine failed
     (an exception, or its error word set) contributes a failure flag to the same
@@ -506,11 +511,13 @@ def _probe_twoshot(rc: "RcclCommunicator", x, lo: int, hi: int) -> int:
         times = torch.zeros(3, device=rc.device)  # [two-shot s, RCCL s, any local failure]
         failed = False
         for i, fn in enumerate((lambda: x.all_reduce_twoshot(t), lambda: rc.native.all_reduce(t, "sum"))):
+            barrier_done = False
             try:
                 for _ in range(2):
                     fn()
                 torch.cuda.synchronize(rc.device)
                 rc.native.barrier()
+                barrier_done = True
                 t0 = time.perf_counter()
                 for _ in range(5):
                     fn()
@@ -520,13 +527,14 @@ def _probe_twoshot(rc: "RcclCommunicator", x, lo: int, hi: int) -> int:
                 if i == 1:
                     raise
                 failed = True
-                rc.native.barrier()  # the barrier the skipped timing loop would have issued
+                if not barrier_done:
+                    rc.native.barrier()  # the barrier the skipped warm-up would have reached
         if failed or x.error() != 0:
             times[2] = 1.0
         rc.native.all_reduce(times, "max")
         ts, rccl, bad = times.tolist()
         if bad != 0.0:
-            return 0
+            return -1
         if ts <= rccl:
             best = nb
         else:

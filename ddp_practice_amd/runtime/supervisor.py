@@ -106,6 +106,13 @@ class Supervisor:
         self.world = world
         torchrun = local_ranks is None
         if torchrun:  # one supervisor per rank, started by torchrun
+            lws = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+            if lws != world:
+                # the children's per-attempt rendezvous store lives on the leader's localhost
+                # (and the xGMI engine is single-node): a rank on another node could only time
+                # out after 300 s and be reported as a communicator failure
+                raise ValueError(f"the rank supervisor is single-node: LOCAL_WORLD_SIZE={lws} != "
+                                 f"WORLD_SIZE={world} (multi-node torchrun is not supported)")
             self.rank = int(os.environ["RANK"])
             self.local_ranks = [self.rank]
             self.local_rank_of = {self.rank: int(os.environ.get("LOCAL_RANK", self.rank))}

@@ -64,6 +64,10 @@ class _Engine:
             self.err = 1  # a timed-out exchange: the engine's error word, no exception
         if self.rank == self.bad and self.bad_kind == "twoshot_raise":
             raise RuntimeError("two-shot launch failed on this rank")
+        self.ts_calls += 1
+        if self.rank == self.bad and self.bad_kind == "twoshot_raise_late" and self.ts_calls > 2:
+            # fails inside the timed loop, i.e. after the probe's barrier
+            raise RuntimeError("two-shot launch failed on this rank (timed loop)")
         # the probe only times the engine: no stand-in gloo traffic that a failing rank
         # would leave unmatched (the real engine's peers time out instead)
         r = t.clone() if self.local_only else self._sum(t, op)
@@ -81,7 +85,12 @@ class _Engine:
         o.copy_(s.repeat(nblk))
 
     err = 0
+    ts_calls = 0
     local_only = False
+    attached = False
+
+    def set_timeout(self, s):
+        pass
 
     def error(self):
         return self.err
@@ -128,5 +137,31 @@ def run_probe(rank, world, port, bad, bad_kind, q):
         dist.all_gather(every, calls)
         dist.destroy_process_group()
         q.put((rank, "ok", (best, [int(c) for c in every])))
+    except Exception:  # noqa: BLE001
+        q.put((rank, "err", traceback.format_exc()))
+
+
+def run_setup(rank, world, port, bad, bad_kind, q):
+    """parallel/comm.setup_xgmi with a stand-in engine whose two-shot probe fails on rank
+    ``bad``: every rank must report the engine off and none may attach it."""
+    try:
+        os.environ.update(client_env(rank, world, port))
+        os.environ["DPA_COMM"] = "auto"
+        dist.init_process_group("gloo")
+        torch.cuda.synchronize = lambda *a, **k: None
+        from ddp_practice_amd.parallel import comm
+
+        rc = _RC(rank, world)
+        eng = _Engine(rank, bad, bad_kind)
+        eng.local_only = True
+        rc.native.attach_xgmi = lambda *a: setattr(eng, "attached", True)
+        comm.open_xgmi = lambda *a, **k: (eng, "")
+        comm._xgmi_selftest = lambda *a, **k: (True, "")
+        status = comm.setup_xgmi(rc, store=object(), key="t")
+        calls = torch.tensor([rc.native.calls])
+        every = [torch.zeros(1, dtype=calls.dtype) for _ in range(world)]
+        dist.all_gather(every, calls)
+        dist.destroy_process_group()
+        q.put((rank, "ok", (status, eng.attached, getattr(rc, "xgmi", None) is not None, [int(c) for c in every])))
     except Exception:  # noqa: BLE001
         q.put((rank, "err", traceback.format_exc()))

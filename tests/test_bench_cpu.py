@@ -114,3 +114,15 @@ def test_bench_under_torchrun_rank_failure_falls_back():
     rec = recs[0]
     assert rec["fallback"] == "rccl" and rec["value"] > 0
     assert "rank 0: exit 7" in rec["comm_error"]
+
+
+def test_supervisor_rejects_multi_node_torchrun(monkeypatch):
+    """The per-attempt child store is on the leader's localhost: a multi-node torchrun run
+    is refused up front instead of timing out as a comm failure."""
+    from ddp_practice_amd.runtime.supervisor import Supervisor
+
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    monkeypatch.setenv("MASTER_PORT", "1")
+    with pytest.raises(ValueError, match="single-node"):
+        Supervisor(16)

@@ -17,13 +17,13 @@ REF_KEYS = ["layer1.0.weight", "layer1.0.bias", "layer1.1.weight", "layer1.1.bia
             "layer2.1.num_batches_tracked", "fc.weight", "fc.bias"]
 
 
-def _run(args, cwd, env_extra=None, timeout=600):
+def _run(args, cwd, env_extra=None, timeout=600, stderr=False):
     env = dict(os.environ)
     env.pop("CUDA_VISIBLE_DEVICES", None)
     env.update(env_extra or {})
     r = subprocess.run([sys.executable, *args], cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stdout + r.stderr
-    return r.stdout
+    return (r.stdout, r.stderr) if stderr else r.stdout
 
 
 def _check_stdout(out, epochs):
@@ -94,3 +94,21 @@ def test_ddp_main_resnet50_cpu(tmp_path):
     from ddp_practice_amd.models import resnet50
 
     assert list(ck["model"]) == ["module." + k for k in resnet50(num_classes=10).state_dict()]
+
+
+@pytest.mark.parametrize("spawn", ["forkserver", "spawn"])
+def test_ddp_main_timer_includes_child_interpreter(tmp_path, spawn):
+    """``time elapsed`` has the reference's scope (/root/reference/ddp_main.py:175-177: the
+    parent times mp.spawn): the interpreter that imports torch for the ranks starts after
+    ``time_start`` -- with the fork server as with plain spawn (Missing 2)."""
+    out, err = _run([os.path.join(ROOT, "ddp_main.py"), "-e", "1", "--synthetic", "--train-samples", "256",
+                     "--test-samples", "64", "--cpu-procs", "2", "--amp-dtype", "fp32"], tmp_path,
+                    {"MASTER_PORT": str(free_port()), "DPA_MASTER_ADDR": "127.0.0.1", "DPA_PHASES": "1",
+                     "DPA_SPAWN": spawn}, stderr=True)
+    _check_stdout(out, 1)
+    t0 = [float(ln.split("wall=")[1]) for ln in err.splitlines() if "time_start wall=" in ln]
+    starts = [float(ln.split("wall=")[1]) for ln in err.splitlines() if "interpreter_start wall=" in ln]
+    assert len(t0) == 1 and len(starts) == 2, err
+    assert all(s >= t0[0] for s in starts), (t0, starts)
+    elapsed = float([ln for ln in out.splitlines() if ln.startswith("time elapsed: ")][0].split()[2])
+    assert elapsed >= max(starts) - t0[0]

@@ -27,15 +27,38 @@ def test_selftest_small_twoshot_bound_passes():
     assert len(set(outs[0][2])) == 1
 
 
-@pytest.mark.parametrize("bad,kind", [(-1, "none"), (1, "twoshot_err"), (0, "twoshot_raise")])
+@pytest.mark.parametrize("bad,kind", [(-1, "none"), (1, "twoshot_err"), (0, "twoshot_raise"),
+                                      (2, "twoshot_raise_late")])
 def test_twoshot_probe_decides_from_reduced_values(bad, kind):
-    """A two-shot failure on ONE rank (error word or exception) makes EVERY rank leave the
-    probe with bound 0 after the same collectives (the local error was checked
-    after the reduction, so ranks could attach with different bounds or hang)."""
+    """A two-shot failure on ONE rank (error word or exception, before or after the probe's
+    barrier) makes EVERY rank leave the probe with the failure bound -1 after the same
+    collectives (the local error was checked after the reduction, so ranks could
+    attach with different bounds or hang; ADVICE r3: a late exception added a barrier)."""
     outs = launch(_selftest_worker.run_probe, 3, (bad, kind), timeout=120)
     bests = {o[0] for o in outs}
     assert len(bests) == 1, outs
     if bad >= 0:
-        assert bests == {0}, outs
+        assert bests == {-1}, outs
+    else:
+        assert bests.pop() >= 0
     counts = outs[0][1]
     assert len(set(counts)) == 1, f"ranks issued different numbers of collectives: {counts}"
+
+
+@pytest.mark.parametrize("bad,kind", [(1, "twoshot_err"), (0, "twoshot_raise")])
+def test_failed_probe_keeps_engine_off(bad, kind):
+    """setup_xgmi must not attach an engine whose two-shot probe failed on any rank: the
+    error word would stay set and every later one-shot exchange would give up at once
+    (ADVICE r3, medium)."""
+    outs = launch(_selftest_worker.run_setup, 2, (bad, kind), timeout=120)
+    for status, attached, has_x, _ in outs:
+        assert status == "off (two-shot probe failed)", outs
+        assert not attached and not has_x, outs
+    assert len(set(outs[0][3])) == 1
+
+
+def test_healthy_probe_attaches_engine():
+    outs = launch(_selftest_worker.run_setup, 2, (-1, "none"), timeout=120)
+    for status, attached, has_x, _ in outs:
+        assert status.startswith("on ("), outs
+        assert attached and has_x, outs

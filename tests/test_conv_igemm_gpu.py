@@ -330,16 +330,14 @@ def test_dgrad_epilogue_bn_backward_sums(C, act, R, shape):
     invstd = torch.rand(Cc, generator=g) + 0.5
     gamma, beta = torch.randn(Cc, generator=g), torch.randn(Cc, generator=g) * 0.3
     bt = BNTap()
-    bt.x, bt.act = x, act
-    bt.save = torch.cat([mean, invstd]).to(DEV)
-    bt.weight, bt.bias = gamma.to(DEV), beta.to(DEV)
-    acc = None
+    y = acc = None
     if act == 1:
-        bt.y = torch.randn(N, Cc, H, W, generator=g).to(**bf).contiguous(memory_format=CL)
+        y = torch.randn(N, Cc, H, W, generator=g).to(**bf).contiguous(memory_format=CL)
         acc = torch.randn(N, Cc, H, W, generator=g).to(**bf).contiguous(memory_format=CL)
+    bt.bind_tensors(x, y, act, torch.cat([mean, invstd]).to(DEV), gamma.to(DEV), beta.to(DEV))
     acc0 = acc.clone() if acc is not None else None
     dx = dgrad_bn(dy, wt, bt, acc, R // 2)
-    assert dx is not None and bt.sums is not None and bt.grad_ptr == dx.data_ptr()
+    assert dx is not None and bt.matches(dx)
     ref = F.conv2d(dy.float(), wt.float(), None, 1, R // 2)
     if acc0 is not None:
         ref = ref + acc0.float()
