@@ -430,8 +430,8 @@ XgmiComm::XgmiComm(int rank, int world, int device, long long slot_bytes, double
     ts_ctr_ = static_cast<uint32_t*>(c2);
   }
   void* tk = nullptr;
-  DPA_CHECK_HIP(hipMalloc(&tk, kSites * sizeof(unsigned long long)));
-  DPA_CHECK_HIP(hipMemset(tk, 0, kSites * sizeof(unsigned long long)));
+  DPA_CHECK_HIP(hipMalloc(&tk, kSites * kTickLanes * kTickStride * sizeof(unsigned long long)));
+  DPA_CHECK_HIP(hipMemset(tk, 0, kSites * kTickLanes * kTickStride * sizeof(unsigned long long)));
   DPA_CHECK_HIP(hipDeviceSynchronize());
   ticks_ = static_cast<unsigned long long*>(tk);
   for (int i = 0; i < kMaxRanks; ++i) peers_.base[i] = nullptr;
@@ -593,7 +593,7 @@ XSite XgmiComm::site(int s) const {
   TORCH_CHECK(s >= 0 && s < kSites, "xgmi: site id out of range");
   XSite x;
   for (int p = 0; p < world_; ++p) x.base[p] = peers_.base[p] + site_off_ + (long long)s * kSiteBytes;
-  x.tick = ticks_ + s;
+  x.tick = ticks_ + (long long)s * kTickLanes * kTickStride;
   x.rank = rank_;
   x.world = world_;
   x.err = dev_words_;
@@ -619,10 +619,10 @@ __global__ void __launch_bounds__(256) site_probe_kernel(XSite xs, const float* 
                                                          float* __restrict__ out, int n) {
   __shared__ float vals[kSiteVals];
   unsigned long long tk = 0;
-  if (threadIdx.x == 0) tk = xsite_ticket(xs);
+  if (threadIdx.x == 0) tk = xsite_ticket(xs, (int)blockIdx.x);
   if ((int)threadIdx.x < n) vals[threadIdx.x] = in[threadIdx.x];
   __syncthreads();
-  xsite_exchange(xs, vals, n, tk, blockIdx.x == 0);
+  xsite_exchange(xs, vals, n, tk, (int)blockIdx.x);
   if ((int)threadIdx.x < n) out[(long long)blockIdx.x * n + threadIdx.x] = vals[threadIdx.x];
 }
 

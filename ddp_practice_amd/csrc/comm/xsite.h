@@ -16,11 +16,17 @@
 // value and tag land in one 8-byte store, no flag, no fence.
 //
 // Epoch without host involvement (graph-replayable, any grid size): every
-// workgroup of a consumer launch takes one ticket from this rank's site word
-// {epoch:32 | tickets:32} with a device-scope atomic; the workgroup that takes
-// the last ticket of the launch returns tickets to 0 and bumps the epoch.  All
-// workgroups of one launch therefore see the same epoch (launches of a site
-// are stream-ordered), and every rank issues the same sequence of launches.
+// workgroup of a consumer launch takes one ticket from one of this rank's
+// kTickLanes site words {epoch:32 | tickets:32} (lane = workgroup index mod the
+// lane count, each word on its own 256-B line) with a device-scope atomic; the
+// workgroup that takes the last ticket of its lane returns that lane's tickets
+// to 0 and bumps its epoch (lanes no workgroup maps to, in launches of fewer
+// than kTickLanes workgroups, are bumped by a workgroup that knows they are
+// idle).  Every lane therefore advances by exactly one per launch, all
+// workgroups of one launch see the same epoch (launches of a site are
+// stream-ordered), and every rank issues the same sequence of launches.
+// (One word per site serialised all of a launch's atomics at one address: 224
+// workgroups of the conv1 weight gradient waited ~2 us for their tickets.)
 // Reuse safety as for the one-shot kernel: a rank writes parity p of epoch e+2
 // only after its launch e+1 read every peer's e+1 row, which each peer wrote
 // after its own launch e had completed.
@@ -34,6 +40,8 @@ namespace dpa {
 namespace xgmi {
 
 constexpr int kMaxRanks = 8;
+constexpr int kTickLanes = 8;    // ticket words per site
+constexpr int kTickStride = 32;  // u64 between them (256 B: distinct lines / channels)
 constexpr int kSites = 8;                                             // sites per communicator
 constexpr int kSiteVals = 128;                                        // floats per rank row (>= 2C+1)
 constexpr long long kSiteSlotBytes = kSiteVals * 8LL;                 // granules
@@ -47,7 +55,8 @@ constexpr int kSiteGrad = kSites - 1;
 
 struct XSite {
   char* base[kMaxRanks] = {};            // this site's region in every rank's workspace (peer-mapped)
-  unsigned long long* tick = nullptr;    // this rank's {epoch | tickets} word; nullptr: site inactive
+  unsigned long long* tick = nullptr;    // this rank's {epoch | tickets} words (kTickLanes, kTickStride
+                                         // apart); nullptr: site inactive
   int rank = 0, world = 1;
   int* err = nullptr;                    // host-mapped: 1 timeout, 2 aborted
   const int* abort_flag = nullptr;
@@ -61,18 +70,27 @@ struct XSite {
 
 // Lane 0 of every workgroup, once per launch, as early as possible (the
 // returned word is only needed by xsite_exchange: the atomic's latency hides
-// behind the caller's slab loads).
-__device__ __forceinline__ unsigned long long xsite_ticket(const XSite& xs) {
-  return __hip_atomic_fetch_add(xs.tick, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// behind the caller's slab loads).  bid: the workgroup's index among the
+// launch's workgroups taking tickets on this site.
+__device__ __forceinline__ unsigned long long xsite_ticket(const XSite& xs, int bid) {
+  const int nblk = xs.nblk > 0 ? xs.nblk : (int)(gridDim.x * gridDim.y * gridDim.z);
+  const int nw = nblk < kTickLanes ? nblk : kTickLanes;
+  return __hip_atomic_fetch_add(xs.tick + (bid % nw) * kTickStride, 1ull, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Lane 0: the launch's epoch from its ticket (the last ticket of the launch
-// re-arms the word for the next launch).
-__device__ __forceinline__ uint32_t xsite_epoch(const XSite& xs, unsigned long long tk) {
-  const uint32_t nblk = xs.nblk > 0 ? (uint32_t)xs.nblk : gridDim.x * gridDim.y * gridDim.z;
-  if ((uint32_t)tk == nblk - 1u)  // last ticket of this launch: next launch, next epoch
-    __hip_atomic_fetch_add(xs.tick, (1ull << 32) - (unsigned long long)nblk, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+// Lane 0: the launch's epoch from its ticket (the last ticket of each lane re-arms
+// that lane's word for the next launch).
+__device__ __forceinline__ uint32_t xsite_epoch(const XSite& xs, unsigned long long tk, int bid) {
+  const int nblk = xs.nblk > 0 ? xs.nblk : (int)(gridDim.x * gridDim.y * gridDim.z);
+  const int nw = nblk < kTickLanes ? nblk : kTickLanes;
+  const int lane = bid % nw;
+  const uint32_t n_lane = (uint32_t)((nblk - lane + nw - 1) / nw);  // workgroups on this lane
+  if ((uint32_t)tk == n_lane - 1u)  // last ticket of this lane: next launch, next epoch
+    __hip_atomic_fetch_add(xs.tick + lane * kTickStride, (1ull << 32) - (unsigned long long)n_lane,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int w = bid + nblk; w < kTickLanes; w += nblk)  // lanes idle in this launch (nblk < kTickLanes)
+    __hip_atomic_fetch_add(xs.tick + w * kTickStride, 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return (uint32_t)(tk >> 32) + 1u;
 }
 
@@ -108,13 +126,14 @@ __device__ __forceinline__ float xsite_wait(const XSite& xs, const unsigned long
 
 // vals: n (<= kSiteVals, <= blockDim.x) floats of LDS holding this rank's local
 // row; replaced by the rank-ordered sum over all ranks.  tk: lane 0's ticket.
-// pusher: exactly one workgroup of the launch (its role's workgroup 0).  Called by every
-// thread of the workgroup; ends with a barrier.
+// bid: the workgroup's index in its role (the role's workgroup 0 pushes).  Called by
+// every thread of the workgroup; ends with a barrier.
 __device__ __forceinline__ void xsite_exchange(const XSite& xs, float* vals, int n, unsigned long long tk,
-                                               bool pusher) {
+                                               int bid) {
   __shared__ uint32_t ep_s;
   const int tid = threadIdx.x;
-  if (tid == 0) ep_s = xsite_epoch(xs, tk);
+  const bool pusher = bid == 0;
+  if (tid == 0) ep_s = xsite_epoch(xs, tk, bid);
   __syncthreads();
   if (tid < n) {
     const uint32_t ep = ep_s;

@@ -226,6 +226,10 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     defer_ = on;
   }
   bool deferred_pending() const { return deferred_; }
+  void set_require_inplace(bool on) {
+    std::lock_guard<std::mutex> g(mu_);
+    require_inplace_ = on;
+  }
   void consume_deferred() {
     std::lock_guard<std::mutex> g(mu_);
     deferred_ = false;
@@ -329,6 +333,10 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
         continue;
       }
       bk.inplace = false;
+      // a gradient still held as a producer's partial rows (a deferred slab, summed inside
+      // the fused optimizer launch) has no values yet: only the in-place bucket is valid then
+      TORCH_CHECK(!require_inplace_, "DDP: the deferred weight-gradient slab needs the zero-copy bucket "
+                                     "(every gradient of a bucket a view of one buffer, tiling it)");
       std::vector<at::Tensor> srcs;
       std::vector<int64_t> offs;
       const double inv_w = defer_ ? 1.0 : 1.0 / (double)comm_->world();  // deferred: averaged by the consumer
@@ -380,6 +388,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   bool hooks_ready_ = false;
   std::vector<std::weak_ptr<torch::autograd::Node>> hooked_;
   bool defer_ = false, deferred_ = false;  // see set_defer
+  bool require_inplace_ = false;           // see set_require_inplace (DDP.set_slab_sink)
   bool join_each_ = false;  // join every bucket immediately (no overlap)
   bool zero_copy_ = true;   // reduce tiled gradient regions in place (DPA_REDUCER_ZERO_COPY=0: always pack)
   std::vector<int64_t> order_;
@@ -408,6 +417,7 @@ void register_reducer(pybind11::module& m) {
       .def("set_record_order", &ddp::Reducer::set_record_order)
       .def("set_defer", &ddp::Reducer::set_defer)
       .def("deferred_pending", &ddp::Reducer::deferred_pending)
+      .def("set_require_inplace", &ddp::Reducer::set_require_inplace)
       .def("consume_deferred", &ddp::Reducer::consume_deferred)
       .def("flush_deferred", &ddp::Reducer::flush_deferred);
 }

@@ -171,8 +171,9 @@ __device__ __forceinline__ float strided_rowsum(const float* __restrict__ src, i
 // kernel had issued so far (a whole memory round trip ahead of the slab loads, head .s).
 template <int C>
 __device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, float* beta_s, float* mean_s,
-                                            float* istd_s, float* part, bool leader) {
+                                            float* istd_s, float* part, int bid) {
   const int tid = threadIdx.x, nthr = NTHR;
+  const bool leader = bid == 0;  // writes fstats / running stats (and pushes the SyncBN row)
   if (bp.train) {
     constexpr int RL = 2 * C + 1;
     const int G = nthr / RL;
@@ -194,7 +195,7 @@ __device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, flo
     // the SyncBN ticket is taken right after the slab loads are issued: its round trip overlaps
     // theirs (taken before them, its returned value's wait held the loads back)
     auto ticket = [&] {
-      if (xon && tid == 0) tk = xgmi::xsite_ticket(bp.xs);
+      if (xon && tid == 0) tk = xgmi::xsite_ticket(bp.xs, bid);
     };
     if (g < G) {
       part[tid] = strided_rowsum(bp.fslab, bp.nrows, RL, j, g, G, ticket);
@@ -211,7 +212,7 @@ __device__ __forceinline__ void bn_finalize(const BNParams& bp, float* sc_s, flo
       part[tid] = t;  // only this thread reads slot tid (its gg = 0 term) before the write
     }
     __syncthreads();
-    if (xon) xgmi::xsite_exchange(bp.xs, part, RL, tk, leader);  // local -> global sums (SyncBN)
+    if (xon) xgmi::xsite_exchange(bp.xs, part, RL, tk, bid);  // local -> global sums (SyncBN)
     if (tid < C) {
       const float n = part[2 * C];
       const float m1 = part[tid] / n;
@@ -331,8 +332,9 @@ __device__ __forceinline__ void colsum_rows(const float* __restrict__ src, int r
 // floats of LDS, sums: >= 2C floats of LDS.  Workgroup `leader` also writes
 // dgamma / dbeta from the local rows.  Ends with a barrier.
 template <int C, typename T>
-__device__ __forceinline__ void bn_bwd_coef(const BwdIn<T>& bi, float* coef, float* part, float* sums, bool leader) {
+__device__ __forceinline__ void bn_bwd_coef(const BwdIn<T>& bi, float* coef, float* part, float* sums, int bid) {
   const int tid = threadIdx.x;
+  const bool leader = bid == 0;
   float n = 0.f, f0 = 0.f, f1 = 0.f, shf = 0.f, gam = 0.f;
   if (tid < C) {  // issued before the reduction: latencies overlap
     n = bi.fstats[2 * C];
@@ -343,7 +345,7 @@ __device__ __forceinline__ void bn_bwd_coef(const BwdIn<T>& bi, float* coef, flo
   }
   const bool xon = bi.xs.active();
   unsigned long long tk = 0;
-  if (xon && tid == 0) tk = xgmi::xsite_ticket(bi.xs);  // latency hides behind the slab loads
+  if (xon && tid == 0) tk = xgmi::xsite_ticket(bi.xs, bid);  // latency hides behind the slab loads
   colsum_rows(bi.gsum, bi.grows, 2 * C, part, sums);
   if (xon) {
     // dgamma / dbeta are this rank's (DDP averages them); the coefficients use the global sums
@@ -351,7 +353,7 @@ __device__ __forceinline__ void bn_bwd_coef(const BwdIn<T>& bi, float* coef, flo
       bi.dgamma[tid] = sums[C + tid];
       bi.dbeta[tid] = sums[tid];
     }
-    xgmi::xsite_exchange(bi.xs, sums, 2 * C, tk, leader);
+    xgmi::xsite_exchange(bi.xs, sums, 2 * C, tk, bid);
   }
   if (tid < C) {
     const float m1 = f0 / n;
@@ -845,7 +847,7 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
         }
       }
       load_wpk();
-      bn_finalize<CIN>(pin.bn, sc_s, beta_s, mean_s, istd_s, part, bid == 0);
+      bn_finalize<CIN>(pin.bn, sc_s, beta_s, mean_s, istd_s, part, bid);
       DPA_STAMP(3);
 #pragma unroll
       for (int i = 0; i < IT8; ++i) {
@@ -887,7 +889,7 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
         }
       }
       load_wpk();
-      bn_finalize<CIN>(pin.bn, sc_s, beta_s, mean_s, istd_s, part, bid == 0);
+      bn_finalize<CIN>(pin.bn, sc_s, beta_s, mean_s, istd_s, part, bid);
       DPA_STAMP(3);
       // the pooled map / index / xhat outputs (for the backward) are written by all
       // nsplit workgroups of the image, each its share (was: split 0 alone)
@@ -917,7 +919,7 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
       st.load(bin, b);
       DPA_STAMP(8);
       load_wpk();
-      bn_bwd_coef<CIN, T>(bin, coef, part, sums, bid == 0);
+      bn_bwd_coef<CIN, T>(bin, coef, part, sums, bid);
       load_epi();
       DPA_STAMP(3);
       st.emit(coef, [&](int h, int ww, int c0, uint4 q00, uint4 q01, uint4 q10, uint4 q11) {
@@ -931,7 +933,7 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
       st.load(bin, b);
       DPA_STAMP(8);
       load_wpk();
-      bn_bwd_coef<CIN, T>(bin, coef, part, sums, bid == 0);
+      bn_bwd_coef<CIN, T>(bin, coef, part, sums, bid);
       load_epi();
       DPA_STAMP(3);
       st.emit(coef, [&](int c, int h, int ww, T v00, T v01, T v10, T v11) {
@@ -1395,7 +1397,7 @@ conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __r
     } else {  // input rows r0-2 .. r0+ROWS+1 -> xpad (kw copies after the barrier below)
       stage_xpad();
     }
-    bn_bwd_coef<COUT, T>(bin, coef, part, sums, bid == 0);
+    bn_bwd_coef<COUT, T>(bin, coef, part, sums, bid);
     DPA_STAMP(3);
     st.emit(coef, [&](int co, int h, int ww, T v00, T v01, T v10, T v11) {
       dyl[co * DYS + h * WP + ww] = v00;

@@ -68,7 +68,7 @@ head_fwd_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__ 
       bot[i] = src[W / 2];
     }
   }
-  bn_finalize<C>(bn, sc_s, beta_s, mean_s, istd_s, part, b == 0);
+  bn_finalize<C>(bn, sc_s, beta_s, mean_s, istd_s, part, b);
   float pf[IT];
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
@@ -274,7 +274,10 @@ void conv2_fwd(at::Tensor y1, c10::optional<at::Tensor> fslab1, at::Tensor fstat
   if (train) TORCH_CHECK(fslab2.has_value() && fslab2->numel() == (int64_t)B * 2 * cb::fslab_row(32));
   if (B == 0) return;
   BNParams bp = bn_params(fslab1, fstats1, g1, b1, rm1, rv1, nbt1, momentum, eps, train, 16);
-  if (train) bp.xs = site_of(xc, xgmi::kSiteFwd1);
+  if (train) {
+    bp.xs = site_of(xc, xgmi::kSiteFwd1);
+    bp.xs.nblk = B * 2;  // the grid (ns workgroups per image)
+  }
   constexpr int ns = 2;
   hipStream_t stream = cur_stream();
   with_t(dt_of(y1), [&](auto tag) {
@@ -473,23 +476,133 @@ void conv2_dgrad(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx
 constexpr int WG2_ROWS_ = 4;
 constexpr int WG1_ROWS_ = 4;
 int64_t wgrad_bn_rows(int64_t layer, int64_t B);
+// fc weight / bias gradient of the per-image head (csrc/kernels/convnet_head.hip): the head's
+// one reduction over the batch, computed by extra workgroups of the conv2 backward launch
+// (which needs none of it) instead of on the head's critical path:
+//   dW[n][k] = sum_b dls[b][n] * p2[b][k],   db[n] = sum_b dls[b][n]
+// dls = d(scale * loss)/dlogits and p2 = the pooled features, both in the storage dtype
+// (autocast's operands); fp32 accumulation in batch order.
+template <typename T>
+struct FcW {
+  const T* dls;  // [B][N]
+  const T* p2;   // [B][K]
+  float* dw;     // [N][K]
+  float* db;     // [N]
+  int B = 0, N = 0;
+};
+constexpr int FC_K = 32 * 49;
+constexpr int FC_COLS = cb::NTHR;  // columns per workgroup, one per lane
+constexpr int FC_BMAX = 64, FC_NMAX = 16;
+constexpr int FC_BLOCKS = (FC_K + FC_COLS - 1) / FC_COLS;
+
+template <typename T>
+__device__ __forceinline__ void fc_wgrad_body(const FcW<T>& f, int wg) {
+  __shared__ __attribute__((aligned(16))) float dl_s[FC_BMAX][FC_NMAX];
+  const int tid = threadIdx.x;
+  const int col = wg * FC_COLS + tid, cc = min(col, FC_K - 1);
+  const int B = f.B, N = f.N;
+  // the dls table (B x N, zero-padded to 16 classes) through LDS, broadcast reads below
+  for (int e = tid; e < FC_BMAX * FC_NMAX; e += cb::NTHR) {
+    const int b = e / FC_NMAX, n = e % FC_NMAX;
+    const float v = Cvt<T>::to_f(f.dls[min(b, B - 1) * N + min(n, N - 1)]);
+    dl_s[b][n] = (b < B && n < N) ? v : 0.f;
+  }
+  float acc[FC_NMAX];
+#pragma unroll
+  for (int n = 0; n < FC_NMAX; ++n) acc[n] = 0.f;
+  __syncthreads();
+  for (int b0 = 0; b0 < B; b0 += 32) {  // 32 rows in flight per batch (one batch at B <= 32)
+    float pv[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const int b = b0 + u;
+      pv[u] = Cvt<T>::to_f(f.p2[(size_t)min(b, B - 1) * FC_K + cc]) * (b < B ? 1.f : 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const f32x4* row = reinterpret_cast<const f32x4*>(dl_s[min(b0 + u, FC_BMAX - 1)]);
+#pragma unroll
+      for (int q = 0; q < FC_NMAX / 4; ++q) {
+        const f32x4 d = row[q];
+        acc[4 * q + 0] += d[0] * pv[u];
+        acc[4 * q + 1] += d[1] * pv[u];
+        acc[4 * q + 2] += d[2] * pv[u];
+        acc[4 * q + 3] += d[3] * pv[u];
+      }
+    }
+  }
+  if (col < FC_K) {
+#pragma unroll
+    for (int n = 0; n < FC_NMAX; ++n)
+      if (n < N) f.dw[(size_t)n * FC_K + col] = acc[n];
+  }
+  if (wg == 0 && tid < N) {
+    float a = 0.f;
+    for (int b = 0; b < B; ++b) a += dl_s[b][tid];
+    f.db[tid] = a;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(cb::NTHR) fc_wgrad_kernel(FcW<T> f) { fc_wgrad_body<T>(f, (int)blockIdx.x); }
+
 template <typename T>
 __global__ void __launch_bounds__(cb::NTHR)
 conv2_bwd_kernel(const T* __restrict__ wpk_d, T* __restrict__ dp1, BwdIn<T> bi_d, BwdEpi<T> ep,
-                 const T* __restrict__ p1, float* __restrict__ wslab2, BwdIn<T> bi_w, int ndg) {
+                 const T* __restrict__ p1, float* __restrict__ wslab2, BwdIn<T> bi_w, int ndg, int nwg, FcW<T> fw) {
   constexpr int nsw = (14 + WG2_ROWS_ - 1) / WG2_ROWS_;
-  if ((int)blockIdx.x < ndg)
+  const int bid = (int)blockIdx.x;
+  if (bid < ndg)
     cb::conv5x5_body<T, 32, 16, 14, 14, 2, 2, 1, 1>(nullptr, nullptr, nullptr, dp1, nullptr, nullptr, nullptr,
-                                                    kDgradSplit, PoolIn<T>{}, bi_d, ep, wpk_d, cb::WPack<T>{},
-                                                    (int)blockIdx.x);
+                                                    kDgradSplit, PoolIn<T>{}, bi_d, ep, wpk_d, cb::WPack<T>{}, bid);
+  else if (bid < ndg + nwg)
+    cb::conv5x5_wgrad_body<T, 16, 32, 14, 14, WG2_ROWS_, 2>(p1, nullptr, wslab2, nsw, bi_w, bid - ndg);
   else
-    cb::conv5x5_wgrad_body<T, 16, 32, 14, 14, WG2_ROWS_, 2>(p1, nullptr, wslab2, nsw, bi_w, (int)blockIdx.x - ndg);
+    fc_wgrad_body<T>(fw, bid - ndg - nwg);
+}
+
+template <typename T>
+static FcW<T> fc_args(const c10::optional<at::Tensor>& dls, const c10::optional<at::Tensor>& p2,
+                      const c10::optional<at::Tensor>& dw, const c10::optional<at::Tensor>& db, int B, at::ScalarType st) {
+  FcW<T> f{};
+  if (!dls.has_value()) return f;
+  TORCH_CHECK(p2.has_value() && dw.has_value() && db.has_value(), "fc weight gradient: dls, p2, dw, db go together");
+  DPA_CHECK_INPUT(*dls); DPA_CHECK_INPUT(*p2); DPA_CHECK_INPUT(*dw); DPA_CHECK_INPUT(*db);
+  const int N = (int)(dls->numel() / std::max(B, 1));
+  TORCH_CHECK(dls->numel() == (int64_t)B * N && N >= 1 && N <= FC_NMAX && B <= FC_BMAX, "fc weight gradient: dls [B][N <= 16]");
+  TORCH_CHECK(dls->scalar_type() == st && p2->scalar_type() == st && p2->numel() == (int64_t)B * FC_K);
+  TORCH_CHECK(dw->scalar_type() == at::kFloat && dw->numel() == (int64_t)N * FC_K && db->scalar_type() == at::kFloat &&
+              db->numel() == N, "fc weight gradient: fp32 dw [N][1568], db [N]");
+  f.dls = dptr<T>(*dls);
+  f.p2 = dptr<T>(*p2);
+  f.dw = dw->data_ptr<float>();
+  f.db = db->data_ptr<float>();
+  f.B = B;
+  f.N = N;
+  return f;
+}
+
+// fc weight / bias gradient as its own launch (fp32 / split-backward paths)
+void fc_wgrad(at::Tensor dls, at::Tensor p2, at::Tensor dw, at::Tensor db) {
+  const int B = (int)(p2.numel() / FC_K);
+  if (B == 0) return;
+  with_t(dt_of(p2), [&](auto tag) {
+    typedef decltype(tag) T;
+    FcW<T> f = fc_args<T>(dls, p2, dw, db, B, p2.scalar_type());
+    hipLaunchKernelGGL(fc_wgrad_kernel<T>, dim3(FC_BLOCKS), dim3(cb::NTHR), 0, cur_stream(), f);
+  });
+  DPA_CHECK_LAUNCH();
 }
 
 // [pool2/ReLU2/BN2 backward] -> {conv2 data grad -> dp1 (+BN1 partial sums), conv2 weight-grad partials}
+// (+ with fc_*: the fc weight / bias gradient of the per-image head in extra workgroups).
+// gsum2: rows of BN2 backward sums ([S1 | S2] per row, summed here); lsum2: this rank's rows
+// when gsum2 was all-reduced; dg2 / dbe2: BN2's dgamma / dbeta, written from this rank's sums.
 void conv2_bwd(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx2, at::Tensor fstats2,
                at::Tensor gsum2, at::Tensor g2, double eps2, at::Tensor dp1, at::Tensor idx1, at::Tensor xh1,
-               at::Tensor bslab1, at::Tensor p1, at::Tensor wslab2, XcPtr xc) {
+               at::Tensor bslab1, at::Tensor p1, at::Tensor wslab2, XcPtr xc, c10::optional<at::Tensor> lsum2,
+               c10::optional<at::Tensor> dg2, c10::optional<at::Tensor> dbe2, c10::optional<at::Tensor> fc_dls,
+               c10::optional<at::Tensor> fc_p2, c10::optional<at::Tensor> fc_dw, c10::optional<at::Tensor> fc_db) {
   DPA_CHECK_INPUT(y2); DPA_CHECK_INPUT(dp1); DPA_CHECK_INPUT(wpk_d); DPA_CHECK_INPUT(p1); DPA_CHECK_INPUT(wslab2);
   TORCH_CHECK(wpk_d.numel() == cb::W2D_LEN && wpk_d.scalar_type() == y2.scalar_type(),
               "packed conv2 data-grad weights");
@@ -498,29 +611,36 @@ void conv2_bwd(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx2,
   TORCH_CHECK(dp1.numel() == (int64_t)B * 16 * 196 && idx1.numel() == dp1.numel() && xh1.numel() == dp1.numel());
   TORCH_CHECK(p1.numel() == dp1.numel() && p1.scalar_type() == y2.scalar_type());
   TORCH_CHECK(bslab1.numel() == dgrad2_rows(B) * 32, "BN1 partial-sum slab size");
+  TORCH_CHECK(dg2.has_value() == dbe2.has_value(), "conv2_bwd: dg2 and dbe2 go together");
+  if (dg2.has_value()) TORCH_CHECK(dg2->numel() == 32 && dbe2->numel() == 32 && dg2->scalar_type() == at::kFloat);
+  if (xc) TORCH_CHECK(!lsum2.has_value(), "fused SyncBN exchange: gsum2 must be this rank's rows (no lsum2)");
   const int ndg = B * kDgradSplit, nwg = (int)wgrad_bn_rows(2, B);
   TORCH_CHECK(wslab2.numel() == (int64_t)nwg * (32 * 400 + 32), "wgrad slab size");
   if (B == 0) return;
   with_t(dt_of(y2), [&](auto tag) {
     typedef decltype(tag) T;
-    BwdIn<T> bd = bwd_in<T>(dp2, idx2, y2, fstats2, gsum2, c10::nullopt, g2, eps2, 32, c10::nullopt, c10::nullopt);
+    BwdIn<T> bd = bwd_in<T>(dp2, idx2, y2, fstats2, gsum2, lsum2, g2, eps2, 32, dg2, dbe2);
     BwdIn<T> bw = bd;
+    bw.dgamma = bw.dbeta = nullptr;  // one writer: the data-gradient role's workgroup 0
     bd.xs = site_of(xc, xgmi::kSiteBwd2Dgrad);
     bw.xs = site_of(xc, xgmi::kSiteBwd2Wgrad);
     bd.xs.nblk = ndg;  // each role's workgroups take tickets on their own site
     bw.xs.nblk = nwg;
     BwdEpi<T> ep{idx1.data_ptr<uint8_t>(), dptr<T>(xh1), bslab1.data_ptr<float>()};
+    FcW<T> fw = fc_args<T>(fc_dls, fc_p2, fc_dw, fc_db, B, y2.scalar_type());
+    const int nfc = fc_dls.has_value() ? FC_BLOCKS : 0;
     if constexpr (std::is_same<T, float>::value) {
-      // fp32 tiles: the two roles' LDS (173 KB) exceed one CU's 160 KB -> two launches
+      // fp32 tiles: the two roles' LDS (173 KB) exceed one CU's 160 KB -> separate launches
       bd.xs.nblk = bw.xs.nblk = 0;
       hipLaunchKernelGGL((cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1, 1>), dim3(ndg), dim3(cb::NTHR), 0,
                          cur_stream(), nullptr, nullptr, nullptr, dptr<T>(dp1), nullptr, nullptr, nullptr,
                          kDgradSplit, PoolIn<T>{}, bd, ep, dptr<T>(wpk_d), cb::WPack<T>{});
       hipLaunchKernelGGL((cb::conv5x5_wgrad_kernel<T, 16, 32, 14, 14, WG2_ROWS_, 2>), dim3(nwg), dim3(cb::NTHR), 0,
                          cur_stream(), dptr<T>(p1), nullptr, wslab2.data_ptr<float>(), nwg / B, bw);
+      if (nfc) hipLaunchKernelGGL(fc_wgrad_kernel<T>, dim3(nfc), dim3(cb::NTHR), 0, cur_stream(), fw);
     } else {
-      hipLaunchKernelGGL(conv2_bwd_kernel<T>, dim3(ndg + nwg), dim3(cb::NTHR), 0, cur_stream(), dptr<T>(wpk_d),
-                         dptr<T>(dp1), bd, ep, dptr<T>(p1), wslab2.data_ptr<float>(), bw, ndg);
+      hipLaunchKernelGGL(conv2_bwd_kernel<T>, dim3(ndg + nwg + nfc), dim3(cb::NTHR), 0, cur_stream(), dptr<T>(wpk_d),
+                         dptr<T>(dp1), bd, ep, dptr<T>(p1), wslab2.data_ptr<float>(), bw, ndg, nwg, fw);
     }
   });
   DPA_CHECK_LAUNCH();
@@ -759,7 +879,7 @@ bool sites_resident(int64_t B, at::ScalarType st) {
          co_resident(reinterpret_cast<const void*>(&head_fwd_kernel<T, 32, 14, 14, 64>), (int)B, HF, 0);
     chk(reinterpret_cast<const void*>(&cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1, 1>), B * kDgradSplit);
     if constexpr (!std::is_same<T, float>::value)
-      chk(reinterpret_cast<const void*>(&conv2_bwd_kernel<T>), B * kDgradSplit + wgrad_bn_rows(2, B));
+      chk(reinterpret_cast<const void*>(&conv2_bwd_kernel<T>), B * kDgradSplit + wgrad_bn_rows(2, B) + FC_BLOCKS);
     chk(reinterpret_cast<const void*>(&cb::conv5x5_wgrad_kernel<T, 16, 32, 14, 14, WG2_ROWS, 2>),
         wgrad_bn_rows(2, B));
     chk(reinterpret_cast<const void*>(&cb::conv5x5_wgrad_kernel<T, 1, 16, 28, 28, WG1_ROWS, 2>),
@@ -800,6 +920,7 @@ void register_convnet_fused(pybind11::module& m) {
   s.attr("W2D_LEN") = cb::W2D_LEN;
   s.def("conv2_dgrad", &cnf::conv2_dgrad);
   s.def("conv2_bwd", &cnf::conv2_bwd);
+  s.def("fc_wgrad", &cnf::fc_wgrad);
   s.def("conv_wgrad_bn", &cnf::conv_wgrad_bn);
   s.def("wgrad_bn_rows", &cnf::wgrad_bn_rows);
   s.def("sites_resident", &cnf::sites_resident);

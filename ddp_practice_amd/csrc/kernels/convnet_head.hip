@@ -2,7 +2,7 @@
 //
 //   [BN2 finalize -> BN -> ReLU -> 2x2 max-pool -> flatten -> Linear]     (forward)
 //   -> CrossEntropy(mean) on the logits + d(scale * loss)/dlogits          (loss)
-//   -> Linear backward (dp2, dW_fc, db_fc) + the BN2 backward sums        (backward)
+//   -> Linear input gradient dp2 + the BN2 backward sums of this image     (backward)
 //
 // Reference ops: /root/reference/origin_main.py:16-24,29-30 (BN2/ReLU/pool2, reshape,
 // fc) and ddp_main.py:89,91 (CrossEntropyLoss on the logits, scaler.scale(loss).backward()).
@@ -12,24 +12,25 @@
 // images; ops/convnet_fused.py) -- the loss call and the head backward then
 // find their results ready and launch nothing.
 //
-// Decomposition: one workgroup per BN2 channel c (C = 32).  A channel owns 49
-// of the 1568 fc inputs, so it computes its BN / ReLU / pool slice and a K = 49
-// split of the logits (MFMA 16x16x32: rows = images, cols = classes).  The
-// partial logits are stored write-through (`sc1`) and every workgroup takes one
-// agent-scope ticket (MI355X_MICROARCH.md "Valid forms" row 1: no release /
-// acquire fence).  Without a backward the last arriver adds the bias, rounds the
-// logits to the storage dtype and runs the loss (16 lanes per row, as head.hip
-// ce_fwd_kernel: same formula, same rounding).  When an active GradScaler
-// supplies the scale, the last ticket releases every workgroup, each of which
-// sums the partials and runs the same loss itself (fixed order: identical
-// d(scale*loss)/dlogits everywhere, no second hand-off) and does its channel's
-// share of the fc backward on MFMA:
-//   dp2[b, c*49 + j]   = sum_n dls[b, n] * W[n, c*49 + j]       (B x 49, K = N)
-//   dW[n, c*49 + j]    = sum_b dls[b, n] * p2[b, c*49 + j]      (N x 49, K = B)
-// plus the BN2 backward sums of channel c (complete: the channel is whole here).
-// All 32 workgroups of the launch must be co-resident (they wait for the last
-// arriver): 32 << 256 CUs, checked on the host (co_resident); every wait is
-// bounded and sets the error word.
+// Decomposition: ONE WORKGROUP PER IMAGE, and no workgroup waits for another.
+// An image's row of the head is independent of every other row except for
+// three batch reductions, each moved off the critical path:
+//   * the loss mean: every workgroup adds its row loss to ONE 64-bit word with a
+//     single atomic, as an integer (fixed point, 2^-24), together with an arrival
+//     count; the workgroup whose add completes the count holds the exact total in
+//     the value its atomic returned (integer addition is associative: the result
+//     does not depend on the arrival order) and writes the loss.  No partial
+//     store, no fence, no wait, no second hand-off;
+//   * the fc weight / bias gradient (a K = batch reduction): computed by extra
+//     workgroups of the next launch (conv2_bwd, csrc/kernels/convnet_fused.hip
+//     fc_wgrad_body), which overlap the conv2 backward;
+//   * the BN2 backward sums: one row of per-channel [S1 | S2] per image, reduced
+//     by the consumer kernel's prologue (cb::bn_bwd_coef, like every other slab).
+// The mean's row count (non-ignored targets) comes from one ballot over the
+// batch's labels, so d(loss)/dlogits of a row is complete inside its workgroup.
+// Round 3's channel-per-workgroup head (32 workgroups, partial logits handed to a
+// last arriver and back: two cross-workgroup round trips on every workgroup's
+// path) took 15.5 us of the 57.7 us step (profiles/r3_head_granule_vs_ticket_ab.txt).
 #include "comm/xgmi.h"
 #include "convblock_impl.h"
 
@@ -42,411 +43,230 @@ using cb::Pair2;
 
 constexpr int NT = 256;    // 4 waves
 constexpr int C = 32, H = 14, W = 14, HO = 7, WO = 7, PP = 49, K = C * PP;
-constexpr int BMAX = 64;   // images (4 MFMA row tiles)
-constexpr int NMAX = 16;   // classes (one MFMA column tile)
-constexpr int KP = 64;     // 49 fc inputs per channel, padded to 2 MFMA k-steps
+constexpr int BMAX = 64;   // images (one ballot counts the batch's rows)
+constexpr int NMAX = 16;   // classes
+constexpr int IT = (K + NT - 1) / NT;  // pooled features per lane (7)
 
-// state: int64[4] zero-initialised once: [0] {generation:32 | tickets:32} (the last
-// ticket stores (generation + 1) << 32: re-arm and release), [1] unused, [2] error word
-struct HeadStep {
+// loss word (state[0], zero-initialised once; the completing workgroup re-arms it):
+// [63:57] arrivals | [56:50] rows whose loss is out of range | [49:0] sum over the
+// counted rows of round((row loss + 1) * 2^24) (the +1 keeps rounding-negative rows,
+// -1e-7 when one logit dominates, representable)
+constexpr int kArrShift = 57, kBadShift = 50;
+constexpr unsigned long long kSumMask = (1ull << kBadShift) - 1ull;
+constexpr double kFix = 16777216.0;   // 2^24
+constexpr float kRowMax = 1048575.f;  // 2^20 - 1: 64 rows of (loss + 1) * 2^24 fit in 50 bits
+
+struct HeadRow {
   const int64_t* target;
   int64_t ignore_index;
   float smoothing;
-  const float* scale;   // GradScaler scale (null: no scaler -> no speculative backward)
-  float* part;          // [C][B][NMAX] partial logits (write-through)
-  unsigned long long* state;
+  const float* scale;   // GradScaler scale (always valid; has_scale = 0: unused)
+  int has_scale;
+  unsigned long long* state;  // [0] loss word
   float* loss;          // [2]: loss, loss * scale
   float* dlog;          // [B][N] (softmax - onehot) / count, f32
   void* dls;            // [B][N] dlog * scale, storage dtype (null without scaler)
-  float* dlsf;          // [B][N] f32 scratch of the earlier two-hand-off protocol (unused; its
-                        // presence still selects the speculative backward on the host)
-  int do_bwd;
-  void* dp2;            // [B][K] storage dtype
-  float* dwfc;          // [N][K]
-  float* dbfc;          // [N]
-  float* dgamma;        // [C]
-  float* dbeta;         // [C]
-  float* bsum;          // [2C]: S1 | S2 (BN2 backward sums, this rank)
-  long long timeout_ticks;
+  void* dp2;            // [B][K] storage dtype (null: forward + loss only)
+  float* bsum;          // [B][2C] BN2 backward sums of each image (S1 | S2)
 };
 
-template <typename T>
-__device__ __forceinline__ void st_wt(float* p, float v) {  // write-through 4-B store (global_store_dword sc1)
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_wt(const float* p) {     // L1-bypassing load (global_load_dword sc1)
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// LDS-only barrier: __syncthreads() is a workgroup fence whose vmcnt(0) would make every
+// wave wait here for its global stores (pooled outputs, dp2) and the loss atomic to retire
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
 }
 
-template <int GL>
-__device__ __forceinline__ float gmax(float v) {
-#pragma unroll
-  for (int o = GL / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-template <int GL>
+template <int G>
 __device__ __forceinline__ float gsum(float v) {
 #pragma unroll
-  for (int o = GL / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
 
-template <typename T, int BM>  // BM: images the tiles are sized for (32 or BM)
+template <typename T, int NM>  // NM: classes the register tiles are sized for (>= N)
 __global__ void __launch_bounds__(NT)
-head_step_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__ wfc, const float* __restrict__ bfc,
-                 T* __restrict__ logits, T* __restrict__ p_out, uint8_t* __restrict__ idx_out,
-                 T* __restrict__ xh_out, int B, int N, HeadStep hs) {
-  typedef MM<T> mm;
-  typedef T E;  // operand tiles in the storage dtype (MM<T>::ld reads 8 of them)
+head_row_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__ wfc, const float* __restrict__ bfc,
+                T* __restrict__ logits, T* __restrict__ p_out, uint8_t* __restrict__ idx_out,
+                T* __restrict__ xh_out, int B, int N, HeadRow hr) {
   typedef typename Pair2<T>::type P;
-  constexpr int ITB = (BM * PP + NT - 1) / NT;  // pooled outputs per lane
   __shared__ float sc_s[C], beta_s[C], mean_s[C], istd_s[C];
   __shared__ float part_s[NT];
-  // MFMA operand tiles (row-major, k contiguous: every fragment is one 16-B read)
-  __shared__ __attribute__((aligned(16))) E pcl[BM * KP];   // A fwd: p2 slice [b][j]
-  // transposed tiles' rows padded by 16 B: their column-wise 2-byte writes (lanes along
-  // the rows) then spread over the banks instead of hitting one bank pair
-  constexpr int PCT_S = BM + 8, WDL_S = 32 + 8, DLT_S = BM + 8;
-  __shared__ __attribute__((aligned(16))) E pct[KP * PCT_S];  // B dW: p2 slice as [j][b]
-  __shared__ __attribute__((aligned(16))) E wcl[NMAX * KP];   // B fwd: W slice [n][j]
-  __shared__ __attribute__((aligned(16))) E wdl[KP * WDL_S];  // B dp2: W slice [j][n] (k = n padded to 32)
-  __shared__ __attribute__((aligned(16))) E dll[BM * 32];   // A dp2: dls [b][n]
-  __shared__ __attribute__((aligned(16))) E dlt[NMAX * DLT_S]; // A dW: dls as [n][b]
-  __shared__ float lg_s[BM * NMAX];                         // logits (rounded) / dls, f32
-  __shared__ float dd_s[BM * NMAX];                         // (softmax - onehot) / count
-  __shared__ int64_t tgt_s[BM];
-  __shared__ float bias_s[NMAX];
-  __shared__ E wdummy_s[2];
-  __shared__ uint8_t ix_s[BM * PP];
-  __shared__ float xh_s[BM * PP];
-  __shared__ float red[2][NT / 64];
-  __shared__ unsigned long long tk_s;
-  __shared__ int cnt_s;
+  __shared__ float red[NT / 64][NM];
+  __shared__ float gs[2][IT * NT];  // per pooled feature: g, g * xhat (BN2 backward sums)
 
-  const int tid = threadIdx.x, c = blockIdx.x;
-  const int lane = tid & 63, wv = tid >> 6, r = lane & 15, q = lane >> 4;
-  const int NPO = B * PP;  // pooled outputs of this channel
+  const int tid = threadIdx.x, b = blockIdx.x;
+  const int lane = tid & 63, wv = tid >> 6;
 
   DPA_STAMP(0);
-  // 1. loads: this channel's pre-BN maps (two row pairs per pooled output) and W slice
-  // Every load below is unconditional (clamped index, the value discarded where out of
-  // range): a conditional load into a register array made hipcc branch around each load
-  // and wait vmcnt(0) after it -- one memory round trip per load (head_step .s, ROCm 7.2).
-  P top[ITB], bot[ITB];
+  // 1. every load of the kernel up front.  Unconditional (clamped index, discarded by a
+  //    multiply): a conditional load into a register array is branched around and waited
+  //    for one by one (head_step .s, ROCm 7.2).
+  const T* yb = y + (size_t)b * C * H * W;
+  P top[IT], bot[IT];
 #pragma unroll
-  for (int i = 0; i < ITB; ++i) {
-    const int e = min(tid + i * NT, NPO - 1);
-    const int b = e / PP, j = e % PP, ho = j / WO, wo = j % WO;
-    const P* src = reinterpret_cast<const P*>(y + (((size_t)b * C + c) * H + 2 * ho) * W + 2 * wo);
+  for (int i = 0; i < IT; ++i) {
+    const int k = min(tid + i * NT, K - 1);
+    const int c = k / PP, j = k % PP, ho = j / WO, wo = j % WO;
+    const P* src = reinterpret_cast<const P*>(yb + ((size_t)c * H + 2 * ho) * W + 2 * wo);
     top[i] = src[0];
     bot[i] = src[W / 2];
   }
-  // the loss' inputs, loaded by every workgroup now (only the last arriver uses them, but
-  // it cannot know it is last yet): no dependent global load on its serial path later
-  const int64_t tgt_ld = hs.target[min(tid, B - 1)];
-  const float bias_ld = bfc[min(tid, N - 1)];
-  const int64_t tgt_r = tid < B ? tgt_ld : hs.ignore_index;
-  const float bias_r = tid < N ? bias_ld : 0.f;
-  const float scale_r = hs.scale != nullptr ? hs.scale[0] : 0.f;
-  constexpr int WIT = (NMAX * PP + NT - 1) / NT;
-  float wv_[WIT];
+  float wq[NM][IT];  // fc weights of this lane's features, every class
 #pragma unroll
-  for (int i = 0; i < WIT; ++i) {
-    const int e = tid + i * NT;
-    const int n = e / PP, j = e % PP;
-    const float v = wfc[(size_t)min(n, N - 1) * K + c * PP + j];  // unconditional (see above)
-    // a multiply, not a select: with a select (or a guarded use below) hipcc re-branches the
-    // load by the condition and waits for it inside the branch
-    wv_[i] = v * ((e < NMAX * PP && n < N) ? 1.f : 0.f);
+  for (int n = 0; n < NM; ++n) {
+    const float* wr = wfc + (size_t)min(n, N - 1) * K;
+#pragma unroll
+    for (int i = 0; i < IT; ++i) wq[n][i] = wr[min(tid + i * NT, K - 1)];
   }
-  DPA_STAMP(8);
-  // zero the tiles' padding (rows past B, k past 49 / N)
-  {  // 16-B LDS writes (every tile is 16-B aligned and a whole number of 16-B chunks)
-    auto zero = [&](E* t, int n) {
-      for (int e = tid; e < n * (int)sizeof(E) / 16; e += NT) reinterpret_cast<f32x4*>(t)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
-    };
-    static_assert((BM * KP) % 8 == 0 && (KP * PCT_S) % 8 == 0 && (BM * 32) % 8 == 0 && (KP * WDL_S) % 8 == 0 &&
-                  (NMAX * DLT_S) % 8 == 0 && (NMAX * KP) % 8 == 0, "head tiles: whole 16-B chunks");
-    zero(pcl, BM * KP);
-    zero(pct, KP * PCT_S);
-    zero(dll, BM * 32);
-    zero(wdl, KP * WDL_S);
-    zero(dlt, NMAX * DLT_S);
-    zero(wcl, NMAX * KP);
-  }
-  DPA_STAMP(9);
-  if (tid < BM) tgt_s[tid] = tgt_r;
-  if (tid < NMAX) bias_s[tid] = bias_r;
-  DPA_STAMP(10);
-  cb::bn_finalize<C>(bn, sc_s, beta_s, mean_s, istd_s, part_s, c == 0);  // ends with a barrier
+  float bias[NM];
+#pragma unroll
+  for (int n = 0; n < NM; ++n) bias[n] = bfc[min(n, N - 1)];
+  const int64_t tgt_lane = hr.target[min(lane, B - 1)];  // the batch's labels, one per lane
+  const int64_t tgt = hr.target[b];
+  const float scv = hr.scale[0];
   DPA_STAMP(1);
-  // W slice -> tiles
-#pragma unroll
-  for (int i = 0; i < WIT; ++i) {  // unconditional stores (lanes past the slice write a dummy word)
-    const int e = tid + i * NT;
-    const bool ok = e < NMAX * PP;
-    const int ec = ok ? e : 0, n = ec / PP, j = ec % PP;
-    const E wq = Cvt<T>::from_f(wv_[i]);
-    *(ok ? &wcl[n * KP + j] : &wdummy_s[0]) = wq;
-    *(ok ? &wdl[j * WDL_S + n] : &wdummy_s[1]) = wq;
-  }
-  // 2. BN -> ReLU -> 2x2 max of this channel; pooled value, argmax|relu index, xhat.
-  //    LDS now; the global copies (read by later kernels) are written after the ticket,
-  //    so the hand-off's vmcnt(0) drains only the partial-logit stores
-  T pvr[ITB], xqr[ITB];
-  uint8_t ixr[ITB];
-  {
-    const float sc = sc_s[c], bt = beta_s[c], mn = mean_s[c], is = istd_s[c];
-#pragma unroll
-    for (int i = 0; i < ITB; ++i) {
-      const int e = tid + i * NT;
-      if (e < NPO) {
-        const int b = e / PP, j = e % PP;
-        float best, xh;
-        int bi;
-        cb::bn_relu_max4x<T>(top[i], bot[i], sc, bt, mn, is, best, bi, xh);
-        pvr[i] = Cvt<T>::from_f(best);
-        ixr[i] = (uint8_t)(bi | (best > 0.f ? IDX_RELU : 0));
-        xqr[i] = Cvt<T>::from_f(xh);
-        pcl[b * KP + j] = pvr[i];
-        pct[j * PCT_S + b] = pvr[i];
-        ix_s[e] = ixr[i];
-        xh_s[e] = Cvt<T>::to_f(xqr[i]);
-      }
-    }
-  }
-  auto store_pooled = [&]() {
-#pragma unroll
-    for (int i = 0; i < ITB; ++i) {
-      const int e = tid + i * NT;
-      if (e < NPO) {
-        const size_t o = (size_t)(e / PP) * K + c * PP + e % PP;
-        p_out[o] = pvr[i];
-        idx_out[o] = ixr[i];
-        xh_out[o] = xqr[i];
-      }
-    }
-  };
-  __syncthreads();
+  cb::bn_finalize<C>(bn, sc_s, beta_s, mean_s, istd_s, part_s, b);  // ends with a barrier
   DPA_STAMP(2);
-  // 3. partial logits of this channel (K = 49 of 1568): wave w owns image rows 16w..16w+15
-  const int MT = (B + 15) / 16;
-  if (wv < MT) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  // 2. BN -> ReLU -> 2x2 max of this image; pooled value, argmax|relu index, xhat
+  float pf[IT], xf[IT];
+  uint8_t ixr[IT];
 #pragma unroll
-    for (int s = 0; s < KP / 32; ++s) {
-      const typename mm::frag a = mm::ld(&pcl[(16 * wv + r) * KP + 32 * s + 8 * q]);
-      const typename mm::frag bf = mm::ld(&wcl[r * KP + 32 * s + 8 * q]);
-      acc = mm::mma(a, bf, acc);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int b = 16 * wv + 4 * q + i;
-      if (b < B) st_wt<T>(&hs.part[((size_t)c * B + b) * NMAX + r], acc[i]);
-    }
-  }
-  // publish (write-through stores drained by every wave, then ONE ticket)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0)
-    tk_s = __hip_atomic_fetch_add(&hs.state[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  DPA_STAMP(3);
-  const unsigned long long tk = tk_s;
-  const uint32_t gen = (uint32_t)(tk >> 32);
-  const bool last = (uint32_t)tk == (uint32_t)(C - 1);  // grid = C workgroups (not gridDim: a hidden-arg load)
-  // The last ticket re-arms the word for the next launch ((gen + 1) << 32: stream order, no
-  // workgroup of this launch takes a ticket after it) and that same store releases the
-  // waiting workgroups: with the speculative backward EVERY workgroup then sums the C
-  // partial logits and runs the loss itself (identical fixed-order arithmetic, so identical
-  // results), instead of the last arriver computing it and publishing the loss gradient
-  // behind a second flag -- one cross-workgroup hand-off on the serial path instead of two.
-  if (last) {
-    if (tid == 0)
-      __hip_atomic_exchange(&hs.state[0], ((unsigned long long)(gen + 1u)) << 32, __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_AGENT);
-  } else if (hs.do_bwd) {
-    // bounded wait for the last ticket: a timeout sets the error word and goes on
-    if (tid == 0) {
-      const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-      while ((uint32_t)(__hip_atomic_load(&hs.state[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) == gen) {
-        __builtin_amdgcn_s_sleep(1);
-        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > hs.timeout_ticks) {
-          __hip_atomic_store(&hs.state[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-      }
-    }
-    __syncthreads();
-  } else {
-    store_pooled();  // no backward: the last arriver alone computes the loss
-    return;
-  }
-  // one writer of the launch-wide outputs (logits, loss, dlog, dls)
-  const bool writer = hs.do_bwd ? c == 0 : true;
-  DPA_STAMP(4);
-  // 4. logits = sum of the C partials + bias, rounded to the storage dtype (every load sc1)
-  constexpr int OIT = BM * NMAX / NT;
-  T lgr[OIT];
-#pragma unroll
-  for (int k = 0; k < OIT; ++k) {
-    const int o = tid + k * NT;
-    const int b = o / NMAX, n = o % NMAX;
-    if (b < B && n < N) {
-      float v[C];
-#pragma unroll
-      for (int cc = 0; cc < C; ++cc) v[cc] = ld_wt(&hs.part[((size_t)cc * B + b) * NMAX + n]);
-      float t = bias_s[n];
-#pragma unroll
-      for (int cc = 0; cc < C; ++cc) t += v[cc];
-      lgr[k] = Cvt<T>::from_f(t);
-      lg_s[o] = Cvt<T>::to_f(lgr[k]);
+  for (int i = 0; i < IT; ++i) {
+    const int k = tid + i * NT;
+    const int c = min(k, K - 1) / PP;
+    float best, xh;
+    int bi;
+    cb::bn_relu_max4x<T>(top[i], bot[i], sc_s[c], beta_s[c], mean_s[c], istd_s[c], best, bi, xh);
+    const T pv = Cvt<T>::from_f(best);
+    const T xq = Cvt<T>::from_f(xh);
+    ixr[i] = (uint8_t)(bi | (best > 0.f ? IDX_RELU : 0));
+    pf[i] = k < K ? Cvt<T>::to_f(pv) : 0.f;
+    xf[i] = Cvt<T>::to_f(xq);
+    if (k < K) {
+      const size_t o = (size_t)b * K + k;
+      p_out[o] = pv;
+      idx_out[o] = ixr[i];
+      xh_out[o] = xq;
     }
   }
-  if (tid == 0) cnt_s = 0;
-  __syncthreads();
-  // 5. cross entropy (mean over non-ignored rows), 16 lanes per row (ce_fwd_kernel's math)
-  if (tid < B && tgt_s[tid] != hs.ignore_index) atomicAdd(&cnt_s, 1);
-  __syncthreads();
-  const float cnt = (float)cnt_s;
-  const float inv = cnt > 0.f ? 1.f / cnt : 0.f;
-  const float scv = scale_r;
-  {
-    const int gl = tid % 16, gr = tid / 16;
-    float lsum = 0.f;
-    for (int r0 = 0; r0 < B; r0 += NT / 16) {
-      const int b = r0 + gr;
-      const bool rv = b < B;
-      const int64_t t = rv ? tgt_s[b] : hs.ignore_index;
-      const float x = (rv && gl < N) ? lg_s[b * NMAX + gl] : -INFINITY;
-      const float mx = gmax<16>(x);
-      const float sx = gsum<16>(gl < N ? (rv ? x : 0.f) : 0.f);
-      const float ex = (rv && gl < N) ? __expf(x - mx) : 0.f;
-      const float se = gsum<16>(ex);
-      const float lse = mx + __logf(se);
-      const bool use = rv && t != hs.ignore_index;
-      if (use && gl == 0) {
-        const float xt = (t >= 0 && t < N) ? lg_s[b * NMAX + (int)t] : NAN;
-        lsum += (1.f - hs.smoothing) * (lse - xt) + hs.smoothing * (lse - sx / (float)N);
-      }
-      if (rv) {
-        float d = 0.f;
-        if (use && gl < N) {
-          const float sm = ex * (1.f / se);
-          const float oh = (gl == t ? 1.f - hs.smoothing : 0.f) + hs.smoothing / (float)N;
-          d = (sm - oh) * inv;
-        }
-        dd_s[b * NMAX + gl] = d;
-      }
-    }
-    if (writer) {
-      lsum = wave_sum(lsum);
-      if (lane == 0) red[0][wv] = lsum;
-    }
-  }
-  __syncthreads();
-  DPA_STAMP(5);
-  if (writer) {  // outputs nobody in this launch waits for
-    if (tid == 0) {
-      float tl = 0.f;
+  // fc weights in the compute dtype (autocast casts the fp32 master weight)
 #pragma unroll
-      for (int i = 0; i < NT / 64; ++i) tl += red[0][i];
-      const float l = cnt > 0.f ? tl / cnt : NAN;
-      hs.loss[0] = l;
-      if (hs.scale != nullptr) hs.loss[1] = l * scv;
-    }
+  for (int n = 0; n < NM; ++n)
 #pragma unroll
-    for (int k = 0; k < OIT; ++k) {
-      const int o = tid + k * NT;
-      const int b = o / NMAX, n = o % NMAX;
-      if (b < B && n < N) {
-        logits[(size_t)b * N + n] = lgr[k];
-        const float d = dd_s[o];
-        hs.dlog[(size_t)b * N + n] = d;
-        if (hs.dls != nullptr) reinterpret_cast<T*>(hs.dls)[(size_t)b * N + n] = Cvt<T>::from_f(d * scv);
-      }
-    }
-  }
-  store_pooled();
-  if (!hs.do_bwd) return;
-  // the loss gradient the scaler seeds: d(scale * loss)/dlogits rounded to the storage dtype
-  for (int o = tid; o < B * NMAX; o += NT) {
-    const int n = o % NMAX;
-    lg_s[o] = n < N ? Cvt<T>::to_f(Cvt<T>::from_f(dd_s[o] * scv)) : 0.f;
-  }
-  __syncthreads();
-  DPA_STAMP(6);
-  // 6. fc backward of channel c on MFMA
-  for (int o = tid; o < B * NMAX; o += NT) {
-    const int b = o / NMAX, n = o % NMAX;
-    const E dq = Cvt<T>::from_f(n < N ? lg_s[o] : 0.f);
-    dll[b * 32 + n] = dq;
-    dlt[n * DLT_S + b] = dq;
-  }
-  __syncthreads();
-  float s1 = 0.f, s2 = 0.f;
-  if (wv < MT) {  // dp2 rows 16w..16w+15, the 49 (-> 64) columns of this channel
-    const typename mm::frag a = mm::ld(&dll[(16 * wv + r) * 32 + 8 * q]);
+    for (int i = 0; i < IT; ++i) wq[n][i] = n < N ? rnd_t<T>(wq[n][i]) : 0.f;
+  // 3. logits = p . W^T + bias: lane-partial dot products, reduced over the wave
+  //    (butterfly) and over the 4 waves (LDS, fixed order)
 #pragma unroll
-    for (int nt = 0; nt < KP / 16; ++nt) {
-      const typename mm::frag bf = mm::ld(&wdl[(16 * nt + r) * WDL_S + 8 * q]);
-      const f32x4 acc = mm::mma(a, bf, f32x4{0.f, 0.f, 0.f, 0.f});
-      const int j = 16 * nt + r;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int b = 16 * wv + 4 * q + i;
-        if (b < B && j < PP) {
-          const T gt = Cvt<T>::from_f(acc[i]);
-          reinterpret_cast<T*>(hs.dp2)[(size_t)b * K + c * PP + j] = gt;
-          const int e = b * PP + j;
-          if (ix_s[e] & IDX_RELU) {
-            const float g = Cvt<T>::to_f(gt);
-            s1 += g;
-            s2 += g * xh_s[e];
-          }
-        }
-      }
-    }
-  }
-  {  // dW rows n (16), columns 16w..16w+15 of this channel, K = images
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < BM / 32; ++s) {
-      const typename mm::frag a = mm::ld(&dlt[r * DLT_S + 32 * s + 8 * q]);
-      const typename mm::frag bf = mm::ld(&pct[(16 * wv + r) * PCT_S + 32 * s + 8 * q]);
-      acc = mm::mma(a, bf, acc);
-    }
-    const int j = 16 * wv + r;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int n = 4 * q + i;
-      if (n < N && j < PP) hs.dwfc[(size_t)n * K + c * PP + j] = acc[i];
-    }
-  }
-  if (c == 0) {  // fc bias gradient: 16 lanes per class (a serial loop over the batch in one
-                 // lane made workgroup 0, and so the launch, ~1 us longer)
-    static_assert(NT == 16 * NMAX, "dbfc: one 16-lane group per class");
-    const int n = tid / 16, l = tid % 16;
+  for (int n = 0; n < NM; ++n) {
     float a = 0.f;
-    if (n < N)
-      for (int b = l; b < B; b += 16) a += lg_s[b * NMAX + n];
-    a = gsum<16>(a);
-    if (n < N && l == 0) hs.dbfc[n] = a;
-  }
-  s1 = wave_sum(s1);
-  s2 = wave_sum(s2);
-  if (lane == 0) { red[0][wv] = s1; red[1][wv] = s2; }
-  __syncthreads();
-  if (tid == 0) {
-    float t1 = 0.f, t2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < NT / 64; ++i) { t1 += red[0][i]; t2 += red[1][i]; }
-    hs.dbeta[c] = t1;
-    hs.dgamma[c] = t2;
-    hs.bsum[c] = t1;
-    hs.bsum[C + c] = t2;
+    for (int i = 0; i < IT; ++i) a += pf[i] * wq[n][i];
+    a = wave_sum(a);
+    if (lane == 0) red[wv][n] = a;
   }
-  DPA_STAMP(7);
+  lds_barrier();
+  DPA_STAMP(3);
+  // 4. cross entropy of this row, computed by every lane (identical arithmetic): the
+  //    same formula and rounding as head.hip ce_fwd_kernel
+  float lg[NM];
+  float mx = -INFINITY, sx = 0.f, xt = 0.f;
+#pragma unroll
+  for (int n = 0; n < NM; ++n) {
+    float t = bias[n];
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) t += red[w][n];
+    lg[n] = rnd_t<T>(t);
+    if (n < N) {
+      mx = fmaxf(mx, lg[n]);
+      sx += lg[n];
+      xt = (n == tgt) ? lg[n] : xt;
+    }
+  }
+  float ex[NM], se = 0.f;
+#pragma unroll
+  for (int n = 0; n < NM; ++n) {
+    ex[n] = n < N ? __expf(lg[n] - mx) : 0.f;
+    se += ex[n];
+  }
+  const float lse = mx + __logf(se);
+  const unsigned long long counted =
+      __ballot(lane < B && tgt_lane != hr.ignore_index);  // the batch's rows in the mean
+  const float cnt = (float)__popcll(counted);
+  const float inv = cnt > 0.f ? 1.f / cnt : 0.f;
+  const bool use = tgt != hr.ignore_index;
+  if (!(tgt >= 0 && tgt < N)) xt = NAN;  // an out-of-range target: NaN loss (torch raises)
+  const float row_loss = use ? (1.f - hr.smoothing) * (lse - xt) + hr.smoothing * (lse - sx / (float)N) : 0.f;
+  float ds[NM];  // d(scale * loss)/dlogits of this row, rounded to the storage dtype
+#pragma unroll
+  for (int n = 0; n < NM; ++n) {
+    float d = 0.f;
+    if (use && n < N) {
+      const float sm = ex[n] * (1.f / se);
+      const float oh = (n == tgt ? 1.f - hr.smoothing : 0.f) + hr.smoothing / (float)N;
+      d = (sm - oh) * inv;
+    }
+    ds[n] = rnd_t<T>(d * scv);
+    if (tid == n && n < N) {  // one lane per class writes the row's outputs
+      const size_t o = (size_t)b * N + n;
+      logits[o] = Cvt<T>::from_f(lg[n]);
+      hr.dlog[o] = d;
+      if (hr.dls != nullptr) reinterpret_cast<T*>(hr.dls)[o] = Cvt<T>::from_f(d * scv);
+    }
+  }
+  if (hr.dp2 != nullptr) {
+    DPA_STAMP(4);
+    // 6. backward of this row: dp2 = dls . W (the same weight registers), and the BN2
+    //    backward sums of each channel over this image's pooled positions
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int k = tid + i * NT;
+      float a = 0.f;
+#pragma unroll
+      for (int n = 0; n < NM; ++n) a += ds[n] * wq[n][i];
+      const T gt = Cvt<T>::from_f(a);
+      if (k < K) reinterpret_cast<T*>(hr.dp2)[(size_t)b * K + k] = gt;
+      const float g = (ixr[i] & IDX_RELU) ? Cvt<T>::to_f(gt) : 0.f;
+      gs[0][k] = g;
+      gs[1][k] = g * xf[i];
+    }
+    lds_barrier();
+    {  // channel c = tid / 8: 8 lanes sum its 49 positions in a fixed order
+      const int c = tid >> 3, j = tid & 7;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int f = j; f < PP; f += 8) {
+        s1 += gs[0][c * PP + f];
+        s2 += gs[1][c * PP + f];
+      }
+      s1 = gsum<8>(s1);
+      s2 = gsum<8>(s2);
+      if (j == 0) {
+        hr.bsum[(size_t)b * 2 * C + c] = s1;
+        hr.bsum[(size_t)b * 2 * C + C + c] = s2;
+      }
+    }
+    DPA_STAMP(5);
+  }
+  // 7. the loss mean (last: nothing in this workgroup waits for the atomic's return but
+  //    the workgroup that completes the batch): one atomic per workgroup (see the loss word above)
+  if (tid == 0) {
+    const bool ok = !use || (row_loss > -1.f && row_loss < kRowMax);
+    const unsigned long long inc =
+        (1ull << kArrShift) +
+        (ok ? (use ? (unsigned long long)(((double)row_loss + 1.0) * kFix + 0.5) : 0ull) : (1ull << kBadShift));
+    const unsigned long long old =
+        __hip_atomic_fetch_add(hr.state, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((int)(old >> kArrShift) == B - 1) {  // this add completed the batch: old + inc is the total
+      const unsigned long long tot = old + inc;
+      const int bad = (int)((tot >> kBadShift) & 127ull);
+      const double sum = (double)(tot & kSumMask) / kFix - (double)cnt;
+      const float l = (cnt > 0.f && bad == 0) ? (float)(sum / (double)cnt) : NAN;
+      hr.loss[0] = l;
+      if (hr.has_scale) hr.loss[1] = l * scv;
+      __hip_atomic_store(hr.state, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -463,43 +283,53 @@ static void with_t(DT dt, F&& f) {
 
 bool supported(int64_t B, int64_t N) { return B >= 1 && B <= BMAX && N >= 1 && N <= NMAX; }
 
-// co-residency of the C = 32 workgroups (they wait for the last arriver)
+// no workgroup of the launch waits for another (SyncBN's in-kernel exchange aside, whose
+// B workgroups are far below one per CU); kept for the host-side dispatch check
 bool resident(at::ScalarType st) {
   bool ok = true;
   with_t(dt_of(at::empty({0}, at::TensorOptions().dtype(st))), [&](auto tag) {
     typedef decltype(tag) T;
-    ok = co_resident(reinterpret_cast<const void*>(&head_step_kernel<T, 32>), C, NT, 0) &&
-         co_resident(reinterpret_cast<const void*>(&head_step_kernel<T, BMAX>), C, NT, 0);
+    ok = co_resident(reinterpret_cast<const void*>(&head_row_kernel<T, 10>), BMAX, NT, 0) &&
+         co_resident(reinterpret_cast<const void*>(&head_row_kernel<T, NMAX>), BMAX, NT, 0);
   });
   return ok;
 }
 
+// Forward + loss (+ with dp2 / bsum: the row backward, the GradScaler's scale seeding it).
+// state: int64[>= 1] zeroed once (the kernel re-arms its loss word).
 void head_step(at::Tensor y2, at::Tensor fslab2, at::Tensor fstats2, at::Tensor g2, at::Tensor b2, at::Tensor rm2,
                at::Tensor rv2, at::Tensor nbt2, double momentum, double eps, at::Tensor wfc, at::Tensor bfc,
                at::Tensor logits, at::Tensor p2, at::Tensor idx2, at::Tensor xh2, at::Tensor target,
-               int64_t ignore_index, double smoothing, c10::optional<at::Tensor> scale, at::Tensor part,
-               at::Tensor state, at::Tensor loss, at::Tensor dlog, c10::optional<at::Tensor> dls,
-               c10::optional<at::Tensor> dlsf, c10::optional<at::Tensor> dp2, c10::optional<at::Tensor> dwfc,
-               c10::optional<at::Tensor> dbfc, c10::optional<at::Tensor> dgamma2, c10::optional<at::Tensor> dbeta2,
-               c10::optional<at::Tensor> bsum2, std::shared_ptr<xgmi::XgmiComm> xc, double timeout_s) {
+               int64_t ignore_index, double smoothing, c10::optional<at::Tensor> scale, at::Tensor state,
+               at::Tensor loss, at::Tensor dlog, c10::optional<at::Tensor> dls, c10::optional<at::Tensor> dp2,
+               c10::optional<at::Tensor> bsum_rows, std::shared_ptr<xgmi::XgmiComm> xc) {
   DPA_CHECK_INPUT(y2); DPA_CHECK_INPUT(wfc); DPA_CHECK_INPUT(logits); DPA_CHECK_INPUT(p2); DPA_CHECK_INPUT(target);
+  DPA_CHECK_INPUT(bfc); DPA_CHECK_INPUT(idx2); DPA_CHECK_INPUT(xh2); DPA_CHECK_INPUT(dlog);
   const int B = (int)y2.size(0), N = (int)wfc.size(0);
   TORCH_CHECK(y2.size(1) == C && y2.size(2) == H && y2.size(3) == W && wfc.size(1) == K, "head_step: ConvNet shapes");
   TORCH_CHECK(supported(B, N), "head_step: B <= ", BMAX, " and N <= ", NMAX);
+  TORCH_CHECK(bfc.numel() == N && wfc.scalar_type() == at::kFloat && bfc.scalar_type() == at::kFloat);
   TORCH_CHECK(logits.numel() == (int64_t)B * N && logits.scalar_type() == y2.scalar_type());
   TORCH_CHECK(p2.numel() == (int64_t)B * K && idx2.numel() == p2.numel() && xh2.numel() == p2.numel());
+  TORCH_CHECK(p2.scalar_type() == y2.scalar_type() && xh2.scalar_type() == y2.scalar_type() &&
+              idx2.scalar_type() == at::kByte);
   TORCH_CHECK(target.scalar_type() == at::kLong && target.numel() == B);
-  TORCH_CHECK(part.numel() >= (int64_t)C * B * NMAX && part.scalar_type() == at::kFloat);
-  TORCH_CHECK(state.numel() >= 4 && state.scalar_type() == at::kLong && state.is_cuda());
-  TORCH_CHECK(loss.numel() >= 2 && dlog.numel() == (int64_t)B * N && dlog.scalar_type() == at::kFloat);
+  TORCH_CHECK(state.numel() >= 1 && state.scalar_type() == at::kLong && state.is_cuda());
+  TORCH_CHECK(loss.numel() >= 2 && loss.scalar_type() == at::kFloat && loss.is_cuda());
+  TORCH_CHECK(dlog.numel() == (int64_t)B * N && dlog.scalar_type() == at::kFloat);
   TORCH_CHECK(scale.has_value() == dls.has_value(), "head_step: scale and dls go together");
-  const bool bwd = dlsf.has_value();
+  const bool bwd = dp2.has_value();
+  TORCH_CHECK(bwd == bsum_rows.has_value(), "head_step: dp2 and bsum_rows go together");
+  if (scale.has_value()) {
+    DPA_CHECK_INPUT(*scale); DPA_CHECK_INPUT(*dls);
+    TORCH_CHECK(scale->numel() >= 1 && scale->scalar_type() == at::kFloat);
+    TORCH_CHECK(dls->numel() == (int64_t)B * N && dls->scalar_type() == y2.scalar_type());
+  }
   if (bwd) {
     TORCH_CHECK(scale.has_value(), "head_step: the speculative backward needs the scaler's loss gradient");
-    TORCH_CHECK(dp2.has_value() && dwfc.has_value() && dbfc.has_value() && dgamma2.has_value() &&
-                dbeta2.has_value() && bsum2.has_value());
-    TORCH_CHECK(dp2->numel() == p2.numel() && dwfc->numel() == wfc.numel() && dbfc->numel() == N &&
-                bsum2->numel() == 2 * C && dlsf->numel() == (int64_t)B * N);
+    DPA_CHECK_INPUT(*dp2); DPA_CHECK_INPUT(*bsum_rows);
+    TORCH_CHECK(dp2->numel() == p2.numel() && dp2->scalar_type() == y2.scalar_type());
+    TORCH_CHECK(bsum_rows->numel() == (int64_t)B * 2 * C && bsum_rows->scalar_type() == at::kFloat);
   }
   if (B == 0) return;
   BNParams bp;
@@ -514,34 +344,28 @@ void head_step(at::Tensor y2, at::Tensor fslab2, at::Tensor fstats2, at::Tensor 
   bp.momentum = (float)momentum;
   bp.eps = (float)eps;
   bp.train = 1;
-  if (xc) bp.xs = xc->site(xgmi::kSiteFwd2);
-  HeadStep hs;
-  hs.target = target.data_ptr<int64_t>();
-  hs.ignore_index = ignore_index;
-  hs.smoothing = (float)smoothing;
-  hs.scale = scale.has_value() ? scale->data_ptr<float>() : nullptr;
-  hs.part = part.data_ptr<float>();
-  hs.state = reinterpret_cast<unsigned long long*>(state.data_ptr<int64_t>());
-  hs.loss = loss.data_ptr<float>();
-  hs.dlog = dlog.data_ptr<float>();
-  hs.dls = dls.has_value() ? dls->data_ptr() : nullptr;
-  hs.dlsf = bwd ? dlsf->data_ptr<float>() : nullptr;
-  hs.do_bwd = bwd ? 1 : 0;
-  hs.dp2 = bwd ? dp2->data_ptr() : nullptr;
-  hs.dwfc = bwd ? dwfc->data_ptr<float>() : nullptr;
-  hs.dbfc = bwd ? dbfc->data_ptr<float>() : nullptr;
-  hs.dgamma = bwd ? dgamma2->data_ptr<float>() : nullptr;
-  hs.dbeta = bwd ? dbeta2->data_ptr<float>() : nullptr;
-  hs.bsum = bwd ? bsum2->data_ptr<float>() : nullptr;
-  hs.timeout_ticks = (long long)(timeout_s * 1e8);
+  if (xc) {
+    bp.xs = xc->site(xgmi::kSiteFwd2);
+    bp.xs.nblk = B;  // the grid (spares the kernel a hidden-argument load)
+  }
+  HeadRow hr;
+  hr.target = target.data_ptr<int64_t>();
+  hr.ignore_index = ignore_index;
+  hr.smoothing = (float)smoothing;
+  hr.scale = scale.has_value() ? scale->data_ptr<float>() : loss.data_ptr<float>();  // unread without a scaler
+  hr.has_scale = scale.has_value() ? 1 : 0;
+  hr.state = reinterpret_cast<unsigned long long*>(state.data_ptr<int64_t>());
+  hr.loss = loss.data_ptr<float>();
+  hr.dlog = dlog.data_ptr<float>();
+  hr.dls = dls.has_value() ? dls->data_ptr() : nullptr;
+  hr.dp2 = bwd ? dp2->data_ptr() : nullptr;
+  hr.bsum = bwd ? bsum_rows->data_ptr<float>() : nullptr;
   with_t(dt_of(y2), [&](auto tag) {
     typedef decltype(tag) T;
-    if (bwd) TORCH_CHECK(dls->scalar_type() == y2.scalar_type() && dp2->scalar_type() == y2.scalar_type());
-    // tiles sized for 32 images where the batch fits (fewer load / zeroing / MFMA iterations)
-    auto kern = B <= 32 ? head_step_kernel<T, 32> : head_step_kernel<T, BMAX>;
-    hipLaunchKernelGGL(kern, dim3(C), dim3(NT), 0, cur_stream(), dptr<T>(y2), bp,
-                       wfc.data_ptr<float>(), bfc.data_ptr<float>(), dptr<T>(logits), dptr<T>(p2),
-                       idx2.data_ptr<uint8_t>(), dptr<T>(xh2), B, N, hs);
+    auto kern = N <= 10 ? head_row_kernel<T, 10> : head_row_kernel<T, NMAX>;
+    hipLaunchKernelGGL(kern, dim3(B), dim3(NT), 0, cur_stream(), dptr<T>(y2), bp, wfc.data_ptr<float>(),
+                       bfc.data_ptr<float>(), dptr<T>(logits), dptr<T>(p2), idx2.data_ptr<uint8_t>(), dptr<T>(xh2), B,
+                       N, hr);
   });
   DPA_CHECK_LAUNCH();
 }

@@ -164,7 +164,7 @@ constexpr int64_t FUSED_MAX = (int64_t)FUSED_MAX_BLOCKS * FUSED_BLOCK_GRAN * 4;
 // -- the reducer launched no collective for these buckets.  U = 1 granule per
 // lane then (one poll round trip of W x 4 granules per lane, 4x the workgroups).
 //
-// SlabSrc (optional, not with XG): one gradient region [out, out + n) is still the
+// SlabSrc (optional; with XG its columns are exchanged like granules): one gradient region [out, out + n) is still the
 // per-workgroup partial rows of a producer (slab [rows][n], e.g. the ConvNet's conv1
 // weight-gradient slab): nblk extra workgroups, appended after the granule grid, own
 // it -- they sum its columns (16 columns x 16 row groups each, the association of the
@@ -219,7 +219,7 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
   if (tid == 0 && grid > 1)
     gen = __hip_atomic_fetch_add(&sync[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   unsigned long long tk = 0;
-  if (XG && tid == 0) tk = xgmi::xsite_ticket(xg);
+  if (XG && tid == 0) tk = xgmi::xsite_ticket(xg, (int)blockIdx.x);
   auto load4 = [](const float* p, int rem) {
     if (rem >= 4) return *reinterpret_cast<const f32x4*>(p);
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -275,7 +275,7 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
         }
         const int o = (gi - soff[lo]) * 4, rem = snum[lo] - o;
         const float* gp = sp1[lo] + o;
-        if (!XG && gp >= ss.out && gp < ss.out + ss.n) continue;  // the slab workgroups own it
+        if (gp >= ss.out && gp < ss.out + ss.n) continue;  // the slab workgroups own it
         tt[k] = lo;
         gv[k] = load4(gp, rem);
         pv[k] = load4(sp0[lo] + o, rem);
@@ -286,7 +286,7 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
   }
   if constexpr (XG) {
     __shared__ uint32_t ep_x;
-    if (tid == 0) ep_x = xgmi::xsite_epoch(xg, tk);
+    if (tid == 0) ep_x = xgmi::xsite_epoch(xg, tk, (int)blockIdx.x);
     __syncthreads();
     const uint32_t ep = ep_x;
     const long long par = (long long)(ep & 1u) * xgmi::kMaxRanks * xg.slot_bytes;
@@ -335,6 +335,35 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
         }
       }
       gv[k] = acc * invw;
+    }
+    if (st_t >= 0) {
+      // a slab column (this lane's element, summed above): the same exchange, one granule
+      // at the element's position in the flat granule space -- the slab region needs no
+      // separate column-sum launch at W > 1 either
+      const long long fo = (long long)(soff[st_t] + st_e / 4) * 32 + (long long)(st_e % 4) * 8;
+      const unsigned long long gm = gran(st_sum);
+      for (int p = 0; p < xg.world; ++p) {
+        if (p == xg.rank) continue;
+        *reinterpret_cast<unsigned long long*>(xg.base[p] + par + (long long)xg.rank * xg.slot_bytes + fo) = gm;
+      }
+      unsigned long long g[xgmi::kMaxRanks];
+      const unsigned long long* src[xgmi::kMaxRanks];
+#pragma unroll
+      for (int p = 0; p < xgmi::kMaxRanks; ++p) {
+        src[p] = reinterpret_cast<const unsigned long long*>(xg.base[xg.rank] + par + (long long)p * xg.slot_bytes +
+                                                             fo);
+        g[p] = (p < xg.world && p != xg.rank) ? __hip_atomic_load(src[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                              : 0ull;
+      }
+      float acc = 0.f;
+#pragma unroll
+      for (int p = 0; p < xgmi::kMaxRanks; ++p) {
+        if (p >= xg.world) continue;
+        const float x = p == xg.rank ? st_sum : xgmi::xsite_wait(xg, src[p], g[p], ep, t0, polls, fail);
+        acc = p == 0 ? x : acc + x;
+      }
+      st_sum = acc * invw;
+      bad |= !isfinite(st_sum);
     }
     // a peer that never arrived (timeout / abort: error word set) leaves a partial sum:
     // take the skip path (no parameter / momentum / scale change) rather than apply it
@@ -768,7 +797,6 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
   SlabSrc ss{nullptr, nullptr, 0, 0, 0};
   TORCH_CHECK(slab.has_value() == slab_out.has_value(), "fused AMP-SGD: slab and slab_out go together");
   if (slab.has_value()) {
-    TORCH_CHECK(!xc, "fused AMP-SGD: a slab-sourced gradient cannot be exchanged in-kernel");
     check_f32(*slab); check_f32(*slab_out);
     const int64_t ncol = slab_out->numel();
     TORCH_CHECK(ncol > 0 && slab->numel() % ncol == 0, "fused AMP-SGD: slab must be [rows][slab_out.numel()]");
@@ -789,6 +817,7 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
   auto launch = [&](auto kern, int bg, xgmi::XSite xg) {
     const int grid = (int)std::max<int64_t>(1, (L.chunk_off[L.n] + bg - 1) / bg) + ss.nblk;
     TORCH_CHECK(grid <= FUSED_MAX_BLOCKS, "fused AMP-SGD: grid exceeds the co-resident bound");
+    if (xg.active()) xg.nblk = grid;  // every workgroup takes a ticket (no hidden-argument load)
     hipLaunchKernelGGL(kern, dim3(grid), dim3(FUSED_THR), 0, cur_stream(), L, scale.data_ptr<float>(),
                        tracker.data_ptr<int>(), found_inf.data_ptr<float>(),
                        reinterpret_cast<unsigned long long*>(sync.data_ptr<int64_t>()), (float)lr, (float)momentum,

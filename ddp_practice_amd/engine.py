@@ -81,7 +81,8 @@ class TrainLoop:
         # DDP + fused AMP step: the optimizer kernel averages the gradients over xGMI
         # (parallel/ddp.py defer_grad_sync_to; a no-op without the engine)
         if scaler is not None and getattr(scaler, "_enabled", False) and hasattr(model, "defer_grad_sync_to"):
-            model.defer_grad_sync_to(optimizer)
+            if model.defer_grad_sync_to(optimizer):
+                model.set_slab_sink(optimizer)  # and the conv1 slab sums (exchanged in the same launch)
         elif scaler is not None and getattr(scaler, "_enabled", False) and hasattr(model, "set_slab_sink"):
             # no DDP: the fused AMP step also sums the conv1 weight-gradient slab (models/convnet.py)
             model.set_slab_sink(optimizer)

@@ -106,8 +106,9 @@ class ConvNet(nn.Module):
     def set_slab_sink(self, optimizer) -> bool:
         """Let ``optimizer`` (optim.SGD) sum the conv1 weight-gradient partial rows inside
         its fused AMP step instead of a separate column-sum launch (ops/convnet_fused.py).
-        Only for a model that is not wrapped by DDP (whose reducer reads ``.grad`` in its
-        autograd hooks); engine.TrainLoop enables it.  Returns whether it was enabled."""
+        Under DDP only through ``DistributedDataParallel.set_slab_sink`` (a reducer that
+        packs gradients reads ``.grad`` in its hooks); engine.TrainLoop enables it.
+        Returns whether it was enabled."""
         if not hasattr(optimizer, "defer_slab") or os.environ.get("DPA_SLAB_SINK", "1") == "0":
             return False
         self._dpa_slab_sink = optimizer

@@ -99,7 +99,6 @@ class PreCE:
 
 
 _HEAD_OK: dict = {}
-HEAD_TIMEOUT_S = float(os.environ.get("DPA_HEAD_TIMEOUT", "30"))
 _HEAD_SPEC = os.environ.get("DPA_HEAD_SPEC", "1") != "0"  # 0: no speculative head backward (A/B)
 
 
@@ -169,29 +168,23 @@ class ConvNetFn(torch.autograd.Function):
 
                 scale = active_scale(dev) if _HEAD_SPEC else None
                 f32 = dict(dtype=torch.float32, device=dev)
-                part = torch.empty(32 * B * 16, **f32)
                 loss_buf = torch.empty(2, **f32)
                 dlog = torch.empty((B, N), **f32)
                 dls = torch.empty((B, N), dtype=cdtype, device=dev) if scale is not None else None
                 spec = None
                 if scale is not None:
-                    s_w1, s_w2, s_wfc = w1.shape, w2.shape, wfc.shape
-                    sizes = [s_w1.numel(), 16, 16, 16, s_w2.numel(), 32, 32, 32, s_wfc.numel(), N]
-                    out = torch.empty(sum(sizes), **f32)
-                    views = out.split(sizes)
+                    # the row backward runs in this launch: dp2 and one row of BN2 backward
+                    # sums per image; the fc weight gradient follows in the conv2 backward
                     dp2 = torch.empty_like(p2)
-                    bsum2 = torch.empty(64, **f32)
-                    dlsf = torch.empty(B * N, **f32)
-                    spec = (dls, out, views, dp2, bsum2)
+                    bsum2 = torch.empty(B * 64, **f32)
+                    spec = (dls, dp2, bsum2)
                     _load_ext().convnet_head.head_step(
                         y2, fslab2, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, wfc, bfc, logits, p2, idx2, xh2, labels,
-                        int(ce_cfg[0]), float(ce_cfg[1]), scale, part, state, loss_buf, dlog, dls, dlsf, dp2,
-                        views[8], views[9], views[6], views[7], bsum2, xc, HEAD_TIMEOUT_S)
+                        int(ce_cfg[0]), float(ce_cfg[1]), scale, state, loss_buf, dlog, dls, dp2, bsum2, xc)
                 else:
                     _load_ext().convnet_head.head_step(
                         y2, fslab2, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, wfc, bfc, logits, p2, idx2, xh2, labels,
-                        int(ce_cfg[0]), float(ce_cfg[1]), None, part, state, loss_buf, dlog, None, None, None, None,
-                        None, None, None, None, xc, HEAD_TIMEOUT_S)
+                        int(ce_cfg[0]), float(ce_cfg[1]), None, state, loss_buf, dlog, None, None, None, xc)
                 ctx.spec = spec
                 if holder is not None:
                     holder["ce"] = PreCE(labels, int(ce_cfg[0]), float(ce_cfg[1]), scale, loss_buf, dlog, dls)
@@ -232,37 +225,49 @@ class ConvNetFn(torch.autograd.Function):
         N = s_wfc[0]
         f32 = dict(dtype=torch.float32, device=dev)
         ctx_spec = ctx.spec
+        # one output buffer for every parameter gradient (views handed to autograd);
+        # [dW1 | db1] and [dW2 | db2] are the rows of the two weight-grad slabs
+        sizes = [n_w1, 16, 16, 16, n_w2, 32, 32, 32, n_wfc, N]
+        out = torch.empty(sum(sizes), **f32)
+        dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, dwfc, dbfc = out.split(sizes)
+        fc = (None, None, None, None)
         if ctx_spec is not None and dlogits.data_ptr() == ctx_spec[0].data_ptr() and \
                 dlogits.dtype == ctx_spec[0].dtype:
             # the gradient is the one the head-step launch predicted (the GradScaler seeded
-            # the loss with its scale): the fc backward and BN2 sums are already computed
-            # (references dropped: autograd then steals the returned gradient tensors
-            #  instead of copying each into .grad)
-            ctx.spec = spec = None
-            _, out, views, dp2, bsum2 = ctx_spec
-            dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, dwfc, dbfc = views
-            del views, ctx_spec
+            # the loss with its scale): dp2 and the per-image BN2 sums are already computed;
+            # the fc weight gradient runs in the conv2 backward launch below (extra workgroups)
+            ctx.spec = None
+            dls, dp2, bsum2 = ctx_spec
+            del ctx_spec
+            fc = (dls, p2, dwfc, dbfc)
+            dgb = (dg2, dbe2)  # BN2 dgamma / dbeta from the summed rows, in the conv2 backward
         else:
-            # one output buffer for every parameter gradient (views handed to autograd);
-            # [dW1 | db1] and [dW2 | db2] are the rows of the two weight-grad slabs
-            sizes = [n_w1, 16, 16, 16, n_w2, 32, 32, 32, n_wfc, N]
-            out = torch.empty(sum(sizes), **f32)
-            dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, dwfc, dbfc = out.split(sizes)
             # 1. fc backward -> dp2, fc grads, BN2 sums (complete per channel on this rank)
             bsum2 = torch.empty(64, **f32)
             dp2 = torch.empty_like(p2)
             cn.head_bwd(dl, wfc, p2, idx2, xh2, dwfc, dbfc, dg2, dbe2, bsum2, dp2)
-        gsum2 = comm.all_reduce(bsum2) if sync and xc is None else bsum2
+            dgb = (None, None)
+        if sync and xc is None:
+            gsum2, lsum2 = comm.all_reduce(bsum2), (bsum2 if dgb[0] is not None else None)
+        else:
+            gsum2, lsum2 = bsum2, None
         # 2+3. BN2 bwd -> {conv2 dgrad -> dp1 (+ BN1 partial sums), conv2 wgrad partials}: one launch
         #      (DPA_SPLIT_BWD2=1: the two as separate launches, A/B runs)
         dp1 = torch.empty((B, 16, 14, 14), dtype=y1.dtype, device=dev)
         bslab1 = torch.empty(cn.dgrad2_rows(B) * 32, **f32)
         wslab2 = torch.empty(cn.wgrad_bn_rows(2, B) * (n_w2 + 32), **f32)
         if _SPLIT_BWD2:
+            if dgb[0] is not None:  # the BN2 parameter grads from the rows (this rank's)
+                rows = (lsum2 if lsum2 is not None else gsum2).view(-1, 64).sum(0)
+                dbe2.copy_(rows[:32])
+                dg2.copy_(rows[32:])
             cn.conv2_dgrad(wpk_d, y2, dp2, idx2, fstats2, gsum2, g2, e2, dp1, idx1, xh1, bslab1, xc)
             cn.conv_wgrad_bn(p1, y2, dp2, idx2, fstats2, gsum2, None, g2, e2, None, None, wslab2, xc)
+            if fc[0] is not None:
+                cn.fc_wgrad(*fc)
         else:
-            cn.conv2_bwd(wpk_d, y2, dp2, idx2, fstats2, gsum2, g2, e2, dp1, idx1, xh1, bslab1, p1, wslab2, xc)
+            cn.conv2_bwd(wpk_d, y2, dp2, idx2, fstats2, gsum2, g2, e2, dp1, idx1, xh1, bslab1, p1, wslab2, xc,
+                         lsum2, dgb[0], dgb[1], *fc)
         # 4+5. BN1 bwd -> conv1 wgrad partials (+ dgamma1 / dbeta1 from the local sums), and the
         #      column sums of both weight-grad slabs -> [dW1 | db1], [dW2 | db2]: one launch
         #      (DPA_SPLIT_WGRAD1=1: wgrad launch + a separate reduction launch, A/B runs)

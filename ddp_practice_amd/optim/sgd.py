@@ -199,9 +199,9 @@ class SGD(Optimizer):
         # gradients a DDP reducer deferred to this step are averaged inside the kernel
         d = getattr(self, "_deferred_ddp", None)
         xc = d[1] if d is not None and d[0].deferred_pending() else None
-        if xc is not None:
-            self.flush_slab()
-        ps = self.__dict__.pop("_pending_slab", None)  # summed inside the launch (SlabSrc)
+        # summed inside the launch (SlabSrc), and exchanged there with the other gradients
+        # when the DDP average is fused in too (xc)
+        ps = self.__dict__.pop("_pending_slab", None)
         O.amp_sgd_fused(params, grads, bufs, group["lr"], group["momentum"], group["dampening"],
                         group["weight_decay"], group["nesterov"], group["maximize"], first,
                         scale, tracker, found_inf, growth, backoff, interval, sync, xc,

@@ -244,6 +244,22 @@ class DistributedDataParallel(nn.Module):
         optimizer._deferred_ddp = (self.reducer, xc)
         return True
 
+    def set_slab_sink(self, optimizer) -> bool:
+        """Let ``optimizer`` also sum the wrapped model's deferred weight-gradient slab
+        (models/convnet.py ``set_slab_sink``) under DDP.  Valid only while this reducer
+        defers the average to that optimizer (``defer_grad_sync_to``) with zero-copy
+        buckets: its hooks then read no gradient values, and the fused launch sums the slab
+        and exchanges the result with the other gradients.  The reducer is told to fail
+        loudly should a bucket ever need packing.  Returns whether it was enabled."""
+        d = getattr(optimizer, "_deferred_ddp", None)
+        if (d is None or d[0] is not self.reducer or not hasattr(self.module, "set_slab_sink")
+                or os.environ.get("DPA_REDUCER_ZERO_COPY", "1") == "0"):
+            return False
+        if not self.module.set_slab_sink(optimizer):
+            return False
+        self.reducer.set_require_inplace(True)
+        return True
+
     # -------------------------------------------------------------- utilities
     def bucket_sizes_bytes(self) -> list[int]:
         if self.reducer is None:

@@ -66,3 +66,7 @@ def test_ddp_exact_shape_and_dtype_check(kind, needle):
         assert outs == ["", ""]
     else:
         assert all(needle in o for o in outs), outs
+
+
+def test_ddp_slab_sink_requires_deferred_zero_copy():
+    assert run(W.ddp_slab_sink_guard, world=2) == [True, True]
