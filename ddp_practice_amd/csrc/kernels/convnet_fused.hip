@@ -19,6 +19,7 @@
 
 #include "convblock_impl.h"
 #include "comm/xgmi.h"
+#include "kernels/amp_step.h"
 
 namespace dpa {
 namespace cnf {
@@ -866,6 +867,144 @@ void conv1_wgrad_slab2(at::Tensor x, at::Tensor y1, at::Tensor dp1, at::Tensor i
   DPA_CHECK_LAUNCH();
 }
 
+// ---------------------------------------------------------------------------
+// The ConvNet's optimizer step with the conv1 weight gradient inside it: ONE launch
+// instead of [conv1 wgrad + conv2 column sums] and [fused AMP step] (optim/sgd.py
+// defer_wgrad1: the backward leaves conv1's weight gradient to the optimizer, which
+// computes it in its own launch -- the update still happens in scaler.step()).
+//   workgroups [0, nw1): producers -- BN1 backward -> conv1 weight-gradient partial row,
+//     stored write-through, then one arrival on w1cnt;
+//   workgroups [nw1, grid): the fused AMP step (csrc/kernels/amp_step.h) with three
+//     slab sources: BN1's [dbeta1 | dgamma1] from the conv2 backward's partial sums,
+//     conv1's [dW1 | db1] (its owners wait for the producers' arrivals) and conv2's
+//     [dW2 | db2] (written by the previous launch: summed at once).
+// Producers come first in the grid, so the in-order dispatcher places all of them before
+// any AMP workgroup: a waiting owner can never hold a slot a producer needs.
+// Reference: /root/reference/ddp_main.py:91-93 (backward, scaler.step, update) and
+// origin_main.py:13-14 (conv1 / BN1, whose gradients these are).
+// ---------------------------------------------------------------------------
+constexpr int CAS_U = 2;  // granules per lane of the AMP workgroups (keeps the AMP grid <= one per CU)
+
+template <typename T, bool XG>
+__global__ void __launch_bounds__(cb::NTHR)
+convnet_amp_step_kernel(const T* __restrict__ x, float* __restrict__ wslab1, BwdIn<T> bi, int nw1,
+                        int* __restrict__ w1cnt, opt::MTList L, float* __restrict__ scale, int* __restrict__ tracker,
+                        float* __restrict__ found_inf, unsigned long long* __restrict__ sync, float lr, float momentum,
+                        float dampening, float wd, int nesterov, int maximize, float growth, float backoff,
+                        int interval, xgmi::XSite xg, int* __restrict__ err, long long barrier_ticks, opt::SlabSet ss,
+                        int grid_amp) {
+  const int bid = (int)blockIdx.x;
+  if (bid < nw1) {
+    constexpr int ns = (28 + WG1_ROWS_ - 1) / WG1_ROWS_;
+    cb::conv5x5_wgrad_body<T, 1, 16, 28, 28, WG1_ROWS_, 2, true>(x, nullptr, wslab1, ns, bi, bid);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's row has left the CU
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(w1cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  opt::amp_sgd_body<CAS_U, XG>(L, scale, tracker, found_inf, sync, lr, momentum, dampening, wd, nesterov, maximize,
+                               growth, backoff, interval, xg, err, barrier_ticks, ss, grid_amp, bid - nw1);
+}
+
+// Launch shape of convnet_amp_step at batch B: (producers, AMP workgroups).
+static std::pair<int, int> cas_shape(int64_t B, int64_t n_params_granules) {
+  const int nw1 = (int)wgrad_bn_rows(1, B);
+  const int nreg = (int)std::max<int64_t>(1, (n_params_granules + opt::FUSED_THR * CAS_U - 1) / (opt::FUSED_THR * CAS_U));
+  const int s0 = (32 + 15) / 16, s1 = (16 * 25 + 16 + 15) / 16, s2 = (32 * 400 + 32 + 63) / 64;
+  return {nw1, nreg + s0 + s1 + s2};
+}
+
+// The AMP workgroups of the launch are co-resident (they meet at a grid barrier) and the
+// producers of one XCD fit beside them once they are done.
+bool convnet_amp_step_ok(int64_t B, int64_t n_params_granules, at::ScalarType st) {
+  const auto sh = cas_shape(B, n_params_granules);
+  bool ok = true;
+  with_t(dt_of(at::empty({0}, at::TensorOptions().dtype(st))), [&](auto tag) {
+    typedef decltype(tag) T;
+    if constexpr (std::is_same<T, float>::value) {
+      ok = false;  // fp32: no scaler in the reference path; the separate launches stay
+    } else {
+      ok = co_resident(reinterpret_cast<const void*>(&convnet_amp_step_kernel<T, false>), sh.second, cb::NTHR, 0) &&
+           co_resident(reinterpret_cast<const void*>(&convnet_amp_step_kernel<T, true>), sh.second, cb::NTHR, 0) &&
+           co_resident(reinterpret_cast<const void*>(&convnet_amp_step_kernel<T, false>), sh.first, cb::NTHR, 0);
+    }
+  });
+  return ok;
+}
+
+// params / grads / bufs / first / lr ... sync / xc: as optim.amp_sgd_fused (one param group).
+// conv1: x (batch images), y1, dp1, idx1, fstats1, gsum1 (BN1 backward sum rows; all-reduced
+// under a host SyncBN), g1, eps1 -> wslab1 (partial rows), w1cnt (int32, zeroed once),
+// out1 = [dW1 | db1]; bn1: the BN1 sum rows of this rank ([S1 | S2] per row) -> out0 =
+// [dbeta1 | dgamma1]; conv2: wslab2 -> out2 = [dW2 | db2].
+void convnet_amp_step(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std::vector<at::Tensor> bufs,
+                      double lr, double momentum, double dampening, double wd, bool nesterov, bool maximize,
+                      std::vector<int64_t> first, at::Tensor scale, at::Tensor tracker, at::Tensor found_inf,
+                      double growth, double backoff, int64_t interval, at::Tensor sync, XcPtr xc, at::Tensor x,
+                      at::Tensor y1, at::Tensor dp1, at::Tensor idx1, at::Tensor fstats1, at::Tensor gsum1,
+                      at::Tensor g1, double eps1, at::Tensor wslab1, at::Tensor w1cnt, at::Tensor out1, at::Tensor bn1,
+                      at::Tensor out0, at::Tensor wslab2, at::Tensor out2) {
+  DPA_CHECK_INPUT(x); DPA_CHECK_INPUT(y1); DPA_CHECK_INPUT(wslab1); DPA_CHECK_INPUT(wslab2); DPA_CHECK_INPUT(w1cnt);
+  const int B = (int)y1.size(0);
+  TORCH_CHECK(x.size(1) == 1 && y1.size(1) == 16 && y1.size(2) == 28 && x.scalar_type() == y1.scalar_type());
+  TORCH_CHECK(w1cnt.scalar_type() == at::kInt && w1cnt.numel() >= 1, "convnet_amp_step: w1cnt int32[1]");
+  TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == at::kLong && sync.numel() >= 4 && sync.is_contiguous(),
+              "convnet_amp_step: sync must be a zero-initialised int64[4] device tensor");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && found_inf.scalar_type() == at::kFloat &&
+              tracker.scalar_type() == at::kInt);
+  constexpr int N1 = 16 * 25 + 16, N2 = 32 * 400 + 32;
+  const int nw1 = (int)wgrad_bn_rows(1, B);
+  TORCH_CHECK(wslab1.numel() == (int64_t)nw1 * N1 && out1.numel() == N1, "convnet_amp_step: conv1 slab sizes");
+  TORCH_CHECK(wslab2.numel() == wgrad_bn_rows(2, B) * N2 && out2.numel() == N2, "convnet_amp_step: conv2 slab sizes");
+  TORCH_CHECK(out0.numel() == 32 && bn1.numel() % 32 == 0, "convnet_amp_step: BN1 sum rows [rows][32] -> 32");
+  if (B == 0) return;
+  opt::MTList L = opt::fused_list(params, grads, bufs, first, momentum);
+  opt::SlabSet ss;
+  opt::add_slab(ss, L, bn1, out0, 16, nullptr, 0);
+  opt::add_slab(ss, L, wslab1, out1, 16, w1cnt.data_ptr<int>(), nw1);
+  opt::add_slab(ss, L, wslab2, out2, 64, nullptr, 0);
+  ss.rearm = w1cnt.data_ptr<int>();
+  const auto sh = cas_shape(B, L.chunk_off[L.n]);
+  int nslab = 0;
+  for (int s = 0; s < ss.ns; ++s) nslab += ss.s[s].nblk;
+  const int nreg = (int)std::max<int64_t>(1, (L.chunk_off[L.n] + opt::FUSED_THR * CAS_U - 1) / (opt::FUSED_THR * CAS_U));
+  const int grid_amp = nreg + nslab;
+  TORCH_CHECK(grid_amp == sh.second && nw1 == sh.first, "convnet_amp_step: launch shape");
+  constexpr double kBarrierSeconds = 10.0;
+  with_t(dt_of(y1), [&](auto tag) {
+    typedef decltype(tag) T;
+    if constexpr (std::is_same<T, float>::value) {
+      TORCH_CHECK(false, "convnet_amp_step: bf16 / fp16 only");
+    } else {
+      // producers: BN1 backward from the rows, no dgamma / dbeta (the BN1 slab source owns them)
+      BwdIn<T> bi = bwd_in<T>(dp1, idx1, y1, fstats1, gsum1, c10::nullopt, g1, eps1, 16, c10::nullopt,
+                              c10::nullopt);
+      if (xc) {
+        bi.xs = site_of(xc, xgmi::kSiteBwd1);
+        bi.xs.nblk = nw1;
+      }
+      xgmi::XSite xg;
+      if (xc) {
+        xg = xc->grad_site();
+        TORCH_CHECK(L.chunk_off[L.n] * 4 <= xg.max_vals, "convnet_amp_step: too many elements for the xGMI engine");
+        xg.nblk = grid_amp;
+      }
+      auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(nw1 + grid_amp), dim3(cb::NTHR), 0, cur_stream(), dptr<T>(x),
+                           wslab1.data_ptr<float>(), bi, nw1, w1cnt.data_ptr<int>(), L, scale.data_ptr<float>(),
+                           tracker.data_ptr<int>(), found_inf.data_ptr<float>(),
+                           reinterpret_cast<unsigned long long*>(sync.data_ptr<int64_t>()), (float)lr,
+                           (float)momentum, (float)dampening, (float)wd, (int)nesterov, (int)maximize, (float)growth,
+                           (float)backoff, (int)interval, xg, reinterpret_cast<int*>(sync.data_ptr<int64_t>() + 3),
+                           (long long)(kBarrierSeconds * 1e8), ss, grid_amp);
+      };
+      if (xc) go(convnet_amp_step_kernel<T, true>);
+      else go(convnet_amp_step_kernel<T, false>);
+    }
+  });
+  DPA_CHECK_LAUNCH();
+}
+
 // Whether every launch that exchanges SyncBN sums in-kernel (comm/xsite.h: all
 // of its workgroups poll the peers' rows) is co-resident at batch B; if not,
 // ops/convnet_fused.py all-reduces between the launches instead.
@@ -926,6 +1065,8 @@ void register_convnet_fused(pybind11::module& m) {
   s.def("sites_resident", &cnf::sites_resident);
   s.def("wgrad1_reduce", &cnf::wgrad1_reduce);
   s.def("conv1_wgrad_slab2", &cnf::conv1_wgrad_slab2);
+  s.def("convnet_amp_step", &cnf::convnet_amp_step);
+  s.def("convnet_amp_step_ok", &cnf::convnet_amp_step_ok);
   s.def("wgrad1_counters", &cnf::wgrad1_counters);
 }
 

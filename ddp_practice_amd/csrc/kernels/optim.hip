@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include "common.h"
 #include "comm/xgmi.h"
+#include "kernels/amp_step.h"
 
 #include <vector>
 
@@ -20,18 +21,7 @@ namespace dpa {
 namespace opt {
 
 constexpr int NTHR = 256;
-constexpr int MAXT = 36;
 constexpr int CHUNK = 4096;
-
-struct MTList {
-  int n;
-  unsigned long long first_bits;  // momentum: bit t set = tensor t's buffer is new (b = d)
-  int64_t numel[MAXT];
-  int64_t chunk_off[MAXT + 1];  // prefix sum of chunks
-  float* p0[MAXT];
-  float* p1[MAXT];
-  float* p2[MAXT];
-};
 
 __device__ __forceinline__ int find_tensor(const MTList& L, int64_t c) {
   int t = 0;
@@ -126,337 +116,19 @@ __global__ void update_scale_kernel(float* scale, int* tracker, float* found_inf
   }
 }
 
-// GradScaler.step + SGD + GradScaler.update in ONE launch over a small grid
-// (the ConvNet: 29,034 floats -> 8 workgroups).  Every lane loads its grads,
-// params (and momentum buffers) into registers, the workgroups agree on
-// found_inf through ONE 64-bit device-scope atomic per generation
-// ({arrivals, non-finite workgroups} in one word: no fence, no flag), and then
-// each applies its own slice: unscaled grads written back (torch semantics),
-// the update applied only if every grad is finite, scale / growth tracker
-// updated and found_inf re-armed by workgroup 0.  p0 = param, p1 = grad,
-// p2 = momentum buffer (or null).
-//
-// Grid barrier state `sync` (int64[3], zero-initialised, one per optimizer and
-// grid size): [0] launch counter g, [1 + (g & 1)] this launch's word.  Block 0
-// resets the other parity's word and bumps g after the barrier; the next launch
-// is stream-ordered after this one, so it always finds its word at zero.  The
-// grid (<= FUSED_MAX_BLOCKS of 256 lanes, one per CU at most) is co-resident.
-constexpr int FUSED_THR = 256;
-constexpr int FUSED_U = 4;                                  // float4 granules per lane
-constexpr int FUSED_BLOCK_GRAN = FUSED_THR * FUSED_U;       // 4096 floats per workgroup
-constexpr int FUSED_MAX_BLOCKS = 128;
-constexpr int64_t FUSED_MAX = (int64_t)FUSED_MAX_BLOCKS * FUSED_BLOCK_GRAN * 4;
-// (A one-workgroup variant of 1024 lanes x 8 granules for the ConvNet measured 10.9 us
-// vs 8.6 us for 8 workgroups + grid barrier: one CU's bandwidth is the limit, not the
-// barrier.  A grid of one still skips the barrier, below.)
-
-// The flat index space is in float4 granules; tensor t owns ceil(numel/4)
-// granules starting at chunk_off[t] (every pointer 16-B aligned, checked on the
-// host), so a granule never straddles two tensors.  Tensor tables live in LDS
-// (per-lane dynamic indexing of the by-value kernel argument is a chain of
-// dependent scalar loads).
-//
-// XG (DDP over the xGMI engine, DistributedDataParallel.defer_grad_sync_to):
-// the gradient all-reduce is fused in as well.  Each lane pushes its local
-// gradient granules to every peer as {value, epoch} granules (the one-shot
-// protocol of comm/xgmi_allreduce.hip, epoch from comm/xsite.h tickets), then
-// sums the W ranks' values in rank order and divides by W before the inf check
-// -- the reducer launched no collective for these buckets.  U = 1 granule per
-// lane then (one poll round trip of W x 4 granules per lane, 4x the workgroups).
-//
-// SlabSrc (optional; with XG its columns are exchanged like granules): one gradient region [out, out + n) is still the
-// per-workgroup partial rows of a producer (slab [rows][n], e.g. the ConvNet's conv1
-// weight-gradient slab): nblk extra workgroups, appended after the granule grid, own
-// it -- they sum its columns (16 columns x 16 row groups each, the association of the
-// column-sum launch), check them, load the matching params / buffers, arrive at the
-// grid barrier like the others and then apply the same update per element (unscaled
-// gradient written to `out`).  The granule workgroups skip the region, and the separate
-// column-sum launch disappears.
-struct SlabSrc {
-  const float* slab;
-  float* out;
-  int rows, n, nblk;
-};
-constexpr int SS_COLS = 16, SS_GROUPS = FUSED_THR / SS_COLS;
-
+// GradScaler.step + SGD + GradScaler.update in ONE launch over a small grid (the
+// ConvNet: 29,034 floats), csrc/kernels/amp_step.h amp_sgd_body.  One optional slab
+// source (ss.ns <= 1): the ConvNet's conv1 weight-gradient slab (optim/sgd.py defer_slab).
 template <int U, bool XG, int THR = FUSED_THR>
 __global__ void __launch_bounds__(THR)
 amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ tracker, float* __restrict__ found_inf,
                      unsigned long long* __restrict__ sync, float lr, float momentum, float dampening, float wd,
                      int nesterov, int maximize, float growth, float backoff, int interval,
-                     xgmi::XSite xg, int* __restrict__ err, long long barrier_ticks, SlabSrc ss, int grid) {
+                     xgmi::XSite xg, int* __restrict__ err, long long barrier_ticks, SlabSet ss, int grid) {
   // grid == the launch's workgroup count, passed in: gridDim is a load from the hidden kernel
   // arguments on gfx950, and its wait at the top of the kernel came before the table loads
-  constexpr int BG = THR * U;  // float4 granules per workgroup
-  __shared__ int soff[MAXT + 1];
-  __shared__ int snum[MAXT];
-  __shared__ float* sp0[MAXT];
-  __shared__ float* sp1[MAXT];
-  __shared__ float* sp2[MAXT];
-  __shared__ int s_bad;
-  const int tid = threadIdx.x;
-  const int n = L.n;
-  {  // the table: every load issued before any LDS write (clamped index; a guarded load was
-     // branched and waited for before the next group's loads were issued)
-    const int ti = min(tid, MAXT - 1);
-    const int64_t co = L.chunk_off[min(tid, MAXT)], nu = L.numel[ti];
-    float* const a0 = L.p0[ti];
-    float* const a1 = L.p1[ti];
-    float* const a2 = L.p2[ti];
-    if (tid <= n) soff[tid] = (int)co;
-    if (tid < n) {
-      snum[tid] = (int)nu;
-      sp0[tid] = a0;
-      sp1[tid] = a1;
-      sp2[tid] = a2;
-    }
-  }
-  __syncthreads();
-  const int total = soff[n];
-  // the barrier generation is only used by lane 0: issued after the table
-  // barrier, its load stays in flight (no LDS round trip) with the gradients'
-  unsigned long long gen = 0;
-  if (tid == 0 && grid > 1)
-    gen = __hip_atomic_fetch_add(&sync[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  unsigned long long tk = 0;
-  if (XG && tid == 0) tk = xgmi::xsite_ticket(xg, (int)blockIdx.x);
-  auto load4 = [](const float* p, int rem) {
-    if (rem >= 4) return *reinterpret_cast<const f32x4*>(p);
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    for (int j = 0; j < rem; ++j) v[j] = p[j];
-    return v;
-  };
-  auto store4 = [](float* p, int rem, f32x4 v) {
-    if (rem >= 4) { *reinterpret_cast<f32x4*>(p) = v; return; }
-    for (int j = 0; j < rem; ++j) p[j] = v[j];
-  };
-  f32x4 gv[U], pv[U], bv[U];
-  int tt[U];  // tensor of each granule (its offset is recomputed after the barrier)
-  bool bad = false;
-  const int nreg = grid - ss.nblk;  // granule workgroups; the rest own the slab region
-  // slab workgroup lane (< SS_COLS): its column's sum, tensor and element, param / buffer
-  float st_sum = 0.f, st_p = 0.f, st_b = 0.f;
-  int st_t = -1, st_e = 0;
-  if ((int)blockIdx.x >= nreg) {
-    __shared__ float spart[SS_GROUPS][SS_COLS + 1];
-    const int c0 = ((int)blockIdx.x - nreg) * SS_COLS;
-    const int col = c0 + tid % SS_COLS, g = tid / SS_COLS;
-    if (tid < SS_COLS && col < ss.n) {  // param / buffer loads in flight with the slab's
-      const float* gp = ss.out + col;
-      for (int i = 0; i < n; ++i)  // the tensor whose gradient holds this column (host-checked: one)
-        if (gp >= sp1[i] && gp < sp1[i] + snum[i]) {
-          st_t = i;
-          st_e = (int)(gp - sp1[i]);
-        }
-      if (st_t >= 0) {
-        st_p = sp0[st_t][st_e];
-        if (momentum != 0.f && !((L.first_bits >> st_t) & 1ull)) st_b = sp2[st_t][st_e];
-      }
-    }
-    spart[g][tid % SS_COLS] = slab_colsum<SS_GROUPS>(ss.slab, ss.rows, ss.n, col, g);  // = slab_reduce
-    __syncthreads();
-    if (tid < SS_COLS && col < ss.n) {
-#pragma unroll
-      for (int gg = 0; gg < SS_GROUPS; ++gg) st_sum += spart[gg][tid];
-      bad = !isfinite(st_sum);
-    }
-#pragma unroll
-    for (int k = 0; k < U; ++k) tt[k] = -1;
-  } else {
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const int gi = blockIdx.x * BG + k * THR + tid;
-      tt[k] = -1;
-      if (gi < total) {
-        int lo = 0, hi = n - 1;  // tensor holding granule gi
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (soff[mid] <= gi) lo = mid; else hi = mid - 1;
-        }
-        const int o = (gi - soff[lo]) * 4, rem = snum[lo] - o;
-        const float* gp = sp1[lo] + o;
-        if (gp >= ss.out && gp < ss.out + ss.n) continue;  // the slab workgroups own it
-        tt[k] = lo;
-        gv[k] = load4(gp, rem);
-        pv[k] = load4(sp0[lo] + o, rem);
-        const bool use_buf = momentum != 0.f && !((L.first_bits >> lo) & 1ull);
-        bv[k] = use_buf ? load4(sp2[lo] + o, rem) : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-  }
-  if constexpr (XG) {
-    __shared__ uint32_t ep_x;
-    if (tid == 0) ep_x = xgmi::xsite_epoch(xg, tk, (int)blockIdx.x);
-    __syncthreads();
-    const uint32_t ep = ep_x;
-    const long long par = (long long)(ep & 1u) * xgmi::kMaxRanks * xg.slot_bytes;
-    auto gran = [ep](float v) { return ((unsigned long long)ep << 32) | (unsigned long long)__float_as_uint(v); };
-    typedef __attribute__((ext_vector_type(2))) unsigned long long u64x2;
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      if (tt[k] < 0) continue;
-      const long long fo = (long long)(blockIdx.x * BG + k * THR + tid) * 32;  // 4 granules of 8 B
-      const u64x2 a = {gran(gv[k][0]), gran(gv[k][1])}, b = {gran(gv[k][2]), gran(gv[k][3])};
-      for (int p = 0; p < xg.world; ++p) {
-        if (p == xg.rank) continue;  // my own values stay in registers
-        u64x2* dst = reinterpret_cast<u64x2*>(xg.base[p] + par + (long long)xg.rank * xg.slot_bytes + fo);
-        dst[0] = a;
-        dst[1] = b;
-      }
-    }
-    const float invw = 1.f / (float)xg.world;
-    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    unsigned polls = 0;
-    bool fail = false;
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      if (tt[k] < 0) continue;
-      const long long fo = (long long)(blockIdx.x * BG + k * THR + tid) * 32;
-      unsigned long long g[xgmi::kMaxRanks][4];
-      const unsigned long long* src[xgmi::kMaxRanks];
-#pragma unroll
-      for (int p = 0; p < xgmi::kMaxRanks; ++p) {  // every load issued before the first tag check
-        src[p] = reinterpret_cast<const unsigned long long*>(xg.base[xg.rank] + par + (long long)p * xg.slot_bytes +
-                                                             fo);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          g[p][j] = (p < xg.world && p != xg.rank)
-                        ? __hip_atomic_load(src[p] + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                        : 0ull;
-      }
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int p = 0; p < xgmi::kMaxRanks; ++p) {
-        if (p >= xg.world) continue;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float x = p == xg.rank ? gv[k][j] : xgmi::xsite_wait(xg, src[p] + j, g[p][j], ep, t0, polls, fail);
-          acc[j] = p == 0 ? x : acc[j] + x;
-        }
-      }
-      gv[k] = acc * invw;
-    }
-    if (st_t >= 0) {
-      // a slab column (this lane's element, summed above): the same exchange, one granule
-      // at the element's position in the flat granule space -- the slab region needs no
-      // separate column-sum launch at W > 1 either
-      const long long fo = (long long)(soff[st_t] + st_e / 4) * 32 + (long long)(st_e % 4) * 8;
-      const unsigned long long gm = gran(st_sum);
-      for (int p = 0; p < xg.world; ++p) {
-        if (p == xg.rank) continue;
-        *reinterpret_cast<unsigned long long*>(xg.base[p] + par + (long long)xg.rank * xg.slot_bytes + fo) = gm;
-      }
-      unsigned long long g[xgmi::kMaxRanks];
-      const unsigned long long* src[xgmi::kMaxRanks];
-#pragma unroll
-      for (int p = 0; p < xgmi::kMaxRanks; ++p) {
-        src[p] = reinterpret_cast<const unsigned long long*>(xg.base[xg.rank] + par + (long long)p * xg.slot_bytes +
-                                                             fo);
-        g[p] = (p < xg.world && p != xg.rank) ? __hip_atomic_load(src[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                                              : 0ull;
-      }
-      float acc = 0.f;
-#pragma unroll
-      for (int p = 0; p < xgmi::kMaxRanks; ++p) {
-        if (p >= xg.world) continue;
-        const float x = p == xg.rank ? st_sum : xgmi::xsite_wait(xg, src[p], g[p], ep, t0, polls, fail);
-        acc = p == 0 ? x : acc + x;
-      }
-      st_sum = acc * invw;
-      bad |= !isfinite(st_sum);
-    }
-    // a peer that never arrived (timeout / abort: error word set) leaves a partial sum:
-    // take the skip path (no parameter / momentum / scale change) rather than apply it
-    bad |= fail;
-  }
-#pragma unroll
-  for (int k = 0; k < U; ++k)
-    if (tt[k] >= 0)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bad |= !isfinite(gv[k][j]);
-  // scale read before arriving: block 0 rewrites it once everyone has arrived, and a
-  // workgroup that reads it late must not unscale with the next step's value
-  const float inv = 1.f / scale[0];
-  const bool block_bad = __syncthreads_or(bad);
-  if (grid == 1) {  // uniform: one workgroup needs no grid barrier
-    if (tid == 0) s_bad = block_bad;
-  } else if (tid == 0) {
-    unsigned long long* word = &sync[1 + (gen & 1)];
-    const unsigned long long G = (unsigned long long)grid;
-    __hip_atomic_fetch_add(word, 1ull | ((unsigned long long)block_bad << 32), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    unsigned long long v;
-    // bounded: the host sizes the grid to be co-resident (amp_sgd_fused), so every workgroup
-    // arrives; should one never do, give up after barrier_ticks, flag it and skip the update
-    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    bool timed_out = false;
-    while (((v = __hip_atomic_fetch_add(word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & 0xffffffffull) <
-           G) {
-      __builtin_amdgcn_s_sleep(1);
-      if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > barrier_ticks) {
-        timed_out = true;
-        if (err != nullptr) __hip_atomic_store(err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-    }
-    s_bad = timed_out || (v >> 32) != 0;
-    if (blockIdx.x == 0) {
-      __hip_atomic_exchange(&sync[1 + ((gen + 1) & 1)], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(&sync[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-  const bool any_bad = s_bad;
-#pragma unroll
-  for (int k = 0; k < U; ++k) {
-    const int t = tt[k];
-    if (t < 0) continue;
-    const int o = (blockIdx.x * BG + k * THR + tid - soff[t]) * 4, rem = snum[t] - o;
-    const f32x4 g = gv[k] * inv;
-    store4(sp1[t] + o, rem, g);
-    if (any_bad) continue;
-    f32x4 d = maximize ? -g : g;
-    if (wd != 0.f) d += wd * pv[k];
-    if (momentum != 0.f) {
-      const bool first = (L.first_bits >> t) & 1ull;
-      const f32x4 bb = first ? d : momentum * bv[k] + (1.f - dampening) * d;
-      store4(sp2[t] + o, rem, bb);
-      d = nesterov ? d + momentum * bb : bb;
-    }
-    store4(sp0[t] + o, rem, pv[k] - lr * d);
-  }
-  if (st_t >= 0) {  // a slab column: the same update, one element
-    const float g = st_sum * inv;
-    sp1[st_t][st_e] = g;
-    if (!any_bad) {
-      float d = maximize ? -g : g;
-      if (wd != 0.f) d += wd * st_p;
-      if (momentum != 0.f) {
-        const bool first = (L.first_bits >> st_t) & 1ull;
-        const float bb = first ? d : momentum * st_b + (1.f - dampening) * d;
-        sp2[st_t][st_e] = bb;
-        d = nesterov ? d + momentum * bb : bb;
-      }
-      sp0[st_t][st_e] = st_p - lr * d;
-    }
-  }
-  if (blockIdx.x == 0 && tid == 0) {
-    // every workgroup read scale[0] before arriving, and block 0 passed the barrier
-    found_inf[0] = 0.f;
-    if (any_bad) {
-      scale[0] = scale[0] * backoff;
-      tracker[0] = 0;
-    } else {
-      const int succ = tracker[0] + 1;
-      if (succ == interval) {
-        const float ns = scale[0] * growth;
-        if (isfinite(ns)) scale[0] = ns;
-        tracker[0] = 0;
-      } else {
-        tracker[0] = succ;
-      }
-    }
-  }
+  amp_sgd_body<U, XG, THR>(L, scale, tracker, found_inf, sync, lr, momentum, dampening, wd, nesterov, maximize,
+                           growth, backoff, interval, xg, err, barrier_ticks, ss, grid, (int)blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -777,45 +449,12 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
   TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == at::kLong && sync.numel() >= 4 && sync.is_contiguous(),
               "fused AMP-SGD: sync must be a zero-initialised int64[4] device tensor");
   TORCH_CHECK(amp_sgd_resident(), "fused AMP-SGD: grid not co-resident on this device (use the unfused step)");
-  MTList L{};
-  L.n = (int)params.size();
-  L.first_bits = first_bits(first, 0, params.size());
-  L.chunk_off[0] = 0;
-  for (size_t i = 0; i < params.size(); ++i) {
-    check_f32(params[i]); check_f32(grads[i]);
-    TORCH_CHECK(params[i].numel() == grads[i].numel());
-    L.numel[i] = params[i].numel();
-    L.p0[i] = params[i].data_ptr<float>();
-    L.p1[i] = grads[i].data_ptr<float>();
-    L.p2[i] = bufs.empty() ? nullptr : bufs[i].data_ptr<float>();
-    L.chunk_off[i + 1] = L.chunk_off[i] + (L.numel[i] + 3) / 4;  // float4-granule prefix for this kernel
-    TORCH_CHECK(momentum == 0.0 || !bufs.empty(), "fused AMP-SGD: momentum needs buffers");
-    auto al = [](const float* q) { return q == nullptr || (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-    TORCH_CHECK(al(L.p0[i]) && al(L.p1[i]) && al(L.p2[i]), "fused AMP-SGD needs 16-byte aligned tensors");
-  }
-  TORCH_CHECK(L.chunk_off[L.n] * 4 <= FUSED_MAX, "fused AMP-SGD handles at most ", FUSED_MAX, " elements");
-  SlabSrc ss{nullptr, nullptr, 0, 0, 0};
+  MTList L = fused_list(params, grads, bufs, first, momentum);
+  SlabSet ss;
   TORCH_CHECK(slab.has_value() == slab_out.has_value(), "fused AMP-SGD: slab and slab_out go together");
-  if (slab.has_value()) {
-    check_f32(*slab); check_f32(*slab_out);
-    const int64_t ncol = slab_out->numel();
-    TORCH_CHECK(ncol > 0 && slab->numel() % ncol == 0, "fused AMP-SGD: slab must be [rows][slab_out.numel()]");
-    TORCH_CHECK((reinterpret_cast<uintptr_t>(slab_out->data_ptr()) & 15) == 0, "fused AMP-SGD: slab_out alignment");
-    // the region must start and end on granule boundaries of the tensors that cover it
-    const float* lo = slab_out->data_ptr<float>();
-    const float* hi = lo + ncol;
-    for (int i = 0; i < L.n; ++i) {
-      const float* a = L.p1[i];
-      const float* b = a + L.numel[i];
-      if (b <= lo || a >= hi) continue;
-      TORCH_CHECK(a >= lo && b <= hi && (L.numel[i] % 4 == 0 || b == hi),
-                  "fused AMP-SGD: every gradient overlapping slab_out must lie inside it, in whole granules");
-    }
-    ss = SlabSrc{slab->data_ptr<float>(), slab_out->data_ptr<float>(), (int)(slab->numel() / ncol), (int)ncol,
-                 (int)((ncol + SS_COLS - 1) / SS_COLS)};
-  }
+  if (slab.has_value()) add_slab(ss, L, *slab, *slab_out, 16, nullptr, 0);
   auto launch = [&](auto kern, int bg, xgmi::XSite xg) {
-    const int grid = (int)std::max<int64_t>(1, (L.chunk_off[L.n] + bg - 1) / bg) + ss.nblk;
+    const int grid = (int)std::max<int64_t>(1, (L.chunk_off[L.n] + bg - 1) / bg) + (ss.ns ? ss.s[0].nblk : 0);
     TORCH_CHECK(grid <= FUSED_MAX_BLOCKS, "fused AMP-SGD: grid exceeds the co-resident bound");
     if (xg.active()) xg.nblk = grid;  // every workgroup takes a ticket (no hidden-argument load)
     hipLaunchKernelGGL(kern, dim3(grid), dim3(FUSED_THR), 0, cur_stream(), L, scale.data_ptr<float>(),

@@ -56,6 +56,21 @@ _SPLIT_BWD2 = os.environ.get("DPA_SPLIT_BWD2", "0") == "1"
 _SPLIT_WGRAD1 = os.environ.get("DPA_SPLIT_WGRAD1", "1") == "1"  # merged launch measured slower (15.0 vs 10.9 us)
 # conv1 wgrad + conv2 slab sums in one launch even without a slab sink (A/B; then a conv1-only sum launch)
 _WGRAD1_SLAB2 = os.environ.get("DPA_WGRAD1_SLAB2", "0") == "1"
+# conv1's weight gradient deferred into the optimizer's fused launch (DPA_DEFER_WGRAD1=0: A/B)
+_DEFER_WGRAD1 = os.environ.get("DPA_DEFER_WGRAD1", "1") == "1"
+_CAS_OK: dict = {}
+
+
+def _wgrad1_deferrable(B: int, dtype: torch.dtype, opt) -> bool:
+    """convnet.convnet_amp_step can run this batch size / dtype on this device (its AMP
+    workgroups co-resident) and the optimizer's step takes the small fused path."""
+    if not getattr(opt, "small_fusable", lambda: False)():
+        return False
+    gran = sum((p.numel() + 3) // 4 for g in opt.param_groups for p in g["params"])
+    key = (B, dtype, gran)
+    if key not in _CAS_OK:
+        _CAS_OK[key] = bool(_load_ext().convnet.convnet_amp_step_ok(B, gran, dtype))
+    return _CAS_OK[key]
 
 
 def _fused_site_engine(comm, batch: int, dtype: torch.dtype):
@@ -202,6 +217,7 @@ class ConvNetFn(torch.autograd.Function):
         ctx.wcnt = wcnt
         ctx.sink = sink
         ctx.w1b1 = (w1, b1) if sink is not None else None
+        ctx.l12 = (w1, b1, g1, be1, w2, b2) if sink is not None else None
         ctx.sync = sync
         ctx.comm = comm
         ctx.xc = xc
@@ -227,9 +243,10 @@ class ConvNetFn(torch.autograd.Function):
         ctx_spec = ctx.spec
         # one output buffer for every parameter gradient (views handed to autograd);
         # [dW1 | db1] and [dW2 | db2] are the rows of the two weight-grad slabs
+        # [dW1 | db1 | dbeta1 | dgamma1] = conv1's slab columns, then BN1's [S1 | S2] sums
         sizes = [n_w1, 16, 16, 16, n_w2, 32, 32, 32, n_wfc, N]
         out = torch.empty(sum(sizes), **f32)
-        dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, dwfc, dbfc = out.split(sizes)
+        dw1, db1, dbe1, dg1, dw2, db2, dg2, dbe2, dwfc, dbfc = out.split(sizes)
         fc = (None, None, None, None)
         if ctx_spec is not None and dlogits.data_ptr() == ctx_spec[0].data_ptr() and \
                 dlogits.dtype == ctx_spec[0].dtype:
@@ -277,15 +294,26 @@ class ConvNetFn(torch.autograd.Function):
         else:
             gsum1, lsum1, xc1 = bslab1, None, xc
         out1, out2 = out.narrow(0, 0, n_w1 + 16), out.narrow(0, n_w1 + 48, n_w2 + 32)
+        out0 = out.narrow(0, n_w1 + 16, 32)  # [dbeta1 | dgamma1]
         sink = ctx.sink
+        w1b1, l12 = ctx.w1b1, ctx.l12
+        ctx.w1b1 = ctx.l12 = None
         if sink is not None:
             sink.flush_slab()  # an earlier backward's sums first (they may be accumulated into)
-            # [dW1 | db1] is left to the optimizer's fused step only when autograd will hand
-            # these views to .grad as they are (no accumulation into an existing .grad)
-            if any(p.grad is not None for p in ctx.w1b1):
+            # a gradient region is left to the optimizer's fused step only when autograd will
+            # hand its views to .grad as they are (no accumulation into an existing .grad)
+            if any(p.grad is not None for p in w1b1):
                 sink = None
-        ctx.w1b1 = None
-        if sink is not None or _WGRAD1_SLAB2:
+        if (sink is not None and _DEFER_WGRAD1 and hasattr(sink, "defer_wgrad1")
+                and all(p.grad is None for p in l12) and _wgrad1_deferrable(B, x.dtype, sink)):
+            # the conv1 weight gradient itself, BN1's and conv2's column sums: all computed
+            # inside the optimizer's fused launch (convnet.convnet_amp_step); the backward
+            # launches nothing more.  Any other gradient reader flushes first (optim.SGD)
+            sink.defer_wgrad1(dict(x=x, y1=y1, dp1=dp1, idx1=idx1, fstats1=fstats1, gsum1=gsum1, lsum1=lsum1, g1=g1,
+                                   e1=e1, dg1=dg1, dbe1=dbe1, wslab1=wslab1, out1=out1,
+                                   bn1=lsum1 if lsum1 is not None else gsum1, out0=out0, wslab2=wslab2, out2=out2,
+                                   xc1=xc1))
+        elif sink is not None or _WGRAD1_SLAB2:
             # conv1 wgrad partials + the conv2 slab's column sums in one launch; the conv1
             # slab's sums run inside the fused AMP-SGD launch (optim.SGD.defer_slab) or next
             cn.conv1_wgrad_slab2(x, y1, dp1, idx1, fstats1, gsum1, lsum1, g1, e1, dg1, dbe1, wslab1, wslab2, out2,

@@ -56,7 +56,23 @@ class SGD(Optimizer):
         self.flush_slab()
         self._pending_slab = (slab, out)
 
+    def defer_wgrad1(self, w: dict) -> None:
+        """The ConvNet's conv1 weight gradient -- with BN1's and conv2's gradient column sums
+        -- left undone by the backward (ops/convnet_fused.py): the next fused AMP step
+        computes it inside its own launch (csrc/kernels/convnet_fused.hip convnet_amp_step),
+        so the update still happens in ``scaler.step()``; any other gradient reader
+        flushes first (``flush_slab``)."""
+        self.flush_slab()
+        self._pending_wgrad1 = w
+
     def flush_slab(self) -> None:
+        w = self.__dict__.pop("_pending_wgrad1", None)
+        if w is not None:  # the launches the deferral saved
+            C = _load_ext()
+            C.convnet.conv1_wgrad_slab2(w["x"], w["y1"], w["dp1"], w["idx1"], w["fstats1"], w["gsum1"], w["lsum1"],
+                                        w["g1"], w["e1"], w["dg1"], w["dbe1"], w["wslab1"], w["wslab2"], w["out2"],
+                                        w["xc1"])
+            C.convblock.slab_reduce(w["wslab1"], w["out1"].numel(), w["out1"])
         ps = self.__dict__.pop("_pending_slab", None)
         if ps is not None:
             _load_ext().convblock.slab_reduce(ps[0], ps[1].numel(), ps[1])
@@ -151,6 +167,21 @@ class SGD(Optimizer):
             return "large"
         return None
 
+    def small_fusable(self) -> bool:
+        """The "small" fused step will apply once the gradients exist (predicted from the
+        parameters: their gradients are then fp32 views of one aligned buffer)."""
+        if len(self.param_groups) != 1:
+            return False
+        ps = self.param_groups[0]["params"]
+        if not ps or not all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and p.data_ptr() % 16 == 0
+                             for p in ps):
+            return False
+        if self.param_groups[0]["momentum"] != 0:
+            return False  # buffers may not exist yet (first step): keep the plain path
+        O = _load_ext().optim
+        return (len(ps) <= O.MAXT and sum((p.numel() + 3) // 4 * 4 for p in ps) <= self.FUSED_AMP_MAX_NUMEL
+                and O.amp_sgd_resident())
+
     def can_fuse_amp(self) -> bool:
         """Unscale + inf-check + SGD + scale update as one launch (see _fuse_kind)."""
         return self._fuse_kind() is not None
@@ -190,6 +221,10 @@ class SGD(Optimizer):
             sync = torch.zeros(4, dtype=torch.int64, device=params[0].device)
             setattr(self, name, sync)
         O = _load_ext().optim
+        w1 = self.__dict__.get("_pending_wgrad1")
+        if w1 is not None and kind != "small":
+            self.flush_slab()
+            w1 = None
         if kind == "large":
             self._flush_deferred()
             O.amp_sgd_large(self._large_table(params, grads, bufs, first), group["lr"], group["momentum"],
@@ -199,6 +234,21 @@ class SGD(Optimizer):
         # gradients a DDP reducer deferred to this step are averaged inside the kernel
         d = getattr(self, "_deferred_ddp", None)
         xc = d[1] if d is not None and d[0].deferred_pending() else None
+        if w1 is not None:
+            # conv1's weight gradient + the slab sums + this step in one launch
+            del self._pending_wgrad1
+            cas = getattr(self, "_amp_sync_cas", None)
+            if cas is None or cas[0].device != params[0].device:
+                cas = self._amp_sync_cas = (torch.zeros(4, dtype=torch.int64, device=params[0].device),
+                                            torch.zeros(1, dtype=torch.int32, device=params[0].device))
+            _load_ext().convnet.convnet_amp_step(
+                params, grads, bufs, group["lr"], group["momentum"], group["dampening"], group["weight_decay"],
+                group["nesterov"], group["maximize"], first, scale, tracker, found_inf, growth, backoff, interval,
+                cas[0], xc, w1["x"], w1["y1"], w1["dp1"], w1["idx1"], w1["fstats1"], w1["gsum1"], w1["g1"], w1["e1"],
+                w1["wslab1"], cas[1], w1["out1"], w1["bn1"], w1["out0"], w1["wslab2"], w1["out2"])
+            if xc is not None:
+                d[0].consume_deferred()
+            return
         # summed inside the launch (SlabSrc), and exchanged there with the other gradients
         # when the DDP average is fused in too (xc)
         ps = self.__dict__.pop("_pending_slab", None)

@@ -287,10 +287,11 @@ def test_deferred_gather_in_conv1(C, dtype):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 def test_slab_sink_matches_separate_sums(C, dtype):
-    """conv1's weight-gradient column sums inside the fused AMP-SGD launch (SGD.defer_slab,
-    csrc/kernels/optim.hip SlabSrc) + conv2's inside the conv1 wgrad launch == the separate
-    column-sum launch, bitwise, eagerly and graph-replayed; no slab_reduce launch is left
-    once the fused step runs, and a .grad reader (unscale_) still sees the summed values."""
+    """With a slab sink the conv1 weight gradient and the BN1 / conv1 / conv2 gradient column
+    sums run inside the optimizer's fused launch (SGD.defer_wgrad1, convnet.convnet_amp_step:
+    5 launches per step) == the separate launches, eagerly and graph-replayed (fp32 sums in
+    another association: allclose, not bitwise); no slab_reduce launch is left once the
+    fused step runs."""
     from ddp_practice_amd.amp import GradScaler
     from ddp_practice_amd.data import DeviceLoader, synthetic
     from ddp_practice_amd.nn import CrossEntropyLoss
@@ -300,6 +301,7 @@ def test_slab_sink_matches_separate_sums(C, dtype):
     ds = synthetic(32 * 12, seed=4)
     runs = []
     orig = C.convblock.slab_reduce
+    orig_cas = C.convnet.convnet_amp_step
     for sink in (False, True):
         m = _model()
         m.amp_dtype = dtype
@@ -308,11 +310,15 @@ def test_slab_sink_matches_separate_sums(C, dtype):
         opt, scaler, crit = SGD(m.parameters(), lr=0.05), GradScaler(), CrossEntropyLoss()
         if sink:
             assert m.set_slab_sink(opt)
-        calls = [0]
+        calls = [0, 0]
 
         def spy(*a, **k):
             calls[0] += 1
             return orig(*a, **k)
+
+        def spy_cas(*a, **k):
+            calls[1] += 1
+            return orig_cas(*a, **k)
 
         def step():
             loader.fill_(images, labels, defer=True)
@@ -323,26 +329,28 @@ def test_slab_sink_matches_separate_sums(C, dtype):
             scaler.update()
 
         C.convblock.slab_reduce = spy
+        C.convnet.convnet_amp_step = spy_cas
         try:
             loader.start_epoch()
-            step()  # the first step is unfused: unscale_ flushes the deferred sums
-            calls[0] = 0
+            step()  # the first step is unfused: unscale_ flushes the deferred work
+            calls[0] = calls[1] = 0
             for _ in range(2):
                 step()
-            eager_calls = calls[0]
+            eager_calls = list(calls)
             runner = CapturedStep(step, warmup=1, steps_per_graph=2)
             assert runner.capture()
             for _ in range(3):
                 runner.run()
         finally:
             C.convblock.slab_reduce = orig
+            C.convnet.convnet_amp_step = orig_cas
         torch.cuda.synchronize()
-        assert "_pending_slab" not in opt.__dict__
+        assert "_pending_slab" not in opt.__dict__ and "_pending_wgrad1" not in opt.__dict__
         runs.append((copy.deepcopy(m.state_dict()), eager_calls))
     (sd_a, calls_a), (sd_b, calls_b) = runs
-    assert calls_a == 2 and calls_b == 0, (calls_a, calls_b)
+    assert calls_a == [2, 0] and calls_b == [0, 2], (calls_a, calls_b)
     for k in sd_a:
-        assert torch.equal(sd_a[k], sd_b[k]), k
+        torch.testing.assert_close(sd_b[k].float(), sd_a[k].float(), rtol=1e-4, atol=1e-6, msg=k)
 
 
 def test_slab_sink_flushes_for_grad_readers(C):
