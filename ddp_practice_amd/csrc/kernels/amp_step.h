@@ -71,11 +71,16 @@ constexpr int64_t FUSED_MAX = (int64_t)FUSED_MAX_BLOCKS * FUSED_BLOCK_GRAN * 4;
 // source with `wait` is produced IN THIS LAUNCH: its owners first wait (bounded) until
 // the producers' arrival counter reaches wait_n and then read the rows with L2-coherent
 // (sc1) loads; block 0 re-arms the counter after the barrier.
+// Association: a column is summed over rows g, g + G, ... (g < G row groups of 256/G lanes)
+// and the G partials are added in group order -- slab_reduce's (G = 16) and the BN
+// backward-coefficient reduction's (cb::colsum_rows over 2C = 32 columns: G = 8), so a
+// gradient summed here is bitwise the one the separate launches produce (the flush path).
 struct SlabSrc {
   const float* slab = nullptr;
   float* out = nullptr;
   int rows = 0, n = 0, nblk = 0;
-  int cols = 16;              // 16 (16 row groups) or 64 (4 row groups)
+  int groups = 16;            // row groups G: 16 (16 columns per chunk) or 8 (32 columns)
+  int chunks = 1;             // column chunks per workgroup: 1 or 4 (G = 16)
   const int* wait = nullptr;  // in-launch producers' arrival counter (nullptr: rows ready)
   int wait_n = 0;
 };
@@ -84,32 +89,47 @@ struct SlabSet {
   SlabSrc s[kMaxSlabs];
   int ns = 0;
   int* rearm = nullptr;  // producer counter zeroed by block 0 after the barrier
+  int blanes = 1;        // grid-barrier arrival words (> 1: kBarStride u64 apart, sync holds
+                         // 1 + 2 * blanes * kBarStride words): arrivals of a few hundred
+                         // workgroups on ONE word serialise (~10 ns each)
 };
+constexpr int kBarStride = 8;  // u64: 64 B
 
 __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Column `col` of a [rows][n] slab summed over rows g, g + G, ... in that order; 16 rows
-// per batch in flight (clamped, masked).  SC1: L2-coherent loads (rows written by other
-// workgroups of this launch).  G = 16 is slab_colsum<16>'s association (the column-sum
-// launch's): the same sums bitwise.
-template <int G, bool SC1>
-__device__ __forceinline__ float slab_colsum_x(const float* __restrict__ slab, int rows, int n, int col, int g) {
-  if (rows <= 0 || n <= 0) return 0.f;
-  const int cc = col < n ? col : n - 1;
-  float a = 0.f;
-  for (int r0 = g; r0 < rows; r0 += 16 * G) {
-    float v[16];
+// K column chunks of CC = 256/G columns at c0, c0 + CC, ...: this lane's column of each
+// chunk (c0 + j*CC + tid % CC) summed over rows g, g + G, ... in that order, g = tid / CC.
+// Every chunk's first 16 rows per lane are loaded before any add (one round trip for the
+// ConvNet's <= 16 G-row slabs); clamped, masked.  SC1: L2-coherent loads (rows written by
+// other workgroups of this launch).
+template <int G, int K, bool SC1>
+__device__ __forceinline__ void slab_colsum_k(const float* __restrict__ slab, int rows, int n, int c0, float* out) {
+  constexpr int CC = 256 / G;
+  const int g = threadIdx.x / CC, cl = threadIdx.x % CC;
+  float v[K][16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const float* p = slab + (size_t)min(r0 + j * G, rows - 1) * n + cc;
-      v[j] = SC1 ? ld_sc1(p) : *p;
+  for (int j = 0; j < K; ++j) {
+    const int cc = min(c0 + j * CC + cl, n - 1);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const float* p = slab + (size_t)min(g + u * G, rows - 1) * n + cc;
+      v[j][u] = SC1 ? ld_sc1(p) : *p;
     }
-#pragma unroll
-    for (int j = 0; j < 16; ++j) a += (r0 + j * G < rows) ? v[j] : 0.f;
   }
-  return col < n ? a : 0.f;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const int cc = min(c0 + j * CC + cl, n - 1);
+    float a = 0.f;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) a += (g + u * G < rows) ? v[j][u] : 0.f;
+    for (int r = g + 16 * G; r < rows; r += G) {  // slabs taller than 16 G rows
+      const float* p = slab + (size_t)r * n + cc;
+      a += SC1 ? ld_sc1(p) : *p;
+    }
+    out[j] = a;
+  }
 }
 
 // bid: this workgroup's index among the launch's AMP workgroups; grid: their count.
@@ -126,7 +146,7 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
   __shared__ float* sp1[MAXT];
   __shared__ float* sp2[MAXT];
   __shared__ int s_bad;
-  __shared__ float spart[THR + 16];  // slab workgroups: (256 / cols) row groups x (cols + 1)
+  __shared__ float spart[16 * 65];   // slab workgroups: G row groups x (columns + 1)
   const int tid = threadIdx.x;
   const int n = L.n;
   {  // the table: every load issued before any LDS write (clamped index; a guarded load was
@@ -145,6 +165,7 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
     }
   }
   __syncthreads();
+  DPA_STAMP(9);
   const int total = soff[n];
   // the barrier generation is only used by lane 0: issued after the table
   // barrier, its load stays in flight (no LDS round trip) with the gradients'
@@ -189,9 +210,9 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
         si = s + 1;
       }
     const SlabSrc S = ss.s[si];
-    const int cols = S.cols, G = THR / cols;
+    const int G = S.groups, CC = THR / G, K = S.chunks, cols = CC * K;
     const int c0 = (bid - base) * cols;
-    const int col = c0 + tid % cols, g = tid / cols;
+    const int col = c0 + tid;  // the column this lane owns (tid < cols)
     if (tid < cols && col < S.n) {  // param / buffer loads in flight with the slab's
       const float* gp = S.out + col;
       for (int i = 0; i < n; ++i)  // the tensor whose gradient holds this column (host-checked: one)
@@ -204,8 +225,9 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
         if (momentum != 0.f && !((L.first_bits >> st_t) & 1ull)) st_b = sp2[st_t][st_e];
       }
     }
-    float v;
-    if (S.wait != nullptr) {
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    const bool sc1 = S.wait != nullptr;
+    if (sc1) {
       // rows produced in this launch: wait (bounded) for every producer's arrival
       if (tid == 0) {
         const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
@@ -219,13 +241,18 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
         }
       }
       __syncthreads();
-      v = G == 16 ? slab_colsum_x<16, true>(S.slab, S.rows, S.n, col, g)
-                  : slab_colsum_x<4, true>(S.slab, S.rows, S.n, col, g);
-    } else {
-      v = G == 16 ? slab_colsum_x<16, false>(S.slab, S.rows, S.n, col, g)
-                  : slab_colsum_x<4, false>(S.slab, S.rows, S.n, col, g);
+      DPA_STAMP(10);
     }
-    spart[g * (cols + 1) + tid % cols] = v;  // = slab_reduce's association (G = 16)
+    if (G == 8)
+      slab_colsum_k<8, 1, false>(S.slab, S.rows, S.n, c0, v);
+    else if (K == 4)
+      slab_colsum_k<16, 4, false>(S.slab, S.rows, S.n, c0, v);
+    else if (sc1)
+      slab_colsum_k<16, 1, true>(S.slab, S.rows, S.n, c0, v);
+    else
+      slab_colsum_k<16, 1, false>(S.slab, S.rows, S.n, c0, v);
+    const int g = tid / CC, cl = tid % CC;
+    for (int j = 0; j < K; ++j) spart[g * (cols + 1) + j * CC + cl] = v[j];
     __syncthreads();
     if (tid < cols && col < S.n) {
       for (int gg = 0; gg < G; ++gg) st_sum += spart[gg * (cols + 1) + tid];
@@ -256,6 +283,7 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
       }
     }
   }
+  DPA_STAMP(11);
   if constexpr (XG) {
     __shared__ uint32_t ep_x;
     if (tid == 0) ep_x = xgmi::xsite_epoch(xg, tk, bid);
@@ -353,17 +381,26 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
   if (grid == 1) {  // uniform: one workgroup needs no grid barrier
     if (tid == 0) s_bad = block_bad;
   } else if (tid == 0) {
-    unsigned long long* word = &sync[1 + (gen & 1)];
+    // arrival words of this launch's parity: one (blanes == 1) or blanes, kBarStride apart
+    const int nl = ss.blanes, st = nl > 1 ? kBarStride : 1;
+    unsigned long long* words = &sync[1 + (int)(gen & 1) * nl * st];
     const unsigned long long Gn = (unsigned long long)grid;
-    __hip_atomic_fetch_add(word, 1ull | ((unsigned long long)block_bad << 32), __ATOMIC_RELAXED,
+    __hip_atomic_fetch_add(words + (bid % nl) * st, 1ull | ((unsigned long long)block_bad << 32), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-    unsigned long long v;
     // bounded: the host sizes the grid to be co-resident, so every workgroup arrives;
-    // should one never do, give up after barrier_ticks, flag it and skip the update
+    // should one never do, give up after barrier_ticks, flag it and skip the update.
+    // Polled with atomic loads (a polling read-modify-write competes with the arrivals)
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    bool timed_out = false;
-    while (((v = __hip_atomic_fetch_add(word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & 0xffffffffull) <
-           Gn) {
+    bool timed_out = false, any = false;
+    for (;;) {
+      unsigned long long cnt = 0;
+      any = false;
+      for (int l = 0; l < nl; ++l) {
+        const unsigned long long v = __hip_atomic_load(words + l * st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cnt += v & 0xffffffffull;
+        any |= (v >> 32) != 0;
+      }
+      if (cnt >= Gn) break;
       __builtin_amdgcn_s_sleep(1);
       if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > barrier_ticks) {
         timed_out = true;
@@ -371,15 +408,18 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
         break;
       }
     }
-    s_bad = timed_out || (v >> 32) != 0;
+    s_bad = timed_out || any;
     if (bid == 0) {
-      __hip_atomic_exchange(&sync[1 + ((gen + 1) & 1)], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned long long* other = &sync[1 + (int)((gen + 1) & 1) * nl * st];
+      for (int l = 0; l < nl; ++l)
+        __hip_atomic_store(other + l * st, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_fetch_add(&sync[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // every slab owner waiting on the in-launch producers passed its wait before arriving
       if (ss.rearm != nullptr) __hip_atomic_store(ss.rearm, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   __syncthreads();
+  DPA_STAMP(12);
   const bool any_bad = s_bad;
 #pragma unroll
   for (int k = 0; k < U; ++k) {
@@ -414,6 +454,7 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
       sp0[st_t][st_e] = st_p - lr * d;
     }
   }
+  DPA_STAMP(13);
   if (bid == 0 && tid == 0) {
     // every workgroup read scale[0] before arriving, and block 0 passed the barrier
     found_inf[0] = 0.f;
@@ -470,10 +511,13 @@ inline MTList fused_list(const std::vector<at::Tensor>& params, const std::vecto
 
 // one slab source: slab [rows][out.numel()] -> the gradient region `out`, which must start
 // and end on granule boundaries of the tensors that cover it
-inline void add_slab(SlabSet& ss, const MTList& L, const at::Tensor& slab, const at::Tensor& out, int cols,
-                     const int* wait, int wait_n) {
+inline void add_slab(SlabSet& ss, const MTList& L, const at::Tensor& slab, const at::Tensor& out, int groups,
+                     int chunks, const int* wait, int wait_n) {
   TORCH_CHECK(ss.ns < kMaxSlabs, "fused AMP-SGD: at most ", kMaxSlabs, " slab sources");
-  TORCH_CHECK(cols == 16 || cols == 64, "fused AMP-SGD: 16 or 64 slab columns per workgroup");
+  TORCH_CHECK((groups == 16 && (chunks == 1 || chunks == 4)) || (groups == 8 && chunks == 1),
+              "fused AMP-SGD: slab layouts G = 16 x 1 | 4 chunks, G = 8 x 1 chunk");
+  TORCH_CHECK(wait == nullptr || (groups == 16 && chunks == 1), "fused AMP-SGD: an in-launch slab is G = 16 x 1");
+  const int cols = 256 / groups * chunks;
   TORCH_CHECK(slab.is_cuda() && slab.is_contiguous() && slab.scalar_type() == at::kFloat && out.is_cuda() &&
                   out.is_contiguous() && out.scalar_type() == at::kFloat, "fused AMP-SGD: f32 slab / out");
   const int64_t ncol = out.numel();
@@ -495,7 +539,8 @@ inline void add_slab(SlabSet& ss, const MTList& L, const at::Tensor& slab, const
   S.out = out.data_ptr<float>();
   S.rows = (int)(slab.numel() / ncol);
   S.n = (int)ncol;
-  S.cols = cols;
+  S.groups = groups;
+  S.chunks = chunks;
   S.nblk = (int)((ncol + cols - 1) / cols);
   S.wait = wait;
   S.wait_n = wait_n;

@@ -894,12 +894,14 @@ convnet_amp_step_kernel(const T* __restrict__ x, float* __restrict__ wslab1, Bwd
                         int interval, xgmi::XSite xg, int* __restrict__ err, long long barrier_ticks, opt::SlabSet ss,
                         int grid_amp) {
   const int bid = (int)blockIdx.x;
+  DPA_STAMP(0);
   if (bid < nw1) {
     constexpr int ns = (28 + WG1_ROWS_ - 1) / WG1_ROWS_;
     cb::conv5x5_wgrad_body<T, 1, 16, 28, 28, WG1_ROWS_, 2, true>(x, nullptr, wslab1, ns, bi, bid);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's row has left the CU
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(w1cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    DPA_STAMP(8);
     return;
   }
   opt::amp_sgd_body<CAS_U, XG>(L, scale, tracker, found_inf, sync, lr, momentum, dampening, wd, nesterov, maximize,
@@ -910,7 +912,7 @@ convnet_amp_step_kernel(const T* __restrict__ x, float* __restrict__ wslab1, Bwd
 static std::pair<int, int> cas_shape(int64_t B, int64_t n_params_granules) {
   const int nw1 = (int)wgrad_bn_rows(1, B);
   const int nreg = (int)std::max<int64_t>(1, (n_params_granules + opt::FUSED_THR * CAS_U - 1) / (opt::FUSED_THR * CAS_U));
-  const int s0 = (32 + 15) / 16, s1 = (16 * 25 + 16 + 15) / 16, s2 = (32 * 400 + 32 + 63) / 64;
+  const int s0 = 1, s1 = (16 * 25 + 16 + 15) / 16, s2 = (32 * 400 + 32 + 63) / 64;
   return {nw1, nreg + s0 + s1 + s2};
 }
 
@@ -948,8 +950,8 @@ void convnet_amp_step(std::vector<at::Tensor> params, std::vector<at::Tensor> gr
   const int B = (int)y1.size(0);
   TORCH_CHECK(x.size(1) == 1 && y1.size(1) == 16 && y1.size(2) == 28 && x.scalar_type() == y1.scalar_type());
   TORCH_CHECK(w1cnt.scalar_type() == at::kInt && w1cnt.numel() >= 1, "convnet_amp_step: w1cnt int32[1]");
-  TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == at::kLong && sync.numel() >= 4 && sync.is_contiguous(),
-              "convnet_amp_step: sync must be a zero-initialised int64[4] device tensor");
+  TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == at::kLong && sync.is_contiguous(),
+              "convnet_amp_step: sync must be a zero-initialised int64 device tensor");
   TORCH_CHECK(scale.scalar_type() == at::kFloat && found_inf.scalar_type() == at::kFloat &&
               tracker.scalar_type() == at::kInt);
   constexpr int N1 = 16 * 25 + 16, N2 = 32 * 400 + 32;
@@ -960,10 +962,15 @@ void convnet_amp_step(std::vector<at::Tensor> params, std::vector<at::Tensor> gr
   if (B == 0) return;
   opt::MTList L = opt::fused_list(params, grads, bufs, first, momentum);
   opt::SlabSet ss;
-  opt::add_slab(ss, L, bn1, out0, 16, nullptr, 0);
-  opt::add_slab(ss, L, wslab1, out1, 16, w1cnt.data_ptr<int>(), nw1);
-  opt::add_slab(ss, L, wslab2, out2, 64, nullptr, 0);
+  // the flush path's associations (bitwise the same gradients): BN1 sums as cb::colsum_rows
+  // (2C = 32 columns, G = 8), the weight-gradient slabs as slab_reduce (G = 16)
+  opt::add_slab(ss, L, bn1, out0, 8, 1, nullptr, 0);
+  opt::add_slab(ss, L, wslab1, out1, 16, 1, w1cnt.data_ptr<int>(), nw1);
+  opt::add_slab(ss, L, wslab2, out2, 16, 4, nullptr, 0);
   ss.rearm = w1cnt.data_ptr<int>();
+  ss.blanes = 8;  // ~240 arriving workgroups: arrivals spread over 8 words
+  TORCH_CHECK(sync.numel() >= 1 + 2 * ss.blanes * opt::kBarStride, "convnet_amp_step: sync must hold ",
+              1 + 2 * ss.blanes * opt::kBarStride, " int64");
   const auto sh = cas_shape(B, L.chunk_off[L.n]);
   int nslab = 0;
   for (int s = 0; s < ss.ns; ++s) nslab += ss.s[s].nblk;
@@ -995,7 +1002,8 @@ void convnet_amp_step(std::vector<at::Tensor> params, std::vector<at::Tensor> gr
                            tracker.data_ptr<int>(), found_inf.data_ptr<float>(),
                            reinterpret_cast<unsigned long long*>(sync.data_ptr<int64_t>()), (float)lr,
                            (float)momentum, (float)dampening, (float)wd, (int)nesterov, (int)maximize, (float)growth,
-                           (float)backoff, (int)interval, xg, reinterpret_cast<int*>(sync.data_ptr<int64_t>() + 3),
+                           (float)backoff, (int)interval, xg,
+                           reinterpret_cast<int*>(sync.data_ptr<int64_t>() + sync.numel() - 1),
                            (long long)(kBarrierSeconds * 1e8), ss, grid_amp);
       };
       if (xc) go(convnet_amp_step_kernel<T, true>);

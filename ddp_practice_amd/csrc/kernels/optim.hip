@@ -452,7 +452,7 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
   MTList L = fused_list(params, grads, bufs, first, momentum);
   SlabSet ss;
   TORCH_CHECK(slab.has_value() == slab_out.has_value(), "fused AMP-SGD: slab and slab_out go together");
-  if (slab.has_value()) add_slab(ss, L, *slab, *slab_out, 16, nullptr, 0);
+  if (slab.has_value()) add_slab(ss, L, *slab, *slab_out, 16, 1, nullptr, 0);
   auto launch = [&](auto kern, int bg, xgmi::XSite xg) {
     const int grid = (int)std::max<int64_t>(1, (L.chunk_off[L.n] + bg - 1) / bg) + (ss.ns ? ss.s[0].nblk : 0);
     TORCH_CHECK(grid <= FUSED_MAX_BLOCKS, "fused AMP-SGD: grid exceeds the co-resident bound");

@@ -56,14 +56,24 @@ _SPLIT_BWD2 = os.environ.get("DPA_SPLIT_BWD2", "0") == "1"
 _SPLIT_WGRAD1 = os.environ.get("DPA_SPLIT_WGRAD1", "1") == "1"  # merged launch measured slower (15.0 vs 10.9 us)
 # conv1 wgrad + conv2 slab sums in one launch even without a slab sink (A/B; then a conv1-only sum launch)
 _WGRAD1_SLAB2 = os.environ.get("DPA_WGRAD1_SLAB2", "0") == "1"
-# conv1's weight gradient deferred into the optimizer's fused launch (DPA_DEFER_WGRAD1=0: A/B)
-_DEFER_WGRAD1 = os.environ.get("DPA_DEFER_WGRAD1", "1") == "1"
+# conv1's weight gradient deferred into the optimizer's fused launch (5 launches per step):
+# measured no faster than the two launches it merges (54.2-54.6 vs 54.1-54.2 us/step,
+# profiles/r4h_defer_wgrad1_ab.txt): the in-launch producer -> slab-owner hand-off (write-
+# through rows, arrival counter, polling) costs ~3 us, more than the kernel boundary it
+# removes.  Opt-in: DPA_DEFER_WGRAD1=1
+_DEFER_WGRAD1 = os.environ.get("DPA_DEFER_WGRAD1", "0") == "1"
 _CAS_OK: dict = {}
 
 
 def _wgrad1_deferrable(B: int, dtype: torch.dtype, opt) -> bool:
     """convnet.convnet_amp_step can run this batch size / dtype on this device (its AMP
-    workgroups co-resident) and the optimizer's step takes the small fused path."""
+    workgroups co-resident) and the optimizer's step takes the small fused path.
+
+    Not for ranks sharing one GPU (DPA_SHARED_GPU=1, bench.py --share-gpu): the launch's
+    ~470 workgroups per rank wait on the peers' exchange inside the kernel, and two ranks'
+    launches do not fit the card together (a peer's workgroups could never be placed)."""
+    if os.environ.get("DPA_SHARED_GPU") == "1" and getattr(opt, "_deferred_ddp", None) is not None:
+        return False
     if not getattr(opt, "small_fusable", lambda: False)():
         return False
     gran = sum((p.numel() + 3) // 4 for g in opt.param_groups for p in g["params"])
@@ -309,10 +319,11 @@ class ConvNetFn(torch.autograd.Function):
             # the conv1 weight gradient itself, BN1's and conv2's column sums: all computed
             # inside the optimizer's fused launch (convnet.convnet_amp_step); the backward
             # launches nothing more.  Any other gradient reader flushes first (optim.SGD)
+            # (only regions of `out` other than the returned views: a second reference to a
+            # returned gradient makes autograd copy it into .grad now, before it is computed)
             sink.defer_wgrad1(dict(x=x, y1=y1, dp1=dp1, idx1=idx1, fstats1=fstats1, gsum1=gsum1, lsum1=lsum1, g1=g1,
-                                   e1=e1, dg1=dg1, dbe1=dbe1, wslab1=wslab1, out1=out1,
-                                   bn1=lsum1 if lsum1 is not None else gsum1, out0=out0, wslab2=wslab2, out2=out2,
-                                   xc1=xc1))
+                                   e1=e1, wslab1=wslab1, out1=out1, bn1=lsum1 if lsum1 is not None else gsum1,
+                                   out0=out0, wslab2=wslab2, out2=out2, xc1=xc1))
         elif sink is not None or _WGRAD1_SLAB2:
             # conv1 wgrad partials + the conv2 slab's column sums in one launch; the conv1
             # slab's sums run inside the fused AMP-SGD launch (optim.SGD.defer_slab) or next

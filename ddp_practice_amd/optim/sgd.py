@@ -69,9 +69,10 @@ class SGD(Optimizer):
         w = self.__dict__.pop("_pending_wgrad1", None)
         if w is not None:  # the launches the deferral saved
             C = _load_ext()
+            out0 = w["out0"]  # [dbeta1 | dgamma1]
             C.convnet.conv1_wgrad_slab2(w["x"], w["y1"], w["dp1"], w["idx1"], w["fstats1"], w["gsum1"], w["lsum1"],
-                                        w["g1"], w["e1"], w["dg1"], w["dbe1"], w["wslab1"], w["wslab2"], w["out2"],
-                                        w["xc1"])
+                                        w["g1"], w["e1"], out0.narrow(0, 16, 16), out0.narrow(0, 0, 16), w["wslab1"],
+                                        w["wslab2"], w["out2"], w["xc1"])
             C.convblock.slab_reduce(w["wslab1"], w["out1"].numel(), w["out1"])
         ps = self.__dict__.pop("_pending_slab", None)
         if ps is not None:
@@ -239,7 +240,8 @@ class SGD(Optimizer):
             del self._pending_wgrad1
             cas = getattr(self, "_amp_sync_cas", None)
             if cas is None or cas[0].device != params[0].device:
-                cas = self._amp_sync_cas = (torch.zeros(4, dtype=torch.int64, device=params[0].device),
+                # grid-barrier state: generation, 2 parities x 8 arrival words 64 B apart, error word
+                cas = self._amp_sync_cas = (torch.zeros(1 + 2 * 8 * 8 + 1, dtype=torch.int64, device=params[0].device),
                                             torch.zeros(1, dtype=torch.int32, device=params[0].device))
             _load_ext().convnet.convnet_amp_step(
                 params, grads, bufs, group["lr"], group["momentum"], group["dampening"], group["weight_decay"],

@@ -54,6 +54,10 @@ wrap(C.convnet, "conv2_bwd", lambda a: [("conv2_bwd/dgrad", slice(0, 2 * B)),
                                          ("conv2_bwd/wgrad", slice(2 * B, 2 * B + 4 * B))])
 wrap(C.convnet, "conv2_fwd", lambda a: [("conv2_fwd", slice(0, 2 * B))])
 wrap(C.convnet, "wgrad1_reduce", lambda a: [("wgrad1_reduce/wgrad", slice(0, 7 * B))])
+wrap(C.convnet, "conv1_wgrad_slab2", lambda a: [("wgrad1_slab2/wgrad", slice(0, 7 * B)),
+                                                 ("wgrad1_slab2/sums", slice(7 * B, 512))])
+wrap(C.convnet, "convnet_amp_step", lambda a: [("amp_step/producers", slice(0, 7 * B)),
+                                                ("amp_step/amp", slice(7 * B, 512))])
 
 from ddp_practice_amd.amp import GradScaler  # noqa: E402
 from ddp_practice_amd.data import DeviceLoader  # noqa: E402
@@ -66,6 +70,7 @@ torch.manual_seed(0)
 m = ConvNet(amp_dtype=torch.bfloat16).to(dev)
 opt = SGD(m.parameters(), lr=1e-4)
 scaler = GradScaler()
+m.set_slab_sink(opt)  # as engine.TrainLoop: conv1's weight gradient inside the optimizer launch
 crit = CrossEntropyLoss()
 for it in range(4):
     x = torch.rand(B, 1, 28, 28, device=dev).to(torch.bfloat16)

@@ -285,13 +285,17 @@ def test_deferred_gather_in_conv1(C, dtype):
         torch.testing.assert_close(sd_a[k].float(), sd_b[k].float(), rtol=1e-5, atol=1e-6, msg=k)
 
 
+@pytest.mark.parametrize("defer", [False, True])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-def test_slab_sink_matches_separate_sums(C, dtype):
+def test_slab_sink_matches_separate_sums(C, dtype, defer, monkeypatch):
     """With a slab sink the conv1 weight gradient and the BN1 / conv1 / conv2 gradient column
     sums run inside the optimizer's fused launch (SGD.defer_wgrad1, convnet.convnet_amp_step:
-    5 launches per step) == the separate launches, eagerly and graph-replayed (fp32 sums in
-    another association: allclose, not bitwise); no slab_reduce launch is left once the
-    fused step runs."""
+    5 launches per step; opt-in, ``defer``) -- or only the conv1 column sums (SGD.defer_slab,
+    the default) -- == the separate launches, bitwise, eagerly and graph-replayed; no
+    slab_reduce launch is left once the fused step runs."""
+    from ddp_practice_amd.ops import convnet_fused
+
+    monkeypatch.setattr(convnet_fused, "_DEFER_WGRAD1", defer)
     from ddp_practice_amd.amp import GradScaler
     from ddp_practice_amd.data import DeviceLoader, synthetic
     from ddp_practice_amd.nn import CrossEntropyLoss
@@ -348,9 +352,10 @@ def test_slab_sink_matches_separate_sums(C, dtype):
         assert "_pending_slab" not in opt.__dict__ and "_pending_wgrad1" not in opt.__dict__
         runs.append((copy.deepcopy(m.state_dict()), eager_calls))
     (sd_a, calls_a), (sd_b, calls_b) = runs
-    assert calls_a == [2, 0] and calls_b == [0, 2], (calls_a, calls_b)
+    assert calls_a == [2, 0] and calls_b == [0, 2 if defer else 0], (calls_a, calls_b)
+    # the merged launch sums in the separate launches' association: bitwise the same training
     for k in sd_a:
-        torch.testing.assert_close(sd_b[k].float(), sd_a[k].float(), rtol=1e-4, atol=1e-6, msg=k)
+        assert torch.equal(sd_a[k], sd_b[k]), k
 
 
 def test_slab_sink_flushes_for_grad_readers(C):
@@ -378,3 +383,95 @@ def test_slab_sink_flushes_for_grad_readers(C):
         grads.append([p.grad.clone() for p in m.parameters()])
     for a, b in zip(*grads):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_deferred_wgrad1_grads_match_flush(C, dtype, monkeypatch):
+    """The optimizer's merged launch (convnet.convnet_amp_step: conv1 weight gradient by
+    producer workgroups, BN1 / conv1 / conv2 column sums by slab workgroups) writes the same
+    unscaled gradients as the flush path (conv1_wgrad_slab2 + slab_reduce), bitwise, per
+    parameter, from the same backward (lr = 0: the update is a no-op)."""
+    from ddp_practice_amd.amp import GradScaler
+    from ddp_practice_amd.nn import CrossEntropyLoss
+    from ddp_practice_amd.ops import convnet_fused
+    from ddp_practice_amd.optim import SGD
+
+    monkeypatch.setattr(convnet_fused, "_DEFER_WGRAD1", True)  # opt-in path (DPA_DEFER_WGRAD1=1)
+    g = torch.Generator(device="cpu").manual_seed(11)
+    m = _model()
+    m.amp_dtype = dtype
+    opt, scaler, crit = SGD(m.parameters(), lr=0.0), GradScaler(init_scale=256.0), CrossEntropyLoss()
+    assert m.set_slab_sink(opt)
+    for it in range(3):
+        x = torch.rand(32, 1, 28, 28, generator=g).to(DEV, dtype)
+        y = torch.randint(0, 10, (32,), generator=g).to(DEV)
+        opt.zero_grad(set_to_none=True)
+        scaler.scale(crit(m(x), y)).backward()
+        pending = opt.__dict__.get("_pending_wgrad1")
+        if it == 0 or pending is None:
+            scaler.step(opt)  # first step: unfused (flushes)
+            scaler.update()
+            continue
+        inv = 1.0 / scaler._scale.item()
+        opt.flush_slab()
+        ref = {n: p.grad.detach().clone() * inv for n, p in m.named_parameters()}
+        # the merged launch must recompute every conv1 partial row before its slab owners
+        # read them: poisoned rows would surface as NaN gradients
+        pending["wslab1"].fill_(float("nan"))
+        opt._pending_wgrad1 = pending  # the same deferred work, now through the merged launch
+        scaler.step(opt)
+        scaler.update()
+        torch.cuda.synchronize()
+        assert "_pending_wgrad1" not in opt.__dict__
+        for n, p in m.named_parameters():  # the flush path's association: bitwise
+            assert torch.equal(p.grad, ref[n]), (n, (p.grad - ref[n]).abs().max().item())
+
+
+def test_deferred_wgrad1_graph_replay_waits_for_producers(C, monkeypatch):
+    """Graph-replayed merged steps (convnet.convnet_amp_step) with the conv1 partial rows
+    poisoned (NaN) before every replay: the slab owners wait for the in-launch producers,
+    so no step sees a NaN gradient (found_inf would halve the scale and skip the step)."""
+    from ddp_practice_amd.amp import GradScaler
+    from ddp_practice_amd.data import DeviceLoader, synthetic
+    from ddp_practice_amd.nn import CrossEntropyLoss
+    from ddp_practice_amd.optim import SGD
+    from ddp_practice_amd.ops import convnet_fused
+    from ddp_practice_amd.runtime import CapturedStep
+
+    monkeypatch.setattr(convnet_fused, "_DEFER_WGRAD1", True)  # opt-in path (DPA_DEFER_WGRAD1=1)
+    ds = synthetic(32 * 24, seed=6)
+    m = _model()
+    m.amp_dtype = torch.bfloat16
+    loader = DeviceLoader(ds, batch_size=32, shuffle=False, device=DEV, dtype=torch.bfloat16)
+    images, labels = loader.static_batch()
+    opt, scaler, crit = SGD(m.parameters(), lr=0.01), GradScaler(init_scale=256.0), CrossEntropyLoss()
+    assert m.set_slab_sink(opt)
+    slabs = []
+    orig = opt.defer_wgrad1
+
+    def record(w):
+        slabs.append(w["wslab1"])
+        return orig(w)
+
+    opt.defer_wgrad1 = record
+
+    def step():
+        loader.fill_(images, labels, defer=True)
+        loss = crit(m(images), labels)
+        opt.zero_grad(set_to_none=True)
+        scaler.scale(loss).backward()
+        scaler.step(opt)
+        scaler.update()
+
+    loader.start_epoch()
+    step()
+    runner = CapturedStep(step, warmup=1, steps_per_graph=1)
+    assert runner.capture()
+    wslab1 = slabs[-1]  # the captured step's buffer (graph pool: fixed across replays)
+    s0 = scaler._scale.item()
+    for _ in range(8):
+        wslab1.fill_(float("nan"))
+        runner.run()
+    torch.cuda.synchronize()
+    assert scaler._scale.item() == s0, "a replay saw a non-finite gradient (stale / poisoned conv1 rows)"
+    assert all(torch.isfinite(p).all() for p in m.parameters())
