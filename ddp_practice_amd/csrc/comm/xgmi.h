@@ -54,6 +54,11 @@ class XgmiComm {
   XSite site(int s) const;
   // the DDP gradient exchange of the fused AMP-SGD step (rows of max_bytes/4 floats)
   XSite grad_site() const;
+  // the ResNet statistics finishers' site (rows of kWideVals floats; nblk set per launch)
+  XSite wide_site() const;
+  // test entry: `nblk` finisher workgroups each exchange a slice of `in` (<= kWideVals
+  // floats) through the wide site with the positioned form; out = the global row
+  void wide_probe(const at::Tensor& in, const at::Tensor& out, int nblk);
   long long max_elems() const { return max_elems_; }
 
  private:
@@ -65,6 +70,7 @@ class XgmiComm {
   unsigned long long* ticks_ = nullptr;  // per-site {epoch | tickets} words (ordinary device memory)
   long long site_off_ = 0;               // byte offset of the fused-site regions in every workspace
   long long grad_off_ = 0;               // byte offset of the gradient-exchange region
+  long long wide_off_ = 0;               // byte offset of the wide site's region
   long long ts_off_ = 0, ts_par_bytes_ = 0, ts_shard_max_ = 0, ts_max_elems_ = 0;  // two-shot region
   int ts_blocks_ = 0, ts_grid_ = 0;
   bool ts_used_ = false;

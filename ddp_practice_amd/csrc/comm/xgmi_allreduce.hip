@@ -409,7 +409,8 @@ XgmiComm::XgmiComm(int rank, int world, int device, long long slot_bytes, double
     ts_blocks_ = kTwoShotMaxBlocks;
     ts_grid_ = (int)std::min<long long>(kTwoShotMaxBlocks, ts_shard_max_ / kChunkElems);
   }
-  ws_bytes_ = ((ts_off_ + 2 * ts_par_bytes_ + 4095) / 4096) * 4096;
+  wide_off_ = ((ts_off_ + 2 * ts_par_bytes_ + 4095) / 4096) * 4096;  // then the wide site: [2][kMaxRanks] rows
+  ws_bytes_ = ((wide_off_ + 2LL * kMaxRanks * kWideVals * 8 + 4095) / 4096) * 4096;
   timeout_ticks_ = (long long)(timeout_s * 1e8);
   c10::hip::HIPGuard guard(device_);
   void* p = nullptr;
@@ -610,6 +611,43 @@ XSite XgmiComm::grad_site() const {
   return x;
 }
 
+XSite XgmiComm::wide_site() const {
+  XSite x = site(kSiteWide);
+  for (int p = 0; p < world_; ++p) x.base[p] = peers_.base[p] + wide_off_;
+  x.slot_bytes = (long long)kWideVals * 8;
+  x.max_vals = kWideVals;
+  return x;
+}
+
+// Test entry for the positioned exchange: finisher b of nblk owns the row positions
+// [b*n/nblk, (b+1)*n/nblk), stored to out from the exchanged slice (the statistics
+// finishers of conv_igemm.hip / bn_nhwc.hip in isolation: sizes up to 2*2048+1).
+__global__ void __launch_bounds__(256) wide_probe_kernel(XSite xs, const float* __restrict__ in,
+                                                         float* __restrict__ out, int n) {
+  __shared__ float vals[kWideVals];
+  const int b = (int)blockIdx.x, nb = (int)gridDim.x;
+  const int lo = (int)((long long)n * b / nb), hi = (int)((long long)n * (b + 1) / nb);
+  unsigned long long tk = 0;
+  if (threadIdx.x == 0) tk = xsite_ticket(xs, b);
+  for (int i = threadIdx.x; i < hi - lo; i += 256) vals[i] = in[lo + i];
+  __syncthreads();
+  xsite_exchange_slice(xs, vals, hi - lo, [&](int i) { return lo + i; }, tk, b, 256);
+  for (int i = threadIdx.x; i < hi - lo; i += 256) out[lo + i] = vals[i];
+}
+
+void XgmiComm::wide_probe(const at::Tensor& in, const at::Tensor& out, int nblk) {
+  TORCH_CHECK(in.is_cuda() && in.scalar_type() == at::kFloat && in.is_contiguous() && in.numel() <= kWideVals &&
+                  in.numel() >= 1,
+              "wide_probe: 1..", kWideVals, " contiguous f32 values");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.numel() == in.numel(), "wide_probe: out like in");
+  TORCH_CHECK(nblk >= 1 && nblk <= in.numel(), "wide_probe: 1..n finishers");
+  XSite xs = wide_site();
+  xs.nblk = nblk;
+  hipLaunchKernelGGL(wide_probe_kernel, dim3(nblk), dim3(256), 0, cur_stream(), xs, in.data_ptr<float>(),
+                     out.data_ptr<float>(), (int)in.numel());
+  DPA_CHECK_LAUNCH();
+}
+
 // Test entry for the in-kernel exchange (comm/xsite.h): `grid` workgroups each
 // exchange the same n (<= kSiteVals) floats through site s and write the
 // rank-ordered global sums to out[block][n] -- the protocol every fused SyncBN
@@ -760,6 +798,7 @@ void register_xgmi(pybind11::module& m) {
              return dst;
            },
            py::arg("t"), py::arg("op") = "sum", py::arg("out") = py::none())
+      .def("wide_probe", &xgmi::XgmiComm::wide_probe, py::arg("inp"), py::arg("out"), py::arg("nblk"))
       .def("site_probe", &xgmi::XgmiComm::site_probe, py::arg("site"), py::arg("inp"), py::arg("out"),
            py::arg("grid") = 1)
       .def("all_reduce_twoshot",

@@ -49,6 +49,11 @@ constexpr long long kSiteBytes = 2LL * kMaxRanks * kSiteSlotBytes;   // both par
 
 // site ids (ops/convnet_fused.py): one per consumer launch of a step
 enum : int { kSiteFwd1 = 0, kSiteFwd2 = 1, kSiteBwd2Dgrad = 2, kSiteBwd2Wgrad = 3, kSiteBwd1 = 4 };
+// the statistics finishers of the ResNet kernels (conv_igemm.hip stat trees, bn_nhwc.hip
+// fwd / bwd statistics): every SyncBN exchange of the network on ONE site, launch after
+// launch on the compute stream, rows of up to kWideVals floats (2C+1, C <= 2048)
+constexpr int kSiteWide = 5;
+constexpr int kWideVals = 4224;
 // the DDP gradient exchange inside the fused AMP-SGD kernel (XgmiComm::grad_site):
 // its own epoch word, slots of the engine's full message size
 constexpr int kSiteGrad = kSites - 1;
@@ -167,6 +172,62 @@ __device__ __forceinline__ void xsite_exchange(const XSite& xs, float* vals, int
     }
     vals[tid] = acc;  // only this lane reads or writes slot tid in here
   }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Positioned form, for launches whose row is split over several finisher workgroups
+// (the last arriver of each channel slice of a statistics tree): each lane exchanges the
+// values it owns at their row positions.  Lane 0 of every finisher takes one ticket
+// (xsite_ticket with XSite.nblk = the launch's finisher count) and the launch's epoch
+// (xsite_epoch); a lane pushes all its positions first (xsite_push_at), then pulls them
+// (xsite_pull_at: every peer's granule, summed in rank order).  Same granules, parities
+// and reuse argument as above: positions are disjoint between a launch's finishers.
+__device__ __forceinline__ void xsite_push_at(const XSite& xs, uint32_t ep, int pos, float mine) {
+  const long long off = (long long)(ep & 1u) * kMaxRanks * xs.slot_bytes + (long long)xs.rank * xs.slot_bytes +
+                        (long long)pos * 8;
+  const unsigned long long gm = ((unsigned long long)ep << 32) | (unsigned long long)__float_as_uint(mine);
+  for (int p = 0; p < xs.world; ++p)
+    if (p != xs.rank) *reinterpret_cast<unsigned long long*>(xs.base[p] + off) = gm;
+}
+
+__device__ __forceinline__ float xsite_pull_at(const XSite& xs, uint32_t ep, int pos, float mine, long long t0,
+                                               unsigned& polls, bool& fail) {
+  const long long off = (long long)(ep & 1u) * kMaxRanks * xs.slot_bytes + (long long)pos * 8;
+  unsigned long long g[kMaxRanks];
+  const unsigned long long* src[kMaxRanks];
+#pragma unroll
+  for (int p = 0; p < kMaxRanks; ++p) {  // every peer's granule in flight before the first check
+    src[p] = reinterpret_cast<const unsigned long long*>(xs.base[xs.rank] + off + (long long)p * xs.slot_bytes);
+    g[p] = (p < xs.world && p != xs.rank) ? __hip_atomic_load(src[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                          : (((unsigned long long)ep << 32) | __float_as_uint(mine));
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int p = 0; p < kMaxRanks; ++p) {
+    if (p >= xs.world) continue;
+    const float x = xsite_wait(xs, src[p], g[p], ep, t0, polls, fail);
+    acc = p == 0 ? x : acc + x;
+  }
+  return acc;
+}
+
+// A finisher's slice in LDS: vals[i] (i < n) sits at row position pos(i); replaced by the
+// rank-ordered global sums.  tk: lane 0's ticket; bid: the finisher's index (< nblk);
+// nthr: the workgroup size.  Called by every thread; ends with a barrier.
+template <typename PosF>
+__device__ __forceinline__ void xsite_exchange_slice(const XSite& xs, float* vals, int n, PosF pos,
+                                                     unsigned long long tk, int bid, int nthr) {
+  __shared__ uint32_t ep_s;
+  const int tid = threadIdx.x;
+  if (tid == 0) ep_s = xsite_epoch(xs, tk, bid);
+  __syncthreads();
+  const uint32_t ep = ep_s;
+  for (int i = tid; i < n; i += nthr) xsite_push_at(xs, ep, pos(i), vals[i]);
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  unsigned polls = 0;
+  bool fail = false;
+  for (int i = tid; i < n; i += nthr) vals[i] = xsite_pull_at(xs, ep, pos(i), vals[i], t0, polls, fail);
   __syncthreads();
 }
 

@@ -31,6 +31,7 @@
 // on every rank) to avoid E[x^2] - E[x]^2 cancellation.  Deterministic: every
 // reduction has a fixed order (no float atomics).
 #include "common.h"
+#include "comm/xgmi.h"
 
 namespace dpa {
 namespace bnh {
@@ -199,8 +200,10 @@ __device__ __noinline__ void sum_rows(const float* __restrict__ src, int n, int 
 // Block partial -> part, then the two-level ticket tree of this chunk.  Returns
 // true in the single workgroup per chunk that ends with the chunk's W totals in
 // red[0, W).  part: [Gc*Gr + Gc*NG][W] floats; tickets: [Gc*NG + Gc].
+// xs active (SyncBN): lane 0 of the chunk's finisher takes the site ticket into *tk before
+// the last level's loads (its round trip overlaps them).
 __device__ bool chunk_reduce(float* __restrict__ part, unsigned* __restrict__ tickets, int W, float* red,
-                             float* scr, int* s_flag, int wt) {
+                             float* scr, int* s_flag, int wt, const xgmi::XSite& xs, unsigned long long* tk) {
   const int Gr = gridDim.x, Gc = gridDim.y, y = blockIdx.y;
   const int NG = (Gr + G1 - 1) / G1;
   float* p1 = part + (size_t)y * Gr * W;
@@ -213,15 +216,34 @@ __device__ bool chunk_reduce(float* __restrict__ part, unsigned* __restrict__ ti
   const int gsz = min(G1, Gr - grp * G1);
   if (!ticket_last(tickets + y * NG + grp, gsz, s_flag, wt)) return false;
   if (NG == 1) {
+    if (xs.active() && threadIdx.x == 0) *tk = xgmi::xsite_ticket(xs, y);
     sum_rows(p1, gsz, W, red, scr, wt, 0);
     __syncthreads();
     return true;
   }
   sum_rows(p1 + (size_t)grp * G1 * W, gsz, W, p2 + (size_t)grp * W, scr, wt, wt);
   if (!ticket_last(tickets + Gc * NG + y, NG, s_flag, wt)) return false;
+  if (xs.active() && threadIdx.x == 0) *tk = xgmi::xsite_ticket(xs, y);
   sum_rows(p2, NG, W, red, scr, wt, 0);
   __syncthreads();
   return true;
+}
+__device__ bool chunk_reduce(float* __restrict__ part, unsigned* __restrict__ tickets, int W, float* red,
+                             float* scr, int* s_flag, int wt) {
+  unsigned long long tk;
+  return chunk_reduce(part, tickets, W, red, scr, s_flag, wt, xgmi::XSite{}, &tk);
+}
+
+// SyncBN inside a statistics finisher (chunk y of Gc, the site's nblk = Gc): red = [S1 | S2]
+// of the chunk's CC channels (+ red[2 CC] = the row count in chunk 0 when `count`), local
+// -> global in place (comm/xsite.h positioned form; row positions S1 at c, S2 at C + c,
+// count at 2C).
+__device__ __forceinline__ void chunk_exchange(const xgmi::XSite& xs, float* red, int CC, int C, bool count,
+                                               unsigned long long tk) {
+  const int y = blockIdx.y, cb = y * CC;
+  const int n = 2 * CC + (count && y == 0 ? 1 : 0);
+  xgmi::xsite_exchange_slice(xs, red, n, [&](int i) { return i < CC ? cb + i : i < 2 * CC ? C + cb + i - CC : 2 * C; },
+                             tk, y, THR);
 }
 
 // Combine the RP row-lanes of the block: red[h*CC + c] = sum_ro acc_h (fixed order).
@@ -252,10 +274,10 @@ template <typename T>
 __global__ void __launch_bounds__(THR)
 fwd_stats_kernel(const T* __restrict__ x, long long M, int C, const float* __restrict__ shift,
                  float* __restrict__ part, unsigned* __restrict__ tickets, float* __restrict__ stats,
-                 int64_t* __restrict__ nbt, int wt) {
+                 int64_t* __restrict__ nbt, int wt, xgmi::XSite xs) {
   constexpr int VEC = V16<T>::N;
   __shared__ float scratch[2 * THR * VEC];
-  __shared__ float red[2 * CC_MAX];
+  __shared__ float red[2 * CC_MAX + 1];
   __shared__ int s_flag;
   const Chunk<VEC> g(C);
   float s1[VEC], s2[VEC], sh[VEC];
@@ -292,7 +314,10 @@ fwd_stats_kernel(const T* __restrict__ x, long long M, int C, const float* __res
     }
   }
   block_combine<VEC>(g, s1, s2, red, scratch);
-  if (!chunk_reduce(part, tickets, 2 * g.CC, red, scratch, &s_flag, wt)) return;
+  unsigned long long tk = 0;
+  if (!chunk_reduce(part, tickets, 2 * g.CC, red, scratch, &s_flag, wt, xs, &tk)) return;
+  if (blockIdx.y == 0 && threadIdx.x == 0) red[2 * g.CC] = (float)M;
+  if (xs.active()) chunk_exchange(xs, red, g.CC, C, true, tk);  // SyncBN: global sums and count
   const int cb = (int)blockIdx.y * g.CC;
   for (int t = threadIdx.x; t < g.CC; t += THR) {
     stats[cb + t] = red[t];
@@ -300,7 +325,7 @@ fwd_stats_kernel(const T* __restrict__ x, long long M, int C, const float* __res
     stats[2 * C + SHIFT_OFF + cb + t] = shift[cb + t];
   }
   if (blockIdx.y == 0 && threadIdx.x == 0) {
-    stats[2 * C] = (float)M;
+    stats[2 * C] = red[2 * g.CC];
     if (nbt != nullptr) nbt[0] = nbt[0] + 1;
   }
 }
@@ -524,7 +549,7 @@ __global__ void __launch_bounds__(THR)
 bwd_stats_kernel(const T* __restrict__ dy, const T* __restrict__ y, const T* __restrict__ x, long long M, int C,
                  const float* __restrict__ save, const float* __restrict__ gamma, const float* __restrict__ beta,
                  float* __restrict__ part, unsigned* __restrict__ tickets, float* __restrict__ out,
-                 float* __restrict__ dgamma, float* __restrict__ dbeta, int wt) {
+                 float* __restrict__ dgamma, float* __restrict__ dbeta, int wt, xgmi::XSite xs) {
   constexpr int VEC = V16<T>::N;
   __shared__ float scratch[2 * THR * VEC];
   __shared__ float red[2 * CC_MAX];
@@ -569,11 +594,17 @@ bwd_stats_kernel(const T* __restrict__ dy, const T* __restrict__ y, const T* __r
     }
   }
   block_combine<VEC>(g, s1, s2, red, scratch);
-  if (!chunk_reduce(part, tickets, 2 * g.CC, red, scratch, &s_flag, wt)) return;
+  unsigned long long tk = 0;
+  if (!chunk_reduce(part, tickets, 2 * g.CC, red, scratch, &s_flag, wt, xs, &tk)) return;
   const int cb = (int)blockIdx.y * g.CC;
+  for (int t = threadIdx.x; t < g.CC; t += THR) {  // this rank's sums (DDP averages them)
+    dbeta[cb + t] = red[t];
+    dgamma[cb + t] = red[g.CC + t];
+  }
+  if (xs.active()) chunk_exchange(xs, red, g.CC, C, false, tk);  // SyncBN: out = the global sums
   for (int t = threadIdx.x; t < g.CC; t += THR) {
-    out[cb + t] = dbeta[cb + t] = red[t];
-    out[C + cb + t] = dgamma[cb + t] = red[g.CC + t];
+    out[cb + t] = red[t];
+    out[C + cb + t] = red[g.CC + t];
   }
 }
 
@@ -922,8 +953,17 @@ static void check_workspace(const Grid2& g, int C, const at::Tensor& part, const
 }
 
 // part: >= 2C*(MAXGR + MAXGR/G1) floats; tickets: >= MAXTICKETS zero-initialised int32 (re-armed by the kernels)
+// SyncBN site (xc, the ResNet finishers' wide site): the statistics leave the launch global
+static xgmi::XSite stats_site(const std::shared_ptr<xgmi::XgmiComm>& xc, int64_t C, int Gc) {
+  if (!xc) return xgmi::XSite{};
+  TORCH_CHECK(2 * C + 1 <= xgmi::kWideVals, "bn_nhwc: SyncBN site row holds 2C+1 <= ", xgmi::kWideVals);
+  xgmi::XSite xs = xc->wide_site();
+  xs.nblk = Gc;  // one finisher per channel chunk
+  return xs;
+}
+
 void fwd_stats(at::Tensor x, int64_t C, at::Tensor shift, at::Tensor part, at::Tensor ticket, at::Tensor stats,
-               c10::optional<at::Tensor> nbt) {
+               c10::optional<at::Tensor> nbt, std::shared_ptr<xgmi::XgmiComm> xc) {
   const long long M = x.numel() / C;
   check_rows(x, M, (int)C);
   TORCH_CHECK(stats.numel() >= 3 * C + SHIFT_OFF && shift.numel() == C);
@@ -934,7 +974,7 @@ void fwd_stats(at::Tensor x, int64_t C, at::Tensor shift, at::Tensor part, at::T
     hipLaunchKernelGGL(fwd_stats_kernel<T>, dim3(g.Gr, g.Gc), dim3(THR), 0, cur_stream(), dp<T>(x), M, (int)C,
                        shift.data_ptr<float>(), part.data_ptr<float>(),
                        reinterpret_cast<unsigned*>(ticket.data_ptr<int>()), stats.data_ptr<float>(),
-                       nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr, g_handoff_wt);
+                       nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr, g_handoff_wt, stats_site(xc, C, g.Gc));
   });
   DPA_CHECK_LAUNCH();
 }
@@ -998,7 +1038,7 @@ void apply_resbn(at::Tensor x, at::Tensor res, at::Tensor y, int64_t C, at::Tens
 // act: 0 = no ReLU, 1 = ReLU derivative from y, 2 = recomputed from x (no residual)
 void bwd_stats(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, int64_t C, int64_t act, at::Tensor save,
                at::Tensor gamma, at::Tensor beta, at::Tensor part, at::Tensor ticket, at::Tensor out,
-               at::Tensor dgamma, at::Tensor dbeta) {
+               at::Tensor dgamma, at::Tensor dbeta, std::shared_ptr<xgmi::XgmiComm> xc) {
   const long long M = x.numel() / C;
   check_rows(x, M, (int)C);
   check_rows(dy, M, (int)C);
@@ -1014,7 +1054,7 @@ void bwd_stats(at::Tensor dy, c10::optional<at::Tensor> y, at::Tensor x, int64_t
                          act == ACT_Y ? dp<T>(*y) : nullptr, dp<T>(x), M, (int)C, save.data_ptr<float>(),
                          gamma.data_ptr<float>(), beta.data_ptr<float>(), part.data_ptr<float>(),
                          reinterpret_cast<unsigned*>(ticket.data_ptr<int>()), out.data_ptr<float>(),
-                         dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), g_handoff_wt);
+                         dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), g_handoff_wt, stats_site(xc, C, g.Gc));
     };
     if (act == ACT_Y) go(bwd_stats_kernel<T, ACT_Y>);
     else if (act == ACT_RECOMPUTE) go(bwd_stats_kernel<T, ACT_RECOMPUTE>);
@@ -1133,13 +1173,18 @@ void avgpool_bwd(at::Tensor dy, at::Tensor dx, int64_t HW) {
 
 void register_bn_nhwc(pybind11::module& m) {
   auto s = m.def_submodule("bn_nhwc", "channels-last BatchNorm(+add)(+ReLU), max-pool 3x3/2, global avg-pool");
-  s.def("fwd_stats", &bnh::fwd_stats);
+  s.def("fwd_stats", &bnh::fwd_stats, pybind11::arg("x"), pybind11::arg("C"), pybind11::arg("shift"),
+        pybind11::arg("part"), pybind11::arg("ticket"), pybind11::arg("stats"), pybind11::arg("nbt"),
+        pybind11::arg("xc") = pybind11::none());
   s.def("set_grid_targets", &bnh::set_grid_targets);
   s.def("set_handoff", &bnh::set_handoff);
   s.def("apply", &bnh::apply);
   s.def("apply_resbn", &bnh::apply_resbn);
   s.def("bwd_elemt_rbn", &bnh::bwd_elemt_rbn);
-  s.def("bwd_stats", &bnh::bwd_stats);
+  s.def("bwd_stats", &bnh::bwd_stats, pybind11::arg("dy"), pybind11::arg("y"), pybind11::arg("x"), pybind11::arg("C"),
+        pybind11::arg("act"), pybind11::arg("save"), pybind11::arg("gamma"), pybind11::arg("beta"),
+        pybind11::arg("part"), pybind11::arg("ticket"), pybind11::arg("out"), pybind11::arg("dgamma"),
+        pybind11::arg("dbeta"), pybind11::arg("xc") = pybind11::none());
   s.def("bwd_elemt", &bnh::bwd_elemt);
   s.def("maxpool_fwd", &bnh::maxpool_fwd);
   s.def("maxpool_bwd", &bnh::maxpool_bwd);

@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "common.h"
+#include "comm/xgmi.h"
 
 namespace dpa {
 namespace igemm {
@@ -81,6 +82,10 @@ struct StatArgs {
   float* dgamma = nullptr;
   float* dbeta = nullptr;
   int bwd = 0;
+  // SyncBN: the finishers of the deferred tree (stat_sum1_kernel / stat_tree_kernel) exchange
+  // their slices through this site (comm/xsite.h positioned form) -- the statistics leave
+  // the launch already global, no all-reduce launch follows.  dgamma / dbeta stay local.
+  xgmi::XSite xs;
 };
 
 // BS (conv_glds_kernel): the output is the gradient dy of a BatchNorm's output; the epilogue
@@ -877,9 +882,16 @@ constexpr int S1_THR = 1024, S1_COLS = 64, S1_RG = S1_THR / S1_COLS, S1_MAXROWS 
 template <int BN, int NL>
 __global__ void __launch_bounds__(S1_THR) stat_sum1_kernel(StatArgs sa, long long M, int BM_, int K) {
   __shared__ float part[S1_RG][S1_COLS];
+  __shared__ uint32_t ep_s;
   const int nct = K / BN, bn = blockIdx.x, c0 = blockIdx.y * S1_COLS;
   const int rows = (int)((M + BM_ - 1) / BM_);
   const int col = threadIdx.x % S1_COLS, rg = threadIdx.x / S1_COLS;
+  // SyncBN: every workgroup of this launch finishes 64 columns; its ticket's round trip
+  // overlaps the row loads
+  const bool xon = sa.xs.active();
+  const int xbid = (int)(blockIdx.x + blockIdx.y * gridDim.x);
+  unsigned long long tk = 0;
+  if (xon && threadIdx.x == 0) tk = xgmi::xsite_ticket(sa.xs, xbid);
   const float* lvl1 = sa.part + (long long)bn * rows * (2 * BN) + c0 + col;
   float v[NL];
 #pragma unroll
@@ -892,6 +904,7 @@ __global__ void __launch_bounds__(S1_THR) stat_sum1_kernel(StatArgs sa, long lon
   for (int u = 0; u < NL; ++u)
     if (rg + u * S1_RG < rows) a += v[u];
   part[rg][col] = a;
+  if (xon && threadIdx.x == 0) ep_s = xgmi::xsite_epoch(sa.xs, tk, xbid);
   __syncthreads();
   if (threadIdx.x >= S1_COLS) return;
   float t = 0.f;
@@ -899,15 +912,32 @@ __global__ void __launch_bounds__(S1_THR) stat_sum1_kernel(StatArgs sa, long lon
   for (int g = 0; g < S1_RG; ++g) t += part[g][threadIdx.x];
   const int cc = c0 + threadIdx.x;  // column of [S1 | S2] (or [sum | sumsq])
   const int h = cc / BN, k = bn * BN + cc % BN;
-  if (sa.bwd) {
-    if (h == 0) sa.stats[k] = sa.dbeta[k] = t;
-    else sa.stats[K + k] = sa.dgamma[k] = t;
+  const bool cnt = !sa.bwd && bn == 0 && cc == 0;  // the lane that writes the row count
+  float tg = t, mg = (float)M;
+  if (xon) {  // local -> global (rank-ordered sums; the count too)
+    const uint32_t ep = ep_s;
+    xgmi::xsite_push_at(sa.xs, ep, h * K + k, t);
+    if (cnt) xgmi::xsite_push_at(sa.xs, ep, 2 * K, mg);
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    unsigned polls = 0;
+    bool fail = false;
+    tg = xgmi::xsite_pull_at(sa.xs, ep, h * K + k, t, t0, polls, fail);
+    if (cnt) mg = xgmi::xsite_pull_at(sa.xs, ep, 2 * K, mg, t0, polls, fail);
+  }
+  if (sa.bwd) {  // dbeta / dgamma: this rank's sums (DDP averages them); out: global
+    if (h == 0) {
+      sa.dbeta[k] = t;
+      sa.stats[k] = tg;
+    } else {
+      sa.dgamma[k] = t;
+      sa.stats[K + k] = tg;
+    }
     return;
   }
-  sa.stats[h * K + k] = t;
+  sa.stats[h * K + k] = tg;
   if (h == 0) sa.stats[2 * K + SHIFT_OFF + k] = sa.shift[k];
-  if (bn == 0 && cc == 0) {
-    sa.stats[2 * K] = (float)M;
+  if (cnt) {
+    sa.stats[2 * K] = mg;
     if (sa.nbt != nullptr) sa.nbt[0] = sa.nbt[0] + 1;
   }
   (void)nct;
@@ -916,7 +946,7 @@ __global__ void __launch_bounds__(S1_THR) stat_sum1_kernel(StatArgs sa, long lon
 template <int BN>
 __global__ void __launch_bounds__(THR) stat_tree_kernel(StatArgs sa, long long M, int BM_, int K) {
   __shared__ float scr[THR];
-  __shared__ float tot[2 * BN];
+  __shared__ float tot[2 * BN + 1];  // + the row count (SyncBN exchange)
   __shared__ int s_flag;
   const int nct = K / BN;
   const long long rows = (M + BM_ - 1) / BM_;
@@ -928,13 +958,33 @@ __global__ void __launch_bounds__(THR) stat_tree_kernel(StatArgs sa, long long M
   float* lvl2 = sa.part + (long long)nct * rows * (2 * BN) + (long long)bn * NG * (2 * BN);
   sum_rows<2 * BN>(lvl1 + (long long)grp * G1 * (2 * BN), gsz, lvl2 + (long long)grp * (2 * BN), scr, true);
   if (!last_arriver(sa.tickets + nct * NG + bn, (unsigned)NG, &s_flag)) return;
+  // SyncBN: the nct finishers exchange their slices (ticket round trip behind the level-2 loads)
+  const bool xon = sa.xs.active();
+  unsigned long long tk = 0;
+  if (xon && tid == 0) tk = xgmi::xsite_ticket(sa.xs, bn);
   sum_rows<2 * BN>(lvl2, NG, tot, scr, false);
   if (sa.bwd) {  // BN backward sums: out = [S1 | S2], dbeta = S1, dgamma = S2 (bn_nhwc layout)
     for (int t = tid; t < BN; t += THR) {
-      sa.stats[k0 + t] = sa.dbeta[k0 + t] = tot[t];
-      sa.stats[K + k0 + t] = sa.dgamma[k0 + t] = tot[BN + t];
+      sa.dbeta[k0 + t] = tot[t];  // this rank's (DDP averages them)
+      sa.dgamma[k0 + t] = tot[BN + t];
+    }
+    if (xon) xgmi::xsite_exchange_slice(sa.xs, tot, 2 * BN, [&](int i) { return i < BN ? k0 + i : K + k0 + i - BN; },
+                                        tk, bn, THR);
+    for (int t = tid; t < BN; t += THR) {
+      sa.stats[k0 + t] = tot[t];
+      sa.stats[K + k0 + t] = tot[BN + t];
     }
     return;
+  }
+  __shared__ float cnt[1];
+  if (tid == 0) cnt[0] = (float)M;
+  if (xon) {
+    // the row count rides with finisher 0's slice (position 2K)
+    const int n = 2 * BN + (bn == 0 ? 1 : 0);
+    if (bn == 0 && tid == 0) tot[2 * BN] = cnt[0];
+    xgmi::xsite_exchange_slice(sa.xs, tot, n, [&](int i) { return i < BN ? k0 + i : i < 2 * BN ? K + k0 + i - BN : 2 * K; },
+                               tk, bn, THR);
+    if (bn == 0 && tid == 0) cnt[0] = tot[2 * BN];
   }
   for (int t = tid; t < BN; t += THR) {
     sa.stats[k0 + t] = tot[t];
@@ -942,7 +992,7 @@ __global__ void __launch_bounds__(THR) stat_tree_kernel(StatArgs sa, long long M
     sa.stats[2 * K + SHIFT_OFF + k0 + t] = sa.shift[k0 + t];
   }
   if (bn == 0 && tid == 0) {
-    sa.stats[2 * K] = (float)M;
+    sa.stats[2 * K] = cnt[0];
     if (sa.nbt != nullptr) sa.nbt[0] = sa.nbt[0] + 1;
   }
 }
@@ -1506,10 +1556,11 @@ int64_t stat_defer_config(int64_t min_blocks) {
   return prev;
 }
 
-static void launch_stat_tree(const StatArgs& sa, long long M, int bm, int K, int BN) {
+static void launch_stat_tree(StatArgs sa, long long M, int bm, int K, int BN) {
   const long long rows = (M + bm - 1) / bm, NG = (rows + G1 - 1) / G1;
   if (rows <= S1_MAXROWS) {  // one level: every row in flight at once, no ticket
     const dim3 gr((unsigned)(K / BN), (unsigned)(2 * BN / S1_COLS)), th(S1_THR);
+    sa.xs.nblk = (int)(gr.x * gr.y);  // SyncBN finishers: every workgroup
     if (rows <= 16 * S1_RG) {
       if (BN == 128) hipLaunchKernelGGL((stat_sum1_kernel<128, 16>), gr, th, 0, cur_stream(), sa, M, bm, K);
       else hipLaunchKernelGGL((stat_sum1_kernel<64, 16>), gr, th, 0, cur_stream(), sa, M, bm, K);
@@ -1521,6 +1572,7 @@ static void launch_stat_tree(const StatArgs& sa, long long M, int bm, int K, int
     return;
   }
   const dim3 gr((unsigned)(NG * (K / BN))), th(THR);
+  sa.xs.nblk = K / BN;  // SyncBN finishers: the last arriver of each channel tile
   if (BN == 128) hipLaunchKernelGGL(stat_tree_kernel<128>, gr, th, 0, cur_stream(), sa, M, bm, K);
   else hipLaunchKernelGGL(stat_tree_kernel<64>, gr, th, 0, cur_stream(), sa, M, bm, K);
   DPA_CHECK_LAUNCH();
@@ -1568,7 +1620,7 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
               c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_y, c10::optional<at::Tensor> bn_save,
               c10::optional<at::Tensor> bn_gamma, c10::optional<at::Tensor> bn_beta,
               c10::optional<at::Tensor> bn_out, c10::optional<at::Tensor> bn_dgamma,
-              c10::optional<at::Tensor> bn_dbeta) {
+              c10::optional<at::Tensor> bn_dbeta, std::shared_ptr<xgmi::XgmiComm> xc) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && y.is_cuda(), "conv_fwd: device tensors");
   TORCH_CHECK(x.scalar_type() == w.scalar_type() && x.scalar_type() == y.scalar_type(), "conv_fwd: one dtype");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "conv_fwd: bf16 / f16");
@@ -1652,6 +1704,12 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
     sa.shift = shift->data_ptr<float>();
     sa.nbt = nbt.has_value() ? nbt->data_ptr<int64_t>() : nullptr;
   }
+  // SyncBN inside the statistics finishers: they run in the deferred tree launch
+  if (xc) {
+    TORCH_CHECK(st || bwdst, "conv_fwd: xc (SyncBN site) goes with statistics");
+    TORCH_CHECK(2 * g.K + 1 <= xgmi::kWideVals, "conv_fwd: SyncBN site row holds 2K+1 <= ", xgmi::kWideVals);
+    sa.xs = xc->wide_site();
+  }
   const int BN0 = tile_n(g.K);
   if (mode == MODE_GEN && g1x1_enabled() && x.numel() < (1LL << 31) && w.numel() < (1LL << 31) &&
       (g3x3_enabled() || (g.R == 1 && g.S == 1 && g.pad == 0))) {
@@ -1661,7 +1719,7 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
     const int BN = BN0 == 128 && BP == 128 && (g.M + 127) / 128 * (g.K / 128) < bn64_below() ? 64 : BN0;
     const long long blocks = (g.M + BP - 1) / BP * (g.K / BN);
     TORCH_CHECK(blocks < (1LL << 31), "conv_fwd: grid too large");
-    sa.defer = st && defer_stats(blocks) ? 1 : 0;
+    sa.defer = st && (defer_stats(blocks) || xc) ? 1 : 0;
     if (bwdst) {  // the BN backward sums: level-1 rows in the conv, the tree after it
       sa.part = part->data_ptr<float>();
       sa.tickets = reinterpret_cast<unsigned*>(tickets->data_ptr<int>());
@@ -1725,7 +1783,7 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
   const long long rows = (g.M + BM - 1) / BM;
   const long long blocks = rows * (g.K / BN) * (mode == MODE_S2T ? 4 : 1);
   TORCH_CHECK(blocks < (1LL << 31), "conv_fwd: grid too large");
-  sa.defer = st && defer_stats(blocks) ? 1 : 0;
+  sa.defer = st && (defer_stats(blocks) || xc) ? 1 : 0;
   auto launch = [&](auto tag) {
     using T = decltype(tag);
     const T* xp = reinterpret_cast<const T*>(x.data_ptr());
@@ -1860,7 +1918,8 @@ void register_conv_igemm(pybind11::module& m) {
         pybind11::arg("bn_x") = pybind11::none(), pybind11::arg("bn_y") = pybind11::none(),
         pybind11::arg("bn_save") = pybind11::none(), pybind11::arg("bn_gamma") = pybind11::none(),
         pybind11::arg("bn_beta") = pybind11::none(), pybind11::arg("bn_out") = pybind11::none(),
-        pybind11::arg("bn_dgamma") = pybind11::none(), pybind11::arg("bn_dbeta") = pybind11::none());
+        pybind11::arg("bn_dgamma") = pybind11::none(), pybind11::arg("bn_dbeta") = pybind11::none(),
+        pybind11::arg("xc") = pybind11::none());
   s.def("supported", &igemm::supported);
   s.def("stat_part_len", &igemm::stat_part_len);
   s.def("stat_tickets_len", &igemm::stat_tickets_len);

@@ -74,13 +74,9 @@ def _conv(x: torch.Tensor, conv: nn.Conv2d, cdtype: torch.dtype, bn: nn.Module |
 
 
 def _comm_of(bn: nn.Module):
-    if not bn.training:
-        return None
-    if isinstance(bn, nn.SyncBatchNorm):
-        from ..parallel.comm import default_comm
+    from ..ops.bn_nhwc import bn_comm  # the same lookup the statistics-producing convs use
 
-        return default_comm()
-    return getattr(bn, "comm", None)
+    return bn_comm(bn)
 
 
 class Bottleneck(nn.Module):

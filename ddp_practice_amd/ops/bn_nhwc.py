@@ -8,7 +8,10 @@ torch semantics (batch stats, biased var for normalisation, unbiased var into
 running_var, momentum / cumulative average) and SyncBatchNorm semantics when a
 communicator is active: ONE all-reduce of [sum, sum_sq, count] (2C+1 floats)
 forward and of [sum dz, sum dz*xhat] (2C) backward, d(gamma) / d(beta) from the
-local sums (torch/nn/modules/_functions.py:10-205).
+local sums (torch/nn/modules/_functions.py:10-205).  With the communicator's xGMI
+engine up (:func:`sync_site`) that all-reduce runs INSIDE the kernel that finishes the
+statistics (the last arriver of each channel slice exchanges its slice with the peers,
+csrc/comm/xsite.h positioned form): no collective launch between producer and consumer.
 """
 from __future__ import annotations
 
@@ -43,6 +46,37 @@ class _Workspace:
         return ws
 
 
+def bn_comm(bn):
+    """The communicator a training BatchNorm module synchronises over (None: local BN)."""
+    if not bn.training:
+        return None
+    if isinstance(bn, torch.nn.SyncBatchNorm):
+        from ..parallel.comm import default_comm
+
+        return default_comm()
+    return getattr(bn, "comm", None)
+
+
+def sync_site(comm):
+    """The xGMI engine whose wide site (csrc/comm/xsite.h kSiteWide) the statistics
+    finishers exchange SyncBN sums through, or None: an all-reduce launch follows each
+    statistics launch.  Producer (ops/conv_igemm.conv_fwd, dgrad_bn) and consumer (the BN
+    functions here) both decide with this function on the same communicator.
+
+    Only the finisher workgroups of a launch wait for the peers (at most a few dozen), so
+    there is no residency condition; ranks sharing one GPU beyond two take the launch path
+    unless DPA_FUSED_SYNC=1 (as ops/convnet_fused._fused_site_engine); DPA_FUSED_SYNC=0
+    forces the launch path (A/B)."""
+    if comm is None or not comm.active:
+        return None
+    flag = os.environ.get("DPA_FUSED_SYNC")
+    if flag == "0":
+        return None
+    if flag != "1" and os.environ.get("DPA_SHARED_GPU") == "1" and getattr(comm, "world_size", 1) > 2:
+        return None
+    return getattr(comm, "xgmi", None)
+
+
 def _cl(t: torch.Tensor) -> torch.Tensor:
     return t if t.is_contiguous(memory_format=_CL) else t.contiguous(memory_format=_CL)
 
@@ -63,7 +97,7 @@ class BNTap:
     second consumer's gradient in place, which keeps the pointer but bumps the version).
     """
 
-    __slots__ = ("_node", "_ix", "_iy", "act", "save", "weight", "bias", "sums", "grad_ptr", "grad_ver")
+    __slots__ = ("_node", "_ix", "_iy", "act", "save", "weight", "bias", "sums", "grad_ptr", "grad_ver", "xc")
 
     def __init__(self):
         self._node = None
@@ -72,22 +106,25 @@ class BNTap:
         self.act = 0
         self.grad_ptr = 0
         self.grad_ver = -1
+        self.xc = None  # the BN's SyncBN site engine (sync_site): the conv's sums leave global
 
-    def bind(self, ctx, ix: int, iy: int, act: int, save, weight, bias) -> None:
+    def bind(self, ctx, ix: int, iy: int, act: int, save, weight, bias, xc=None) -> None:
         """``ctx``: the BN's autograd node; ``ix`` / ``iy``: positions of x / y in its saved
-        tensors (``iy`` -1: y not needed)."""
+        tensors (``iy`` -1: y not needed); ``xc``: the BN's :func:`sync_site`."""
         self._node = weakref.ref(ctx)
         self._ix, self._iy = ix, iy
         self.act, self.save, self.weight, self.bias = act, save, weight, bias
         self.sums = None
+        self.xc = xc
 
-    def bind_tensors(self, x, y, act: int, save, weight, bias) -> None:
+    def bind_tensors(self, x, y, act: int, save, weight, bias, xc=None) -> None:
         """Direct binding (kernel tests, no autograd node): holds x / y strongly."""
         held = type("_Held", (), {"saved_tensors": (x, y)})()
         self._node = lambda: held
         self._ix, self._iy = 0, (1 if y is not None else -1)
         self.act, self.save, self.weight, self.bias = act, save, weight, bias
         self.sums = None
+        self.xc = xc
 
     def _saved(self, i: int):
         node = self._node() if self._node is not None else None
@@ -109,7 +146,7 @@ class BNTap:
 
     def clear(self):
         self._node = None
-        self.save = self.weight = self.bias = self.sums = None
+        self.save = self.weight = self.bias = self.sums = self.xc = None
 
 
 class BNActFn(torch.autograd.Function):
@@ -125,14 +162,15 @@ class BNActFn(torch.autograd.Function):
         mom = -1.0 if momentum is None else float(momentum)
         f32 = dict(dtype=torch.float32, device=dev)
         if training:
+            sync = comm is not None and comm.active
+            xc = sync_site(comm)  # SyncBN inside the statistics finishers (also the producing conv's)
             if pre is not None:  # computed in the producing conv's epilogue (ops/conv_igemm.py)
                 stats = pre
             else:
                 part, ticket = _Workspace.get(dev, C)
                 stats = torch.empty(3 * C + 4, **f32)
-                K.fwd_stats(x, C, running_mean, part, ticket, stats, nbt)
-            sync = comm is not None and comm.active
-            if sync:
+                K.fwd_stats(x, C, running_mean, part, ticket, stats, nbt, xc=xc)
+            if sync and xc is None:
                 comm.all_reduce_(stats.narrow(0, 0, 2 * C + 1))
             save = torch.empty(2 * C, **f32)
             K.apply(x, resc, y, C, stats, weight, bias, running_mean, running_var, nbt, mom, float(eps), True,
@@ -140,11 +178,11 @@ class BNActFn(torch.autograd.Function):
             # ReLU derivative: from y after a residual add, else recomputed from x (y not kept)
             ctx.act = (1 if res is not None else 2) if relu else 0
             ctx.save_for_backward(x, y if ctx.act == 1 else None, weight, bias, save, stats)
-            ctx.sync, ctx.comm, ctx.has_res = sync, comm, res is not None
+            ctx.sync, ctx.comm, ctx.xc, ctx.has_res = sync, comm, xc, res is not None
             ctx.tap = tap if res is not None else None
             ctx.btap = btap if ctx.act in (1, 2) else None
             if ctx.btap is not None:
-                ctx.btap.bind(ctx, 0, 1 if ctx.act == 1 else -1, ctx.act, save, weight, bias)
+                ctx.btap.bind(ctx, 0, 1 if ctx.act == 1 else -1, ctx.act, save, weight, bias, xc)
         else:
             dummy = torch.empty(2 * C + 1, **f32)
             K.apply(x, resc, y, C, dummy, weight, bias, running_mean, running_var, nbt, mom, float(eps), False,
@@ -169,11 +207,12 @@ class BNActFn(torch.autograd.Function):
             out = torch.empty(2 * C, **f32)
             dgamma = torch.empty(C, **f32)
             dbeta = torch.empty(C, **f32)
-            K.bwd_stats(dy, y, x, C, ctx.act, save, weight, bias, part, ticket, out, dgamma, dbeta)
+            K.bwd_stats(dy, y, x, C, ctx.act, save, weight, bias, part, ticket, out, dgamma, dbeta, xc=ctx.xc)
         if bt is not None:
             bt.clear()
             ctx.btap = None
-        sums = ctx.comm.all_reduce(out) if ctx.sync else out
+        # out is already global when the finishers exchanged it (ctx.xc)
+        sums = ctx.comm.all_reduce(out) if (ctx.sync and ctx.xc is None) else out
         dx = torch.empty_like(x, memory_format=_CL)
         dres = torch.empty_like(x, memory_format=_CL) if ctx.has_res else None
         K.bwd_elemt(dy, y, x, C, ctx.act, save, sums, stats, weight, bias, dx, dres)
@@ -215,17 +254,19 @@ class BNResBNFn(torch.autograd.Function):
         y = torch.empty_like(x, memory_format=_CL)
         training = bn.training
         stats = rstats = None
+        xc = None
         if training:
             stats, rstats = pre, rpre
+            sync = comm is not None and comm.active
+            xc = sync_site(comm)
             part, ticket = _Workspace.get(dev, C)
             if stats is None:
                 stats = torch.empty(3 * C + 4, **f32)
-                K.fwd_stats(x, C, bn.running_mean, part, ticket, stats, bn.num_batches_tracked)
+                K.fwd_stats(x, C, bn.running_mean, part, ticket, stats, bn.num_batches_tracked, xc=xc)
             if rstats is None:
                 rstats = torch.empty(3 * C + 4, **f32)
-                K.fwd_stats(r, C, rbn.running_mean, part, ticket, rstats, rbn.num_batches_tracked)
-            sync = comm is not None and comm.active
-            if sync:
+                K.fwd_stats(r, C, rbn.running_mean, part, ticket, rstats, rbn.num_batches_tracked, xc=xc)
+            if sync and xc is None:
                 comm.all_reduce_(stats.narrow(0, 0, 2 * C + 1))
                 comm.all_reduce_(rstats.narrow(0, 0, 2 * C + 1))
         else:
@@ -240,10 +281,10 @@ class BNResBNFn(torch.autograd.Function):
         ctx.training = training
         if training:
             ctx.save_for_backward(x, y, weight, bias, save, stats, r, rweight, rbias, rsave, rstats)
-            ctx.sync, ctx.comm = sync, comm
+            ctx.sync, ctx.comm, ctx.xc = sync, comm, xc
             ctx.btap = btap
             if btap is not None:
-                btap.bind(ctx, 0, 1, 1, save, weight, bias)
+                btap.bind(ctx, 0, 1, 1, save, weight, bias, xc)
         return y
 
     @staticmethod
@@ -261,11 +302,11 @@ class BNResBNFn(torch.autograd.Function):
             out, dgamma, dbeta = bt.sums
         else:
             out, dgamma, dbeta = torch.empty(2 * C, **f32), torch.empty(C, **f32), torch.empty(C, **f32)
-            K.bwd_stats(dy, y, x, C, 1, save, weight, bias, part, ticket, out, dgamma, dbeta)
+            K.bwd_stats(dy, y, x, C, 1, save, weight, bias, part, ticket, out, dgamma, dbeta, xc=ctx.xc)
         if bt is not None:
             bt.clear()
             ctx.btap = None
-        sums = ctx.comm.all_reduce(out) if ctx.sync else out
+        sums = ctx.comm.all_reduce(out) if (ctx.sync and ctx.xc is None) else out
         dx = torch.empty_like(x, memory_format=_CL)
         dz = torch.empty_like(x, memory_format=_CL)
         # bn's elementwise backward, which also takes the downsample BN's sums of dz
@@ -275,9 +316,9 @@ class BNResBNFn(torch.autograd.Function):
                             rdgamma, rdbeta)
         else:  # A/B: the elementwise pass, then the downsample BN's own statistics pass
             K.bwd_elemt(dy, y, x, C, 1, save, sums, stats, weight, bias, dx, dz)
-            K.bwd_stats(dz, None, r, C, 0, rsave, rweight, rbias, part, ticket, rout, rdgamma, rdbeta)
-        # the downsample BN (no ReLU) on dz
-        rsums = ctx.comm.all_reduce(rout) if ctx.sync else rout
+            K.bwd_stats(dz, None, r, C, 0, rsave, rweight, rbias, part, ticket, rout, rdgamma, rdbeta, xc=ctx.xc)
+        # the downsample BN (no ReLU) on dz (rout global when bwd_stats exchanged it)
+        rsums = ctx.comm.all_reduce(rout) if (ctx.sync and (ctx.xc is None or _FUSE_RBN_SUMS)) else rout
         dr = torch.empty_like(r, memory_format=_CL)
         K.bwd_elemt(dz, None, r, C, 0, rsave, rsums, rstats, rweight, rbias, dr, None)
         return dx, dgamma, dbeta, dr, rdgamma, rdbeta, None, None, None, None, None, None

@@ -15,6 +15,7 @@ import os
 import torch
 
 from .._ext import load as _load_ext
+from .bn_nhwc import bn_comm, sync_site
 
 _CL = torch.channels_last
 ENABLED = os.environ.get("DPA_IGEMM", "1") != "0"  # 0: MIOpen / hipBLASLt forward + separate stats (A/B)
@@ -82,8 +83,10 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, bn=None, a
         return y, None
     part, tickets = _StatWS.get(x.device, N * OH * OW, K)
     stats = torch.empty(3 * K + 4, dtype=torch.float32, device=x.device)
+    # SyncBN: the statistics finishers exchange with the peers (the BN then skips its all-reduce)
+    xc = sync_site(bn_comm(bn))
     _K().conv_fwd(x, w, y, stride, pad, part, tickets, stats, bn.running_mean, bn.num_batches_tracked, mode=mode,
-                  aux=aux)
+                  aux=aux, xc=xc)
     return y, stats
 
 
@@ -118,7 +121,7 @@ def dgrad_bn(dy: torch.Tensor, wt: torch.Tensor, bt, acc: torch.Tensor | None = 
     dx = acc if acc is not None else torch.empty(shape, dtype=dy.dtype, device=dy.device, memory_format=_CL)
     _K().conv_fwd(dy, wt, dx, 1, pad, part, tickets, accumulate=acc is not None, bn_x=bx,
                   bn_y=bt.y if bt.act == 1 else None, bn_save=bt.save, bn_gamma=bt.weight, bn_beta=bt.bias,
-                  bn_out=out, bn_dgamma=dgamma, bn_dbeta=dbeta)
+                  bn_out=out, bn_dgamma=dgamma, bn_dbeta=dbeta, xc=bt.xc)
     bt.sums = (out, dgamma, dbeta)
     bt.grad_ptr = dx.data_ptr()
     bt.grad_ver = dx._version

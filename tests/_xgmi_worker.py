@@ -88,6 +88,51 @@ def worker(rank, world, port, mode, q):
             x.close()
             q.put((rank, "ok", out))
             return
+        if mode == "wide":
+            # the ResNet statistics finishers' positioned exchange (csrc/comm/xsite.h, wide
+            # site): rows up to 2*2048+1 floats split over 1..64 finisher workgroups, the
+            # finisher count changing launch to launch (ticket lanes, idle-lane bumps), then
+            # graph-replayed; rank-ordered sums bit-identical on every rank
+            out = {}
+            cases = [(4097, 16), (4097, 1), (129, 3), (2049, 64), (1, 1), (513, 8), (4097, 9), (300, 7)]
+            for it in range(24):
+                n, nb = cases[it % len(cases)]
+                t = _data(rank, n, torch.float32, it).to(dev)
+                o = torch.full((n,), float("nan"), device=dev)
+                x.wide_probe(t, o, nb)
+                torch.cuda.synchronize()
+                assert x.error() == 0, x.error_string()
+                _check(o, _expect(world, n, torch.float32, it, "sum"), torch.float32, ("wide", it, n, nb))
+                out[f"wide{it}"] = o.cpu().numpy().tobytes()
+            t = torch.zeros(4097, device=dev)
+            o = torch.empty(4097, device=dev)
+            t2 = torch.zeros(257, device=dev)
+            o2 = torch.empty(257, device=dev)
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                x.wide_probe(t, o, 32)
+                x.wide_probe(t2, o2, 2)
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                x.wide_probe(t, o, 32)
+                x.wide_probe(t2, o2, 2)
+            for r in range(8):
+                t.copy_(_data(rank, 4097, torch.float32, 200 + r).to(dev))
+                t2.copy_(_data(rank, 257, torch.float32, 300 + r).to(dev))
+                g.replay()
+                torch.cuda.synchronize()
+                assert x.error() == 0, x.error_string()
+                _check(o, _expect(world, 4097, torch.float32, 200 + r, "sum"), torch.float32, ("wide graph", r))
+                _check(o2, _expect(world, 257, torch.float32, 300 + r, "sum"), torch.float32, ("wide graph 2", r))
+                out[f"wg{r}"] = o.cpu().numpy().tobytes()
+            store.set(f"done{rank}", "1")
+            store.wait([f"done{r}" for r in range(world)])
+            x.close()
+            q.put((rank, "ok", out))
+            return
         if mode == "twoshot":
             x.set_twoshot_blocks(48)  # all ranks' grids resident together on the one shared GPU
             # reduce-scatter + all-gather engine: 1 / 8 / 32 MiB, ragged sizes, every dtype

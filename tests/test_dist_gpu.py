@@ -121,3 +121,79 @@ def test_xgmi_engine_passes_its_selftest_at_forced_world1(rccl):
     probed a SyncBN site with 1568 floats > its 128-float row and failed on every box)."""
     assert rccl.xgmi_status.startswith("on"), rccl.xgmi_status
     assert rccl.xgmi is not None and rccl.xgmi_max_bytes > 0
+
+
+@pytest.mark.parametrize("amp", [None, torch.bfloat16])
+def test_resnet_syncbn_sites_match_launch_path(rccl, monkeypatch, amp):
+    """ResNet-50 SyncBN with the statistics exchanged inside the finisher workgroups (the
+    xGMI engine's wide site, ops/bn_nhwc.sync_site) == the all-reduce-launch path
+    (DPA_FUSED_SYNC=0).  At W=1 both reduce to the local sums, so the output, every
+    gradient and every buffer must be bitwise equal -- and the site path must launch no
+    all-reduce kernel for the statistics."""
+    import torch.nn.functional as F
+
+    from ddp_practice_amd.models import resnet50
+    from ddp_practice_amd.ops.bn_nhwc import sync_site
+    from ddp_practice_amd.parallel import convert_sync_batchnorm
+
+    assert sync_site(rccl) is not None
+    torch.manual_seed(0)
+    base = convert_sync_batchnorm(resnet50(num_classes=10, amp_dtype=amp)).cuda()
+    x = torch.rand(8, 3, 64, 64, device="cuda")
+    y = torch.randint(0, 10, (8,), device="cuda")
+    res = {}
+    calls = {}
+    # a warm-up pass first: library convolutions (the fp32 model's) pick their algorithms on
+    # the first call of a shape, which must not land on one of the two compared runs
+    for flag in ("w", "0", "1"):
+        monkeypatch.setenv("DPA_FUSED_SYNC", "0" if flag == "w" else flag)
+        m = copy.deepcopy(base)
+        n = [0]
+        orig = type(rccl).all_reduce_, type(rccl).all_reduce
+
+        def count_(self, t, op="sum", _f=orig[0]):
+            n[0] += 1
+            return _f(self, t, op)
+
+        def count(self, t, op="sum", _f=orig[1]):
+            n[0] += 1
+            return _f(self, t, op)
+
+        monkeypatch.setattr(type(rccl), "all_reduce_", count_)
+        monkeypatch.setattr(type(rccl), "all_reduce", count)
+        out = m(x)
+        F.cross_entropy(out.float(), y).backward()
+        torch.cuda.synchronize()
+        monkeypatch.setattr(type(rccl), "all_reduce_", orig[0])
+        monkeypatch.setattr(type(rccl), "all_reduce", orig[1])
+        calls[flag] = n[0]
+        res[flag] = (out.detach().clone(), {k: p.grad.clone() for k, p in m.named_parameters()},
+                     {k: b.clone() for k, b in m.named_buffers()})
+    assert rccl.xgmi.error() == 0, rccl.xgmi.error_string()
+    assert calls["0"] >= 2 * 53 and calls["1"] == 0, calls  # 53 BatchNorms, fwd + bwd each
+    (o0, g0, b0), (o1, g1, b1), (ow, gw, _) = res["0"], res["1"], res["w"]
+
+    def rel(a, b):
+        return ((a.double() - b.double()).norm() / (b.double().norm() + 1e-30)).item()
+
+    # bf16: every kernel of the step is the framework's own (deterministic): bitwise.  fp32:
+    # the library convolutions vary run to run (~1e-5): within a few times that spread
+    bitwise = amp is not None
+    if bitwise:
+        assert torch.equal(ow, o0), ("launch path run to run", rel(ow, o0))
+    floor = 0.0 if bitwise else 10 * max(rel(ow, o0), max(rel(gw[k], g0[k]) for k in g0), 1e-6)
+
+    def same(a, b, what):
+        if bitwise:
+            assert torch.equal(a, b), (what, rel(a, b))
+        else:
+            assert rel(a, b) <= floor, (what, rel(a, b), floor)
+
+    same(o1, o0, "output")
+    for k in g0:
+        same(g1[k], g0[k], k)
+    for k in b0:
+        if b0[k].dtype.is_floating_point:
+            same(b1[k], b0[k], k)
+        else:
+            assert torch.equal(b0[k], b1[k]), k

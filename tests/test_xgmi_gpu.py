@@ -35,6 +35,16 @@ def test_xsite_exchange_multiprocess(C, world):
             assert v == outs[r][k], f"rank {r} differs from rank 0 on {k}"
 
 
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_wide_site_exchange_multiprocess(C, world):
+    """The positioned exchange of the ResNet statistics finishers (SyncBN rows up to
+    2*2048+1 floats over several finisher workgroups, csrc/comm/xsite.h kSiteWide)."""
+    outs = _run(world, "wide")
+    for k, v in outs[0].items():
+        for r in range(1, world):
+            assert v == outs[r][k], f"rank {r} differs from rank 0 on {k}"
+
+
 @pytest.mark.parametrize("mode", ["site_timeout", "sgd_timeout"])
 def test_in_kernel_exchange_wait_is_bounded(C, mode):
     """A fused SyncBN site and the fused AMP-SGD gradient exchange whose peer never
