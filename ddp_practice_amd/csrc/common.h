@@ -117,6 +117,42 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// Lane-group sums without an LDS round trip.  __shfl_xor compiles to ds_bpermute_b32, each
+// step an LDS round trip waited with lgkmcnt(0): the ConvNet head's ten 64-lane reductions
+// were 60 serialized round trips (~3.5 us, head_row_kernel ISA).  Here: DPP lane moves inside
+// 16-lane rows (quad butterflies, half-row and row mirrors) and gfx950's v_permlane16_swap /
+// v_permlane32_swap across rows -- all VALU.  group_sum<G>: every lane gets the sum over its
+// aligned group of G lanes, in a fixed association (deterministic, the same in every lane of
+// the group).  Needs all lanes of the group active (a DPP read of an inactive lane sees a
+// stale register).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+// v[l] + v[l ^ 16] (low row first) in every lane
+__device__ __forceinline__ float xor16_sum(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+// v[l] + v[l ^ 32] (low half first) in every lane
+__device__ __forceinline__ float xor32_sum(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+  static_assert(G == 2 || G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "lane group of 2..64");
+  v += dpp_mov<0xB1>(v);                       // quad_perm [1,0,3,2]: pairs
+  if constexpr (G >= 4) v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]: quads
+  if constexpr (G >= 8) v += dpp_mov<0x141>(v);  // row_half_mirror: the other quad of the 8
+  if constexpr (G >= 16) v += dpp_mov<0x140>(v); // row_mirror: the other 8 of the row
+  if constexpr (G >= 32) v = xor16_sum(v);
+  if constexpr (G >= 64) v = xor32_sum(v);
+  return v;
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) { return group_sum<64>(v); }
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

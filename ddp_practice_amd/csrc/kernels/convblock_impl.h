@@ -1019,11 +1019,8 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
   if constexpr (MODE == 0 || EPI == 1) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      float a1 = s1[nt], a2 = s2[nt];
-      a1 += __shfl_xor(a1, 16, 64);
-      a1 += __shfl_xor(a1, 32, 64);
-      a2 += __shfl_xor(a2, 16, 64);
-      a2 += __shfl_xor(a2, 32, 64);
+      // lanes r, r+16, r+32, r+48 (VALU permlane swaps, no LDS round trip; every lane active)
+      const float a1 = xor32_sum(xor16_sum(s1[nt])), a2 = xor32_sum(xor16_sum(s2[nt]));
       if (q == 0) {  // per-wave partials, summed below in a fixed order (deterministic)
         lstat[wv * 2 * COUT + nt * 16 + r] = a1;
         lstat[wv * 2 * COUT + COUT + nt * 16 + r] = a2;
@@ -1460,8 +1457,7 @@ conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __r
 #pragma unroll
       for (int j = 0; j < 8; ++j) a += Cvt<T>::to_f(e[j]);
     }
-#pragma unroll
-    for (int o = TPC / 2; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    a = group_sum<TPC>(a);  // VALU lane moves (every lane active here)
     if (sub == 0) put(&row_out[COUT * N + co], a);
   }
   DPA_STAMP(6);

@@ -31,6 +31,8 @@
 // Round 3's channel-per-workgroup head (32 workgroups, partial logits handed to a
 // last arriver and back: two cross-workgroup round trips on every workgroup's
 // path) took 15.5 us of the 57.7 us step (profiles/r3_head_granule_vs_ticket_ab.txt).
+#include <cstdlib>
+
 #include "comm/xgmi.h"
 #include "convblock_impl.h"
 
@@ -41,11 +43,14 @@ using cb::BNParams;
 using cb::IDX_RELU;
 using cb::Pair2;
 
-constexpr int NT = 256;    // 4 waves
+// workgroup size (template parameter NT of head_row_kernel): 256 lanes, or 1024 with
+// DPA_HEAD_NT=1024 (16 waves, 4 per SIMD).  Same-box A/B with the DPP lane sums: 0.0520 /
+// 0.0519 vs 0.0519 / 0.0523 ms per step (profiles/r4n_head_dpp_nt_ab.txt): the BN-pool / GEMV
+// phase was the ds_bpermute chain, not lane count
+constexpr int NT_MAX = 1024;
 constexpr int C = 32, H = 14, W = 14, HO = 7, WO = 7, PP = 49, K = C * PP;
 constexpr int BMAX = 64;   // images (one ballot counts the batch's rows)
 constexpr int NMAX = 16;   // classes
-constexpr int IT = (K + NT - 1) / NT;  // pooled features per lane (7)
 
 // loss word (state[0], zero-initialised once; the completing workgroup re-arms it):
 // [63:57] arrivals | [56:50] rows whose loss is out of range | [49:0] sum over the
@@ -77,22 +82,21 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
-template <int G>
-__device__ __forceinline__ float gsum(float v) {
-#pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
 
-template <typename T, int NM>  // NM: classes the register tiles are sized for (>= N)
+// NM: classes the register tiles are sized for (>= N); NT: workgroup size (256 | 1024)
+template <typename T, int NM, int NT>
 __global__ void __launch_bounds__(NT)
 head_row_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__ wfc, const float* __restrict__ bfc,
                 T* __restrict__ logits, T* __restrict__ p_out, uint8_t* __restrict__ idx_out,
                 T* __restrict__ xh_out, int B, int N, HeadRow hr) {
   typedef typename Pair2<T>::type P;
+  constexpr int IT = (K + NT - 1) / NT;  // pooled features per lane (7 | 2)
+  constexpr int NW = NT / 64;
+  constexpr int CL = NT / C;             // lanes per channel in the BN2 backward sums (8 | 32)
   __shared__ float sc_s[C], beta_s[C], mean_s[C], istd_s[C];
   __shared__ float part_s[NT];
-  __shared__ float red[NT / 64][NM];
+  __shared__ float red[NW][NM];
+  __shared__ float lgs[NM];
   __shared__ float gs[2][IT * NT];  // per pooled feature: g, g * xhat (BN2 backward sums)
 
   const int tid = threadIdx.x, b = blockIdx.x;
@@ -162,10 +166,21 @@ head_row_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__ 
     float a = 0.f;
 #pragma unroll
     for (int i = 0; i < IT; ++i) a += pf[i] * wq[n][i];
-    a = wave_sum(a);
+    a = wave_sum_dpp(a);  // every lane active here (full-wave DPP)
     if (lane == 0) red[wv][n] = a;
   }
   lds_barrier();
+  if (NW > 4) {  // 16 wave partials: one lane per class adds them (fixed order), then broadcast
+    if (tid < NM) {
+      float t = 0.f;
+#pragma unroll
+      for (int n = 0; n < NM; ++n) t = tid == n ? bias[n] : t;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) t += red[w][tid];
+      lgs[tid] = t;
+    }
+    lds_barrier();
+  }
   DPA_STAMP(3);
   // 4. cross entropy of this row, computed by every lane (identical arithmetic): the
   //    same formula and rounding as head.hip ce_fwd_kernel
@@ -173,9 +188,14 @@ head_row_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__ 
   float mx = -INFINITY, sx = 0.f, xt = 0.f;
 #pragma unroll
   for (int n = 0; n < NM; ++n) {
-    float t = bias[n];
+    float t;
+    if (NW > 4) {
+      t = lgs[n];
+    } else {
+      t = bias[n];
 #pragma unroll
-    for (int w = 0; w < NT / 64; ++w) t += red[w][n];
+      for (int w = 0; w < NW; ++w) t += red[w][n];
+    }
     lg[n] = rnd_t<T>(t);
     if (n < N) {
       mx = fmaxf(mx, lg[n]);
@@ -231,16 +251,16 @@ head_row_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__ 
       gs[1][k] = g * xf[i];
     }
     lds_barrier();
-    {  // channel c = tid / 8: 8 lanes sum its 49 positions in a fixed order
-      const int c = tid >> 3, j = tid & 7;
+    {  // channel c = tid / CL: CL lanes sum its 49 positions in a fixed order
+      const int c = tid / CL, j = tid % CL;
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-      for (int f = j; f < PP; f += 8) {
+      for (int f = j; f < PP; f += CL) {
         s1 += gs[0][c * PP + f];
         s2 += gs[1][c * PP + f];
       }
-      s1 = gsum<8>(s1);
-      s2 = gsum<8>(s2);
+      s1 = group_sum<CL>(s1);  // every lane active (DPP)
+      s2 = group_sum<CL>(s2);
       if (j == 0) {
         hr.bsum[(size_t)b * 2 * C + c] = s1;
         hr.bsum[(size_t)b * 2 * C + C + c] = s2;
@@ -289,8 +309,8 @@ bool resident(at::ScalarType st) {
   bool ok = true;
   with_t(dt_of(at::empty({0}, at::TensorOptions().dtype(st))), [&](auto tag) {
     typedef decltype(tag) T;
-    ok = co_resident(reinterpret_cast<const void*>(&head_row_kernel<T, 10>), BMAX, NT, 0) &&
-         co_resident(reinterpret_cast<const void*>(&head_row_kernel<T, NMAX>), BMAX, NT, 0);
+    ok = co_resident(reinterpret_cast<const void*>(&head_row_kernel<T, 10, NT_MAX>), BMAX, NT_MAX, 0) &&
+         co_resident(reinterpret_cast<const void*>(&head_row_kernel<T, NMAX, 256>), BMAX, 256, 0);
   });
   return ok;
 }
@@ -362,8 +382,15 @@ void head_step(at::Tensor y2, at::Tensor fslab2, at::Tensor fstats2, at::Tensor 
   hr.bsum = bwd ? bsum_rows->data_ptr<float>() : nullptr;
   with_t(dt_of(y2), [&](auto tag) {
     typedef decltype(tag) T;
-    auto kern = N <= 10 ? head_row_kernel<T, 10> : head_row_kernel<T, NMAX>;
-    hipLaunchKernelGGL(kern, dim3(B), dim3(NT), 0, cur_stream(), dptr<T>(y2), bp, wfc.data_ptr<float>(),
+    static const int nt = [] {
+      const char* e = std::getenv("DPA_HEAD_NT");
+      return e != nullptr && std::atoi(e) == NT_MAX ? NT_MAX : 256;
+    }();
+    // 16-class tiles stay at 256 lanes (at 1024 the 128-VGPR budget spills them)
+    const int ntl = N <= 10 ? nt : 256;
+    auto kern = N > 10 ? head_row_kernel<T, NMAX, 256>
+                       : (nt == 256 ? head_row_kernel<T, 10, 256> : head_row_kernel<T, 10, NT_MAX>);
+    hipLaunchKernelGGL(kern, dim3(B), dim3(ntl), 0, cur_stream(), dptr<T>(y2), bp, wfc.data_ptr<float>(),
                        bfc.data_ptr<float>(), dptr<T>(logits), dptr<T>(p2), idx2.data_ptr<uint8_t>(), dptr<T>(xh2), B,
                        N, hr);
   });

@@ -622,6 +622,7 @@ void register_optim(pybind11::module& m) {
   s.attr("FUSED_MAX") = opt::FUSED_MAX;
   s.attr("MAXT") = opt::MAXT;
   s.def("flat_copy", &opt::flat_copy);
+  DPA_DEF_STAMP_FNS(s);
 }
 
 }  // namespace dpa

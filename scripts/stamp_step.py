@@ -1,6 +1,8 @@
 """Phase timing of the fused ConvNet step kernels (experiment build with -DDPA_TIMING):
     DPA_BUILD_TAG=timing DPA_EXTRA_CFLAGS=-DDPA_TIMING python -m ddp_practice_amd.build
-    DPA_EXT_SO=ddp_practice_amd/_C_timing.so python scripts/stamp_step.py
+    DPA_EXT_SO=ddp_practice_amd/_C_timing.so python scripts/stamp_step.py [--forced]
+--forced: the W>1 step shape on one GPU (DDP + SyncBN with every collective forced at W=1,
+the xGMI engine's in-kernel exchanges), as bench.py --force-collectives.
 For the head step (convnet_head.head_step) and the merged layer-2 backward
 (convnet.conv2_bwd, roles split by block range): blocks, span (first start ->
 last stamp), start skew, and the mean time of each stamped phase relative to
@@ -58,6 +60,17 @@ wrap(C.convnet, "conv1_wgrad_slab2", lambda a: [("wgrad1_slab2/wgrad", slice(0, 
                                                  ("wgrad1_slab2/sums", slice(7 * B, 512))])
 wrap(C.convnet, "convnet_amp_step", lambda a: [("amp_step/producers", slice(0, 7 * B)),
                                                 ("amp_step/amp", slice(7 * B, 512))])
+wrap(C.optim, "amp_sgd_fused", lambda a: [("amp_sgd_fused", slice(0, 512))])
+FORCED = "--forced" in sys.argv
+if FORCED:
+    from ddp_practice_amd.parallel import comm as comm_mod  # noqa: E402
+    import ddp_practice_amd.distributed as ddist  # noqa: E402
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29517"), RANK="0",
+                      WORLD_SIZE="1", LOCAL_RANK="0")
+    comm_mod.Communicator.force_active = True
+    torch.cuda.set_device(0)
+    ddist.init_process_group("nccl")
 
 from ddp_practice_amd.amp import GradScaler  # noqa: E402
 from ddp_practice_amd.data import DeviceLoader  # noqa: E402
@@ -68,9 +81,14 @@ from ddp_practice_amd.optim import SGD  # noqa: E402
 dev = torch.device("cuda", 0)
 torch.manual_seed(0)
 m = ConvNet(amp_dtype=torch.bfloat16).to(dev)
+if FORCED:
+    from ddp_practice_amd.parallel import DistributedDataParallel, convert_sync_batchnorm  # noqa: E402
+
+    m = DistributedDataParallel(convert_sync_batchnorm(m), device_ids=[0])
 opt = SGD(m.parameters(), lr=1e-4)
 scaler = GradScaler()
-m.set_slab_sink(opt)  # as engine.TrainLoop: conv1's weight gradient inside the optimizer launch
+if not FORCED or m.defer_grad_sync_to(opt):  # as engine.TrainLoop
+    m.set_slab_sink(opt)  # conv1's weight-gradient sums inside the optimizer launch
 crit = CrossEntropyLoss()
 for it in range(4):
     x = torch.rand(B, 1, 28, 28, device=dev).to(torch.bfloat16)
