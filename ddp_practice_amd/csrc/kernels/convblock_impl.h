@@ -772,6 +772,19 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
     store_epi();
   }
   DPA_STAMP(2);
+  // PRO 1: this lane's pooled map / index / xhat outputs (for the backward) are stored AFTER
+  // the compute barrier: __syncthreads() waits vmcnt(0), so issued before it they held the
+  // whole workgroup until they retired; issued after it they overlap the MFMA loop (step
+  // -0.4 us; the same deferral of conv1's gather stores measured no gain,
+  // profiles/r4p_deferred_stores_ab.txt)
+  constexpr int DQ = PRO != 1 ? 1
+                     : (CIN % 8 == 0 && sizeof(T) == 2) ? 8 * ((CIN / 8 * HW + NTHR - 1) / NTHR)
+                                                          : (CIN * HW + NTHR - 1) / NTHR;
+  int dq_e[DQ];  // pooled-output element of entry d, -1: none
+  T dq_p[DQ], dq_x[DQ];
+  uint8_t dq_i[DQ];
+#pragma unroll
+  for (int d = 0; d < DQ; ++d) dq_e[d] = -1;
   if constexpr (PRO == 0) {
     stage_chw<T, CIN, H, W>(xb, [&](int ci, int h, int ww, T a, T bb) {
       img[imo((h + 2) * WPD + (ww + 2), ci)] = a;
@@ -865,11 +878,11 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
             const unsigned bits = __builtin_bit_cast(unsigned short, pvj);
             if (j & 1) pk[j >> 1] |= bits << 16; else pk[j >> 1] = bits;
             const int e = ci * HW + pix;  // (ci, pix) index of the pooled outputs
-            if (wr && e >= e_lo && e < e_hi) {
-              pin.p_out[(size_t)b * NPO + e] = pvj;
-              pin.idx_out[(size_t)b * NPO + e] = (uint8_t)(bi | (best > 0.f ? IDX_RELU : 0));
-              pin.xh_out[(size_t)b * NPO + e] = Cvt<T>::from_f(xh);
-            }
+            const int d = i * 8 + j;
+            dq_e[d] = wr && e >= e_lo && e < e_hi ? e : -1;
+            dq_p[d] = pvj;
+            dq_i[d] = (uint8_t)(bi | (best > 0.f ? IDX_RELU : 0));
+            dq_x[d] = Cvt<T>::from_f(xh);
           }
           // imo keeps each 8-channel group of a pixel contiguous (the swizzle moves groups)
           *reinterpret_cast<uint4*>(&img[imo((ho + 2) * WPD + (wo + 2), 8 * o)]) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
@@ -903,11 +916,10 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
           bn_relu_max4x<T>(top[i], bot[i], sc_s[ci], beta_s[ci], mean_s[ci], istd_s[ci], best, bi, xh);
           const T pv = Cvt<T>::from_f(best);
           img[imo((ho + 2) * WPD + (wo + 2), ci)] = pv;
-          if (wr && e >= e_lo && e < e_hi) {
-            pin.p_out[(size_t)b * NPO + e] = pv;
-            pin.idx_out[(size_t)b * NPO + e] = (uint8_t)(bi | (best > 0.f ? IDX_RELU : 0));
-            pin.xh_out[(size_t)b * NPO + e] = Cvt<T>::from_f(xh);
-          }
+          dq_e[i] = wr && e >= e_lo && e < e_hi ? e : -1;
+          dq_p[i] = pv;
+          dq_i[i] = (uint8_t)(bi | (best > 0.f ? IDX_RELU : 0));
+          dq_x[i] = Cvt<T>::from_f(xh);
         }
       }
     }
@@ -948,6 +960,17 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
   DPA_STAMP(4);
   __syncthreads();
   DPA_STAMP(5);
+  if constexpr (PRO == 1) {  // the deferred pooled outputs (see dq_e)
+    constexpr int NPO = CIN * HW;
+#pragma unroll
+    for (int d = 0; d < DQ; ++d)
+      if (dq_e[d] >= 0) {
+        const size_t o = (size_t)b * NPO + dq_e[d];
+        pin.p_out[o] = dq_p[d];
+        pin.idx_out[o] = dq_i[d];
+        pin.xh_out[o] = dq_x[d];
+      }
+  }
 
   const int lane = tid & 63, wv = tid >> 6;
   const int r = lane & 15, q = lane >> 4;
