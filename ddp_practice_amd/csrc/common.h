@@ -117,6 +117,14 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// LDS-only workgroup barrier: __syncthreads() is a workgroup fence whose s_waitcnt vmcnt(0)
+// makes every wave wait for ALL its outstanding global memory operations (stores included)
+// before the barrier.  Where the barrier only orders LDS accesses, wait for LDS alone.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
 // Lane-group sums without an LDS round trip.  __shfl_xor compiles to ds_bpermute_b32, each
 // step an LDS round trip waited with lgkmcnt(0): the ConvNet head's ten 64-lane reductions
 // were 60 serialized round trips (~3.5 us, head_row_kernel ISA).  Here: DPP lane moves inside

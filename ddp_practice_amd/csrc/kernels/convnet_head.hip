@@ -75,12 +75,7 @@ struct HeadRow {
   float* bsum;          // [B][2C] BN2 backward sums of each image (S1 | S2)
 };
 
-// LDS-only barrier: __syncthreads() is a workgroup fence whose vmcnt(0) would make every
-// wave wait here for its global stores (pooled outputs, dp2) and the loss atomic to retire
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-}
+// lds_barrier (common.h): the global stores (pooled outputs, dp2) and the loss atomic are not waited
 
 
 // NM: classes the register tiles are sized for (>= N); NT: workgroup size (256 | 1024)
