@@ -77,8 +77,10 @@ static __device__ unsigned long long dpa_stamps[DPA_MAX_STAMP_BLOCKS * DPA_NSTAM
 #define DPA_CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a HIP device tensor")
 #define DPA_CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
 #define DPA_CHECK_INPUT(t) \
-  DPA_CHECK_DEV(t);        \
-  DPA_CHECK_CONTIG(t)
+  do {                     \
+    DPA_CHECK_DEV(t);      \
+    DPA_CHECK_CONTIG(t);   \
+  } while (0)
 
 // Storage dtype tags for activations: fp32, bf16, fp16.
 enum class DT : int { F32 = 0, BF16 = 1, F16 = 2 };
