@@ -47,10 +47,16 @@ inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(
 #define DPA_NSTAMPS 16
 // one copy per translation unit (-fno-gpu-rdc): read back from the TU that owns the kernels
 static __device__ unsigned long long dpa_stamps[DPA_MAX_STAMP_BLOCKS * DPA_NSTAMPS];
+// The clock is read first (volatile asm, its own wait): with the builtin, the compiler put the
+// scalar load of the stamp array's address in front of it, and the read queued behind that
+// load's miss -- workgroup starts looked 2-4 us late (scripts/exp/dispatch_skew.hip: real
+// dispatch skew <= 0.4 us).
 #define DPA_STAMP(i)                                                                                     \
   do {                                                                                                   \
+    unsigned long long dpa_t_;                                                                           \
+    asm volatile("s_memrealtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(dpa_t_));                             \
     if (threadIdx.x == 0 && blockIdx.x < DPA_MAX_STAMP_BLOCKS)                                           \
-      dpa_stamps[blockIdx.x * DPA_NSTAMPS + (i)] = __builtin_amdgcn_s_memrealtime();                     \
+      dpa_stamps[blockIdx.x * DPA_NSTAMPS + (i)] = dpa_t_;                                               \
   } while (0)
 // read_stamps() / clear_stamps() of the calling translation unit's stamp array
 #define DPA_DEF_STAMP_FNS(s)                                                                          \

@@ -19,9 +19,25 @@ C = _ext.load()
 report = []
 
 
+DUMP_STARTS = "--starts" in sys.argv
+
+
+def starts_line(name, rows):
+    """Workgroup start offsets (us after the first) by block index: dispatch order / rate."""
+    st = (rows[:, 0] - rows[:, 0].min()) / 100
+    n = len(st)
+    q = [st[int(i * (n - 1) / 8)].item() for i in range(9)]
+    srt = st.sort().values
+    qs = [srt[int(i * (n - 1) / 8)].item() for i in range(9)]
+    return (f"{name:18s} start by block index (every n/8-th): " + " ".join(f"{v:4.2f}" for v in q) +
+            " | sorted quantiles: " + " ".join(f"{v:4.2f}" for v in qs))
+
+
 def summarize(name, rows):
     if len(rows) == 0:
         return f"{name:18s} no stamps"
+    if DUMP_STARTS:
+        report.append(starts_line(name, rows))
     t0 = rows[:, 0].min()
     end = rows.max(dim=1).values
     line = (f"{name:18s} blocks={len(rows):4d} span={(end.max() - t0).item() / 100:6.2f}us "
