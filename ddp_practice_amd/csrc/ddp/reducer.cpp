@@ -202,13 +202,21 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
       deferred_ = true;  // the buckets hold this rank's gradients until flush_deferred() / a fused consumer
     else
       for (size_t b = 0; b < buckets_.size(); ++b) comm_->wait((int)b, on_cuda_ ? work_stream_ : nullptr);
-    // grads become views of the all-reduced buckets (in-place buckets: they already are)
+    // grads become views of the all-reduced buckets (in-place buckets: they already are);
+    // gradient_as_bucket_view=False: the averaged values are copied back into the gradient
+    // tensors autograd produced (their identity and storage are kept, torch's default layout)
     for (auto& bk : buckets_) {
       if (bk.inplace) continue;
       for (size_t j = 0; j < bk.params.size(); ++j) {
         auto& p = params_[bk.params[j]];
         at::Tensor view = bk.flat.narrow(0, bk.offsets[j], p.numel()).view(p.sizes());
-        p.mutable_grad() = view;
+        if (grad_as_view_) {
+          p.mutable_grad() = view;
+        } else if (p.grad().defined() && p.grad().sizes() == p.sizes()) {
+          p.mutable_grad().copy_(view);
+        } else {
+          p.mutable_grad() = view.clone();  // an unused parameter: the reduced (zero) gradient
+        }
       }
     }
     finalized_ = true;
@@ -226,6 +234,11 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     defer_ = on;
   }
   bool deferred_pending() const { return deferred_; }
+  void set_grad_as_view(bool on) {
+    std::lock_guard<std::mutex> g(mu_);
+    TORCH_CHECK(on || !defer_, "DDP: gradient_as_bucket_view=False with deferred gradient averaging");
+    grad_as_view_ = on;
+  }
   void set_require_inplace(bool on) {
     std::lock_guard<std::mutex> g(mu_);
     require_inplace_ = on;
@@ -390,6 +403,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   bool defer_ = false, deferred_ = false;  // see set_defer
   bool require_inplace_ = false;           // see set_require_inplace (DDP.set_slab_sink)
   bool join_each_ = false;  // join every bucket immediately (no overlap)
+  bool grad_as_view_ = true;  // param.grad = views of the buckets (gradient_as_bucket_view)
   bool zero_copy_ = true;   // reduce tiled gradient regions in place (DPA_REDUCER_ZERO_COPY=0: always pack)
   std::vector<int64_t> order_;
   std::mutex mu_;
@@ -418,6 +432,7 @@ void register_reducer(pybind11::module& m) {
       .def("set_defer", &ddp::Reducer::set_defer)
       .def("deferred_pending", &ddp::Reducer::deferred_pending)
       .def("set_require_inplace", &ddp::Reducer::set_require_inplace)
+      .def("set_grad_as_view", &ddp::Reducer::set_grad_as_view)
       .def("consume_deferred", &ddp::Reducer::consume_deferred)
       .def("flush_deferred", &ddp::Reducer::flush_deferred);
 }

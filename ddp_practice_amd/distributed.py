@@ -19,6 +19,8 @@ communicators (gloo on CPU) complete before returning.
 """
 from __future__ import annotations
 
+import time
+
 import torch
 import torch.distributed as _tdist
 
@@ -42,8 +44,9 @@ def get_backend(group=None) -> str:
 class Work:
     """torch.distributed.Work for a stream-ordered collective (see the module docstring)."""
 
-    def __init__(self, result, device: torch.device | None):
+    def __init__(self, result, device: torch.device | None, comm=None):
         self._result = result
+        self._comm = comm if comm is not None else default_comm()
         self._event = None
         if device is not None and device.type == "cuda" and torch.cuda.is_available():
             self._event = torch.cuda.Event()
@@ -51,20 +54,42 @@ class Work:
 
     def wait(self, timeout=None) -> bool:
         """Order the current stream after the collective (already true: the collective was
-        enqueued on it); a different current stream waits on the collective's event."""
+        enqueued on it); a different current stream waits on the collective's event.  With a
+        ``timeout`` (seconds or ``datetime.timedelta``), also block the host until the
+        collective completes, raising ``RuntimeError`` when it has not after ``timeout`` or
+        when the communicator reported an error (torch's blocking-wait behaviour)."""
         if self._event is not None:
             torch.cuda.current_stream().wait_event(self._event)
+        if timeout is not None:
+            secs = timeout.total_seconds() if hasattr(timeout, "total_seconds") else float(timeout)
+            deadline = time.monotonic() + max(secs, 0.0)
+            while not self.is_completed():
+                exc = self.exception()
+                if exc is not None:
+                    raise exc
+                if time.monotonic() >= deadline:
+                    raise RuntimeError(f"collective work timed out after {secs:.3f} s")
+                time.sleep(1e-4)
+            exc = self.exception()
+            if exc is not None:
+                raise exc
         return True
 
     def is_completed(self) -> bool:
         return self._event is None or self._event.query()
 
+    def _error(self) -> str:
+        fn = getattr(self._comm, "async_error", None)
+        err = fn() if fn is not None else ""
+        return "" if (not err or err == "destroyed") else err
+
     def is_success(self) -> bool:
-        err = default_comm().async_error()
-        return not err or err == "destroyed"
+        return not self._error()
 
     def exception(self):
-        return None
+        """The communicator's asynchronous error as an exception (None when healthy)."""
+        err = self._error()
+        return RuntimeError(f"collective failed: {err}") if err else None
 
     def synchronize(self) -> None:
         if self._event is not None:
@@ -84,7 +109,7 @@ def _done(result, comm, async_op: bool):
     if not async_op:
         return None
     dev = getattr(comm, "device", None)
-    return Work(result, dev)
+    return Work(result, dev, comm)
 
 
 def all_reduce(tensor: torch.Tensor, op=ReduceOp.SUM, group=None, async_op: bool = False):

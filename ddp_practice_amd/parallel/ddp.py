@@ -24,7 +24,6 @@ from __future__ import annotations
 
 import contextlib
 import os
-import warnings
 
 import torch
 import torch.nn as nn
@@ -78,8 +77,9 @@ class DistributedDataParallel(nn.Module):
         self.broadcast_buffers = broadcast_buffers
         self.find_unused_parameters = find_unused_parameters
         self.static_graph = static_graph
-        if not gradient_as_bucket_view:
-            warnings.warn("gradient_as_bucket_view=False is not supported; grads are bucket views")
+        # False (torch's default): after the all-reduce the averaged values are copied back into
+        # the gradient tensors autograd produced; True: param.grad become views of the buckets
+        self.gradient_as_bucket_view = gradient_as_bucket_view
         self.comm = process_group if isinstance(process_group, _comm.Communicator) else _comm.default_comm()
         self.bucket_cap_bytes = (bucket_cap_mb if bucket_cap_mb is not None else DEFAULT_BUCKET_CAP_MB) * 2 ** 20
         self.first_bucket_bytes = (first_bucket_mb if first_bucket_mb is not None
@@ -100,6 +100,8 @@ class DistributedDataParallel(nn.Module):
         if self.comm.active and self._params:
             buckets = compute_bucket_assignment(self._params, self.bucket_cap_bytes, self.first_bucket_bytes)
             self.reducer = _load_ext().ddp.Reducer(self._params, buckets, self.comm.native, find_unused_parameters)
+            if not gradient_as_bucket_view:
+                self.reducer.set_grad_as_view(False)
 
     # ------------------------------------------------------------- init sync
     def _owner_of_buffer(self, name: str):
@@ -229,8 +231,8 @@ class DistributedDataParallel(nn.Module):
         parameter belongs to this module, and the gradients fit one exchange.
         ``DPA_FUSED_GRAD=0`` disables it.  Returns whether it was enabled.
         """
-        if os.environ.get("DPA_FUSED_GRAD", "1") == "0" or self.reducer is None:
-            return False
+        if os.environ.get("DPA_FUSED_GRAD", "1") == "0" or self.reducer is None or not self.gradient_as_bucket_view:
+            return False  # (the fused consumer writes the averaged gradients into the bucket views)
         xc = getattr(self.comm, "xgmi", None)
         if xc is None or not hasattr(optimizer, "fused_amp_step"):
             return False

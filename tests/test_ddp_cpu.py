@@ -70,3 +70,11 @@ def test_ddp_exact_shape_and_dtype_check(kind, needle):
 
 def test_ddp_slab_sink_requires_deferred_zero_copy():
     assert run(W.ddp_slab_sink_guard, world=2) == [True, True]
+
+
+def test_ddp_gradient_as_bucket_view_false_copies_back():
+    """gradient_as_bucket_view=False keeps autograd's gradient tensors (values averaged
+    into them), VERDICT r3 minor API item."""
+    from ._ddp_workers import ddp_grad_not_bucket_view
+
+    assert all(run(ddp_grad_not_bucket_view, world=2))
