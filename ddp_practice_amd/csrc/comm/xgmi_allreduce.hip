@@ -431,8 +431,8 @@ XgmiComm::XgmiComm(int rank, int world, int device, long long slot_bytes, double
     ts_ctr_ = static_cast<uint32_t*>(c2);
   }
   void* tk = nullptr;
-  DPA_CHECK_HIP(hipMalloc(&tk, kSites * kTickLanes * kTickStride * sizeof(unsigned long long)));
-  DPA_CHECK_HIP(hipMemset(tk, 0, kSites * kTickLanes * kTickStride * sizeof(unsigned long long)));
+  DPA_CHECK_HIP(hipMalloc(&tk, kSites * kEpochWords * sizeof(unsigned long long)));
+  DPA_CHECK_HIP(hipMemset(tk, 0, kSites * kEpochWords * sizeof(unsigned long long)));
   DPA_CHECK_HIP(hipDeviceSynchronize());
   ticks_ = static_cast<unsigned long long*>(tk);
   for (int i = 0; i < kMaxRanks; ++i) peers_.base[i] = nullptr;
@@ -594,7 +594,7 @@ XSite XgmiComm::site(int s) const {
   TORCH_CHECK(s >= 0 && s < kSites, "xgmi: site id out of range");
   XSite x;
   for (int p = 0; p < world_; ++p) x.base[p] = peers_.base[p] + site_off_ + (long long)s * kSiteBytes;
-  x.tick = ticks_ + (long long)s * kTickLanes * kTickStride;
+  x.tick = ticks_ + (long long)s * kEpochWords;
   x.rank = rank_;
   x.world = world_;
   x.err = dev_words_;

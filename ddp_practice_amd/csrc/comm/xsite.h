@@ -15,18 +15,16 @@
 // The granule protocol is the one-shot all-reduce's (comm/xgmi_allreduce.hip):
 // value and tag land in one 8-byte store, no flag, no fence.
 //
-// Epoch without host involvement (graph-replayable, any grid size): every
-// workgroup of a consumer launch takes one ticket from one of this rank's
-// kTickLanes site words {epoch:32 | tickets:32} (lane = workgroup index mod the
-// lane count, each word on its own 256-B line) with a device-scope atomic; the
-// workgroup that takes the last ticket of its lane returns that lane's tickets
-// to 0 and bumps its epoch (lanes no workgroup maps to, in launches of fewer
-// than kTickLanes workgroups, are bumped by a workgroup that knows they are
-// idle).  Every lane therefore advances by exactly one per launch, all
-// workgroups of one launch see the same epoch (launches of a site are
-// stream-ordered), and every rank issues the same sequence of launches.
-// (One word per site serialised all of a launch's atomics at one address: 224
-// workgroups of the conv1 weight gradient waited ~2 us for their tickets.)
+// Epoch without host involvement (graph-replayable, any grid size <= kEpochWords): every
+// site keeps one epoch word per workgroup index in this rank's memory.  Workgroup b of a
+// launch reads word b (no atomic read-modify-write, no contention: its round trip hides
+// behind the caller's slab loads), uses epoch = word + 1, and writes that epoch to words
+// b, b + nblk, b + 2 nblk, ... -- so every word advances by exactly one per launch whatever
+// the launch's workgroup count, all workgroups of a launch see the same epoch (launches of
+// a site are stream-ordered; kernel boundaries make the words visible across XCDs), and
+// every rank issues the same sequence of launches.  (Round 3 took tickets from shared
+// words with device-scope atomics: same-address atomics of up to 224 workgroups serialized,
+// and the last ticket of each word re-armed it with a second atomic.)
 // Reuse safety as for the one-shot kernel: a rank writes parity p of epoch e+2
 // only after its launch e+1 read every peer's e+1 row, which each peer wrote
 // after its own launch e had completed.
@@ -40,8 +38,7 @@ namespace dpa {
 namespace xgmi {
 
 constexpr int kMaxRanks = 8;
-constexpr int kTickLanes = 8;    // ticket words per site
-constexpr int kTickStride = 32;  // u64 between them (256 B: distinct lines / channels)
+constexpr int kEpochWords = 512;  // epoch words per site: the largest site grid (7 x 64 images: conv1 weight gradient)
 constexpr int kSites = 8;                                             // sites per communicator
 constexpr int kSiteVals = 128;                                        // floats per rank row (>= 2C+1)
 constexpr long long kSiteSlotBytes = kSiteVals * 8LL;                 // granules
@@ -60,8 +57,8 @@ constexpr int kSiteGrad = kSites - 1;
 
 struct XSite {
   char* base[kMaxRanks] = {};            // this site's region in every rank's workspace (peer-mapped)
-  unsigned long long* tick = nullptr;    // this rank's {epoch | tickets} words (kTickLanes, kTickStride
-                                         // apart); nullptr: site inactive
+  unsigned long long* tick = nullptr;    // this rank's kEpochWords epoch words of the site;
+                                         // nullptr: site inactive
   int rank = 0, world = 1;
   int* err = nullptr;                    // host-mapped: 1 timeout, 2 aborted
   const int* abort_flag = nullptr;
@@ -73,30 +70,33 @@ struct XSite {
   __host__ __device__ bool active() const { return tick != nullptr; }
 };
 
-// Lane 0 of every workgroup, once per launch, as early as possible (the
-// returned word is only needed by xsite_exchange: the atomic's latency hides
-// behind the caller's slab loads).  bid: the workgroup's index among the
-// launch's workgroups taking tickets on this site.
+// Lane 0 of every workgroup, once per launch, as early as possible (the returned word is
+// only needed by xsite_exchange: its round trip hides behind the caller's slab loads).
+// bid: the workgroup's index among the launch's workgroups on this site.
 __device__ __forceinline__ unsigned long long xsite_ticket(const XSite& xs, int bid) {
-  const int nblk = xs.nblk > 0 ? xs.nblk : (int)(gridDim.x * gridDim.y * gridDim.z);
-  const int nw = nblk < kTickLanes ? nblk : kTickLanes;
-  return __hip_atomic_fetch_add(xs.tick + (bid % nw) * kTickStride, 1ull, __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(xs.tick + (bid < kEpochWords ? bid : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Lane 0: the launch's epoch from its ticket (the last ticket of each lane re-arms
-// that lane's word for the next launch).
+// The launch's epoch from the word xsite_ticket read.
 __device__ __forceinline__ uint32_t xsite_epoch(const XSite& xs, unsigned long long tk, int bid) {
+  (void)xs;
+  (void)bid;
+  return (uint32_t)tk + 1u;
+}
+
+// Every thread of workgroup bid (nthr threads), after the epoch is known: advance this
+// workgroup's residue class of epoch words (b, b + nblk, ...) to ep.  A grid larger than
+// kEpochWords cannot keep its workgroups' epochs equal: flagged as an error (the exchange
+// then gives up), and the host checks grids against it.
+__device__ __forceinline__ void xsite_advance(const XSite& xs, uint32_t ep, int bid, int nthr) {
   const int nblk = xs.nblk > 0 ? xs.nblk : (int)(gridDim.x * gridDim.y * gridDim.z);
-  const int nw = nblk < kTickLanes ? nblk : kTickLanes;
-  const int lane = bid % nw;
-  const uint32_t n_lane = (uint32_t)((nblk - lane + nw - 1) / nw);  // workgroups on this lane
-  if ((uint32_t)tk == n_lane - 1u)  // last ticket of this lane: next launch, next epoch
-    __hip_atomic_fetch_add(xs.tick + lane * kTickStride, (1ull << 32) - (unsigned long long)n_lane,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (int w = bid + nblk; w < kTickLanes; w += nblk)  // lanes idle in this launch (nblk < kTickLanes)
-    __hip_atomic_fetch_add(xs.tick + w * kTickStride, 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return (uint32_t)(tk >> 32) + 1u;
+  const int tid = threadIdx.x;
+  if (nblk > kEpochWords) {
+    if (tid == 0) __hip_atomic_store(xs.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  for (int w = bid + tid * nblk; w < kEpochWords; w += nthr * nblk)
+    __hip_atomic_store(xs.tick + w, (unsigned long long)ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Checked every 256 polls of a bounded wait: 2 = aborted (watchdog), 1 = this wait timed
@@ -134,12 +134,13 @@ __device__ __forceinline__ float xsite_wait(const XSite& xs, const unsigned long
 // bid: the workgroup's index in its role (the role's workgroup 0 pushes).  Called by
 // every thread of the workgroup; ends with a barrier.
 __device__ __forceinline__ void xsite_exchange(const XSite& xs, float* vals, int n, unsigned long long tk,
-                                               int bid) {
+                                               int bid, int nthr = 256 /* <= the workgroup size */) {
   __shared__ uint32_t ep_s;
   const int tid = threadIdx.x;
   const bool pusher = bid == 0;
   if (tid == 0) ep_s = xsite_epoch(xs, tk, bid);
   __syncthreads();
+  xsite_advance(xs, ep_s, bid, nthr);
   if (tid < n) {
     const uint32_t ep = ep_s;
     const long long par = (long long)(ep & 1u) * kMaxRanks * xs.slot_bytes;
@@ -223,6 +224,7 @@ __device__ __forceinline__ void xsite_exchange_slice(const XSite& xs, float* val
   if (tid == 0) ep_s = xsite_epoch(xs, tk, bid);
   __syncthreads();
   const uint32_t ep = ep_s;
+  xsite_advance(xs, ep, bid, nthr);
   for (int i = tid; i < n; i += nthr) xsite_push_at(xs, ep, pos(i), vals[i]);
   const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
   unsigned polls = 0;

@@ -289,6 +289,7 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
     if (tid == 0) ep_x = xgmi::xsite_epoch(xg, tk, bid);
     __syncthreads();
     const uint32_t ep = ep_x;
+    xgmi::xsite_advance(xg, ep, bid, THR);
     const long long par = (long long)(ep & 1u) * xgmi::kMaxRanks * xg.slot_bytes;
     auto gran = [ep](float v) { return ((unsigned long long)ep << 32) | (unsigned long long)__float_as_uint(v); };
     typedef __attribute__((ext_vector_type(2))) unsigned long long u64x2;

@@ -906,6 +906,7 @@ __global__ void __launch_bounds__(S1_THR) stat_sum1_kernel(StatArgs sa, long lon
   part[rg][col] = a;
   if (xon && threadIdx.x == 0) ep_s = xgmi::xsite_epoch(sa.xs, tk, xbid);
   __syncthreads();
+  if (xon) xgmi::xsite_advance(sa.xs, ep_s, xbid, S1_THR);
   if (threadIdx.x >= S1_COLS) return;
   float t = 0.f;
 #pragma unroll
