@@ -213,21 +213,25 @@ head_row_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__ 
   if (!(tgt >= 0 && tgt < N)) xt = NAN;  // an out-of-range target: NaN loss (torch raises)
   const float row_loss = use ? (1.f - hr.smoothing) * (lse - xt) + hr.smoothing * (lse - sx / (float)N) : 0.f;
   float ds[NM];  // d(scale * loss)/dlogits of this row, rounded to the storage dtype
+  float my_lg = 0.f, my_d = 0.f;  // lane n < N: class n's logit and gradient (selected, no branch)
+  const float rse = 1.f / se, sm0 = hr.smoothing / (float)N;
 #pragma unroll
   for (int n = 0; n < NM; ++n) {
     float d = 0.f;
     if (use && n < N) {
-      const float sm = ex[n] * (1.f / se);
-      const float oh = (n == tgt ? 1.f - hr.smoothing : 0.f) + hr.smoothing / (float)N;
+      const float sm = ex[n] * rse;
+      const float oh = (n == tgt ? 1.f - hr.smoothing : 0.f) + sm0;
       d = (sm - oh) * inv;
     }
     ds[n] = rnd_t<T>(d * scv);
-    if (tid == n && n < N) {  // one lane per class writes the row's outputs
-      const size_t o = (size_t)b * N + n;
-      logits[o] = Cvt<T>::from_f(lg[n]);
-      hr.dlog[o] = d;
-      if (hr.dls != nullptr) reinterpret_cast<T*>(hr.dls)[o] = Cvt<T>::from_f(d * scv);
-    }
+    my_lg = tid == n ? lg[n] : my_lg;
+    my_d = tid == n ? d : my_d;
+  }
+  if (tid < N) {  // one lane per class writes the row's outputs (one branch, not one per class)
+    const size_t o = (size_t)b * N + tid;
+    logits[o] = Cvt<T>::from_f(my_lg);
+    hr.dlog[o] = my_d;
+    if (hr.dls != nullptr) reinterpret_cast<T*>(hr.dls)[o] = Cvt<T>::from_f(my_d * scv);
   }
   if (hr.dp2 != nullptr) {
     DPA_STAMP(4);

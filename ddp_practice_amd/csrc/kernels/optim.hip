@@ -127,6 +127,7 @@ amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ trac
                      xgmi::XSite xg, int* __restrict__ err, long long barrier_ticks, SlabSet ss, int grid) {
   // grid == the launch's workgroup count, passed in: gridDim is a load from the hidden kernel
   // arguments on gfx950, and its wait at the top of the kernel came before the table loads
+  DPA_STAMP(0);
   amp_sgd_body<U, XG, THR>(L, scale, tracker, found_inf, sync, lr, momentum, dampening, wd, nesterov, maximize,
                            growth, backoff, interval, xg, err, barrier_ticks, ss, grid, (int)blockIdx.x);
 }
