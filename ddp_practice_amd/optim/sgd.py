@@ -47,6 +47,13 @@ class SGD(Optimizer):
         defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
                         nesterov=nesterov, maximize=maximize)
         super().__init__(params, defaults)
+        # grid-barrier state of the fused AMP step, zeroed here, outside any graph capture:
+        # created lazily inside a capture, its zero-fill became a graph node that re-ran on
+        # every replay (profiles/r4final_convnet_steady.txt)
+        ps = [p for g in self.param_groups for p in g["params"]]
+        if ps and all(p.is_cuda for p in ps) and len({p.device for p in ps}) == 1:
+            self._amp_sync = torch.zeros(4, dtype=torch.int64, device=ps[0].device)
+            self._amp_sync_large = torch.zeros(4, dtype=torch.int64, device=ps[0].device)
 
     def defer_slab(self, slab: torch.Tensor, out: torch.Tensor) -> None:
         """A gradient region ``out`` that is still the partial rows ``slab`` [rows][out.numel()]
