@@ -17,6 +17,18 @@ struct Peers {
   char* base[kMaxRanks];  // every rank's workspace, mapped into this process
 };
 
+// Host side of xsite_advance's limit: a launch whose workgroups on an active site
+// outnumber the site's kEpochWords epoch words cannot advance every word by one, so the
+// next launch on the site would re-use this epoch and read the peers' previous rows.
+// Every launcher that attaches a site sets its workgroup count through this check.
+inline bool site_grid_fits(long long nblk) { return nblk >= 1 && nblk <= kEpochWords; }
+inline void set_site_grid(XSite& xs, long long nblk, const char* what) {
+  if (!xs.active()) return;
+  TORCH_CHECK(site_grid_fits(nblk), what, ": ", nblk, " workgroups on one in-kernel exchange site (at most ",
+              kEpochWords, "); the caller must take the all-reduce launch path");
+  xs.nblk = (int)nblk;
+}
+
 class XgmiComm {
  public:
   // max_bytes: largest message this engine takes; timeout_s: bound on every wait

@@ -642,7 +642,7 @@ void XgmiComm::wide_probe(const at::Tensor& in, const at::Tensor& out, int nblk)
   TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.numel() == in.numel(), "wide_probe: out like in");
   TORCH_CHECK(nblk >= 1 && nblk <= in.numel(), "wide_probe: 1..n finishers");
   XSite xs = wide_site();
-  xs.nblk = nblk;
+  set_site_grid(xs, nblk, "wide_probe");
   hipLaunchKernelGGL(wide_probe_kernel, dim3(nblk), dim3(256), 0, cur_stream(), xs, in.data_ptr<float>(),
                      out.data_ptr<float>(), (int)in.numel());
   DPA_CHECK_LAUNCH();
@@ -669,7 +669,10 @@ void XgmiComm::site_probe(int s, const at::Tensor& in, const at::Tensor& out, in
               "site_probe: <= ", kSiteVals, " contiguous f32 values");
   TORCH_CHECK(out.numel() == (int64_t)grid * in.numel() && out.scalar_type() == at::kFloat && grid >= 1);
   TORCH_CHECK(s >= 0 && s < kSiteGrad, "site_probe: SyncBN site id");
-  hipLaunchKernelGGL(site_probe_kernel, dim3(grid), dim3(256), 0, cur_stream(), site(s), in.data_ptr<float>(),
+  XSite xs = site(s);
+  set_site_grid(xs, grid, "site_probe");
+  xs.nblk = 0;  // the whole grid
+  hipLaunchKernelGGL(site_probe_kernel, dim3(grid), dim3(256), 0, cur_stream(), xs, in.data_ptr<float>(),
                      out.data_ptr<float>(), (int)in.numel());
   DPA_CHECK_LAUNCH();
 }

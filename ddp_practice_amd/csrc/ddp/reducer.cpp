@@ -232,6 +232,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     std::lock_guard<std::mutex> g(mu_);
     TORCH_CHECK(!(defer_ && !on && deferred_), "DDP: gradients still pending a deferred all-reduce");
     defer_ = on;
+    if (!on) require_inplace_ = false;  // only the deferred slab sink needs in-place buckets
   }
   bool deferred_pending() const { return deferred_; }
   void set_grad_as_view(bool on) {

@@ -958,7 +958,7 @@ static xgmi::XSite stats_site(const std::shared_ptr<xgmi::XgmiComm>& xc, int64_t
   if (!xc) return xgmi::XSite{};
   TORCH_CHECK(2 * C + 1 <= xgmi::kWideVals, "bn_nhwc: SyncBN site row holds 2C+1 <= ", xgmi::kWideVals);
   xgmi::XSite xs = xc->wide_site();
-  xs.nblk = Gc;  // one finisher per channel chunk
+  xgmi::set_site_grid(xs, Gc, "bn_nhwc statistics");  // one finisher per channel chunk
   return xs;
 }
 

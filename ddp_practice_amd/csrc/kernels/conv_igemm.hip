@@ -1561,7 +1561,7 @@ static void launch_stat_tree(StatArgs sa, long long M, int bm, int K, int BN) {
   const long long rows = (M + bm - 1) / bm, NG = (rows + G1 - 1) / G1;
   if (rows <= S1_MAXROWS) {  // one level: every row in flight at once, no ticket
     const dim3 gr((unsigned)(K / BN), (unsigned)(2 * BN / S1_COLS)), th(S1_THR);
-    sa.xs.nblk = (int)(gr.x * gr.y);  // SyncBN finishers: every workgroup
+    xgmi::set_site_grid(sa.xs, (long long)gr.x * gr.y, "stat_sum1");  // SyncBN finishers: every workgroup
     if (rows <= 16 * S1_RG) {
       if (BN == 128) hipLaunchKernelGGL((stat_sum1_kernel<128, 16>), gr, th, 0, cur_stream(), sa, M, bm, K);
       else hipLaunchKernelGGL((stat_sum1_kernel<64, 16>), gr, th, 0, cur_stream(), sa, M, bm, K);
@@ -1573,7 +1573,7 @@ static void launch_stat_tree(StatArgs sa, long long M, int bm, int K, int BN) {
     return;
   }
   const dim3 gr((unsigned)(NG * (K / BN))), th(THR);
-  sa.xs.nblk = K / BN;  // SyncBN finishers: the last arriver of each channel tile
+  xgmi::set_site_grid(sa.xs, K / BN, "stat_tree");  // SyncBN finishers: the last arriver of each channel tile
   if (BN == 128) hipLaunchKernelGGL(stat_tree_kernel<128>, gr, th, 0, cur_stream(), sa, M, bm, K);
   else hipLaunchKernelGGL(stat_tree_kernel<64>, gr, th, 0, cur_stream(), sa, M, bm, K);
   DPA_CHECK_LAUNCH();

@@ -277,7 +277,7 @@ void conv2_fwd(at::Tensor y1, c10::optional<at::Tensor> fslab1, at::Tensor fstat
   BNParams bp = bn_params(fslab1, fstats1, g1, b1, rm1, rv1, nbt1, momentum, eps, train, 16);
   if (train) {
     bp.xs = site_of(xc, xgmi::kSiteFwd1);
-    bp.xs.nblk = B * 2;  // the grid (ns workgroups per image)
+    xgmi::set_site_grid(bp.xs, B * 2, "conv2_fwd");  // the grid (ns workgroups per image)
   }
   constexpr int ns = 2;
   hipStream_t stream = cur_stream();
@@ -316,7 +316,11 @@ void head_fwd(at::Tensor y2, c10::optional<at::Tensor> fslab2, at::Tensor fstats
                 xh2_out->numel() == p2_out->numel());
   if (B == 0) return;
   BNParams bp = bn_params(fslab2, fstats2, g2, b2, rm2, rv2, nbt2, momentum, eps, train, 32);
-  if (train) bp.xs = site_of(xc, xgmi::kSiteFwd2);
+  if (train) {
+    bp.xs = site_of(xc, xgmi::kSiteFwd2);
+    xgmi::set_site_grid(bp.xs, B, "head_fwd");  // one workgroup per image
+    bp.xs.nblk = 0;                             // (the kernel reads the grid)
+  }
   hipStream_t stream = cur_stream();
   with_t(dt_of(y2), [&](auto tag) {
     typedef decltype(tag) T;
@@ -460,6 +464,7 @@ void conv2_dgrad(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx
     typedef decltype(tag) T;
     BwdIn<T> bi = bwd_in<T>(dp2, idx2, y2, fstats2, gsum2, c10::nullopt, g2, eps2, 32, c10::nullopt, c10::nullopt);
     bi.xs = site_of(xc, xgmi::kSiteBwd2Dgrad);
+    xgmi::set_site_grid(bi.xs, B * kDgradSplit, "conv2_dgrad");
     BwdEpi<T> ep{idx1.data_ptr<uint8_t>(), dptr<T>(xh1), bslab1.data_ptr<float>()};
     hipLaunchKernelGGL((cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1, 1>), dim3(B * kDgradSplit), dim3(cb::NTHR),
                        0, cur_stream(), nullptr, nullptr, nullptr, dptr<T>(dp1), nullptr, nullptr, nullptr,
@@ -625,14 +630,14 @@ void conv2_bwd(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx2,
     bw.dgamma = bw.dbeta = nullptr;  // one writer: the data-gradient role's workgroup 0
     bd.xs = site_of(xc, xgmi::kSiteBwd2Dgrad);
     bw.xs = site_of(xc, xgmi::kSiteBwd2Wgrad);
-    bd.xs.nblk = ndg;  // each role's workgroups take tickets on their own site
-    bw.xs.nblk = nwg;
+    xgmi::set_site_grid(bd.xs, ndg, "conv2_bwd data gradient");  // each role's workgroups take
+    xgmi::set_site_grid(bw.xs, nwg, "conv2_bwd weight gradient");  // tickets on their own site
     BwdEpi<T> ep{idx1.data_ptr<uint8_t>(), dptr<T>(xh1), bslab1.data_ptr<float>()};
     FcW<T> fw = fc_args<T>(fc_dls, fc_p2, fc_dw, fc_db, B, y2.scalar_type());
     const int nfc = fc_dls.has_value() ? FC_BLOCKS : 0;
     if constexpr (std::is_same<T, float>::value) {
       // fp32 tiles: the two roles' LDS (173 KB) exceed one CU's 160 KB -> separate launches
-      bd.xs.nblk = bw.xs.nblk = 0;
+      bd.xs.nblk = bw.xs.nblk = 0;  // each launch is its site's whole grid (ndg, nwg: checked above)
       hipLaunchKernelGGL((cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1, 1>), dim3(ndg), dim3(cb::NTHR), 0,
                          cur_stream(), nullptr, nullptr, nullptr, dptr<T>(dp1), nullptr, nullptr, nullptr,
                          kDgradSplit, PoolIn<T>{}, bd, ep, dptr<T>(wpk_d), cb::WPack<T>{});
@@ -814,7 +819,7 @@ void wgrad1_reduce(at::Tensor x, at::Tensor y1, at::Tensor dp1, at::Tensor idx1,
     if (xc) {
       TORCH_CHECK(!lsum.has_value(), "fused SyncBN exchange: gsum must be this rank's rows (no lsum)");
       bi.xs = site_of(xc, xgmi::kSiteBwd1);
-      bi.xs.nblk = nwg1;  // the reduction workgroups take no tickets
+      xgmi::set_site_grid(bi.xs, nwg1, "wgrad1_reduce");  // the reduction workgroups take no tickets
     }
     hipLaunchKernelGGL(wgrad1_reduce_kernel<T>, dim3(nwg1 + nred), dim3(cb::NTHR), 0, cur_stream(), dptr<T>(x),
                        wslab1.data_ptr<float>(), gslab1.data_ptr<float>(), out1.data_ptr<float>(), bi, nwg1,
@@ -858,7 +863,7 @@ void conv1_wgrad_slab2(at::Tensor x, at::Tensor y1, at::Tensor dp1, at::Tensor i
     if (xc) {
       TORCH_CHECK(!lsum.has_value(), "fused SyncBN exchange: gsum must be this rank's rows (no lsum)");
       bi.xs = site_of(xc, xgmi::kSiteBwd1);
-      bi.xs.nblk = nwg1;  // the reduction workgroups take no tickets
+      xgmi::set_site_grid(bi.xs, nwg1, "conv1_wgrad_slab2");  // the reduction workgroups take no tickets
     }
     hipLaunchKernelGGL(wgrad1_slab2_kernel<T>, dim3(nwg1 + nred), dim3(cb::NTHR), 0, cur_stream(), dptr<T>(x),
                        wslab1.data_ptr<float>(), bi, nwg1, wslab2.data_ptr<float>(), rows2, N2,
@@ -931,7 +936,9 @@ bool convnet_amp_step_ok(int64_t B, int64_t n_params_granules, at::ScalarType st
            co_resident(reinterpret_cast<const void*>(&convnet_amp_step_kernel<T, false>), sh.first, cb::NTHR, 0);
     }
   });
-  return ok;
+  // with the xGMI engine both the conv1 BN site (sh.first workgroups) and the gradient
+  // site (sh.second) ride this launch: each must fit its epoch words (comm/xgmi.h)
+  return ok && xgmi::site_grid_fits(sh.first) && xgmi::site_grid_fits(sh.second);
 }
 
 // params / grads / bufs / first / lr ... sync / xc: as optim.amp_sgd_fused (one param group).
@@ -988,13 +995,13 @@ void convnet_amp_step(std::vector<at::Tensor> params, std::vector<at::Tensor> gr
                               c10::nullopt);
       if (xc) {
         bi.xs = site_of(xc, xgmi::kSiteBwd1);
-        bi.xs.nblk = nw1;
+        xgmi::set_site_grid(bi.xs, nw1, "convnet_amp_step conv1 weight gradient");
       }
       xgmi::XSite xg;
       if (xc) {
         xg = xc->grad_site();
         TORCH_CHECK(L.chunk_off[L.n] * 4 <= xg.max_vals, "convnet_amp_step: too many elements for the xGMI engine");
-        xg.nblk = grid_amp;
+        xgmi::set_site_grid(xg, grid_amp, "convnet_amp_step");
       }
       auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(nw1 + grid_amp), dim3(cb::NTHR), 0, cur_stream(), dptr<T>(x),
@@ -1017,7 +1024,10 @@ void convnet_amp_step(std::vector<at::Tensor> params, std::vector<at::Tensor> gr
 // of its workgroups poll the peers' rows) is co-resident at batch B; if not,
 // ops/convnet_fused.py all-reduces between the launches instead.
 bool sites_resident(int64_t B, at::ScalarType st) {
-  bool ok = true;
+  // every site launch must also fit its site's epoch words (comm/xgmi.h set_site_grid):
+  // the conv1 weight gradient's 7 B workgroups pass kEpochWords at B >= 74
+  bool ok = xgmi::site_grid_fits(wgrad_bn_rows(1, B)) && xgmi::site_grid_fits(wgrad_bn_rows(2, B)) &&
+            xgmi::site_grid_fits(B * kDgradSplit) && xgmi::site_grid_fits(2 * B);
   auto chk = [&](const void* k, int64_t grid) { ok = ok && co_resident(k, (int)grid, cb::NTHR, 0); };
   with_t(dt_of(at::empty({0}, at::TensorOptions().dtype(st))), [&](auto tag) {
     typedef decltype(tag) T;

@@ -365,7 +365,7 @@ void head_step(at::Tensor y2, at::Tensor fslab2, at::Tensor fstats2, at::Tensor 
   bp.train = 1;
   if (xc) {
     bp.xs = xc->site(xgmi::kSiteFwd2);
-    bp.xs.nblk = B;  // the grid (spares the kernel a hidden-argument load)
+    xgmi::set_site_grid(bp.xs, B, "convnet head");  // the grid (spares the kernel a hidden-argument load)
   }
   HeadRow hr;
   hr.target = target.data_ptr<int64_t>();

@@ -457,7 +457,7 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
   auto launch = [&](auto kern, int bg, xgmi::XSite xg) {
     const int grid = (int)std::max<int64_t>(1, (L.chunk_off[L.n] + bg - 1) / bg) + (ss.ns ? ss.s[0].nblk : 0);
     TORCH_CHECK(grid <= FUSED_MAX_BLOCKS, "fused AMP-SGD: grid exceeds the co-resident bound");
-    if (xg.active()) xg.nblk = grid;  // every workgroup takes a ticket (no hidden-argument load)
+    xgmi::set_site_grid(xg, grid, "fused AMP-SGD");  // every workgroup takes a ticket (no hidden-argument load)
     hipLaunchKernelGGL(kern, dim3(grid), dim3(FUSED_THR), 0, cur_stream(), L, scale.data_ptr<float>(),
                        tracker.data_ptr<int>(), found_inf.data_ptr<float>(),
                        reinterpret_cast<unsigned long long*>(sync.data_ptr<int64_t>()), (float)lr, (float)momentum,

@@ -54,6 +54,10 @@ class SGD(Optimizer):
         if ps and all(p.is_cuda for p in ps) and len({p.device for p in ps}) == 1:
             self._amp_sync = torch.zeros(4, dtype=torch.int64, device=ps[0].device)
             self._amp_sync_large = torch.zeros(4, dtype=torch.int64, device=ps[0].device)
+            # the deferred-wgrad1 launch's barrier state (convnet_amp_step): generation,
+            # 2 parities x 8 arrival words 64 B apart, error word; and the conv1 arrival counter
+            self._amp_sync_cas = (torch.zeros(1 + 2 * 8 * 8 + 1, dtype=torch.int64, device=ps[0].device),
+                                  torch.zeros(1, dtype=torch.int32, device=ps[0].device))
 
     def defer_slab(self, slab: torch.Tensor, out: torch.Tensor) -> None:
         """A gradient region ``out`` that is still the partial rows ``slab`` [rows][out.numel()]
@@ -226,6 +230,9 @@ class SGD(Optimizer):
         if sync is None or sync.device != params[0].device:
             # grid-barrier state of the fused kernel (allocated before any graph capture:
             # the first step runs eagerly)
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("SGD: the fused AMP step's barrier state must exist before graph capture "
+                                   "(run one eager step first)")
             sync = torch.zeros(4, dtype=torch.int64, device=params[0].device)
             setattr(self, name, sync)
         O = _load_ext().optim
@@ -247,7 +254,12 @@ class SGD(Optimizer):
             del self._pending_wgrad1
             cas = getattr(self, "_amp_sync_cas", None)
             if cas is None or cas[0].device != params[0].device:
-                # grid-barrier state: generation, 2 parities x 8 arrival words 64 B apart, error word
+                # allocated in __init__; created here only for parameters moved since, and
+                # never inside a capture (its zero-fill would become a node re-run, and the
+                # barrier generation reset, on every replay)
+                if torch.cuda.is_current_stream_capturing():
+                    raise RuntimeError("SGD: the fused AMP step's barrier state must exist before graph capture "
+                                       "(run one eager step first)")
                 cas = self._amp_sync_cas = (torch.zeros(1 + 2 * 8 * 8 + 1, dtype=torch.int64, device=params[0].device),
                                             torch.zeros(1, dtype=torch.int32, device=params[0].device))
             _load_ext().convnet.convnet_amp_step(

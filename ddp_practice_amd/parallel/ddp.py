@@ -254,7 +254,10 @@ class DistributedDataParallel(nn.Module):
         and exchanges the result with the other gradients.  The reducer is told to fail
         loudly should a bucket ever need packing.  Returns whether it was enabled."""
         d = getattr(optimizer, "_deferred_ddp", None)
-        if (d is None or d[0] is not self.reducer or not hasattr(self.module, "set_slab_sink")
+        # find_unused_parameters: a bucket holding an unused parameter is never tiled by the
+        # fused gradient buffer, so the slab's required in-place bucket could not exist
+        if (d is None or d[0] is not self.reducer or self.find_unused_parameters
+                or not hasattr(self.module, "set_slab_sink")
                 or os.environ.get("DPA_REDUCER_ZERO_COPY", "1") == "0"):
             return False
         if not self.module.set_slab_sink(optimizer):
