@@ -44,26 +44,32 @@ def prepare():
     os.environ["MASTER_PORT"] = os.environ.get("MASTER_PORT", "19198")
     from ddp_practice_amd.runtime.device import select_devices
 
-    select_devices(args.gpu)
+    if args.share_gpu:  # every rank on the first listed device, one rank per --gpu entry
+        select_devices(args.gpu.split(",")[0])
+    else:
+        select_devices(args.gpu)
     import torch
 
     world_size = torch.cuda.device_count()
+    if args.share_gpu and world_size:
+        world_size = len(args.gpu.split(","))
     if world_size == 0:
         world_size = max(1, args.cpu_procs)
     os.environ["WORLD_SIZE"] = str(world_size)
     return args
 
 
-def init_ddp(local_rank):
+def init_ddp(local_rank, args=None):
     import torch
 
     import ddp_practice_amd.distributed as dist
+    from ddp_practice_amd.cli import dist_backend, rank_device_index
 
     if torch.cuda.is_available():
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(rank_device_index(args, local_rank))
     os.environ["RANK"] = str(local_rank)
     os.environ["LOCAL_RANK"] = str(local_rank)
-    dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo", init_method="env://")
+    dist.init_process_group(backend=dist_backend(args) if torch.cuda.is_available() else "gloo", init_method="env://")
 
 
 def main(local_rank, args, env=None):
@@ -87,7 +93,7 @@ def main(local_rank, args, env=None):
         print(f"[phase pid={os.getpid()}] interpreter_start wall={ddp_practice_amd._IMPORT_WALL:.6f}",
               file=sys.stderr, flush=True)
     phase("child start")
-    init_ddp(local_rank)
+    init_ddp(local_rank, args)
     phase("init_process_group")
     run(args, distributed=True, local_rank=local_rank, generator_seed=3407 + local_rank)
 

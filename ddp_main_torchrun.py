@@ -31,7 +31,7 @@ def prepare():
     apply_env(args)
     from ddp_practice_amd.runtime.device import select_devices
 
-    select_devices(args.gpu)  # specify the GPUs to use
+    select_devices(args.gpu.split(",")[0] if args.share_gpu else args.gpu)  # specify the GPUs to use
     return args
 
 
@@ -39,13 +39,13 @@ def main(args):
     import torch
 
     import ddp_practice_amd.distributed as dist
-    from ddp_practice_amd.cli import run
+    from ddp_practice_amd.cli import dist_backend, rank_device_index, run
 
     local_rank = int(os.environ["LOCAL_RANK"])
     gpu = torch.cuda.is_available()
     if gpu:
-        torch.cuda.set_device(local_rank)
-    dist.init_process_group(backend="nccl" if gpu else "gloo")
+        torch.cuda.set_device(rank_device_index(args, local_rank))
+    dist.init_process_group(backend=dist_backend(args) if gpu else "gloo")
     run(args, distributed=True, local_rank=local_rank, generator_seed=3407 + local_rank)
 
 

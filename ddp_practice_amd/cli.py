@@ -66,12 +66,31 @@ def add_run_args(parser, amp_default: str, checkpoint: str, distributed: bool) -
         parser.add_argument("--first-bucket-mb", type=float, default=None)
         parser.add_argument("--comm", default=None, choices=["auto", "rccl", "xgmi"],
                             help="collective algorithm: auto (size-selected xGMI engine / RCCL), rccl, xgmi")
+        parser.add_argument("--share-gpu", action="store_true",
+                            help="one-GPU rehearsal of the multi-rank program: every rank on the first --gpu "
+                                 "device (ddp_main.py: one rank per --gpu entry), all-reduces and the in-kernel "
+                                 "exchanges on the xGMI engine's peer stores, host collectives on gloo")
 
 
 def apply_env(args) -> None:
     """Flags that must reach every rank before ``init_process_group`` (spawned children inherit the env)."""
     if getattr(args, "comm", None):
         os.environ["DPA_COMM"] = args.comm
+    if getattr(args, "share_gpu", False):
+        # ranks sharing one device: 3+ ranks' spinning in-kernel exchanges are not co-resident
+        # on one card, so those take one launch per collective (ops/convnet_fused.py)
+        os.environ["DPA_SHARED_GPU"] = "1"
+
+
+def rank_device_index(args, local_rank: int) -> int:
+    """The device a rank runs on: its local rank, or device 0 for every rank with --share-gpu."""
+    return 0 if getattr(args, "share_gpu", False) else local_rank
+
+
+def dist_backend(args) -> str:
+    """init_process_group backend of a GPU rank: RCCL, or -- ranks sharing one device, which
+    RCCL refuses -- the xGMI engine's rehearsal backend (parallel/comm.py init_process_group)."""
+    return "xgmi" if getattr(args, "share_gpu", False) else "nccl"
 
 
 def load_checkpoint(path: str, model, scaler=None) -> None:
@@ -218,7 +237,7 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
     if args.seed is not None:
         torch.manual_seed(args.seed)
     gpu = torch.cuda.is_available()
-    dev = torch.device("cuda", local_rank if distributed else 0) if gpu else torch.device("cpu")
+    dev = torch.device("cuda", rank_device_index(args, local_rank) if distributed else 0) if gpu else torch.device("cpu")
     rank = dist.get_rank() if distributed else 0
     world = dist.get_world_size() if distributed else 1
     comm = dist.default_comm() if distributed else None
@@ -243,13 +262,13 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
 
         if not args.no_sync_bn:
             model = convert_sync_batchnorm(model)
-        model = DistributedDataParallel(model, device_ids=[local_rank] if gpu else None,
+        model = DistributedDataParallel(model, device_ids=[dev.index] if gpu else None,
                                         bucket_cap_mb=args.bucket_cap_mb, first_bucket_mb=args.first_bucket_mb)
     elif distributed:
         if not args.no_sync_bn and gpu:  # torch's SyncBatchNorm has no CPU path
             model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
         kw = {} if args.bucket_cap_mb is None else {"bucket_cap_mb": args.bucket_cap_mb}
-        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local_rank] if gpu else None, **kw)
+        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index] if gpu else None, **kw)
     criterion = (CrossEntropyLoss() if native else torch.nn.CrossEntropyLoss()).to(dev)
     optimizer = SGD(model.parameters(), 1e-4) if native else torch.optim.SGD(model.parameters(), 1e-4)
     phase("model")
@@ -315,6 +334,9 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
                 if scaler is not None and distributed:
                     state["scaler"] = scaler.state_dict()
                 torch.save(state, args.checkpoint)
+        if distributed and os.environ.get("DPA_CHECKPOINT_EVERY_RANK") == "1":
+            # debugging / tests: every rank's own parameters (DDP keeps them bitwise equal)
+            torch.save({"model": model.state_dict()}, f"{args.checkpoint}.rank{rank}")
     finally:
         if watchdog is not None:
             watchdog.stop()

@@ -481,15 +481,15 @@ conv_fwd_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict_
 //     vmcnt(0) before each K-step's first LDS read, cdna_hip_programming.md §5);
 //   * the epilogue of the general kernel: rounded tile staged through LDS, the next
 //     BN's statistics tree, whole-row stores, accumulate / aux for the fused gradients.
-template <typename T, int BP, int BN, int NS = 2>
+template <typename T, int BP, int BN, int NS = 2, int NW = 4>
 struct G1x1Lds {
   static constexpr int STAGE = (BP + BN) * BK;            // elements per buffer
   static constexpr int RS = BN + 8;                       // epilogue tile row stride
   static constexpr int TILE = BP * RS * (int)sizeof(T);   // epilogue tile bytes
   static constexpr int RED = TILE;                        // float red[4][2][BN]
-  static constexpr int FLAG = RED + 4 * 2 * BN * 4;       // int s_flag
+  static constexpr int FLAG = RED + NW * 2 * BN * 4;      // int s_flag
   static constexpr int SCR = FLAG + 16;                   // float scr[THR]
-  static constexpr int EPI = SCR + THR * 4;
+  static constexpr int EPI = SCR + 64 * NW * 4;
   static constexpr int MAIN = NS * STAGE * (int)sizeof(T);
   static constexpr int SHIFT = MAIN > EPI ? MAIN : EPI;  // float shift[BN] (statistics only)
   static constexpr int BWC = SHIFT + BN * 4;              // float mean|invstd|gamma|beta [4][BN] (BS)
@@ -509,25 +509,37 @@ __device__ __forceinline__ void glds16(const void* src, void* dst) {
 // zero-fill; its per-lane source address can point here instead)
 __device__ __attribute__((aligned(16))) unsigned char g_zero16[16] = {0};
 
-// NS = 3 (DPA_GLDS_STAGES=3): three LDS buffers, two tiles in flight across every barrier --
+// NS = 3 | 4 (DPA_GLDS_STAGES): three or four LDS buffers, NS - 1 tiles in flight across every barrier --
 // the wait is a counted vmcnt (this wave's DMAs of the newest tile stay outstanding) and the
-// barrier a raw s_barrier (__syncthreads() would add vmcnt(0)); one workgroup per CU (96 KB).
-template <typename T, int BP, int BN, int BS = BS_NONE, bool KXK = false, int NS = 2>
-__global__ void __launch_bounds__(THR)
+// barrier a raw s_barrier (__syncthreads() would add vmcnt(0)); one workgroup per CU (96 or 128 KB).
+//
+// NWP x NWC waves (pixels x channels; default 2 x 2 = 256 threads): the wide tiles run 8
+// waves -- 256 x 128 (4 x 2) or 256 x 256 (2 x 4, wave tile 128 x 64) -- so each LDS-DMA byte
+// feeds 1.33x / 2x the MFMAs of the 128 x 128 tile (its per-K-step cost is the DMA issue:
+// profiles/r5b_stage_ab.txt, two or three tiles in flight gained nothing), and the second
+// wave on every SIMD hides the first's fragment-read waits.  The wide variants always defer
+// the statistics tree (stat_sum1_kernel / stat_tree_kernel).
+template <typename T, int BP, int BN, int BS = BS_NONE, bool KXK = false, int NS = 2, int NWP = 2, int NWC = 2>
+__global__ void __launch_bounds__(64 * NWP * NWC)
 conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__ y, StatArgs sa, Geom g,
                BwdStatArgs<T> bs) {
   using MMT = MM<T>;
-  using L = G1x1Lds<T, BP, BN, NS>;
-  static_assert(NS == 2 || (NS == 3 && BS == BS_NONE), "three stages: forward / plain data gradients only");
+  constexpr int NW = NWP * NWC, NT = 64 * NW;  // waves, threads
+  using L = G1x1Lds<T, BP, BN, NS, NW>;
+  static_assert(NS == 2 || ((NS == 3 || NS == 4) && BS == BS_NONE), "3-4 stages: forward / plain data gradients only");
+  static_assert(NW == 4 || BS == BS_NONE || BP == 128, "wide pixel tiles: forward / plain data gradients only");
   typedef typename MMT::frag frag;
-  constexpr int CT = BN / 32;  // 16-channel tiles per wave
-  constexpr int PT = BP / 32;  // 16-pixel tiles per wave
-  constexpr int AR = BP / 32;  // pixel rows per lane per K-step (8 rows per wave-instruction)
-  constexpr int WR = BN / 32;  // filter rows per lane per K-step
+  constexpr int CT = BN / (16 * NWC);  // 16-channel tiles per wave
+  constexpr int PT = BP / (16 * NWP);  // 16-pixel tiles per wave
+  constexpr int AR = BP / (8 * NW);    // pixel rows per lane per K-step (8 rows per wave-instruction)
+  constexpr int WR = BN / (8 * NW);    // filter rows per lane per K-step
+  static_assert(CT >= 1 && PT >= 1 && AR >= 1 && WR >= 1 && AR * 8 * NW == BP && WR * 8 * NW == BN, "tile / waves");
+  // the in-launch statistics tree (sum_rows) is written for 256 threads and 2 BN <= 256
+  constexpr bool kInTree = NT == THR && 2 * BN <= THR;
   __shared__ __attribute__((aligned(16))) unsigned char smem[L::BYTES];
   T* const lds = reinterpret_cast<T*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wp = wave & 1, wc = wave >> 1;
+  const int wp = wave % NWP, wc = wave / NWP;
   const int nct = g.K / BN;
   // XCD-aware order (as conv_fwd_kernel): the channel tiles of one pixel tile share an L2
   const unsigned nwg = gridDim.x, hw = blockIdx.x;
@@ -537,7 +549,7 @@ conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict
   const int bn = (int)(lid % nct);
   const long long p0 = bm * BP;
   const int k0 = bn * BN;
-  // this lane's source rows: wave-instruction i covers rows (4i + wave) * 8 .. + 7, the lane
+  // this lane's source rows: wave-instruction i covers rows (NW i + wave) * 8 .. + 7, the lane
   // row (lane >> 3) of them, logical chunk (lane & 7) ^ (row & 7) (row & 7 == lane >> 3).
   // KXK: a K-step is one filter tap (r, s) x 64 input channels (C % 64 == 0): the pixel's
   // input row is (n, oh*st - pad + r, ow*st - pad + s) and a padding tap reads the zero
@@ -548,7 +560,7 @@ conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict
   int ih0[AR], iw0[AR];
 #pragma unroll
   for (int i = 0; i < AR; ++i) {
-    long long p = p0 + (i * 4 + wave) * 8 + lr;
+    long long p = p0 + (i * NW + wave) * 8 + lr;
     p = p < g.M ? p : g.M - 1;  // ragged tail: a valid row, its output is not stored
     if constexpr (KXK) {
       const int ow = (int)(p % g.OW);
@@ -573,14 +585,14 @@ conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict
   }
   const int wrow = KXK ? g.R * g.S * g.C : g.C;
 #pragma unroll
-  for (int i = 0; i < WR; ++i) wo[i] = (unsigned)((k0 + (i * 4 + wave) * 8 + lr) * wrow + chunk * 8);
+  for (int i = 0; i < WR; ++i) wo[i] = (unsigned)((k0 + (i * NW + wave) * 8 + lr) * wrow + chunk * 8);
   const int cpt = g.C / BK;
   const int KT = KXK ? g.R * g.S * cpt : cpt;
   auto issue = [&](int kt, int buf) {
     T* base = lds + buf * L::STAGE;
 #pragma unroll
     for (int i = 0; i < WR; ++i)
-      glds16(w + wo[i] + kt * BK, base + (i * 4 + wave) * 8 * BK);
+      glds16(w + wo[i] + kt * BK, base + (i * NW + wave) * 8 * BK);
     if constexpr (KXK) {
       const int rs = kt / cpt, c0 = (kt - rs * cpt) * BK;  // wave-uniform
       const int r = rs / g.S, s = rs - r * g.S;
@@ -589,11 +601,11 @@ conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict
       for (int i = 0; i < AR; ++i) {
         const bool ok = (unsigned)(ih0[i] + r) < (unsigned)g.H && (unsigned)(iw0[i] + s) < (unsigned)g.W;
         glds16(ok ? (const void*)(x + (int)xo[i] + xk) : (const void*)g_zero16,
-               base + (BN + (i * 4 + wave) * 8) * BK);
+               base + (BN + (i * NW + wave) * 8) * BK);
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < AR; ++i) glds16(x + xo[i] + kt * BK, base + (BN + (i * 4 + wave) * 8) * BK);
+      for (int i = 0; i < AR; ++i) glds16(x + xo[i] + kt * BK, base + (BN + (i * NW + wave) * 8) * BK);
     }
   };
   f32x4 acc[CT][PT];
@@ -610,12 +622,12 @@ conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict
   // lane's epilogue chunks of x (and y, and the accumulated-onto gradient) are loaded into
   // registers now -- they land with tile 0 instead of stalling the epilogue
   constexpr int CPR = BN / 8;     // 16-B chunks per pixel row (epilogue)
-  constexpr int RPI = THR / CPR;  // pixel rows per pass
+  constexpr int RPI = NT / CPR;   // pixel rows per pass
   constexpr int NIT = BS != BS_NONE ? BP / RPI : 1;
   const int ch = tid % CPR;
   f32x4 bxr[NIT], byr[NIT], bor[NIT];
   if constexpr (BS != BS_NONE) {
-    if (lane < BN / 4 && (BS == BS_REC || wave < 2)) {
+    if (lane < BN / 4 && (BS == BS_REC ? wave < 4 : wave < 2)) {
       const float* src = wave == 0 ? bs.save + k0 : wave == 1 ? bs.save + g.K + k0 : wave == 2 ? bs.gamma + k0
                                                                                                 : bs.beta + k0;
       glds16(src + lane * 4, reinterpret_cast<float*>(smem + L::BWC) + wave * BN);
@@ -632,7 +644,8 @@ conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict
     }
   }
   issue(0, 0);
-  if (NS == 3 && KT > 1) issue(1, 1);
+  if (NS >= 3 && KT > 1) issue(1, 1);
+  if (NS == 4 && KT > 2) issue(2, 2);
   int buf = 0;
   for (int kt = 0; kt < KT; ++kt) {
     if constexpr (NS == 2) {
@@ -641,13 +654,15 @@ conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict
       __syncthreads();  // ... every wave's, and tile kt-1 (the other buffer) is no longer read
       if (kt + 1 < KT) issue(kt + 1, buf ^ 1);
     } else {
-      // tile kt landed (tile kt+1's WR + AR DMAs of this wave may still be in flight);
-      // the barrier orders every wave's DMAs of tile kt before any read, and every wave's
-      // reads of buffer (kt+2)%3 (= tile kt-1, done: its MFMAs have issued) before refill
-      if (kt + 1 < KT) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WR + AR) : "memory");
+      // tile kt landed (the WR + AR DMAs per younger tile of this wave -- up to NS - 2 of
+      // them -- may still be in flight); the barrier orders every wave's DMAs of tile kt
+      // before any read, and every wave's reads of buffer (kt-1)%NS (tile kt-1, done: its
+      // MFMAs have issued) before its refill with tile kt+NS-1
+      if (NS == 4 && kt + 2 < KT) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (WR + AR)) : "memory");
+      else if (kt + 1 < KT) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WR + AR) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (kt + 2 < KT) issue(kt + 2, buf == 0 ? 2 : buf - 1);
+      if (kt + NS - 1 < KT) issue(kt + NS - 1, buf == 0 ? NS - 1 : buf - 1);
     }
     const T* A = lds + buf * L::STAGE;  // filter rows [0, BN)
     const T* B = A + BN * BK;           // pixel rows [0, BP)
@@ -656,31 +671,38 @@ conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict
       frag fa[CT], fb[PT];
 #pragma unroll
       for (int a = 0; a < CT; ++a)
-        fa[a] = *reinterpret_cast<const frag*>(A + swz(wc * (BN / 2) + a * 16 + fr, kk * 4 + fq));
+        fa[a] = *reinterpret_cast<const frag*>(A + swz(wc * (BN / NWC) + a * 16 + fr, kk * 4 + fq));
 #pragma unroll
       for (int b = 0; b < PT; ++b)
-        fb[b] = *reinterpret_cast<const frag*>(B + swz(wp * (BP / 2) + b * 16 + fr, kk * 4 + fq));
+        fb[b] = *reinterpret_cast<const frag*>(B + swz(wp * (BP / NWP) + b * 16 + fr, kk * 4 + fq));
 #pragma unroll
       for (int a = 0; a < CT; ++a)
 #pragma unroll
         for (int b = 0; b < PT; ++b) acc[a][b] = MMT::mma(fa[a], fb[b], acc[a][b]);
     }
-    if constexpr (NS == 3) buf = buf == 2 ? 0 : buf + 1;
+    if constexpr (NS >= 3) buf = buf == NS - 1 ? 0 : buf + 1;
   }
   __syncthreads();  // the last tile is read: the buffers become the epilogue's tile
   // ---- epilogue (conv_fwd_kernel's, for a BP-pixel tile) ----
   constexpr int RS = L::RS;
   T* tile = lds;
   float(*red)[2][BN] = reinterpret_cast<float(*)[2][BN]>(smem + L::RED);
+  auto wave_sum = [&](int t) {  // column t of [2][BN] summed over the waves, in wave order
+    const int q = t / BN, c = t % BN;
+    float v = red[0][q][c];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) v += red[w][q][c];
+    return v;
+  };
   int* s_flag = reinterpret_cast<int*>(smem + L::FLAG);
   float* scr = reinterpret_cast<float*>(smem + L::SCR);
   const float* shl = reinterpret_cast<const float*>(smem + L::SHIFT);
 #pragma unroll
   for (int a = 0; a < CT; ++a) {
-    const int cl = wc * (BN / 2) + a * 16 + 4 * fq;
+    const int cl = wc * (BN / NWC) + a * 16 + 4 * fq;
 #pragma unroll
     for (int b = 0; b < PT; ++b) {
-      const int pl = wp * (BP / 2) + b * 16 + fr;
+      const int pl = wp * (BP / NWP) + b * 16 + fr;
       T v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = Cvt<T>::from_f(acc[a][b][j]);
@@ -756,7 +778,7 @@ conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict
   // Without statistics, or with the tree deferred to stat_tree_kernel, the stores leave
   // first and drain while the sums are taken from the tile still in LDS; with the
   // in-launch tree they follow the ticket (its vmcnt(0) must not wait for the tile).
-  const bool stores_first = !stats || sa.defer;
+  const bool stores_first = !stats || sa.defer || !kInTree;
   if (stores_first) store_tile();
   if constexpr (BS != BS_NONE) {  // -> level-1 row of this pixel tile (stat_tree_kernel follows)
 #pragma unroll
@@ -776,10 +798,7 @@ conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict
     __builtin_amdgcn_s_barrier();
     const long long nrows = (g.M + BP - 1) / BP;
     float* lvl1 = sa.part + (long long)bn * nrows * (2 * BN);
-    for (int t = tid; t < 2 * BN; t += THR) {
-      const int q = t / BN, c = t % BN;
-      lvl1[bm * (2 * BN) + t] = red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c];
-    }
+    for (int t = tid; t < 2 * BN; t += NT) lvl1[bm * (2 * BN) + t] = wave_sum(t);
     return;
   }
   bool last1 = false;
@@ -829,16 +848,10 @@ conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict
     rows = (g.M + BP - 1) / BP;
     NG = (int)((rows + G1 - 1) / G1);
     float* lvl1 = sa.part + (long long)bn * rows * (2 * BN);
-    if (sa.defer) {  // plain stores; the tree runs in stat_tree_kernel after this launch
-      for (int t = tid; t < 2 * BN; t += THR) {
-        const int q = t / BN, c = t % BN;
-        lvl1[bm * (2 * BN) + t] = red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c];
-      }
+    if (sa.defer || !kInTree) {  // plain stores; the tree runs in stat_tree_kernel after this launch
+      for (int t = tid; t < 2 * BN; t += NT) lvl1[bm * (2 * BN) + t] = wave_sum(t);
     } else {
-      for (int t = tid; t < 2 * BN; t += THR) {
-        const int q = t / BN, c = t % BN;
-        st_wt(lvl1 + bm * (2 * BN) + t, red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c]);
-      }
+      for (int t = tid; t < 2 * BN; t += NT) st_wt(lvl1 + bm * (2 * BN) + t, wave_sum(t));
       grp = (int)(bm / G1);
       gsz = (int)min((long long)G1, rows - (long long)grp * G1);
       last1 = last_arriver(sa.tickets + bn * NG + grp, (unsigned)gsz, s_flag);
@@ -846,21 +859,23 @@ conv_glds_kernel(const T* __restrict__ x, const T* __restrict__ w, T* __restrict
   }
   if (!stores_first) store_tile();
   if (!last1) return;
-  __syncthreads();
-  float* lvl1 = sa.part + (long long)bn * rows * (2 * BN);
-  float* lvl2 = sa.part + (long long)nct * rows * (2 * BN) + (long long)bn * NG * (2 * BN);
-  sum_rows<2 * BN>(lvl1 + (long long)grp * G1 * (2 * BN), gsz, lvl2 + (long long)grp * (2 * BN), scr, true);
-  if (!last_arriver(sa.tickets + nct * NG + bn, (unsigned)NG, s_flag)) return;
-  float* tot = &red[0][0][0];
-  sum_rows<2 * BN>(lvl2, NG, tot, scr, false);
-  for (int t = tid; t < BN; t += THR) {
-    sa.stats[k0 + t] = tot[t];
-    sa.stats[g.K + k0 + t] = tot[BN + t];
-    sa.stats[2 * g.K + SHIFT_OFF + k0 + t] = sa.shift[k0 + t];
-  }
-  if (bn == 0 && tid == 0) {
-    sa.stats[2 * g.K] = (float)g.M;
-    if (sa.nbt != nullptr) sa.nbt[0] = sa.nbt[0] + 1;
+  if constexpr (kInTree) {  // (wide tiles always defer: last1 is false there)
+    __syncthreads();
+    float* lvl1 = sa.part + (long long)bn * rows * (2 * BN);
+    float* lvl2 = sa.part + (long long)nct * rows * (2 * BN) + (long long)bn * NG * (2 * BN);
+    sum_rows<2 * BN>(lvl1 + (long long)grp * G1 * (2 * BN), gsz, lvl2 + (long long)grp * (2 * BN), scr, true);
+    if (!last_arriver(sa.tickets + nct * NG + bn, (unsigned)NG, s_flag)) return;
+    float* tot = &red[0][0][0];
+    sum_rows<2 * BN>(lvl2, NG, tot, scr, false);
+    for (int t = tid; t < BN; t += NT) {
+      sa.stats[k0 + t] = tot[t];
+      sa.stats[g.K + k0 + t] = tot[BN + t];
+      sa.stats[2 * g.K + SHIFT_OFF + k0 + t] = sa.shift[k0 + t];
+    }
+    if (bn == 0 && tid == 0) {
+      sa.stats[2 * g.K] = (float)g.M;
+      if (sa.nbt != nullptr) sa.nbt[0] = sa.nbt[0] + 1;
+    }
   }
 }
 
@@ -1167,19 +1182,23 @@ conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __re
 // One barrier per 64-pixel step: wait the landed step (vmcnt(0)) + barrier, issue step
 // t+1 into the other buffer, MFMA on step t (as conv_glds_kernel).
 
-template <typename T, int BM, int BN>
-__global__ void __launch_bounds__(THR)
+// NWM x NWN waves (default 2 x 2; 2 x 4 = 8 waves, DPA_WGRAD_WAVES=8: the second wave on
+// every SIMD hides the other's transposed-read waits, as the forward's 8-wave tiles do).
+template <typename T, int BM, int BN, int NWM = 2, int NWN = 2>
+__global__ void __launch_bounds__(64 * NWM * NWN)
 conv_wgrad_glds_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ slab, Geom g,
                        int splits, long long pps) {
   typedef typename MM<T>::frag frag;
   constexpr int BP = 64;
   constexpr int CHA = BM / 8, CHB = BN / 8;
-  constexpr int IA = CHA / 4, IB = CHB / 4;  // wave-instructions per wave per step
-  constexpr int MT = BM / 32, NT = BN / 32;
+  constexpr int NW = NWM * NWN;
+  constexpr int IA = CHA / NW, IB = CHB / NW;  // wave-instructions per wave per step
+  constexpr int MT = BM / (16 * NWM), NT = BN / (16 * NWN);
+  static_assert(IA >= 1 && IB >= 1 && IA * NW == CHA && IB * NW == CHB && MT >= 1 && NT >= 1, "tile / waves");
   constexpr int STAGE = BP * (BM + BN);
   __shared__ __attribute__((aligned(16))) T lds[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 1, wn = wave >> 1;
+  const int wm = wave % NWM, wn = wave / NWM;
   const int RSC = g.R * g.S * g.C;
   const int tm = g.K / BM, tn = RSC / BN, tiles = tm * tn;
   const unsigned nwg = gridDim.x, hw = blockIdx.x;
@@ -1199,15 +1218,15 @@ conv_wgrad_glds_kernel(const T* __restrict__ dy, const T* __restrict__ x, float*
     const long long pbase = pa + (long long)t * BP;
 #pragma unroll
     for (int i = 0; i < IA; ++i) {
-      const int row = (i * 4 + wave) * (64 / CHA) + ra;
+      const int row = (i * NW + wave) * (64 / CHA) + ra;
       const int ck = (lane % CHA) ^ wswz_xor<CHA>(row);
       const long long p = pbase + row;
       const void* src = p < pb ? (const void*)(dy + p * g.K + k0 + ck * 8) : (const void*)g_zero16;
-      glds16(src, A + (i * 4 + wave) * (64 / CHA) * BM);
+      glds16(src, A + (i * NW + wave) * (64 / CHA) * BM);
     }
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
-      const int row = (i * 4 + wave) * (64 / CHB) + rb;
+      const int row = (i * NW + wave) * (64 / CHB) + rb;
       const int ck = (lane % CHB) ^ wswz_xor<CHB>(row);
       const long long p = pbase + row;
       const void* src = g_zero16;
@@ -1224,7 +1243,7 @@ conv_wgrad_glds_kernel(const T* __restrict__ dy, const T* __restrict__ x, float*
             src = x + (((long long)n * g.H + ih) * g.W + iw) * g.C + c0 + ck * 8;
         }
       }
-      glds16(src, B + (i * 4 + wave) * (64 / CHB) * BN);
+      glds16(src, B + (i * NW + wave) * (64 / CHB) * BN);
     }
   };
   const int grp = lane >> 4, gi = lane & 15, q = gi >> 2, pq = gi & 3;
@@ -1257,10 +1276,10 @@ conv_wgrad_glds_kernel(const T* __restrict__ dy, const T* __restrict__ x, float*
       frag fa[MT], fb[NT];
 #pragma unroll
       for (int a = 0; a < MT; ++a)
-        fa[a] = trfrag(A, kk, wm * (BM / 2) + a * 16, std::integral_constant<int, CHA>{});
+        fa[a] = trfrag(A, kk, wm * (BM / NWM) + a * 16, std::integral_constant<int, CHA>{});
 #pragma unroll
       for (int b = 0; b < NT; ++b)
-        fb[b] = trfrag(B, kk, wn * (BN / 2) + b * 16, std::integral_constant<int, CHB>{});
+        fb[b] = trfrag(B, kk, wn * (BN / NWN) + b * 16, std::integral_constant<int, CHB>{});
 #pragma unroll
       for (int a = 0; a < MT; ++a)
 #pragma unroll
@@ -1274,7 +1293,7 @@ conv_wgrad_glds_kernel(const T* __restrict__ dy, const T* __restrict__ x, float*
     for (int b = 0; b < NT; ++b)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int m = k0 + wm * (BM / 2) + a * 16 + 4 * grp + j, n = n0 + wn * (BN / 2) + b * 16 + gi;
+        const int m = k0 + wm * (BM / NWM) + a * 16 + 4 * grp + j, n = n0 + wn * (BN / NWN) + b * 16 + gi;
         out[(long long)m * RSC + n] = acc[a][b][j];
       }
 }
@@ -1322,6 +1341,74 @@ wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ grad, in
     const int c = (int)(n % C), rs = (int)(n / C), r = rs / S, s = rs - r * S;
     if (r < Rd && s < Sd) {
       float* o = grad + (((long long)k * Cd + c) * Rd + r) * Sd + s;
+      const int st = Rd * Sd;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (c + j < Cd) o[j * st] = t[j];
+    }
+  }
+}
+
+// The same reduction for a whole backward pass's weight gradients in ONE launch
+// (ops/conv_igemm.WgradBatch): every conv left its split partials in a slab of its own, and
+// at the end of the backward one grid covers all of them -- instead of one small, tail-bound
+// launch per conv (53 launches, ~9 us each on ResNet-50: profiles/r5a_rn_steady.txt).  The
+// entries ride in the kernel arguments by value (graph-capturable, no table upload); a
+// workgroup finds its entry by its block index (prefix blk0).  Same per-block association
+// as wgrad_reduce_kernel: bitwise the same gradients.
+constexpr int WB_MAX = 48;
+struct WBEntry {
+  const float* slab;
+  float* grad;
+  int splits, K, C, R, S, Cd, Rd, Sd;
+  long long blk0;  // first block of this entry
+};
+struct WBList {
+  int n;
+  WBEntry e[WB_MAX];
+};
+
+__global__ void __launch_bounds__(256) wgrad_reduce_batch_kernel(WBList L) {
+  constexpr int QC = WR_QC, SG = 256 / WR_QC;
+  __shared__ f32x4 part[SG][QC];
+  const long long b = blockIdx.x;
+  int lo = 0, hi = L.n - 1;  // the entry holding block b
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (L.e[mid].blk0 <= b) lo = mid; else hi = mid - 1;
+  }
+  const WBEntry& E = L.e[lo];
+  const float* __restrict__ slab = E.slab;
+  const int splits = E.splits, C = E.C, S = E.S, Cd = E.Cd, Rd = E.Rd, Sd = E.Sd;
+  const long long RSC = (long long)E.R * S * C, total = (long long)E.K * RSC;
+  const int qd = threadIdx.x % QC, rg = threadIdx.x / QC;
+  const long long col = ((b - E.blk0) * QC + qd) * 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (col < total) {
+    int sp = rg;
+    for (; sp + 3 * SG < splits; sp += 4 * SG) {
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(slab + (long long)sp * total + col);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(slab + (long long)(sp + SG) * total + col);
+      const f32x4 v2 = *reinterpret_cast<const f32x4*>(slab + (long long)(sp + 2 * SG) * total + col);
+      const f32x4 v3 = *reinterpret_cast<const f32x4*>(slab + (long long)(sp + 3 * SG) * total + col);
+      acc += v0;
+      acc += v1;
+      acc += v2;
+      acc += v3;
+    }
+    for (; sp < splits; sp += SG) acc += *reinterpret_cast<const f32x4*>(slab + (long long)sp * total + col);
+  }
+  part[rg][qd] = acc;
+  __syncthreads();
+  if (rg == 0 && col < total) {
+    f32x4 t = part[0][qd];
+#pragma unroll
+    for (int gg = 1; gg < SG; ++gg) t += part[gg][qd];
+    const int k = (int)(col / RSC);
+    const long long n = col - (long long)k * RSC;
+    const int c = (int)(n % C), rs = (int)(n / C), r = rs / S, s_ = rs - r * S;
+    if (r < Rd && s_ < Sd) {
+      float* o = E.grad + (((long long)k * Cd + c) * Rd + r) * Sd + s_;
       const int st = Rd * Sd;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -1485,14 +1572,14 @@ static int g_glds_stages = -1;
 static int glds_stages() {
   if (g_glds_stages < 0) {
     const char* e = std::getenv("DPA_GLDS_STAGES");
-    g_glds_stages = e != nullptr && std::atoi(e) == 3 ? 3 : 2;
+    g_glds_stages = e != nullptr && (std::atoi(e) == 3 || std::atoi(e) == 4) ? std::atoi(e) : 2;
   }
   return g_glds_stages;
 }
 int64_t glds_config(int64_t stages) {
   glds_stages();
   const int64_t prev = g_glds_stages;
-  if (stages == 2 || stages == 3) g_glds_stages = (int)stages;
+  if (stages >= 2 && stages <= 4) g_glds_stages = (int)stages;
   return prev;
 }
 
@@ -1529,6 +1616,43 @@ int64_t g3x3_config(int64_t on) {
   return prev;
 }
 
+// Wide 8-wave tiles of conv_glds_kernel for the forward / plain data-gradient convs
+// (DPA_WIDE; wide_config at run time): 0 off, 1 auto (see wide_pick), 2 force 256 x 128,
+// 3 force 256 x 256, 4 force 128 x 128 on 8 waves.  Shapes a forced tile does not fit keep
+// the 4-wave kernel.
+static int g_wide = -1;
+static int wide_mode() {
+  if (g_wide < 0) {
+    const char* e = std::getenv("DPA_WIDE");
+    g_wide = e != nullptr ? std::atoi(e) : 1;
+  }
+  return g_wide;
+}
+int64_t wide_config(int64_t m) {
+  wide_mode();
+  const int64_t prev = g_wide;
+  if (m >= 0) g_wide = (int)m;
+  return prev;
+}
+// -> 0 (the 4-wave 128 x 128 / x 64 tiles), 1 (256 x 128), 2 (256 x 256), 3 (128 x 128, 8 waves).
+// Auto (profiles/r5c_wide_ab.txt, every ResNet-50 forward shape): 8 waves on the 128 x 128
+// tile wherever Cout % 128 == 0 (the second wave on each SIMD hides the other's fragment-read
+// waits: network forward convs 2459 -> 2380 us); 256 x 256 where the reduction is deep
+// (C R S >= 1024) and the grid still fills the chip (>= 196 workgroups: 40.5 vs 42.9-44.3 us
+// on 1024 -> 512 at 14x14).  bs: BN backward sums in the epilogue (128-pixel tiles only).
+static int wide_pick(long long M, int64_t K, int64_t CRS, bool bs) {
+  const int m = wide_mode();
+  const long long r256 = (M + 255) / 256;
+  const bool ok2 = !bs && K % 256 == 0 && r256 <= S1_MAXROWS;  // the deferred tree: one level at BN = 256
+  const bool ok1 = K % 128 == 0;
+  if (m == 2) return ok1 && !bs ? 1 : 0;
+  if (m == 3) return ok2 ? 2 : 0;
+  if (m == 4) return ok1 ? 3 : 0;
+  if (m != 1) return 0;
+  if (ok2 && CRS >= 1024 && r256 * (K / 256) >= 196) return 2;
+  return ok1 ? 3 : 0;
+}
+
 // pixel tile of conv_glds_kernel: 256 when the grid still has >= min256 workgroups (default
 // 2 per CU: the 96 KB of LDS leave one 256-pixel workgroup per CU), else 128 (64 KB: two
 // per CU); DPA_G1X1_BP=128|256 forces one.
@@ -1563,15 +1687,18 @@ static void launch_stat_tree(StatArgs sa, long long M, int bm, int K, int BN) {
     const dim3 gr((unsigned)(K / BN), (unsigned)(2 * BN / S1_COLS)), th(S1_THR);
     xgmi::set_site_grid(sa.xs, (long long)gr.x * gr.y, "stat_sum1");  // SyncBN finishers: every workgroup
     if (rows <= 16 * S1_RG) {
-      if (BN == 128) hipLaunchKernelGGL((stat_sum1_kernel<128, 16>), gr, th, 0, cur_stream(), sa, M, bm, K);
+      if (BN == 256) hipLaunchKernelGGL((stat_sum1_kernel<256, 16>), gr, th, 0, cur_stream(), sa, M, bm, K);
+      else if (BN == 128) hipLaunchKernelGGL((stat_sum1_kernel<128, 16>), gr, th, 0, cur_stream(), sa, M, bm, K);
       else hipLaunchKernelGGL((stat_sum1_kernel<64, 16>), gr, th, 0, cur_stream(), sa, M, bm, K);
     } else {
-      if (BN == 128) hipLaunchKernelGGL((stat_sum1_kernel<128, S1_MAXROWS / S1_RG>), gr, th, 0, cur_stream(), sa, M, bm, K);
+      if (BN == 256) hipLaunchKernelGGL((stat_sum1_kernel<256, S1_MAXROWS / S1_RG>), gr, th, 0, cur_stream(), sa, M, bm, K);
+      else if (BN == 128) hipLaunchKernelGGL((stat_sum1_kernel<128, S1_MAXROWS / S1_RG>), gr, th, 0, cur_stream(), sa, M, bm, K);
       else hipLaunchKernelGGL((stat_sum1_kernel<64, S1_MAXROWS / S1_RG>), gr, th, 0, cur_stream(), sa, M, bm, K);
     }
     DPA_CHECK_LAUNCH();
     return;
   }
+  TORCH_CHECK(BN <= 128, "stat_tree: 256-channel tiles need <= ", S1_MAXROWS, " pixel tiles");
   const dim3 gr((unsigned)(NG * (K / BN))), th(THR);
   xgmi::set_site_grid(sa.xs, K / BN, "stat_tree");  // SyncBN finishers: the last arriver of each channel tile
   if (BN == 128) hipLaunchKernelGGL(stat_tree_kernel<128>, gr, th, 0, cur_stream(), sa, M, bm, K);
@@ -1716,11 +1843,16 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
       (g3x3_enabled() || (g.R == 1 && g.S == 1 && g.pad == 0))) {
     // the glds-staged implicit-GEMM kernel (pixel tile 256 or 128, see g1x1_bp; 64-channel
     // tiles when 128-channel ones leave the grid below g_bn64_below workgroups)
-    const int BP = (bwdst || !(g.R == 1 && g.S == 1 && g.pad == 0)) ? 128 : g1x1_bp(g.M, g.K);
-    const int BN = BN0 == 128 && BP == 128 && (g.M + 127) / 128 * (g.K / 128) < bn64_below() ? 64 : BN0;
+    const int wide = wide_pick(g.M, g.K, (int64_t)g.C * g.R * g.S, bwdst);
+    int BP = (bwdst || !(g.R == 1 && g.S == 1 && g.pad == 0)) ? 128 : g1x1_bp(g.M, g.K);
+    int BN = BN0 == 128 && BP == 128 && (g.M + 127) / 128 * (g.K / 128) < bn64_below() ? 64 : BN0;
+    if (wide == 1 || wide == 2) BP = 256;
+    if (wide == 1 || wide == 3) BN = 128;
+    if (wide == 2) BN = 256;
+    if (wide == 3) BP = 128;
     const long long blocks = (g.M + BP - 1) / BP * (g.K / BN);
     TORCH_CHECK(blocks < (1LL << 31), "conv_fwd: grid too large");
-    sa.defer = st && (defer_stats(blocks) || xc) ? 1 : 0;
+    sa.defer = st && (defer_stats(blocks) || xc || wide) ? 1 : 0;
     if (bwdst) {  // the BN backward sums: level-1 rows in the conv, the tree after it
       sa.part = part->data_ptr<float>();
       sa.tickets = reinterpret_cast<unsigned*>(tickets->data_ptr<int>());
@@ -1743,25 +1875,48 @@ void conv_fwd(at::Tensor x, at::Tensor w, at::Tensor y, int64_t stride, int64_t 
         bs.save = bn_save->data_ptr<float>();
         bs.gamma = bn_gamma.has_value() ? bn_gamma->data_ptr<float>() : nullptr;
         bs.beta = bn_beta.has_value() ? bn_beta->data_ptr<float>() : nullptr;
+        const dim3 t8(512);
         if (!(g.R == 1 && g.S == 1 && g.pad == 0)) {  // KxK data gradient (recomputed ReLU mask)
           TORCH_CHECK(!bn_y.has_value(), "conv_fwd: KxK BN sums take the recomputed mask");
-          if (BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_REC, true>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+          if (wide == 3) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_REC, true, 2, 2, 4>), gr, t8, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+          else if (BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_REC, true>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
           else hipLaunchKernelGGL((conv_glds_kernel<T, 128, 64, BS_REC, true>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
         } else if (bn_y.has_value()) {
-          if (BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_Y>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+          // BS_Y stays on 4 waves unless forced (DPA_WIDE=4): its epilogue prefetches three
+          // operand rows, and 8 waves measured +218 us over the network's 12 launches
+          // (profiles/r5d_resnet50_steady_wide.txt)
+          if (wide == 3 && wide_mode() == 4) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_Y, false, 2, 2, 4>), gr, t8, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+          else if (BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_Y>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
           else hipLaunchKernelGGL((conv_glds_kernel<T, 128, 64, BS_Y>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
         } else {
-          if (BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_REC>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+          if (wide == 3) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_REC, false, 2, 2, 4>), gr, t8, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+          else if (BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_REC>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
           else hipLaunchKernelGGL((conv_glds_kernel<T, 128, 64, BS_REC>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
         }
         return;
       }
       const bool kxk = !(g.R == 1 && g.S == 1 && g.pad == 0);
+      if (wide) {  // 8 waves
+        if (wide == 1 && kxk) hipLaunchKernelGGL((conv_glds_kernel<T, 256, 128, BS_NONE, true, 2, 4, 2>), gr, dim3(512), 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        else if (wide == 1) hipLaunchKernelGGL((conv_glds_kernel<T, 256, 128, BS_NONE, false, 2, 4, 2>), gr, dim3(512), 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        else if (wide == 2 && kxk) hipLaunchKernelGGL((conv_glds_kernel<T, 256, 256, BS_NONE, true, 2, 2, 4>), gr, dim3(512), 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        else if (wide == 2) hipLaunchKernelGGL((conv_glds_kernel<T, 256, 256, BS_NONE, false, 2, 2, 4>), gr, dim3(512), 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        else if (kxk) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_NONE, true, 2, 2, 4>), gr, dim3(512), 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        else hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_NONE, false, 2, 2, 4>), gr, dim3(512), 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        return;
+      }
       if (glds_stages() == 3 && BP == 128) {  // three LDS buffers (one workgroup per CU)
         if (kxk && BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_NONE, true, 3>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
         else if (kxk) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 64, BS_NONE, true, 3>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
         else if (BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_NONE, false, 3>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
         else hipLaunchKernelGGL((conv_glds_kernel<T, 128, 64, BS_NONE, false, 3>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        return;
+      }
+      if (glds_stages() == 4 && BP == 128) {  // four LDS buffers (three tiles in flight)
+        if (kxk && BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_NONE, true, 4>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        else if (kxk) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 64, BS_NONE, true, 4>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        else if (BN == 128) hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, BS_NONE, false, 4>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
+        else hipLaunchKernelGGL((conv_glds_kernel<T, 128, 64, BS_NONE, false, 4>), gr, th, 0, cur_stream(), xp, wp, yp, sa, g, bs);
         return;
       }
       if (kxk) {  // KxK: tap-walking loader (128-pixel tiles)
@@ -1813,7 +1968,9 @@ static int g_wgrad_glds = -1;
 static int wgrad_glds() {
   if (g_wgrad_glds < 0) {
     const char* e = std::getenv("DPA_WGRAD_GLDS");
-    g_wgrad_glds = e == nullptr ? 1 : std::atoi(e);
+    // 2 (every MODE_GEN conv, 3x3 included, with 8-wave workgroups): network wgrad 2600 vs
+    // 2668 us (1x1 only) vs 2760 (4 waves): profiles/r5d_wgrad_ab.txt
+    g_wgrad_glds = e == nullptr ? 2 : std::atoi(e);
   }
   return g_wgrad_glds;
 }
@@ -1821,6 +1978,21 @@ int64_t wgrad_config(int64_t glds) {
   wgrad_glds();
   const int64_t prev = g_wgrad_glds;
   if (glds >= 0) g_wgrad_glds = (int)glds;
+  return prev;
+}
+// waves per workgroup of conv_wgrad_glds_kernel: 8 (default) or 4 (DPA_WGRAD_WAVES; wgrad_waves_config)
+static int g_wgrad_waves = -1;
+static int wgrad_waves() {
+  if (g_wgrad_waves < 0) {
+    const char* e = std::getenv("DPA_WGRAD_WAVES");
+    g_wgrad_waves = e != nullptr && std::atoi(e) == 4 ? 4 : 8;  // 8: network wgrad 2668 vs 2760 us
+  }
+  return g_wgrad_waves;
+}
+int64_t wgrad_waves_config(int64_t w) {
+  wgrad_waves();
+  const int64_t prev = g_wgrad_waves;
+  if (w == 4 || w == 8) g_wgrad_waves = (int)w;
   return prev;
 }
 
@@ -1848,8 +2020,8 @@ int64_t wgrad_splits(int64_t M, int64_t K, int64_t C, int64_t R, int64_t S) {
 // dy: [N, K, OH, OW] channels_last; x: [N, C, H, W] channels_last; grad: fp32 [K, C, R, S]
 // contiguous (written, not accumulated); slab: fp32 >= splits * K * R*S*C.
 // mode MODE_STEM: x = the stem_pack image [N, 4, H, W], grad [K, 3, 7, 7] (stride 2, pad 3).
-void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor grad, int64_t stride, int64_t pad, at::Tensor slab,
-                int64_t mode) {
+std::vector<int64_t> conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor grad, int64_t stride, int64_t pad,
+                                at::Tensor slab, int64_t mode, bool reduce) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && grad.is_cuda() && slab.is_cuda(), "conv_wgrad: device tensors");
   TORCH_CHECK(dy.scalar_type() == x.scalar_type() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf),
               "conv_wgrad: bf16 / f16 activations");
@@ -1885,6 +2057,14 @@ void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor grad, int64_t stride, in
     const dim3 gr((unsigned)blocks), th(THR);
     // 1x1 (mode 1, default) or every MODE_GEN conv (mode 2): on 3x3 it measured ~5 % slower
     if (!stem && ((g.R == 1 && g.S == 1 && wgrad_glds() >= 1) || wgrad_glds() == 2)) {
+      if (wgrad_waves() == 8) {
+        const dim3 t8(512);
+        if (BM == 128 && BN == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 128, 128, 2, 4>), gr, t8, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+        else if (BM == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 128, 64, 4, 2>), gr, t8, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+        else if (BN == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 64, 128, 2, 4>), gr, t8, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+        else hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 64, 64, 2, 4>), gr, t8, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+        return;
+      }
       if (BM == 128 && BN == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 128, 128>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
       else if (BM == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 128, 64>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
       else if (BN == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 64, 128>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
@@ -1900,11 +2080,47 @@ void conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor grad, int64_t stride, in
   };
   if (x.scalar_type() == at::kBFloat16) launch(__hip_bfloat16{}); else launch(__half{});
   DPA_CHECK_LAUNCH();
+  // reduce = false: the slab stays for wgrad_reduce_batch (the geometry below is its entry)
+  std::vector<int64_t> geo{sp, g.K, g.C, SR, SS, Cd, Rd, Sd};
+  if (!reduce) return geo;
   const long long total = (long long)g.K * RSC;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + 4 * WR_QC - 1) / (4 * WR_QC))), dim3(256), 0,
                      cur_stream(),
                      slab.data_ptr<float>(), grad.data_ptr<float>(), (int)sp, g.K, g.C, SR, SS, Cd, Rd, Sd);
   DPA_CHECK_LAUNCH();
+  return geo;
+}
+
+// One launch reducing every (slab, grad) pair of a backward pass (conv_wgrad with reduce =
+// false; geo = the geometry it returned), WB_MAX entries per launch.
+void wgrad_reduce_batch(std::vector<at::Tensor> slabs, std::vector<at::Tensor> grads,
+                        std::vector<std::vector<int64_t>> geos) {
+  TORCH_CHECK(slabs.size() == grads.size() && slabs.size() == geos.size(), "wgrad_reduce_batch: one geometry per pair");
+  for (size_t s0 = 0; s0 < slabs.size(); s0 += WB_MAX) {
+    WBList L{};
+    long long blk = 0;
+    const size_t e = std::min(slabs.size(), s0 + (size_t)WB_MAX);
+    for (size_t i = s0; i < e; ++i) {
+      const auto& q = geos[i];
+      TORCH_CHECK(q.size() == 8, "wgrad_reduce_batch: geometry {splits, K, C, R, S, Cd, Rd, Sd}");
+      const long long total = q[1] * q[3] * q[4] * q[2];
+      TORCH_CHECK(slabs[i].is_cuda() && slabs[i].scalar_type() == at::kFloat && slabs[i].numel() >= q[0] * total,
+                  "wgrad_reduce_batch: slab");
+      TORCH_CHECK(grads[i].is_cuda() && grads[i].scalar_type() == at::kFloat && grads[i].is_contiguous() &&
+                      grads[i].numel() == q[1] * q[5] * q[6] * q[7], "wgrad_reduce_batch: fp32 OIHW grad");
+      WBEntry& E = L.e[i - s0];
+      E.slab = slabs[i].data_ptr<float>();
+      E.grad = grads[i].data_ptr<float>();
+      E.splits = (int)q[0]; E.K = (int)q[1]; E.C = (int)q[2]; E.R = (int)q[3]; E.S = (int)q[4];
+      E.Cd = (int)q[5]; E.Rd = (int)q[6]; E.Sd = (int)q[7];
+      E.blk0 = blk;
+      blk += (total + 4 * WR_QC - 1) / (4 * WR_QC);
+    }
+    L.n = (int)(e - s0);
+    if (blk == 0) continue;
+    hipLaunchKernelGGL(wgrad_reduce_batch_kernel, dim3((unsigned)blk), dim3(256), 0, cur_stream(), L);
+    DPA_CHECK_LAUNCH();
+  }
 }
 
 }  // namespace igemm
@@ -1925,7 +2141,10 @@ void register_conv_igemm(pybind11::module& m) {
   s.def("stat_part_len", &igemm::stat_part_len);
   s.def("stat_tickets_len", &igemm::stat_tickets_len);
   s.def("conv_wgrad", &igemm::conv_wgrad, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("grad"),
-        pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("slab"), pybind11::arg("mode") = 0);
+        pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("slab"), pybind11::arg("mode") = 0,
+        pybind11::arg("reduce") = true);
+  s.def("wgrad_reduce_batch", &igemm::wgrad_reduce_batch);
+  s.def("wgrad_waves_config", &igemm::wgrad_waves_config, pybind11::arg("waves") = -1);
   s.def("stem_pack", &igemm::stem_pack);
   s.attr("MODE_STEM") = igemm::MODE_STEM;
   s.attr("MODE_S2T") = igemm::MODE_S2T;
@@ -1934,6 +2153,7 @@ void register_conv_igemm(pybind11::module& m) {
   s.def("wgrad_config", &igemm::wgrad_config, pybind11::arg("glds") = -1);
   s.def("g3x3_config", &igemm::g3x3_config, pybind11::arg("on") = -1);
   s.def("glds_config", &igemm::glds_config, pybind11::arg("stages") = -1);
+  s.def("wide_config", &igemm::wide_config, pybind11::arg("mode") = -1);
   s.def("bn64_config", &igemm::bn64_config, pybind11::arg("below") = -1);
   s.def("stat_defer_config", &igemm::stat_defer_config, pybind11::arg("min_blocks") = -2);
   s.def("g1x1_config", &igemm::g1x1_config, pybind11::arg("on") = -1, pybind11::arg("bp") = -1,

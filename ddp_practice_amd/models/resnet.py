@@ -73,6 +73,19 @@ def _conv(x: torch.Tensor, conv: nn.Conv2d, cdtype: torch.dtype, bn: nn.Module |
             out.contiguous(memory_format=torch.channels_last)), None
 
 
+def _multi_rank() -> bool:
+    import torch.distributed as tdist
+
+    from .. import distributed as ddist
+
+    if tdist.is_available() and tdist.is_initialized() and tdist.get_world_size() > 1:
+        return True
+    try:
+        return ddist.is_initialized() and ddist.get_world_size() > 1
+    except Exception:  # noqa: BLE001 -- no facade state: a single process
+        return False
+
+
 def _comm_of(bn: nn.Module):
     from ..ops.bn_nhwc import bn_comm  # the same lookup the statistics-producing convs use
 
@@ -201,6 +214,10 @@ class ResNet(nn.Module):
 
         cdtype = compute_dtype(x) if self.amp_dtype is not None else torch.float32
         _PACKS.clear()
+        # the weight-gradient reductions of this step's backward in one launch, unless a DDP
+        # reducer (or a peer rank) may read gradients while the backward still runs
+        _igemm.WgradBatch.active = (torch.is_grad_enabled() and not getattr(self, "_dpa_ddp_wrapped", False)
+                                    and not _multi_rank())
         if _igemm.ENABLED and cdtype in (torch.bfloat16, torch.float16):
             # every implicit-GEMM conv's filters for this step in one launch (with the flipped
             # transpose where the data gradient runs on the kernels: every 3x3, and the 1x1

@@ -92,6 +92,7 @@ class Conv1x1Fn(torch.autograd.Function):
         ctx.tap = tap
         ctx.xtap = xtap
         ctx.wshape = weight.shape
+        ctx.wparam = weight  # the leaf parameter (ops/conv_igemm.WgradBatch)
         C = x.shape[1]
         # packed: this step's compute-dtype filter (and its transpose) from ops/conv_igemm.WeightPack
         w = packed[0].view(weight.shape[0], C) if packed is not None else weight.reshape(weight.shape[0], C).to(cdtype)
@@ -171,11 +172,12 @@ class Conv1x1Fn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             if ctx.lazy_rows and _igemm.usable(dyc, w.view(ctx.wshape), w.dtype):
                 # implicit-GEMM weight gradient over the (strided) input pixels, fp32 out
-                dw = _igemm.conv_wgrad(dyc, saved, tuple(ctx.wshape), stride, 0)
+                dw = _igemm.conv_wgrad(dyc, saved, tuple(ctx.wshape), stride, 0, ctx.wparam)
             else:
                 # saved: the [P, C] rows, or (lazy) the unstrided input
                 rows = _rows(saved[:, :, ::stride, ::stride] if stride != 1 else saved) if ctx.lazy_rows else saved
                 dw = _wgrad(dyr, rows).view(ctx.wshape)
+        ctx.wparam = None
         return dx, dw, None, None, None, None, None, None, None
 
     @staticmethod

@@ -167,6 +167,7 @@ class StemConvFn(torch.autograd.Function):
         y, stats = conv_fwd(x4, w4, 2, 3, bn, mode=_K().MODE_STEM)
         ctx.save_for_backward(x4)
         ctx.wshape = tuple(weight.shape)
+        ctx.wparam = weight  # the leaf parameter (WgradBatch: is its .grad still unset?)
         ctx.set_materialize_grads(False)
         if stats is not None:
             ctx.mark_non_differentiable(stats)
@@ -182,15 +183,70 @@ class StemConvFn(torch.autograd.Function):
         K = ctx.wshape[0]
         N, _, OH, OW = dy.shape
         sp = int(_K().wgrad_splits(N * OH * OW, K, 4, 8, 8))
-        slab = _WgradWS.get(dy.device, sp * K * 256)
         grad = torch.empty(ctx.wshape, dtype=torch.float32, device=dy.device)
-        _K().conv_wgrad(dy, x4, grad, 2, 3, slab, mode=_K().MODE_STEM)
+        if WgradBatch.wants(ctx.wparam):
+            slab = torch.empty(sp * K * 256, dtype=torch.float32, device=dy.device)
+            WgradBatch.add(slab, grad, ctx.wparam,
+                           _K().conv_wgrad(dy, x4, grad, 2, 3, slab, mode=_K().MODE_STEM, reduce=False))
+        else:
+            slab = _WgradWS.get(dy.device, sp * K * 256)
+            _K().conv_wgrad(dy, x4, grad, 2, 3, slab, mode=_K().MODE_STEM)
+        ctx.wparam = None
         return None, grad, None, None
 
 
 def stem_conv(x: torch.Tensor, conv, cdtype: torch.dtype, bn=None):
     """(output channels_last in ``cdtype``, statistics of ``bn`` or None)."""
     return StemConvFn.apply(x, conv.weight, cdtype, bn if (bn is not None and bn.training) else None)
+
+
+class WgradBatch:
+    """Weight-gradient split-K reductions of a whole backward pass in ONE launch.
+
+    Each implicit-GEMM weight gradient writes fp32 partial tiles (one per pixel split) that
+    a reduction folds into the OIHW ``.grad``: 53 small launches per ResNet-50 step, ~9 us
+    each, tail-bound (profiles/r5a_rn_steady.txt).  While ``active`` (set by the native
+    ResNet-50 forward when no DDP reducer or peer rank can read the gradients mid-backward),
+    a conv whose weight has no ``.grad`` yet (autograd then adopts the returned tensor
+    without reading it) keeps its partials in a slab of its own and the reductions of the
+    whole pass run in one launch from an end-of-backward callback (csrc/kernels/
+    conv_igemm.hip wgrad_reduce_batch: the same association, bitwise the same gradients),
+    before ``backward()`` returns.
+
+    Opt-in (DPA_WGRAD_BATCH=1): measured slower on ResNet-50 (14.63 vs 14.52-14.56 ms/step,
+    profiles/r5d_*): the reductions are bound by the ~1 GB of fp32 partials they re-read,
+    not by launch count, and batched at the end of the backward those partials have left
+    the 256 MB MALL that the per-conv reduction reads them from."""
+
+    enabled = os.environ.get("DPA_WGRAD_BATCH", "0") == "1"
+    active = False
+    _pending: list = []
+
+    @classmethod
+    def wants(cls, wparam) -> bool:
+        return cls.enabled and cls.active and wparam is not None and wparam.grad is None
+
+    @classmethod
+    def add(cls, slab: torch.Tensor, grad: torch.Tensor, wparam, geo) -> None:
+        # no reference to ``grad`` is kept: autograd adopts a gradient tensor as ``.grad``
+        # only while nothing else holds it (otherwise it clones it -- reading it now); the
+        # flush finds it again as ``wparam.grad`` and checks it is the same memory
+        cls._pending.append((slab, grad.data_ptr(), wparam, list(geo)))
+        # one callback per deferral (the first flushes them all): a backward that raised
+        # part-way leaves no stale "already queued" state behind
+        torch.autograd.Variable._execution_engine.queue_callback(cls.flush)
+
+    @classmethod
+    def flush(cls) -> None:
+        if not cls._pending:
+            return
+        p, cls._pending = cls._pending, []
+        grads = [w.grad for _, _, w, _ in p]
+        for (_, ptr, w, _), g in zip(p, grads):
+            if g is None or g.data_ptr() != ptr:
+                raise RuntimeError("WgradBatch: a deferred weight gradient was not adopted as .grad (a hook or "
+                                   "accumulation read it before its reduction); set DPA_WGRAD_BATCH=0")
+        _K().wgrad_reduce_batch([a for a, _, _, _ in p], grads, [c for _, _, _, c in p])
 
 
 class _WgradWS:
@@ -204,14 +260,19 @@ class _WgradWS:
         return ws
 
 
-def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, wshape, stride: int, pad: int) -> torch.Tensor:
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, wshape, stride: int, pad: int, wparam=None) -> torch.Tensor:
     """fp32 OIHW weight gradient of a conv on the implicit-GEMM kernel (pixel-split
-    partials reduced straight into the OIHW layout); dy, x channels_last."""
+    partials reduced straight into the OIHW layout); dy, x channels_last.  ``wparam``: the
+    weight parameter (the reduction may then join the pass's batch, :class:`WgradBatch`)."""
     K, C, R, S = wshape
     N, _, OH, OW = dy.shape
     sp = int(_K().wgrad_splits(N * OH * OW, K, C, R, S))
-    slab = _WgradWS.get(dy.device, sp * K * C * R * S)
     grad = torch.empty(wshape, dtype=torch.float32, device=dy.device)
+    if WgradBatch.wants(wparam):
+        slab = torch.empty(sp * K * C * R * S, dtype=torch.float32, device=dy.device)
+        WgradBatch.add(slab, grad, wparam, _K().conv_wgrad(dy, x, grad, stride, pad, slab, reduce=False))
+        return grad
+    slab = _WgradWS.get(dy.device, sp * K * C * R * S)
     _K().conv_wgrad(dy, x, grad, stride, pad, slab)
     return grad
 

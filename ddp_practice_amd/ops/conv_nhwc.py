@@ -32,6 +32,7 @@ class ConvNHWCFn(torch.autograd.Function):
             w.copy_(weight)  # fp32 NCHW -> cdtype NHWC in one kernel
         ctx.wt = packed[1] if packed is not None else None
         ctx.btap = btap  # ops/bn_nhwc.BNTap of the BN that produced x (stride-1 dgrad takes its sums)
+        ctx.wparam = weight  # the leaf parameter (ops/conv_igemm.WgradBatch)
         stats = None
         if (_igemm.usable(x, weight, cdtype) and stride[0] == stride[1] and padding[0] == padding[1]):
             # hand-written implicit GEMM (+ the next BN's statistics in its epilogue)
@@ -84,7 +85,7 @@ class ConvNHWCFn(torch.autograd.Function):
         if (ctx.needs_input_grad[1] and ctx.wdtype == torch.float32 and stride[0] == stride[1]
                 and padding[0] == padding[1] and _igemm.usable(dy, w, w.dtype)):
             # weight gradient on the implicit-GEMM kernel, written as the fp32 OIHW .grad
-            dw = _igemm.conv_wgrad(dy, xc, tuple(w.shape), stride[0], padding[0])
+            dw = _igemm.conv_wgrad(dy, xc, tuple(w.shape), stride[0], padding[0], ctx.wparam)
         mask = [ctx.needs_input_grad[0] and dx is None, ctx.needs_input_grad[1] and dw is None, False]
         if mask[0] or mask[1]:
             dx2, dw2, _ = torch.ops.aten.convolution_backward(dy, xc, w, None, stride, padding, [1, 1], False,
@@ -95,6 +96,7 @@ class ConvNHWCFn(torch.autograd.Function):
                 dw = torch.empty(dw2.shape, dtype=ctx.wdtype, device=dw2.device)
                 dw.copy_(dw2)  # cdtype NHWC -> fp32 NCHW in one kernel
         ctx.btap = None
+        ctx.wparam = None
         return dx, dw, None, None, None, None, None, None
 
 

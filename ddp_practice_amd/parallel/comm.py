@@ -380,7 +380,26 @@ class XgmiCommunicator(Communicator):
         return t
 
     def broadcast_(self, t, src=0):
+        if t.is_cuda and torch.cuda.is_current_stream_capturing():
+            # inside a captured step (DDP's per-step buffer broadcast without SyncBN): the
+            # host path cannot run; broadcast through the engine instead
+            return self._broadcast_engine(t, src)
         return self._host(lambda h: dist.broadcast(h, src, group=self.group), t)
+
+    def _broadcast_engine(self, t, src):
+        """Bit-exact broadcast as an all-reduce: the bytes as 16-bit pieces, each an fp32 integer
+        in [0, 65536) (exact), zero on every rank but ``src``; any dtype, NaN payloads and
+        signed zeros included.  Graph-capturable."""
+        flat = t.detach().reshape(-1)
+        if (flat.numel() * flat.element_size()) % 2 or not flat.is_contiguous():
+            raise RuntimeError("xgmi broadcast under capture: needs a contiguous tensor of whole 16-bit pieces")
+        pieces = flat.view(torch.int16)
+        f = (pieces.to(torch.int32) & 0xFFFF).to(torch.float32)
+        if self.rank != src:
+            f.zero_()
+        self.all_reduce_(f)
+        pieces.copy_(f.to(torch.int32).to(torch.int16))  # 16-bit truncation: the same bits
+        return t
 
     def reduce_(self, t, dst=0, op="sum"):
         return self._host(lambda h: dist.reduce(h, dst, _TORCH_OPS[_op_name(op)], group=self.group), t)

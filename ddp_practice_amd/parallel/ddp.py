@@ -73,6 +73,9 @@ class DistributedDataParallel(nn.Module):
                  first_bucket_mb: float | None = None):
         super().__init__()
         self.module = module
+        # the wrapped model's gradients are read by the reducer's hooks mid-backward: no
+        # end-of-backward deferral of their values (ops/conv_igemm.WgradBatch)
+        module._dpa_ddp_wrapped = True
         self.device_ids = device_ids
         self.broadcast_buffers = broadcast_buffers
         self.find_unused_parameters = find_unused_parameters

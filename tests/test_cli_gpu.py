@@ -109,3 +109,61 @@ def test_origin_main_resnet50_gpu(C, tmp_path):
     m.load_state_dict(ck["model"])
     assert int(m.bn1.num_batches_tracked) == 3
     assert all(torch.isfinite(v).all() for v in ck["model"].values() if v.is_floating_point())
+
+
+def _shared_env(extra=None):
+    env = {"MASTER_PORT": str(free_port()), "DPA_MASTER_ADDR": "127.0.0.1", "DPA_CHECKPOINT_EVERY_RANK": "1",
+           "DPA_WATCHDOG_TIMEOUT": "90"}
+    env.update(extra or {})
+    return env
+
+
+def _check_ranks_equal(tmp_path, world):
+    """DDP keeps every rank's parameters and buffers bitwise equal: each rank's own file."""
+    ref = torch.load(tmp_path / "ddp_checkpoint.pt.rank0", weights_only=True)["model"]
+    for r in range(1, world):
+        other = torch.load(tmp_path / f"ddp_checkpoint.pt.rank{r}", weights_only=True)["model"]
+        assert list(other) == list(ref)
+        for k, v in ref.items():
+            assert torch.equal(v, other[k]), (r, k)
+
+
+@pytest.mark.parametrize("launcher", ["spawn", "torchrun"])
+def test_ddp_cli_two_ranks_sharing_gpu(C, tmp_path, launcher):
+    """The reference's multi-rank programs at W=2 (/root/reference/ddp_main.py:115-178,
+    ddp_main_torchrun.py:101-168) on one GPU: ``--share-gpu`` puts both ranks on device 0,
+    DDP + SyncBN over the xGMI engine (in-kernel SyncBN / gradient exchanges through IPC
+    peer stores), host collectives on gloo.  Checks the rank-0 stdout contract, the
+    rank-0 checkpoint (module. keys + scaler dict, weights_only-loadable), bitwise-equal
+    parameters on both ranks, and the evaluation's reduce to rank 0."""
+    if launcher == "spawn":
+        args = [os.path.join(ROOT, "ddp_main.py"), "--gpu", "0,1", "--share-gpu"]
+    else:
+        args = ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr=127.0.0.1",
+                f"--master-port={free_port()}", os.path.join(ROOT, "ddp_main_torchrun.py"), "--gpu", "0,1",
+                "--share-gpu"]
+    out = _run(args + ["-e", "2", "--synthetic", "--amp-dtype", "bf16", "--seed", "0"], tmp_path, _shared_env())
+    acc = _check_stdout(out, 2)
+    assert acc > 30.0
+    assert out.count("begin testing") == 1  # rank 0 only
+    ck = torch.load(tmp_path / "ddp_checkpoint.pt", weights_only=True)
+    assert list(ck["model"]) == ["module." + k for k in REF_KEYS]
+    assert set(ck["scaler"]) == {"scale", "growth_factor", "backoff_factor", "growth_interval", "_growth_tracker"}
+    m = _load_into_torch(ck["model"])
+    # every optimizer step of both epochs on 2 ranks (938 batches per rank per epoch)
+    assert int(m.layer1[1].num_batches_tracked) == 2 * 938
+    _check_ranks_equal(tmp_path, 2)
+
+
+def test_ddp_cli_two_ranks_accuracy_parity_with_torch(C, tmp_path):
+    """W=2 sharing one GPU, same data / seed / order: the native program vs the same program on
+    torch's DDP (gloo with device tensors, the only torch backend two ranks on one device can
+    use; SyncBN off on both sides: torch's SyncBatchNorm needs an NCCL group)."""
+    args = [os.path.join(ROOT, "ddp_main.py"), "--gpu", "0,1", "--share-gpu", "-e", "2", "--synthetic", "--seed", "0",
+            "--no-sync-bn"]
+    (tmp_path / "n").mkdir()
+    (tmp_path / "t").mkdir()
+    a_native = _acc(_run(args, tmp_path / "n", _shared_env()))
+    a_torch = _acc(_run(args + ["--impl", "torch"], tmp_path / "t", _shared_env(), timeout=220))
+    print(f"W=2 shared GPU: native {a_native:.2f}% torch {a_torch:.2f}%")
+    assert abs(a_native - a_torch) <= 1.0, (a_native, a_torch)

@@ -74,7 +74,7 @@ def test_rccl_under_graph_capture(rccl):
     assert y[0].item() == 8.0
 
 
-def _train(model, steps, images, labels, scaler_on, use_graph):
+def _train(model, steps, images, labels, scaler_on, use_graph, batch=32):
     from ddp_practice_amd.amp import GradScaler
     from ddp_practice_amd.data import DeviceLoader, ImageDataset
     from ddp_practice_amd.engine import TrainLoop
@@ -82,7 +82,7 @@ def _train(model, steps, images, labels, scaler_on, use_graph):
     from ddp_practice_amd.optim import SGD
 
     ds = ImageDataset(images, labels)
-    loader = DeviceLoader(ds, batch_size=32, shuffle=False, device="cuda",
+    loader = DeviceLoader(ds, batch_size=batch, shuffle=False, device="cuda",
                           dtype=torch.bfloat16 if scaler_on else torch.float32)
     opt = SGD(model.parameters(), lr=0.05)
     scaler = GradScaler() if scaler_on else None
@@ -113,6 +113,30 @@ def test_ddp_syncbn_fused_graph_matches_plain(rccl, amp, graph):
     for (n, p), (_, q) in zip(ddp.module.state_dict().items(), plain.state_dict().items()):
         torch.testing.assert_close(p.float(), q.float(), rtol=tol, atol=tol, msg=n)
     assert int(ddp.module.layer1[1].num_batches_tracked) == 2 * 10
+
+
+def test_ddp_syncbn_batch80_takes_launch_path(rccl):
+    """Batch 80: the conv1 weight-gradient site would need 7 * 80 = 560 workgroups, more than
+    a site's 512 epoch words (comm/xsite.h kEpochWords), so the ConvNet must take the
+    all-reduce launch path (ops/convnet_fused._fused_site_engine) -- and still train exactly
+    like the plain model (advisor round 4: the words were not checked on the host)."""
+    from ddp_practice_amd._ext import load
+    from ddp_practice_amd.data import synthetic
+    from ddp_practice_amd.models import ConvNet
+    from ddp_practice_amd.parallel import DistributedDataParallel, convert_sync_batchnorm
+
+    C = load()
+    assert C.convnet.sites_resident(32, torch.bfloat16)
+    assert not C.convnet.sites_resident(80, torch.bfloat16)
+    ds = synthetic(80 * 3 + 7, seed=5)
+    torch.manual_seed(0)
+    plain = ConvNet(amp_dtype=torch.bfloat16).cuda()
+    ddp = DistributedDataParallel(convert_sync_batchnorm(copy.deepcopy(plain)), device_ids=[0])
+    _train(plain, 2, ds.images, ds.labels, True, use_graph=False, batch=80)
+    _train(ddp, 2, ds.images, ds.labels, True, use_graph=True, batch=80)
+    for (n, p), (_, q) in zip(ddp.module.state_dict().items(), plain.state_dict().items()):
+        torch.testing.assert_close(p.float(), q.float(), rtol=2e-3, atol=2e-3, msg=n)
+    assert rccl.xgmi is not None and rccl.xgmi.error() == 0
 
 
 def test_xgmi_engine_passes_its_selftest_at_forced_world1(rccl):

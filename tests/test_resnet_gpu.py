@@ -180,6 +180,33 @@ def test_resnet50_native_matches_torch_path(C, amp):
     assert e < max(fac * e_ref, floor), (e, e_ref)
 
 
+def test_wgrad_batch_matches_per_conv_reduction(monkeypatch):
+    """The weight-gradient reductions of a backward pass batched into one end-of-backward
+    launch (ops/conv_igemm.WgradBatch) give bitwise the gradients of one reduction per conv,
+    are complete when backward() returns, and are skipped when a gradient already exists
+    (autograd reads it to accumulate): a second backward accumulates exactly as without."""
+    from ddp_practice_amd.models import resnet50
+    from ddp_practice_amd.ops import conv_igemm
+
+    torch.manual_seed(0)
+    base = resnet50(num_classes=10, amp_dtype=torch.bfloat16).to(DEV)
+    x = torch.rand(8, 3, 96, 96, device=DEV)
+    y = torch.randint(0, 10, (8,), device=DEV)
+    one, two = {}, {}
+    for on in (False, True):
+        monkeypatch.setattr(conv_igemm.WgradBatch, "enabled", on)
+        m = copy.deepcopy(base)
+        F.cross_entropy(m(x).float(), y).backward()
+        assert not conv_igemm.WgradBatch._pending
+        one[on] = {n: p.grad.clone() for n, p in m.named_parameters()}
+        F.cross_entropy(m(x).float(), y).backward()
+        assert not conv_igemm.WgradBatch._pending
+        two[on] = {n: p.grad.clone() for n, p in m.named_parameters()}
+    bad1 = [n for n, g in one[False].items() if not torch.equal(g, one[True][n])]
+    bad2 = [n for n, g in two[False].items() if not torch.equal(g, two[True][n])]
+    assert not bad1 and not bad2, (bad1[:8], bad2[:8])
+
+
 @pytest.mark.parametrize("C", [256, 64, 24])
 def test_bn_res_bn_fwd_bwd(C):
     """relu(bn(x) + bn_r(r)) in one pass (ops/bn_nhwc.bn_res_bn) == float64 torch: output,
