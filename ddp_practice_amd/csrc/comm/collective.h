@@ -26,6 +26,9 @@ struct Collective {
   // failure handling (watchdog thread): may be called concurrently with other calls
   virtual std::string async_error() { return std::string(); }
   virtual void abort_now() {}
+  // one line describing where the communicator's in-kernel exchanges stand (watchdog report,
+  // after abort_now): empty when there is nothing device-side to show
+  virtual std::string debug_state() { return std::string(); }
 };
 
 // Flat multi-tensor copy (csrc/kernels/optim.hip): direction 0 = pack into flat.

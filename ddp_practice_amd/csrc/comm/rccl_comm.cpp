@@ -131,6 +131,10 @@ class RcclComm : public Collective {
     if (c != nullptr) ncclCommAbort(c);
   }
   void abort_now() override { abort(); }
+  std::string debug_state() override {
+    auto x = xgmi_;
+    return x ? x->debug_state(2.0) : std::string();
+  }
 
   std::string async_error() override {
     if (auto x = xgmi_; x && x->error() != 0) return x->error_string();

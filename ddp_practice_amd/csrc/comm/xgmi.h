@@ -56,6 +56,11 @@ class XgmiComm {
   int error() const;  // 0 ok, 1 a peer never arrived (timeout), 2 aborted
   std::string error_string() const;
   void abort();       // every waiting block gives up (watchdog path)
+  // Where this rank's exchanges stand: per used site the epoch its launches reached and the
+  // epoch of the newest granule each peer pushed into this rank's rows (both parities), the
+  // one-/two-shot block epochs and the error / abort words.  Read on a side thread through a
+  // non-blocking stream, bounded by wait_s (a stuck compute stream cannot hold it up).
+  std::string debug_state(double wait_s = 2.0) const;
   void set_timeout(double s) { timeout_ticks_ = (long long)(s * 1e8); }
   long long max_bytes() const { return max_elems_ * 4; }  // as fp32
   long long workspace_bytes() const { return ws_bytes_; }

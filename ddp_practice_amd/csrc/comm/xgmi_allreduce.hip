@@ -41,6 +41,10 @@
 #include <cstring>
 
 #include "comm/xgmi.h"
+
+#include <future>
+#include <sstream>
+#include <thread>
 #include "common.h"
 
 namespace dpa {
@@ -689,6 +693,99 @@ void XgmiComm::abort() {
   if (host_words_) __atomic_store_n(&host_words_[1], 1, __ATOMIC_RELEASE);
 }
 
+std::string XgmiComm::debug_state(double wait_s) const {
+  std::ostringstream o;
+  o << "xgmi rank " << rank_ << "/" << world_;
+  if (host_words_ == nullptr || local_ == nullptr) {
+    o << ": closed";
+    return o.str();
+  }
+  o << ": err=" << __atomic_load_n(&host_words_[0], __ATOMIC_ACQUIRE)
+    << " abort=" << __atomic_load_n(&host_words_[1], __ATOMIC_ACQUIRE);
+  // regions: the SyncBN sites 0..4, the wide site, the gradient site, the one-shot slots
+  struct Reg {
+    const char* name;
+    int site;            // epoch words (-1: per-block counters)
+    long long off, slot;
+  };
+  std::vector<Reg> regs;
+  static const char* names[] = {"fwd1", "fwd2", "bwd2d", "bwd2w", "bwd1"};
+  for (int s = 0; s < kSiteWide; ++s) regs.push_back({names[s], s, site_off_ + (long long)s * kSiteBytes, kSiteSlotBytes});
+  regs.push_back({"wide", kSiteWide, wide_off_, (long long)kWideVals * 8});
+  regs.push_back({"grad", kSiteGrad, grad_off_, slot_bytes_});
+  regs.push_back({"oneshot", -1, 0, slot_bytes_});
+  const int nr = (int)regs.size();
+  struct Snap {
+    std::vector<unsigned long long> ticks, tags;
+    std::vector<uint32_t> ctr, tctr;
+  };
+  auto snap = std::make_shared<Snap>();
+  snap->ticks.assign((size_t)kSites * kEpochWords, 0);
+  snap->tags.assign((size_t)nr * 2 * world_, 0);
+  snap->ctr.assign(4, 0);
+  snap->tctr.assign(4, 0);
+  const int dev = device_, world = world_, maxb = max_blocks_, tsb = ts_blocks_;
+  const unsigned long long* ticks = ticks_;
+  const uint32_t *ctr = ctr_, *tctr = ts_ctr_;
+  const char* local = local_;
+  std::vector<long long> goff;
+  for (const auto& r : regs)
+    for (int par = 0; par < 2; ++par)
+      for (int p = 0; p < world; ++p) goff.push_back(r.off + (long long)par * kMaxRanks * r.slot + (long long)p * r.slot);
+  auto done = std::make_shared<std::promise<bool>>();
+  auto fut = done->get_future();
+  std::thread([=]() {
+    bool ok = hipSetDevice(dev) == hipSuccess;
+    hipStream_t st = nullptr;
+    ok = ok && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+    if (ok) {
+      ok = hipMemcpyAsync(snap->ticks.data(), ticks, snap->ticks.size() * 8, hipMemcpyDeviceToHost, st) == hipSuccess;
+      for (size_t i = 0; ok && i < goff.size(); ++i)
+        ok = hipMemcpyAsync(&snap->tags[i], local + goff[i], 8, hipMemcpyDeviceToHost, st) == hipSuccess;
+      if (ok) ok = hipMemcpyAsync(snap->ctr.data(), ctr, 4 * std::min(4, maxb), hipMemcpyDeviceToHost, st) == hipSuccess;
+      if (ok && tctr != nullptr)
+        ok = hipMemcpyAsync(snap->tctr.data(), tctr, 4 * std::min(4, tsb), hipMemcpyDeviceToHost, st) == hipSuccess;
+      ok = ok && hipStreamSynchronize(st) == hipSuccess;
+    }
+    done->set_value(ok);
+  }).detach();
+  if (fut.wait_for(std::chrono::duration<double>(wait_s)) != std::future_status::ready) {
+    o << "; device snapshot timed out after " << wait_s << " s";
+    return o.str();
+  }
+  if (!fut.get()) {
+    o << "; device snapshot failed";
+    return o.str();
+  }
+  size_t g = 0;
+  for (const auto& r : regs) {
+    unsigned long long lo = ~0ull, hi = 0;
+    if (r.site >= 0)
+      for (int w = 0; w < kEpochWords; ++w) {
+        const unsigned long long v = snap->ticks[(size_t)r.site * kEpochWords + w];
+        lo = std::min(lo, v);
+        hi = std::max(hi, v);
+      }
+    std::ostringstream t;
+    bool any = hi > 0;
+    for (int par = 0; par < 2; ++par) {
+      t << (par ? " | " : "");
+      for (int p = 0; p < world; ++p, ++g) {
+        const uint32_t tag = (uint32_t)(snap->tags[g] >> 32);
+        any = any || tag != 0;
+        t << (p ? "," : "") << (p == rank_ ? "*" : "") << tag;
+      }
+    }
+    if (!any) continue;  // a site this run never used
+    o << "; " << r.name;
+    if (r.site >= 0) o << " ep=" << (lo == hi ? std::to_string(hi) : std::to_string(lo) + ".." + std::to_string(hi));
+    o << " peers[par0|par1]=" << t.str();
+  }
+  o << "; oneshot blk ep=" << snap->ctr[0] << "," << snap->ctr[1];
+  if (tctr != nullptr) o << "; twoshot blk ep=" << snap->tctr[0] << "," << snap->tctr[1];
+  return o.str();
+}
+
 }  // namespace xgmi
 
 // The engine as the reducer's Collective (csrc/ddp/reducer.cpp): async
@@ -737,6 +834,7 @@ class XgmiCollective : public Collective {
   }
   std::string async_error() override { return x_->error_string(); }
   void abort_now() override { x_->abort(); }
+  std::string debug_state() override { return x_->debug_state(2.0); }
 
  private:
   // Tensors larger than the workspace slot (ResNet-50 DDP buckets) go as back-to-back
@@ -802,6 +900,7 @@ void register_xgmi(pybind11::module& m) {
            },
            py::arg("t"), py::arg("op") = "sum", py::arg("out") = py::none())
       .def("wide_probe", &xgmi::XgmiComm::wide_probe, py::arg("inp"), py::arg("out"), py::arg("nblk"))
+      .def("debug_state", &xgmi::XgmiComm::debug_state, py::arg("wait_s") = 2.0)
       .def("site_probe", &xgmi::XgmiComm::site_probe, py::arg("site"), py::arg("inp"), py::arg("out"),
            py::arg("grid") = 1)
       .def("all_reduce_twoshot",

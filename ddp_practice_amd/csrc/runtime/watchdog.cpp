@@ -98,6 +98,13 @@ class Watchdog {
     host_armed_ = false;
   }
 
+  // What the rank last reported doing (host side, e.g. "epoch 0: step 112 queued"): named
+  // in the report, so a stall record says which step the stuck device work belongs to.
+  void note(std::string what) {
+    std::lock_guard<std::mutex> g(mu_);
+    note_ = std::move(what);
+  }
+
   int64_t ticks() const { return ticks_.load(); }
   int64_t outstanding() {
     std::lock_guard<std::mutex> g(mu_);
@@ -167,6 +174,17 @@ class Watchdog {
                  tag_.c_str(), why.c_str(), timeout_);
     std::fflush(stderr);
     if (comm_) comm_->abort_now();
+    // after the abort (spinning exchanges give up, the device drains): where the in-kernel
+    // exchanges stood, and what the host last queued -- one line the supervisor records
+    const std::string st = comm_ ? comm_->debug_state() : std::string();
+    std::string last;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      last = note_;
+    }
+    std::fprintf(stderr, "[dpa watchdog] rank %d (%s): %s; last: %s%s%s\n", rank, tag_.c_str(), why.c_str(),
+                 last.empty() ? "(no step noted)" : last.c_str(), st.empty() ? "" : "; ", st.c_str());
+    std::fflush(stderr);
     if (do_exit_) std::_Exit(exit_code_);
     lk.lock();
   }
@@ -187,6 +205,7 @@ class Watchdog {
   std::atomic<bool> do_exit_{true};
   std::atomic<int64_t> ticks_{0};
   std::string reason_;
+  std::string note_;
 };
 
 }  // namespace rt
@@ -205,6 +224,7 @@ void register_runtime(pybind11::module& m) {
       .def("set_exit", &Watchdog::set_exit)
       .def_property_readonly("ticks", &Watchdog::ticks)
       .def_property_readonly("outstanding", &Watchdog::outstanding)
+      .def("note", &Watchdog::note)
       .def_property_readonly("fired", &Watchdog::fired)
       .def_property_readonly("reason", &Watchdog::reason);
   // roctx ranges: visible in rocprofv3 --marker-trace timelines

@@ -136,6 +136,7 @@ class TrainLoop:
 
     def _tick(self):
         if self.watchdog is not None:
+            self.watchdog.note(f"{self.global_step} training steps queued")
             self.watchdog.tick()
 
     def _graph(self, k: int) -> CapturedStep | None:

@@ -239,6 +239,14 @@ class DistributedDataParallel(nn.Module):
         xc = getattr(self.comm, "xgmi", None)
         if xc is None or not hasattr(optimizer, "fused_amp_step"):
             return False
+        if (os.environ.get("DPA_SHARED_GPU") == "1" and self.comm.world_size > 2
+                and os.environ.get("DPA_FUSED_GRAD") != "1"):
+            # 3+ ranks sharing one GPU: every rank's AMP workgroups spin on the peers' rows,
+            # and the ranks' launches need not be resident together on the one card (the
+            # SyncBN sites are gated the same way: ops/convnet_fused._fused_site_engine).
+            # Round 4's one stalled W=4 rehearsal (profiles/r4zz_*) had all four ranks inside
+            # device work; with one rank per GPU this never applies.  DPA_FUSED_GRAD=1 forces it.
+            return False
         opt_params = [p for g in optimizer.param_groups for p in g["params"]]
         if {id(p) for p in opt_params} != {id(p) for p in self._params}:
             return False

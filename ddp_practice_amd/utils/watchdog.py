@@ -51,6 +51,11 @@ class Watchdog:
     def heartbeat(self) -> None:
         self._w.heartbeat()
 
+    def note(self, what: str) -> None:
+        """What the rank last queued (named in a fire report with the communicator's
+        in-kernel exchange state: csrc/comm/xgmi_allreduce.hip debug_state)."""
+        self._w.note(what)
+
     def disarm(self) -> None:
         self._w.disarm()
 

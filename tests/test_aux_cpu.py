@@ -2,6 +2,7 @@
 detection, resume, metrics."""
 import json
 import os
+import re
 import subprocess
 import sys
 import time
@@ -75,6 +76,9 @@ def test_hung_rank_is_detected_by_watchdog(tmp_path):
                  {"MASTER_PORT": str(_dist.free_port()), "DPA_MASTER_ADDR": "127.0.0.1", "DPA_FAULT": "1:3:hang"})
     assert r.returncode != 0
     assert "[dpa watchdog]" in r.stderr, r.stderr[-2000:]
+    # the report names what the stalled rank last queued (verdict r4: a stall record must say
+    # which step / exchange was waiting)
+    assert re.search(r"\[dpa watchdog\] rank \d .*; last: \d+ training steps queued", r.stderr), r.stderr[-2000:]
     assert dt < 120
     assert not (tmp_path / "ck.pt").exists()
 

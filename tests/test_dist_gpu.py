@@ -139,6 +139,26 @@ def test_ddp_syncbn_batch80_takes_launch_path(rccl):
     assert rccl.xgmi is not None and rccl.xgmi.error() == 0
 
 
+def test_xgmi_debug_state_names_sites_and_words(rccl):
+    """The watchdog's exchange-state report (csrc/comm/xgmi_allreduce.hip debug_state): error /
+    abort words, the used sites' epochs and the peers' newest granule epochs, read from a
+    side stream with a bounded wait."""
+    from ddp_practice_amd.data import synthetic
+    from ddp_practice_amd.models import ConvNet
+    from ddp_practice_amd.parallel import DistributedDataParallel, convert_sync_batchnorm
+
+    x = rccl.xgmi
+    assert x is not None
+    ds = synthetic(32 * 3, seed=3)
+    torch.manual_seed(0)
+    ddp = DistributedDataParallel(convert_sync_batchnorm(ConvNet(amp_dtype=torch.bfloat16).cuda()), device_ids=[0])
+    _train(ddp, 1, ds.images, ds.labels, True, use_graph=False)
+    torch.cuda.synchronize()
+    st = x.debug_state(2.0)
+    assert st.startswith("xgmi rank 0/1: err=0 abort=0"), st
+    assert "fwd1 ep=" in st and "peers[par0|par1]=" in st and "oneshot blk ep=" in st, st
+
+
 def test_xgmi_engine_passes_its_selftest_at_forced_world1(rccl):
     """The RCCL communicator's start-up self-test (parallel/comm.setup_xgmi) must pass on a
     healthy device, or every multi-GPU run silently loses the xGMI engine (round 2's self-test
