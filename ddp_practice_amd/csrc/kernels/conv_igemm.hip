@@ -1616,6 +1616,11 @@ int64_t g3x3_config(int64_t on) {
   return prev;
 }
 
+// Measured and not kept (profiles/r5j_wide_ns_ab.txt): the 8-wave 128 x 128 tile with three or
+// four LDS stages (two / three tiles in flight, one workgroup per CU) -- no faster even where
+// the grid is one workgroup per CU anyway (512 -> 512 3x3 at 7x7: 56.1 vs 57.9 / 58.1 us),
+// 23 % slower over the network: the K-loop does not wait on DMA latency (PMC,
+// profiles/r5i_conv_pmc.txt: MFMA busy 27-32 %, waits at the barrier / LDS-read counters).
 // Wide 8-wave tiles of conv_glds_kernel for the forward / plain data-gradient convs
 // (DPA_WIDE; wide_config at run time): 0 off, 1 auto (see wide_pick), 2 force 256 x 128,
 // 3 force 256 x 256, 4 force 128 x 128 on 8 waves.  Shapes a forced tile does not fit keep

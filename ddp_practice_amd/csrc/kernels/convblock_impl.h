@@ -47,7 +47,10 @@ __host__ __device__ constexpr int fslab_row(int C) { return 2 * C + 1; }
 
 template <int I> struct SH;
 template <> struct SH<0> { static constexpr int CIN = 1, COUT = 16, H = 28, W = 28, SPLIT = 4, WROWS = 28; };
-template <> struct SH<1> { static constexpr int CIN = 16, COUT = 32, H = 14, W = 14, SPLIT = 2, WROWS = 14; };
+#ifndef DPA_FWD2_SPLIT
+#define DPA_FWD2_SPLIT 2  // workgroups per image of the conv2 forward (experiment builds: -DDPA_FWD2_SPLIT=4)
+#endif
+template <> struct SH<1> { static constexpr int CIN = 16, COUT = 32, H = 14, W = 14, SPLIT = DPA_FWD2_SPLIT, WROWS = 14; };
 constexpr int kBwdSplit = 8;  // batch split of bwd_reduce
 
 // ---------------------------------------------------------------------------

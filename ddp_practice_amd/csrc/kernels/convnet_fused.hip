@@ -272,14 +272,14 @@ void conv2_fwd(at::Tensor y1, c10::optional<at::Tensor> fslab1, at::Tensor fstat
   if (p1_out.has_value())
     TORCH_CHECK(p1_out->numel() == (int64_t)B * 16 * 196 && idx1_out->numel() == p1_out->numel() &&
                 xh1_out->numel() == p1_out->numel());
-  if (train) TORCH_CHECK(fslab2.has_value() && fslab2->numel() == (int64_t)B * 2 * cb::fslab_row(32));
+  constexpr int ns = cb::SH<1>::SPLIT;  // workgroups per image
+  if (train) TORCH_CHECK(fslab2.has_value() && fslab2->numel() == (int64_t)B * ns * cb::fslab_row(32));
   if (B == 0) return;
   BNParams bp = bn_params(fslab1, fstats1, g1, b1, rm1, rv1, nbt1, momentum, eps, train, 16);
   if (train) {
     bp.xs = site_of(xc, xgmi::kSiteFwd1);
-    xgmi::set_site_grid(bp.xs, B * 2, "conv2_fwd");  // the grid (ns workgroups per image)
+    xgmi::set_site_grid(bp.xs, B * ns, "conv2_fwd");  // the grid (ns workgroups per image)
   }
-  constexpr int ns = 2;
   hipStream_t stream = cur_stream();
   with_t(dt_of(y1), [&](auto tag) {
     typedef decltype(tag) T;
@@ -445,7 +445,10 @@ void conv1_fwd_pack_gather(at::Tensor x, at::Tensor w1, at::Tensor b1, at::Tenso
   DPA_CHECK_LAUNCH();
 }
 
-constexpr int kDgradSplit = 2;
+#ifndef DPA_DGRAD2_SPLIT
+#define DPA_DGRAD2_SPLIT 2  // workgroups per image of the conv2 data gradient (-DDPA_DGRAD2_SPLIT=4)
+#endif
+constexpr int kDgradSplit = DPA_DGRAD2_SPLIT;
 int64_t dgrad2_rows(int64_t B) { return B * kDgradSplit; }
 
 // [pool2/ReLU2/BN2 backward] -> conv2 data grad -> dp1 (+ BN1 partial sums rows).
@@ -1027,11 +1030,11 @@ bool sites_resident(int64_t B, at::ScalarType st) {
   // every site launch must also fit its site's epoch words (comm/xgmi.h set_site_grid):
   // the conv1 weight gradient's 7 B workgroups pass kEpochWords at B >= 74
   bool ok = xgmi::site_grid_fits(wgrad_bn_rows(1, B)) && xgmi::site_grid_fits(wgrad_bn_rows(2, B)) &&
-            xgmi::site_grid_fits(B * kDgradSplit) && xgmi::site_grid_fits(2 * B);
+            xgmi::site_grid_fits(B * kDgradSplit) && xgmi::site_grid_fits(cb::SH<1>::SPLIT * B);
   auto chk = [&](const void* k, int64_t grid) { ok = ok && co_resident(k, (int)grid, cb::NTHR, 0); };
   with_t(dt_of(at::empty({0}, at::TensorOptions().dtype(st))), [&](auto tag) {
     typedef decltype(tag) T;
-    chk(reinterpret_cast<const void*>(&cb::conv5x5_kernel<T, 16, 32, 14, 14, 0, 1, 0, 1>), B * 2);
+    chk(reinterpret_cast<const void*>(&cb::conv5x5_kernel<T, 16, 32, 14, 14, 0, 1, 0, 1>), B * cb::SH<1>::SPLIT);
     ok = ok && co_resident(reinterpret_cast<const void*>(&head_fwd_kernel<T, 32, 14, 14, 16>), (int)B, HF, 0) &&
          co_resident(reinterpret_cast<const void*>(&head_fwd_kernel<T, 32, 14, 14, 64>), (int)B, HF, 0);
     chk(reinterpret_cast<const void*>(&cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1, 1>), B * kDgradSplit);
