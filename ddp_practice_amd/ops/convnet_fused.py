@@ -189,9 +189,9 @@ class ConvNetFn(torch.autograd.Function):
             if labels is not None and state is not None and _head_step_ok(B, N, cdtype):
                 # labels known now (paired by the device loader): head forward + loss (+ the head
                 # backward when a GradScaler will seed it with its scale) in one launch
-                from ..amp.grad_scaler import active_scale
+                from .head import seed_scale
 
-                scale = active_scale(dev) if _HEAD_SPEC else None
+                scale = seed_scale(dev) if _HEAD_SPEC else None
                 f32 = dict(dtype=torch.float32, device=dev)
                 loss_buf = torch.empty(2, **f32)
                 dlog = torch.empty((B, N), **f32)

@@ -8,6 +8,8 @@ loss math is fp32).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .._ext import load as _load_ext
@@ -126,24 +128,92 @@ class PrecomputedCEFn(torch.autograd.Function):
         return out, None
 
 
+_UNIT: dict = {}
+_UNIT_SEED = os.environ.get("DPA_UNIT_SEED", "1") != "0"  # 0: no unit-seed speculation (A/B)
+
+
+def unit_scale(device: torch.device) -> torch.Tensor:
+    """A persistent device ``[1.0]``: the "scale" a loss is pre-differentiated with when no
+    GradScaler is active (fp32 training, /root/reference/origin_main.py:57-66)."""
+    t = _UNIT.get(device)
+    if t is None:
+        t = _UNIT[device] = torch.ones(1, dtype=torch.float32, device=device)
+    return t
+
+
+def seed_scale(device: torch.device):
+    """The scale a native loss kernel pre-differentiates for: the active GradScaler's (its
+    scaled backward seeds the loss with it), else -- on a HIP device -- the unit tensor,
+    which the loss's own ``backward()`` then seeds with (no ones() fill, no CE backward
+    launch; the fused ConvNet head also runs its backward rows in the forward launch).
+    None on CPU or with DPA_UNIT_SEED=0."""
+    from ..amp.grad_scaler import active_scale
+
+    s = active_scale(device)
+    if s is None and _UNIT_SEED and device.type == "cuda":
+        s = unit_scale(device)
+    return s
+
+
+class _LossViewFn(torch.autograd.Function):
+    """The loss as a view of itself (no launch): the tensor a unit-seeded loss is handed out
+    as, so the ``backward`` override stored on it can hold the real loss strongly."""
+
+    @staticmethod
+    def forward(ctx, loss):
+        return loss.view_as(loss)
+
+    @staticmethod
+    def backward(ctx, grad):
+        return grad
+
+
+def _unit_seeded(loss: torch.Tensor, node, unit: torch.Tensor) -> torch.Tensor:
+    """``loss.backward()`` of an unscaled native CE loss: seed with the unit tensor the loss
+    was pre-differentiated for (grad 1, as autograd's implicit seed) and let the CE node hand
+    back the gradient its forward already wrote; any other call goes through torch.
+
+    Returns the tensor to hand out.  The override lives on a view of the loss and holds the
+    loss itself: ``f(x).backward()`` drops the last reference to the returned temporary
+    before the bound call runs (so a weak reference would be dead), and a strong reference
+    from the loss's own attribute would be a cycle keeping the step's autograd graph alive
+    until the cyclic GC (as in amp/grad_scaler.py's scaled loss)."""
+    from ..amp.grad_scaler import _seeded_backward
+
+    seed = unit.view(())
+    out = _LossViewFn.apply(loss)
+
+    def _backward(gradient=None, retain_graph=None, create_graph=False, inputs=None):
+        if gradient is None and not create_graph:
+            node.token.seeded = True
+            try:
+                _seeded_backward(loss, seed, retain_graph, inputs)
+            finally:
+                node.token.seeded = False
+        else:
+            torch.Tensor.backward(loss, gradient, retain_graph, create_graph, inputs)
+
+    out.backward = _backward
+    return out
+
+
 def cross_entropy(logits, target, ignore_index=-100, label_smoothing=0.0):
     if logits.dim() != 2:
         raise ValueError("native cross_entropy expects [B, C] logits")
-    from ..amp.grad_scaler import active_scale
-
-    scale = active_scale(logits.device) if logits.requires_grad else None
+    scale = seed_scale(logits.device) if logits.requires_grad else None
     pre = getattr(logits, "_dpa_pre_ce", None)
     if (pre is not None and pre.target is target and pre.ignore_index == ignore_index
             and pre.smoothing == label_smoothing and pre.scale is scale and logits.requires_grad):
         loss = PrecomputedCEFn.apply(logits, pre)
-        if scale is not None and loss.grad_fn is not None:
-            loss._dpa_ce = (loss.grad_fn, scale)
-        return loss
-    loss = CrossEntropyFn.apply(logits, target, ignore_index, label_smoothing, scale)
+    else:
+        loss = CrossEntropyFn.apply(logits, target, ignore_index, label_smoothing, scale)
     if scale is not None and loss.grad_fn is not None:
         node = loss.grad_fn
-        # the token / pre-scaled value travel with the loss tensor to GradScaler.scale
-        loss._dpa_ce = (node, scale)
+        if scale is _UNIT.get(logits.device):
+            loss = _unit_seeded(loss, node, scale)
+        else:
+            # the token / pre-scaled value travel with the loss tensor to GradScaler.scale
+            loss._dpa_ce = (node, scale)
     return loss
 
 
