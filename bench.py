@@ -665,10 +665,12 @@ def _headline(ctx, amp, steady: bool) -> dict:
     train_ds = ctx["train_ds"]
     model, optimizer, scaler = _build(ctx, amp, 1)
     crit = CrossEntropyLoss().to(dev)
-    fused_grad = ctx["dist_path"] and amp is not None and model.defer_grad_sync_to(optimizer)
-    # conv1's weight-gradient column sums run inside the fused AMP step (engine.TrainLoop does the
+    # the fused optimizer launch: the AMP step, or fp32's plain step (optim/sgd.py)
+    fusable = amp is not None or getattr(optimizer, "plain_fused", False)
+    fused_grad = ctx["dist_path"] and fusable and model.defer_grad_sync_to(optimizer)
+    # conv1's weight-gradient column sums run inside the fused step (engine.TrainLoop does the
     # same): without DDP, and under DDP when the step also averages the gradients (fused_grad)
-    if amp is not None and (fused_grad or not ctx["dist_path"]):
+    if fusable and (fused_grad or not ctx["dist_path"]):
         model.set_slab_sink(optimizer)
     sampler = DistributedSampler(train_ds, num_replicas=world, rank=rank)
     loader = DeviceLoader(train_ds, batch_size=B, sampler=sampler, device=dev, dtype=act)

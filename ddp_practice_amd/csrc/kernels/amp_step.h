@@ -149,6 +149,11 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
   __shared__ float spart[16 * 65];   // slab workgroups: G row groups x (columns + 1)
   const int tid = threadIdx.x;
   const int n = L.n;
+  // scale == nullptr: the plain (unscaled fp32) SGD step -- no unscale, no non-finite
+  // agreement, no grid barrier, no scale update: torch.optim.SGD's semantics, with the
+  // slab sums and the DDP average (XG) still inside this launch.  A workgroup whose slab
+  // producers or peers never arrived (error word set) skips its own update only.
+  const bool amp = scale != nullptr;
   {  // the table: every load issued before any LDS write (clamped index; a guarded load was
      // branched and waited for before the next group's loads were issued)
     const int ti = min(tid, MAXT - 1);
@@ -170,7 +175,7 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
   // the barrier generation is only used by lane 0: issued after the table
   // barrier, its load stays in flight (no LDS round trip) with the gradients'
   unsigned long long gen = 0;
-  if (tid == 0 && grid > 1)
+  if (tid == 0 && grid > 1 && amp)
     gen = __hip_atomic_fetch_add(&sync[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   unsigned long long tk = 0;
   if (XG && tid == 0) tk = xgmi::xsite_ticket(xg, bid);
@@ -256,7 +261,7 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
     __syncthreads();
     if (tid < cols && col < S.n) {
       for (int gg = 0; gg < G; ++gg) st_sum += spart[gg * (cols + 1) + tid];
-      bad = !isfinite(st_sum);
+      bad = amp && !isfinite(st_sum);
     }
     bad |= wait_fail;
 #pragma unroll
@@ -364,22 +369,23 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
         acc = p == 0 ? x : acc + x;
       }
       st_sum = acc * invw;
-      bad |= !isfinite(st_sum);
+      bad |= amp && !isfinite(st_sum);
     }
     // a peer that never arrived (timeout / abort: error word set) leaves a partial sum:
     // take the skip path (no parameter / momentum / scale change) rather than apply it
     bad |= fail;
   }
+  if (amp)
 #pragma unroll
-  for (int k = 0; k < U; ++k)
-    if (tt[k] >= 0)
+    for (int k = 0; k < U; ++k)
+      if (tt[k] >= 0)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bad |= !isfinite(gv[k][j]);
+        for (int j = 0; j < 4; ++j) bad |= !isfinite(gv[k][j]);
   // scale read before arriving: block 0 rewrites it once everyone has arrived, and a
   // workgroup that reads it late must not unscale with the next step's value
-  const float inv = 1.f / scale[0];
+  const float inv = amp ? 1.f / scale[0] : 1.f;
   const bool block_bad = __syncthreads_or(bad);
-  if (grid == 1) {  // uniform: one workgroup needs no grid barrier
+  if (grid == 1 || !amp) {  // uniform: one workgroup (or the plain step) needs no grid barrier
     if (tid == 0) s_bad = block_bad;
   } else if (tid == 0) {
     // arrival words of this launch's parity: one (blanes == 1) or blanes, kBarStride apart
@@ -428,7 +434,7 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
     if (t < 0) continue;
     const int o = (bid * BG + k * THR + tid - soff[t]) * 4, rem = snum[t] - o;
     const f32x4 g = gv[k] * inv;
-    store4(sp1[t] + o, rem, g);
+    if (amp || XG) store4(sp1[t] + o, rem, g);  // plain step: the gradient is unchanged
     if (any_bad) continue;
     f32x4 d = maximize ? -g : g;
     if (wd != 0.f) d += wd * pv[k];
@@ -456,7 +462,7 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
     }
   }
   DPA_STAMP(13);
-  if (bid == 0 && tid == 0) {
+  if (amp && bid == 0 && tid == 0) {
     // every workgroup read scale[0] before arriving, and block 0 passed the barrier
     found_inf[0] = 0.f;
     if (any_bad) {

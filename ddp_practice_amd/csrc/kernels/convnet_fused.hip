@@ -570,6 +570,19 @@ conv2_bwd_kernel(const T* __restrict__ wpk_d, T* __restrict__ dp1, BwdIn<T> bi_d
     fc_wgrad_body<T>(fw, bid - ndg - nwg);
 }
 
+// fp32: the conv2 weight-gradient role and the fc weight gradient in one launch (the
+// data-gradient role's LDS does not fit beside the weight gradient's, conv2_bwd below)
+template <typename T>
+__global__ void __launch_bounds__(cb::NTHR)
+conv2_wgrad_fc_kernel(const T* __restrict__ p1, float* __restrict__ wslab2, BwdIn<T> bi_w, int nwg, FcW<T> fw) {
+  constexpr int nsw = (14 + WG2_ROWS_ - 1) / WG2_ROWS_;
+  const int bid = (int)blockIdx.x;
+  if (bid < nwg)
+    cb::conv5x5_wgrad_body<T, 16, 32, 14, 14, WG2_ROWS_, 2>(p1, nullptr, wslab2, nsw, bi_w, bid);
+  else
+    fc_wgrad_body<T>(fw, bid - nwg);
+}
+
 template <typename T>
 static FcW<T> fc_args(const c10::optional<at::Tensor>& dls, const c10::optional<at::Tensor>& p2,
                       const c10::optional<at::Tensor>& dw, const c10::optional<at::Tensor>& db, int B, at::ScalarType st) {
@@ -640,13 +653,14 @@ void conv2_bwd(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx2,
     const int nfc = fc_dls.has_value() ? FC_BLOCKS : 0;
     if constexpr (std::is_same<T, float>::value) {
       // fp32 tiles: the two roles' LDS (173 KB) exceed one CU's 160 KB -> separate launches
-      bd.xs.nblk = bw.xs.nblk = 0;  // each launch is its site's whole grid (ndg, nwg: checked above)
+      // (the fc weight gradient: extra workgroups of the weight-gradient launch; its site's
+      // tickets are the nwg conv workgroups', set above)
+      bd.xs.nblk = 0;  // the data-gradient launch is its site's whole grid (ndg: checked above)
       hipLaunchKernelGGL((cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1, 1>), dim3(ndg), dim3(cb::NTHR), 0,
                          cur_stream(), nullptr, nullptr, nullptr, dptr<T>(dp1), nullptr, nullptr, nullptr,
                          kDgradSplit, PoolIn<T>{}, bd, ep, dptr<T>(wpk_d), cb::WPack<T>{});
-      hipLaunchKernelGGL((cb::conv5x5_wgrad_kernel<T, 16, 32, 14, 14, WG2_ROWS_, 2>), dim3(nwg), dim3(cb::NTHR), 0,
-                         cur_stream(), dptr<T>(p1), nullptr, wslab2.data_ptr<float>(), nwg / B, bw);
-      if (nfc) hipLaunchKernelGGL(fc_wgrad_kernel<T>, dim3(nfc), dim3(cb::NTHR), 0, cur_stream(), fw);
+      hipLaunchKernelGGL(conv2_wgrad_fc_kernel<T>, dim3(nwg + nfc), dim3(cb::NTHR), 0, cur_stream(), dptr<T>(p1),
+                         wslab2.data_ptr<float>(), bw, nwg, fw);
     } else {
       hipLaunchKernelGGL(conv2_bwd_kernel<T>, dim3(ndg + nwg + nfc), dim3(cb::NTHR), 0, cur_stream(), dptr<T>(wpk_d),
                          dptr<T>(dp1), bd, ep, dptr<T>(p1), wslab2.data_ptr<float>(), bw, ndg, nwg, fw);

@@ -438,15 +438,25 @@ constexpr double kBarrierSeconds = 10.0;
 
 void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads, std::vector<at::Tensor> bufs,
                    double lr, double momentum, double dampening, double wd, bool nesterov, bool maximize,
-                   std::vector<int64_t> first, at::Tensor scale, at::Tensor tracker, at::Tensor found_inf,
-                   double growth, double backoff, int64_t interval, at::Tensor sync,
-                   std::shared_ptr<xgmi::XgmiComm> xc, c10::optional<at::Tensor> slab, c10::optional<at::Tensor> slab_out) {
+                   std::vector<int64_t> first, c10::optional<at::Tensor> scale, c10::optional<at::Tensor> tracker,
+                   c10::optional<at::Tensor> found_inf, double growth, double backoff, int64_t interval,
+                   at::Tensor sync, std::shared_ptr<xgmi::XgmiComm> xc, c10::optional<at::Tensor> slab,
+                   c10::optional<at::Tensor> slab_out) {
   TORCH_CHECK(params.size() == grads.size() && params.size() <= (size_t)MAXT, "fused AMP-SGD: <= ", MAXT,
               " tensors");
   TORCH_CHECK(bufs.empty() || bufs.size() == params.size());
   TORCH_CHECK(first.empty() || first.size() == params.size(), "fused AMP-SGD: one first flag per tensor");
-  check_f32(scale); check_f32(found_inf);
-  TORCH_CHECK(tracker.scalar_type() == at::kInt);
+  // no scale: the plain SGD step (amp_step.h amp_sgd_body), tracker / found_inf unused
+  const bool amp = scale.has_value();
+  TORCH_CHECK(tracker.has_value() == amp && found_inf.has_value() == amp,
+              "fused SGD: scale, tracker and found_inf go together");
+  if (amp) {
+    check_f32(*scale); check_f32(*found_inf);
+    TORCH_CHECK(tracker->scalar_type() == at::kInt);
+  }
+  float* const sc = amp ? scale->data_ptr<float>() : nullptr;
+  int* const tr = amp ? tracker->data_ptr<int>() : nullptr;
+  float* const fi = amp ? found_inf->data_ptr<float>() : nullptr;
   TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == at::kLong && sync.numel() >= 4 && sync.is_contiguous(),
               "fused AMP-SGD: sync must be a zero-initialised int64[4] device tensor");
   TORCH_CHECK(amp_sgd_resident(), "fused AMP-SGD: grid not co-resident on this device (use the unfused step)");
@@ -458,8 +468,7 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
     const int grid = (int)std::max<int64_t>(1, (L.chunk_off[L.n] + bg - 1) / bg) + (ss.ns ? ss.s[0].nblk : 0);
     TORCH_CHECK(grid <= FUSED_MAX_BLOCKS, "fused AMP-SGD: grid exceeds the co-resident bound");
     xgmi::set_site_grid(xg, grid, "fused AMP-SGD");  // every workgroup takes a ticket (no hidden-argument load)
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(FUSED_THR), 0, cur_stream(), L, scale.data_ptr<float>(),
-                       tracker.data_ptr<int>(), found_inf.data_ptr<float>(),
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(FUSED_THR), 0, cur_stream(), L, sc, tr, fi,
                        reinterpret_cast<unsigned long long*>(sync.data_ptr<int64_t>()), (float)lr, (float)momentum,
                        (float)dampening, (float)wd, (int)nesterov, (int)maximize, (float)growth, (float)backoff,
                        (int)interval, xg, reinterpret_cast<int*>(sync.data_ptr<int64_t>() + 3),

@@ -80,11 +80,14 @@ class TrainLoop:
         self.faults = faults if faults else None  # utils.FaultInjector (DPA_FAULT)
         # DDP + fused AMP step: the optimizer kernel averages the gradients over xGMI
         # (parallel/ddp.py defer_grad_sync_to; a no-op without the engine)
-        if scaler is not None and getattr(scaler, "_enabled", False) and hasattr(model, "defer_grad_sync_to"):
+        # (fp32 without a scaler: the optimizer's plain step is the same fused launch, optim/sgd.py)
+        fused = (getattr(scaler, "_enabled", False) if scaler is not None
+                 else getattr(optimizer, "plain_fused", False))
+        if fused and hasattr(model, "defer_grad_sync_to"):
             if model.defer_grad_sync_to(optimizer):
                 model.set_slab_sink(optimizer)  # and the conv1 slab sums (exchanged in the same launch)
-        elif scaler is not None and getattr(scaler, "_enabled", False) and hasattr(model, "set_slab_sink"):
-            # no DDP: the fused AMP step also sums the conv1 weight-gradient slab (models/convnet.py)
+        elif fused and hasattr(model, "set_slab_sink"):
+            # no DDP: the fused step also sums the conv1 weight-gradient slab (models/convnet.py)
             model.set_slab_sink(optimizer)
         self.global_step = 0
         # the model's first kernel gathers the batch itself (no gather launch per step)

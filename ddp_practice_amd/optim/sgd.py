@@ -9,6 +9,8 @@ reference: /root/reference/origin_main.py:87, ddp_main.py:125 —
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch.optim import Optimizer
 
@@ -26,8 +28,16 @@ def _undecorated(name):
     return getattr(fn, "__wrapped__", fn)
 
 
+# the plain step on the fused launch (slab sums and the deferred DDP average inside it);
+# DPA_PLAIN_FUSED=0: the multi-tensor SGD launch after separate reductions (A/B runs)
+_PLAIN_FUSED = os.environ.get("DPA_PLAIN_FUSED", "1") != "0"
+
+
 class SGD(Optimizer):
     supports_device_found_inf = True
+    # step() without a GradScaler runs the fused launch when _fuse_kind() is "small", so
+    # the engine may hand it the deferred slab / DDP average (engine.TrainLoop)
+    plain_fused = _PLAIN_FUSED
 
     add_param_group = _undecorated("add_param_group")
     zero_grad = _undecorated("zero_grad")
@@ -99,6 +109,9 @@ class SGD(Optimizer):
 
     @torch.no_grad()
     def step(self, closure=None, found_inf: torch.Tensor | None = None):
+        if closure is None and found_inf is None and _PLAIN_FUSED and self._fuse_kind() == "small":
+            self._fused_plain_step()
+            return None
         self._flush_deferred()
         loss = None
         if closure is not None:
@@ -277,6 +290,29 @@ class SGD(Optimizer):
                         group["weight_decay"], group["nesterov"], group["maximize"], first,
                         scale, tracker, found_inf, growth, backoff, interval, sync, xc,
                         ps[0] if ps is not None else None, ps[1] if ps is not None else None)
+        if xc is not None:
+            d[0].consume_deferred()
+
+    def _fused_plain_step(self):
+        """torch.optim.SGD's update as one launch of the fused kernel without a scale
+        (csrc/kernels/amp_step.h amp_sgd_body, plain mode): a deferred conv1 slab is summed
+        and a deferred DDP average exchanged inside it, as in the AMP step."""
+        (group, params, grads, bufs, first), = self._collect()
+        if "_pending_wgrad1" in self.__dict__:
+            self.flush_slab()  # the AMP-only deferral (convnet_amp_step): its launches first
+        sync = getattr(self, "_amp_sync", None)
+        if sync is None or sync.device != params[0].device:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("SGD: the fused step's state must exist before graph capture "
+                                   "(run one eager step first)")
+            sync = self._amp_sync = torch.zeros(4, dtype=torch.int64, device=params[0].device)
+        d = getattr(self, "_deferred_ddp", None)
+        xc = d[1] if d is not None and d[0].deferred_pending() else None
+        ps = self.__dict__.pop("_pending_slab", None)
+        _load_ext().optim.amp_sgd_fused(params, grads, bufs, group["lr"], group["momentum"], group["dampening"],
+                                        group["weight_decay"], group["nesterov"], group["maximize"], first,
+                                        None, None, None, 1.0, 1.0, 1, sync, xc,
+                                        ps[0] if ps is not None else None, ps[1] if ps is not None else None)
         if xc is not None:
             d[0].consume_deferred()
 

@@ -21,8 +21,9 @@ def _train(model, ds, batch, scaler_on, use_graph, sampler=None, epochs=2):
     opt = SGD(model.parameters(), lr=0.05)
     scaler = GradScaler() if scaler_on else None
     loop = TrainLoop(model, CrossEntropyLoss(), opt, loader, scaler, use_graph=use_graph, steps_per_graph=4)
-    if scaler_on and hasattr(model, "defer_grad_sync_to"):
-        # DDP + fused AMP step over the xGMI engine: gradients averaged inside the optimizer kernel
+    if (scaler_on or opt.plain_fused) and hasattr(model, "defer_grad_sync_to"):
+        # DDP + fused step (AMP, or fp32's plain one) over the xGMI engine: gradients averaged
+        # inside the optimizer kernel
         assert getattr(opt, "_deferred_ddp", None) is not None
     for e in range(epochs):
         if sampler is not None:

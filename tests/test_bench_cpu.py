@@ -56,7 +56,10 @@ def test_bench_hung_rank_falls_back_with_comm_error():
     """rank 1 hangs at step 3 -> both ranks' watchdogs report and exit 124 (no
     30-min gloo stall), the supervisor re-runs fresh ranks (--comm rccl) and prints ONE line
     carrying the value, ``fallback`` and the first attempt's ``comm_error``; rc 0."""
-    r = _bench(_SMALL, extra_env={"DPA_FAULT": "1:3:hang", "DPA_BENCH_WATCHDOG": "4"})
+    # the healthy fallback must not trip the watchdog: scripts/asan_check.sh runs every step
+    # several times slower and stretches the budget through DPA_TEST_TIME_SCALE
+    wd = 4 * float(os.environ.get("DPA_TEST_TIME_SCALE", "1"))
+    r = _bench(_SMALL, extra_env={"DPA_FAULT": "1:3:hang", "DPA_BENCH_WATCHDOG": f"{wd:g}"})
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
     recs = _json_lines(r.stdout)
     assert len(recs) == 1

@@ -360,6 +360,66 @@ def test_slab_sink_matches_separate_sums(C, dtype, defer, monkeypatch):
         assert torch.equal(sd_a[k], sd_b[k]), k
 
 
+def test_fp32_plain_fused_step_with_slab_sink(C, monkeypatch):
+    """fp32 without a GradScaler: SGD.step() runs the fused launch (no scale), which also sums
+    the conv1 weight-gradient slab -- no slab_reduce, no multi-tensor SGD launch -- and the fc
+    weight gradient rides in the conv2 weight-gradient launch; the training equals the
+    separate launches (DPA_PLAIN_FUSED=0 path), eagerly and graph-replayed."""
+    from ddp_practice_amd.data import DeviceLoader, synthetic
+    from ddp_practice_amd.nn import CrossEntropyLoss
+    from ddp_practice_amd.optim import SGD, sgd as sgd_mod
+    from ddp_practice_amd.runtime import CapturedStep
+
+    ds = synthetic(32 * 12, seed=5)
+    runs = []
+    orig_sr, orig_sgd, orig_fc = C.convblock.slab_reduce, C.optim.sgd_step, C.convnet.fc_wgrad
+    for fused in (False, True):
+        monkeypatch.setattr(sgd_mod, "_PLAIN_FUSED", fused)
+        m = _model()
+        loader = DeviceLoader(ds, batch_size=32, shuffle=False, device=DEV, dtype=torch.float32)
+        images, labels = loader.static_batch()
+        opt, crit = SGD(m.parameters(), lr=0.05, momentum=0.9), CrossEntropyLoss()
+        if fused:
+            assert m.set_slab_sink(opt)
+        calls = [0, 0, 0]
+
+        def spy(i, f):
+            def g(*a, **k):
+                calls[i] += 1
+                return f(*a, **k)
+            return g
+
+        def step():
+            loader.fill_(images, labels, defer=True)
+            loss = crit(m(images), labels)
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+            opt.step()
+
+        C.convblock.slab_reduce, C.optim.sgd_step = spy(0, orig_sr), spy(1, orig_sgd)
+        C.convnet.fc_wgrad = spy(2, orig_fc)
+        try:
+            loader.start_epoch()
+            step()  # momentum buffers created: the first step may take either path
+            calls[:] = [0, 0, 0]
+            for _ in range(2):
+                step()
+            eager_calls = list(calls)
+            runner = CapturedStep(step, warmup=1, steps_per_graph=2)
+            assert runner.capture()
+            for _ in range(3):
+                runner.run()
+        finally:
+            C.convblock.slab_reduce, C.optim.sgd_step, C.convnet.fc_wgrad = orig_sr, orig_sgd, orig_fc
+        torch.cuda.synchronize()
+        assert "_pending_slab" not in opt.__dict__
+        runs.append((copy.deepcopy(m.state_dict()), eager_calls))
+    (sd_a, calls_a), (sd_b, calls_b) = runs
+    assert calls_a == [2, 2, 0] and calls_b == [0, 0, 0], (calls_a, calls_b)
+    for k in sd_a:
+        torch.testing.assert_close(sd_a[k].float(), sd_b[k].float(), rtol=1e-5, atol=1e-6, msg=k)
+
+
 def test_slab_sink_flushes_for_grad_readers(C):
     """With a slab sink, .grad read through GradScaler.unscale_ (or accumulated over two
     backward passes) equals the no-sink gradients."""

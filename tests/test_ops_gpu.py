@@ -290,6 +290,56 @@ def test_fused_amp_sgd_matches_unfused(C, momentum, sizes):
     assert int(sync[0]) == (0 if solo else 8)
 
 
+@pytest.mark.parametrize("momentum,damp,nesterov", [(0.0, 0.0, False), (0.9, 0.0, True), (0.9, 0.1, False)])
+@pytest.mark.parametrize("sizes", [(7, 3000, 29034), (5, 200001, 33), (7, 33, 100)])
+def test_fused_plain_sgd_matches_torch_sgd(C, momentum, damp, nesterov, sizes):
+    """The fused launch without a scale (optim.SGD's plain step) == torch.optim.SGD: no
+    unscale, no skip on non-finite gradients (torch applies them), no barrier generation
+    used; eager and graph-replayed."""
+    torch.manual_seed(1)
+    ps = [torch.randn(n, device=DEV) for n in sizes]
+    pa = [p.clone() for p in ps]
+    pr = [nn.Parameter(p.clone()) for p in ps]
+    ref = torch.optim.SGD(pr, lr=0.05, momentum=momentum, dampening=damp, nesterov=nesterov, weight_decay=1e-4)
+    ba = [torch.zeros_like(p) for p in ps]
+    ga = [torch.empty_like(p) for p in ps]
+    sync = torch.zeros(4, dtype=torch.int64, device=DEV)
+
+    def fused(first):
+        C.optim.amp_sgd_fused(pa, ga, ba if momentum else [], 0.05, momentum, damp, 1e-4, nesterov, False,
+                              [int(first)] * len(ps) if momentum and damp else [], None, None, None, 1.0, 1.0, 1,
+                              sync, None)
+
+    graph = None
+    for it in range(6):
+        gs = [torch.randn_like(p) for p in ps]
+        if it == 5:
+            gs[0][3] = float("nan")
+        for x, g in zip(ga, gs):
+            x.copy_(g)
+        for q, g in zip(pr, gs):
+            q.grad = g.clone()
+        if it < 3:
+            fused(it == 0)
+        else:
+            if graph is None:
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    fused(False)
+            graph.replay()
+        ref.step()
+        torch.cuda.synchronize()
+        for x, q, g in zip(pa, pr, gs):
+            torch.testing.assert_close(x, q.detach(), rtol=1e-6, atol=1e-6, equal_nan=True)
+        for x, g in zip(ga, gs):
+            assert torch.equal(x, g) or torch.equal(x.isnan(), g.isnan())  # the gradient is left as it was
+        if momentum:
+            for b, q in zip(ba, pr):
+                torch.testing.assert_close(b, ref.state[q]["momentum_buffer"], rtol=1e-6, atol=1e-6, equal_nan=True)
+    assert bool(pa[0][3].isnan())  # applied, as torch does
+    assert int(sync[0]) == 0 and int(sync[3]) == 0  # no barrier generation, no error
+
+
 def test_grad_scaler_fast_backward_and_fused_step(C):
     """scaler.scale(loss).backward() seeds with the scale; fused step == torch GradScaler + SGD."""
     from ddp_practice_amd.amp import GradScaler
