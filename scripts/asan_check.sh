@@ -18,6 +18,8 @@ export DPA_EXT_SO=$ROOT/ddp_practice_amd/_C_asan.so
 # is invalid accesses, use-after-free, races on object lifetimes and UB
 export ASAN_OPTIONS=detect_leaks=0:abort_on_error=1:print_summary=1:halt_on_error=1
 export UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1
+# time budgets in the tests (watchdogs) stretch for the sanitized interpreter
+export DPA_TEST_TIME_SCALE=4
 TESTS=${*:-tests/test_ddp_cpu.py tests/test_aux_cpu.py tests/test_amp_optim_cpu.py tests/test_data_cpu.py tests/test_resnet_cpu.py tests/test_bench_cpu.py tests/test_comm_selftest_cpu.py tests/test_bntap_cpu.py tests/test_ext_digest_cpu.py}
 ./build/asan_python -c "import ctypes, sys; from ddp_practice_amd import _ext; C = _ext.load(); \
 print('extension:', C.__file__, '| asan runtime:', hasattr(ctypes.CDLL(None), '__asan_init'))" \
