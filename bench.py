@@ -365,7 +365,7 @@ class _Chunks:
         self.step, self.spg, self.loader, self.nfull = step, max(1, spg), loader, nfull
         self.graphs = graphs
         self.health = health
-        self._mk = lambda k: CapturedStep(step, warmup=1, steps_per_graph=k, enabled=graphs,
+        self._mk = lambda k: CapturedStep(step, warmup=2, steps_per_graph=k, enabled=graphs,
                                           pre_capture=lambda: loader.set_step(0))
         self.runners: dict = {}
         self.pos = 0

@@ -38,6 +38,7 @@
 #include <c10/hip/HIPGuard.h>
 
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 
 #include "comm/xgmi.h"

@@ -74,8 +74,16 @@ struct XSite {
 // only needed by xsite_exchange: its round trip hides behind the caller's slab loads).
 // bid: the workgroup's index among the launch's workgroups on this site.
 __device__ __forceinline__ unsigned long long xsite_ticket(const XSite& xs, int bid) {
+  // (a plain load and advancing the words after the exchange measured no faster on the
+  // forced step: profiles/r5o_xsite_mode_ab.txt)
   return __hip_atomic_load(xs.tick + (bid < kEpochWords ? bid : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+#if defined(DPA_TIMING) && defined(DPA_STAMP)
+#define DPA_XS_STAMP(i) DPA_STAMP(i)
+#else
+#define DPA_XS_STAMP(i) do {} while (0)
+#endif
 
 // The launch's epoch from the word xsite_ticket read.
 __device__ __forceinline__ uint32_t xsite_epoch(const XSite& xs, unsigned long long tk, int bid) {
@@ -140,6 +148,7 @@ __device__ __forceinline__ void xsite_exchange(const XSite& xs, float* vals, int
   const bool pusher = bid == 0;
   if (tid == 0) ep_s = xsite_epoch(xs, tk, bid);
   __syncthreads();
+  DPA_XS_STAMP(13);
   xsite_advance(xs, ep_s, bid, nthr);
   if (tid < n) {
     const uint32_t ep = ep_s;
@@ -173,7 +182,9 @@ __device__ __forceinline__ void xsite_exchange(const XSite& xs, float* vals, int
     }
     vals[tid] = acc;  // only this lane reads or writes slot tid in here
   }
+  DPA_XS_STAMP(14);
   __syncthreads();
+  DPA_XS_STAMP(15);
 }
 
 // ---------------------------------------------------------------------------

@@ -231,6 +231,13 @@ void register_runtime(pybind11::module& m) {
   s.def("range_push", [](const std::string& name) { return roctxRangePushA(name.c_str()); });
   s.def("range_pop", []() { return roctxRangePop(); });
   s.def("mark", [](const std::string& name) { roctxMarkA(name.c_str()); });
+  // Upload an instantiated graph (torch.cuda.CUDAGraph.raw_cuda_graph_exec()) to the device on
+  // the current stream without running it: the first replay of a captured step otherwise pays
+  // the upload inside the timed / training loop (runtime/graph.py CapturedStep.capture)
+  s.def("graph_upload", [](uintptr_t exec) {
+    TORCH_CHECK(exec != 0, "graph_upload: no instantiated graph");
+    DPA_CHECK_HIP(hipGraphUpload(reinterpret_cast<hipGraphExec_t>(exec), c10::hip::getCurrentHIPStream().stream()));
+  });
 }
 
 }  // namespace dpa

@@ -148,7 +148,7 @@ class TrainLoop:
         if k in self._graphs:
             return self._graphs[k]
         snap = _snapshot(self.model, self.optimizer, self.scaler)
-        g = CapturedStep(lambda: self._step(), warmup=1, steps_per_graph=k,
+        g = CapturedStep(lambda: self._step(), warmup=2, steps_per_graph=k,
                          pre_capture=lambda: _restore(self.model, self.optimizer, self.scaler, snap))
         ctr = self.loader._ctr.clone() if self.loader._ctr is not None else None
         ok = g.capture()

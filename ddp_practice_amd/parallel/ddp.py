@@ -186,7 +186,14 @@ class DistributedDataParallel(nn.Module):
     def forward(self, *inputs, **kwargs):
         if self.reducer is not None and torch.is_grad_enabled() and self.module.training:
             if self._iteration == 1 and not self._rebuilt:
-                self._rebuild_buckets()
+                if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+                    # a re-plan inside a hipGraph capture would allocate and zero the new bucket
+                    # buffers as graph nodes (a fill re-run on every replay), and graphs captured
+                    # later would hold other buffers than this one: keep the first plan (warm up
+                    # with two eager steps to get the ready-order one, as engine / bench do)
+                    self._rebuilt = True
+                else:
+                    self._rebuild_buckets()
             self.reducer.prepare_for_backward(self._sync_enabled)
             self._iteration += 1
         if self._buffers_need_sync and self.comm.active and self.require_forward_param_sync:

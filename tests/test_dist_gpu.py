@@ -241,3 +241,48 @@ def test_resnet_syncbn_sites_match_launch_path(rccl, monkeypatch, amp):
             same(b1[k], b0[k], k)
         else:
             assert torch.equal(b0[k], b1[k]), k
+
+
+def test_ddp_bucket_replan_never_inside_capture(rccl):
+    """DDP re-plans its buckets at iteration 1's forward; when that forward is being captured
+    (CapturedStep warm-up of one step) the plan is kept instead: a re-plan would allocate and
+    zero the new bucket buffers as graph nodes re-run on every replay (round 4's forced
+    steady table showed that FillFunctor<float>).  No fill / zero op is issued under capture."""
+    from torch.utils._python_dispatch import TorchDispatchMode
+
+    from ddp_practice_amd.models import ConvNet
+    from ddp_practice_amd.nn import CrossEntropyLoss
+    from ddp_practice_amd.optim import SGD
+    from ddp_practice_amd.parallel import DistributedDataParallel
+    from ddp_practice_amd.runtime import CapturedStep
+
+    torch.manual_seed(0)
+    ddp = DistributedDataParallel(ConvNet().cuda(), device_ids=[0], bucket_cap_mb=0.01)
+    opt, crit = SGD(ddp.parameters(), lr=0.01), CrossEntropyLoss()
+    x = torch.randn(32, 1, 28, 28, device="cuda")
+    y = torch.randint(0, 10, (32,), device="cuda")
+    fills = []
+
+    class Spy(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            name = func.__name__.split(".")[0].strip("_")
+            if name in ("fill", "zero", "zeros", "full") and torch.cuda.is_current_stream_capturing():
+                fills.append(str(func))
+            return func(*args, **(kwargs or {}))
+
+    def step():
+        loss = crit(ddp(x), y)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+
+    before = [list(b) for b in ddp.reducer.bucket_indices()]
+    runner = CapturedStep(step, warmup=1, steps_per_graph=2)
+    with Spy():
+        assert runner.capture()
+    assert fills == [], fills
+    assert ddp._rebuilt and [list(b) for b in ddp.reducer.bucket_indices()] == before
+    for _ in range(3):
+        runner.run()
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(p).all() for p in ddp.parameters())
