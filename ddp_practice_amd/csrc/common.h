@@ -30,6 +30,23 @@ typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
 
 inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
+// Non-finite check of AMP gradients by the kernels that produce them (the ConvNet's
+// pre-checked optimizer step, optim/sgd.py): the step's head launch clears word[0] (and
+// records the scale in word[1]); a producer lane that writes a (scaled) value that is
+// non-finite -- or, for partial rows summed later, could overflow the sum (|v| > bound =
+// FLT_MAX / rows) -- sets word[0].  The fused AMP step reads the word and agrees on found_inf
+// without a grid barrier.  Scaled and unscaled finiteness agree while the scale is >= 1
+// (unscaling only shrinks); the step takes the barrier for a smaller scale.
+struct GradChk {
+  int* word = nullptr;  // nullptr: no check
+  __device__ __forceinline__ static bool bad(float v, float bound) {
+    return !(fabsf(v) <= bound);  // NaN / inf / beyond the bound
+  }
+  __device__ __forceinline__ void flag(bool b) const {
+    if (b) *word = 1;  // (every writer stores the same value; ordered by the kernel boundary)
+  }
+};
+
 #define DPA_CHECK_HIP(expr)                                                          \
   do {                                                                               \
     hipError_t _e = (expr);                                                          \

@@ -138,7 +138,8 @@ __device__ __forceinline__ void
 amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ tracker, float* __restrict__ found_inf,
              unsigned long long* __restrict__ sync, float lr, float momentum, float dampening, float wd, int nesterov,
              int maximize, float growth, float backoff, int interval, const xgmi::XSite& xg, int* __restrict__ err,
-             long long barrier_ticks, const SlabSet& ss, int grid, int bid) {
+             long long barrier_ticks, const SlabSet& ss, int grid, int bid, const int* __restrict__ chk = nullptr,
+             int nchk = 0) {
   constexpr int BG = THR * U;  // float4 granules per workgroup
   __shared__ int soff[MAXT + 1];
   __shared__ int snum[MAXT];
@@ -179,6 +180,17 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
     gen = __hip_atomic_fetch_add(&sync[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   unsigned long long tk = 0;
   if (XG && tid == 0) tk = xgmi::xsite_ticket(xg, bid);
+  // chk (pre-checked gradients, common.h GradChk): the producers' words -- every workgroup
+  // reads all of them, so all agree on found_inf with no grid barrier -- and the scale of the
+  // step (word nchk: block 0 may rewrite scale[0] while a late workgroup starts).  Valid for
+  // a scale >= 1 only (the words describe the scaled values): else the barrier, as without
+  bool cbad = false;
+  float cscale = 1.f;
+  if (chk != nullptr) {
+    for (int i = tid; i < nchk; i += THR) cbad |= chk[i] != 0;
+    cscale = __int_as_float(chk[nchk]);
+  }
+  const bool pre = chk != nullptr && cscale >= 1.f;  // uniform: every workgroup reads the same word
   auto load4 = [](const float* p, int rem) {
     if (rem >= 4) return *reinterpret_cast<const f32x4*>(p);
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -383,9 +395,9 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
         for (int j = 0; j < 4; ++j) bad |= !isfinite(gv[k][j]);
   // scale read before arriving: block 0 rewrites it once everyone has arrived, and a
   // workgroup that reads it late must not unscale with the next step's value
-  const float inv = amp ? 1.f / scale[0] : 1.f;
-  const bool block_bad = __syncthreads_or(bad);
-  if (grid == 1 || !amp) {  // uniform: one workgroup (or the plain step) needs no grid barrier
+  const float inv = pre ? 1.f / cscale : amp ? 1.f / scale[0] : 1.f;
+  const bool block_bad = __syncthreads_or(pre ? cbad : bad);
+  if (grid == 1 || !amp || pre) {  // uniform: one workgroup, the plain step or pre-checked gradients need no grid barrier
     if (tid == 0) s_bad = block_bad;
   } else if (tid == 0) {
     // arrival words of this launch's parity: one (blanes == 1) or blanes, kBarStride apart

@@ -311,6 +311,10 @@ struct BwdIn {
   float* dgamma;          // written by workgroup 0 when non-null
   float* dbeta;
   xgmi::XSite xs;         // active: gsum holds local rows, exchanged in here (comm/xsite.h)
+  GradChk chk;            // producer-side non-finite check (common.h; not with xs active):
+  int chk_coef = 0;       //   1: workgroup 0's dgamma / dbeta
+  int chk_rows = 0;       //   1: the weight-gradient workgroups' partial rows (|v| <= chk_row_bound)
+  float chk_row_bound = 0.f;
 };
 
 // Column sums of rows x RL floats (row-major) -> out[0..RL) in LDS, using the
@@ -349,6 +353,7 @@ __device__ __forceinline__ void bn_bwd_coef(const BwdIn<T>& bi, float* coef, flo
   const bool xon = bi.xs.active();
   unsigned long long tk = 0;
   if (xon && tid == 0) tk = xgmi::xsite_ticket(bi.xs, bid);  // latency hides behind the slab loads
+  const bool cchk = leader && bi.dgamma != nullptr && bi.chk_coef && !xon;  // producer-side check
   colsum_rows(bi.gsum, bi.grows, 2 * C, part, sums);
   if (xon) {
     // dgamma / dbeta are this rank's (DDP averages them); the coefficients use the global sums
@@ -380,6 +385,8 @@ __device__ __forceinline__ void bn_bwd_coef(const BwdIn<T>& bi, float* coef, flo
       bi.dbeta[tid] = sums[tid];
     }
   }
+  if (cchk && tid < C)  // the values just written
+    bi.chk.flag(GradChk::bad(sums[C + tid], 3.402823466e38f) || GradChk::bad(sums[tid], 3.402823466e38f));
 }
 
 // Produce dy[c][h][w] of image b for every 2x2 window.  Two phases so that the
@@ -1301,7 +1308,7 @@ bwd_elemt_kernel(const T* __restrict__ dp, const T* __restrict__ p, const uint8_
 // (bin: backward through MaxPool -> ReLU -> BN); needs ROWS == H.
 // WT: the partial row is stored write-through (sc1) for an in-launch reduction
 // (MI355X_MICROARCH.md "Valid forms" row 1; convnet_fused.hip wgrad1_reduce_kernel).
-template <typename T, int CIN, int COUT, int H, int W, int ROWS, int PRO = 0, bool WT = false>
+template <typename T, int CIN, int COUT, int H, int W, int ROWS, int PRO = 0, bool WT = false, bool CHK = false>
 __device__ __forceinline__ void
 conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __restrict__ wslab, int nsplit,
                    const BwdIn<T>& bin, const int bid) {
@@ -1346,6 +1353,8 @@ conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __r
   const int tid = threadIdx.x;
   const int b = bid / nsplit, sp = bid % nsplit;
   DPA_STAMP(0);
+  // producer-side check of this workgroup's partial row (BwdIn::chk_row_slot0, common.h)
+  const bool rchk = CHK && bin.chk_rows;  // (compiled only where a launch can ask for it)
   const int r0 = sp * ROWS;
   const T* xb = x + (size_t)b * CIN * H * W;
   // input rows r0-2 .. r0+ROWS+1 -> xpad interior; all loads issued before the
@@ -1521,6 +1530,7 @@ conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __r
       for (int i = 0; i < 4; ++i) {
         if constexpr (STAGE) wtile[(mt * 16 + 4 * q + i) * N + nat] = acc[i];
         else put(&row_out[(mt * 16 + 4 * q + i) * N + nat], acc[i]);
+        if (rchk) bin.chk.flag(GradChk::bad(acc[i], bin.chk_row_bound));
       }
     }
   }
@@ -1556,7 +1566,8 @@ conv5x5_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, float* _
 constexpr int SR_COLS = 16, SR_GROUPS = NTHR / SR_COLS;
 __device__ __forceinline__ void slab_reduce_body(const float* __restrict__ slab1, int rows1, int n1,
                                                  float* __restrict__ out1, const float* __restrict__ slab2, int rows2,
-                                                 int n2, float* __restrict__ out2, int bid) {
+                                                 int n2, float* __restrict__ out2, int bid,
+                                                 GradChk chk = GradChk{}) {
   __shared__ float part[SR_GROUPS][SR_COLS + 1];
   const int nb1 = (n1 + SR_COLS - 1) / SR_COLS;
   const bool first = bid < nb1;
@@ -1573,6 +1584,7 @@ __device__ __forceinline__ void slab_reduce_body(const float* __restrict__ slab1
 #pragma unroll
     for (int gg = 0; gg < SR_GROUPS; ++gg) t += part[gg][threadIdx.x];
     out[c0 + threadIdx.x] = t;
+    if (chk.word != nullptr) chk.flag(GradChk::bad(t, 3.402823466e38f));  // (producer-side check, common.h)
   }
 }
 static __global__ void __launch_bounds__(NTHR)

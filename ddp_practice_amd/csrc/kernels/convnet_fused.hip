@@ -498,6 +498,7 @@ struct FcW {
   float* dw;     // [N][K]
   float* db;     // [N]
   int B = 0, N = 0;
+  GradChk chk;   // producer-side check (common.h)
 };
 constexpr int FC_K = 32 * 49;
 constexpr int FC_COLS = cb::NTHR;  // columns per workgroup, one per lane
@@ -510,6 +511,7 @@ __device__ __forceinline__ void fc_wgrad_body(const FcW<T>& f, int wg) {
   const int tid = threadIdx.x;
   const int col = wg * FC_COLS + tid, cc = min(col, FC_K - 1);
   const int B = f.B, N = f.N;
+  const bool chk = f.chk.word != nullptr;  // producer-side check (common.h GradChk)
   // the dls table (B x N, zero-padded to 16 classes) through LDS, broadcast reads below
   for (int e = tid; e < FC_BMAX * FC_NMAX; e += cb::NTHR) {
     const int b = e / FC_NMAX, n = e % FC_NMAX;
@@ -540,16 +542,22 @@ __device__ __forceinline__ void fc_wgrad_body(const FcW<T>& f, int wg) {
       }
     }
   }
+  bool bad = false;
   if (col < FC_K) {
 #pragma unroll
     for (int n = 0; n < FC_NMAX; ++n)
-      if (n < N) f.dw[(size_t)n * FC_K + col] = acc[n];
+      if (n < N) {
+        f.dw[(size_t)n * FC_K + col] = acc[n];
+        bad |= GradChk::bad(acc[n], 3.402823466e38f);
+      }
   }
   if (wg == 0 && tid < N) {
     float a = 0.f;
     for (int b = 0; b < B; ++b) a += dl_s[b][tid];
     f.db[tid] = a;
+    bad |= GradChk::bad(a, 3.402823466e38f);
   }
+  if (chk) f.chk.flag(bad);
 }
 
 template <typename T>
@@ -616,6 +624,18 @@ void fc_wgrad(at::Tensor dls, at::Tensor p2, at::Tensor dw, at::Tensor db) {
   DPA_CHECK_LAUNCH();
 }
 
+// The producer-side gradient check's words (optim/sgd.py prechecked AMP step; common.h
+// GradChk): int32[2], [0] cleared by the head launch and set by any producer lane that
+// writes a bad value, [1] the step's scale (recorded by the head launch).
+static GradChk grad_chk_of(const c10::optional<at::Tensor>& chk) {
+  GradChk g;
+  if (!chk.has_value()) return g;
+  DPA_CHECK_INPUT(*chk);
+  TORCH_CHECK(chk->scalar_type() == at::kInt && chk->numel() == 2, "gradient check: int32[2] words");
+  g.word = chk->data_ptr<int>();
+  return g;
+}
+
 // [pool2/ReLU2/BN2 backward] -> {conv2 data grad -> dp1 (+BN1 partial sums), conv2 weight-grad partials}
 // (+ with fc_*: the fc weight / bias gradient of the per-image head in extra workgroups).
 // gsum2: rows of BN2 backward sums ([S1 | S2] per row, summed here); lsum2: this rank's rows
@@ -624,7 +644,8 @@ void conv2_bwd(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx2,
                at::Tensor gsum2, at::Tensor g2, double eps2, at::Tensor dp1, at::Tensor idx1, at::Tensor xh1,
                at::Tensor bslab1, at::Tensor p1, at::Tensor wslab2, XcPtr xc, c10::optional<at::Tensor> lsum2,
                c10::optional<at::Tensor> dg2, c10::optional<at::Tensor> dbe2, c10::optional<at::Tensor> fc_dls,
-               c10::optional<at::Tensor> fc_p2, c10::optional<at::Tensor> fc_dw, c10::optional<at::Tensor> fc_db) {
+               c10::optional<at::Tensor> fc_p2, c10::optional<at::Tensor> fc_dw, c10::optional<at::Tensor> fc_db,
+               c10::optional<at::Tensor> chk) {
   DPA_CHECK_INPUT(y2); DPA_CHECK_INPUT(dp1); DPA_CHECK_INPUT(wpk_d); DPA_CHECK_INPUT(p1); DPA_CHECK_INPUT(wslab2);
   TORCH_CHECK(wpk_d.numel() == cb::W2D_LEN && wpk_d.scalar_type() == y2.scalar_type(),
               "packed conv2 data-grad weights");
@@ -651,6 +672,11 @@ void conv2_bwd(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx2,
     BwdEpi<T> ep{idx1.data_ptr<uint8_t>(), dptr<T>(xh1), bslab1.data_ptr<float>()};
     FcW<T> fw = fc_args<T>(fc_dls, fc_p2, fc_dw, fc_db, B, y2.scalar_type());
     const int nfc = fc_dls.has_value() ? FC_BLOCKS : 0;
+    if (chk.has_value()) {  // every gradient this launch finishes: BN2's, the fc layer's
+      TORCH_CHECK(!xc && nfc > 0 && dg2.has_value(), "gradient check: the single-rank launch with the fc role");
+      bd.chk = fw.chk = grad_chk_of(chk);
+      bd.chk_coef = 1;
+    }
     if constexpr (std::is_same<T, float>::value) {
       // fp32 tiles: the two roles' LDS (173 KB) exceed one CU's 160 KB -> separate launches
       // (the fc weight gradient: extra workgroups of the weight-gradient launch; its site's
@@ -853,17 +879,18 @@ void wgrad1_reduce(at::Tensor x, at::Tensor y1, at::Tensor dp1, at::Tensor idx1,
 template <typename T>
 __global__ void __launch_bounds__(cb::NTHR)
 wgrad1_slab2_kernel(const T* __restrict__ x, float* __restrict__ wslab1, BwdIn<T> bi, int nwg1,
-                    const float* __restrict__ wslab2, int rows2, int n2, float* __restrict__ out2) {
+                    const float* __restrict__ wslab2, int rows2, int n2, float* __restrict__ out2, GradChk rc) {
   constexpr int ns = (28 + WG1_ROWS_ - 1) / WG1_ROWS_;
   if ((int)blockIdx.x < nwg1)
-    cb::conv5x5_wgrad_body<T, 1, 16, 28, 28, WG1_ROWS_, 2>(x, nullptr, wslab1, ns, bi, (int)blockIdx.x);
+    cb::conv5x5_wgrad_body<T, 1, 16, 28, 28, WG1_ROWS_, 2, false, true>(x, nullptr, wslab1, ns, bi, (int)blockIdx.x);
   else
-    cb::slab_reduce_body(nullptr, 0, 0, nullptr, wslab2, rows2, n2, out2, (int)blockIdx.x - nwg1);
+    cb::slab_reduce_body(nullptr, 0, 0, nullptr, wslab2, rows2, n2, out2, (int)blockIdx.x - nwg1, rc);
 }
 
 void conv1_wgrad_slab2(at::Tensor x, at::Tensor y1, at::Tensor dp1, at::Tensor idx1, at::Tensor fstats1,
                        at::Tensor gsum, c10::optional<at::Tensor> lsum, at::Tensor g1, double eps1, at::Tensor dg1,
-                       at::Tensor dbe1, at::Tensor wslab1, at::Tensor wslab2, at::Tensor out2, XcPtr xc) {
+                       at::Tensor dbe1, at::Tensor wslab1, at::Tensor wslab2, at::Tensor out2, XcPtr xc,
+                       c10::optional<at::Tensor> chk) {
   DPA_CHECK_INPUT(x); DPA_CHECK_INPUT(y1); DPA_CHECK_INPUT(wslab1); DPA_CHECK_INPUT(wslab2); DPA_CHECK_INPUT(out2);
   const int B = (int)y1.size(0);
   TORCH_CHECK(x.size(1) == 1 && y1.size(1) == 16 && y1.size(2) == 28 && x.scalar_type() == y1.scalar_type());
@@ -882,9 +909,17 @@ void conv1_wgrad_slab2(at::Tensor x, at::Tensor y1, at::Tensor dp1, at::Tensor i
       bi.xs = site_of(xc, xgmi::kSiteBwd1);
       xgmi::set_site_grid(bi.xs, nwg1, "conv1_wgrad_slab2");  // the reduction workgroups take no tickets
     }
+    GradChk rc;
+    if (chk.has_value()) {  // BN1's gradients, conv1's partial rows, conv2's column sums
+      TORCH_CHECK(!xc, "gradient check: the single-rank launch");
+      rc = bi.chk = grad_chk_of(chk);
+      bi.chk_coef = 1;
+      bi.chk_rows = 1;
+      bi.chk_row_bound = 3.402823466e38f / (float)nwg1;
+    }
     hipLaunchKernelGGL(wgrad1_slab2_kernel<T>, dim3(nwg1 + nred), dim3(cb::NTHR), 0, cur_stream(), dptr<T>(x),
                        wslab1.data_ptr<float>(), bi, nwg1, wslab2.data_ptr<float>(), rows2, N2,
-                       out2.data_ptr<float>());
+                       out2.data_ptr<float>(), rc);
   });
   DPA_CHECK_LAUNCH();
 }

@@ -73,6 +73,8 @@ struct HeadRow {
   void* dls;            // [B][N] dlog * scale, storage dtype (null without scaler)
   void* dp2;            // [B][K] storage dtype (null: forward + loss only)
   float* bsum;          // [B][2C] BN2 backward sums of each image (S1 | S2)
+  int* chk;             // producer-side gradient check words (common.h GradChk) or null:
+                        // cleared here, [1] = this step's scale
 };
 
 // lds_barrier (common.h): the global stores (pooled outputs, dp2) and the loss atomic are not waited
@@ -127,6 +129,10 @@ head_row_kernel(const T* __restrict__ y, BNParams bn, const float* __restrict__ 
   DPA_STAMP(1);
   cb::bn_finalize<C>(bn, sc_s, beta_s, mean_s, istd_s, part_s, b);  // ends with a barrier
   DPA_STAMP(2);
+  if (hr.chk != nullptr && b == 0 && tid == 0) {  // the step's gradient-check words (GradChk)
+    hr.chk[0] = 0;
+    hr.chk[1] = __float_as_int(scv);
+  }
   // 2. BN -> ReLU -> 2x2 max of this image; pooled value, argmax|relu index, xhat
   float pf[IT], xf[IT];
   uint8_t ixr[IT];
@@ -321,7 +327,8 @@ void head_step(at::Tensor y2, at::Tensor fslab2, at::Tensor fstats2, at::Tensor 
                at::Tensor logits, at::Tensor p2, at::Tensor idx2, at::Tensor xh2, at::Tensor target,
                int64_t ignore_index, double smoothing, c10::optional<at::Tensor> scale, at::Tensor state,
                at::Tensor loss, at::Tensor dlog, c10::optional<at::Tensor> dls, c10::optional<at::Tensor> dp2,
-               c10::optional<at::Tensor> bsum_rows, std::shared_ptr<xgmi::XgmiComm> xc) {
+               c10::optional<at::Tensor> bsum_rows, std::shared_ptr<xgmi::XgmiComm> xc,
+               c10::optional<at::Tensor> chk) {
   DPA_CHECK_INPUT(y2); DPA_CHECK_INPUT(wfc); DPA_CHECK_INPUT(logits); DPA_CHECK_INPUT(p2); DPA_CHECK_INPUT(target);
   DPA_CHECK_INPUT(bfc); DPA_CHECK_INPUT(idx2); DPA_CHECK_INPUT(xh2); DPA_CHECK_INPUT(dlog);
   const int B = (int)y2.size(0), N = (int)wfc.size(0);
@@ -373,6 +380,13 @@ void head_step(at::Tensor y2, at::Tensor fslab2, at::Tensor fstats2, at::Tensor 
   hr.smoothing = (float)smoothing;
   hr.scale = scale.has_value() ? scale->data_ptr<float>() : loss.data_ptr<float>();  // unread without a scaler
   hr.has_scale = scale.has_value() ? 1 : 0;
+  hr.chk = nullptr;
+  if (chk.has_value()) {
+    DPA_CHECK_INPUT(*chk);
+    TORCH_CHECK(chk->scalar_type() == at::kInt && chk->numel() == 2 && scale.has_value() && !xc,
+                "head_step: gradient-check words need the scaler's scale, one rank, int32[2]");
+    hr.chk = chk->data_ptr<int>();
+  }
   hr.state = reinterpret_cast<unsigned long long*>(state.data_ptr<int64_t>());
   hr.loss = loss.data_ptr<float>();
   hr.dlog = dlog.data_ptr<float>();

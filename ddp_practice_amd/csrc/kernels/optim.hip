@@ -124,12 +124,13 @@ __global__ void __launch_bounds__(THR)
 amp_sgd_fused_kernel(MTList L, float* __restrict__ scale, int* __restrict__ tracker, float* __restrict__ found_inf,
                      unsigned long long* __restrict__ sync, float lr, float momentum, float dampening, float wd,
                      int nesterov, int maximize, float growth, float backoff, int interval,
-                     xgmi::XSite xg, int* __restrict__ err, long long barrier_ticks, SlabSet ss, int grid) {
+                     xgmi::XSite xg, int* __restrict__ err, long long barrier_ticks, SlabSet ss, int grid,
+                     const int* __restrict__ chk, int nchk) {
   // grid == the launch's workgroup count, passed in: gridDim is a load from the hidden kernel
   // arguments on gfx950, and its wait at the top of the kernel came before the table loads
   DPA_STAMP(0);
   amp_sgd_body<U, XG, THR>(L, scale, tracker, found_inf, sync, lr, momentum, dampening, wd, nesterov, maximize,
-                           growth, backoff, interval, xg, err, barrier_ticks, ss, grid, (int)blockIdx.x);
+                           growth, backoff, interval, xg, err, barrier_ticks, ss, grid, (int)blockIdx.x, chk, nchk);
 }
 
 // ---------------------------------------------------------------------------
@@ -441,7 +442,7 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
                    std::vector<int64_t> first, c10::optional<at::Tensor> scale, c10::optional<at::Tensor> tracker,
                    c10::optional<at::Tensor> found_inf, double growth, double backoff, int64_t interval,
                    at::Tensor sync, std::shared_ptr<xgmi::XgmiComm> xc, c10::optional<at::Tensor> slab,
-                   c10::optional<at::Tensor> slab_out) {
+                   c10::optional<at::Tensor> slab_out, c10::optional<at::Tensor> prechk) {
   TORCH_CHECK(params.size() == grads.size() && params.size() <= (size_t)MAXT, "fused AMP-SGD: <= ", MAXT,
               " tensors");
   TORCH_CHECK(bufs.empty() || bufs.size() == params.size());
@@ -459,6 +460,16 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
   float* const fi = amp ? found_inf->data_ptr<float>() : nullptr;
   TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == at::kLong && sync.numel() >= 4 && sync.is_contiguous(),
               "fused AMP-SGD: sync must be a zero-initialised int64[4] device tensor");
+  // prechk: the producer kernels' gradient-check words + the scale they used (common.h GradChk)
+  const int* chk = nullptr;
+  int nchk = 0;
+  if (prechk.has_value()) {
+    DPA_CHECK_INPUT(*prechk);
+    TORCH_CHECK(amp && !xc && prechk->scalar_type() == at::kInt && prechk->numel() >= 2,
+                "fused AMP-SGD: pre-checked gradients need the scaler, one rank and int32 words");
+    chk = prechk->data_ptr<int>();
+    nchk = (int)prechk->numel() - 1;
+  }
   TORCH_CHECK(amp_sgd_resident(), "fused AMP-SGD: grid not co-resident on this device (use the unfused step)");
   MTList L = fused_list(params, grads, bufs, first, momentum);
   SlabSet ss;
@@ -472,7 +483,7 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
                        reinterpret_cast<unsigned long long*>(sync.data_ptr<int64_t>()), (float)lr, (float)momentum,
                        (float)dampening, (float)wd, (int)nesterov, (int)maximize, (float)growth, (float)backoff,
                        (int)interval, xg, reinterpret_cast<int*>(sync.data_ptr<int64_t>() + 3),
-                       (long long)(kBarrierSeconds * 1e8), ss, grid);
+                       (long long)(kBarrierSeconds * 1e8), ss, grid, chk, nchk);
   };
   if (xc) {
     const xgmi::XSite xg = xc->grad_site();
@@ -621,7 +632,8 @@ void register_optim(pybind11::module& m) {
         pybind11::arg("nesterov"), pybind11::arg("maximize"), pybind11::arg("first"), pybind11::arg("scale"),
         pybind11::arg("tracker"), pybind11::arg("found_inf"), pybind11::arg("growth"), pybind11::arg("backoff"),
         pybind11::arg("interval"), pybind11::arg("sync"), pybind11::arg("xc"),
-        pybind11::arg("slab") = pybind11::none(), pybind11::arg("slab_out") = pybind11::none());
+        pybind11::arg("slab") = pybind11::none(), pybind11::arg("slab_out") = pybind11::none(),
+        pybind11::arg("prechk") = pybind11::none());
   s.def("amp_sgd_xg_max", &opt::amp_sgd_xg_max);
   s.def("amp_sgd_resident", &opt::amp_sgd_resident);
   s.def("amp_sgd_table", &opt::amp_sgd_table, pybind11::arg("params"), pybind11::arg("grads"), pybind11::arg("bufs"),

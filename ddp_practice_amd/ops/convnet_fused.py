@@ -62,6 +62,9 @@ _WGRAD1_SLAB2 = os.environ.get("DPA_WGRAD1_SLAB2", "0") == "1"
 # through rows, arrival counter, polling) costs ~3 us, more than the kernel boundary it
 # removes.  Opt-in: DPA_DEFER_WGRAD1=1
 _DEFER_WGRAD1 = os.environ.get("DPA_DEFER_WGRAD1", "0") == "1"
+# producer-side gradient checks instead of the fused AMP step's grid barrier (single rank);
+# DPA_PRECHECK=0: the barrier (A/B runs)
+_PRECHECK = os.environ.get("DPA_PRECHECK", "1") != "0"
 _CAS_OK: dict = {}
 
 
@@ -186,6 +189,7 @@ class ConvNetFn(torch.autograd.Function):
             if sync and xc is None:
                 comm.all_reduce_(fslab2)
             ctx.spec = None
+            ctx.chk = ctx.chk_scale = None
             if labels is not None and state is not None and _head_step_ok(B, N, cdtype):
                 # labels known now (paired by the device loader): head forward + loss (+ the head
                 # backward when a GradScaler will seed it with its scale) in one launch
@@ -203,13 +207,21 @@ class ConvNetFn(torch.autograd.Function):
                     dp2 = torch.empty_like(p2)
                     bsum2 = torch.empty(B * 64, **f32)
                     spec = (dls, dp2, bsum2)
+                    # pre-checked gradients (single rank, slab sink): this launch clears the check
+                    # word the backward's producers set (optim/sgd.py set_prechecked)
+                    chk = None
+                    if (sink is not None and _PRECHECK and not sync and xc is None
+                            and hasattr(sink, "set_prechecked")):
+                        sink.clear_prechecked()  # the device word is reset below
+                        chk = sink.grad_chk(2, dev)
+                    ctx.chk, ctx.chk_scale = chk, (scale if chk is not None else None)
                     _load_ext().convnet_head.head_step(
                         y2, fslab2, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, wfc, bfc, logits, p2, idx2, xh2, labels,
-                        int(ce_cfg[0]), float(ce_cfg[1]), scale, state, loss_buf, dlog, dls, dp2, bsum2, xc)
+                        int(ce_cfg[0]), float(ce_cfg[1]), scale, state, loss_buf, dlog, dls, dp2, bsum2, xc, chk)
                 else:
                     _load_ext().convnet_head.head_step(
                         y2, fslab2, fstats2, g2, be2, rm2, rv2, nbt2, m2, e2, wfc, bfc, logits, p2, idx2, xh2, labels,
-                        int(ce_cfg[0]), float(ce_cfg[1]), None, state, loss_buf, dlog, None, None, None, xc)
+                        int(ce_cfg[0]), float(ce_cfg[1]), None, state, loss_buf, dlog, None, None, None, xc, None)
                 ctx.spec = spec
                 if holder is not None:
                     holder["ce"] = PreCE(labels, int(ce_cfg[0]), float(ce_cfg[1]), scale, loss_buf, dlog, dls)
@@ -228,6 +240,7 @@ class ConvNetFn(torch.autograd.Function):
         ctx.sink = sink
         ctx.w1b1 = (w1, b1) if sink is not None else None
         ctx.l12 = (w1, b1, g1, be1, w2, b2) if sink is not None else None
+        ctx.allp = (w1, b1, g1, be1, w2, b2, g2, be2, wfc, bfc) if sink is not None else None
         ctx.sync = sync
         ctx.comm = comm
         ctx.xc = xc
@@ -278,6 +291,17 @@ class ConvNetFn(torch.autograd.Function):
             gsum2, lsum2 = comm.all_reduce(bsum2), (bsum2 if dgb[0] is not None else None)
         else:
             gsum2, lsum2 = bsum2, None
+        # Pre-checked gradients (single rank, slab sink, AMP): the producer launches below record
+        # per workgroup whether a gradient they finish is non-finite once unscaled, so the fused
+        # AMP step agrees on found_inf without its grid barrier (optim/sgd.py set_prechecked)
+        sink0 = ctx.sink
+        chk, cscale = getattr(ctx, "chk", None), getattr(ctx, "chk_scale", None)
+        ctx.chk = ctx.chk_scale = None
+        if sink0 is not None and hasattr(sink0, "set_prechecked"):
+            sink0.clear_prechecked()  # an earlier backward's check no longer describes .grad
+        if not (chk is not None and fc[0] is not None and not _SPLIT_BWD2 and not _DEFER_WGRAD1
+                and all(p.grad is None for p in ctx.allp)):
+            chk = cscale = None
         # 2+3. BN2 bwd -> {conv2 dgrad -> dp1 (+ BN1 partial sums), conv2 wgrad partials}: one launch
         #      (DPA_SPLIT_BWD2=1: the two as separate launches, A/B runs)
         dp1 = torch.empty((B, 16, 14, 14), dtype=y1.dtype, device=dev)
@@ -294,7 +318,7 @@ class ConvNetFn(torch.autograd.Function):
                 cn.fc_wgrad(*fc)
         else:
             cn.conv2_bwd(wpk_d, y2, dp2, idx2, fstats2, gsum2, g2, e2, dp1, idx1, xh1, bslab1, p1, wslab2, xc,
-                         lsum2, dgb[0], dgb[1], *fc)
+                         lsum2, dgb[0], dgb[1], *fc, chk)
         # 4+5. BN1 bwd -> conv1 wgrad partials (+ dgamma1 / dbeta1 from the local sums), and the
         #      column sums of both weight-grad slabs -> [dW1 | db1], [dW2 | db2]: one launch
         #      (DPA_SPLIT_WGRAD1=1: wgrad launch + a separate reduction launch, A/B runs)
@@ -327,10 +351,14 @@ class ConvNetFn(torch.autograd.Function):
         elif sink is not None or _WGRAD1_SLAB2:
             # conv1 wgrad partials + the conv2 slab's column sums in one launch; the conv1
             # slab's sums run inside the fused AMP-SGD launch (optim.SGD.defer_slab) or next
+            if sink is None:
+                chk = cscale = None
             cn.conv1_wgrad_slab2(x, y1, dp1, idx1, fstats1, gsum1, lsum1, g1, e1, dg1, dbe1, wslab1, wslab2, out2,
-                                 xc1)
+                                 xc1, chk)
             if sink is not None:
                 sink.defer_slab(wslab1, out1)
+                if chk is not None:
+                    sink.set_prechecked(chk, cscale, out)
             else:
                 cb.slab_reduce(wslab1, n_w1 + 16, out1)
         elif _SPLIT_WGRAD1 or ctx.wcnt is None:

@@ -86,14 +86,35 @@ class SGD(Optimizer):
         self.flush_slab()
         self._pending_wgrad1 = w
 
+    def grad_chk(self, n: int, device) -> torch.Tensor | None:
+        """The int32 words of the ConvNet's producer-side gradient check (ops/convnet_fused.py:
+        the head launch clears them, the backward launches set them; no zero-fill).  Created
+        outside a graph capture only; None inside one when they do not exist yet."""
+        t = self.__dict__.get("_grad_chk")
+        if t is None or t.numel() != n or t.device != device:
+            if torch.cuda.is_current_stream_capturing():
+                return None
+            t = self._grad_chk = torch.empty(n, dtype=torch.int32, device=device)
+        return t
+
+    def set_prechecked(self, chk: torch.Tensor, scale: torch.Tensor, out: torch.Tensor) -> None:
+        """The gradients in ``out`` (one buffer holding every parameter's) were checked by their
+        producers against ``scale``: the next fused AMP step may read ``chk`` instead of agreeing
+        on found_inf at a grid barrier.  Any other gradient reader drops it (flush_slab)."""
+        self._prechecked = (chk, scale, out.data_ptr(), out.data_ptr() + out.numel() * out.element_size())
+
+    def clear_prechecked(self) -> None:
+        self.__dict__.pop("_prechecked", None)
+
     def flush_slab(self) -> None:
+        self.__dict__.pop("_prechecked", None)  # .grad may be read or changed from here on
         w = self.__dict__.pop("_pending_wgrad1", None)
         if w is not None:  # the launches the deferral saved
             C = _load_ext()
             out0 = w["out0"]  # [dbeta1 | dgamma1]
             C.convnet.conv1_wgrad_slab2(w["x"], w["y1"], w["dp1"], w["idx1"], w["fstats1"], w["gsum1"], w["lsum1"],
                                         w["g1"], w["e1"], out0.narrow(0, 16, 16), out0.narrow(0, 0, 16), w["wslab1"],
-                                        w["wslab2"], w["out2"], w["xc1"])
+                                        w["wslab2"], w["out2"], w["xc1"], None)
             C.convblock.slab_reduce(w["wslab1"], w["out1"].numel(), w["out1"])
         ps = self.__dict__.pop("_pending_slab", None)
         if ps is not None:
@@ -249,6 +270,7 @@ class SGD(Optimizer):
             sync = torch.zeros(4, dtype=torch.int64, device=params[0].device)
             setattr(self, name, sync)
         O = _load_ext().optim
+        pc = self.__dict__.pop("_prechecked", None)
         w1 = self.__dict__.get("_pending_wgrad1")
         if w1 is not None and kind != "small":
             self.flush_slab()
@@ -286,10 +308,16 @@ class SGD(Optimizer):
         # summed inside the launch (SlabSrc), and exchanged there with the other gradients
         # when the DDP average is fused in too (xc)
         ps = self.__dict__.pop("_pending_slab", None)
+        # producer-checked gradients (ops/convnet_fused.py): every gradient lies in the checked
+        # buffer and was unscaled against this scale -> no grid barrier in the launch
+        prechk = None
+        if (pc is not None and xc is None and ps is not None and pc[1] is scale
+                and all(pc[2] <= g.data_ptr() < pc[3] for g in grads)):
+            prechk = pc[0]
         O.amp_sgd_fused(params, grads, bufs, group["lr"], group["momentum"], group["dampening"],
                         group["weight_decay"], group["nesterov"], group["maximize"], first,
                         scale, tracker, found_inf, growth, backoff, interval, sync, xc,
-                        ps[0] if ps is not None else None, ps[1] if ps is not None else None)
+                        ps[0] if ps is not None else None, ps[1] if ps is not None else None, prechk)
         if xc is not None:
             d[0].consume_deferred()
 

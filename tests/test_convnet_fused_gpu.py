@@ -537,3 +537,117 @@ def test_deferred_wgrad1_graph_replay_waits_for_producers(C, monkeypatch):
     torch.cuda.synchronize()
     assert scaler._scale.item() == s0, "a replay saw a non-finite gradient (stale / poisoned conv1 rows)"
     assert all(torch.isfinite(p).all() for p in m.parameters())
+
+
+def _amp_run(dtype, precheck, monkeypatch, steps=3, scale=None, poison=False, graph=True):
+    """ConvNet AMP training with the slab sink (as engine.TrainLoop sets it up); returns the
+    final state, the scaler state and how many fused steps ran pre-checked."""
+    from ddp_practice_amd.amp import GradScaler
+    from ddp_practice_amd.data import DeviceLoader, synthetic
+    from ddp_practice_amd.nn import CrossEntropyLoss
+    from ddp_practice_amd.ops import convnet_fused
+    from ddp_practice_amd.optim import SGD
+    from ddp_practice_amd.runtime import CapturedStep
+
+    monkeypatch.setattr(convnet_fused, "_PRECHECK", precheck)
+    ds = synthetic(32 * 12, seed=7)
+    if poison:
+        ds.images[5] = 255  # a saturated image is still finite: the check must not trip on it
+    m = _model(seed=3)
+    m.amp_dtype = dtype
+    loader = DeviceLoader(ds, batch_size=32, shuffle=False, device=DEV, dtype=dtype)
+    images, labels = loader.static_batch()
+    opt, scaler, crit = SGD(m.parameters(), lr=0.05), GradScaler(), CrossEntropyLoss()
+    assert m.set_slab_sink(opt)
+    C = __import__("ddp_practice_amd._ext", fromlist=["load"]).load()
+    orig = C.optim.amp_sgd_fused
+    seen = []
+
+    def spy(*a, **k):
+        seen.append(a[-1] is not None if len(a) > 20 else k.get("prechk") is not None)
+        return orig(*a, **k)
+
+    def step():
+        loader.fill_(images, labels, defer=True)
+        loss = crit(m(images), labels)
+        opt.zero_grad(set_to_none=True)
+        scaler.scale(loss).backward()
+        scaler.step(opt)
+        scaler.update()
+
+    C.optim.amp_sgd_fused = spy
+    try:
+        loader.start_epoch()
+        step()
+        if scale is not None:
+            scaler._scale.fill_(scale)
+        for _ in range(steps):
+            step()
+        if graph:
+            runner = CapturedStep(step, warmup=1, steps_per_graph=2)
+            assert runner.capture()
+            for _ in range(2):
+                runner.run()
+    finally:
+        C.optim.amp_sgd_fused = orig
+    torch.cuda.synchronize()
+    return copy.deepcopy(m.state_dict()), scaler._scale.item(), scaler._growth_tracker.item(), seen
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_prechecked_amp_step_matches_barrier(C, dtype, monkeypatch):
+    """Producer-checked gradients (the backward launches record per workgroup whether a
+    gradient they finish is non-finite once unscaled; the fused AMP step then needs no grid
+    barrier) == the barrier step, bitwise, eagerly and graph-replayed."""
+    sd_a, s_a, t_a, seen_a = _amp_run(dtype, False, monkeypatch)
+    sd_b, s_b, t_b, seen_b = _amp_run(dtype, True, monkeypatch)
+    assert not any(seen_a) and all(seen_b[1:]), (seen_a, seen_b)
+    assert (s_a, t_a) == (s_b, t_b)
+    for k in sd_a:
+        assert torch.equal(sd_a[k], sd_b[k]), k
+
+
+@pytest.mark.parametrize("scale", [2.0 ** 127, float("inf"), 0.25])
+def test_prechecked_amp_step_skips_overflow(C, scale, monkeypatch):
+    """A scale that overflows the scaled gradients (or is infinite): every pre-checked step is
+    skipped and the scale backs off exactly as with the barrier step; parameters stay equal.
+    A scale below 1 (the words describe scaled values) takes the barrier inside the launch."""
+    runs = [_amp_run(torch.float16, pc, monkeypatch, steps=2, scale=scale, graph=False) for pc in (False, True)]
+    (sd_a, s_a, t_a, _), (sd_b, s_b, t_b, seen_b) = runs
+    assert all(seen_b[1:])
+    assert (s_a, t_a) == (s_b, t_b) and (s_b < 2.0 ** 127 or scale == float("inf"))  # inf * backoff stays inf
+    for k in sd_a:
+        assert torch.equal(sd_a[k], sd_b[k]), k
+
+
+def test_prechecked_dropped_by_grad_readers(C, monkeypatch):
+    """Reading .grad between backward and step (GradScaler.unscale_ flushes the deferred work)
+    drops the producer checks: that step agrees on found_inf at the barrier instead."""
+    from ddp_practice_amd.amp import GradScaler
+    from ddp_practice_amd.data import DeviceLoader, synthetic
+    from ddp_practice_amd.nn import CrossEntropyLoss
+    from ddp_practice_amd.ops import convnet_fused
+    from ddp_practice_amd.optim import SGD
+
+    monkeypatch.setattr(convnet_fused, "_PRECHECK", True)
+    m = _model(seed=1)
+    m.amp_dtype = torch.bfloat16
+    loader = DeviceLoader(synthetic(64, seed=2), batch_size=32, shuffle=False, device=DEV, dtype=torch.bfloat16)
+    images, labels = loader.static_batch()
+    opt, scaler, crit = SGD(m.parameters(), lr=0.05), GradScaler(), CrossEntropyLoss()
+    assert m.set_slab_sink(opt)
+    loader.start_epoch()
+    for unscale in (False, True):
+        loader.fill_(images, labels, defer=True)
+        loss = crit(m(images), labels)
+        opt.zero_grad(set_to_none=True)
+        scaler.scale(loss).backward()
+        assert "_prechecked" in opt.__dict__
+        if unscale:
+            scaler.unscale_(opt)
+            assert "_prechecked" not in opt.__dict__
+        scaler.step(opt)
+        scaler.update()
+        assert "_prechecked" not in opt.__dict__
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(p).all() for p in m.parameters())
