@@ -36,9 +36,12 @@ inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(
 // non-finite -- or, for partial rows summed later, could overflow the sum (|v| > bound =
 // FLT_MAX / rows) -- sets word[0].  The fused AMP step reads the word and agrees on found_inf
 // without a grid barrier.  Scaled and unscaled finiteness agree while the scale is >= 1
-// (unscaling only shrinks); the step takes the barrier for a smaller scale.
+// (unscaling only shrinks); the step takes the barrier for a smaller scale.  At W > 1 the
+// bound is FLT_MAX / W (the step's average of W checked values cannot overflow) and a
+// flagged rank pushes NaN to its peers in the step's gradient exchange, so every rank skips.
 struct GradChk {
   int* word = nullptr;  // nullptr: no check
+  float bound = 3.402823466e38f;  // |final value| limit (FLT_MAX / world)
   __device__ __forceinline__ static bool bad(float v, float bound) {
     return !(fabsf(v) <= bound);  // NaN / inf / beyond the bound
   }

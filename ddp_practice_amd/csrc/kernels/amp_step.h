@@ -191,6 +191,11 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
     cscale = __int_as_float(chk[nchk]);
   }
   const bool pre = chk != nullptr && cscale >= 1.f;  // uniform: every workgroup reads the same word
+  // XG: a flagged rank pushes NaN in place of its values, so every peer's workgroup sees a
+  // non-finite average of each element it owns and skips -- the ranks agree without a word
+  // exchange (the producers' bound keeps a sum of W checked values finite)
+  const bool poison = XG && pre && cbad;
+  const float nanf_ = __int_as_float(0x7fc00000);
   auto load4 = [](const float* p, int rem) {
     if (rem >= 4) return *reinterpret_cast<const f32x4*>(p);
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -314,7 +319,8 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
     for (int k = 0; k < U; ++k) {
       if (tt[k] < 0) continue;
       const long long fo = (long long)(bid * BG + k * THR + tid) * 32;  // 4 granules of 8 B
-      const u64x2 a = {gran(gv[k][0]), gran(gv[k][1])}, b = {gran(gv[k][2]), gran(gv[k][3])};
+      const f32x4 pv_ = poison ? f32x4{nanf_, nanf_, nanf_, nanf_} : gv[k];
+      const u64x2 a = {gran(pv_[0]), gran(pv_[1])}, b = {gran(pv_[2]), gran(pv_[3])};
       for (int p = 0; p < xg.world; ++p) {
         if (p == xg.rank) continue;  // my own values stay in registers
         u64x2* dst = reinterpret_cast<u64x2*>(xg.base[p] + par + (long long)xg.rank * xg.slot_bytes + fo);
@@ -359,7 +365,7 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
       // at the element's position in the flat granule space -- the slab regions need no
       // separate column-sum launch at W > 1 either
       const long long fo = (long long)(soff[st_t] + st_e / 4) * 32 + (long long)(st_e % 4) * 8;
-      const unsigned long long gm = gran(st_sum);
+      const unsigned long long gm = gran(poison ? nanf_ : st_sum);
       for (int p = 0; p < xg.world; ++p) {
         if (p == xg.rank) continue;
         *reinterpret_cast<unsigned long long*>(xg.base[p] + par + (long long)xg.rank * xg.slot_bytes + fo) = gm;
@@ -396,7 +402,8 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
   // scale read before arriving: block 0 rewrites it once everyone has arrived, and a
   // workgroup that reads it late must not unscale with the next step's value
   const float inv = pre ? 1.f / cscale : amp ? 1.f / scale[0] : 1.f;
-  const bool block_bad = __syncthreads_or(pre ? cbad : bad);
+  // pre-checked: this rank's word (XG: and the peers' NaN in the averages, with `bad`)
+  const bool block_bad = __syncthreads_or(pre ? (cbad || (XG && bad)) : bad);
   if (grid == 1 || !amp || pre) {  // uniform: one workgroup, the plain step or pre-checked gradients need no grid barrier
     if (tid == 0) s_bad = block_bad;
   } else if (tid == 0) {

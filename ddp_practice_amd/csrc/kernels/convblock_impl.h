@@ -353,13 +353,14 @@ __device__ __forceinline__ void bn_bwd_coef(const BwdIn<T>& bi, float* coef, flo
   const bool xon = bi.xs.active();
   unsigned long long tk = 0;
   if (xon && tid == 0) tk = xgmi::xsite_ticket(bi.xs, bid);  // latency hides behind the slab loads
-  const bool cchk = leader && bi.dgamma != nullptr && bi.chk_coef && !xon;  // producer-side check
+  const bool cchk = leader && bi.dgamma != nullptr && bi.chk_coef && !xon;  // producer-side check (xon: above)
   colsum_rows(bi.gsum, bi.grows, 2 * C, part, sums);
   if (xon) {
     // dgamma / dbeta are this rank's (DDP averages them); the coefficients use the global sums
     if (leader && bi.dgamma != nullptr && tid < C) {
       bi.dgamma[tid] = sums[C + tid];
       bi.dbeta[tid] = sums[tid];
+      if (bi.chk_coef) bi.chk.flag(GradChk::bad(sums[C + tid], bi.chk.bound) || GradChk::bad(sums[tid], bi.chk.bound));
     }
     xgmi::xsite_exchange(bi.xs, sums, 2 * C, tk, bid);
   }
@@ -386,7 +387,7 @@ __device__ __forceinline__ void bn_bwd_coef(const BwdIn<T>& bi, float* coef, flo
     }
   }
   if (cchk && tid < C)  // the values just written
-    bi.chk.flag(GradChk::bad(sums[C + tid], 3.402823466e38f) || GradChk::bad(sums[tid], 3.402823466e38f));
+    bi.chk.flag(GradChk::bad(sums[C + tid], bi.chk.bound) || GradChk::bad(sums[tid], bi.chk.bound));
 }
 
 // Produce dy[c][h][w] of image b for every 2x2 window.  Two phases so that the
@@ -1584,7 +1585,7 @@ __device__ __forceinline__ void slab_reduce_body(const float* __restrict__ slab1
 #pragma unroll
     for (int gg = 0; gg < SR_GROUPS; ++gg) t += part[gg][threadIdx.x];
     out[c0 + threadIdx.x] = t;
-    if (chk.word != nullptr) chk.flag(GradChk::bad(t, 3.402823466e38f));  // (producer-side check, common.h)
+    if (chk.word != nullptr) chk.flag(GradChk::bad(t, chk.bound));  // (producer-side check, common.h)
   }
 }
 static __global__ void __launch_bounds__(NTHR)

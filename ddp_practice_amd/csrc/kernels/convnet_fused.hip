@@ -548,14 +548,14 @@ __device__ __forceinline__ void fc_wgrad_body(const FcW<T>& f, int wg) {
     for (int n = 0; n < FC_NMAX; ++n)
       if (n < N) {
         f.dw[(size_t)n * FC_K + col] = acc[n];
-        bad |= GradChk::bad(acc[n], 3.402823466e38f);
+        bad |= GradChk::bad(acc[n], f.chk.bound);
       }
   }
   if (wg == 0 && tid < N) {
     float a = 0.f;
     for (int b = 0; b < B; ++b) a += dl_s[b][tid];
     f.db[tid] = a;
-    bad |= GradChk::bad(a, 3.402823466e38f);
+    bad |= GradChk::bad(a, f.chk.bound);
   }
   if (chk) f.chk.flag(bad);
 }
@@ -627,12 +627,13 @@ void fc_wgrad(at::Tensor dls, at::Tensor p2, at::Tensor dw, at::Tensor db) {
 // The producer-side gradient check's words (optim/sgd.py prechecked AMP step; common.h
 // GradChk): int32[2], [0] cleared by the head launch and set by any producer lane that
 // writes a bad value, [1] the step's scale (recorded by the head launch).
-static GradChk grad_chk_of(const c10::optional<at::Tensor>& chk) {
+static GradChk grad_chk_of(const c10::optional<at::Tensor>& chk, const XcPtr& xc) {
   GradChk g;
   if (!chk.has_value()) return g;
   DPA_CHECK_INPUT(*chk);
   TORCH_CHECK(chk->scalar_type() == at::kInt && chk->numel() == 2, "gradient check: int32[2] words");
   g.word = chk->data_ptr<int>();
+  g.bound = 3.402823466e38f / (float)(xc ? xc->world() : 1);
   return g;
 }
 
@@ -673,8 +674,8 @@ void conv2_bwd(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx2,
     FcW<T> fw = fc_args<T>(fc_dls, fc_p2, fc_dw, fc_db, B, y2.scalar_type());
     const int nfc = fc_dls.has_value() ? FC_BLOCKS : 0;
     if (chk.has_value()) {  // every gradient this launch finishes: BN2's, the fc layer's
-      TORCH_CHECK(!xc && nfc > 0 && dg2.has_value(), "gradient check: the single-rank launch with the fc role");
-      bd.chk = fw.chk = grad_chk_of(chk);
+      TORCH_CHECK(nfc > 0 && dg2.has_value(), "gradient check: the launch with the fc role and BN2's gradients");
+      bd.chk = fw.chk = grad_chk_of(chk, xc);
       bd.chk_coef = 1;
     }
     if constexpr (std::is_same<T, float>::value) {
@@ -911,11 +912,10 @@ void conv1_wgrad_slab2(at::Tensor x, at::Tensor y1, at::Tensor dp1, at::Tensor i
     }
     GradChk rc;
     if (chk.has_value()) {  // BN1's gradients, conv1's partial rows, conv2's column sums
-      TORCH_CHECK(!xc, "gradient check: the single-rank launch");
-      rc = bi.chk = grad_chk_of(chk);
+      rc = bi.chk = grad_chk_of(chk, xc);
       bi.chk_coef = 1;
       bi.chk_rows = 1;
-      bi.chk_row_bound = 3.402823466e38f / (float)nwg1;
+      bi.chk_row_bound = rc.bound / (float)nwg1;
     }
     hipLaunchKernelGGL(wgrad1_slab2_kernel<T>, dim3(nwg1 + nred), dim3(cb::NTHR), 0, cur_stream(), dptr<T>(x),
                        wslab1.data_ptr<float>(), bi, nwg1, wslab2.data_ptr<float>(), rows2, N2,

@@ -383,8 +383,8 @@ void head_step(at::Tensor y2, at::Tensor fslab2, at::Tensor fstats2, at::Tensor 
   hr.chk = nullptr;
   if (chk.has_value()) {
     DPA_CHECK_INPUT(*chk);
-    TORCH_CHECK(chk->scalar_type() == at::kInt && chk->numel() == 2 && scale.has_value() && !xc,
-                "head_step: gradient-check words need the scaler's scale, one rank, int32[2]");
+    TORCH_CHECK(chk->scalar_type() == at::kInt && chk->numel() == 2 && scale.has_value(),
+                "head_step: gradient-check words need the scaler's scale and int32[2]");
     hr.chk = chk->data_ptr<int>();
   }
   hr.state = reinterpret_cast<unsigned long long*>(state.data_ptr<int64_t>());

@@ -465,8 +465,8 @@ void amp_sgd_fused(std::vector<at::Tensor> params, std::vector<at::Tensor> grads
   int nchk = 0;
   if (prechk.has_value()) {
     DPA_CHECK_INPUT(*prechk);
-    TORCH_CHECK(amp && !xc && prechk->scalar_type() == at::kInt && prechk->numel() >= 2,
-                "fused AMP-SGD: pre-checked gradients need the scaler, one rank and int32 words");
+    TORCH_CHECK(amp && prechk->scalar_type() == at::kInt && prechk->numel() >= 2,
+                "fused AMP-SGD: pre-checked gradients need the scaler and int32 words");
     chk = prechk->data_ptr<int>();
     nchk = (int)prechk->numel() - 1;
   }

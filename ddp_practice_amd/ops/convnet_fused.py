@@ -207,10 +207,11 @@ class ConvNetFn(torch.autograd.Function):
                     dp2 = torch.empty_like(p2)
                     bsum2 = torch.empty(B * 64, **f32)
                     spec = (dls, dp2, bsum2)
-                    # pre-checked gradients (single rank, slab sink): this launch clears the check
-                    # word the backward's producers set (optim/sgd.py set_prechecked)
+                    # pre-checked gradients (slab sink; one rank, or the DDP average inside the
+                    # AMP step over the xGMI engine): this launch clears the check word the
+                    # backward's producers set (optim/sgd.py set_prechecked)
                     chk = None
-                    if (sink is not None and _PRECHECK and not sync and xc is None
+                    if (sink is not None and _PRECHECK and (xc is not None or not sync)
                             and hasattr(sink, "set_prechecked")):
                         sink.clear_prechecked()  # the device word is reset below
                         chk = sink.grad_chk(2, dev)

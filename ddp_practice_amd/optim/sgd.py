@@ -309,9 +309,11 @@ class SGD(Optimizer):
         # when the DDP average is fused in too (xc)
         ps = self.__dict__.pop("_pending_slab", None)
         # producer-checked gradients (ops/convnet_fused.py): every gradient lies in the checked
-        # buffer and was unscaled against this scale -> no grid barrier in the launch
+        # buffer and was checked against this scale -> no grid barrier in the launch.  Under a
+        # deferring DDP reducer only with the average in this launch (xc: a flagged rank
+        # poisons its pushed values, csrc/kernels/amp_step.h), never after a reducer all-reduce
         prechk = None
-        if (pc is not None and xc is None and ps is not None and pc[1] is scale
+        if (pc is not None and ps is not None and pc[1] is scale and (xc is not None or d is None)
                 and all(pc[2] <= g.data_ptr() < pc[3] for g in grads)):
             prechk = pc[0]
         O.amp_sgd_fused(params, grads, bufs, group["lr"], group["momentum"], group["dampening"],

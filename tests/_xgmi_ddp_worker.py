@@ -133,3 +133,67 @@ def worker(rank, world, port, amp, graph, q):
         q.close()
         q.join_thread()
         os._exit(0)
+
+
+def worker_poison(rank, world, port, q):
+    """Pre-checked AMP step under DDP over the xGMI engine: rank 1's gradients overflow (its
+    scale is made infinite), rank 0's are finite -- rank 1's AMP step pushes NaN in place of
+    its values, so rank 0 skips the step too: parameters unchanged, scale backed off."""
+    try:
+        from ._dist import client_env
+
+        os.environ.update(client_env(rank, world, port))
+        torch.cuda.set_device(0)
+        import ddp_practice_amd.distributed as dist
+        from ddp_practice_amd import _ext
+        from ddp_practice_amd.amp import GradScaler
+        from ddp_practice_amd.data import DeviceLoader, DistributedSampler, synthetic
+        from ddp_practice_amd.engine import TrainLoop
+        from ddp_practice_amd.models import ConvNet
+        from ddp_practice_amd.nn import CrossEntropyLoss
+        from ddp_practice_amd.optim import SGD
+        from ddp_practice_amd.parallel import DistributedDataParallel, convert_sync_batchnorm
+
+        dist.init_process_group("xgmi")
+        torch.manual_seed(0)
+        ddp = DistributedDataParallel(convert_sync_batchnorm(ConvNet(amp_dtype=torch.bfloat16).cuda()), device_ids=[0])
+        ds = synthetic(16 * world * 6, seed=11)
+        sampler = DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=False)
+        loader = DeviceLoader(ds, batch_size=16, shuffle=False, sampler=sampler, device="cuda", dtype=torch.bfloat16)
+        opt, scaler = SGD(ddp.parameters(), lr=0.05), GradScaler()
+        loop = TrainLoop(ddp, CrossEntropyLoss(), opt, loader, scaler, use_graph=False)
+        assert getattr(opt, "_deferred_ddp", None) is not None
+        C = _ext.load()
+        orig = C.optim.amp_sgd_fused
+        seen = []
+
+        def spy(*a, **k):
+            seen.append(len(a) > 20 and a[-1] is not None)
+            return orig(*a, **k)
+
+        C.optim.amp_sgd_fused = spy
+        loader.start_epoch()
+        for _ in range(3):
+            loop._eager_step()
+        torch.cuda.synchronize()
+        before = {k: p.detach().clone() for k, p in ddp.module.named_parameters()}
+        s0 = scaler._scale.item()
+        if rank == 1:
+            scaler._scale.fill_(float("inf"))
+        seen.clear()
+        loop._eager_step()
+        torch.cuda.synchronize()
+        C.optim.amp_sgd_fused = orig
+        assert seen == [True], seen  # the step ran pre-checked (no grid barrier) on this rank
+        changed = [k for k, p in ddp.module.named_parameters() if not torch.equal(p.detach(), before[k])]
+        assert changed == [], changed
+        if rank == 0:
+            assert scaler._scale.item() == s0 * 0.5, (s0, scaler._scale.item())
+        dist.destroy_process_group()
+        q.put((rank, "ok", {"scale": scaler._scale.item()}))
+    except Exception:  # pragma: no cover - reported to the parent
+        q.put((rank, "err", traceback.format_exc()))
+    finally:
+        q.close()
+        q.join_thread()
+        os._exit(0)

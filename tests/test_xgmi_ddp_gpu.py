@@ -18,3 +18,12 @@ def test_ddp_syncbn_xgmi_two_processes(C, amp, graph):
     print("grad errs", res[0]["grad_errs"])
     print("param errs", res[0]["errs"])
     assert res[0]["digest"] == res[1]["digest"], "ranks diverged"
+
+
+def test_prechecked_step_agrees_across_ranks(C):
+    """DDP + SyncBN ConvNet over the xGMI engine with the pre-checked AMP step: one rank's
+    overflow makes every rank skip (the flagged rank pushes NaN in its gradient exchange)."""
+    from ._xgmi_ddp_worker import worker_poison
+
+    outs = launch(worker_poison, 2, (), timeout=240)
+    assert len(outs) == 2 and outs[0]["scale"] < outs[1]["scale"]  # rank 0 backed off; rank 1 stays inf
