@@ -92,7 +92,7 @@ class SGD(Optimizer):
         outside a graph capture only; None inside one when they do not exist yet."""
         t = self.__dict__.get("_grad_chk")
         if t is None or t.numel() != n or t.device != device:
-            if torch.cuda.is_current_stream_capturing():
+            if device.type == "cuda" and torch.cuda.is_current_stream_capturing():
                 return None
             t = self._grad_chk = torch.empty(n, dtype=torch.int32, device=device)
         return t

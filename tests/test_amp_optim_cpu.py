@@ -151,3 +151,25 @@ def test_optimizer_and_scaler_do_not_import_dynamo_or_sympy():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_prechecked_bookkeeping():
+    """The producer-check registration (ops/convnet_fused.py -> SGD.set_prechecked) lasts until
+    the next fused step or any gradient reader: flush_slab (GradScaler.unscale_, DDP flush,
+    grad hooks) and a new backward drop it, and the check words are never created inside a
+    graph capture (here: none on CPU either way)."""
+    p = torch.nn.Parameter(torch.zeros(8))
+    opt = SGD([p], lr=0.1)
+    out = torch.zeros(8)
+    chk = torch.zeros(2, dtype=torch.int32)
+    scale = torch.ones(1)
+    opt.set_prechecked(chk, scale, out)
+    pc = opt.__dict__["_prechecked"]
+    assert pc[0] is chk and pc[1] is scale and pc[3] - pc[2] == out.numel() * out.element_size()
+    opt.flush_slab()
+    assert "_prechecked" not in opt.__dict__
+    opt.set_prechecked(chk, scale, out)
+    opt.clear_prechecked()
+    assert "_prechecked" not in opt.__dict__
+    t = opt.grad_chk(2, torch.device("cpu"))
+    assert t.dtype == torch.int32 and t.numel() == 2 and opt.grad_chk(2, torch.device("cpu")) is t
