@@ -398,11 +398,16 @@ class _Chunks:
 
     def run(self, n: int) -> None:
         tick = self.health.tick if self.health is not None else None
+        # the short remainder graph first: the device starts on it while the host submits the
+        # first full graph (DPA_BENCH_REMAINDER_LAST=1: the old order, A/B runs)
+        first = n % self.spg and os.environ.get("DPA_BENCH_REMAINDER_LAST") != "1"
+        if first:
+            self._chunk(n % self.spg)
         for i in range(n // self.spg):
             self._chunk(self.spg)
             if tick is not None and i % 64 == 63:
                 tick()
-        if n % self.spg:
+        if n % self.spg and not first:
             self._chunk(n % self.spg)
         if tick is not None:
             tick()

@@ -14,6 +14,20 @@ for i in 1 2; do
     echo "plain $v $i $(grep -o '"ms_per_step": [0-9.]*' $OUT/p_${v}_$i.json | head -1)"
   done
 done
+for i in 1 2; do
+  for v in atomic plain; do
+    E=""; [ $v = plain ] && E="DPA_EXT_SO=ddp_practice_amd/_C_xsplain.so"
+    env $E timeout -k 10 200 python bench.py --force-collectives --steps 2000 --warmup 50 --no-baseline --extra-dtypes "" --epochs 0 --no-steady > $OUT/x_${v}_$i.json 2> $OUT/x_${v}_$i.err || { tail -5 $OUT/x_${v}_$i.err; exit 1; }
+    echo "forced epoch-advance $v $i $(grep -o '"ms_per_step": [0-9.]*' $OUT/x_${v}_$i.json | head -1)"
+  done
+done
+for i in 1 2 3; do
+  for v in first last; do
+    E=""; [ $v = last ] && E="DPA_BENCH_REMAINDER_LAST=1"
+    env $E timeout -k 10 100 python bench.py --steps 20 --warmup 5 --no-baseline --extra-dtypes "" --no-steady > $OUT/s_${v}_$i.json 2> $OUT/s_${v}_$i.err || { tail -5 $OUT/s_${v}_$i.err; exit 1; }
+    echo "short(20/5) remainder-$v $i $(grep -o '"ms_per_step": [0-9.]*' $OUT/s_${v}_$i.json | head -1)"
+  done
+done
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/prof -o run -- \
   python3 $R/bench.py --force-collectives --steps 640 --warmup 64 --extra-dtypes "" --no-baseline --epochs 0 --no-steady > $OUT/prof.json 2> $OUT/prof.err || { tail -20 $OUT/prof.err; exit 1; }
