@@ -74,8 +74,8 @@ struct XSite {
 // only needed by xsite_exchange: its round trip hides behind the caller's slab loads).
 // bid: the workgroup's index among the launch's workgroups on this site.
 __device__ __forceinline__ unsigned long long xsite_ticket(const XSite& xs, int bid) {
-  // (a plain load and advancing the words after the exchange measured no faster on the
-  // forced step: profiles/r5o_xsite_mode_ab.txt)
+  // (a plain load, plain epoch stores and advancing the words after the exchange measured no
+  // faster on the forced step: profiles/r5o_xsite_mode_ab.txt, r5s_xsite_plain_ab.txt)
   return __hip_atomic_load(xs.tick + (bid < kEpochWords ? bid : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
