@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <torch/extension.h>
 
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -96,6 +97,10 @@ class XgmiComm {
   int* host_words_ = nullptr;  // [0] error, [1] abort (host-mapped, coherent)
   int* dev_words_ = nullptr;
   bool opened_ = false;
+  // what this rank's host has issued (debug_state, readable when the device is wedged):
+  // launches attached to each site, one- / two-shot all-reduces and the last one's bytes
+  mutable std::atomic<long long> site_calls_[kSites] = {};
+  std::atomic<long long> ar_calls_{0}, ts_calls_{0}, ar_last_bytes_{0};
 };
 
 }  // namespace xgmi

@@ -506,6 +506,8 @@ void XgmiComm::all_reduce(const at::Tensor& in, const at::Tensor& out, RedOp op,
                   in.scalar_type() == out.scalar_type(),
               "xgmi all_reduce: unsupported tensor (device/dtype/size/alignment)");
   TORCH_CHECK(op != RedOp::PROD, "xgmi all_reduce: prod is not supported");
+  ar_calls_.fetch_add(1, std::memory_order_relaxed);
+  ar_last_bytes_.store((long long)in.nbytes(), std::memory_order_relaxed);
   Args a;
   a.peers = peers_;
   a.in = in.data_ptr();
@@ -558,6 +560,8 @@ void XgmiComm::all_reduce_twoshot(const at::Tensor& in, const at::Tensor& out, R
                   in.scalar_type() == out.scalar_type(),
               "xgmi two-shot all_reduce: unsupported tensor (device/dtype/size/alignment)");
   TORCH_CHECK(op != RedOp::PROD, "xgmi all_reduce: prod is not supported");
+  ts_calls_.fetch_add(1, std::memory_order_relaxed);
+  ar_last_bytes_.store((long long)in.nbytes(), std::memory_order_relaxed);
   TSArgs a;
   for (int p = 0; p < kMaxRanks; ++p) a.peers.base[p] = peers_.base[p] ? peers_.base[p] + ts_off_ : nullptr;
   a.in = in.data_ptr();
@@ -597,6 +601,7 @@ void XgmiComm::all_reduce_twoshot(const at::Tensor& in, const at::Tensor& out, R
 XSite XgmiComm::site(int s) const {
   TORCH_CHECK(opened_ && local_ != nullptr, "xgmi: site of a closed or unopened communicator");
   TORCH_CHECK(s >= 0 && s < kSites, "xgmi: site id out of range");
+  site_calls_[s].fetch_add(1, std::memory_order_relaxed);  // (a handle per attached launch)
   XSite x;
   for (int p = 0; p < world_; ++p) x.base[p] = peers_.base[p] + site_off_ + (long long)s * kSiteBytes;
   x.tick = ticks_ + (long long)s * kEpochWords;
@@ -703,6 +708,11 @@ std::string XgmiComm::debug_state(double wait_s) const {
   }
   o << ": err=" << __atomic_load_n(&host_words_[0], __ATOMIC_ACQUIRE)
     << " abort=" << __atomic_load_n(&host_words_[1], __ATOMIC_ACQUIRE);
+  // host side first (needs no device work): equal counts on every rank mean the ranks issued
+  // the same sequence, so a stall is co-residency / scheduling, not a diverged protocol
+  o << "; host issued: oneshot " << ar_calls_.load() << " twoshot " << ts_calls_.load() << " (last "
+    << ar_last_bytes_.load() << " B), site handles";
+  for (int s = 0; s < kSites; ++s) o << (s ? "," : " ") << site_calls_[s].load();
   // regions: the SyncBN sites 0..4, the wide site, the gradient site, the one-shot slots
   struct Reg {
     const char* name;

@@ -157,6 +157,13 @@ def test_xgmi_debug_state_names_sites_and_words(rccl):
     st = x.debug_state(2.0)
     assert st.startswith("xgmi rank 0/1: err=0 abort=0"), st
     assert "fwd1 ep=" in st and "peers[par0|par1]=" in st and "oneshot blk ep=" in st, st
+    # the host-side issue counts (readable when the device is wedged): the training above
+    # attached launches to the SyncBN sites
+    import re
+
+    m = re.search(r"host issued: oneshot (\d+) twoshot (\d+) \(last (\d+) B\), site handles ([\d,]+)", st)
+    assert m is not None, st
+    assert sum(int(v) for v in m.group(4).split(",")) > 0, st
 
 
 def test_xgmi_engine_passes_its_selftest_at_forced_world1(rccl):
