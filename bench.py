@@ -430,10 +430,12 @@ def run_rank(args) -> int:
     if args.comm:
         os.environ["DPA_COMM"] = args.comm
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.share_gpu:  # ranks share one device (ops/convnet_fused.py; one HW queue each at 3+)
+        from ddp_practice_amd.runtime.device import shared_gpu_env
+
+        shared_gpu_env(world)  # before the first HIP call below
     gpu = torch.cuda.is_available()
     local_rank = 0 if args.share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
-    if args.share_gpu:
-        os.environ["DPA_SHARED_GPU"] = "1"  # ranks share one device (ops/convnet_fused.py)
     if gpu:
         torch.cuda.set_device(local_rank)
         dev = torch.device("cuda", local_rank)
@@ -815,8 +817,10 @@ def bench_resnet(args) -> int:
         os.environ["DPA_COMM"] = args.comm
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = 0 if args.share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
-    if args.share_gpu:
-        os.environ["DPA_SHARED_GPU"] = "1"  # ranks share one device (ops/convnet_fused.py)
+    if args.share_gpu:  # ranks share one device (one HW queue each at 3+: runtime/device.py)
+        from ddp_practice_amd.runtime.device import shared_gpu_env
+
+        shared_gpu_env(world)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist_path = world > 1 or args.force_collectives

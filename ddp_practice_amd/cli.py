@@ -78,8 +78,13 @@ def apply_env(args) -> None:
         os.environ["DPA_COMM"] = args.comm
     if getattr(args, "share_gpu", False):
         # ranks sharing one device: 3+ ranks' spinning in-kernel exchanges are not co-resident
-        # on one card, so those take one launch per collective (ops/convnet_fused.py)
-        os.environ["DPA_SHARED_GPU"] = "1"
+        # on one card, so those take one launch per collective (ops/convnet_fused.py), and
+        # each rank process gets one hardware queue (runtime/device.shared_gpu_env)
+        from .runtime.device import shared_gpu_env
+
+        gpus = [g for g in str(getattr(args, "gpu", "") or "").split(",") if g.strip()]
+        world = int(os.environ["WORLD_SIZE"]) if "WORLD_SIZE" in os.environ else (len(gpus) or None)
+        shared_gpu_env(world)
 
 
 def rank_device_index(args, local_rank: int) -> int:

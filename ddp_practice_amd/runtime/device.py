@@ -26,3 +26,22 @@ def local_device():
     lr = int(os.environ.get("LOCAL_RANK", "0"))
     n = torch.cuda.device_count()
     return torch.device("cuda", lr % max(n, 1))
+
+
+def shared_gpu_env(world: int | None) -> None:
+    """Environment of ranks that share one device (``--share-gpu`` rehearsals): the fused
+    paths' gates (``DPA_SHARED_GPU``) and, for 3+ ranks, one HIP hardware queue per process.
+
+    With HIP's default 4 queues per process, 4 processes on one MI355X stalled at the same
+    point of the 3-epoch phase twice (every rank's host had issued the same collectives;
+    their one-shot all-reduce kernels waited on a peer whose work never ran), and completed
+    twice at 836-841k img/s with one queue each (``profiles/r5v_shared_gpu_hw_queues.txt``):
+    more queues than the scheduler maps at once leave a rank unscheduled while its peers
+    spin.  ``DPA_SHARED_HW_QUEUES`` overrides the count.  Before the first HIP call only.
+    """
+    os.environ["DPA_SHARED_GPU"] = "1"
+    q = os.environ.get("DPA_SHARED_HW_QUEUES")
+    if q is None and (world is None or world >= 3):
+        q = "1"
+    if q:
+        os.environ["GPU_MAX_HW_QUEUES"] = q

@@ -112,3 +112,19 @@ def test_ddp_main_timer_includes_child_interpreter(tmp_path, spawn):
     assert all(s >= t0[0] for s in starts), (t0, starts)
     elapsed = float([ln for ln in out.splitlines() if ln.startswith("time elapsed: ")][0].split()[2])
     assert elapsed >= max(starts) - t0[0]
+
+
+def test_shared_gpu_env_one_hw_queue_from_three_ranks(monkeypatch):
+    """--share-gpu: ranks get the fused-path gates, and from 3 ranks one HIP hardware queue
+    per process (4 processes with 4 queues each stalled on one MI355X; profiles/r5v_*)."""
+    from ddp_practice_amd.runtime.device import shared_gpu_env
+
+    for k in ("DPA_SHARED_GPU", "GPU_MAX_HW_QUEUES", "DPA_SHARED_HW_QUEUES"):
+        monkeypatch.delenv(k, raising=False)
+    shared_gpu_env(2)
+    assert os.environ["DPA_SHARED_GPU"] == "1" and "GPU_MAX_HW_QUEUES" not in os.environ
+    shared_gpu_env(4)
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "1"
+    monkeypatch.setenv("DPA_SHARED_HW_QUEUES", "2")
+    shared_gpu_env(4)
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "2"
