@@ -708,16 +708,28 @@ def _headline(ctx, amp, steady: bool) -> dict:
     if chunks.capture_error is not None and rank == 0:
         print(f"[bench] graph capture failed, eager fallback: {chunks.capture_error!r}", file=sys.stderr)
 
+    ev = ctx["gpu"] and os.environ.get("DPA_BENCH_EVENTS") == "1"  # diagnostics: device-side span
+
     def timed(n: int) -> float:
         ddist.barrier()
         if ctx["gpu"]:
             torch.cuda.synchronize()
         t0 = time.perf_counter()
+        if ev:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         chunks.run(n)
+        if ev:
+            e1.record()
+            th = time.perf_counter() - t0
         if ctx["gpu"]:
             torch.cuda.synchronize()
         ddist.barrier()
-        return ddist.max_over_ranks(time.perf_counter() - t0)
+        dt = time.perf_counter() - t0
+        if ev:
+            print(f"[bench] {n} steps: wall {dt * 1e6:.1f} us, device span {e0.elapsed_time(e1) * 1e3:.1f} us, "
+                  f"host issue {th * 1e6:.1f} us", file=sys.stderr)
+        return ddist.max_over_ranks(dt)
 
     chunks.run(args.warmup)
     dt = timed(args.steps)
