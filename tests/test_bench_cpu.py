@@ -129,3 +129,28 @@ def test_supervisor_rejects_multi_node_torchrun(monkeypatch):
     monkeypatch.setenv("MASTER_PORT", "1")
     with pytest.raises(ValueError, match="single-node"):
         Supervisor(16)
+
+
+def test_timed_chunk_plan_covers_exactly_the_steps(monkeypatch):
+    """bench.py's timed regions replay graphs in a plan of a one-step lead, the remainder and
+    full graphs: it runs exactly the requested number of steps, with a lead step unless
+    DPA_BENCH_LEAD=0 or one step per graph."""
+    import importlib.util
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+
+    class Plan(bench._Chunks):
+        def __init__(self, spg):  # no graphs, no loader: the plan only
+            self.spg = spg
+
+    for spg, n in [(16, 20), (16, 2000), (16, 1875), (16, 5), (16, 1), (16, 17), (1, 7), (16, 0)]:
+        plan = Plan(spg)._plan(n)
+        assert sum(plan) == n and all(1 <= k <= spg for k in plan), (spg, n, plan)
+        if n and spg > 1:
+            assert plan[0] == 1
+    assert Plan(16)._plan(20) == [1, 3, 16]
+    monkeypatch.setenv("DPA_BENCH_LEAD", "0")
+    assert Plan(16)._plan(20) == [4, 16]
