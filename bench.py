@@ -596,7 +596,8 @@ def _build(ctx, amp, seed: int):
     if ctx["dist_path"]:
         if not ctx["args"].no_sync_bn:
             model = convert_sync_batchnorm(model)
-        model = DistributedDataParallel(model, device_ids=[ctx["local_rank"]] if ctx["gpu"] else None)
+        model = DistributedDataParallel(model, device_ids=[ctx["local_rank"]] if ctx["gpu"] else None,
+                                        gradient_as_bucket_view=True)
     return model, SGD(model.parameters(), lr=1e-4), GradScaler(enabled=amp is not None)
 
 
@@ -863,7 +864,7 @@ def bench_resnet(args) -> int:
     if dist_path:
         if not args.no_sync_bn:
             model = convert_sync_batchnorm(model)
-        model = DistributedDataParallel(model, device_ids=[local_rank])
+        model = DistributedDataParallel(model, device_ids=[local_rank], gradient_as_bucket_view=True)
     optimizer = SGD(model.parameters(), lr=1e-4)
     scaler = GradScaler(enabled=amp is not None)
     g = torch.Generator(device="cpu").manual_seed(rank)

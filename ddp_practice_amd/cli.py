@@ -268,7 +268,9 @@ def run(args, distributed: bool, local_rank: int = 0, generator_seed: int | None
         if not args.no_sync_bn:
             model = convert_sync_batchnorm(model)
         model = DistributedDataParallel(model, device_ids=[dev.index] if gpu else None,
-                                        bucket_cap_mb=args.bucket_cap_mb, first_bucket_mb=args.first_bucket_mb)
+                                        bucket_cap_mb=args.bucket_cap_mb, first_bucket_mb=args.first_bucket_mb,
+                                        # zero-copy buckets: the fused optimizer step reads them
+                                        gradient_as_bucket_view=True)
     elif distributed:
         if not args.no_sync_bn and gpu:  # torch's SyncBatchNorm has no CPU path
             model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)

@@ -111,10 +111,9 @@ __global__ __launch_bounds__(kThreads) void oneshot_kernel(Args a) {
         reinterpret_cast<unsigned long long*>(a.peers.base[p] + par_off + (long long)a.rank * a.slot_bytes) + e0;
     if (ne == kPerThread) {
 #pragma unroll
-      for (int j = 0; j < kPerThread; j += 2)
-        *reinterpret_cast<u64x2*>(dst + j) = u64x2{granule(v[j], ep), granule(v[j + 1], ep)};
+      for (int j = 0; j < kPerThread; j += 2) xgmi_put2(dst + j, granule(v[j], ep), granule(v[j + 1], ep));
     } else {
-      for (int j = 0; j < ne; ++j) dst[j] = granule(v[j], ep);
+      for (int j = 0; j < ne; ++j) xgmi_put(dst + j, granule(v[j], ep));
     }
   }
 
@@ -288,8 +287,7 @@ __device__ __forceinline__ void ts_store8(T* p, long long e0, long long n, const
 
 __device__ __forceinline__ void push8(unsigned long long* dst, const float (&v)[kPerThread], uint32_t ep) {
 #pragma unroll
-  for (int j = 0; j < kPerThread; j += 2)
-    *reinterpret_cast<u64x2*>(dst + j) = u64x2{granule(v[j], ep), granule(v[j + 1], ep)};
+  for (int j = 0; j < kPerThread; j += 2) xgmi_put2(dst + j, granule(v[j], ep), granule(v[j + 1], ep));
 }
 
 // op: 0 sum, 1 avg, 2 max, 3 min.  A FIXED grid of G blocks (every call): block b

@@ -70,6 +70,29 @@ struct XSite {
   __host__ __device__ bool active() const { return tick != nullptr; }
 };
 
+// Every remote granule push of the engine (one-shot, two-shot, sites, the AMP-SGD gradient
+// exchange) goes through these: a system-scope relaxed atomic store, so a granule's
+// visibility to the peer's system-scope polls is explicit in the memory model and does not
+// rest on the peer mapping's memory type (hipDeviceMallocUncached).  8-byte granules are the
+// unit of atomicity (value and epoch tag together); the 16-byte form is two of them.
+// DPA_PUSH_PLAIN (experiment builds only) restores plain stores for the A/B.
+__device__ __forceinline__ void xgmi_put(unsigned long long* dst, unsigned long long g) {
+#ifdef DPA_PUSH_PLAIN
+  *dst = g;
+#else
+  __hip_atomic_store(dst, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
+}
+__device__ __forceinline__ void xgmi_put2(unsigned long long* dst, unsigned long long a, unsigned long long b) {
+#ifdef DPA_PUSH_PLAIN
+  typedef __attribute__((ext_vector_type(2))) unsigned long long v2;
+  *reinterpret_cast<v2*>(dst) = v2{a, b};
+#else
+  __hip_atomic_store(dst, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(dst + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
+}
+
 // Lane 0 of every workgroup, once per launch, as early as possible (the returned word is
 // only needed by xsite_exchange: its round trip hides behind the caller's slab loads).
 // bid: the workgroup's index among the launch's workgroups on this site.
@@ -158,8 +181,9 @@ __device__ __forceinline__ void xsite_exchange(const XSite& xs, float* vals, int
     if (pusher)
       for (int p = 0; p < xs.world; ++p)
         if (p != xs.rank)
-          *reinterpret_cast<unsigned long long*>(xs.base[p] + par + (long long)xs.rank * xs.slot_bytes +
-                                                 (long long)tid * 8) = gm;
+          xgmi_put(reinterpret_cast<unsigned long long*>(xs.base[p] + par + (long long)xs.rank * xs.slot_bytes +
+                                                         (long long)tid * 8),
+                   gm);
     // every peer's granule loaded before the first tag check (one round trip)
     unsigned long long g[kMaxRanks];
     const unsigned long long* src[kMaxRanks];
@@ -200,7 +224,7 @@ __device__ __forceinline__ void xsite_push_at(const XSite& xs, uint32_t ep, int 
                         (long long)pos * 8;
   const unsigned long long gm = ((unsigned long long)ep << 32) | (unsigned long long)__float_as_uint(mine);
   for (int p = 0; p < xs.world; ++p)
-    if (p != xs.rank) *reinterpret_cast<unsigned long long*>(xs.base[p] + off) = gm;
+    if (p != xs.rank) xgmi_put(reinterpret_cast<unsigned long long*>(xs.base[p] + off), gm);
 }
 
 __device__ __forceinline__ float xsite_pull_at(const XSite& xs, uint32_t ep, int pos, float mine, long long t0,

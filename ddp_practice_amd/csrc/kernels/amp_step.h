@@ -323,9 +323,10 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
       const u64x2 a = {gran(pv_[0]), gran(pv_[1])}, b = {gran(pv_[2]), gran(pv_[3])};
       for (int p = 0; p < xg.world; ++p) {
         if (p == xg.rank) continue;  // my own values stay in registers
-        u64x2* dst = reinterpret_cast<u64x2*>(xg.base[p] + par + (long long)xg.rank * xg.slot_bytes + fo);
-        dst[0] = a;
-        dst[1] = b;
+        unsigned long long* dst =
+            reinterpret_cast<unsigned long long*>(xg.base[p] + par + (long long)xg.rank * xg.slot_bytes + fo);
+        xgmi::xgmi_put2(dst, a[0], a[1]);
+        xgmi::xgmi_put2(dst + 2, b[0], b[1]);
       }
     }
     const float invw = 1.f / (float)xg.world;
@@ -368,7 +369,8 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
       const unsigned long long gm = gran(poison ? nanf_ : st_sum);
       for (int p = 0; p < xg.world; ++p) {
         if (p == xg.rank) continue;
-        *reinterpret_cast<unsigned long long*>(xg.base[p] + par + (long long)xg.rank * xg.slot_bytes + fo) = gm;
+        xgmi::xgmi_put(reinterpret_cast<unsigned long long*>(xg.base[p] + par + (long long)xg.rank * xg.slot_bytes + fo),
+                       gm);
       }
       unsigned long long g[xgmi::kMaxRanks];
       const unsigned long long* src[xgmi::kMaxRanks];
@@ -482,9 +484,17 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
   }
   DPA_STAMP(13);
   if (amp && bid == 0 && tid == 0) {
-    // every workgroup read scale[0] before arriving, and block 0 passed the barrier
+    // every workgroup read scale[0] before arriving, and block 0 passed the barrier.
+    // Without the barrier (pre-checked / XG) a peer that never arrived skips only the
+    // workgroups that timed out; block 0 also backs off when the engine's error word is set
+    // (any workgroup's timeout, or an earlier failure).  The ranks' parameters may then
+    // differ: an engine error is fatal -- the watchdog aborts the job and cli.check_health
+    // refuses to checkpoint (tests/test_aux_cpu.py, utils/watchdog.py).
+    bool eng_bad = false;
+    if constexpr (XG)
+      eng_bad = xg.err != nullptr && __hip_atomic_load(xg.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
     found_inf[0] = 0.f;
-    if (any_bad) {
+    if (any_bad || eng_bad) {
       scale[0] = scale[0] * backoff;
       tracker[0] = 0;
     } else {

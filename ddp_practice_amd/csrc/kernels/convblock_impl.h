@@ -1494,7 +1494,11 @@ conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __r
       for (int j = 0; j < 8; ++j) a += Cvt<T>::to_f(e[j]);
     }
     a = group_sum<TPC>(a);  // VALU lane moves (every lane active here)
-    if (sub == 0) put(&row_out[COUT * N + co], a);
+    if (sub == 0) {
+      put(&row_out[COUT * N + co], a);
+      // the bias column is summed by the AMP step like the weight columns: same row bound
+      if (rchk) bin.chk.flag(GradChk::bad(a, bin.chk_row_bound));
+    }
   }
   DPA_STAMP(6);
   const int ks = KSPLIT > 1 ? wv % KSPLIT : 0;

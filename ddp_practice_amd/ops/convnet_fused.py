@@ -210,8 +210,17 @@ class ConvNetFn(torch.autograd.Function):
                     # pre-checked gradients (slab sink; one rank, or the DDP average inside the
                     # AMP step over the xGMI engine): this launch clears the check word the
                     # backward's producers set (optim/sgd.py set_prechecked)
+                    # Only for a GradScaler's scale (fp32's unit seed has no step to pre-check),
+                    # and only where the producers' row bound FLT_MAX / W uses the world of the
+                    # gradient exchange: the SyncBN site engine's (xc), or one rank.  Plain BN
+                    # under a deferring DDP (--no-sync-bn: no xc, DDP world > 1) keeps the barrier.
+                    from .head import _UNIT
+
+                    ddp = getattr(sink, "_deferred_ddp", None) if sink is not None else None
+                    ddp_world = int(ddp[1].world_size) if ddp is not None and ddp[1] is not None else 1
                     chk = None
-                    if (sink is not None and _PRECHECK and (xc is not None or not sync)
+                    if (sink is not None and _PRECHECK and scale is not _UNIT.get(dev)
+                            and (xc is not None or (not sync and ddp_world == 1))
                             and hasattr(sink, "set_prechecked")):
                         sink.clear_prechecked()  # the device word is reset below
                         chk = sink.grad_chk(2, dev)

@@ -69,7 +69,7 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, output_device=None, dim: int = 0,
                  broadcast_buffers: bool = True, process_group=None, bucket_cap_mb: float | None = None,
                  find_unused_parameters: bool = False, check_reduction: bool = False,
-                 gradient_as_bucket_view: bool = True, static_graph: bool = False,
+                 gradient_as_bucket_view: bool = False, static_graph: bool = False,
                  first_bucket_mb: float | None = None):
         super().__init__()
         self.module = module
@@ -201,8 +201,9 @@ class DistributedDataParallel(nn.Module):
             if bufs:
                 self._flat_broadcast(bufs)
         out = self.module(*inputs, **kwargs)
-        if not self.module.training:
-            pass
+        # torch's _post_forward (distributed.py:1604-1617): the next forward broadcasts the
+        # buffers only after a forward whose backward will sync (grad enabled, not no_sync)
+        self.require_forward_param_sync = torch.is_grad_enabled() and self._sync_enabled
         return out
 
     def _rebuild_buckets(self):

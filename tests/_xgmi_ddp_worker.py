@@ -46,6 +46,16 @@ def worker(rank, world, port, amp, graph, q):
         from ._dist import client_env
 
         os.environ.update(client_env(rank, world, port))
+        if world >= 3:
+            # several ranks on one card (runtime/device.shared_gpu_env: one HW queue each, and
+            # no launch whose own grid barrier needs a whole card per rank -- the deferred conv1
+            # weight gradient); the in-kernel SyncBN sites and the AMP-SGD gradient exchange
+            # forced on: at 8 images per rank all eight ranks' exchanging grids fit together
+            from ddp_practice_amd.runtime.device import shared_gpu_env
+
+            shared_gpu_env(world)
+            os.environ["DPA_FUSED_SYNC"] = "1"
+            os.environ["DPA_FUSED_GRAD"] = "1"
         torch.cuda.set_device(0)
         import ddp_practice_amd.distributed as dist
         from ddp_practice_amd.data import DistributedSampler, synthetic
@@ -54,11 +64,18 @@ def worker(rank, world, port, amp, graph, q):
 
         c = dist.init_process_group("xgmi")
         assert isinstance(c, XgmiCommunicator)
-        per_rank = 16
+        from ddp_practice_amd.ops.convnet_fused import _fused_site_engine
+
+        # the SyncBN sums are exchanged inside the kernels (not one launch per collective)
+        assert _fused_site_engine(c, 16 if world <= 2 else 8, torch.bfloat16 if amp else torch.float32) is not None
+        # 8 ranks on one card: 8 images each, so every rank's exchanging grids (in-kernel
+        # SyncBN sites, the AMP-SGD gradient exchange) are co-resident
+        per_rank = 16 if world <= 2 else 8
         ds = synthetic(per_rank * world * 9 + 3 * world, seed=11)  # 9 full steps + a partial step per epoch
         torch.manual_seed(rank)  # different init per rank: DDP must broadcast rank 0's
         dt = torch.bfloat16 if amp else None
-        ddp = DistributedDataParallel(convert_sync_batchnorm(ConvNet(amp_dtype=dt).cuda()), device_ids=[0])
+        ddp = DistributedDataParallel(convert_sync_batchnorm(ConvNet(amp_dtype=dt).cuda()), device_ids=[0],
+                                      gradient_as_bucket_view=True)
         assert ddp.reducer is not None
         init = copy.deepcopy(ddp.module.state_dict())
         # one step, gradients: DDP-averaged grads of the rank batches == grads of the global batch
@@ -68,7 +85,7 @@ def worker(rank, world, port, amp, graph, q):
         gx = torch.rand(per_rank * world, 1, 28, 28, generator=g).cuda()
         gy = torch.randint(0, 10, (per_rank * world,), generator=g).cuda()
         one = copy.deepcopy(ddp.module)
-        ddp1 = DistributedDataParallel(one, device_ids=[0])
+        ddp1 = DistributedDataParallel(one, device_ids=[0], gradient_as_bucket_view=True)
         sl = slice(rank * per_rank, (rank + 1) * per_rank)
         cross_entropy(ddp1(gx[sl].to(dt or torch.float32)), gy[sl]).backward()
         grads = {k: p.grad.detach().clone() for k, p in one.named_parameters()}
@@ -156,7 +173,8 @@ def worker_poison(rank, world, port, q):
 
         dist.init_process_group("xgmi")
         torch.manual_seed(0)
-        ddp = DistributedDataParallel(convert_sync_batchnorm(ConvNet(amp_dtype=torch.bfloat16).cuda()), device_ids=[0])
+        ddp = DistributedDataParallel(convert_sync_batchnorm(ConvNet(amp_dtype=torch.bfloat16).cuda()), device_ids=[0],
+                                      gradient_as_bucket_view=True)
         ds = synthetic(16 * world * 6, seed=11)
         sampler = DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=False)
         loader = DeviceLoader(ds, batch_size=16, shuffle=False, sampler=sampler, device="cuda", dtype=torch.bfloat16)

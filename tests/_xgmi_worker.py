@@ -37,6 +37,8 @@ def _check(got, exp, dt, what):
 
 def worker(rank, world, port, mode, q):
     try:
+        if world >= 3:  # several ranks on one card: one HW queue each (runtime/device.shared_gpu_env)
+            os.environ["GPU_MAX_HW_QUEUES"] = "1"
         from ddp_practice_amd import _ext
 
         C = _ext.load()

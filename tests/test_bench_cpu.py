@@ -97,6 +97,31 @@ def test_bench_under_torchrun_one_line():
     assert recs[0]["n_gpus"] == 2 and recs[0]["ranks_seen"] == 2 and recs[0]["comm_error"] == ""
 
 
+def test_bench_under_torchrun_eight_ranks():
+    """The driver's N = 8 launch shape on gloo: 8 torchrun workers, each supervising one
+    fresh rank; an epoch of one full batch and a 12-sample tail per rank; rank 0 prints
+    the only line and saw all 8 ranks."""
+    from tests._dist import free_port
+
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    args = ["--gpus", "8", "--steps", "3", "--warmup", "2", "--epochs", "1", "--train-samples", str(8 * 44),
+            "--test-samples", str(8 * 34)]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+                        os.path.join(ROOT, "bench.py"), *args], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout
+    rec = recs[0]
+    assert rec["n_gpus"] == 8 and rec["ranks_seen"] == 8 and rec["comm_error"] == ""
+    assert rec["config"]["parallelism"] == "dp8" and rec["config"]["global_batch"] == 256
+    assert rec["steps"] == 3 and rec["steps_per_rank_per_epoch"] == 2  # 32 + the 12-sample tail
+
+
 def test_bench_under_torchrun_rank_failure_falls_back():
     """torchrun shape with rank 0's child dying at step 2: every worker's supervisor sees the
     shared failure flag, kills its child, and all of them re-run fresh children; rank 0's

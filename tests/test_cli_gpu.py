@@ -155,6 +155,33 @@ def test_ddp_cli_two_ranks_sharing_gpu(C, tmp_path, launcher):
     _check_ranks_equal(tmp_path, 2)
 
 
+@pytest.mark.parametrize("launcher,fused", [("spawn", False), ("torchrun", True)])
+def test_ddp_cli_eight_ranks_sharing_gpu(C, tmp_path, launcher, fused):
+    """W = 8, the driver's node size, on one GPU: eight ranks of the reference's programs
+    (mp.spawn / torchrun), batch 8 per rank, one epoch (938 steps of 8 + a tail of 4 per
+    rank), DDP + SyncBN over the xGMI engine -- launches per collective by default at 3+
+    shared ranks; ``fused``: DPA_FUSED_SYNC=1 DPA_FUSED_GRAD=1 force the in-kernel SyncBN
+    sites and the AMP-SGD gradient exchange, 8 rows and 7 peers each.  The stdout contract,
+    a weights_only checkpoint with module. keys, and eight bitwise-equal rank checkpoints."""
+    gpus = ",".join(str(i) for i in range(8))
+    if launcher == "spawn":
+        args = [os.path.join(ROOT, "ddp_main.py"), "--gpu", gpus, "--share-gpu"]
+    else:
+        args = ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8", "--master-addr=127.0.0.1",
+                f"--master-port={free_port()}", os.path.join(ROOT, "ddp_main_torchrun.py"), "--gpu", gpus,
+                "--share-gpu"]
+    extra = {"DPA_FUSED_SYNC": "1", "DPA_FUSED_GRAD": "1"} if fused else {}
+    out = _run(args + ["-e", "1", "-b", "8", "--synthetic", "--amp-dtype", "bf16", "--seed", "0"], tmp_path,
+               _shared_env(extra), timeout=240)
+    _check_stdout(out, 1)
+    assert out.count("begin testing") == 1  # rank 0 only
+    ck = torch.load(tmp_path / "ddp_checkpoint.pt", weights_only=True)
+    assert list(ck["model"]) == ["module." + k for k in REF_KEYS]
+    m = _load_into_torch(ck["model"])
+    assert int(m.layer1[1].num_batches_tracked) == 938  # ceil(ceil(60000 / 8) / 8) steps per rank
+    _check_ranks_equal(tmp_path, 8)
+
+
 def test_ddp_cli_two_ranks_accuracy_parity_with_torch(C, tmp_path):
     """W=2 sharing one GPU, same data / seed / order: the native program vs the same program on
     torch's DDP (gloo with device tensors, the only torch backend two ranks on one device can

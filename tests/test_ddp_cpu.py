@@ -78,3 +78,17 @@ def test_ddp_gradient_as_bucket_view_false_copies_back():
     from ._ddp_workers import ddp_grad_not_bucket_view
 
     assert all(run(ddp_grad_not_bucket_view, world=2))
+
+
+def test_ddp_syncbn_world8_epoch_tail():
+    """World 8 (BASELINE configs 3-5) on gloo: the per-rank tail of an epoch (12 train /
+    2 test samples per rank, as MNIST's at W=8), padding wrapped from the front, SyncBN
+    statistics over 8 ranks, DDP average of 8 and test() reduced to rank 0 -- the
+    result equals one process on each step's concatenated global batch."""
+    world, batch = 8, 32
+    n_train, n_test = world * (batch + 12) - 3, world * (batch + 2)
+    outs = run(W.ddp_syncbn_epoch_tail, world=world, args=(n_train, n_test, batch), timeout=600)
+    for o in outs:
+        assert o["sizes"] == [32, 12] and o["test_sizes"] == [32, 2]
+    assert outs[0]["size"] == world * (batch + 2)  # the padded test set: 272 samples counted
+    assert 0 <= outs[0]["correct"] <= outs[0]["size"]

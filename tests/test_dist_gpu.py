@@ -105,7 +105,7 @@ def test_ddp_syncbn_fused_graph_matches_plain(rccl, amp, graph):
     torch.manual_seed(0)
     dt = torch.bfloat16 if amp else None
     plain = ConvNet(amp_dtype=dt).cuda()
-    ddp = DistributedDataParallel(convert_sync_batchnorm(copy.deepcopy(plain)), device_ids=[0])
+    ddp = DistributedDataParallel(convert_sync_batchnorm(copy.deepcopy(plain)), device_ids=[0], gradient_as_bucket_view=True)
     assert ddp.reducer is not None
     _train(plain, 2, ds.images, ds.labels, amp, use_graph=False)
     _train(ddp, 2, ds.images, ds.labels, amp, use_graph=graph)
@@ -131,7 +131,7 @@ def test_ddp_syncbn_batch80_takes_launch_path(rccl):
     ds = synthetic(80 * 3 + 7, seed=5)
     torch.manual_seed(0)
     plain = ConvNet(amp_dtype=torch.bfloat16).cuda()
-    ddp = DistributedDataParallel(convert_sync_batchnorm(copy.deepcopy(plain)), device_ids=[0])
+    ddp = DistributedDataParallel(convert_sync_batchnorm(copy.deepcopy(plain)), device_ids=[0], gradient_as_bucket_view=True)
     _train(plain, 2, ds.images, ds.labels, True, use_graph=False, batch=80)
     _train(ddp, 2, ds.images, ds.labels, True, use_graph=True, batch=80)
     for (n, p), (_, q) in zip(ddp.module.state_dict().items(), plain.state_dict().items()):
@@ -151,7 +151,7 @@ def test_xgmi_debug_state_names_sites_and_words(rccl):
     assert x is not None
     ds = synthetic(32 * 3, seed=3)
     torch.manual_seed(0)
-    ddp = DistributedDataParallel(convert_sync_batchnorm(ConvNet(amp_dtype=torch.bfloat16).cuda()), device_ids=[0])
+    ddp = DistributedDataParallel(convert_sync_batchnorm(ConvNet(amp_dtype=torch.bfloat16).cuda()), device_ids=[0], gradient_as_bucket_view=True)
     _train(ddp, 1, ds.images, ds.labels, True, use_graph=False)
     torch.cuda.synchronize()
     st = x.debug_state(2.0)
@@ -264,7 +264,7 @@ def test_ddp_bucket_replan_never_inside_capture(rccl):
     from ddp_practice_amd.runtime import CapturedStep
 
     torch.manual_seed(0)
-    ddp = DistributedDataParallel(ConvNet().cuda(), device_ids=[0], bucket_cap_mb=0.01)
+    ddp = DistributedDataParallel(ConvNet().cuda(), device_ids=[0], bucket_cap_mb=0.01, gradient_as_bucket_view=True)
     opt, crit = SGD(ddp.parameters(), lr=0.01), CrossEntropyLoss()
     x = torch.randn(32, 1, 28, 28, device="cuda")
     y = torch.randint(0, 10, (32,), device="cuda")

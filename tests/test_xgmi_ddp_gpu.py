@@ -1,4 +1,4 @@
-"""DDP + SyncBN ConvNet with 2 processes on the test box's single GPU, all
+"""DDP + SyncBN ConvNet with 2 and 8 processes on the test box's single GPU, all
 all-reduces on the one-shot xGMI engine: the result must equal one process
 training on the global batch, and every rank must end bit-identical."""
 import pytest
@@ -8,16 +8,20 @@ from ._dist import launch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("amp,graph", [(False, False), (False, True), (True, True)])
-def test_ddp_syncbn_xgmi_two_processes(C, amp, graph):
+@pytest.mark.parametrize("world,amp,graph", [(2, False, False), (2, False, True), (2, True, True),
+                                             (8, False, False), (8, True, True)])
+def test_ddp_syncbn_xgmi_processes(C, world, amp, graph):
+    """World 8 (the driver's node size, 8 images per rank, one HW queue per process):
+    8-row SyncBN sites, 7-peer gradient pushes in the AMP-SGD launch and a partial last
+    batch of 3 per rank, each epoch, against one process on the global batch."""
     from ._xgmi_ddp_worker import worker
 
-    world = 2
-    outs = launch(worker, world, (amp, graph), timeout=240)
+    outs = launch(worker, world, (amp, graph), timeout=240 if world <= 2 else 360)
     res = dict(enumerate(outs))
     print("grad errs", res[0]["grad_errs"])
     print("param errs", res[0]["errs"])
-    assert res[0]["digest"] == res[1]["digest"], "ranks diverged"
+    for r in range(1, world):
+        assert res[0]["digest"] == res[r]["digest"], f"rank {r} diverged from rank 0"
 
 
 def test_prechecked_step_agrees_across_ranks(C):
