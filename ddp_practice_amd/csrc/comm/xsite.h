@@ -34,6 +34,24 @@
 
 #include <cstdint>
 
+// The exchange's two workgroup barriers order LDS only (the epoch broadcast, the summed
+// row): an LDS-only barrier (s_waitcnt lgkmcnt(0) + s_barrier) instead of __syncthreads(),
+// whose vmcnt(0) made every wave wait for ALL its outstanding global operations -- the
+// epoch-word stores and peer pushes just issued, and whatever loads the caller had in
+// flight -- at every exchange, with nothing to wait for at W = 1.  Nothing after an
+// exchange reads those stores inside the launch (the epoch words are read by the next
+// launch, the pushes by the peers' polls).  DPA_XS_FULLBAR (experiment builds): the
+// __syncthreads() form, for the A/B.
+#ifdef DPA_XS_FULLBAR
+#define DPA_XS_BARRIER() __syncthreads()
+#else
+#define DPA_XS_BARRIER()                          \
+  do {                                            \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+    __builtin_amdgcn_s_barrier();                 \
+  } while (0)
+#endif
+
 namespace dpa {
 namespace xgmi {
 
@@ -163,14 +181,14 @@ __device__ __forceinline__ float xsite_wait(const XSite& xs, const unsigned long
 // vals: n (<= kSiteVals, <= blockDim.x) floats of LDS holding this rank's local
 // row; replaced by the rank-ordered sum over all ranks.  tk: lane 0's ticket.
 // bid: the workgroup's index in its role (the role's workgroup 0 pushes).  Called by
-// every thread of the workgroup; ends with a barrier.
+// every thread of the workgroup; ends with an LDS-only barrier.
 __device__ __forceinline__ void xsite_exchange(const XSite& xs, float* vals, int n, unsigned long long tk,
                                                int bid, int nthr = 256 /* <= the workgroup size */) {
   __shared__ uint32_t ep_s;
   const int tid = threadIdx.x;
   const bool pusher = bid == 0;
   if (tid == 0) ep_s = xsite_epoch(xs, tk, bid);
-  __syncthreads();
+  DPA_XS_BARRIER();
   DPA_XS_STAMP(13);
   xsite_advance(xs, ep_s, bid, nthr);
   if (tid < n) {
@@ -207,7 +225,7 @@ __device__ __forceinline__ void xsite_exchange(const XSite& xs, float* vals, int
     vals[tid] = acc;  // only this lane reads or writes slot tid in here
   }
   DPA_XS_STAMP(14);
-  __syncthreads();
+  DPA_XS_BARRIER();
   DPA_XS_STAMP(15);
 }
 
@@ -257,7 +275,7 @@ __device__ __forceinline__ void xsite_exchange_slice(const XSite& xs, float* val
   __shared__ uint32_t ep_s;
   const int tid = threadIdx.x;
   if (tid == 0) ep_s = xsite_epoch(xs, tk, bid);
-  __syncthreads();
+  DPA_XS_BARRIER();
   const uint32_t ep = ep_s;
   xsite_advance(xs, ep, bid, nthr);
   for (int i = tid; i < n; i += nthr) xsite_push_at(xs, ep, pos(i), vals[i]);
@@ -265,7 +283,7 @@ __device__ __forceinline__ void xsite_exchange_slice(const XSite& xs, float* val
   unsigned polls = 0;
   bool fail = false;
   for (int i = tid; i < n; i += nthr) vals[i] = xsite_pull_at(xs, ep, pos(i), vals[i], t0, polls, fail);
-  __syncthreads();
+  DPA_XS_BARRIER();
 }
 
 }  // namespace xgmi

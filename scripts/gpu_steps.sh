@@ -1,0 +1,72 @@
+#!/bin/bash
+# usage: bash scripts/gpu_steps.sh TAG STEP [STEP ...]
+# Named GPU measurement steps (each under its own time limit, output under gpurun_out/TAG/,
+# the first failing step ends the run).  Steps:
+#   push_ab      xGMI granule pushes: system-scope atomic vs plain stores (scripts/exp/push_ab.py,
+#                W = 2 and 8 sharing the GPU; needs the _C_pushplain.so experiment build)
+#   xsbar_ab     forced (W>1-shaped) ConvNet step: LDS-only exchange barriers vs __syncthreads
+#                (needs _C_fullbar.so), 3 interleaved rounds
+#   stamps       phase stamps of the fused ConvNet kernels, plain and forced (needs _C_timing.so)
+#   steady       ConvNet steady-state kernel table (rocprofv3 kernel trace), plain and forced
+#   rn_steady    ResNet-50 steady-state kernel table
+#   bench        the driver's bench command and the default 2000-step run
+#   rn_bench     ResNet-50 bench (bs 128, bf16)
+#   rehearse8    bench.py with 8 ranks sharing the GPU under torchrun (scripts/gpu_rehearse.sh)
+#   cli8         the 8-rank shared-GPU CLI tests (tests/test_cli_gpu.py -k eight)
+#   ddp8         the 8-rank DDP + SyncBN xGMI tests, streaming the workers' stall reports
+#   gputests     the whole GPU test tier
+set -o pipefail
+TAG=$1; shift
+cd "$(dirname "$0")/.." && export TMPDIR=/tmp && OUT=$PWD/gpurun_out/$TAG && mkdir -p "$OUT"
+PYT="python -u -m pytest -x -v --timeout-method thread"
+step() {
+  case $1 in
+    push_ab)
+      for W in 2 8; do
+        timeout -k 10 120 python scripts/exp/push_ab.py $W atomic >> "$OUT/push_ab.txt" 2>&1 &&
+        DPA_EXT_SO=ddp_practice_amd/_C_pushplain.so timeout -k 10 120 python scripts/exp/push_ab.py $W plain \
+          >> "$OUT/push_ab.txt" 2>&1 || return 1
+      done ;;
+    xsbar_ab)
+      bash scripts/ab_bench.sh "$OUT/xsbar_ab.txt" 3 "--force-collectives --steps 2000 --warmup 50 --no-baseline \
+--epochs 0 --no-steady --extra-dtypes ," ldsbar=default fullbar=ddp_practice_amd/_C_fullbar.so ;;
+    stamps)
+      DPA_EXT_SO=ddp_practice_amd/_C_timing.so timeout -k 10 120 python scripts/stamp_step.py > "$OUT/stamps_plain.txt" 2>&1 &&
+      DPA_EXT_SO=ddp_practice_amd/_C_timing.so timeout -k 10 120 python scripts/stamp_step.py --forced \
+        > "$OUT/stamps_forced.txt" 2>&1 ;;
+    steady)
+      for m in plain forced; do
+        local F=""; [ $m = forced ] && F=--force-collectives
+        timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/prof_$m" -o run -- python3 bench.py \
+          --steps 640 --warmup 64 --extra-dtypes , --no-baseline --epochs 0 --no-steady $F > "$OUT/prof_$m.json" \
+          2> "$OUT/prof_$m.err" || return 1
+        python3 scripts/trace_steady.py "$(find "$OUT/prof_$m" -name '*kernel_trace.csv' -print -quit)" sgd 128 \
+          > "$OUT/steady_$m.txt" || return 1
+        rm -rf "$OUT/prof_$m"
+      done ;;
+    rn_steady)
+      timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$OUT/prof_rn" -o run -- python3 bench.py \
+        --model resnet50 --steps 20 --warmup 5 > "$OUT/rn_steady.json" 2> "$OUT/rn_steady.err" &&
+      python3 scripts/trace_steady.py "$(find "$OUT/prof_rn" -name '*kernel_trace.csv' -print -quit)" amp_sgd 5 \
+        > "$OUT/rn_steady.txt" && rm -rf "$OUT/prof_rn" ;;
+    bench)
+      timeout -k 10 300 python bench.py --steps 20 --warmup 5 > "$OUT/bench_driver.json" 2> "$OUT/bench_driver.err" &&
+      timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
+    rn_bench)
+      timeout -k 10 400 python bench.py --model resnet50 --steps 20 --warmup 5 > "$OUT/rn_bench.json" 2> "$OUT/rn_bench.err" ;;
+    rehearse8)
+      bash scripts/gpu_rehearse.sh 8 "$TAG/rehearse8" > "$OUT/rehearse8.txt" 2>&1 ;;
+    cli8)
+      timeout -k 10 600 $PYT --timeout 200 tests/test_cli_gpu.py -k eight > "$OUT/cli8.txt" 2>&1 ;;
+    ddp8)
+      DPA_TEST_PROGRESS=1 timeout -k 10 400 $PYT -s --timeout 170 tests/test_xgmi_ddp_gpu.py -k "8-" > "$OUT/ddp8.txt" 2>&1 ;;
+    gputests)
+      timeout -k 10 1100 $PYT --timeout 200 -m gpu tests > "$OUT/gputests.txt" 2>&1 ;;
+    *) echo "unknown step $1"; return 2 ;;
+  esac
+}
+for s in "$@"; do
+  echo "[gpu_steps] $s start $(date +%T)" | tee -a "$OUT/steps.log"
+  step "$s" || { echo "[gpu_steps] $s FAILED" | tee -a "$OUT/steps.log"; exit 1; }
+  echo "[gpu_steps] $s ok $(date +%T)" | tee -a "$OUT/steps.log"
+done

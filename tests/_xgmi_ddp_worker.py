@@ -29,8 +29,32 @@ def _train(model, ds, batch, scaler_on, use_graph, sampler=None, epochs=2):
         if sampler is not None:
             sampler.set_epoch(e)
         loop.run_epoch()
+        if os.environ.get("DPA_TEST_PROGRESS") == "1":
+            import sys
+
+            torch.cuda.synchronize()
+            print(f"[pid {os.getpid()}] epoch {e} done", file=sys.stderr, flush=True)
     assert loop.graph_error is None, loop.graph_error
     return model
+
+
+def _stall_report(c, rank, after_s):
+    """Print this rank's engine state (host-issued counts, every site's epoch words and the
+    peers' newest granule epochs: XgmiComm.debug_state) if the worker is still running
+    after ``after_s`` -- a stall then names its exchange instead of timing out silently."""
+    import sys
+    import threading
+
+    def dump():
+        try:
+            print(f"[rank {rank}] still running after {after_s:.0f} s: {c.xgmi.debug_state(1.0)}", file=sys.stderr,
+                  flush=True)
+        except Exception as e:  # pragma: no cover - diagnostics only
+            print(f"[rank {rank}] debug_state failed: {e!r}", file=sys.stderr, flush=True)
+
+    t = threading.Timer(after_s, dump)
+    t.daemon = True
+    t.start()
 
 
 def _digest(sd):
@@ -56,6 +80,8 @@ def worker(rank, world, port, amp, graph, q):
             shared_gpu_env(world)
             os.environ["DPA_FUSED_SYNC"] = "1"
             os.environ["DPA_FUSED_GRAD"] = "1"
+            # a stalled exchange gives up (error word) well inside the test's budget
+            os.environ.setdefault("DPA_XGMI_TIMEOUT", "45")
         torch.cuda.set_device(0)
         import ddp_practice_amd.distributed as dist
         from ddp_practice_amd.data import DistributedSampler, synthetic
@@ -64,6 +90,8 @@ def worker(rank, world, port, amp, graph, q):
 
         c = dist.init_process_group("xgmi")
         assert isinstance(c, XgmiCommunicator)
+        if world >= 3:
+            _stall_report(c, rank, 40.0)
         from ddp_practice_amd.ops.convnet_fused import _fused_site_engine
 
         # the SyncBN sums are exchanged inside the kernels (not one launch per collective)

@@ -171,8 +171,9 @@ def test_ddp_cli_eight_ranks_sharing_gpu(C, tmp_path, launcher, fused):
                 f"--master-port={free_port()}", os.path.join(ROOT, "ddp_main_torchrun.py"), "--gpu", gpus,
                 "--share-gpu"]
     extra = {"DPA_FUSED_SYNC": "1", "DPA_FUSED_GRAD": "1"} if fused else {}
+    extra["DPA_WATCHDOG_TIMEOUT"] = "60"  # a stall ends the run (exit 124, site dump) inside the budget
     out = _run(args + ["-e", "1", "-b", "8", "--synthetic", "--amp-dtype", "bf16", "--seed", "0"], tmp_path,
-               _shared_env(extra), timeout=240)
+               _shared_env(extra), timeout=160)
     _check_stdout(out, 1)
     assert out.count("begin testing") == 1  # rank 0 only
     ck = torch.load(tmp_path / "ddp_checkpoint.pt", weights_only=True)

@@ -16,7 +16,7 @@ def test_ddp_syncbn_xgmi_processes(C, world, amp, graph):
     batch of 3 per rank, each epoch, against one process on the global batch."""
     from ._xgmi_ddp_worker import worker
 
-    outs = launch(worker, world, (amp, graph), timeout=240 if world <= 2 else 360)
+    outs = launch(worker, world, (amp, graph), timeout=240 if world <= 2 else 150)
     res = dict(enumerate(outs))
     print("grad errs", res[0]["grad_errs"])
     print("param errs", res[0]["errs"])
