@@ -437,9 +437,10 @@ def run_rank(args) -> int:
         os.environ["DPA_COMM"] = args.comm
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.share_gpu:  # ranks share one device (ops/convnet_fused.py; one HW queue each at 3+)
-        from ddp_practice_amd.runtime.device import shared_gpu_env
+        from ddp_practice_amd.runtime.device import shared_cu_mask, shared_gpu_env
 
         shared_gpu_env(world)  # before the first HIP call below
+        shared_cu_mask(world, int(os.environ.get("RANK", "0")))
     gpu = torch.cuda.is_available()
     local_rank = 0 if args.share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     if gpu:
@@ -837,9 +838,10 @@ def bench_resnet(args) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = 0 if args.share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     if args.share_gpu:  # ranks share one device (one HW queue each at 3+: runtime/device.py)
-        from ddp_practice_amd.runtime.device import shared_gpu_env
+        from ddp_practice_amd.runtime.device import shared_cu_mask, shared_gpu_env
 
         shared_gpu_env(world)
+        shared_cu_mask(world, int(os.environ.get("RANK", "0")))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist_path = world > 1 or args.force_collectives

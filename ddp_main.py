@@ -63,8 +63,9 @@ def init_ddp(local_rank, args=None):
     import torch
 
     import ddp_practice_amd.distributed as dist
-    from ddp_practice_amd.cli import dist_backend, rank_device_index
+    from ddp_practice_amd.cli import dist_backend, rank_device_index, share_gpu_rank_env
 
+    share_gpu_rank_env(args, local_rank)
     if torch.cuda.is_available():
         torch.cuda.set_device(rank_device_index(args, local_rank))
     os.environ["RANK"] = str(local_rank)

@@ -39,9 +39,10 @@ def main(args):
     import torch
 
     import ddp_practice_amd.distributed as dist
-    from ddp_practice_amd.cli import dist_backend, rank_device_index, run
+    from ddp_practice_amd.cli import dist_backend, rank_device_index, run, share_gpu_rank_env
 
     local_rank = int(os.environ["LOCAL_RANK"])
+    share_gpu_rank_env(args, local_rank)
     gpu = torch.cuda.is_available()
     if gpu:
         torch.cuda.set_device(rank_device_index(args, local_rank))

@@ -87,6 +87,16 @@ def apply_env(args) -> None:
         shared_gpu_env(world)
 
 
+def share_gpu_rank_env(args, local_rank: int) -> None:
+    """The per-rank part of ``--share-gpu`` (runtime/device.shared_cu_mask: this rank's own
+    range of compute units from 3 ranks).  Before the rank's first HIP call, which
+    ``torch.cuda.is_available()`` is."""
+    if getattr(args, "share_gpu", False):
+        from .runtime.device import shared_cu_mask
+
+        shared_cu_mask(int(os.environ.get("WORLD_SIZE", "1")), local_rank)
+
+
 def rank_device_index(args, local_rank: int) -> int:
     """The device a rank runs on: its local rank, or device 0 for every rank with --share-gpu."""
     return 0 if getattr(args, "share_gpu", False) else local_rank

@@ -19,6 +19,7 @@
 #include <ATen/hip/HIPContext.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 namespace dpa {
 
@@ -307,11 +308,22 @@ constexpr int ceil_to(int x, int m) { return (x + m - 1) / m * m; }
 // can over-report by one workgroup per CU for SGPR-heavy kernels
 // (MI355X_MICROARCH.md "Residency and cooperative launch"), so one is taken
 // off whenever it reports more than one.
+// The CUs this process's workgroups may use: the device's, or fewer for a rank confined to a
+// CU range (runtime/device.shared_cu_mask: HSA_CU_MASK, DPA_RESIDENT_CUS).
+inline int resident_cus(int device_cus) {
+  static const int cap = [] {
+    const char* e = std::getenv("DPA_RESIDENT_CUS");
+    return e != nullptr ? std::atoi(e) : 0;
+  }();
+  return cap > 0 && cap < device_cus ? cap : device_cus;
+}
+
 inline bool co_resident(const void* kernel, int grid, int threads, size_t lds = 0) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return false;
   int cus = 0, per_cu = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+  cus = resident_cus(cus);
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds) != hipSuccess) return false;
   const int eff = per_cu > 1 ? per_cu - 1 : per_cu;
   return (long long)grid <= (long long)eff * cus;

@@ -515,6 +515,7 @@ static int large_grid() {
     int dev = 0, cus = 0;
     DPA_CHECK_HIP(hipGetDevice(&dev));
     DPA_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    cus = resident_cus(cus);
     const void* k = reinterpret_cast<const void*>(&amp_sgd_large_kernel);
     for (int per = 2; per >= 1; --per)
       if (co_resident(k, cus * per, LARGE_THR)) return cus * per;

@@ -45,3 +45,27 @@ def shared_gpu_env(world: int | None) -> None:
         q = "1"
     if q:
         os.environ["GPU_MAX_HW_QUEUES"] = q
+
+
+def shared_cu_mask(world: int | None, rank: int) -> str | None:
+    """Ranks sharing one device (``--share-gpu`` rehearsals), 3 or more: rank ``rank`` runs on
+    its own 1/world of the compute units (``HSA_CU_MASK``, read by the HSA runtime when it
+    creates the process's queues), and the residency checks of the fused kernels count only
+    those (``DPA_RESIDENT_CUS``, csrc/common.h co_resident).
+
+    Why: every rank's in-kernel exchanges and grid barriers spin until their peers / their
+    own workgroups arrive.  With one rank per GPU (the driver's multi-GPU run) a rank's
+    kernels always have a whole card; eight ranks on ONE card without masks let the spinning
+    workgroups of seven ranks occupy the CUs a waiting eighth rank needs -- the world-8
+    rehearsals stalled so (profiles/r6c_rehearse8_stall.txt).  Disjoint CU ranges make each
+    rank a small "GPU" of its own.  ``DPA_SHARED_CUS`` is the device's CU count (MI355X: 256),
+    ``DPA_SHARED_CU_MASK=0`` disables the masks.  Before the rank's first HIP call only."""
+    if world is None or world < 3 or os.environ.get("DPA_SHARED_CU_MASK", "1") == "0":
+        return None
+    n = int(os.environ.get("DPA_SHARED_CUS", "256"))
+    per = max(1, n // world)
+    lo = (rank % world) * per
+    mask = f"0:{lo}-{lo + per - 1}"
+    os.environ["HSA_CU_MASK"] = mask
+    os.environ["DPA_RESIDENT_CUS"] = str(per)
+    return mask

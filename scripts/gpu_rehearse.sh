@@ -1,10 +1,12 @@
 #!/bin/bash
 # usage: bash scripts/gpu_rehearse.sh W TAG
 # W ranks of bench.py sharing the ONE GPU of the box under torchrun (the driver's N-GPU launch
-# shape; one HIP hardware queue per rank at 3+, runtime/device.shared_gpu_env):
+# shape; one HIP hardware queue and 1/W of the CUs per rank at 3+, runtime/device.py):
+#   share_w${W}_host.json  --comm host: DDP / SyncBN collectives staged through gloo (no
+#                        spinning kernel anywhere: the rank logic alone at world W)
 #   share_w$W.json       default --share-gpu path: the xGMI engine, one launch per SyncBN
 #                        collective at 3+ shared ranks (ops/convnet_fused._fused_site_engine)
-#   share_w${W}_fused.json  batch 8, DPA_FUSED_SYNC=1 DPA_FUSED_GRAD=1: the in-kernel SyncBN
+#   share_w${W}_fused.json  batch 4, DPA_FUSED_SYNC=1 DPA_FUSED_GRAD=1: the in-kernel SyncBN
 #                        sites and the AMP-SGD gradient exchange forced on (W rows, W-1 peers)
 # Each JSON line must carry fallback null, comm_error "" and ranks_seen == W.
 set -o pipefail
@@ -27,6 +29,7 @@ print(sys.argv[1].rsplit("/", 1)[-1], {k: rec.get(k) for k in keys})
 assert rec["ranks_seen"] == int(sys.argv[2]) and rec["fallback"] is None and not rec["comm_error"], rec
 EOF
 }
-run share_w$W DPA_BENCH_WATCHDOG=120 -- --steps 300 --warmup 32 --no-baseline --no-steady && \
-run share_w${W}_fused DPA_FUSED_SYNC=1 DPA_FUSED_GRAD=1 DPA_BENCH_WATCHDOG=120 -- --steps 300 --warmup 32 \
-  --batch-size 8 --no-baseline --no-steady
+run share_w${W}_host DPA_BENCH_WATCHDOG=60 -- --steps 300 --warmup 32 --no-baseline --no-steady --comm host --no-graph && \
+run share_w$W DPA_BENCH_WATCHDOG=60 -- --steps 300 --warmup 32 --no-baseline --no-steady && \
+run share_w${W}_fused DPA_FUSED_SYNC=1 DPA_FUSED_GRAD=1 DPA_BENCH_WATCHDOG=60 -- --steps 300 --warmup 32 \
+  --batch-size 4 --no-baseline --no-steady

@@ -14,6 +14,7 @@
 #   rehearse8    bench.py with 8 ranks sharing the GPU under torchrun (scripts/gpu_rehearse.sh)
 #   cli8         the 8-rank shared-GPU CLI tests (tests/test_cli_gpu.py -k eight)
 #   ddp8         the 8-rank DDP + SyncBN xGMI tests, streaming the workers' stall reports
+#   branches     do captured hipGraph fork/join branches overlap? (scripts/exp/graph_branches.py)
 #   gputests     the whole GPU test tier
 set -o pipefail
 TAG=$1; shift
@@ -60,6 +61,10 @@ step() {
       timeout -k 10 600 $PYT --timeout 200 tests/test_cli_gpu.py -k eight > "$OUT/cli8.txt" 2>&1 ;;
     ddp8)
       DPA_TEST_PROGRESS=1 timeout -k 10 400 $PYT -s --timeout 170 tests/test_xgmi_ddp_gpu.py -k "8-" > "$OUT/ddp8.txt" 2>&1 ;;
+    branches)
+      for e in "X=0" "DEBUG_CLR_GRAPH_PACKET_CAPTURE=0" "DEBUG_HIP_FORCE_GRAPH_QUEUES=4" "GPU_MAX_HW_QUEUES=8"; do
+        env $e timeout -k 10 60 python scripts/exp/graph_branches.py >> "$OUT/branches.txt" 2>&1 || return 1
+      done ;;
     gputests)
       timeout -k 10 1100 $PYT --timeout 200 -m gpu tests > "$OUT/gputests.txt" 2>&1 ;;
     *) echo "unknown step $1"; return 2 ;;

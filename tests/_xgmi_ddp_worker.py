@@ -74,10 +74,11 @@ def worker(rank, world, port, amp, graph, q):
             # several ranks on one card (runtime/device.shared_gpu_env: one HW queue each, and
             # no launch whose own grid barrier needs a whole card per rank -- the deferred conv1
             # weight gradient); the in-kernel SyncBN sites and the AMP-SGD gradient exchange
-            # forced on: at 8 images per rank all eight ranks' exchanging grids fit together
-            from ddp_practice_amd.runtime.device import shared_gpu_env
+            # forced on
+            from ddp_practice_amd.runtime.device import shared_cu_mask, shared_gpu_env
 
             shared_gpu_env(world)
+            shared_cu_mask(world, rank)  # this rank's own CU range: a small "GPU" per rank
             os.environ["DPA_FUSED_SYNC"] = "1"
             os.environ["DPA_FUSED_GRAD"] = "1"
             # a stalled exchange gives up (error word) well inside the test's budget
@@ -95,10 +96,11 @@ def worker(rank, world, port, amp, graph, q):
         from ddp_practice_amd.ops.convnet_fused import _fused_site_engine
 
         # the SyncBN sums are exchanged inside the kernels (not one launch per collective)
-        assert _fused_site_engine(c, 16 if world <= 2 else 8, torch.bfloat16 if amp else torch.float32) is not None
-        # 8 ranks on one card: 8 images each, so every rank's exchanging grids (in-kernel
-        # SyncBN sites, the AMP-SGD gradient exchange) are co-resident
-        per_rank = 16 if world <= 2 else 8
+        assert _fused_site_engine(c, 16 if world <= 2 else 4, torch.bfloat16 if amp else torch.float32) is not None
+        # 8 ranks on one card, 32 CUs each (shared_cu_mask): 4 images per rank, so every
+        # exchanging grid (in-kernel SyncBN sites, the AMP-SGD gradient exchange) is co-resident
+        # within the rank's CUs
+        per_rank = 16 if world <= 2 else 4
         ds = synthetic(per_rank * world * 9 + 3 * world, seed=11)  # 9 full steps + a partial step per epoch
         torch.manual_seed(rank)  # different init per rank: DDP must broadcast rank 0's
         dt = torch.bfloat16 if amp else None

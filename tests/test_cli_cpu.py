@@ -114,6 +114,22 @@ def test_ddp_main_timer_includes_child_interpreter(tmp_path, spawn):
     assert elapsed >= max(starts) - t0[0]
 
 
+def test_shared_cu_mask_gives_each_rank_its_own_cus(monkeypatch):
+    """--share-gpu from 3 ranks: disjoint CU ranges (HSA_CU_MASK) covering the device, and the
+    residency checks told the per-rank count (DPA_RESIDENT_CUS)."""
+    from ddp_practice_amd.runtime.device import shared_cu_mask
+
+    for k in ("HSA_CU_MASK", "DPA_RESIDENT_CUS", "DPA_SHARED_CUS", "DPA_SHARED_CU_MASK"):
+        monkeypatch.delenv(k, raising=False)
+    assert shared_cu_mask(2, 1) is None and "HSA_CU_MASK" not in os.environ
+    masks = [shared_cu_mask(8, r) for r in range(8)]
+    assert masks[0] == "0:0-31" and masks[7] == "0:224-255" and os.environ["DPA_RESIDENT_CUS"] == "32"
+    cus = [set(range(int(m[2:].split("-")[0]), int(m.split("-")[1]) + 1)) for m in masks]
+    assert set().union(*cus) == set(range(256)) and sum(len(c) for c in cus) == 256
+    monkeypatch.setenv("DPA_SHARED_CU_MASK", "0")
+    assert shared_cu_mask(8, 3) is None
+
+
 def test_shared_gpu_env_one_hw_queue_from_three_ranks(monkeypatch):
     """--share-gpu: ranks get the fused-path gates, and from 3 ranks one HIP hardware queue
     per process (4 processes with 4 queues each stalled on one MI355X; profiles/r5v_*)."""

@@ -158,10 +158,11 @@ def test_ddp_cli_two_ranks_sharing_gpu(C, tmp_path, launcher):
 @pytest.mark.parametrize("launcher,fused", [("spawn", False), ("torchrun", True)])
 def test_ddp_cli_eight_ranks_sharing_gpu(C, tmp_path, launcher, fused):
     """W = 8, the driver's node size, on one GPU: eight ranks of the reference's programs
-    (mp.spawn / torchrun), batch 8 per rank, one epoch (938 steps of 8 + a tail of 4 per
-    rank), DDP + SyncBN over the xGMI engine -- launches per collective by default at 3+
-    shared ranks; ``fused``: DPA_FUSED_SYNC=1 DPA_FUSED_GRAD=1 force the in-kernel SyncBN
-    sites and the AMP-SGD gradient exchange, 8 rows and 7 peers each.  The stdout contract,
+    (mp.spawn / torchrun), each on its own 32 CUs (runtime/device.shared_cu_mask), one epoch,
+    DDP + SyncBN over the xGMI engine -- batch 8 (937 steps + a tail of 4 per rank) with one
+    launch per SyncBN collective, the default at 3+ shared ranks; ``fused``: batch 4 with
+    DPA_FUSED_SYNC=1 DPA_FUSED_GRAD=1 forcing the in-kernel SyncBN sites and the AMP-SGD
+    gradient exchange, 8 rows and 7 peers each.  The stdout contract,
     a weights_only checkpoint with module. keys, and eight bitwise-equal rank checkpoints."""
     gpus = ",".join(str(i) for i in range(8))
     if launcher == "spawn":
@@ -172,14 +173,15 @@ def test_ddp_cli_eight_ranks_sharing_gpu(C, tmp_path, launcher, fused):
                 "--share-gpu"]
     extra = {"DPA_FUSED_SYNC": "1", "DPA_FUSED_GRAD": "1"} if fused else {}
     extra["DPA_WATCHDOG_TIMEOUT"] = "60"  # a stall ends the run (exit 124, site dump) inside the budget
-    out = _run(args + ["-e", "1", "-b", "8", "--synthetic", "--amp-dtype", "bf16", "--seed", "0"], tmp_path,
+    b = 4 if fused else 8  # fused: every exchanging grid co-resident on the rank's 32 CUs
+    out = _run(args + ["-e", "1", "-b", str(b), "--synthetic", "--amp-dtype", "bf16", "--seed", "0"], tmp_path,
                _shared_env(extra), timeout=160)
     _check_stdout(out, 1)
     assert out.count("begin testing") == 1  # rank 0 only
     ck = torch.load(tmp_path / "ddp_checkpoint.pt", weights_only=True)
     assert list(ck["model"]) == ["module." + k for k in REF_KEYS]
     m = _load_into_torch(ck["model"])
-    assert int(m.layer1[1].num_batches_tracked) == 938  # ceil(ceil(60000 / 8) / 8) steps per rank
+    assert int(m.layer1[1].num_batches_tracked) == -(-7500 // b)  # ceil(ceil(60000 / 8) / b) steps per rank
     _check_ranks_equal(tmp_path, 8)
 
 

@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("world,amp,graph", [(2, False, False), (2, False, True), (2, True, True),
                                              (8, False, False), (8, True, True)])
 def test_ddp_syncbn_xgmi_processes(C, world, amp, graph):
-    """World 8 (the driver's node size, 8 images per rank, one HW queue per process):
+    """World 8 (the driver's node size; per rank 4 images, one HW queue and 32 CUs):
     8-row SyncBN sites, 7-peer gradient pushes in the AMP-SGD launch and a partial last
     batch of 3 per rank, each epoch, against one process on the global batch."""
     from ._xgmi_ddp_worker import worker
