@@ -810,8 +810,10 @@ def _torchref_resnet_step(model, images, labels, amp, lr: float):
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
+    from ddp_practice_amd.runtime.graph import gc_paused
+
     try:
-        with torch.cuda.graph(g):
+        with gc_paused(), torch.cuda.graph(g):
             step()
     except Exception as e:  # noqa: BLE001 - reported in the JSON line, eager fallback
         torch.cuda.synchronize()

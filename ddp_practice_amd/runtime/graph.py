@@ -14,6 +14,8 @@ compiler here, just stream capture of the exact eager kernel sequence.
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 import os
 from typing import Callable
 
@@ -34,6 +36,24 @@ def _upload(g: "torch.cuda.CUDAGraph") -> None:
 
     _load_ext().runtime.graph_upload(exec_)
     torch.cuda.synchronize()
+
+
+@contextlib.contextmanager
+def gc_paused():
+    """No automatic garbage collection while a stream is being captured.  A collection that
+    runs inside the capture -- in any thread, the autograd engine's included -- and frees an
+    unreachable earlier graph destroys its executable then, which HIP refuses during a
+    capture (hipErrorStreamCaptureUnsupported from ~CUDAGraph: a terminate in the 8-rank
+    shared-GPU rehearsal, profiles/r6d_rehearse8_gc_in_capture.txt).  Collected before,
+    paused during, restored after."""
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 class CapturedStep:
@@ -62,7 +82,7 @@ class CapturedStep:
             self.pre_capture()
         g = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.graph(g):
+            with gc_paused(), torch.cuda.graph(g):
                 for _ in range(self.steps_per_graph):
                     self.fn()
         except Exception as e:  # pragma: no cover - depends on the device runtime
