@@ -602,6 +602,7 @@ XSite XgmiComm::site(int s) const {
   site_calls_[s].fetch_add(1, std::memory_order_relaxed);  // (a handle per attached launch)
   XSite x;
   for (int p = 0; p < world_; ++p) x.base[p] = peers_.base[p] + site_off_ + (long long)s * kSiteBytes;
+  x.mine = x.base[rank_];
   x.tick = ticks_ + (long long)s * kEpochWords;
   x.rank = rank_;
   x.world = world_;
@@ -614,6 +615,7 @@ XSite XgmiComm::site(int s) const {
 XSite XgmiComm::grad_site() const {
   XSite x = site(kSiteGrad);
   for (int p = 0; p < world_; ++p) x.base[p] = peers_.base[p] + grad_off_;
+  x.mine = x.base[rank_];
   x.slot_bytes = slot_bytes_;
   x.max_vals = max_elems_;
   return x;
@@ -622,6 +624,7 @@ XSite XgmiComm::grad_site() const {
 XSite XgmiComm::wide_site() const {
   XSite x = site(kSiteWide);
   for (int p = 0; p < world_; ++p) x.base[p] = peers_.base[p] + wide_off_;
+  x.mine = x.base[rank_];
   x.slot_bytes = (long long)kWideVals * 8;
   x.max_vals = kWideVals;
   return x;

@@ -75,6 +75,7 @@ constexpr int kSiteGrad = kSites - 1;
 
 struct XSite {
   char* base[kMaxRanks] = {};            // this site's region in every rank's workspace (peer-mapped)
+  char* mine = nullptr;                  // base[rank]: polled without a rank-indexed kernel-argument load
   unsigned long long* tick = nullptr;    // this rank's kEpochWords epoch words of the site;
                                          // nullptr: site inactive
   int rank = 0, world = 1;
@@ -105,6 +106,12 @@ __device__ __forceinline__ void xgmi_put2(unsigned long long* dst, unsigned long
 #ifdef DPA_PUSH_PLAIN
   typedef __attribute__((ext_vector_type(2))) unsigned long long v2;
   *reinterpret_cast<v2*>(dst) = v2{a, b};
+#elif defined(DPA_PUSH_ASM)
+  // one 16-B vector store with the system-scope cache policy bits (sc0 sc1), as the 8-B
+  // system-scope atomic store is encoded; a vector store (never the scalar cache)
+  typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+  const u32x4 v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(v) : "memory");
 #else
   __hip_atomic_store(dst, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(dst + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -190,24 +197,27 @@ __device__ __forceinline__ void xsite_exchange(const XSite& xs, float* vals, int
   if (tid == 0) ep_s = xsite_epoch(xs, tk, bid);
   DPA_XS_BARRIER();
   DPA_XS_STAMP(13);
-  xsite_advance(xs, ep_s, bid, nthr);
+  const uint32_t ep = ep_s;
   if (tid < n) {
-    const uint32_t ep = ep_s;
     const long long par = (long long)(ep & 1u) * kMaxRanks * xs.slot_bytes;
     const float mine = vals[tid];
     const unsigned long long gm = ((unsigned long long)ep << 32) | (unsigned long long)__float_as_uint(mine);
-    if (pusher)
-      for (int p = 0; p < xs.world; ++p)
-        if (p != xs.rank)
+    // peers unrolled with a predicate: the kernel-argument loads of base[p] carry static
+    // offsets (issued together, not a rank-indexed dependent chain in a loop)
+    if (pusher) {
+#pragma unroll
+      for (int p = 0; p < kMaxRanks; ++p)
+        if (p < xs.world && p != xs.rank)
           xgmi_put(reinterpret_cast<unsigned long long*>(xs.base[p] + par + (long long)xs.rank * xs.slot_bytes +
                                                          (long long)tid * 8),
                    gm);
+    }
     // every peer's granule loaded before the first tag check (one round trip)
     unsigned long long g[kMaxRanks];
     const unsigned long long* src[kMaxRanks];
 #pragma unroll
     for (int p = 0; p < kMaxRanks; ++p) {
-      src[p] = reinterpret_cast<const unsigned long long*>(xs.base[xs.rank] + par + (long long)p * xs.slot_bytes +
+      src[p] = reinterpret_cast<const unsigned long long*>(xs.mine + par + (long long)p * xs.slot_bytes +
                                                            (long long)tid * 8);
       g[p] = (p < xs.world && p != xs.rank) ? __hip_atomic_load(src[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                             : gm;
@@ -225,6 +235,10 @@ __device__ __forceinline__ void xsite_exchange(const XSite& xs, float* vals, int
     vals[tid] = acc;  // only this lane reads or writes slot tid in here
   }
   DPA_XS_STAMP(14);
+  // the epoch words last: read only by the site's next launch, so their stores drain behind
+  // the LDS-only barrier and the caller's work instead of ahead of the polls' first wait
+  // (an s_waitcnt vmcnt(0) there also retired every store issued before it)
+  xsite_advance(xs, ep, bid, nthr);
   DPA_XS_BARRIER();
   DPA_XS_STAMP(15);
 }
@@ -241,8 +255,9 @@ __device__ __forceinline__ void xsite_push_at(const XSite& xs, uint32_t ep, int 
   const long long off = (long long)(ep & 1u) * kMaxRanks * xs.slot_bytes + (long long)xs.rank * xs.slot_bytes +
                         (long long)pos * 8;
   const unsigned long long gm = ((unsigned long long)ep << 32) | (unsigned long long)__float_as_uint(mine);
-  for (int p = 0; p < xs.world; ++p)
-    if (p != xs.rank) xgmi_put(reinterpret_cast<unsigned long long*>(xs.base[p] + off), gm);
+#pragma unroll
+  for (int p = 0; p < kMaxRanks; ++p)
+    if (p < xs.world && p != xs.rank) xgmi_put(reinterpret_cast<unsigned long long*>(xs.base[p] + off), gm);
 }
 
 __device__ __forceinline__ float xsite_pull_at(const XSite& xs, uint32_t ep, int pos, float mine, long long t0,
@@ -252,7 +267,7 @@ __device__ __forceinline__ float xsite_pull_at(const XSite& xs, uint32_t ep, int
   const unsigned long long* src[kMaxRanks];
 #pragma unroll
   for (int p = 0; p < kMaxRanks; ++p) {  // every peer's granule in flight before the first check
-    src[p] = reinterpret_cast<const unsigned long long*>(xs.base[xs.rank] + off + (long long)p * xs.slot_bytes);
+    src[p] = reinterpret_cast<const unsigned long long*>(xs.mine + off + (long long)p * xs.slot_bytes);
     g[p] = (p < xs.world && p != xs.rank) ? __hip_atomic_load(src[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                           : (((unsigned long long)ep << 32) | __float_as_uint(mine));
   }
@@ -277,12 +292,12 @@ __device__ __forceinline__ void xsite_exchange_slice(const XSite& xs, float* val
   if (tid == 0) ep_s = xsite_epoch(xs, tk, bid);
   DPA_XS_BARRIER();
   const uint32_t ep = ep_s;
-  xsite_advance(xs, ep, bid, nthr);
   for (int i = tid; i < n; i += nthr) xsite_push_at(xs, ep, pos(i), vals[i]);
   const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
   unsigned polls = 0;
   bool fail = false;
   for (int i = tid; i < n; i += nthr) vals[i] = xsite_pull_at(xs, ep, pos(i), vals[i], t0, polls, fail);
+  xsite_advance(xs, ep, bid, nthr);  // last, as in xsite_exchange
   DPA_XS_BARRIER();
 }
 

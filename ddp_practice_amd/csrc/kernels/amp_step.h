@@ -341,7 +341,7 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
       const unsigned long long* src[xgmi::kMaxRanks];
 #pragma unroll
       for (int p = 0; p < xgmi::kMaxRanks; ++p) {  // every load issued before the first tag check
-        src[p] = reinterpret_cast<const unsigned long long*>(xg.base[xg.rank] + par + (long long)p * xg.slot_bytes +
+        src[p] = reinterpret_cast<const unsigned long long*>(xg.mine + par + (long long)p * xg.slot_bytes +
                                                              fo);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -376,7 +376,7 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
       const unsigned long long* src[xgmi::kMaxRanks];
 #pragma unroll
       for (int p = 0; p < xgmi::kMaxRanks; ++p) {
-        src[p] = reinterpret_cast<const unsigned long long*>(xg.base[xg.rank] + par + (long long)p * xg.slot_bytes +
+        src[p] = reinterpret_cast<const unsigned long long*>(xg.mine + par + (long long)p * xg.slot_bytes +
                                                              fo);
         g[p] = (p < xg.world && p != xg.rank) ? __hip_atomic_load(src[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                               : 0ull;

@@ -2,8 +2,12 @@
 # usage: bash scripts/gpu_steps.sh TAG STEP [STEP ...]
 # Named GPU measurement steps (each under its own time limit, output under gpurun_out/TAG/,
 # the first failing step ends the run).  Steps:
-#   push_ab      xGMI granule pushes: system-scope atomic vs plain stores (scripts/exp/push_ab.py,
-#                W = 2 and 8 sharing the GPU; needs the _C_pushplain.so experiment build)
+#   push_ab      xGMI granule pushes: 2 x 8-B system-scope atomic stores vs one 16-B sc0 sc1 store
+#                vs plain 16-B stores (scripts/exp/push_ab.py, W = 2 and 8 sharing the GPU; needs
+#                the _C_pushasm.so / _C_pushplain.so experiment builds)
+#   xsord_ab     forced step: exchange with epoch words advanced last / static peer unroll vs the
+#                previous exchange (_C_xsold.so)
+#   cumask       does HSA_CU_MASK / ROC_GLOBAL_CU_MASK confine a process's kernels? (GEMM rate)
 #   xsbar_ab     forced (W>1-shaped) ConvNet step: LDS-only exchange barriers vs __syncthreads
 #                (needs _C_fullbar.so), 3 interleaved rounds
 #   stamps       phase stamps of the fused ConvNet kernels, plain and forced (needs _C_timing.so)
@@ -15,6 +19,7 @@
 #   cli8         the 8-rank shared-GPU CLI tests (tests/test_cli_gpu.py -k eight)
 #   ddp8         the 8-rank DDP + SyncBN xGMI tests, streaming the workers' stall reports
 #   branches     do captured hipGraph fork/join branches overlap? (scripts/exp/graph_branches.py)
+#   xtests       the xGMI / distributed / SyncBN / fused-ConvNet GPU tests (world-8 DDP excluded)
 #   gputests     the whole GPU test tier
 set -o pipefail
 TAG=$1; shift
@@ -24,9 +29,17 @@ step() {
   case $1 in
     push_ab)
       for W in 2 8; do
-        timeout -k 10 120 python scripts/exp/push_ab.py $W atomic >> "$OUT/push_ab.txt" 2>&1 &&
-        DPA_EXT_SO=ddp_practice_amd/_C_pushplain.so timeout -k 10 120 python scripts/exp/push_ab.py $W plain \
-          >> "$OUT/push_ab.txt" 2>&1 || return 1
+        for v in atomic asm plain; do
+          local so=""; [ $v = asm ] && so=ddp_practice_amd/_C_pushasm.so; [ $v = plain ] && so=ddp_practice_amd/_C_pushplain.so
+          DPA_EXT_SO=$so timeout -k 10 120 python scripts/exp/push_ab.py $W $v >> "$OUT/push_ab.txt" 2>&1 || return 1
+        done
+      done ;;
+    xsord_ab)
+      DPA_ALLOW_STALE_EXT=1 bash scripts/ab_bench.sh "$OUT/xsord_ab.txt" 3 "--force-collectives --steps 2000 --warmup 50 \
+--no-baseline --epochs 0 --no-steady --extra-dtypes ," new=default old=ddp_practice_amd/_C_xsold.so ;;
+    cumask)
+      for e in "X=0" "HSA_CU_MASK=0:0-31" "ROC_GLOBAL_CU_MASK=0xffffffff"; do
+        env $e timeout -k 10 60 python scripts/exp/cu_mask_probe.py >> "$OUT/cumask.txt" 2>&1 || return 1
       done ;;
     xsbar_ab)
       bash scripts/ab_bench.sh "$OUT/xsbar_ab.txt" 3 "--force-collectives --steps 2000 --warmup 50 --no-baseline \
@@ -65,6 +78,9 @@ step() {
       for e in "X=0" "DEBUG_CLR_GRAPH_PACKET_CAPTURE=0" "DEBUG_HIP_FORCE_GRAPH_QUEUES=4" "GPU_MAX_HW_QUEUES=8"; do
         env $e timeout -k 10 60 python scripts/exp/graph_branches.py >> "$OUT/branches.txt" 2>&1 || return 1
       done ;;
+    xtests)
+      timeout -k 10 900 $PYT --timeout 200 -m gpu tests/test_xgmi_gpu.py tests/test_dist_gpu.py tests/test_syncbn_gpu.py \
+        tests/test_xgmi_ddp_gpu.py tests/test_convnet_fused_gpu.py -k "not 8-" > "$OUT/xtests.txt" 2>&1 ;;
     gputests)
       timeout -k 10 1100 $PYT --timeout 200 -m gpu tests > "$OUT/gputests.txt" 2>&1 ;;
     *) echo "unknown step $1"; return 2 ;;
