@@ -90,31 +90,25 @@ struct XSite {
 };
 
 // Every remote granule push of the engine (one-shot, two-shot, sites, the AMP-SGD gradient
-// exchange) goes through these: a system-scope relaxed atomic store, so a granule's
-// visibility to the peer's system-scope polls is explicit in the memory model and does not
-// rest on the peer mapping's memory type (hipDeviceMallocUncached).  8-byte granules are the
-// unit of atomicity (value and epoch tag together); the 16-byte form is two of them.
-// DPA_PUSH_PLAIN (experiment builds only) restores plain stores for the A/B.
+// exchange) goes through these.  8-byte granules are the unit of atomicity (value and epoch
+// tag together).  A single granule (sites, positioned rows, slab columns) is a system-scope
+// relaxed atomic store: its visibility to the peer's system-scope polls is explicit in the
+// memory model and costs nothing over a plain 8-B store (same instruction, sc0 sc1 bits).
+// A granule PAIR (the bandwidth paths) is one naturally aligned 16-B vector store into the
+// peer's hipDeviceMallocUncached workspace: as two 8-B system-scope atomic stores the
+// two-shot all-reduce of 8 MiB took 96 vs 62 us with 2 ranks and 1040 vs 651 us with 8
+// (profiles/r6c_push_store_ab.txt), twice the store instructions and half-width writes over
+// the links.  DPA_PUSH_ATOMIC2 (experiment builds) selects the atomic pair for the A/B.
 __device__ __forceinline__ void xgmi_put(unsigned long long* dst, unsigned long long g) {
-#ifdef DPA_PUSH_PLAIN
-  *dst = g;
-#else
   __hip_atomic_store(dst, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#endif
 }
 __device__ __forceinline__ void xgmi_put2(unsigned long long* dst, unsigned long long a, unsigned long long b) {
-#ifdef DPA_PUSH_PLAIN
-  typedef __attribute__((ext_vector_type(2))) unsigned long long v2;
-  *reinterpret_cast<v2*>(dst) = v2{a, b};
-#elif defined(DPA_PUSH_ASM)
-  // one 16-B vector store with the system-scope cache policy bits (sc0 sc1), as the 8-B
-  // system-scope atomic store is encoded; a vector store (never the scalar cache)
-  typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
-  const u32x4 v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
-  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(v) : "memory");
-#else
+#ifdef DPA_PUSH_ATOMIC2
   __hip_atomic_store(dst, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(dst + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+  typedef __attribute__((ext_vector_type(2))) unsigned long long v2;
+  *reinterpret_cast<v2*>(dst) = v2{a, b};
 #endif
 }
 

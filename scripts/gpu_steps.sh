@@ -2,9 +2,9 @@
 # usage: bash scripts/gpu_steps.sh TAG STEP [STEP ...]
 # Named GPU measurement steps (each under its own time limit, output under gpurun_out/TAG/,
 # the first failing step ends the run).  Steps:
-#   push_ab      xGMI granule pushes: 2 x 8-B system-scope atomic stores vs one 16-B sc0 sc1 store
-#                vs plain 16-B stores (scripts/exp/push_ab.py, W = 2 and 8 sharing the GPU; needs
-#                the _C_pushasm.so / _C_pushplain.so experiment builds)
+#   push_ab      xGMI granule-pair pushes: one 16-B store (kept) vs two 8-B system-scope atomic
+#                stores (scripts/exp/push_ab.py, W = 2 and 8 sharing the GPU; needs the
+#                _C_pushatomic.so experiment build: DPA_EXTRA_CFLAGS=-DDPA_PUSH_ATOMIC2)
 #   xsord_ab     forced step: exchange with epoch words advanced last / static peer unroll vs the
 #                previous exchange (_C_xsold.so)
 #   cumask       does HSA_CU_MASK / ROC_GLOBAL_CU_MASK confine a process's kernels? (GEMM rate)
@@ -12,6 +12,7 @@
 #                (needs _C_fullbar.so), 3 interleaved rounds
 #   stamps       phase stamps of the fused ConvNet kernels, plain and forced (needs _C_timing.so)
 #   steady       ConvNet steady-state kernel table (rocprofv3 kernel trace), plain and forced
+#                (STEADY_MODES="plain forced fp32" adds the fp32 step)
 #   rn_steady    ResNet-50 steady-state kernel table
 #   bench        the driver's bench command and the default 2000-step run
 #   rn_bench     ResNet-50 bench (bs 128, bf16)
@@ -29,10 +30,9 @@ step() {
   case $1 in
     push_ab)
       for W in 2 8; do
-        for v in atomic asm plain; do
-          local so=""; [ $v = asm ] && so=ddp_practice_amd/_C_pushasm.so; [ $v = plain ] && so=ddp_practice_amd/_C_pushplain.so
-          DPA_EXT_SO=$so timeout -k 10 120 python scripts/exp/push_ab.py $W $v >> "$OUT/push_ab.txt" 2>&1 || return 1
-        done
+        timeout -k 10 120 python scripts/exp/push_ab.py $W kept >> "$OUT/push_ab.txt" 2>&1 &&
+        DPA_EXT_SO=ddp_practice_amd/_C_pushatomic.so timeout -k 10 120 python scripts/exp/push_ab.py $W atomic2 \
+          >> "$OUT/push_ab.txt" 2>&1 || return 1
       done ;;
     xsord_ab)
       DPA_ALLOW_STALE_EXT=1 bash scripts/ab_bench.sh "$OUT/xsord_ab.txt" 3 "--force-collectives --steps 2000 --warmup 50 \
@@ -49,8 +49,8 @@ step() {
       DPA_EXT_SO=ddp_practice_amd/_C_timing.so timeout -k 10 120 python scripts/stamp_step.py --forced \
         > "$OUT/stamps_forced.txt" 2>&1 ;;
     steady)
-      for m in plain forced; do
-        local F=""; [ $m = forced ] && F=--force-collectives
+      for m in ${STEADY_MODES:-plain forced}; do
+        local F=""; [ $m = forced ] && F=--force-collectives; [ $m = fp32 ] && F="--amp-dtype fp32"
         timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/prof_$m" -o run -- python3 bench.py \
           --steps 640 --warmup 64 --extra-dtypes , --no-baseline --epochs 0 --no-steady $F > "$OUT/prof_$m.json" \
           2> "$OUT/prof_$m.err" || return 1
