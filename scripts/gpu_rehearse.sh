@@ -30,6 +30,6 @@ assert rec["ranks_seen"] == int(sys.argv[2]) and rec["fallback"] is None and not
 EOF
 }
 run share_w${W}_host DPA_BENCH_WATCHDOG=60 -- --steps 300 --warmup 32 --no-baseline --no-steady --comm host --no-graph && \
-run share_w$W DPA_BENCH_WATCHDOG=60 -- --steps 300 --warmup 32 --no-baseline --no-steady && \
 run share_w${W}_fused DPA_FUSED_SYNC=1 DPA_FUSED_GRAD=1 DPA_BENCH_WATCHDOG=60 -- --steps 300 --warmup 32 \
-  --batch-size 4 --no-baseline --no-steady
+  --batch-size 4 --no-baseline --no-steady && \
+run share_w$W DPA_BENCH_WATCHDOG=60 -- --steps 300 --warmup 32 --no-baseline --no-steady

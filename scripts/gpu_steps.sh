@@ -72,6 +72,11 @@ step() {
       bash scripts/gpu_rehearse.sh 8 "$TAG/rehearse8" > "$OUT/rehearse8.txt" 2>&1 ;;
     cli8)
       timeout -k 10 600 $PYT --timeout 200 tests/test_cli_gpu.py -k eight > "$OUT/cli8.txt" 2>&1 ;;
+    cli8q4)  # the same with 4 HIP hardware queues per rank (the CU masks keep ranks apart)
+      DPA_SHARED_HW_QUEUES=4 timeout -k 10 600 $PYT --timeout 200 tests/test_cli_gpu.py -k "eight and spawn" \
+        > "$OUT/cli8q4.txt" 2>&1 ;;
+    rehearse8q4)
+      DPA_SHARED_HW_QUEUES=4 bash scripts/gpu_rehearse.sh 8 "$TAG/rehearse8q4" > "$OUT/rehearse8q4.txt" 2>&1 ;;
     ddp8)
       DPA_TEST_PROGRESS=1 timeout -k 10 400 $PYT -s --timeout 170 tests/test_xgmi_ddp_gpu.py -k "8-" > "$OUT/ddp8.txt" 2>&1 ;;
     branches)
