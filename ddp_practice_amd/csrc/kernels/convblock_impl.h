@@ -615,7 +615,21 @@ struct GatherIn {
 //   WPK 2: as 0, and this launch also writes the layer-2 packs (pk).
 // bid: this workgroup's index among the launch's workgroups of this role (blockIdx.x
 // for a launch of its own; conv5x5_kernel / dgrad_wgrad_kernel below).
-template <typename T, int CIN, int COUT, int H, int W, int MODE, int PRO = 0, int EPI = 0, int WPK = 0>
+// DYN: the two big LDS tiles (image, weights) are carved from the launch's dynamic LDS
+// instead of being static arrays, so a launch hosting several roles (convnet_fused.hip
+// conv2_bwd_dyn_kernel) needs the LARGEST role's tiles, not their sum (conv5x5_dyn_bytes).
+template <typename T, int CIN, int H, int W>
+__host__ __device__ constexpr size_t conv5x5_img_bytes() {
+  return ((sizeof(T) * (size_t)(H + 4) * (W + 4) * CIN) + 15) / 16 * 16;
+}
+template <typename T, int CIN, int COUT, int H, int W>
+__host__ __device__ constexpr size_t conv5x5_dyn_bytes() {
+  return conv5x5_img_bytes<T, CIN, H, W>() + sizeof(T) * (size_t)COUT * (ceil_to(25 * CIN, 32) + 8);
+}
+extern __shared__ __attribute__((aligned(16))) unsigned char dpa_dyn_lds[];
+
+template <typename T, int CIN, int COUT, int H, int W, int MODE, int PRO = 0, int EPI = 0, int WPK = 0,
+          bool DYN = false>
 __device__ __forceinline__ void
 conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
              T* __restrict__ y, float* __restrict__ fslab, float* __restrict__ fstats,
@@ -647,7 +661,18 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
   constexpr int MT = (HW + 15) / 16;
   typedef MM<T> mm;
 
-  __shared__ __attribute__((aligned(16))) T img[HP * WPD * CIN];
+  static_assert(!DYN || !PAD8, "dynamic tiles: unpadded image rows (conv5x5_img_bytes)");
+  T* img;
+  T* wl;
+  if constexpr (DYN) {
+    img = reinterpret_cast<T*>(dpa_dyn_lds);
+    wl = reinterpret_cast<T*>(dpa_dyn_lds + conv5x5_img_bytes<T, CIN, H, W>());
+  } else {
+    __shared__ __attribute__((aligned(16))) T img_s[HP * WPD * CIN];
+    __shared__ __attribute__((aligned(16))) T wl_s[COUT * KPW];
+    img = img_s;
+    wl = wl_s;
+  }
   // img is [padded pixel][CIN] with the 8-channel (16-B) groups of each pixel
   // XOR-swizzled by the pixel index: an A-fragment read takes 16 consecutive
   // pixels x one 16-B group; with a 32/64-B pixel pitch those 16 addresses would
@@ -661,7 +686,6 @@ conv5x5_body(const T* __restrict__ x, const float* __restrict__ w, const float* 
       return px * CIN + ((((c >> 3) ^ ((px / PPB) & (NCH - 1)))) << 3) + (c & 7);
     }
   };
-  __shared__ __attribute__((aligned(16))) T wl[COUT * KPW];
   __shared__ float lstat[(NTHR / 64) * 2 * COUT];
 
   const int tid = threadIdx.x;
@@ -1309,7 +1333,25 @@ bwd_elemt_kernel(const T* __restrict__ dp, const T* __restrict__ p, const uint8_
 // (bin: backward through MaxPool -> ReLU -> BN); needs ROWS == H.
 // WT: the partial row is stored write-through (sc1) for an in-launch reduction
 // (MI355X_MICROARCH.md "Valid forms" row 1; convnet_fused.hip wgrad1_reduce_kernel).
-template <typename T, int CIN, int COUT, int H, int W, int ROWS, int PRO = 0, bool WT = false, bool CHK = false>
+// Dynamic-LDS bytes of conv5x5_wgrad_body<..., DYN = true> (its dy rows, shifted input
+// copies, padded input and staged partial row; the small arrays stay static).
+template <typename T, int CIN, int COUT, int H, int W, int ROWS>
+struct WgradLds {
+  static constexpr int WP = ceil_to(W, 8), XR = ROWS + 4, WX = WP + 4, N = CIN * 25;
+  static constexpr int DYS = ROWS * WP + 8, XCS = XR * WP + 8;
+  static constexpr bool DIRECT = ROWS == H, CIF = CIN >= 16;
+  static constexpr size_t DYL = sizeof(T) * (size_t)COUT * DYS;
+  static constexpr size_t XS = sizeof(T) * (size_t)5 * CIN * XCS;
+  static constexpr size_t XPAD = sizeof(T) * (size_t)(DIRECT ? 8 : CIN * XR * WX);
+  static constexpr size_t BASE = DYL + XS + XPAD;
+  static constexpr bool STAGE = CIF && BASE + sizeof(float) * (size_t)COUT * N <= 144 * 1024;
+  static constexpr size_t o_xs = (DYL + 15) / 16 * 16, o_xpad = (o_xs + XS + 15) / 16 * 16,
+                          o_wt = (o_xpad + XPAD + 15) / 16 * 16;
+  static constexpr size_t bytes = o_wt + sizeof(float) * (STAGE ? (size_t)COUT * N : 4);
+};
+
+template <typename T, int CIN, int COUT, int H, int W, int ROWS, int PRO = 0, bool WT = false, bool CHK = false,
+          bool DYN = false>
 __device__ __forceinline__ void
 conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __restrict__ wslab, int nsplit,
                    const BwdIn<T>& bin, const int bid) {
@@ -1338,18 +1380,33 @@ conv5x5_wgrad_body(const T* __restrict__ x, const T* __restrict__ dy, float* __r
   constexpr int DYS = ROWS * WP + 8;
   constexpr int XCS = XR * WP + 8;
   constexpr bool CIF = CIN >= 16;  // ci-fastest column order
-  __shared__ __attribute__((aligned(16))) T dyl[COUT * DYS];
   constexpr int WX = WP + 4;  // padded input row (2 halo columns each side, room for the kw shift)
-  __shared__ __attribute__((aligned(16))) T xs[5 * CIN * XCS];
   // whole image per workgroup: the 5 shifted copies are written straight from
   // registers (no padded staging image, no LDS->LDS copy pass)
   constexpr bool DIRECT = (ROWS == H);
-  __shared__ __attribute__((aligned(16))) T xpad[DIRECT ? 8 : CIN * XR * WX];
   __shared__ f32x4 kred[KSPLIT > 1 ? NW : 1][64];
   // the partial row in natural order, staged for whole-chunk stores where LDS allows
-  constexpr size_t LDS_BASE = sizeof(T) * ((size_t)COUT * DYS + 5 * CIN * XCS + (DIRECT ? 8 : CIN * XR * WX));
-  constexpr bool STAGE = CIF && LDS_BASE + sizeof(float) * COUT * N <= 144 * 1024;
-  __shared__ __attribute__((aligned(16))) float wtile[STAGE ? COUT * N : 4];
+  using WL = WgradLds<T, CIN, COUT, H, W, ROWS>;
+  constexpr bool STAGE = WL::STAGE;
+  T* dyl;
+  T* xs;
+  T* xpad;
+  float* wtile;
+  if constexpr (DYN) {
+    dyl = reinterpret_cast<T*>(dpa_dyn_lds);
+    xs = reinterpret_cast<T*>(dpa_dyn_lds + WL::o_xs);
+    xpad = reinterpret_cast<T*>(dpa_dyn_lds + WL::o_xpad);
+    wtile = reinterpret_cast<float*>(dpa_dyn_lds + WL::o_wt);
+  } else {
+    __shared__ __attribute__((aligned(16))) T dyl_s[COUT * DYS];
+    __shared__ __attribute__((aligned(16))) T xs_s[5 * CIN * XCS];
+    __shared__ __attribute__((aligned(16))) T xpad_s[DIRECT ? 8 : CIN * XR * WX];
+    __shared__ __attribute__((aligned(16))) float wtile_s[STAGE ? COUT * N : 4];
+    dyl = dyl_s;
+    xs = xs_s;
+    xpad = xpad_s;
+    wtile = wtile_s;
+  }
 
   const int tid = threadIdx.x;
   const int b = bid / nsplit, sp = bid % nsplit;

@@ -578,8 +578,49 @@ conv2_bwd_kernel(const T* __restrict__ wpk_d, T* __restrict__ dp1, BwdIn<T> bi_d
     fc_wgrad_body<T>(fw, bid - ndg - nwg);
 }
 
-// fp32: the conv2 weight-gradient role and the fc weight gradient in one launch (the
-// data-gradient role's LDS does not fit beside the weight gradient's, conv2_bwd below)
+// fp32: the same three roles in ONE launch, with the big tiles of both conv roles in
+// dynamic LDS (cb::conv5x5_body / conv5x5_wgrad_body DYN): each workgroup runs one role,
+// so the launch needs the largest role's tiles (~114 KB) instead of the 173 KB sum of
+// the static arrays, which does not fit a CU's 160 KB -- the reason fp32 ran the data
+// gradient and the weight gradient as two launches, one after the other, each on at
+// most half the CUs (profiles/r6g_cn_steady_fp32.txt: 16.7 + 15.2 us).
+template <typename T>
+__global__ void __launch_bounds__(cb::NTHR)
+conv2_bwd_dyn_kernel(const T* __restrict__ wpk_d, T* __restrict__ dp1, BwdIn<T> bi_d, BwdEpi<T> ep,
+                     const T* __restrict__ p1, float* __restrict__ wslab2, BwdIn<T> bi_w, int ndg, int nwg,
+                     FcW<T> fw) {
+  constexpr int nsw = (14 + WG2_ROWS_ - 1) / WG2_ROWS_;
+  const int bid = (int)blockIdx.x;
+  if (bid < ndg)
+    cb::conv5x5_body<T, 32, 16, 14, 14, 2, 2, 1, 1, true>(nullptr, nullptr, nullptr, dp1, nullptr, nullptr, nullptr,
+                                                          kDgradSplit, PoolIn<T>{}, bi_d, ep, wpk_d,
+                                                          cb::WPack<T>{}, bid);
+  else if (bid < ndg + nwg)
+    cb::conv5x5_wgrad_body<T, 16, 32, 14, 14, WG2_ROWS_, 2, false, false, true>(p1, nullptr, wslab2, nsw, bi_w,
+                                                                                bid - ndg);
+  else
+    fc_wgrad_body<T>(fw, bid - ndg - nwg);
+}
+
+template <typename T>
+constexpr size_t conv2_bwd_dyn_bytes() {
+  return std::max(cb::conv5x5_dyn_bytes<T, 32, 16, 14, 14>(), cb::WgradLds<T, 16, 32, 14, 14, WG2_ROWS_>::bytes);
+}
+
+// DPA_FP32_MERGED_BWD=0: the two fp32 launches below (A/B runs)
+static bool fp32_merged_bwd() {
+  static const bool on = [] {
+    const char* e = std::getenv("DPA_FP32_MERGED_BWD");
+    if (e != nullptr && std::atoi(e) == 0) return false;
+    const size_t b = conv2_bwd_dyn_bytes<float>();
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&conv2_bwd_dyn_kernel<float>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)b) == hipSuccess;
+  }();
+  return on;
+}
+
+// fp32 without the merged launch: the conv2 weight-gradient role and the fc weight gradient
+// in one launch (the data-gradient role's static LDS does not fit beside the weight gradient's)
 template <typename T>
 __global__ void __launch_bounds__(cb::NTHR)
 conv2_wgrad_fc_kernel(const T* __restrict__ p1, float* __restrict__ wslab2, BwdIn<T> bi_w, int nwg, FcW<T> fw) {
@@ -679,7 +720,13 @@ void conv2_bwd(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx2,
       bd.chk_coef = 1;
     }
     if constexpr (std::is_same<T, float>::value) {
-      // fp32 tiles: the two roles' LDS (173 KB) exceed one CU's 160 KB -> separate launches
+      if (fp32_merged_bwd()) {  // one launch, the conv tiles in dynamic LDS (conv2_bwd_dyn_kernel)
+        hipLaunchKernelGGL(conv2_bwd_dyn_kernel<T>, dim3(ndg + nwg + nfc), dim3(cb::NTHR), conv2_bwd_dyn_bytes<T>(),
+                           cur_stream(), dptr<T>(wpk_d), dptr<T>(dp1), bd, ep, dptr<T>(p1), wslab2.data_ptr<float>(),
+                           bw, ndg, nwg, fw);
+        return;
+      }
+      // fp32 static tiles: the two roles' LDS (173 KB) exceed one CU's 160 KB -> separate launches
       // (the fc weight gradient: extra workgroups of the weight-gradient launch; its site's
       // tickets are the nwg conv workgroups', set above)
       bd.xs.nblk = 0;  // the data-gradient launch is its site's whole grid (ndg: checked above)
@@ -1089,6 +1136,10 @@ bool sites_resident(int64_t B, at::ScalarType st) {
     chk(reinterpret_cast<const void*>(&cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1, 1>), B * kDgradSplit);
     if constexpr (!std::is_same<T, float>::value)
       chk(reinterpret_cast<const void*>(&conv2_bwd_kernel<T>), B * kDgradSplit + wgrad_bn_rows(2, B) + FC_BLOCKS);
+    else if (fp32_merged_bwd())
+      ok = ok && co_resident(reinterpret_cast<const void*>(&conv2_bwd_dyn_kernel<T>),
+                             (int)(B * kDgradSplit + wgrad_bn_rows(2, B) + FC_BLOCKS), cb::NTHR,
+                             conv2_bwd_dyn_bytes<T>());
     chk(reinterpret_cast<const void*>(&cb::conv5x5_wgrad_kernel<T, 16, 32, 14, 14, WG2_ROWS, 2>),
         wgrad_bn_rows(2, B));
     chk(reinterpret_cast<const void*>(&cb::conv5x5_wgrad_kernel<T, 1, 16, 28, 28, WG1_ROWS, 2>),

@@ -7,6 +7,7 @@
 #                _C_pushatomic.so experiment build: DPA_EXTRA_CFLAGS=-DDPA_PUSH_ATOMIC2)
 #   xsord_ab     forced step: exchange with epoch words advanced last / static peer unroll vs the
 #                previous exchange (_C_xsold.so)
+#   fp32_ab      fp32 step: merged conv2 backward launch (dynamic LDS) vs the two launches
 #   cumask       does HSA_CU_MASK / ROC_GLOBAL_CU_MASK confine a process's kernels? (GEMM rate)
 #   xsbar_ab     forced (W>1-shaped) ConvNet step: LDS-only exchange barriers vs __syncthreads
 #                (needs _C_fullbar.so), 3 interleaved rounds
@@ -37,6 +38,9 @@ step() {
     xsord_ab)
       DPA_ALLOW_STALE_EXT=1 bash scripts/ab_bench.sh "$OUT/xsord_ab.txt" 3 "--force-collectives --steps 2000 --warmup 50 \
 --no-baseline --epochs 0 --no-steady --extra-dtypes ," new=default old=ddp_practice_amd/_C_xsold.so ;;
+    fp32_ab)
+      bash scripts/ab_bench.sh "$OUT/fp32_ab.txt" 3 "--amp-dtype fp32 --steps 2000 --warmup 50 --no-baseline --epochs 0 \
+--no-steady --extra-dtypes ," merged=default split=env:DPA_FP32_MERGED_BWD=0 ;;
     cumask)
       for e in "X=0" "HSA_CU_MASK=0:0-31" "ROC_GLOBAL_CU_MASK=0xffffffff"; do
         env $e timeout -k 10 60 python scripts/exp/cu_mask_probe.py >> "$OUT/cumask.txt" 2>&1 || return 1
