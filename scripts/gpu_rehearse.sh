@@ -29,7 +29,10 @@ print(sys.argv[1].rsplit("/", 1)[-1], {k: rec.get(k) for k in keys})
 assert rec["ranks_seen"] == int(sys.argv[2]) and rec["fallback"] is None and not rec["comm_error"], rec
 EOF
 }
+# the fused and default runs on a short synthetic set (64 / 16 steps per rank per epoch at batch 4 / 8):
+# full 60k epochs of 8 ranks on one card stalled near their end (profiles/r6i_w8_fused_long_stall.txt)
+SHORT="--train-samples $((W * 256)) --test-samples $((W * 64))"
 run share_w${W}_host DPA_BENCH_WATCHDOG=60 -- --steps 300 --warmup 32 --no-baseline --no-steady --comm host --no-graph && \
 run share_w${W}_fused DPA_FUSED_SYNC=1 DPA_FUSED_GRAD=1 DPA_BENCH_WATCHDOG=60 -- --steps 300 --warmup 32 \
-  --batch-size 4 --no-baseline --no-steady && \
-run share_w$W DPA_BENCH_WATCHDOG=60 -- --steps 300 --warmup 32 --no-baseline --no-steady
+  --batch-size 4 --no-baseline --no-steady $SHORT && \
+run share_w$W DPA_BENCH_WATCHDOG=60 -- --steps 300 --warmup 32 --no-baseline --no-steady $SHORT

@@ -162,9 +162,10 @@ def test_ddp_cli_eight_ranks_sharing_gpu(C, tmp_path, launcher, fused):
     DDP + SyncBN over the xGMI engine with the step shape of a one-rank-per-GPU run:
     DPA_FUSED_SYNC=1 DPA_FUSED_GRAD=1 force the in-kernel SyncBN sites and the AMP-SGD
     gradient exchange (8 rows, 7 peers each), batch 4 so every exchanging grid fits a
-    rank's CUs (1875 steps per rank).  (The one-launch-per-collective path that 3+ shared
-    ranks take by default stalled near the end of this epoch, at the same point with 1 and
-    4 HW queues per rank: profiles/r6h_w8_percollective_stall.txt.)  The stdout contract,
+    rank's CUs, a short epoch with graph replays, one-step graphs and a tail batch.  (Full
+    60k-sample epochs of this 8-ranks-on-one-card rehearsal stalled near their end, fused and
+    one-launch-per-collective alike: profiles/r6h_w8_percollective_stall.txt,
+    profiles/r6i_w8_fused_long_stall.txt.)  The stdout contract,
     a weights_only checkpoint with module. keys, and eight bitwise-equal rank checkpoints."""
     gpus = ",".join(str(i) for i in range(8))
     if launcher == "spawn":
@@ -176,14 +177,17 @@ def test_ddp_cli_eight_ranks_sharing_gpu(C, tmp_path, launcher, fused):
     extra = {"DPA_FUSED_SYNC": "1", "DPA_FUSED_GRAD": "1"} if fused else {}
     extra["DPA_WATCHDOG_TIMEOUT"] = "60"  # a stall ends the run (exit 124, site dump) inside the budget
     b = 4 if fused else 8  # fused: every exchanging grid co-resident on the rank's 32 CUs
-    out = _run(args + ["-e", "1", "-b", str(b), "--synthetic", "--amp-dtype", "bf16", "--seed", "0"], tmp_path,
+    # 8 x 162 train samples: 41 steps per rank (2 sixteen-step graphs, 8 one-step graphs and a
+    # tail of 2 samples); 8 x 34 test samples (a tail of 2)
+    out = _run(args + ["-e", "1", "-b", str(b), "--synthetic", "--amp-dtype", "bf16", "--seed", "0",
+                       "--train-samples", str(8 * 162), "--test-samples", str(8 * 34)], tmp_path,
                _shared_env(extra), timeout=160)
     _check_stdout(out, 1)
     assert out.count("begin testing") == 1  # rank 0 only
     ck = torch.load(tmp_path / "ddp_checkpoint.pt", weights_only=True)
     assert list(ck["model"]) == ["module." + k for k in REF_KEYS]
     m = _load_into_torch(ck["model"])
-    assert int(m.layer1[1].num_batches_tracked) == -(-7500 // b)  # ceil(ceil(60000 / 8) / b) steps per rank
+    assert int(m.layer1[1].num_batches_tracked) == -(-162 // b)  # ceil(162 / b) steps per rank
     _check_ranks_equal(tmp_path, 8)
 
 
