@@ -79,6 +79,12 @@ step() {
     cli8q4)  # the same with 4 HIP hardware queues per rank (the CU masks keep ranks apart)
       DPA_SHARED_HW_QUEUES=4 timeout -k 10 600 $PYT --timeout 200 tests/test_cli_gpu.py -k "eight and spawn" \
         > "$OUT/cli8q4.txt" 2>&1 ;;
+    cli8ab)  # the short 8-rank CLI test with the previous exchange build, then the current one
+      DPA_EXT_SO=$PWD/ddp_practice_amd/_C_xsold.so DPA_ALLOW_STALE_EXT=1 timeout -k 10 300 $PYT --timeout 200 \
+        tests/test_cli_gpu.py -k "eight and spawn" > "$OUT/cli8_xsold.txt" 2>&1
+      echo "xsold rc=$?" >> "$OUT/cli8ab.txt"
+      timeout -k 10 300 $PYT --timeout 200 tests/test_cli_gpu.py -k "eight and spawn" > "$OUT/cli8_new.txt" 2>&1
+      echo "new rc=$?" >> "$OUT/cli8ab.txt" ;;
     rehearse8q4)
       DPA_SHARED_HW_QUEUES=4 bash scripts/gpu_rehearse.sh 8 "$TAG/rehearse8q4" > "$OUT/rehearse8q4.txt" 2>&1 ;;
     ddp8)
