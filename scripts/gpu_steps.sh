@@ -18,7 +18,8 @@
 #   bench        the driver's bench command and the default 2000-step run
 #   rn_bench     ResNet-50 bench (bs 128, bf16)
 #   rehearse8    bench.py with 8 ranks sharing the GPU under torchrun (scripts/gpu_rehearse.sh)
-#   cli8         the 8-rank shared-GPU CLI tests (tests/test_cli_gpu.py -k eight)
+#   cli8         the 8-rank shared-GPU CLI tests (tests/test_cli_gpu.py -k eight; DPA_GPU_W8=1)
+#   w8tests      the world-8 xGMI engine tests (DPA_GPU_W8=1)
 #   ddp8         the 8-rank DDP + SyncBN xGMI tests, streaming the workers' stall reports
 #   branches     do captured hipGraph fork/join branches overlap? (scripts/exp/graph_branches.py)
 #   xtests       the xGMI / distributed / SyncBN / fused-ConvNet GPU tests (world-8 DDP excluded)
@@ -75,20 +76,23 @@ step() {
     rehearse8)
       bash scripts/gpu_rehearse.sh 8 "$TAG/rehearse8" > "$OUT/rehearse8.txt" 2>&1 ;;
     cli8)
-      timeout -k 10 600 $PYT --timeout 200 tests/test_cli_gpu.py -k eight > "$OUT/cli8.txt" 2>&1 ;;
+      DPA_GPU_W8=1 timeout -k 10 600 $PYT --timeout 200 tests/test_cli_gpu.py -k eight > "$OUT/cli8.txt" 2>&1 ;;
+    w8tests)  # the world-8 xGMI engine tests (opt-in: DPA_GPU_W8=1)
+      DPA_GPU_W8=1 timeout -k 10 900 $PYT --timeout 330 tests/test_xgmi_gpu.py -k "8" > "$OUT/w8tests.txt" 2>&1 ;;
     cli8q4)  # the same with 4 HIP hardware queues per rank (the CU masks keep ranks apart)
-      DPA_SHARED_HW_QUEUES=4 timeout -k 10 600 $PYT --timeout 200 tests/test_cli_gpu.py -k "eight and spawn" \
+      DPA_GPU_W8=1 DPA_SHARED_HW_QUEUES=4 timeout -k 10 600 $PYT --timeout 200 tests/test_cli_gpu.py -k "eight and spawn" \
         > "$OUT/cli8q4.txt" 2>&1 ;;
     cli8ab)  # the short 8-rank CLI test with the previous exchange build, then the current one
-      DPA_EXT_SO=$PWD/ddp_practice_amd/_C_xsold.so DPA_ALLOW_STALE_EXT=1 timeout -k 10 300 $PYT --timeout 200 \
+      DPA_GPU_W8=1 DPA_EXT_SO=$PWD/ddp_practice_amd/_C_xsold.so DPA_ALLOW_STALE_EXT=1 timeout -k 10 300 $PYT --timeout 200 \
         tests/test_cli_gpu.py -k "eight and spawn" > "$OUT/cli8_xsold.txt" 2>&1
       echo "xsold rc=$?" >> "$OUT/cli8ab.txt"
-      timeout -k 10 300 $PYT --timeout 200 tests/test_cli_gpu.py -k "eight and spawn" > "$OUT/cli8_new.txt" 2>&1
+      DPA_GPU_W8=1 timeout -k 10 300 $PYT --timeout 200 tests/test_cli_gpu.py -k "eight and spawn" > "$OUT/cli8_new.txt" 2>&1
       echo "new rc=$?" >> "$OUT/cli8ab.txt" ;;
     rehearse8q4)
       DPA_SHARED_HW_QUEUES=4 bash scripts/gpu_rehearse.sh 8 "$TAG/rehearse8q4" > "$OUT/rehearse8q4.txt" 2>&1 ;;
     ddp8)
-      DPA_TEST_PROGRESS=1 timeout -k 10 400 $PYT -s --timeout 170 tests/test_xgmi_ddp_gpu.py -k "8-" > "$OUT/ddp8.txt" 2>&1 ;;
+      DPA_GPU_W8=1 DPA_TEST_PROGRESS=1 timeout -k 10 400 $PYT -s --timeout 170 tests/test_xgmi_ddp_gpu.py -k "8-" \
+        > "$OUT/ddp8.txt" 2>&1 ;;
     branches)
       for e in "X=0" "DEBUG_CLR_GRAPH_PACKET_CAPTURE=0" "DEBUG_HIP_FORCE_GRAPH_QUEUES=4" "GPU_MAX_HW_QUEUES=8"; do
         env $e timeout -k 10 60 python scripts/exp/graph_branches.py >> "$OUT/branches.txt" 2>&1 || return 1

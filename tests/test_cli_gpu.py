@@ -17,6 +17,7 @@ import pytest
 import torch
 
 from ._dist import free_port
+from .conftest import W8
 from .test_cli_cpu import REF_KEYS, _check_stdout
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -155,6 +156,7 @@ def test_ddp_cli_two_ranks_sharing_gpu(C, tmp_path, launcher):
     _check_ranks_equal(tmp_path, 2)
 
 
+@W8
 @pytest.mark.parametrize("launcher,fused", [("spawn", True), ("torchrun", True)])
 def test_ddp_cli_eight_ranks_sharing_gpu(C, tmp_path, launcher, fused):
     """W = 8, the driver's node size, on one GPU: eight ranks of the reference's programs

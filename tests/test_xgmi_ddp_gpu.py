@@ -4,12 +4,14 @@ training on the global batch, and every rank must end bit-identical."""
 import pytest
 
 from ._dist import launch
+from .conftest import W8
 
 pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("world,amp,graph", [(2, False, False), (2, False, True), (2, True, True),
-                                             (8, False, False), (8, True, True)])
+                                             pytest.param(8, False, False, marks=W8),
+                                             pytest.param(8, True, True, marks=W8)])
 def test_ddp_syncbn_xgmi_processes(C, world, amp, graph):
     """World 8 (the driver's node size; per rank 4 images, one HW queue and 32 CUs):
     8-row SyncBN sites, 7-peer gradient pushes in the AMP-SGD launch and a partial last

@@ -6,6 +6,7 @@ two-shot shards of 1/8) runs here before it runs on eight GPUs."""
 import pytest
 
 from ._dist import launch
+from .conftest import W8
 
 pytestmark = pytest.mark.gpu
 
@@ -17,7 +18,7 @@ def _run(world, mode, timeout=None):
     return launch(worker, world, (mode,), timeout)
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("world", [2, 4, pytest.param(8, marks=W8)])
 def test_xgmi_allreduce_multiprocess(C, world):
     outs = _run(world, "full")
     for k, v in outs[0].items():
@@ -29,7 +30,7 @@ def test_xgmi_wait_is_bounded(C):
     _run(2, "timeout")
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("world", [2, 3, pytest.param(8, marks=W8)])
 def test_xsite_exchange_multiprocess(C, world):
     """The in-kernel SyncBN exchange (csrc/comm/xsite.h) every fused consumer runs."""
     outs = _run(world, "site")
@@ -38,7 +39,7 @@ def test_xsite_exchange_multiprocess(C, world):
             assert v == outs[r][k], f"rank {r} differs from rank 0 on {k}"
 
 
-@pytest.mark.parametrize("world", [1, 2, 4, 8])
+@pytest.mark.parametrize("world", [1, 2, 4, pytest.param(8, marks=W8)])
 def test_wide_site_exchange_multiprocess(C, world):
     """The positioned exchange of the ResNet statistics finishers (SyncBN rows up to
     2*2048+1 floats over several finisher workgroups, csrc/comm/xsite.h kSiteWide)."""
@@ -55,7 +56,7 @@ def test_in_kernel_exchange_wait_is_bounded(C, mode):
     _run(2, mode)
 
 
-@pytest.mark.parametrize("world", [2, 3, 4, 8])
+@pytest.mark.parametrize("world", [2, 3, 4, pytest.param(8, marks=W8)])
 def test_xgmi_twoshot_multiprocess(C, world):
     """Two-shot (reduce-scatter + all-gather) engine for large messages: 1-32 MiB,
     ragged sizes, every dtype/op, interleaved sizes, graph replay; bit-identical ranks."""
