@@ -23,7 +23,8 @@
 #   ddp8         the 8-rank DDP + SyncBN xGMI tests, streaming the workers' stall reports
 #   branches     do captured hipGraph fork/join branches overlap? (scripts/exp/graph_branches.py)
 #   xtests       the xGMI / distributed / SyncBN / fused-ConvNet GPU tests (world-8 DDP excluded)
-#   gputests     the whole GPU test tier
+#   smoke        __graft_entry__.smoke()
+#   gputests     the whole GPU test tier (as the driver runs it: world-8 rehearsals opt-in)
 set -o pipefail
 TAG=$1; shift
 cd "$(dirname "$0")/.." && export TMPDIR=/tmp && OUT=$PWD/gpurun_out/$TAG && mkdir -p "$OUT"
@@ -100,6 +101,8 @@ step() {
     xtests)
       timeout -k 10 900 $PYT --timeout 200 -m gpu tests/test_xgmi_gpu.py tests/test_dist_gpu.py tests/test_syncbn_gpu.py \
         tests/test_xgmi_ddp_gpu.py tests/test_convnet_fused_gpu.py -k "not 8-" > "$OUT/xtests.txt" 2>&1 ;;
+    smoke)
+      timeout -k 10 200 python __graft_entry__.py > "$OUT/smoke.txt" 2>&1 ;;
     gputests)
       timeout -k 10 1100 $PYT --timeout 200 -m gpu tests > "$OUT/gputests.txt" 2>&1 ;;
     *) echo "unknown step $1"; return 2 ;;
