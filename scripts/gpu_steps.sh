@@ -43,6 +43,11 @@ step() {
     fp32_ab)
       bash scripts/ab_bench.sh "$OUT/fp32_ab.txt" 3 "--amp-dtype fp32 --steps 2000 --warmup 50 --no-baseline --epochs 0 \
 --no-steady --extra-dtypes ," merged=default split=env:DPA_FP32_MERGED_BWD=0 ;;
+    split_ab)  # workgroups per image of the conv2 forward / data gradient (experiment builds)
+      for dt in fp32 bf16; do
+        bash scripts/ab_bench.sh "$OUT/split_ab_$dt.txt" 3 "--amp-dtype $dt --steps 2000 --warmup 50 --no-baseline \
+--epochs 0 --no-steady --extra-dtypes ," base=default fwd4=ddp_practice_amd/_C_fwd4.so dg4=ddp_practice_amd/_C_dg4.so || return 1
+      done ;;
     cumask)
       for e in "X=0" "HSA_CU_MASK=0:0-31" "ROC_GLOBAL_CU_MASK=0xffffffff"; do
         env $e timeout -k 10 60 python scripts/exp/cu_mask_probe.py >> "$OUT/cumask.txt" 2>&1 || return 1
