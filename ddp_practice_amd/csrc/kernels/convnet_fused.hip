@@ -256,6 +256,15 @@ static BwdIn<T> bwd_in(at::Tensor dp, at::Tensor idx, at::Tensor y, at::Tensor f
 typedef std::shared_ptr<xgmi::XgmiComm> XcPtr;
 static xgmi::XSite site_of(const XcPtr& xc, int s) { return xc ? xc->site(s) : xgmi::XSite{}; }
 
+// Workgroups per image of the conv2 forward.  bf16 / fp16: cb::SH<1>::SPLIT (2); fp32, whose
+// 16x16x4 MFMA chain per output tile is 4x as long, runs 4 shorter workgroups per image: fp32
+// step 0.0640 -> 0.0617 ms, while bf16 at 4 is 0.6 us slower (profiles/r6m_split_ab.txt).
+// The consumers take the slab's row count from its size (nrows).
+#ifndef DPA_FWD2_SPLIT_F32
+#define DPA_FWD2_SPLIT_F32 4
+#endif
+int64_t fwd2_split(bool fp32) { return fp32 ? DPA_FWD2_SPLIT_F32 : cb::SH<1>::SPLIT; }
+
 // [BN1 -> ReLU -> pool1] -> conv2 (+ BN2 partial sums when training).
 void conv2_fwd(at::Tensor y1, c10::optional<at::Tensor> fslab1, at::Tensor fstats1, at::Tensor g1, at::Tensor b1,
                at::Tensor rm1, at::Tensor rv1, at::Tensor nbt1, double momentum, double eps, bool train, at::Tensor w2,
@@ -272,7 +281,7 @@ void conv2_fwd(at::Tensor y1, c10::optional<at::Tensor> fslab1, at::Tensor fstat
   if (p1_out.has_value())
     TORCH_CHECK(p1_out->numel() == (int64_t)B * 16 * 196 && idx1_out->numel() == p1_out->numel() &&
                 xh1_out->numel() == p1_out->numel());
-  constexpr int ns = cb::SH<1>::SPLIT;  // workgroups per image
+  const int ns = fwd2_split(y1.scalar_type() == at::kFloat);  // workgroups per image
   if (train) TORCH_CHECK(fslab2.has_value() && fslab2->numel() == (int64_t)B * ns * cb::fslab_row(32));
   if (B == 0) return;
   BNParams bp = bn_params(fslab1, fstats1, g1, b1, rm1, rv1, nbt1, momentum, eps, train, 16);
@@ -1126,11 +1135,12 @@ bool sites_resident(int64_t B, at::ScalarType st) {
   // every site launch must also fit its site's epoch words (comm/xgmi.h set_site_grid):
   // the conv1 weight gradient's 7 B workgroups pass kEpochWords at B >= 74
   bool ok = xgmi::site_grid_fits(wgrad_bn_rows(1, B)) && xgmi::site_grid_fits(wgrad_bn_rows(2, B)) &&
-            xgmi::site_grid_fits(B * kDgradSplit) && xgmi::site_grid_fits(cb::SH<1>::SPLIT * B);
+            xgmi::site_grid_fits(B * kDgradSplit) && xgmi::site_grid_fits(fwd2_split(st == at::kFloat) * B);
   auto chk = [&](const void* k, int64_t grid) { ok = ok && co_resident(k, (int)grid, cb::NTHR, 0); };
   with_t(dt_of(at::empty({0}, at::TensorOptions().dtype(st))), [&](auto tag) {
     typedef decltype(tag) T;
-    chk(reinterpret_cast<const void*>(&cb::conv5x5_kernel<T, 16, 32, 14, 14, 0, 1, 0, 1>), B * cb::SH<1>::SPLIT);
+    chk(reinterpret_cast<const void*>(&cb::conv5x5_kernel<T, 16, 32, 14, 14, 0, 1, 0, 1>),
+        B * fwd2_split(std::is_same<T, float>::value));
     ok = ok && co_resident(reinterpret_cast<const void*>(&head_fwd_kernel<T, 32, 14, 14, 16>), (int)B, HF, 0) &&
          co_resident(reinterpret_cast<const void*>(&head_fwd_kernel<T, 32, 14, 14, 64>), (int)B, HF, 0);
     chk(reinterpret_cast<const void*>(&cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1, 1>), B * kDgradSplit);
@@ -1184,6 +1194,7 @@ void register_convnet_fused(pybind11::module& m) {
   s.def("conv_wgrad_bn", &cnf::conv_wgrad_bn);
   s.def("wgrad_bn_rows", &cnf::wgrad_bn_rows);
   s.def("sites_resident", &cnf::sites_resident);
+  s.def("fwd2_split", &cnf::fwd2_split, py::arg("fp32"));
   s.def("wgrad1_reduce", &cnf::wgrad1_reduce);
   s.def("conv1_wgrad_slab2", &cnf::conv1_wgrad_slab2);
   s.def("convnet_amp_step", &cnf::convnet_amp_step);

@@ -168,7 +168,9 @@ class ConvNetFn(torch.autograd.Function):
         fstats2 = torch.empty(cb.stats_len(32), dtype=torch.float32, device=dev)
         if training:
             fslab1 = torch.empty(cb.fwd_rows(1, 16, 28, 28, B) * cb.fslab_row(16), dtype=torch.float32, device=dev)
-            fslab2 = torch.empty(cb.fwd_rows(16, 32, 14, 14, B) * cb.fslab_row(32), dtype=torch.float32, device=dev)
+            # conv2's workgroups per image depend on the dtype (convnet_fused.hip fwd2_split)
+            fslab2 = torch.empty(B * cn.fwd2_split(cdtype == torch.float32) * cb.fslab_row(32), dtype=torch.float32,
+                                 device=dev)
             # pooled maps, argmax|relu index and xhat at the argmax of both blocks (for the backward)
             p1 = torch.empty((B, 16, 14, 14), dtype=cdtype, device=dev)
             idx1 = torch.empty((B, 16, 14, 14), dtype=torch.uint8, device=dev)
