@@ -301,6 +301,34 @@ template <typename T> inline T* dptr(const at::Tensor& t) {
 
 constexpr int ceil_to(int x, int m) { return (x + m - 1) / m * m; }
 
+// torch.optim.SGD's update with ATen's foreach rounding, spelled out: d = g + wd*p (one fma),
+// buf = buf*momentum (rounded) + (1-dampening)*d (one fma), d = d + momentum*buf (nesterov,
+// one fma), p = p - lr*d (one fma).  Every SGD kernel of the package (optim.hip,
+// amp_step.h) goes through it, so the fused, multi-tensor and slab-column updates round alike
+// and train bit-identically (left to -ffp-contract, the same source line was contracted
+// differently in different kernels, and the 1-ulp differences grew over a few steps).
+__device__ __forceinline__ float sgd_rule(float p, float g, float& buf, bool first, float lr, float momentum,
+                                          float dampening, float wd, int nesterov, int maximize) {
+  float d = maximize ? -g : g;
+  if (wd != 0.f) d = __builtin_fmaf(wd, p, d);
+  if (momentum != 0.f) {
+    const float mb = momentum * buf;  // its own rounding (ATen: a separate _foreach_mul_)
+    buf = first ? d : __builtin_fmaf(1.f - dampening, d, mb);
+    d = nesterov ? __builtin_fmaf(momentum, buf, d) : buf;
+  }
+  return __builtin_fmaf(-lr, d, p);
+}
+// four lanes of a granule: p, buf updated in place
+__device__ __forceinline__ void sgd_rule4(f32x4& p, f32x4 g, f32x4& buf, bool first, float lr, float momentum,
+                                          float dampening, float wd, int nesterov, int maximize) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float b = buf[j];
+    p[j] = sgd_rule(p[j], g[j], b, first, lr, momentum, dampening, wd, nesterov, maximize);
+    buf[j] = b;
+  }
+}
+
 // Can every workgroup of a `grid` x `threads` launch of `kernel` (dynamic LDS
 // `lds`) be resident on the current device at once?  Launches whose
 // workgroups wait on each other (grid barriers, in-kernel exchanges polled by

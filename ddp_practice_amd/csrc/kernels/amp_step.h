@@ -457,29 +457,19 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
     const f32x4 g = gv[k] * inv;
     if (amp || XG) store4(sp1[t] + o, rem, g);  // plain step: the gradient is unchanged
     if (any_bad) continue;
-    f32x4 d = maximize ? -g : g;
-    if (wd != 0.f) d += wd * pv[k];
-    if (momentum != 0.f) {
-      const bool first = (L.first_bits >> t) & 1ull;
-      const f32x4 bb = first ? d : momentum * bv[k] + (1.f - dampening) * d;
-      store4(sp2[t] + o, rem, bb);
-      d = nesterov ? d + momentum * bb : bb;
-    }
-    store4(sp0[t] + o, rem, pv[k] - lr * d);
+    f32x4 pn = pv[k], bb = bv[k];
+    sgd_rule4(pn, g, bb, (L.first_bits >> t) & 1ull, lr, momentum, dampening, wd, nesterov, maximize);
+    if (momentum != 0.f) store4(sp2[t] + o, rem, bb);
+    store4(sp0[t] + o, rem, pn);
   }
   if (st_t >= 0) {  // a slab column: the same update, one element
     const float g = st_sum * inv;
     sp1[st_t][st_e] = g;
     if (!any_bad) {
-      float d = maximize ? -g : g;
-      if (wd != 0.f) d += wd * st_p;
-      if (momentum != 0.f) {
-        const bool first = (L.first_bits >> st_t) & 1ull;
-        const float bb = first ? d : momentum * st_b + (1.f - dampening) * d;
-        sp2[st_t][st_e] = bb;
-        d = nesterov ? d + momentum * bb : bb;
-      }
-      sp0[st_t][st_e] = st_p - lr * d;
+      float bb = st_b;
+      sp0[st_t][st_e] = sgd_rule(st_p, g, bb, (L.first_bits >> st_t) & 1ull, lr, momentum, dampening, wd, nesterov,
+                                 maximize);
+      if (momentum != 0.f) sp2[st_t][st_e] = bb;
     }
   }
   DPA_STAMP(13);

@@ -46,11 +46,25 @@ constexpr int U = 4;         // rows in flight per lane
 constexpr int UF = 8;        // rows in flight per lane, forward statistics (one input)
 constexpr int MAXTICKETS = 2048;
 
+// Streaming (non-temporal) 16-B activation loads / stores in load_vec / store_vec (A/B builds:
+// -DDPA_BN_NT_LOAD=0 / -DDPA_BN_NT_STORE=1).  Loads: ResNet-50 step 14.13 -> 13.93 ms; stores:
+// no change (profiles/r6o_bn_nt_ab.txt).
+#ifndef DPA_BN_NT_LOAD
+#define DPA_BN_NT_LOAD 1
+#endif
+#ifndef DPA_BN_NT_STORE
+#define DPA_BN_NT_STORE 0
+#endif
+
 template <typename T> struct V16 { static constexpr int N = 16 / sizeof(T); };
 
 template <typename T>
 __device__ __forceinline__ void load_vec(const T* p, float* f) {
+#if DPA_BN_NT_LOAD
+  const f32x4 raw = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+#else
   const f32x4 raw = *reinterpret_cast<const f32x4*>(p);
+#endif
   const T* e = reinterpret_cast<const T*>(&raw);
 #pragma unroll
   for (int j = 0; j < V16<T>::N; ++j) f[j] = Cvt<T>::to_f(e[j]);
@@ -61,7 +75,11 @@ __device__ __forceinline__ void store_vec(T* p, const float* f) {
   T* e = reinterpret_cast<T*>(&raw);
 #pragma unroll
   for (int j = 0; j < V16<T>::N; ++j) e[j] = Cvt<T>::from_f(f[j]);
+#if DPA_BN_NT_STORE
+  __builtin_nontemporal_store(raw, reinterpret_cast<f32x4*>(p));
+#else
   *reinterpret_cast<f32x4*>(p) = raw;
+#endif
 }
 
 // VEC consecutive floats (VEC % 4 == 0, 16-B aligned) as 16-B loads

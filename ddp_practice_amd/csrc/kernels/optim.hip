@@ -83,15 +83,9 @@ sgd_kernel(MTList L, float lr, float momentum, float dampening, float wd, int ne
     for (int k = 0; k < CHUNK / NTHR; ++k) {
       const int64_t i = base + k * NTHR + threadIdx.x;
       if (i >= end) continue;
-      float d = gv[k] * gs;
-      if (maximize) d = -d;
-      if (wd != 0.f) d += wd * pv[k];
-      if (momentum != 0.f) {
-        const float b = first ? d : momentum * bv0[k] + (1.f - dampening) * d;
-        buf[i] = b;
-        d = nesterov ? d + momentum * b : b;
-      }
-      p[i] = pv[k] - lr * d;
+      float b = bv0[k];
+      p[i] = sgd_rule(pv[k], gv[k] * gs, b, first, lr, momentum, dampening, wd, nesterov, maximize);
+      if (momentum != 0.f) buf[i] = b;
     }
   }
 }
@@ -304,14 +298,10 @@ amp_sgd_large_kernel(const int64_t* __restrict__ table, float* __restrict__ scal
         const f32x4 g = gv[u] * inv;
         store4(sp1[tu] + o, rem, g);
         if (any_bad) continue;
-        f32x4 d = maximize ? -g : g;
-        if (wd != 0.f) d += wd * pv[u];
-        if (momentum != 0.f) {
-          const f32x4 bb = sfirst[tu] ? d : momentum * bv[u] + (1.f - dampening) * d;
-          store4(sp2[tu] + o, rem, bb);
-          d = nesterov ? d + momentum * bb : bb;
-        }
-        store4(sp0[tu] + o, rem, pv[u] - lr * d);
+        f32x4 pn = pv[u], bb = bv[u];
+        sgd_rule4(pn, g, bb, sfirst[tu], lr, momentum, dampening, wd, nesterov, maximize);
+        if (momentum != 0.f) store4(sp2[tu] + o, rem, bb);
+        store4(sp0[tu] + o, rem, pn);
       }
     }
   }

@@ -23,6 +23,8 @@
 #   ddp8         the 8-rank DDP + SyncBN xGMI tests, streaming the workers' stall reports
 #   branches     do captured hipGraph fork/join branches overlap? (scripts/exp/graph_branches.py)
 #   xtests       the xGMI / distributed / SyncBN / fused-ConvNet GPU tests (world-8 DDP excluded)
+#   fp32det      fp32 slab-sink / bitwise-determinism tests, default and fp32 split-2 builds
+#   bn_nt_ab     ResNet-50 A/B of non-temporal BN stores / loads
 #   smoke        __graft_entry__.smoke()
 #   gputests     the whole GPU test tier (as the driver runs it: world-8 rehearsals opt-in)
 set -o pipefail
@@ -48,6 +50,27 @@ step() {
         bash scripts/ab_bench.sh "$OUT/split_ab_$dt.txt" 3 "--amp-dtype $dt --steps 2000 --warmup 50 --no-baseline \
 --epochs 0 --no-steady --extra-dtypes ," base=default fwd4=ddp_practice_amd/_C_fwd4.so dg4=ddp_practice_amd/_C_dg4.so || return 1
       done ;;
+    fp32det)  # fp32 slab-sink step + bitwise determinism, current build then the fp32 split-2 build
+      local K="fp32_plain_fused or bitwise_deterministic" rc
+      timeout -k 10 300 $PYT --timeout 120 -p no:cacheprovider tests/test_convnet_fused_gpu.py -k "$K" \
+        > "$OUT/fp32det_default.txt" 2>&1; rc=$?; echo "default rc=$rc" >> "$OUT/fp32det.txt"
+      [ $rc -le 1 ] || return 1  # 0 pass, 1 test failure; anything else (timeout, abort): stop
+      DPA_EXT_SO=$PWD/ddp_practice_amd/_C_sp2.so timeout -k 10 300 $PYT --timeout 120 -p no:cacheprovider \
+        tests/test_convnet_fused_gpu.py -k "$K" > "$OUT/fp32det_sp2.txt" 2>&1; rc=$?
+      echo "sp2 rc=$rc" >> "$OUT/fp32det.txt"; [ $rc -le 1 ] ;;
+    fp32diag)  # localise the fp32 split-4 slab-sink mismatch (scripts/exp/fp32_sink_diff.py)
+      timeout -k 10 200 $PYT --timeout 120 -p no:cacheprovider tests/test_convnet_fused_gpu.py -k bitwise \
+        > "$OUT/fp32diag_bitwise.txt" 2>&1; local rc=$?; echo "bitwise rc=$rc" >> "$OUT/fp32diag.txt"
+      [ $rc -le 1 ] || return 1
+      local IFS=,; local runs=(${FP32DIAG_ARGS:-1 0,3 0,3 3}); unset IFS  # comma-separated "eager graph" pairs
+      for a in "${runs[@]}"; do
+        timeout -k 10 200 python scripts/exp/fp32_sink_diff.py $a >> "$OUT/fp32diag.txt" 2>&1 || return 1
+      done
+      DPA_EXT_SO=$PWD/ddp_practice_amd/_C_sp2.so timeout -k 10 200 python scripts/exp/fp32_sink_diff.py 3 0 \
+        >> "$OUT/fp32diag.txt" 2>&1 ;;
+    bn_nt_ab)  # ResNet-50: streaming (non-temporal) BN activation stores / loads (experiment builds)
+      bash scripts/ab_bench.sh "$OUT/bn_nt_ab.txt" 2 "--model resnet50 --steps 100 --warmup 10 --no-baseline" base=default \
+        ntst=ddp_practice_amd/_C_ntst.so ntld=ddp_practice_amd/_C_ntld.so ;;
     cumask)
       for e in "X=0" "HSA_CU_MASK=0:0-31" "ROC_GLOBAL_CU_MASK=0xffffffff"; do
         env $e timeout -k 10 60 python scripts/exp/cu_mask_probe.py >> "$OUT/cumask.txt" 2>&1 || return 1

@@ -364,7 +364,7 @@ def test_fp32_plain_fused_step_with_slab_sink(C, monkeypatch):
     """fp32 without a GradScaler: SGD.step() runs the fused launch (no scale), which also sums
     the conv1 weight-gradient slab -- no slab_reduce, no multi-tensor SGD launch -- and the fc
     weight gradient rides in the conv2 weight-gradient launch; the training equals the
-    separate launches (DPA_PLAIN_FUSED=0 path), eagerly and graph-replayed."""
+    separate launches (DPA_PLAIN_FUSED=0 path) bit for bit, eagerly and graph-replayed."""
     from ddp_practice_amd.data import DeviceLoader, synthetic
     from ddp_practice_amd.nn import CrossEntropyLoss
     from ddp_practice_amd.optim import SGD, sgd as sgd_mod
@@ -416,8 +416,41 @@ def test_fp32_plain_fused_step_with_slab_sink(C, monkeypatch):
         runs.append((copy.deepcopy(m.state_dict()), eager_calls))
     (sd_a, calls_a), (sd_b, calls_b) = runs
     assert calls_a == [2, 2, 0] and calls_b == [0, 0, 0], (calls_a, calls_b)
+    # bit-identical: the slab columns are summed in slab_reduce's order and every SGD kernel
+    # rounds through one rule (common.h sgd_rule); with a tolerance instead, the 1-ulp
+    # differences of two roundings grew past it within ten steps of this fp32 training
     for k in sd_a:
-        torch.testing.assert_close(sd_a[k].float(), sd_b[k].float(), rtol=1e-5, atol=1e-6, msg=k)
+        assert torch.equal(sd_a[k], sd_b[k]), (k, (sd_a[k].float() - sd_b[k].float()).abs().max().item())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B", [32, 7])
+def test_convnet_fused_bitwise_deterministic(C, dtype, B):
+    """Two identical fused forward + backward passes give bit-identical logits, running
+    statistics and gradients: every reduction of the fused kernels (BN partial rows, ticket
+    trees, weight-gradient slabs) has a fixed order, whatever the workgroups' timing."""
+    from ddp_practice_amd.ops import convnet_fused
+
+    g = torch.Generator(device="cpu").manual_seed(11)
+    x = torch.rand(B, 1, 28, 28, generator=g).to(DEV)
+    go = torch.randn(B, 10, generator=g).to(DEV)
+    res = []
+    for _ in range(2):
+        m = _model()
+        outs = []
+        for _ in range(3):  # three passes: the running statistics feed the next forward's shift
+            out = convnet_fused.convnet_forward(m, x, cdtype=dtype)
+            out.backward(go.to(dtype))
+            outs.append(out.detach().clone())
+        torch.cuda.synchronize()
+        state = {k: v.detach().clone() for k, v in m.state_dict().items()}
+        state.update({"grad." + n: p.grad.detach().clone() for n, p in m.named_parameters()})
+        res.append((outs, state))
+    (oa, sa), (ob, sb) = res
+    for i, (a, b) in enumerate(zip(oa, ob)):
+        assert torch.equal(a, b), ("logits", i, (a.float() - b.float()).abs().max().item())
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), (k, (sa[k].float() - sb[k].float()).abs().max().item())
 
 
 def test_slab_sink_flushes_for_grad_readers(C):
