@@ -2,7 +2,11 @@
 torch.optim.SGD's foreach implementation on this device?  Prints the largest parameter /
 momentum-buffer difference after a few steps for several hyper-parameter sets.
     python scripts/exp/sgd_torch_bitwise.py"""
+import sys
+
 import torch
+
+sys.path.insert(0, ".")
 
 
 def run(opt_cls, kw, shapes, steps, fused=None, seed=0):

@@ -290,12 +290,44 @@ def test_fused_amp_sgd_matches_unfused(C, momentum, sizes):
     assert int(sync[0]) == (0 if solo else 8)
 
 
+@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("kw", [dict(lr=0.05, momentum=0.9), dict(lr=0.1, momentum=0.9, weight_decay=5e-4),
+                                dict(lr=0.1, momentum=0.9, dampening=0.1),
+                                dict(lr=0.1, momentum=0.9, nesterov=True, weight_decay=1e-4), dict(lr=0.01),
+                                dict(lr=0.05, momentum=0.9, maximize=True)])
+def test_sgd_bitwise_equals_torch_foreach_sgd(C, kw, fused, monkeypatch):
+    """optim.SGD -- the multi-tensor launch and the fused plain launch -- gives the same bits
+    as torch.optim.SGD(foreach=True) over several steps: every update kernel rounds through
+    common.h sgd_rule (one fma per ATen foreach op, momentum*buf rounded on its own)."""
+    from ddp_practice_amd.optim import SGD, sgd as sgd_mod
+
+    monkeypatch.setattr(sgd_mod, "_PLAIN_FUSED", fused)
+    shapes = [(400,), (16,), (32, 16, 5, 5), (10, 1568), (7,), (4099,)]
+    res = []
+    for make in (lambda ps: torch.optim.SGD(ps, foreach=True, **kw), lambda ps: SGD(ps, **kw)):
+        g = torch.Generator(device="cpu").manual_seed(0)
+        ps = [torch.randn(s, generator=g).to(DEV).requires_grad_() for s in shapes]
+        opt = make(ps)
+        for _ in range(4):
+            for p in ps:
+                p.grad = torch.randn(p.shape, generator=g).to(DEV)
+            opt.step()
+        torch.cuda.synchronize()
+        res.append(([p.detach().clone() for p in ps], [opt.state[p].get("momentum_buffer") for p in ps]))
+    (rp, rb), (mp, mb) = res
+    for i, (a, b) in enumerate(zip(mp, rp)):
+        assert torch.equal(a, b), ("param", i, (a - b).abs().max().item())
+    for i, (a, b) in enumerate(zip(mb, rb)):
+        assert (a is None) == (b is None), i
+        assert a is None or torch.equal(a, b), ("momentum_buffer", i, (a - b).abs().max().item())
+
+
 @pytest.mark.parametrize("momentum,damp,nesterov", [(0.0, 0.0, False), (0.9, 0.0, True), (0.9, 0.1, False)])
 @pytest.mark.parametrize("sizes", [(7, 3000, 29034), (5, 200001, 33), (7, 33, 100)])
 def test_fused_plain_sgd_matches_torch_sgd(C, momentum, damp, nesterov, sizes):
-    """The fused launch without a scale (optim.SGD's plain step) == torch.optim.SGD: no
-    unscale, no skip on non-finite gradients (torch applies them), no barrier generation
-    used; eager and graph-replayed."""
+    """The fused launch without a scale (optim.SGD's plain step) == torch.optim.SGD bit for
+    bit: no unscale, no skip on non-finite gradients (torch applies them), no barrier
+    generation used; eager and graph-replayed."""
     torch.manual_seed(1)
     ps = [torch.randn(n, device=DEV) for n in sizes]
     pa = [p.clone() for p in ps]
@@ -329,8 +361,8 @@ def test_fused_plain_sgd_matches_torch_sgd(C, momentum, damp, nesterov, sizes):
             graph.replay()
         ref.step()
         torch.cuda.synchronize()
-        for x, q, g in zip(pa, pr, gs):
-            torch.testing.assert_close(x, q.detach(), rtol=1e-6, atol=1e-6, equal_nan=True)
+        for x, q, g in zip(pa, pr, gs):  # bit for bit (common.h sgd_rule rounds as ATen's foreach SGD)
+            torch.testing.assert_close(x, q.detach(), rtol=0, atol=0, equal_nan=True)
         for x, g in zip(ga, gs):
             assert torch.equal(x, g) or torch.equal(x.isnan(), g.isnan())  # the gradient is left as it was
         if momentum:
