@@ -112,6 +112,18 @@ def parse(argv=None):
 
 
 # ----------------------------------------------------------------------------- entry
+def _spin_sync(torch, device: int):
+    """hipDeviceScheduleSpin before the device's first use (runtime/device.spin_sync, opt-in
+    DPA_SPIN_SYNC=1: no measured difference on the timed window).  Returns "spin", "default"
+    or "spin failed: <hipError>"."""
+    if torch.cuda.device_count() == 0:
+        return "default"
+    from ddp_practice_amd.runtime.device import spin_sync
+
+    rc = spin_sync(device)
+    return "default" if rc is None else "spin" if rc == 0 else f"spin failed: {rc}"
+
+
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     args = parse(argv)
@@ -441,8 +453,9 @@ def run_rank(args) -> int:
 
         shared_gpu_env(world)  # before the first HIP call below
         shared_cu_mask(world, int(os.environ.get("RANK", "0")))
-    gpu = torch.cuda.is_available()
     local_rank = 0 if args.share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
+    spin_rc = _spin_sync(torch, local_rank)  # opt-in busy-polled host waits (runtime/device.spin_sync)
+    gpu = torch.cuda.is_available()
     if gpu:
         torch.cuda.set_device(local_rank)
         dev = torch.device("cuda", local_rank)
@@ -564,7 +577,7 @@ def run_rank(args) -> int:
                 "sync_bn": dist_path and not args.no_sync_bn,
                 "amp": f"autocast {args.amp_dtype} + GradScaler" if amp is not None else "fp32",
                 "optimizer": "SGD(lr=1e-4)",
-                "hipgraph": bool(h["captured"]),
+                "hipgraph": bool(h["captured"]), "host_wait": spin_rc,
                 "steps_per_graph": h["spg"],
                 "comm": _comm_desc(comm) if dist_path else "none (1 rank)",
                 "grad_avg": h["grad_avg"],
@@ -844,6 +857,7 @@ def bench_resnet(args) -> int:
 
         shared_gpu_env(world)
         shared_cu_mask(world, int(os.environ.get("RANK", "0")))
+    spin_rc = _spin_sync(torch, local_rank)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist_path = world > 1 or args.force_collectives
@@ -939,7 +953,7 @@ def bench_resnet(args) -> int:
             "config": {"model": "ResNet-50 (25,557,032 params)", "global_batch": bs * world, "seq_len": None,
                        "parallelism": f"dp{world}", "per_rank_batch": bs, "impl": args.resnet_impl,
                        "sync_bn": dist_path and not args.no_sync_bn, "optimizer": "SGD(lr=1e-4)",
-                       "comm": _comm_desc(c) if dist_path else "none", "hipgraph": bool(captured),
+                       "comm": _comm_desc(c) if dist_path else "none", "hipgraph": bool(captured), "host_wait": spin_rc,
                        "shared_gpu": bool(args.share_gpu),
                        "stack": ("torch nn + torch.autocast + F.cross_entropy + torch.optim.SGD(foreach)"
                                  + (" + torch.amp.GradScaler" if amp == torch.float16 else " (bf16: no GradScaler)")

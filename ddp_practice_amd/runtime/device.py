@@ -28,6 +28,41 @@ def local_device():
     return torch.device("cuda", lr % max(n, 1))
 
 
+def _loaded_hip():
+    """The HIP runtime this process already loaded (torch's bundled libamdhip64), or None.  Opening
+    another copy by name could bring up a second runtime whose settings torch never sees."""
+    import ctypes
+
+    try:
+        with open("/proc/self/maps") as f:
+            paths = {ln.split()[-1] for ln in f if "libamdhip64" in ln}
+    except OSError:
+        return None
+    return ctypes.CDLL(sorted(paths)[0]) if paths else None
+
+
+def spin_sync(device: int = 0) -> int | None:
+    """Host waits on the GPU (``torch.cuda.synchronize``, event and stream waits) busy-poll:
+    ``hipSetDeviceFlags(hipDeviceScheduleSpin)`` on ``device``.  HIP's default (Auto) yields
+    the CPU whenever the host has more logical CPUs than HIP contexts -- always, here -- and a
+    yielding wait notices completion later.  Call after ``import torch`` and before the
+    device's first use (hipErrorSetOnActiveProcess after it).  Opt-in (``DPA_SPIN_SYNC=1``): on
+    the driver's 20-step ConvNet window it measured no difference (0.0491-0.0518 vs
+    0.0491-0.0504 ms, profiles/r6u_spin_sync_ab.txt).  Returns the hipError code, None when
+    skipped (not opted in, or no HIP runtime loaded)."""
+    if os.environ.get("DPA_SPIN_SYNC", "0") != "1":
+        return None
+    import ctypes
+
+    lib = _loaded_hip()
+    if lib is None:
+        return None
+    rc = lib.hipSetDevice(ctypes.c_int(device))
+    if rc != 0:
+        return int(rc)
+    return int(lib.hipSetDeviceFlags(ctypes.c_uint(1)))  # hipDeviceScheduleSpin
+
+
 def shared_gpu_env(world: int | None) -> None:
     """Environment of ranks that share one device (``--share-gpu`` rehearsals): the fused
     paths' gates (``DPA_SHARED_GPU``) and, for 3+ ranks, one HIP hardware queue per process.

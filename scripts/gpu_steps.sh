@@ -25,6 +25,7 @@
 #   xtests       the xGMI / distributed / SyncBN / fused-ConvNet GPU tests (world-8 DDP excluded)
 #   fp32det      fp32 slab-sink / bitwise-determinism tests, default and fp32 split-2 builds
 #   bn_nt_ab     ResNet-50 A/B of non-temporal BN stores / loads
+#   spin_ab      driver command, spinning vs yielding host waits
 #   smoke        __graft_entry__.smoke()
 #   gputests     the whole GPU test tier (as the driver runs it: world-8 rehearsals opt-in)
 set -o pipefail
@@ -68,6 +69,8 @@ step() {
       done
       DPA_EXT_SO=$PWD/ddp_practice_amd/_C_sp2.so timeout -k 10 200 python scripts/exp/fp32_sink_diff.py 3 0 \
         >> "$OUT/fp32diag.txt" 2>&1 ;;
+    spin_ab)  # busy-polled host waits (runtime/device.spin_sync) on the driver's command
+      bash scripts/ab_bench.sh "$OUT/spin_ab.txt" 4 "--steps 20 --warmup 5" spin=env:DPA_SPIN_SYNC=1 yield=default ;;
     bn_nt_ab)  # ResNet-50: streaming (non-temporal) BN activation stores / loads (experiment builds)
       bash scripts/ab_bench.sh "$OUT/bn_nt_ab.txt" 2 "--model resnet50 --steps 100 --warmup 10 --no-baseline" base=default \
         ntst=ddp_practice_amd/_C_ntst.so ntld=ddp_practice_amd/_C_ntld.so ;;
