@@ -1184,10 +1184,13 @@ conv_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __re
 
 // NWM x NWN waves (default 2 x 2; 2 x 4 = 8 waves, DPA_WGRAD_WAVES=8: the second wave on
 // every SIMD hides the other's transposed-read waits, as the forward's 8-wave tiles do).
-template <typename T, int BM, int BN, int NWM = 2, int NWN = 2>
+// FIX (DPA_WGRAD_FIXUP_MAXSP, opt-in): the split-K reduction in this launch -- partial
+// tiles stored write-through, one ticket per output tile, and the tile's last arriver sums
+// the splits in split order and writes the fp32 OIHW gradient (no wgrad_reduce launch).
+template <typename T, int BM, int BN, int NWM = 2, int NWN = 2, bool FIX = false>
 __global__ void __launch_bounds__(64 * NWM * NWN)
 conv_wgrad_glds_kernel(const T* __restrict__ dy, const T* __restrict__ x, float* __restrict__ slab, Geom g,
-                       int splits, long long pps) {
+                       int splits, long long pps, float* __restrict__ grad, unsigned* __restrict__ tickets) {
   typedef typename MM<T>::frag frag;
   constexpr int BP = 64;
   constexpr int CHA = BM / 8, CHB = BN / 8;
@@ -1294,8 +1297,34 @@ conv_wgrad_glds_kernel(const T* __restrict__ dy, const T* __restrict__ x, float*
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int m = k0 + wm * (BM / NWM) + a * 16 + 4 * grp + j, n = n0 + wn * (BN / NWN) + b * 16 + gi;
-        out[(long long)m * RSC + n] = acc[a][b][j];
+        if constexpr (FIX) st_wt(out + (long long)m * RSC + n, acc[a][b][j]);
+        else out[(long long)m * RSC + n] = acc[a][b][j];
       }
+  if constexpr (FIX) {
+    __shared__ int s_flag;
+    // (last_arriver: this wave's write-through stores drained, one ticket per workgroup)
+    if (!last_arriver(tickets + tile, (unsigned)splits, &s_flag)) return;
+    // the tile's splits in split order, 8 loads in flight per lane; consecutive lanes take
+    // consecutive columns (channels of one tap: unit-stride OIHW writes on a 1x1 conv)
+    const long long plane = (long long)g.K * RSC;
+    const int st = g.R * g.S;
+    for (int e = tid; e < BM * BN; e += 64 * NW) {
+      const int r = e / BN, cn = e - r * BN;
+      const long long off = (long long)(k0 + r) * RSC + n0 + cn;
+      float t = 0.f;
+      int s0 = 0;
+      for (; s0 + 8 <= splits; s0 += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = ld_wt(slab + (s0 + u) * plane + off);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t += v[u];
+      }
+      for (; s0 < splits; ++s0) t += ld_wt(slab + s0 * plane + off);
+      const int n = n0 + cn, c = n % g.C, rs = n / g.C;  // (r*S + s)*C + c
+      grad[((long long)(k0 + r) * g.C + c) * st + rs] = t;
+    }
+  }
 }
 
 constexpr int WR_QC = 16;  // float4 columns per wgrad_reduce_kernel workgroup
@@ -2004,6 +2033,46 @@ int64_t wgrad_waves_config(int64_t w) {
 // wgrad tile shapes: BM | Cout, BN | C (a column tile stays inside one filter tap)
 static int wtile(int64_t v) { return v % 128 == 0 ? 128 : 64; }
 
+// In-launch split-K reduction (conv_wgrad_glds_kernel FIX) for convs of at most
+// DPA_WGRAD_FIXUP_MAXSP splits (default 0: off; wgrad_fixup_config sets it).  Measured
+// slower on ResNet-50 at every bound -- 13.77 ms off, 14.02 at 8 splits, 14.74 at 32, 17.69
+// for every conv (profiles/r6v_wgrad_fixup_ab.txt): the partial tiles' write-through stores
+// and each tile's serial last-arriver sum cost more than the separate, fully parallel launch.  Tickets: one
+// zeroed device array per device, re-armed by every tile's last arriver; allocated outside
+// any capture (a first use inside one takes the reduce launch instead).
+static long long g_fix_maxsp = -1;
+static long long fix_maxsp() {
+  if (g_fix_maxsp < 0) {
+    const char* e = std::getenv("DPA_WGRAD_FIXUP_MAXSP");
+    g_fix_maxsp = e != nullptr ? std::atoll(e) : 0LL;
+  }
+  return g_fix_maxsp;
+}
+int64_t wgrad_fixup_config(int64_t maxsp) {
+  const int64_t prev = fix_maxsp();
+  if (maxsp >= 0) g_fix_maxsp = maxsp;
+  return prev;
+}
+constexpr int kFixTickets = 4096;
+static unsigned* fix_tickets(long long tiles) {
+  static unsigned* per_dev[64] = {};
+  if (tiles > kFixTickets) return nullptr;
+  int dev = 0;
+  DPA_CHECK_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return nullptr;
+  if (per_dev[dev] == nullptr) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    DPA_CHECK_HIP(hipStreamIsCapturing(cur_stream(), &st));
+    if (st != hipStreamCaptureStatusNone) return nullptr;
+    unsigned* p = nullptr;
+    DPA_CHECK_HIP(hipMalloc(&p, kFixTickets * sizeof(unsigned)));
+    DPA_CHECK_HIP(hipMemset(p, 0, kFixTickets * sizeof(unsigned)));
+    DPA_CHECK_HIP(hipDeviceSynchronize());
+    per_dev[dev] = p;
+  }
+  return per_dev[dev];
+}
+
 int64_t wgrad_splits(int64_t M, int64_t K, int64_t C, int64_t R, int64_t S) {
   // ~2 workgroups per CU, each at least 16 K-steps of 64 pixels, and the fp32
   // partials at most ~48 MB (written and re-read once: ~12 us at HBM rate)
@@ -2054,6 +2123,11 @@ std::vector<int64_t> conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor grad, in
   const long long pps = ((g.M + sp - 1) / sp + 63) / 64 * 64;
   const int BM = wtile(g.K), BN = wtile(g.C);
   const long long blocks = sp * (g.K / BM) * (RSC / BN);
+  // in-launch split-K reduction: 8-wave LDS-DMA kernels, reduced gradients wanted
+  const bool glds = !stem && ((g.R == 1 && g.S == 1 && wgrad_glds() >= 1) || wgrad_glds() == 2);
+  unsigned* tk = nullptr;
+  const bool fixed = reduce && glds && wgrad_waves() == 8 && sp <= fix_maxsp() &&
+                     (tk = fix_tickets((g.K / BM) * (RSC / BN))) != nullptr;
   auto launch = [&](auto tag) {
     using T = decltype(tag);
     const T* dp = reinterpret_cast<const T*>(dy.data_ptr());
@@ -2062,18 +2136,26 @@ std::vector<int64_t> conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor grad, in
     const dim3 gr((unsigned)blocks), th(THR);
     // 1x1 (mode 1, default) or every MODE_GEN conv (mode 2): on 3x3 it measured ~5 % slower
     if (!stem && ((g.R == 1 && g.S == 1 && wgrad_glds() >= 1) || wgrad_glds() == 2)) {
+      float* gp = grad.data_ptr<float>();
       if (wgrad_waves() == 8) {
         const dim3 t8(512);
-        if (BM == 128 && BN == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 128, 128, 2, 4>), gr, t8, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
-        else if (BM == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 128, 64, 4, 2>), gr, t8, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
-        else if (BN == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 64, 128, 2, 4>), gr, t8, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
-        else hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 64, 64, 2, 4>), gr, t8, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+        if (fixed) {
+          if (BM == 128 && BN == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 128, 128, 2, 4, true>), gr, t8, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps, gp, tk);
+          else if (BM == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 128, 64, 4, 2, true>), gr, t8, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps, gp, tk);
+          else if (BN == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 64, 128, 2, 4, true>), gr, t8, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps, gp, tk);
+          else hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 64, 64, 2, 4, true>), gr, t8, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps, gp, tk);
+          return;
+        }
+        if (BM == 128 && BN == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 128, 128, 2, 4>), gr, t8, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps, gp, nullptr);
+        else if (BM == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 128, 64, 4, 2>), gr, t8, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps, gp, nullptr);
+        else if (BN == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 64, 128, 2, 4>), gr, t8, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps, gp, nullptr);
+        else hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 64, 64, 2, 4>), gr, t8, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps, gp, nullptr);
         return;
       }
-      if (BM == 128 && BN == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 128, 128>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
-      else if (BM == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 128, 64>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
-      else if (BN == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 64, 128>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
-      else hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 64, 64>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
+      if (BM == 128 && BN == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 128, 128>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps, gp, nullptr);
+      else if (BM == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 128, 64>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps, gp, nullptr);
+      else if (BN == 128) hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 64, 128>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps, gp, nullptr);
+      else hipLaunchKernelGGL((conv_wgrad_glds_kernel<T, 64, 64>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps, gp, nullptr);
       return;
     }
     if (stem && BM == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 64, MODE_STEM>), gr, th, 0, cur_stream(), dp, xp, sl, g, (int)sp, pps);
@@ -2087,7 +2169,7 @@ std::vector<int64_t> conv_wgrad(at::Tensor dy, at::Tensor x, at::Tensor grad, in
   DPA_CHECK_LAUNCH();
   // reduce = false: the slab stays for wgrad_reduce_batch (the geometry below is its entry)
   std::vector<int64_t> geo{sp, g.K, g.C, SR, SS, Cd, Rd, Sd};
-  if (!reduce) return geo;
+  if (!reduce || fixed) return geo;
   const long long total = (long long)g.K * RSC;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + 4 * WR_QC - 1) / (4 * WR_QC))), dim3(256), 0,
                      cur_stream(),
@@ -2155,6 +2237,7 @@ void register_conv_igemm(pybind11::module& m) {
   s.attr("MODE_S2T") = igemm::MODE_S2T;
   s.def("pack_weights", &igemm::pack_weights);
   s.def("wgrad_splits", &igemm::wgrad_splits);
+  s.def("wgrad_fixup_config", &igemm::wgrad_fixup_config, pybind11::arg("maxsp") = -1);
   s.def("wgrad_config", &igemm::wgrad_config, pybind11::arg("glds") = -1);
   s.def("g3x3_config", &igemm::g3x3_config, pybind11::arg("on") = -1);
   s.def("glds_config", &igemm::glds_config, pybind11::arg("stages") = -1);

@@ -26,6 +26,7 @@
 #   fp32det      fp32 slab-sink / bitwise-determinism tests, default and fp32 split-2 builds
 #   bn_nt_ab     ResNet-50 A/B of non-temporal BN stores / loads
 #   spin_ab      driver command, spinning vs yielding host waits
+#   fixup_ab     ResNet-50 in-launch split-K weight-gradient reduction (tests, then A/B)
 #   smoke        __graft_entry__.smoke()
 #   gputests     the whole GPU test tier (as the driver runs it: world-8 rehearsals opt-in)
 set -o pipefail
@@ -69,6 +70,11 @@ step() {
       done
       DPA_EXT_SO=$PWD/ddp_practice_amd/_C_sp2.so timeout -k 10 200 python scripts/exp/fp32_sink_diff.py 3 0 \
         >> "$OUT/fp32diag.txt" 2>&1 ;;
+    fixup_ab)  # ResNet-50: split-K weight-gradient reduction inside the launch, by split bound
+      timeout -k 10 300 $PYT --timeout 120 -p no:cacheprovider tests/test_conv_igemm_gpu.py -k "fixup or wgrad" \
+        > "$OUT/fixup_tests.txt" 2>&1 &&
+      bash scripts/ab_bench.sh "$OUT/fixup_ab.txt" 2 "--model resnet50 --steps 100 --warmup 10 --no-baseline" \
+        off=default sp8=env:DPA_WGRAD_FIXUP_MAXSP=8 sp32=env:DPA_WGRAD_FIXUP_MAXSP=32 all=env:DPA_WGRAD_FIXUP_MAXSP=100000 ;;
     spin_ab)  # busy-polled host waits (runtime/device.spin_sync) on the driver's command
       bash scripts/ab_bench.sh "$OUT/spin_ab.txt" 4 "--steps 20 --warmup 5" spin=env:DPA_SPIN_SYNC=1 yield=default ;;
     bn_nt_ab)  # ResNet-50: streaming (non-temporal) BN activation stores / loads (experiment builds)

@@ -309,6 +309,52 @@ def test_conv_wgrad_glds_matches_register_staged(C, shape):
     assert err < 1e-2, err
 
 
+@pytest.mark.parametrize("shape", [
+    (2, 64, 14, 14, 64, 3, 1, 1),     # 3x3, one tile x splits
+    (3, 256, 7, 7, 128, 1, 1, 0),     # 1x1, ragged pixel count (split past the end)
+    (2, 128, 14, 14, 256, 1, 2, 0),   # 1x1 stride 2
+    (4, 64, 28, 28, 128, 3, 1, 1),    # several pixel splits
+    (8, 256, 14, 14, 512, 1, 1, 0),   # 4 x 2 tiles
+])
+def test_conv_wgrad_fixup_matches_reduce_launch(C, shape):
+    """The split-K reduction inside the weight-gradient launch (the tile's last arriver sums
+    the splits, conv_igemm.wgrad_fixup_config) == the separate wgrad_reduce launch up to
+    summation order, == fp32 torch, bit-identical from run to run (the tickets re-arm), and
+    graph-replayable."""
+    from ddp_practice_amd.ops.conv_igemm import conv_wgrad
+
+    K_ = C.conv_igemm
+    N, Cin, H, W, K, R, stride, pad = shape
+    g = torch.Generator().manual_seed(31)
+    x = torch.randn(N, Cin, H, W, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=CL)
+    OH = (H + 2 * pad - R) // stride + 1
+    dy = torch.randn(N, K, OH, OH, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=CL)
+    prev_g, prev_f = K_.wgrad_config(2), K_.wgrad_fixup_config(0)
+    try:
+        ref = conv_wgrad(dy, x, (K, Cin, R, R), stride, pad)
+        K_.wgrad_fixup_config(1 << 20)
+        got = conv_wgrad(dy, x, (K, Cin, R, R), stride, pad)
+        again = conv_wgrad(dy, x, (K, Cin, R, R), stride, pad)
+        out = torch.empty_like(got)
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            out.copy_(conv_wgrad(dy, x, (K, Cin, R, R), stride, pad))
+        for _ in range(2):
+            out.zero_()
+            gr.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(out, got)
+    finally:
+        K_.wgrad_config(prev_g)
+        K_.wgrad_fixup_config(prev_f)
+    assert torch.equal(got, again)
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5 * ref.abs().max().item())
+    w = torch.zeros(K, Cin, R, R, device=DEV, requires_grad=True)
+    F.conv2d(x.float(), w, None, stride, pad).backward(dy.float())
+    err = ((got - w.grad).abs().max() / w.grad.abs().max()).item()
+    assert err < 1e-2, err
+
+
 @pytest.mark.parametrize("act,R", [(1, 1), (2, 1), (2, 3)])
 @pytest.mark.parametrize("shape", [(2, 128, 14, 14, 64), (3, 64, 7, 7, 256), (2, 256, 28, 28, 128),
                                    (12, 64, 56, 56, 64)])
