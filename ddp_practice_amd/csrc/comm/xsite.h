@@ -44,6 +44,8 @@
 // __syncthreads() form, for the A/B.
 #ifdef DPA_XS_FULLBAR
 #define DPA_XS_BARRIER() __syncthreads()
+#elif defined(DPA_XS_NO_BAR)
+#define DPA_XS_BARRIER() do {} while (0)
 #else
 #define DPA_XS_BARRIER()                          \
   do {                                            \
@@ -115,7 +117,22 @@ __device__ __forceinline__ void xgmi_put2(unsigned long long* dst, unsigned long
 // Lane 0 of every workgroup, once per launch, as early as possible (the returned word is
 // only needed by xsite_exchange: its round trip hides behind the caller's slab loads).
 // bid: the workgroup's index among the launch's workgroups on this site.
+// DPA_XS_NOOP (experiment builds, world-1 A/Bs only): ticket, exchange and advance compiled
+// out -- the floor of what the exchanges cost a forced (W > 1-shaped) step on one GPU.
+// Finer world-1 bisection switches (experiment builds): DPA_XS_NO_TICKET (no ticket load),
+// DPA_XS_NO_ADVANCE (no epoch-word stores), DPA_XS_NO_BAR (no barriers in the exchange),
+// DPA_XS_NO_XG (the AMP step's gradient average only).
+#if defined(DPA_XS_NOOP) || defined(DPA_XS_NO_XG)
+constexpr bool kXsNoop = true;
+#else
+constexpr bool kXsNoop = false;
+#endif
 __device__ __forceinline__ unsigned long long xsite_ticket(const XSite& xs, int bid) {
+#if defined(DPA_XS_NOOP) || defined(DPA_XS_NO_TICKET)
+  (void)xs;
+  (void)bid;
+  return 0ull;
+#endif
   // (a plain load, plain epoch stores and advancing the words after the exchange measured no
   // faster on the forced step: profiles/r5o_xsite_mode_ab.txt, r5s_xsite_plain_ab.txt)
   return __hip_atomic_load(xs.tick + (bid < kEpochWords ? bid : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -139,6 +156,9 @@ __device__ __forceinline__ uint32_t xsite_epoch(const XSite& xs, unsigned long l
 // kEpochWords cannot keep its workgroups' epochs equal: flagged as an error (the exchange
 // then gives up), and the host checks grids against it.
 __device__ __forceinline__ void xsite_advance(const XSite& xs, uint32_t ep, int bid, int nthr) {
+#ifdef DPA_XS_NO_ADVANCE
+  return;
+#endif
   const int nblk = xs.nblk > 0 ? xs.nblk : (int)(gridDim.x * gridDim.y * gridDim.z);
   const int tid = threadIdx.x;
   if (nblk > kEpochWords) {
@@ -185,6 +205,9 @@ __device__ __forceinline__ float xsite_wait(const XSite& xs, const unsigned long
 // every thread of the workgroup; ends with an LDS-only barrier.
 __device__ __forceinline__ void xsite_exchange(const XSite& xs, float* vals, int n, unsigned long long tk,
                                                int bid, int nthr = 256 /* <= the workgroup size */) {
+#ifdef DPA_XS_NOOP
+  return;
+#endif
   __shared__ uint32_t ep_s;
   const int tid = threadIdx.x;
   const bool pusher = bid == 0;
@@ -281,6 +304,9 @@ __device__ __forceinline__ float xsite_pull_at(const XSite& xs, uint32_t ep, int
 template <typename PosF>
 __device__ __forceinline__ void xsite_exchange_slice(const XSite& xs, float* vals, int n, PosF pos,
                                                      unsigned long long tk, int bid, int nthr) {
+#ifdef DPA_XS_NOOP
+  return;
+#endif
   __shared__ uint32_t ep_s;
   const int tid = threadIdx.x;
   if (tid == 0) ep_s = xsite_epoch(xs, tk, bid);

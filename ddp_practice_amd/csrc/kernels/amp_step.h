@@ -306,10 +306,16 @@ amp_sgd_body(const MTList& L, float* __restrict__ scale, int* __restrict__ track
     }
   }
   DPA_STAMP(11);
-  if constexpr (XG) {
+  if constexpr (XG && !xgmi::kXsNoop) {
     __shared__ uint32_t ep_x;
     if (tid == 0) ep_x = xgmi::xsite_epoch(xg, tk, bid);
+#ifdef DPA_XG_LDSBAR
+    // LDS-only broadcast of the epoch: the gradient / parameter loads above stay in flight
+    // while the epoch words are stored and the peers' granules are polled
+    DPA_XS_BARRIER();
+#else
     __syncthreads();
+#endif
     const uint32_t ep = ep_x;
     xgmi::xsite_advance(xg, ep, bid, THR);
     const long long par = (long long)(ep & 1u) * xgmi::kMaxRanks * xg.slot_bytes;

@@ -27,6 +27,9 @@
 #   bn_nt_ab     ResNet-50 A/B of non-temporal BN stores / loads
 #   spin_ab      driver command, spinning vs yielding host waits
 #   fixup_ab     ResNet-50 in-launch split-K weight-gradient reduction (tests, then A/B)
+#   xsnoop_ab    forced step with the exchanges compiled out vs as built, and the plain step
+#   xsbis_ab     the forced step's exchange cost bisected (experiment builds)
+#   xglds_ab     AMP gradient average with an LDS-only epoch broadcast (W=2 tests + forced A/B)
 #   smoke        __graft_entry__.smoke()
 #   gputests     the whole GPU test tier (as the driver runs it: world-8 rehearsals opt-in)
 set -o pipefail
@@ -75,6 +78,21 @@ step() {
         > "$OUT/fixup_tests.txt" 2>&1 &&
       bash scripts/ab_bench.sh "$OUT/fixup_ab.txt" 2 "--model resnet50 --steps 100 --warmup 10 --no-baseline" \
         off=default sp8=env:DPA_WGRAD_FIXUP_MAXSP=8 sp32=env:DPA_WGRAD_FIXUP_MAXSP=32 all=env:DPA_WGRAD_FIXUP_MAXSP=100000 ;;
+    xsnoop_ab)  # the forced step with every exchange compiled out (world 1) vs as built, and the plain step
+      bash scripts/ab_bench.sh "$OUT/xsnoop_ab.txt" 3 "--force-collectives --steps 2000 --warmup 50 --no-baseline \
+--epochs 0 --no-steady --extra-dtypes ," forced=default noop=ddp_practice_amd/_C_xsnoop.so &&
+      bash scripts/ab_bench.sh "$OUT/xsnoop_ab.txt" 3 "--steps 2000 --warmup 50 --no-baseline --epochs 0 --no-steady \
+--extra-dtypes ," plain=default ;;
+    xsbis_ab)  # the forced step's exchange cost, bisected: no ticket / advance / barriers / AMP average
+      local so=ddp_practice_amd
+      bash scripts/ab_bench.sh "$OUT/xsbis_ab.txt" 3 "--force-collectives --steps 2000 --warmup 50 --no-baseline \
+--epochs 0 --no-steady --extra-dtypes ," forced=default notk=$so/_C_xsnotk.so noadv=$so/_C_xsnoadv.so \
+        nobar=$so/_C_xsnobar.so noxg=$so/_C_xsnoxg.so noop=$so/_C_xsnoop.so ;;
+    xglds_ab)  # AMP gradient average: LDS-only epoch broadcast (experiment build) -- W=2 tests, then the forced A/B
+      DPA_EXT_SO=$PWD/ddp_practice_amd/_C_xglds.so timeout -k 10 400 $PYT --timeout 170 -p no:cacheprovider \
+        tests/test_xgmi_ddp_gpu.py -k "not 8-" > "$OUT/xglds_tests.txt" 2>&1 &&
+      bash scripts/ab_bench.sh "$OUT/xglds_ab.txt" 3 "--force-collectives --steps 2000 --warmup 50 --no-baseline \
+--epochs 0 --no-steady --extra-dtypes ," forced=default xglds=ddp_practice_amd/_C_xglds.so ;;
     spin_ab)  # busy-polled host waits (runtime/device.spin_sync) on the driver's command
       bash scripts/ab_bench.sh "$OUT/spin_ab.txt" 4 "--steps 20 --warmup 5" spin=env:DPA_SPIN_SYNC=1 yield=default ;;
     bn_nt_ab)  # ResNet-50: streaming (non-temporal) BN activation stores / loads (experiment builds)

@@ -653,6 +653,43 @@ def test_prechecked_amp_step_skips_overflow(C, scale, monkeypatch):
         assert torch.equal(sd_a[k], sd_b[k]), k
 
 
+@pytest.mark.parametrize("dp,xval,flagged", [(4e36, 0.0, True), (1.0, 0.0, False), (1.0, 0.5, False)])
+def test_conv1_bias_partials_are_prechecked(C, dp, xval, flagged):
+    """The producer-side gradient check covers the conv1 BIAS partial rows, not only the
+    weight partials: with a zero input image every weight partial is exactly 0 while the
+    bias partials (sums of BN1's backward output over a workgroup's pixels) exceed the row
+    bound FLT_MAX / rows -- the check word must be set (a step would otherwise apply an
+    overflowing bias sum unskipped)."""
+    cn, cb = C.convnet, C.convblock
+    B, dt = 2, torch.bfloat16
+    g = torch.Generator().manual_seed(4)
+    x = torch.full((B, 1, 28, 28), xval).to(DEV, dt)
+    y1 = torch.randn(B, 16, 28, 28, generator=g).to(DEV, dt)
+    dp1 = torch.full((B, 16, 14, 14), dp).to(DEV, dt)
+    idx1 = torch.full((B, 16, 14, 14), 4, dtype=torch.uint8, device=DEV)  # window position 0, ReLU open
+    n = float(B * 28 * 28)
+    fstats1 = torch.zeros(cb.stats_len(16), device=DEV)
+    fstats1[16:32] = n  # sum((y - shift)^2) = n: unit variance, zero mean, zero shift
+    fstats1[32] = n
+    gsum1 = torch.zeros(cn.dgrad2_rows(B) * 32, device=DEV)  # BN1 backward sums: zero
+    g1 = torch.ones(16, device=DEV)
+    dg1, dbe1 = torch.empty(16, device=DEV), torch.empty(16, device=DEV)
+    nwg1, rows2 = cn.wgrad_bn_rows(1, B), cn.wgrad_bn_rows(2, B)
+    wslab1 = torch.empty(nwg1 * (16 * 25 + 16), device=DEV)
+    wslab2 = torch.zeros(rows2 * (32 * 400 + 32), device=DEV)
+    out2 = torch.empty(32 * 400 + 32, device=DEV)
+    chk = torch.zeros(2, dtype=torch.int32, device=DEV)
+    cn.conv1_wgrad_slab2(x, y1, dp1, idx1, fstats1, gsum1, None, g1, 1e-5, dg1, dbe1, wslab1, wslab2, out2, None, chk)
+    torch.cuda.synchronize()
+    rows = wslab1.view(nwg1, 16 * 25 + 16)
+    if xval == 0.0:
+        assert bool((rows[:, :400] == 0).all())  # the weight partials: exactly zero
+    assert bool(torch.isfinite(rows).all())
+    if flagged:
+        assert rows[:, 400:].abs().max().item() > 3.402823466e38 / nwg1  # only the bias partials exceed
+    assert (int(chk[0]) != 0) == flagged, (int(chk[0]), rows[:, 400:].abs().max().item())
+
+
 def test_prechecked_dropped_by_grad_readers(C, monkeypatch):
     """Reading .grad between backward and step (GradScaler.unscale_ flushes the deferred work)
     drops the producer checks: that step agrees on found_inf at the barrier instead."""
