@@ -42,7 +42,10 @@ constexpr int CC_ELT = 256;  // channels per column chunk, elementwise kernels (
 constexpr int G1 = 128;      // level-1 group size of the ticket tree (one level up to 128 row blocks)
 constexpr int MAXGR = 1024;  // row blocks per chunk in the statistics kernels
 constexpr int SHIFT_OFF = 4; // stats layout: [0,C) s1, [C,2C) s2, [2C] n, shift copy at 2C+SHIFT_OFF (16-B aligned)
-constexpr int U = 4;         // rows in flight per lane
+#ifndef DPA_BN_U
+#define DPA_BN_U 4
+#endif
+constexpr int U = DPA_BN_U;  // rows in flight per lane (A/B builds: -DDPA_BN_U=2|8)
 constexpr int UF = 8;        // rows in flight per lane, forward statistics (one input)
 constexpr int MAXTICKETS = 2048;
 

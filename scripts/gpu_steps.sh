@@ -30,6 +30,7 @@
 #   xsnoop_ab    forced step with the exchanges compiled out vs as built, and the plain step
 #   xsbis_ab     the forced step's exchange cost bisected (experiment builds)
 #   xglds_ab     AMP gradient average with an LDS-only epoch broadcast (W=2 tests + forced A/B)
+#   bnu_ab       ResNet-50, BN rows in flight per lane 2 / 4 / 8
 #   smoke        __graft_entry__.smoke()
 #   gputests     the whole GPU test tier (as the driver runs it: world-8 rehearsals opt-in)
 set -o pipefail
@@ -93,6 +94,9 @@ step() {
         tests/test_xgmi_ddp_gpu.py -k "not 8-" > "$OUT/xglds_tests.txt" 2>&1 &&
       bash scripts/ab_bench.sh "$OUT/xglds_ab.txt" 3 "--force-collectives --steps 2000 --warmup 50 --no-baseline \
 --epochs 0 --no-steady --extra-dtypes ," forced=default xglds=ddp_practice_amd/_C_xglds.so ;;
+    bnu_ab)  # ResNet-50: rows in flight per lane of the NHWC BatchNorm kernels (experiment builds)
+      bash scripts/ab_bench.sh "$OUT/bnu_ab.txt" 2 "--model resnet50 --steps 100 --warmup 10 --no-baseline" u4=default \
+        u2=ddp_practice_amd/_C_bnu2.so u8=ddp_practice_amd/_C_bnu8.so ;;
     spin_ab)  # busy-polled host waits (runtime/device.spin_sync) on the driver's command
       bash scripts/ab_bench.sh "$OUT/spin_ab.txt" 4 "--steps 20 --warmup 5" spin=env:DPA_SPIN_SYNC=1 yield=default ;;
     bn_nt_ab)  # ResNet-50: streaming (non-temporal) BN activation stores / loads (experiment builds)
