@@ -214,6 +214,15 @@ def worker(rank, world, port, mode, q):
                     for p, b in zip(ps, before):
                         assert torch.equal(p, b), "partial-sum update applied after a failed exchange"
                     assert sc.item() == 4.0 and tr.item() == 0  # skipped step: back-off, as for an inf
+                    # the engine's error word stays set: the next fused step gives up at once
+                    # (no new wait) and skips and backs off again -- the ranks' parameters
+                    # never take a partial average after a failed exchange
+                    C.optim.amp_sgd_fused(ps, gs, [], 0.1, 0.0, 0.0, 0.0, False, False, [], sc, tr, fi, 2.0, 0.5,
+                                          2000, sync, x)
+                    torch.cuda.synchronize()
+                    for p, b in zip(ps, before):
+                        assert torch.equal(p, b), "update applied with the engine's error word set"
+                    assert sc.item() == 2.0 and tr.item() == 0
                 assert x.error() == 1, x.error()
             store.set(f"done{rank}", "1")
             store.wait([f"done{r}" for r in range(world)])

@@ -130,6 +130,27 @@ def test_shared_cu_mask_gives_each_rank_its_own_cus(monkeypatch):
     assert shared_cu_mask(8, 3) is None
 
 
+def test_spin_sync_is_opt_in_and_uses_the_loaded_runtime(monkeypatch):
+    """runtime/device.spin_sync: nothing without DPA_SPIN_SYNC=1; opted in, it talks only to
+    the HIP runtime this process already loaded (torch's), never a second copy by name --
+    with torch's runtime loaded on a GPU-less host it calls it and reports the hipError."""
+    import torch  # noqa: F401  (loads torch's libamdhip64, as bench.py has by then)
+
+    from ddp_practice_amd.runtime import device
+
+    monkeypatch.delenv("DPA_SPIN_SYNC", raising=False)
+    assert device.spin_sync(0) is None
+    monkeypatch.setenv("DPA_SPIN_SYNC", "1")
+    lib = device._loaded_hip()
+    rc = device.spin_sync(0)
+    if lib is None:  # a CPU-only torch build: no HIP runtime in the process
+        assert rc is None
+    else:
+        assert isinstance(rc, int)  # hipSuccess on a GPU box, an error code (no device) here
+    monkeypatch.setattr(device, "_loaded_hip", lambda: None)
+    assert device.spin_sync(0) is None
+
+
 def test_shared_gpu_env_one_hw_queue_from_three_ranks(monkeypatch):
     """--share-gpu: ranks get the fused-path gates, and from 3 ranks one HIP hardware queue
     per process (4 processes with 4 queues each stalled on one MI355X; profiles/r5v_*)."""
