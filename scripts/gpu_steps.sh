@@ -31,6 +31,7 @@
 #   xsbis_ab     the forced step's exchange cost bisected (experiment builds)
 #   xglds_ab     AMP gradient average with an LDS-only epoch broadcast (W=2 tests + forced A/B)
 #   bnu_ab       ResNet-50, BN rows in flight per lane 2 / 4 / 8
+#   rn_bw        ResNet-50 per-kernel HBM bytes (PMC) and achieved bandwidth
 #   smoke        __graft_entry__.smoke()
 #   gputests     the whole GPU test tier (as the driver runs it: world-8 rehearsals opt-in)
 set -o pipefail
@@ -97,6 +98,18 @@ step() {
     bnu_ab)  # ResNet-50: rows in flight per lane of the NHWC BatchNorm kernels (experiment builds)
       bash scripts/ab_bench.sh "$OUT/bnu_ab.txt" 2 "--model resnet50 --steps 100 --warmup 10 --no-baseline" u4=default \
         u2=ddp_practice_amd/_C_bnu2.so u8=ddp_practice_amd/_C_bnu8.so ;;
+    rn_bw)  # ResNet-50 per-kernel HBM traffic (PMC FETCH_SIZE / WRITE_SIZE, one pass each) and bandwidth
+      local RB="bench.py --model resnet50 --steps 3 --warmup 2 --no-graph --no-baseline"
+      timeout -k 10 -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/bw_f" -o run -- python3 $RB \
+        > "$OUT/bw_f.json" 2> "$OUT/bw_f.err" &&
+      timeout -k 10 -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/bw_w" -o run -- python3 $RB \
+        > "$OUT/bw_w.json" 2> "$OUT/bw_w.err" &&
+      timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d "$OUT/bw_t" -o run -- python3 $RB \
+        > "$OUT/bw_t.json" 2> "$OUT/bw_t.err" &&
+      python3 scripts/bw_table.py "$(find "$OUT/bw_f" -name '*counter_collection.csv' -print -quit)" \
+        "$(find "$OUT/bw_w" -name '*counter_collection.csv' -print -quit)" \
+        "$(find "$OUT/bw_t" -name '*kernel_trace.csv' -print -quit)" 45 > "$OUT/rn_bw.txt" &&
+      rm -rf "$OUT/bw_f" "$OUT/bw_w" "$OUT/bw_t" ;;
     spin_ab)  # busy-polled host waits (runtime/device.spin_sync) on the driver's command
       bash scripts/ab_bench.sh "$OUT/spin_ab.txt" 4 "--steps 20 --warmup 5" spin=env:DPA_SPIN_SYNC=1 yield=default ;;
     bn_nt_ab)  # ResNet-50: streaming (non-temporal) BN activation stores / loads (experiment builds)
