@@ -32,6 +32,7 @@
 #   xglds_ab     AMP gradient average with an LDS-only epoch broadcast (W=2 tests + forced A/B)
 #   bnu_ab       ResNet-50, BN rows in flight per lane 2 / 4 / 8
 #   rn_bw        ResNet-50 per-kernel HBM bytes (PMC) and achieved bandwidth
+#   rn_rehearse8 ResNet-50 DDP with 8 ranks sharing the card (torchrun, bs 16 per rank)
 #   smoke        __graft_entry__.smoke()
 #   gputests     the whole GPU test tier (as the driver runs it: world-8 rehearsals opt-in)
 set -o pipefail
@@ -110,6 +111,16 @@ step() {
         "$(find "$OUT/bw_w" -name '*counter_collection.csv' -print -quit)" \
         "$(find "$OUT/bw_t" -name '*kernel_trace.csv' -print -quit)" 45 > "$OUT/rn_bw.txt" &&
       rm -rf "$OUT/bw_f" "$OUT/bw_w" "$OUT/bw_t" ;;
+    rn_rehearse8)  # ResNet-50 DDP at world 8 on one card (torchrun, --share-gpu: 1/8 of the CUs per rank, bs 16)
+      PYTHONFAULTHANDLER=1 DPA_BENCH_WATCHDOG=90 timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+        --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 300)) bench.py --model resnet50 --gpus 8 --share-gpu \
+        --no-fallback --batch-size 16 --steps 10 --warmup 3 --no-baseline > "$OUT/rn_share_w8.json" \
+        2> "$OUT/rn_share_w8.err" ;;
+    rn_rehearse2)  # the same at world 2, Python stacks on a fatal signal (PYTHONFAULTHANDLER)
+      PYTHONFAULTHANDLER=1 DPA_BENCH_WATCHDOG=90 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 300)) bench.py --model resnet50 \
+        --gpus 2 --share-gpu --no-fallback --batch-size 16 --steps 10 --warmup 3 --no-baseline \
+        > "$OUT/rn_share_w2.json" 2> "$OUT/rn_share_w2.err" ;;
     spin_ab)  # busy-polled host waits (runtime/device.spin_sync) on the driver's command
       bash scripts/ab_bench.sh "$OUT/spin_ab.txt" 4 "--steps 20 --warmup 5" spin=env:DPA_SPIN_SYNC=1 yield=default ;;
     bn_nt_ab)  # ResNet-50: streaming (non-temporal) BN activation stores / loads (experiment builds)
