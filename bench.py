@@ -852,9 +852,13 @@ def bench_resnet(args) -> int:
         os.environ["DPA_COMM"] = args.comm
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = 0 if args.share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
-    if args.share_gpu:  # ranks share one device (one HW queue each at 3+: runtime/device.py)
+    if args.share_gpu:  # ranks share one device (runtime/device.py)
         from ddp_practice_amd.runtime.device import shared_cu_mask, shared_gpu_env
 
+        # 4 HIP queues per rank, not the one-queue default from 3 ranks: with one queue every
+        # rank segfaulted inside hipGraphLaunch at the first replay of the ResNet-50 step
+        # graph (profiles/r6ag_resnet50_share_w4_q1_segv.txt; 4 queues: r6ah, r6ai)
+        os.environ.setdefault("DPA_SHARED_HW_QUEUES", "4")
         shared_gpu_env(world)
         shared_cu_mask(world, int(os.environ.get("RANK", "0")))
     spin_rc = _spin_sync(torch, local_rank)

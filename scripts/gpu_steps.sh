@@ -121,6 +121,32 @@ step() {
         --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 300)) bench.py --model resnet50 \
         --gpus 2 --share-gpu --no-fallback --batch-size 16 --steps 10 --warmup 3 --no-baseline \
         > "$OUT/rn_share_w2.json" 2> "$OUT/rn_share_w2.err" ;;
+    rn_rehearse4s)  # world 4 on one card, eager and kernel-serialized (AMD_SERIALIZE_KERNEL=3): a fault is then
+      # reported at the launch that caused it
+      AMD_SERIALIZE_KERNEL=3 PYTHONFAULTHANDLER=1 DPA_BENCH_WATCHDOG=120 timeout -k 10 900 python -m torch.distributed.run \
+        --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 300)) bench.py \
+        --model resnet50 --gpus 4 --share-gpu --no-fallback --batch-size 16 --steps 4 --warmup 2 --no-baseline --no-graph \
+        > "$OUT/rn_share_w4s.json" 2> "$OUT/rn_share_w4s.err" ;;
+    rn_rehearse4)  # world 4 on one card, graph-captured as the bench runs it
+      PYTHONFAULTHANDLER=1 DPA_BENCH_WATCHDOG=120 timeout -k 10 900 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 4 --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 300)) bench.py --model resnet50 \
+        --gpus 4 --share-gpu --no-fallback --batch-size 16 --steps 10 --warmup 3 --no-baseline \
+        > "$OUT/rn_share_w4.json" 2> "$OUT/rn_share_w4.err" ;;
+    rn_rehearse4q)  # world 4 on one card, graph-captured, 4 HIP queues per rank (the 1-queue default from 3 ranks off)
+      DPA_SHARED_HW_QUEUES=4 PYTHONFAULTHANDLER=1 DPA_BENCH_WATCHDOG=120 timeout -k 10 900 python -m torch.distributed.run \
+        --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 300)) bench.py \
+        --model resnet50 --gpus 4 --share-gpu --no-fallback --batch-size 16 --steps 10 --warmup 3 --no-baseline \
+        > "$OUT/rn_share_w4q.json" 2> "$OUT/rn_share_w4q.err" ;;
+    rn_rehearse8q)  # world 8 on one card, graph-captured, 4 HIP queues per rank
+      DPA_SHARED_HW_QUEUES=4 PYTHONFAULTHANDLER=1 DPA_BENCH_WATCHDOG=120 timeout -k 10 900 python -m torch.distributed.run \
+        --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 300)) bench.py \
+        --model resnet50 --gpus 8 --share-gpu --no-fallback --batch-size 16 --steps 10 --warmup 3 --no-baseline \
+        > "$OUT/rn_share_w8q.json" 2> "$OUT/rn_share_w8q.err" ;;
+    rn_rehearse8e)  # world 8 on one card, eager (no graph)
+      PYTHONFAULTHANDLER=1 DPA_BENCH_WATCHDOG=120 timeout -k 10 900 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 8 --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 300)) bench.py --model resnet50 \
+        --gpus 8 --share-gpu --no-fallback --batch-size 16 --steps 4 --warmup 2 --no-baseline --no-graph \
+        > "$OUT/rn_share_w8e.json" 2> "$OUT/rn_share_w8e.err" ;;
     spin_ab)  # busy-polled host waits (runtime/device.spin_sync) on the driver's command
       bash scripts/ab_bench.sh "$OUT/spin_ab.txt" 4 "--steps 20 --warmup 5" spin=env:DPA_SPIN_SYNC=1 yield=default ;;
     bn_nt_ab)  # ResNet-50: streaming (non-temporal) BN activation stores / loads (experiment builds)
