@@ -245,3 +245,82 @@ def worker_poison(rank, world, port, q):
         q.close()
         q.join_thread()
         os._exit(0)
+
+
+def worker_resnet(rank, world, port, q):
+    """ResNet-50 (native bf16 kernels) with SyncBN under DDP over the xGMI engine, one
+    forward + backward on each rank's slice of a global batch: the DDP-averaged gradients
+    are bit-identical on every rank; the SyncBN statistics equal one process's on the
+    global batch; the gradients are as close to that process's as its own are to a run on
+    the same batch in another order (a random-init ResNet-50 in bf16 is chaotic: the BN
+    summation order alone moves its gradients by O(1), profiles/r6aq_resnet50_ddp_conditioning.txt);
+    then one SGD step keeps the ranks bit-identical."""
+    try:
+        from ._dist import client_env
+
+        os.environ.update(client_env(rank, world, port))
+        torch.cuda.set_device(0)
+        import ddp_practice_amd.distributed as dist
+        from ddp_practice_amd.models import resnet50
+        from ddp_practice_amd.ops.head import cross_entropy
+        from ddp_practice_amd.optim import SGD
+        from ddp_practice_amd.parallel import DistributedDataParallel, XgmiCommunicator, convert_sync_batchnorm
+
+        c = dist.init_process_group("xgmi")
+        assert isinstance(c, XgmiCommunicator)
+        per_rank = 4
+        torch.manual_seed(rank)  # different init per rank: DDP must broadcast rank 0's
+        model = convert_sync_batchnorm(resnet50(num_classes=10, amp_dtype=torch.bfloat16)).cuda()
+        ddp = DistributedDataParallel(model, device_ids=[0], gradient_as_bucket_view=True)
+        init = copy.deepcopy(ddp.module.state_dict())
+        g = torch.Generator().manual_seed(21)
+        hw = int(os.environ.get("DPA_TEST_IMG", "64"))
+        gx = torch.rand(per_rank * world, 3, hw, hw, generator=g).cuda()
+        gx += torch.arange(per_rank * world, device="cuda").div(per_rank, rounding_mode="floor").view(-1, 1, 1, 1)
+        # (rank r's images brighter by r: unsynchronised statistics would differ by tens of percent)
+        gy = torch.randint(0, 10, (per_rank * world,), generator=g).cuda()
+        sl = slice(rank * per_rank, (rank + 1) * per_rank)
+        cross_entropy(ddp(gx[sl]), gy[sl]).backward()
+        torch.cuda.synchronize()
+        assert c.async_error() == "", c.async_error()
+        bufs_after = {k: b.detach().clone() for k, b in ddp.module.named_buffers()}
+        grads = {k: p.grad.detach().clone() for k, p in ddp.module.named_parameters()}
+        res = {"grad_digest": _digest(grads)}
+        opt = SGD(ddp.module.parameters(), lr=0.01, momentum=0.9)
+        opt.step()
+        torch.cuda.synchronize()
+        res["digest"] = _digest(ddp.module.state_dict())
+        if rank == 0:
+            def run(order):
+                m = resnet50(num_classes=10, amp_dtype=torch.bfloat16).cuda()  # plain BN, one process
+                m.load_state_dict(init)
+                cross_entropy(m(gx[order]), gy[order]).backward()
+                return m
+
+            def rel(a, b):
+                return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-30)).item()
+
+            med = lambda d: sorted(d.values())[len(d) // 2]  # noqa: E731
+            one = run(torch.arange(per_rank * world).cuda())
+            two = run(torch.cat([torch.arange(per_rank, per_rank * world), torch.arange(per_rank)]).cuda())
+            gone, gtwo = dict(one.named_parameters()), dict(two.named_parameters())
+            errs = {k: rel(grads[k], p.grad) for k, p in gone.items() if p.grad.norm() > 0}
+            spread = {k: rel(gtwo[k].grad, p.grad) for k, p in gone.items() if p.grad.norm() > 0}
+            # SyncBN statistics: the running-statistics update of the stem BN and layer1 (before the
+            # chaos builds up) vs the single process's
+            berr = {}
+            for k, b in one.named_buffers():
+                if b.dtype.is_floating_point and k.startswith(("bn1.", "layer1.")):
+                    d = b.float() - init[k].float()
+                    berr[k] = rel(bufs_after[k].float() - init[k].float(), d)
+            res.update(grad_err_median=med(errs), spread_median=med(spread), stat_err_max=max(berr.values()))
+            assert max(berr.values()) < 2e-3, sorted(berr.items(), key=lambda t: -t[1])[:5]
+            assert med(errs) < 1.5 * med(spread) + 0.05, (med(errs), med(spread))
+        dist.destroy_process_group()
+        q.put((rank, "ok", res))
+    except Exception:  # pragma: no cover - reported to the parent
+        q.put((rank, "err", traceback.format_exc()))
+    finally:
+        q.close()
+        q.join_thread()
+        os._exit(0)
