@@ -33,6 +33,7 @@
 #   bnu_ab       ResNet-50, BN rows in flight per lane 2 / 4 / 8
 #   rn_bw        ResNet-50 per-kernel HBM bytes (PMC) and achieved bandwidth
 #   rn_rehearse8 ResNet-50 DDP with 8 ranks sharing the card (torchrun, bs 16 per rank)
+#   lpdyn_ab     bf16 conv2 backward tiles in dynamic LDS (tests + A/B)
 #   smoke        __graft_entry__.smoke()
 #   gputests     the whole GPU test tier (as the driver runs it: world-8 rehearsals opt-in)
 set -o pipefail
@@ -147,6 +148,16 @@ step() {
         --nproc-per-node 8 --master-addr 127.0.0.1 --master-port $((29600 + RANDOM % 300)) bench.py --model resnet50 \
         --gpus 8 --share-gpu --no-fallback --batch-size 16 --steps 4 --warmup 2 --no-baseline --no-graph \
         > "$OUT/rn_share_w8e.json" 2> "$OUT/rn_share_w8e.err" ;;
+    lpdyn_ab)  # bf16 conv2 backward with the roles' tiles in dynamic LDS (DPA_LP_DYN_BWD=1): tests, then A/B
+      DPA_LP_DYN_BWD=1 timeout -k 10 300 $PYT --timeout 120 -p no:cacheprovider tests/test_convnet_fused_gpu.py \
+        -k "fwd_bwd or bitwise or slab_sink or prechecked" > "$OUT/lpdyn_tests.txt" 2>&1 &&
+      bash scripts/ab_bench.sh "$OUT/lpdyn_ab.txt" 3 "--steps 2000 --warmup 50 --no-baseline --epochs 0 --no-steady \
+--extra-dtypes ," static=env:DPA_LP_DYN_BWD=0 dyn=default ;;
+    lpdyn_ab2)  # the same A/B, more rounds, plain and forced (in-kernel exchange sites)
+      bash scripts/ab_bench.sh "$OUT/lpdyn_ab2.txt" 5 "--steps 2000 --warmup 50 --no-baseline --epochs 0 --no-steady \
+--extra-dtypes ," static=env:DPA_LP_DYN_BWD=0 dyn=default &&
+      bash scripts/ab_bench.sh "$OUT/lpdyn_ab2.txt" 3 "--force-collectives --steps 2000 --warmup 50 --no-baseline \
+--epochs 0 --no-steady --extra-dtypes ," static=env:DPA_LP_DYN_BWD=0 dyn=default ;;
     spin_ab)  # busy-polled host waits (runtime/device.spin_sync) on the driver's command
       bash scripts/ab_bench.sh "$OUT/spin_ab.txt" 4 "--steps 20 --warmup 5" spin=env:DPA_SPIN_SYNC=1 yield=default ;;
     bn_nt_ab)  # ResNet-50: streaming (non-temporal) BN activation stores / loads (experiment builds)
