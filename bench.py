@@ -401,6 +401,18 @@ class _Chunks:
         the device runs the previous one.  DPA_BENCH_LEAD=0: remainder first, no lead step."""
         if n <= 0:
             return []
+        if self.spg > 1 and os.environ.get("DPA_BENCH_PLAN") == "geo":
+            # A/B: 1, 2, 4, ... steps per graph (capped at spg), each next graph submitted while
+            # the device runs the previous one: no gain -- the device span of the 20-step window
+            # is already 20 steady steps; the fixed cost is launch / sync latency outside it
+            # (profiles/r6av_window_plan_ab.txt)
+            plan, k, left = [], 1, n
+            while left > 0:
+                c = min(k, self.spg, left)
+                plan.append(c)
+                left -= c
+                k *= 2
+            return plan
         lead = 1 if (self.spg > 1 and os.environ.get("DPA_BENCH_LEAD") != "0") else 0
         m = n - lead
         plan = [lead] if lead else []

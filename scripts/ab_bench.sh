@@ -19,7 +19,8 @@ for r in $(seq 1 "$ROUNDS"); do
     elif [ "${so#env:}" != "$so" ]; then unset DPA_EXT_SO; envs=("${so#env:}")  # label=env:VAR=VAL
     else export DPA_EXT_SO=$so; fi
     line=$(env "${envs[@]}" timeout -k 10 300 python bench.py $ARGS 2> "$OUT.$label.err") || { echo "$label failed" >> "$OUT"; tail -20 "$OUT.$label.err"; exit 1; }
-    echo "$label $r $(echo "$line" | grep -o '"ms_per_step": [0-9.]*' | head -1)" >> "$OUT"
+    ev=$(grep -m1 '^\[bench\] [0-9]* steps: wall' "$OUT.$label.err" || true)  # DPA_BENCH_EVENTS=1 runs
+    echo "$label $r $(echo "$line" | grep -o '"ms_per_step": [0-9.]*' | head -1) $ev" >> "$OUT"
   done
 done
 unset DPA_EXT_SO

@@ -34,6 +34,7 @@
 #   rn_bw        ResNet-50 per-kernel HBM bytes (PMC) and achieved bandwidth
 #   rn_rehearse8 ResNet-50 DDP with 8 ranks sharing the card (torchrun, bs 16 per rank)
 #   lpdyn_ab     bf16 conv2 backward tiles in dynamic LDS (tests + A/B)
+#   plan_ab      driver window: lead + remainder graphs vs geometric graph sizes
 #   smoke        __graft_entry__.smoke()
 #   gputests     the whole GPU test tier (as the driver runs it: world-8 rehearsals opt-in)
 set -o pipefail
@@ -158,6 +159,9 @@ step() {
 --extra-dtypes ," static=env:DPA_LP_DYN_BWD=0 dyn=default &&
       bash scripts/ab_bench.sh "$OUT/lpdyn_ab2.txt" 3 "--force-collectives --steps 2000 --warmup 50 --no-baseline \
 --epochs 0 --no-steady --extra-dtypes ," static=env:DPA_LP_DYN_BWD=0 dyn=default ;;
+    plan_ab)  # the driver's 20-step window: lead graph + remainder (default) vs geometric graph sizes 1, 2, 4, ...
+      DPA_BENCH_EVENTS=1 bash scripts/ab_bench.sh "$OUT/plan_ab.txt" 4 "--steps 20 --warmup 5" lead=default \
+        geo=env:DPA_BENCH_PLAN=geo ;;
     spin_ab)  # busy-polled host waits (runtime/device.spin_sync) on the driver's command
       bash scripts/ab_bench.sh "$OUT/spin_ab.txt" 4 "--steps 20 --warmup 5" spin=env:DPA_SPIN_SYNC=1 yield=default ;;
     bn_nt_ab)  # ResNet-50: streaming (non-temporal) BN activation stores / loads (experiment builds)
