@@ -29,8 +29,13 @@ def starts_line(name, rows):
     q = [st[int(i * (n - 1) / 8)].item() for i in range(9)]
     srt = st.sort().values
     qs = [srt[int(i * (n - 1) / 8)].item() for i in range(9)]
+    # the hardware deals workgroup i to XCD i % 8: mean start per XCD (a consistent late XCD
+    # would be worth giving the least work)
+    bx = torch.arange(n) % 8
+    xcd = [st[bx == x].mean().item() if (bx == x).any() else float("nan") for x in range(8)]
     return (f"{name:18s} start by block index (every n/8-th): " + " ".join(f"{v:4.2f}" for v in q) +
-            " | sorted quantiles: " + " ".join(f"{v:4.2f}" for v in qs))
+            " | sorted quantiles: " + " ".join(f"{v:4.2f}" for v in qs) +
+            " | mean by XCD: " + " ".join(f"{v:4.2f}" for v in xcd))
 
 
 def summarize(name, rows):
