@@ -162,6 +162,11 @@ step() {
     plan_ab)  # the driver's 20-step window: lead graph + remainder (default) vs geometric graph sizes 1, 2, 4, ...
       DPA_BENCH_EVENTS=1 bash scripts/ab_bench.sh "$OUT/plan_ab.txt" 4 "--steps 20 --warmup 5" lead=default \
         geo=env:DPA_BENCH_PLAN=geo ;;
+    dg4_ab)  # conv2 data gradient at 4 workgroups per image with the dynamic-LDS backward (experiment build)
+      timeout -k 10 300 env DPA_EXT_SO=$PWD/ddp_practice_amd/_C_dg4.so $PYT --timeout 120 -p no:cacheprovider \
+        tests/test_convnet_fused_gpu.py -k "fwd_bwd or bitwise" > "$OUT/dg4_tests.txt" 2>&1 &&
+      bash scripts/ab_bench.sh "$OUT/dg4_ab.txt" 4 "--steps 2000 --warmup 50 --no-baseline --epochs 0 --no-steady \
+--extra-dtypes ," dg2=default dg4=ddp_practice_amd/_C_dg4.so ;;
     spin_ab)  # busy-polled host waits (runtime/device.spin_sync) on the driver's command
       bash scripts/ab_bench.sh "$OUT/spin_ab.txt" 4 "--steps 20 --warmup 5" spin=env:DPA_SPIN_SYNC=1 yield=default ;;
     bn_nt_ab)  # ResNet-50: streaming (non-temporal) BN activation stores / loads (experiment builds)
