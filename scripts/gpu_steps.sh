@@ -35,6 +35,13 @@
 #   rn_rehearse8 ResNet-50 DDP with 8 ranks sharing the card (torchrun, bs 16 per rank)
 #   lpdyn_ab     bf16 conv2 backward tiles in dynamic LDS (tests + A/B)
 #   plan_ab      driver window: lead + remainder graphs vs geometric graph sizes
+#   fp32diag     per-key fp32 slab-sink vs separate-launch training (scripts/exp/fp32_sink_diff.py)
+#   rn_rehearse2 / rn_rehearse4 / rn_rehearse4s / rn_rehearse4q / rn_rehearse8q / rn_rehearse8e
+#                ResNet-50 DDP under torchrun sharing the card: world 2, 4 (graphs / serialized eager /
+#                4 queues), 8 (4 queues / eager)
+#   lpdyn_ab2    the same A/B as lpdyn_ab, more rounds, plain and forced
+#   dg4_ab       conv2 data gradient at 4 workgroups per image (experiment build _C_dg4.so)
+#   rtenv_ab     HIP runtime knobs (HIP_FORCE_DEV_KERNARG, DEBUG_CLR_GRAPH_PACKET_CAPTURE) on the driver command
 #   smoke        __graft_entry__.smoke()
 #   gputests     the whole GPU test tier (as the driver runs it: world-8 rehearsals opt-in)
 set -o pipefail
@@ -167,6 +174,9 @@ step() {
         tests/test_convnet_fused_gpu.py -k "fwd_bwd or bitwise" > "$OUT/dg4_tests.txt" 2>&1 &&
       bash scripts/ab_bench.sh "$OUT/dg4_ab.txt" 4 "--steps 2000 --warmup 50 --no-baseline --epochs 0 --no-steady \
 --extra-dtypes ," dg2=default dg4=ddp_practice_amd/_C_dg4.so ;;
+    rtenv_ab)  # HIP runtime knobs on the driver's command: kernel arguments in device memory, graph packet capture
+      bash scripts/ab_bench.sh "$OUT/rtenv_ab.txt" 3 "--steps 20 --warmup 5 --no-baseline --epochs 0 --extra-dtypes ," \
+        base=default kd1=env:HIP_FORCE_DEV_KERNARG=1 kd0=env:HIP_FORCE_DEV_KERNARG=0 gpc0=env:DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 ;;
     spin_ab)  # busy-polled host waits (runtime/device.spin_sync) on the driver's command
       bash scripts/ab_bench.sh "$OUT/spin_ab.txt" 4 "--steps 20 --warmup 5" spin=env:DPA_SPIN_SYNC=1 yield=default ;;
     bn_nt_ab)  # ResNet-50: streaming (non-temporal) BN activation stores / loads (experiment builds)
