@@ -60,7 +60,8 @@ _WGRAD1_SLAB2 = os.environ.get("DPA_WGRAD1_SLAB2", "0") == "1"
 # measured no faster than the two launches it merges (54.2-54.6 vs 54.1-54.2 us/step,
 # profiles/r4h_defer_wgrad1_ab.txt): the in-launch producer -> slab-owner hand-off (write-
 # through rows, arrival counter, polling) costs ~3 us, more than the kernel boundary it
-# removes.  Opt-in: DPA_DEFER_WGRAD1=1
+# removes; round 6, with the pre-checked step it gives up: 0.0516 vs 0.0482 ms
+# (profiles/r6az_defer_wgrad1_ab.txt).  Opt-in: DPA_DEFER_WGRAD1=1
 _DEFER_WGRAD1 = os.environ.get("DPA_DEFER_WGRAD1", "0") == "1"
 # producer-side gradient checks instead of the fused AMP step's grid barrier (single rank);
 # DPA_PRECHECK=0: the barrier (A/B runs)

@@ -41,6 +41,7 @@
 #                4 queues), 8 (4 queues / eager)
 #   lpdyn_ab2    the same A/B as lpdyn_ab, more rounds, plain and forced
 #   dg4_ab       conv2 data gradient at 4 workgroups per image (experiment build _C_dg4.so)
+#   defer_ab     conv1 weight gradient inside the optimizer launch (DPA_DEFER_WGRAD1=1) vs as built
 #   rtenv_ab     HIP runtime knobs (HIP_FORCE_DEV_KERNARG, DEBUG_CLR_GRAPH_PACKET_CAPTURE) on the driver command
 #   smoke        __graft_entry__.smoke()
 #   gputests     the whole GPU test tier (as the driver runs it: world-8 rehearsals opt-in)
@@ -177,6 +178,9 @@ step() {
     rtenv_ab)  # HIP runtime knobs on the driver's command: kernel arguments in device memory, graph packet capture
       bash scripts/ab_bench.sh "$OUT/rtenv_ab.txt" 3 "--steps 20 --warmup 5 --no-baseline --epochs 0 --extra-dtypes ," \
         base=default kd1=env:HIP_FORCE_DEV_KERNARG=1 kd0=env:HIP_FORCE_DEV_KERNARG=0 gpc0=env:DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 ;;
+    defer_ab)  # conv1 weight gradient deferred into the optimizer's launch (DPA_DEFER_WGRAD1=1) vs as built
+      bash scripts/ab_bench.sh "$OUT/defer_ab.txt" 3 "--steps 2000 --warmup 50 --no-baseline --epochs 0 --no-steady \
+--extra-dtypes ," base=default defer=env:DPA_DEFER_WGRAD1=1 ;;
     spin_ab)  # busy-polled host waits (runtime/device.spin_sync) on the driver's command
       bash scripts/ab_bench.sh "$OUT/spin_ab.txt" 4 "--steps 20 --warmup 5" spin=env:DPA_SPIN_SYNC=1 yield=default ;;
     bn_nt_ab)  # ResNet-50: streaming (non-temporal) BN activation stores / loads (experiment builds)
