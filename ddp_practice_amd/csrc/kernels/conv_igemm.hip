@@ -2081,9 +2081,9 @@ int64_t wgrad_splits(int64_t M, int64_t K, int64_t C, int64_t R, int64_t S) {
     const char* e = std::getenv("DPA_WGRAD_BLOCKS");
     return e != nullptr ? std::atoll(e) : 512LL;  // ResNet-50 sweep: 384 15.01, 512 14.50, 768 14.59, 1024 14.67 ms
   }();
-  static const int64_t minpix = [] {
-    const char* e = std::getenv("DPA_WGRAD_MINPIX");
-    return e != nullptr ? std::atoll(e) : 1024LL;
+  static const int64_t minpix = [] {  // round 6 re-sweep: 1024 13.81, 512 13.73, 384 13.74, 256 13.72 ms
+    const char* e = std::getenv("DPA_WGRAD_MINPIX");    // (profiles/r6bb_rn_wgrad_minpix.txt)
+    return e != nullptr ? std::atoll(e) : 512LL;
   }();
   int64_t sp = std::max<int64_t>(1, target / tiles);
   sp = std::min<int64_t>(sp, std::max<int64_t>(1, M / minpix));

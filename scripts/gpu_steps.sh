@@ -42,6 +42,7 @@
 #   lpdyn_ab2    the same A/B as lpdyn_ab, more rounds, plain and forced
 #   dg4_ab       conv2 data gradient at 4 workgroups per image (experiment build _C_dg4.so)
 #   defer_ab     conv1 weight gradient inside the optimizer launch (DPA_DEFER_WGRAD1=1) vs as built
+#   rn_knobs     ResNet-50 conv tuning knobs re-swept (wgrad blocks / min pixels, 1x1 pixel tile, stats defer)
 #   rtenv_ab     HIP runtime knobs (HIP_FORCE_DEV_KERNARG, DEBUG_CLR_GRAPH_PACKET_CAPTURE) on the driver command
 #   smoke        __graft_entry__.smoke()
 #   gputests     the whole GPU test tier (as the driver runs it: world-8 rehearsals opt-in)
@@ -181,6 +182,13 @@ step() {
     defer_ab)  # conv1 weight gradient deferred into the optimizer's launch (DPA_DEFER_WGRAD1=1) vs as built
       bash scripts/ab_bench.sh "$OUT/defer_ab.txt" 3 "--steps 2000 --warmup 50 --no-baseline --epochs 0 --no-steady \
 --extra-dtypes ," base=default defer=env:DPA_DEFER_WGRAD1=1 ;;
+    rn_knobs)  # ResNet-50: re-sweep of the conv tuning knobs on this tree
+      bash scripts/ab_bench.sh "$OUT/rn_knobs.txt" 2 "--model resnet50 --steps 100 --warmup 10 --no-baseline" base=default \
+        wb384=env:DPA_WGRAD_BLOCKS=384 wb768=env:DPA_WGRAD_BLOCKS=768 mp512=env:DPA_WGRAD_MINPIX=512 \
+        mp2048=env:DPA_WGRAD_MINPIX=2048 bp128=env:DPA_G1X1_BP=128 nodefer=env:DPA_STAT_DEFER_MIN=-1 ;;
+    rn_minpix)  # ResNet-50: weight-gradient split floor (pixels per split) 1024 / 512 / 384 / 256
+      bash scripts/ab_bench.sh "$OUT/rn_minpix.txt" 3 "--model resnet50 --steps 100 --warmup 10 --no-baseline" \
+        mp1024=env:DPA_WGRAD_MINPIX=1024 mp512=default mp384=env:DPA_WGRAD_MINPIX=384 mp256=env:DPA_WGRAD_MINPIX=256 ;;
     spin_ab)  # busy-polled host waits (runtime/device.spin_sync) on the driver's command
       bash scripts/ab_bench.sh "$OUT/spin_ab.txt" 4 "--steps 20 --warmup 5" spin=env:DPA_SPIN_SYNC=1 yield=default ;;
     bn_nt_ab)  # ResNet-50: streaming (non-temporal) BN activation stores / loads (experiment builds)
