@@ -189,6 +189,10 @@ step() {
     rn_minpix)  # ResNet-50: weight-gradient split floor (pixels per split) 1024 / 512 / 384 / 256
       bash scripts/ab_bench.sh "$OUT/rn_minpix.txt" 3 "--model resnet50 --steps 100 --warmup 10 --no-baseline" \
         mp1024=env:DPA_WGRAD_MINPIX=1024 mp512=default mp384=env:DPA_WGRAD_MINPIX=384 mp256=env:DPA_WGRAD_MINPIX=256 ;;
+    rn_knobs2)  # ResNet-50: 64-channel tiles for small grids, wide-tile modes
+      bash scripts/ab_bench.sh "$OUT/rn_knobs2.txt" 2 "--model resnet50 --steps 100 --warmup 10 --no-baseline" base=default \
+        b64_256=env:DPA_G1X1_BN64_BELOW=256 b64_512=env:DPA_G1X1_BN64_BELOW=512 b64_1024=env:DPA_G1X1_BN64_BELOW=1024 \
+        wide0=env:DPA_WIDE=0 wide2=env:DPA_WIDE=2 ;;
     spin_ab)  # busy-polled host waits (runtime/device.spin_sync) on the driver's command
       bash scripts/ab_bench.sh "$OUT/spin_ab.txt" 4 "--steps 20 --warmup 5" spin=env:DPA_SPIN_SYNC=1 yield=default ;;
     bn_nt_ab)  # ResNet-50: streaming (non-temporal) BN activation stores / loads (experiment builds)
