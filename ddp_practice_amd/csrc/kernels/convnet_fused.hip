@@ -454,11 +454,20 @@ void conv1_fwd_pack_gather(at::Tensor x, at::Tensor w1, at::Tensor b1, at::Tenso
   DPA_CHECK_LAUNCH();
 }
 
+// Workgroups per image of the conv2 data gradient: 2 for bf16 / fp16 (4: +2.5 us,
+// profiles/r6m_split_ab.txt, r6ax_*), 4 for fp32, whose 16x16x4 MFMA chains are 4x as long
+// (profiles/r6bf_fp32_dgrad_split_ab.txt).  Compile-time per dtype: the kernels take it as a
+// constant (kDgradSplitT<T>), the host sizes follow from the tensor dtype (dgrad_split).
 #ifndef DPA_DGRAD2_SPLIT
-#define DPA_DGRAD2_SPLIT 2  // workgroups per image of the conv2 data gradient (-DDPA_DGRAD2_SPLIT=4)
+#define DPA_DGRAD2_SPLIT 2
 #endif
-constexpr int kDgradSplit = DPA_DGRAD2_SPLIT;
-int64_t dgrad2_rows(int64_t B) { return B * kDgradSplit; }
+#ifndef DPA_DGRAD2_SPLIT_F32
+#define DPA_DGRAD2_SPLIT_F32 4
+#endif
+template <typename T>
+constexpr int kDgradSplitT = std::is_same<T, float>::value ? DPA_DGRAD2_SPLIT_F32 : DPA_DGRAD2_SPLIT;
+static int dgrad_split(bool fp32) { return fp32 ? DPA_DGRAD2_SPLIT_F32 : DPA_DGRAD2_SPLIT; }
+int64_t dgrad2_rows(int64_t B, bool fp32) { return B * dgrad_split(fp32); }
 
 // [pool2/ReLU2/BN2 backward] -> conv2 data grad -> dp1 (+ BN1 partial sums rows).
 void conv2_dgrad(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx2, at::Tensor fstats2,
@@ -470,23 +479,24 @@ void conv2_dgrad(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx
   const int B = (int)y2.size(0);
   TORCH_CHECK(y2.size(1) == 32 && y2.size(2) == 14 && dp2.numel() == (int64_t)B * 32 * 49);
   TORCH_CHECK(dp1.numel() == (int64_t)B * 16 * 196 && idx1.numel() == dp1.numel() && xh1.numel() == dp1.numel());
-  TORCH_CHECK(bslab1.numel() == dgrad2_rows(B) * 32, "BN1 partial-sum slab size");
+  TORCH_CHECK(bslab1.numel() == dgrad2_rows(B, y2.scalar_type() == at::kFloat) * 32, "BN1 partial-sum slab size");
   if (B == 0) return;
   with_t(dt_of(y2), [&](auto tag) {
     typedef decltype(tag) T;
+    constexpr int ds = kDgradSplitT<T>;
     BwdIn<T> bi = bwd_in<T>(dp2, idx2, y2, fstats2, gsum2, c10::nullopt, g2, eps2, 32, c10::nullopt, c10::nullopt);
     bi.xs = site_of(xc, xgmi::kSiteBwd2Dgrad);
-    xgmi::set_site_grid(bi.xs, B * kDgradSplit, "conv2_dgrad");
+    xgmi::set_site_grid(bi.xs, B * ds, "conv2_dgrad");
     BwdEpi<T> ep{idx1.data_ptr<uint8_t>(), dptr<T>(xh1), bslab1.data_ptr<float>()};
-    hipLaunchKernelGGL((cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1, 1>), dim3(B * kDgradSplit), dim3(cb::NTHR),
+    hipLaunchKernelGGL((cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1, 1>), dim3(B * ds), dim3(cb::NTHR),
                        0, cur_stream(), nullptr, nullptr, nullptr, dptr<T>(dp1), nullptr, nullptr, nullptr,
-                       kDgradSplit, PoolIn<T>{}, bi, ep, dptr<T>(wpk_d), cb::WPack<T>{});
+                       ds, PoolIn<T>{}, bi, ep, dptr<T>(wpk_d), cb::WPack<T>{});
   });
   DPA_CHECK_LAUNCH();
 }
 
 // The backward through [BN2 -> ReLU2 -> pool2] feeds two independent products of
-// layer 2: the data grad (-> dp1 + BN1 partial sums, kDgradSplit workgroups per
+// layer 2: the data grad (-> dp1 + BN1 partial sums, kDgradSplitT<T> workgroups per
 // image) and the weight-grad partials (WG2_ROWS-row chunks).  One launch hosts
 // both roles -- workgroups [0, ndg) the data grad, [ndg, grid) the weight grad --
 // so they overlap on the chip instead of running back to back (each alone fills
@@ -580,7 +590,7 @@ conv2_bwd_kernel(const T* __restrict__ wpk_d, T* __restrict__ dp1, BwdIn<T> bi_d
   const int bid = (int)blockIdx.x;
   if (bid < ndg)
     cb::conv5x5_body<T, 32, 16, 14, 14, 2, 2, 1, 1>(nullptr, nullptr, nullptr, dp1, nullptr, nullptr, nullptr,
-                                                    kDgradSplit, PoolIn<T>{}, bi_d, ep, wpk_d, cb::WPack<T>{}, bid);
+                                                    kDgradSplitT<T>, PoolIn<T>{}, bi_d, ep, wpk_d, cb::WPack<T>{}, bid);
   else if (bid < ndg + nwg)
     cb::conv5x5_wgrad_body<T, 16, 32, 14, 14, WG2_ROWS_, 2>(p1, nullptr, wslab2, nsw, bi_w, bid - ndg);
   else
@@ -602,7 +612,7 @@ conv2_bwd_dyn_kernel(const T* __restrict__ wpk_d, T* __restrict__ dp1, BwdIn<T> 
   const int bid = (int)blockIdx.x;
   if (bid < ndg)
     cb::conv5x5_body<T, 32, 16, 14, 14, 2, 2, 1, 1, true>(nullptr, nullptr, nullptr, dp1, nullptr, nullptr, nullptr,
-                                                          kDgradSplit, PoolIn<T>{}, bi_d, ep, wpk_d,
+                                                          kDgradSplitT<T>, PoolIn<T>{}, bi_d, ep, wpk_d,
                                                           cb::WPack<T>{}, bid);
   else if (bid < ndg + nwg)
     cb::conv5x5_wgrad_body<T, 16, 32, 14, 14, WG2_ROWS_, 2, false, false, true>(p1, nullptr, wslab2, nsw, bi_w,
@@ -723,11 +733,11 @@ void conv2_bwd(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx2,
   TORCH_CHECK(y2.size(1) == 32 && y2.size(2) == 14 && dp2.numel() == (int64_t)B * 32 * 49);
   TORCH_CHECK(dp1.numel() == (int64_t)B * 16 * 196 && idx1.numel() == dp1.numel() && xh1.numel() == dp1.numel());
   TORCH_CHECK(p1.numel() == dp1.numel() && p1.scalar_type() == y2.scalar_type());
-  TORCH_CHECK(bslab1.numel() == dgrad2_rows(B) * 32, "BN1 partial-sum slab size");
+  TORCH_CHECK(bslab1.numel() == dgrad2_rows(B, y2.scalar_type() == at::kFloat) * 32, "BN1 partial-sum slab size");
   TORCH_CHECK(dg2.has_value() == dbe2.has_value(), "conv2_bwd: dg2 and dbe2 go together");
   if (dg2.has_value()) TORCH_CHECK(dg2->numel() == 32 && dbe2->numel() == 32 && dg2->scalar_type() == at::kFloat);
   if (xc) TORCH_CHECK(!lsum2.has_value(), "fused SyncBN exchange: gsum2 must be this rank's rows (no lsum2)");
-  const int ndg = B * kDgradSplit, nwg = (int)wgrad_bn_rows(2, B);
+  const int ndg = B * dgrad_split(y2.scalar_type() == at::kFloat), nwg = (int)wgrad_bn_rows(2, B);
   TORCH_CHECK(wslab2.numel() == (int64_t)nwg * (32 * 400 + 32), "wgrad slab size");
   if (B == 0) return;
   with_t(dt_of(y2), [&](auto tag) {
@@ -760,7 +770,7 @@ void conv2_bwd(at::Tensor wpk_d, at::Tensor y2, at::Tensor dp2, at::Tensor idx2,
       bd.xs.nblk = 0;  // the data-gradient launch is its site's whole grid (ndg: checked above)
       hipLaunchKernelGGL((cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1, 1>), dim3(ndg), dim3(cb::NTHR), 0,
                          cur_stream(), nullptr, nullptr, nullptr, dptr<T>(dp1), nullptr, nullptr, nullptr,
-                         kDgradSplit, PoolIn<T>{}, bd, ep, dptr<T>(wpk_d), cb::WPack<T>{});
+                         kDgradSplitT<T>, PoolIn<T>{}, bd, ep, dptr<T>(wpk_d), cb::WPack<T>{});
       hipLaunchKernelGGL(conv2_wgrad_fc_kernel<T>, dim3(nwg + nfc), dim3(cb::NTHR), 0, cur_stream(), dptr<T>(p1),
                          wslab2.data_ptr<float>(), bw, nwg, fw);
     } else if (lp_dyn_bwd()) {  // the roles' tiles in dynamic LDS (the largest role's bytes)
@@ -1158,7 +1168,8 @@ bool sites_resident(int64_t B, at::ScalarType st) {
   // every site launch must also fit its site's epoch words (comm/xgmi.h set_site_grid):
   // the conv1 weight gradient's 7 B workgroups pass kEpochWords at B >= 74
   bool ok = xgmi::site_grid_fits(wgrad_bn_rows(1, B)) && xgmi::site_grid_fits(wgrad_bn_rows(2, B)) &&
-            xgmi::site_grid_fits(B * kDgradSplit) && xgmi::site_grid_fits(fwd2_split(st == at::kFloat) * B);
+            xgmi::site_grid_fits(B * dgrad_split(st == at::kFloat)) &&
+            xgmi::site_grid_fits(fwd2_split(st == at::kFloat) * B);
   auto chk = [&](const void* k, int64_t grid) { ok = ok && co_resident(k, (int)grid, cb::NTHR, 0); };
   with_t(dt_of(at::empty({0}, at::TensorOptions().dtype(st))), [&](auto tag) {
     typedef decltype(tag) T;
@@ -1166,17 +1177,17 @@ bool sites_resident(int64_t B, at::ScalarType st) {
         B * fwd2_split(std::is_same<T, float>::value));
     ok = ok && co_resident(reinterpret_cast<const void*>(&head_fwd_kernel<T, 32, 14, 14, 16>), (int)B, HF, 0) &&
          co_resident(reinterpret_cast<const void*>(&head_fwd_kernel<T, 32, 14, 14, 64>), (int)B, HF, 0);
-    chk(reinterpret_cast<const void*>(&cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1, 1>), B * kDgradSplit);
+    chk(reinterpret_cast<const void*>(&cb::conv5x5_kernel<T, 32, 16, 14, 14, 2, 2, 1, 1>), B * kDgradSplitT<T>);
     if constexpr (!std::is_same<T, float>::value) {
       if (lp_dyn_bwd())
         ok = ok && co_resident(reinterpret_cast<const void*>(&conv2_bwd_dyn_kernel<T>),
-                               (int)(B * kDgradSplit + wgrad_bn_rows(2, B) + FC_BLOCKS), cb::NTHR,
+                               (int)(B * kDgradSplitT<T> + wgrad_bn_rows(2, B) + FC_BLOCKS), cb::NTHR,
                                conv2_bwd_dyn_bytes<T>());
       else
-        chk(reinterpret_cast<const void*>(&conv2_bwd_kernel<T>), B * kDgradSplit + wgrad_bn_rows(2, B) + FC_BLOCKS);
+        chk(reinterpret_cast<const void*>(&conv2_bwd_kernel<T>), B * kDgradSplitT<T> + wgrad_bn_rows(2, B) + FC_BLOCKS);
     } else if (fp32_merged_bwd())
       ok = ok && co_resident(reinterpret_cast<const void*>(&conv2_bwd_dyn_kernel<T>),
-                             (int)(B * kDgradSplit + wgrad_bn_rows(2, B) + FC_BLOCKS), cb::NTHR,
+                             (int)(B * kDgradSplitT<T> + wgrad_bn_rows(2, B) + FC_BLOCKS), cb::NTHR,
                              conv2_bwd_dyn_bytes<T>());
     chk(reinterpret_cast<const void*>(&cb::conv5x5_wgrad_kernel<T, 16, 32, 14, 14, WG2_ROWS, 2>),
         wgrad_bn_rows(2, B));
@@ -1197,7 +1208,7 @@ void register_convnet_fused(pybind11::module& m) {
   s.def("head_fwd", &cnf::head_fwd);
   s.def("head_bwd", &cnf::head_bwd);
   s.def("head_bwd_lds", &cnf::head_bwd_lds);
-  s.def("dgrad2_rows", &cnf::dgrad2_rows);
+  s.def("dgrad2_rows", &cnf::dgrad2_rows, py::arg("B"), py::arg("fp32") = false);
   s.def("conv1_fwd_pack", &cnf::conv1_fwd_pack);
   s.def("conv1_fwd_pack_gather", &cnf::conv1_fwd_pack_gather);
 #ifdef DPA_TIMING

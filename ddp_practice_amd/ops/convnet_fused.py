@@ -318,7 +318,7 @@ class ConvNetFn(torch.autograd.Function):
         # 2+3. BN2 bwd -> {conv2 dgrad -> dp1 (+ BN1 partial sums), conv2 wgrad partials}: one launch
         #      (DPA_SPLIT_BWD2=1: the two as separate launches, A/B runs)
         dp1 = torch.empty((B, 16, 14, 14), dtype=y1.dtype, device=dev)
-        bslab1 = torch.empty(cn.dgrad2_rows(B) * 32, **f32)
+        bslab1 = torch.empty(cn.dgrad2_rows(B, y1.dtype == torch.float32) * 32, **f32)
         wslab2 = torch.empty(cn.wgrad_bn_rows(2, B) * (n_w2 + 32), **f32)
         if _SPLIT_BWD2:
             if dgb[0] is not None:  # the BN2 parameter grads from the rows (this rank's)

@@ -41,6 +41,7 @@
 #                4 queues), 8 (4 queues / eager)
 #   lpdyn_ab2    the same A/B as lpdyn_ab, more rounds, plain and forced
 #   dg4_ab       conv2 data gradient at 4 workgroups per image (experiment build _C_dg4.so)
+#   fp32dg_ab    fp32 conv2 data gradient split 4 vs 2 (experiment build _C_dgf2.so)
 #   defer_ab     conv1 weight gradient inside the optimizer launch (DPA_DEFER_WGRAD1=1) vs as built
 #   rn_knobs     ResNet-50 conv tuning knobs re-swept (wgrad blocks / min pixels, 1x1 pixel tile, stats defer)
 #   rtenv_ab     HIP runtime knobs (HIP_FORCE_DEV_KERNARG, DEBUG_CLR_GRAPH_PACKET_CAPTURE) on the driver command
@@ -193,6 +194,9 @@ step() {
       bash scripts/ab_bench.sh "$OUT/rn_knobs2.txt" 2 "--model resnet50 --steps 100 --warmup 10 --no-baseline" base=default \
         b64_256=env:DPA_G1X1_BN64_BELOW=256 b64_512=env:DPA_G1X1_BN64_BELOW=512 b64_1024=env:DPA_G1X1_BN64_BELOW=1024 \
         wide0=env:DPA_WIDE=0 wide2=env:DPA_WIDE=2 ;;
+    fp32dg_ab)  # fp32 conv2 data gradient at 4 workgroups per image (default) vs 2 (_C_dgf2.so)
+      bash scripts/ab_bench.sh "$OUT/fp32dg_ab.txt" 4 "--amp-dtype fp32 --steps 2000 --warmup 50 --no-baseline --epochs 0 \
+--no-steady --extra-dtypes ," dg4=default dg2=ddp_practice_amd/_C_dgf2.so ;;
     spin_ab)  # busy-polled host waits (runtime/device.spin_sync) on the driver's command
       bash scripts/ab_bench.sh "$OUT/spin_ab.txt" 4 "--steps 20 --warmup 5" spin=env:DPA_SPIN_SYNC=1 yield=default ;;
     bn_nt_ab)  # ResNet-50: streaming (non-temporal) BN activation stores / loads (experiment builds)
